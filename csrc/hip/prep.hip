@@ -1,0 +1,300 @@
+// Preprocessing kernels: token histogram, per-transaction frequent counts,
+// transaction compression to sorted rank lists, row hashing for dedup, and the
+// vertical (item-major) bitmap build.
+//
+// Reference sites: FastApriori.scala:55-57 (histogram),
+// :66-70 (compress + size filter), :71-79 (dedup), :195-210 (vertical transpose,
+// done there as F1 separate Spark jobs producing 1 byte per transaction).
+#include "fa_hip.h"
+
+namespace fa {
+
+// ---------------------------------------------------------------------------
+// Histogram over token ids.  V <= kLdsBins: LDS-privatised per workgroup, one
+// global atomic per non-zero bin per workgroup; otherwise global atomics.
+// ---------------------------------------------------------------------------
+constexpr int kLdsBins = 16384;
+
+template <bool kLds, bool kVec>
+__global__ __launch_bounds__(256) void k_histogram(const int32_t* __restrict__ items, int64_t nnz,
+                                                   int32_t V, uint32_t* __restrict__ counts) {
+  __shared__ uint32_t sh[kLds ? kLdsBins : 1];
+  if (kLds) {
+    for (int i = threadIdx.x; i < V; i += blockDim.x) sh[i] = 0;
+    __syncthreads();
+  }
+  auto add = [&](int32_t v) {
+    if (kLds) atomicAdd(&sh[v], 1u); else atomicAdd(&counts[v], 1u);
+  };
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n4 = kVec ? (nnz >> 2) : 0;
+  const int4* it4 = reinterpret_cast<const int4*>(items);
+  for (int64_t i = gid; i < n4; i += stride) {
+    int4 v = it4[i];
+    add(v.x); add(v.y); add(v.z); add(v.w);
+  }
+  for (int64_t i = (n4 << 2) + gid; i < nnz; i += stride) add(items[i]);
+  if (kLds) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < V; i += blockDim.x)
+      if (sh[i]) atomicAdd(&counts[i], sh[i]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Number of frequent ids in every transaction (ids are distinct per line).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_txn_freq_count(const int64_t* __restrict__ off,
+                                                        const int32_t* __restrict__ items, int64_t n,
+                                                        const int32_t* __restrict__ lut,
+                                                        int32_t* __restrict__ cnt) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  int32_t c = 0;
+  for (int64_t i = off[t], e = off[t + 1]; i < e; ++i) c += lut[items[i]] >= 0;
+  cnt[t] = c;
+}
+
+// ---------------------------------------------------------------------------
+// Compression: kept transaction x -> its frequent ranks, sorted ascending, at
+// ranks[roff[x] .. roff[x+1]).  Short rows are sorted in registers with an
+// unrolled bitonic network (static indices only, so nothing spills to
+// scratch); rows longer than N go to an overflow list for the next tier.
+// ---------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void bitonic_regs(uint32_t (&a)[N]) {
+#pragma unroll
+  for (int k = 2; k <= N; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const int l = i ^ j;
+        if (l > i) {
+          uint32_t x = a[i], y = a[l];
+          uint32_t lo = x < y ? x : y, hi = x < y ? y : x;
+          if ((i & k) == 0) { a[i] = lo; a[l] = hi; } else { a[i] = hi; a[l] = lo; }
+        }
+      }
+    }
+  }
+}
+
+template <int N>
+__global__ __launch_bounds__(256) void k_compress_regs(
+    const int64_t* __restrict__ off, const int32_t* __restrict__ items, const int32_t* __restrict__ lut,
+    const int32_t* __restrict__ rows, int64_t nrows, const int32_t* __restrict__ kept,
+    const int64_t* __restrict__ roff, int32_t* __restrict__ ranks, int32_t* __restrict__ overflow,
+    int32_t* __restrict__ n_overflow) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nrows) return;
+  const int32_t x = rows ? rows[i] : (int32_t)i;
+  const int64_t t = kept[x];
+  const int64_t s = off[t];
+  const int64_t L = off[t + 1] - s;
+  if (L > N) {
+    overflow[atomicAdd(n_overflow, 1)] = x;
+    return;
+  }
+  uint32_t a[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    int32_t r = j < L ? lut[items[s + j]] : -1;
+    a[j] = r < 0 ? 0xFFFFFFFFu : (uint32_t)r;
+  }
+  bitonic_regs<N>(a);
+  const int64_t o = roff[x];
+  const int64_t c = roff[x + 1] - o;
+#pragma unroll
+  for (int j = 0; j < N; ++j)
+    if (j < c) ranks[o + j] = (int32_t)a[j];
+}
+
+// Long rows: one 256-thread workgroup per row, bitonic sort in LDS (<= 16384).
+constexpr int kLongMax = 16384;
+__global__ __launch_bounds__(256) void k_compress_lds(
+    const int64_t* __restrict__ off, const int32_t* __restrict__ items, const int32_t* __restrict__ lut,
+    const int32_t* __restrict__ rows, const int32_t* __restrict__ kept, const int64_t* __restrict__ roff,
+    int32_t* __restrict__ ranks, int32_t* __restrict__ too_long, int32_t* __restrict__ n_too_long) {
+  __shared__ uint32_t sh[kLongMax];
+  const int32_t x = rows[blockIdx.x];
+  const int64_t t = kept[x];
+  const int64_t s = off[t];
+  const int64_t L = off[t + 1] - s;
+  if (L > kLongMax) {
+    if (threadIdx.x == 0) too_long[atomicAdd(n_too_long, 1)] = x;
+    return;
+  }
+  int P = 1;
+  while (P < L) P <<= 1;
+  for (int j = threadIdx.x; j < P; j += blockDim.x) {
+    int32_t r = j < L ? lut[items[s + j]] : -1;
+    sh[j] = r < 0 ? 0xFFFFFFFFu : (uint32_t)r;
+  }
+  __syncthreads();
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < P; i += blockDim.x) {
+        const int l = i ^ j;
+        if (l > i) {
+          uint32_t a = sh[i], b = sh[l];
+          bool up = (i & k) == 0;
+          if ((a > b) == up) { sh[i] = b; sh[l] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const int64_t o = roff[x];
+  const int64_t c = roff[x + 1] - o;
+  for (int j = threadIdx.x; j < c; j += blockDim.x) ranks[o + j] = (int32_t)sh[j];
+}
+
+// ---------------------------------------------------------------------------
+// Order-sensitive 128-bit hash of each compressed row (rows are sorted, so equal
+// sets <=> equal sequences).  Used to find duplicate transactions.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t dmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_row_hash(const int64_t* __restrict__ roff,
+                                                  const int32_t* __restrict__ ranks, int64_t T,
+                                                  int64_t* __restrict__ h1, int64_t* __restrict__ h2) {
+  const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= T) return;
+  uint64_t a = 0x243F6A8885A308D3ull, b = 0x13198A2E03707344ull;
+  const int64_t s = roff[x], e = roff[x + 1];
+  for (int64_t i = s; i < e; ++i) {
+    uint64_t r = (uint32_t)ranks[i];
+    a = dmix64(a ^ r);
+    b = dmix64(b + r * 0xD6E8FEB86659FD93ull);
+  }
+  a = dmix64(a ^ (uint64_t)(e - s));
+  // keep the sign bit clear so signed sorts order like unsigned ones
+  h1[x] = (int64_t)(a >> 1);
+  h2[x] = (int64_t)(b >> 1);
+}
+
+// ---------------------------------------------------------------------------
+// Vertical bitmap build from the compressed rows.  Workgroup (wx, ry) owns the
+// WT-word column block wx and the rank slice [ry*R, ry*R+R): it ORs bits into an
+// LDS tile with ds_or_b32, then writes each rank's WT words (coalesced per row).
+// Column c holds compressed row src[c] (src == nullptr: identity; -1: padding).
+// Every word of [F1][Wp] is written, so the output needs no zeroing.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_build_bitmaps(
+    const int64_t* __restrict__ roff, const int32_t* __restrict__ ranks, const int32_t* __restrict__ src,
+    int64_t ncols, int32_t F1, int64_t Wp, int WT, int R, uint64_t* __restrict__ bm) {
+  extern __shared__ uint32_t tile[];   // [R][2*WT]
+  const int hw = 2 * WT;
+  const int r0 = blockIdx.y * R;
+  const int r1 = min(F1, r0 + R);
+  const int nr = r1 - r0;
+  for (int i = threadIdx.x; i < nr * hw; i += blockDim.x) tile[i] = 0;
+  __syncthreads();
+  const int64_t c0 = (int64_t)blockIdx.x * WT * 64;
+  for (int j = threadIdx.x; j < WT * 64; j += blockDim.x) {
+    const int64_t c = c0 + j;
+    if (c >= ncols) break;
+    const int64_t row = src ? (int64_t)src[c] : c;
+    if (row < 0) continue;
+    int64_t s = roff[row];
+    const int64_t e = roff[row + 1];
+    // ranks are sorted: skip to r0, stop at r1
+    int64_t lo = s, hi = e;
+    while (lo < hi) {
+      int64_t mid = (lo + hi) >> 1;
+      if (ranks[mid] < r0) lo = mid + 1; else hi = mid;
+    }
+    const uint32_t bit = 1u << (j & 31);
+    const int word = j >> 5;
+    for (int64_t i = lo; i < e; ++i) {
+      const int r = ranks[i];
+      if (r >= r1) break;
+      atomicOr(&tile[(r - r0) * hw + word], bit);
+    }
+  }
+  __syncthreads();
+  uint32_t* out = reinterpret_cast<uint32_t*>(bm);
+  const int64_t base = c0 >> 5;
+  for (int i = threadIdx.x; i < nr * hw; i += blockDim.x) {
+    const int r = i / hw, w = i - r * hw;
+    out[(int64_t)(r0 + r) * (2 * Wp) + base + w] = tile[i];
+  }
+}
+
+}  // namespace fa
+
+using namespace fa;
+
+FA_API int fa_hip_histogram(const int32_t* items, int64_t nnz, int32_t V, uint32_t* counts,
+                            hipStream_t st) {
+  if (nnz <= 0) return 0;
+  int64_t blocks = std::min<int64_t>((nnz + 256 * 16 - 1) / (256 * 16), 2048);
+  const bool aligned = ((uintptr_t)items & 15) == 0;
+  dim3 g((unsigned)blocks), b(256);
+  if (V <= kLdsBins) {
+    if (aligned) hipLaunchKernelGGL((k_histogram<true, true>), g, b, 0, st, items, nnz, V, counts);
+    else hipLaunchKernelGGL((k_histogram<true, false>), g, b, 0, st, items, nnz, V, counts);
+  } else {
+    if (aligned) hipLaunchKernelGGL((k_histogram<false, true>), g, b, 0, st, items, nnz, V, counts);
+    else hipLaunchKernelGGL((k_histogram<false, false>), g, b, 0, st, items, nnz, V, counts);
+  }
+  FA_LAUNCH_RET();
+}
+
+FA_API int fa_hip_txn_freq_count(const int64_t* off, const int32_t* items, int64_t n,
+                                 const int32_t* lut, int32_t* cnt, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_txn_freq_count, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, off, items, n, lut, cnt);
+  FA_LAUNCH_RET();
+}
+
+// tier: 16 / 64 register networks over `rows` (nullptr = all kept rows 0..nrows)
+FA_API int fa_hip_compress_regs(int tier, const int64_t* off, const int32_t* items, const int32_t* lut,
+                                const int32_t* rows, int64_t nrows, const int32_t* kept,
+                                const int64_t* roff, int32_t* ranks, int32_t* overflow,
+                                int32_t* n_overflow, hipStream_t st) {
+  if (nrows <= 0) return 0;
+  dim3 g((unsigned)((nrows + 255) / 256));
+  if (tier == 16)
+    hipLaunchKernelGGL(k_compress_regs<16>, g, dim3(256), 0, st, off, items, lut, rows, nrows, kept, roff, ranks, overflow, n_overflow);
+  else if (tier == 64)
+    hipLaunchKernelGGL(k_compress_regs<64>, g, dim3(256), 0, st, off, items, lut, rows, nrows, kept, roff, ranks, overflow, n_overflow);
+  else
+    return 1;
+  FA_LAUNCH_RET();
+}
+
+FA_API int fa_hip_compress_lds(const int64_t* off, const int32_t* items, const int32_t* lut,
+                               const int32_t* rows, int64_t nrows, const int32_t* kept,
+                               const int64_t* roff, int32_t* ranks, int32_t* too_long,
+                               int32_t* n_too_long, hipStream_t st) {
+  if (nrows <= 0) return 0;
+  hipLaunchKernelGGL(k_compress_lds, dim3((unsigned)nrows), dim3(256), 0, st, off, items, lut, rows, kept, roff, ranks, too_long, n_too_long);
+  FA_LAUNCH_RET();
+}
+
+FA_API int fa_hip_row_hash(const int64_t* roff, const int32_t* ranks, int64_t T, int64_t* h1,
+                           int64_t* h2, hipStream_t st) {
+  if (T <= 0) return 0;
+  hipLaunchKernelGGL(k_row_hash, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, st, roff, ranks, T, h1, h2);
+  FA_LAUNCH_RET();
+}
+
+// Wp must be a multiple of WT.  LDS = R * 2 * WT * 4 bytes.
+FA_API int fa_hip_build_bitmaps(const int64_t* roff, const int32_t* ranks, const int32_t* src,
+                                int64_t ncols, int32_t F1, int64_t Wp, int WT, int R, uint64_t* bm,
+                                hipStream_t st) {
+  if (F1 <= 0 || Wp <= 0) return 0;
+  if (Wp % WT) return 1;
+  dim3 g((unsigned)(Wp / WT), (unsigned)((F1 + R - 1) / R));
+  size_t lds = (size_t)R * 2 * WT * 4;
+  hipLaunchKernelGGL(k_build_bitmaps, g, dim3(256), lds, st, roff, ranks, src, ncols, F1, Wp, WT, R, bm);
+  FA_LAUNCH_RET();
+}

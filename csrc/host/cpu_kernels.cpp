@@ -1,0 +1,147 @@
+// CPU implementations of the mining primitives.
+//
+// These serve two roles: (1) the device path for CPU tensors, used by the
+// gloo multi-process tests and the BASELINE "CPU world_size=1 plumbing"
+// config; (2) an independent reference for the HIP kernels in csrc/hip/.
+// Layout conventions are identical to the HIP side:
+//   bitmaps  uint64 [F1][Wp], bit (c & 63) of word c >> 6 = column c;
+//   wword    optional int32 per word: weight of every column in that word
+//            (columns are grouped by dedup weight class, padded to 64);
+//   counts   int64.
+#include "fa_common.h"
+
+using namespace fa;
+
+FA_API void fa_cpu_histogram(const int32_t* items, int64_t nnz, int64_t V, int64_t* out,
+                             int nthreads) {
+  if (V <= 0) return;
+  int nt = std::max(1, nthreads);
+  if (V > (1 << 22) || nnz < (1 << 16)) nt = 1;
+  std::vector<std::vector<int64_t>> loc(nt);
+  parallel_for_threads(nt, [&](int t) {
+    auto& h = loc[t];
+    h.assign((size_t)V, 0);
+    int64_t b = nnz * t / nt, e = nnz * (t + 1) / nt;
+    for (int64_t i = b; i < e; ++i) h[items[i]]++;
+  });
+  for (int t = 0; t < nt; ++t)
+    for (int64_t v = 0; v < V; ++v) out[v] += loc[t][v];
+}
+
+FA_API void fa_cpu_txn_freq_count(const int64_t* off, const int32_t* items, int64_t n,
+                                  const int32_t* lut, int32_t* out, int nthreads) {
+  parallel_for(n, nthreads, 1 << 14, [&](int64_t b, int64_t e, int) {
+    for (int64_t t = b; t < e; ++t) {
+      int32_t c = 0;
+      for (int64_t i = off[t]; i < off[t + 1]; ++i) c += lut[items[i]] >= 0;
+      out[t] = c;
+    }
+  });
+}
+
+// Column c holds compressed row src[c] (src == nullptr: identity; -1: padding).
+// out must be zero-initialised, [F1][Wp].
+FA_API void fa_cpu_build_bitmaps(const int64_t* roff, const int32_t* ranks, const int32_t* src,
+                                 int64_t ncols, int64_t Wp, uint64_t* out, int nthreads) {
+  const int64_t W = (ncols + 63) / 64;
+  parallel_for(W, nthreads, 256, [&](int64_t wb, int64_t we, int) {
+    for (int64_t c = wb * 64; c < std::min(ncols, we * 64); ++c) {
+      int64_t row = src ? (int64_t)src[c] : c;
+      if (row < 0) continue;
+      const uint64_t bit = 1ull << (c & 63);
+      const int64_t w = c >> 6;
+      for (int64_t i = roff[row]; i < roff[row + 1]; ++i) out[(int64_t)ranks[i] * Wp + w] |= bit;
+    }
+  });
+}
+
+// Same hash as the device k_row_hash (csrc/hip/prep.hip).
+FA_API void fa_cpu_row_hash(const int64_t* roff, const int32_t* ranks, int64_t T, int64_t* h1,
+                            int64_t* h2, int nthreads) {
+  parallel_for(T, nthreads, 1 << 14, [&](int64_t b, int64_t e, int) {
+    for (int64_t x = b; x < e; ++x) {
+      uint64_t a = 0x243F6A8885A308D3ull, c = 0x13198A2E03707344ull;
+      for (int64_t i = roff[x]; i < roff[x + 1]; ++i) {
+        uint64_t r = (uint32_t)ranks[i];
+        a = mix64(a ^ r);
+        c = mix64(c + r * 0xD6E8FEB86659FD93ull);
+      }
+      a = mix64(a ^ (uint64_t)(roff[x + 1] - roff[x]));
+      h1[x] = (int64_t)(a >> 1);
+      h2[x] = (int64_t)(c >> 1);
+    }
+  });
+}
+
+// Upper-triangular pair supports from bitmaps (out[i*F1+j], i<j).  out zeroed.
+FA_API void fa_cpu_pair_gram(const uint64_t* bm, int32_t F1, int64_t Wp, int64_t W,
+                             const int32_t* wword, int64_t* out, int nthreads) {
+  parallel_for(F1, nthreads, 1, [&](int64_t i0, int64_t i1, int) {
+    for (int64_t i = i0; i < i1; ++i) {
+      const uint64_t* a = bm + i * Wp;
+      for (int64_t j = i + 1; j < F1; ++j) {
+        const uint64_t* b = bm + j * Wp;
+        int64_t s = 0;
+        if (wword) {
+          for (int64_t w = 0; w < W; ++w) s += (int64_t)__builtin_popcountll(a[w] & b[w]) * wword[w];
+        } else {
+          for (int64_t w = 0; w < W; ++w) s += __builtin_popcountll(a[w] & b[w]);
+        }
+        out[i * F1 + j] = s;
+      }
+    }
+  });
+}
+
+// Pair supports from compressed rows (sorted ranks): every pair (a < c) of a
+// row gets +weight.  out zeroed, [F1][F1].
+FA_API void fa_cpu_pair_horizontal(const int64_t* roff, const int32_t* ranks, int64_t T,
+                                   const int32_t* wrow, int32_t F1, int64_t* out, int nthreads) {
+  int nt = std::max(1, nthreads);
+  if ((int64_t)F1 * F1 > (1 << 22) || T < 4096) nt = 1;
+  std::vector<std::vector<int64_t>> loc(nt);
+  parallel_for_threads(nt, [&](int tid) {
+    int64_t* acc = out;
+    if (nt > 1) { loc[tid].assign((size_t)F1 * F1, 0); acc = loc[tid].data(); }
+    int64_t b = T * tid / nt, e = T * (tid + 1) / nt;
+    for (int64_t x = b; x < e; ++x) {
+      const int64_t w = wrow ? wrow[x] : 1;
+      if (w == 0) continue;
+      for (int64_t i = roff[x]; i < roff[x + 1]; ++i)
+        for (int64_t j = i + 1; j < roff[x + 1]; ++j) acc[(int64_t)ranks[i] * F1 + ranks[j]] += w;
+    }
+  });
+  if (nt > 1)
+    for (int t = 0; t < nt; ++t)
+      for (int64_t i = 0; i < (int64_t)F1 * F1; ++i) out[i] += loc[t][i];
+}
+
+// Prefix-shared candidate support (FastApriori.scala:132-160 semantics):
+// group g = prefix ranks prefix[g][0..m) + extensions ext[ext_off[g]..ext_off[g+1]).
+FA_API void fa_cpu_count_candidates(const uint64_t* bm, int64_t Wp, int64_t W,
+                                    const int32_t* prefix, int32_t m, const int64_t* ext_off,
+                                    const int32_t* ext, int64_t G, const int32_t* wword,
+                                    int64_t* out, int nthreads) {
+  parallel_for(G, nthreads, 4, [&](int64_t g0, int64_t g1, int) {
+    std::vector<uint64_t> common((size_t)std::max<int64_t>(1, W));
+    for (int64_t g = g0; g < g1; ++g) {
+      const int32_t* p = prefix + g * m;
+      const uint64_t* r0 = bm + (int64_t)p[0] * Wp;
+      for (int64_t w = 0; w < W; ++w) common[w] = r0[w];
+      for (int q = 1; q < m; ++q) {
+        const uint64_t* rq = bm + (int64_t)p[q] * Wp;
+        for (int64_t w = 0; w < W; ++w) common[w] &= rq[w];
+      }
+      for (int64_t e = ext_off[g]; e < ext_off[g + 1]; ++e) {
+        const uint64_t* re = bm + (int64_t)ext[e] * Wp;
+        int64_t s = 0;
+        if (wword) {
+          for (int64_t w = 0; w < W; ++w) s += (int64_t)__builtin_popcountll(common[w] & re[w]) * wword[w];
+        } else {
+          for (int64_t w = 0; w < W; ++w) s += __builtin_popcountll(common[w] & re[w]);
+        }
+        out[e] = s;
+      }
+    }
+  });
+}

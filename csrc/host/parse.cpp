@@ -1,0 +1,263 @@
+// Transaction-file parser: mmap + multithreaded tokeniser -> CSR of token ids.
+//
+// Reproduces the reference's input semantics (Utils.scala:19-27):
+//   * lines split like Hadoop's LineRecordReader (\n, \r\n or \r);
+//   * each line -> trim() -> split("\\s+"); an empty line is the single token "";
+//   * a byte range [begin, end) owns exactly the lines that START inside it, so
+//     disjoint ranges partition the file (used for one shard per rank).
+// Output invariant used by every kernel downstream: the ids inside one
+// transaction are DISTINCT.  Repeated tokens of a line are reported separately
+// as "extras" (one entry per repeated occurrence) because the reference's F1
+// counts occurrences (FastApriori.scala:55) while k>=2 counts sets (:69).
+//
+// Two id spaces:
+//   numeric : every token is a canonical decimal "0" | [1-9][0-9]* <= 2^31-2;
+//             id = value + 1, id 0 = the empty token "".  No dictionary needed
+//             and ids agree across ranks by construction.
+//   dict    : any other vocabulary; per-shard dictionary (id -> bytes) plus a
+//             64-bit hash per entry used to agree on identity across ranks.
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <unordered_map>
+
+#include "fa_common.h"
+#include "txndb.h"
+
+namespace fa {
+
+static inline bool is_sep(uint8_t c) { return c == ' ' || c == '\t' || c == 0x0B || c == '\f'; }
+
+int64_t next_line_start(const char* d, int64_t size, int64_t pos) {
+  if (pos <= 0) return 0;
+  for (int64_t i = pos - 1; i < size; ++i) {
+    char c = d[i];
+    if (c == '\n') return i + 1;
+    if (c == '\r') return (i + 1 < size && d[i + 1] == '\n') ? i + 2 : i + 1;
+  }
+  return size;
+}
+
+// Calls tok(ptr, len) for every token of the line [ls, le) (terminator excluded).
+template <class F>
+static inline void for_each_token(const char* d, int64_t ls, int64_t le, F&& tok) {
+  while (ls < le && (uint8_t)d[ls] <= 0x20) ++ls;
+  while (le > ls && (uint8_t)d[le - 1] <= 0x20) --le;
+  if (ls == le) { tok(d + ls, 0); return; }
+  int64_t i = ls;
+  while (i < le) {
+    int64_t s = i;
+    while (i < le && !is_sep((uint8_t)d[i])) ++i;
+    tok(d + s, i - s);
+    while (i < le && is_sep((uint8_t)d[i])) ++i;
+  }
+}
+
+// Returns id (>=0) for a canonical numeric token, or -1.
+static inline int32_t numeric_id(const char* p, int64_t n) {
+  if (n == 0) return 0;
+  if (n > 10) return -1;
+  if (p[0] == '0' && n > 1) return -1;
+  uint64_t v = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    uint8_t c = (uint8_t)p[i] - '0';
+    if (c > 9) return -1;
+    v = v * 10 + c;
+  }
+  if (v > 2147483646ull) return -1;
+  return (int32_t)(v + 1);
+}
+
+// Appends the distinct ids of `line` to items; repeats go to extras.
+static inline void emit_distinct(std::vector<int32_t>& line, std::vector<int32_t>& items,
+                                 std::vector<int32_t>& extras, std::vector<int32_t>& table) {
+  const size_t L = line.size();
+  if (L <= 24) {
+    for (size_t i = 0; i < L; ++i) {
+      bool dup = false;
+      for (size_t j = 0; j < i; ++j) if (line[j] == line[i]) { dup = true; break; }
+      if (dup) extras.push_back(line[i]); else items.push_back(line[i]);
+    }
+    return;
+  }
+  size_t cap = 64;
+  while (cap < 2 * L) cap <<= 1;
+  table.assign(cap, -1);
+  for (size_t i = 0; i < L; ++i) {
+    int32_t v = line[i];
+    size_t h = (size_t)mix64((uint64_t)(uint32_t)v) & (cap - 1);
+    bool dup = false;
+    while (table[h] != -1) {
+      if (table[h] == v) { dup = true; break; }
+      h = (h + 1) & (cap - 1);
+    }
+    if (dup) { extras.push_back(v); continue; }
+    table[h] = v;
+    items.push_back(v);
+  }
+}
+
+struct MappedFile {
+  const char* data = nullptr;
+  int64_t size = 0;
+  int fd = -1;
+  bool open(const char* path) {
+    fd = ::open(path, O_RDONLY);
+    if (fd < 0) return false;
+    struct stat st;
+    if (fstat(fd, &st) != 0) return false;
+    size = st.st_size;
+    if (size == 0) return true;
+    void* p = mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
+    if (p == MAP_FAILED) return false;
+    madvise(p, size, MADV_SEQUENTIAL);
+    data = (const char*)p;
+    return true;
+  }
+  ~MappedFile() {
+    if (data) munmap((void*)data, size);
+    if (fd >= 0) ::close(fd);
+  }
+};
+
+struct ThreadDict {
+  std::unordered_map<std::string_view, int32_t> map;
+  std::vector<std::string_view> strs;
+  int32_t get(std::string_view s) {
+    auto it = map.find(s);
+    if (it != map.end()) return it->second;
+    int32_t id = (int32_t)strs.size();
+    map.emplace(s, id);
+    strs.push_back(s);
+    return id;
+  }
+};
+
+// Parse lines starting in [b, e) of an in-memory buffer.
+static int parse_buffer(const char* d, int64_t size, int64_t b, int64_t e, int mode, int nthreads,
+                        TxnDB* db) {
+  b = std::max<int64_t>(0, std::min(b, size));
+  e = std::max<int64_t>(b, std::min(e, size));
+  int64_t first = next_line_start(d, size, b);
+  // per-thread sub-ranges with the same ownership rule
+  int nt = std::max(1, nthreads);
+  if (e - b < (int64_t)nt * 65536) nt = std::max<int64_t>(1, (e - b) / 65536);
+  std::vector<int64_t> cuts(nt + 1);
+  for (int t = 0; t <= nt; ++t) cuts[t] = b + (e - b) * t / nt;
+  db->chunks.assign(nt, TxnChunk());
+  std::vector<std::vector<int32_t>> extras(nt);
+  std::vector<ThreadDict> dicts(mode == 1 ? nt : 0);
+  std::atomic<bool> non_numeric{false};
+
+  parallel_for_threads(nt, [&](int t) {
+    int64_t lo = (t == 0) ? first : next_line_start(d, size, cuts[t]);
+    int64_t hi = cuts[t + 1];
+    TxnChunk& ch = db->chunks[t];
+    std::vector<int32_t> line, table;
+    int64_t p = lo;
+    while (p < hi && p < size) {
+      int64_t q = p;
+      while (q < size && d[q] != '\n' && d[q] != '\r') ++q;
+      line.clear();
+      if (mode == 0) {
+        bool ok = true;
+        for_each_token(d, p, q, [&](const char* s, int64_t n) {
+          int32_t id = numeric_id(s, n);
+          if (id < 0) ok = false; else line.push_back(id);
+        });
+        if (!ok) { non_numeric.store(true); return; }
+      } else {
+        ThreadDict& td = dicts[t];
+        for_each_token(d, p, q, [&](const char* s, int64_t n) {
+          line.push_back(td.get(std::string_view(s, (size_t)n)));
+        });
+      }
+      emit_distinct(line, ch.items, extras[t], table);
+      ch.lens.push_back((int64_t)(ch.items.size()));  // cumulative end within chunk
+      if (q >= size) { p = size; break; }
+      p = (d[q] == '\r' && q + 1 < size && d[q + 1] == '\n') ? q + 2 : q + 1;
+      if (non_numeric.load(std::memory_order_relaxed)) return;
+    }
+  });
+  if (mode == 0 && non_numeric.load()) return 1;
+
+  db->numeric = (mode == 0);
+  if (mode == 0) {
+    int32_t mx = -1;
+    for (auto& ch : db->chunks) for (int32_t v : ch.items) mx = std::max(mx, v);
+    for (auto& ex : extras) for (int32_t v : ex) mx = std::max(mx, v);
+    db->vocab = (int64_t)mx + 1;
+  } else {
+    // merge thread dictionaries into one shard dictionary, remap ids
+    std::unordered_map<std::string_view, int32_t> global;
+    std::vector<std::string_view> gstrs;
+    for (int t = 0; t < nt; ++t) {
+      auto& td = dicts[t];
+      std::vector<int32_t> remap(td.strs.size());
+      for (size_t i = 0; i < td.strs.size(); ++i) {
+        auto it = global.find(td.strs[i]);
+        if (it == global.end()) {
+          int32_t id = (int32_t)gstrs.size();
+          global.emplace(td.strs[i], id);
+          gstrs.push_back(td.strs[i]);
+          remap[i] = id;
+        } else {
+          remap[i] = it->second;
+        }
+      }
+      for (auto& v : db->chunks[t].items) v = remap[v];
+      for (auto& v : extras[t]) v = remap[v];
+    }
+    db->dict.reserve(gstrs.size());
+    for (auto& s : gstrs) db->dict.emplace_back(s);
+    db->vocab = (int64_t)gstrs.size();
+  }
+  for (auto& ex : extras) db->extras.insert(db->extras.end(), ex.begin(), ex.end());
+  return 0;
+}
+
+}  // namespace fa
+
+using namespace fa;
+
+// mode: 0 = auto (numeric if every token is canonical numeric, else dict), 1 = dict.
+// On failure returns nullptr and sets *err (1 = cannot open, 2 = mmap).
+FA_API TxnDB* fa_parse_file(const char* path, int64_t byte_begin, int64_t byte_end, int mode,
+                            int nthreads, int* err) {
+  *err = 0;
+  MappedFile mf;
+  if (!mf.open(path)) { *err = 1; return nullptr; }
+  if (byte_end < 0) byte_end = mf.size;
+  auto* db = new TxnDB();
+  if (mode == 0) {
+    if (parse_buffer(mf.data, mf.size, byte_begin, byte_end, 0, nthreads, db) == 0) return db;
+    delete db;
+    db = new TxnDB();
+  }
+  parse_buffer(mf.data, mf.size, byte_begin, byte_end, 1, nthreads, db);
+  return db;
+}
+
+FA_API TxnDB* fa_parse_buffer(const char* data, int64_t size, int mode, int nthreads) {
+  auto* db = new TxnDB();
+  if (mode == 0) {
+    if (parse_buffer(data, size, 0, size, 0, nthreads, db) == 0) return db;
+    delete db;
+    db = new TxnDB();
+  }
+  parse_buffer(data, size, 0, size, 1, nthreads, db);
+  return db;
+}
+
+FA_API int64_t fa_file_size(const char* path) {
+  struct stat st;
+  if (stat(path, &st) != 0) return -1;
+  return st.st_size;
+}
+
+// Line start helper exposed for tests of the sharding rule.
+FA_API int64_t fa_next_line_start(const char* data, int64_t size, int64_t pos) {
+  return next_line_start(data, size, pos);
+}

@@ -1,0 +1,203 @@
+// IBM-Quest-style synthetic transaction generator (Agrawal & Srikant, VLDB'94):
+// "T<avg txn len>I<avg pattern len>D<n txns>" with |L| potentially-large
+// patterns over N items.  Used for BASELINE.json's configs (T10I4D100K,
+// T10I4D100M, T40I10D100M) since no dataset can be downloaded.
+//
+// Counter-based: transaction t is generated from mix64(seed, t) alone, so any
+// shard [begin, end) of the database is identical no matter how the database
+// is split across ranks/threads (the pattern table depends only on the seed).
+// Departure from the original generator (documented): a pattern that does not
+// fit is added with probability 1/2 and otherwise dropped instead of being
+// carried to the next transaction (carry-over would serialise generation).
+#include <cmath>
+#include <cstdio>
+
+#include "fa_common.h"
+#include "txndb.h"
+
+namespace fa {
+
+struct QuestParams {
+  double avg_len, avg_pat_len;
+  int64_t n_patterns, n_items;
+  uint64_t seed;
+  double correlation = 0.5, corrupt_mean = 0.5, corrupt_sd = 0.1;
+};
+
+static int64_t poisson(Rng& r, double mean) {
+  if (mean <= 0) return 0;
+  if (mean < 40) {
+    double L = std::exp(-mean), p = 1.0;
+    int64_t k = 0;
+    do { ++k; p *= r.uniform(); } while (p > L);
+    return k - 1;
+  }
+  double u1 = std::max(r.uniform(), 1e-300), u2 = r.uniform();
+  double z = std::sqrt(-2 * std::log(u1)) * std::cos(6.283185307179586 * u2);
+  return std::max<int64_t>(0, (int64_t)std::llround(mean + std::sqrt(mean) * z));
+}
+
+static double normal(Rng& r, double mu, double sd) {
+  double u1 = std::max(r.uniform(), 1e-300), u2 = r.uniform();
+  return mu + sd * std::sqrt(-2 * std::log(u1)) * std::cos(6.283185307179586 * u2);
+}
+
+struct PatternTable {
+  std::vector<std::vector<int32_t>> pats;   // item values in [1, n_items]
+  std::vector<double> cdf;
+  std::vector<double> corrupt;
+
+  explicit PatternTable(const QuestParams& q) {
+    Rng r(mix64(q.seed ^ 0x5157455354ull));
+    pats.resize(q.n_patterns);
+    cdf.resize(q.n_patterns);
+    corrupt.resize(q.n_patterns);
+    double tot = 0;
+    auto contains = [](const std::vector<int32_t>& v, int32_t x) {
+      return std::find(v.begin(), v.end(), x) != v.end();
+    };
+    for (int64_t p = 0; p < q.n_patterns; ++p) {
+      int64_t sz = std::max<int64_t>(1, poisson(r, q.avg_pat_len));
+      sz = std::min<int64_t>(sz, q.n_items);
+      auto& cur = pats[p];
+      if (p > 0) {
+        const auto& prev = pats[p - 1];
+        double frac = std::min(1.0, -q.correlation * std::log(std::max(r.uniform(), 1e-300)));
+        int64_t take = std::min<int64_t>({sz, (int64_t)std::llround(frac * sz), (int64_t)prev.size()});
+        std::vector<int32_t> pool(prev);
+        for (int64_t i = 0; i < take; ++i) {
+          size_t j = (size_t)r.below(pool.size());
+          cur.push_back(pool[j]);
+          pool[j] = pool.back();
+          pool.pop_back();
+        }
+      }
+      while ((int64_t)cur.size() < sz) {
+        int32_t x = (int32_t)(1 + r.below((uint64_t)q.n_items));
+        if (!contains(cur, x)) cur.push_back(x);
+      }
+      double w = -std::log(std::max(r.uniform(), 1e-300));
+      tot += w;
+      cdf[p] = tot;
+      corrupt[p] = std::min(1.0, std::max(0.0, normal(r, q.corrupt_mean, q.corrupt_sd)));
+    }
+    for (auto& c : cdf) c /= tot;
+  }
+
+  int64_t pick(Rng& r) const {
+    double u = r.uniform();
+    int64_t i = std::lower_bound(cdf.begin(), cdf.end(), u) - cdf.begin();
+    return std::min<int64_t>(i, (int64_t)cdf.size() - 1);
+  }
+};
+
+// Generates transaction t into `out` (sorted, distinct item values).
+static void gen_txn(const QuestParams& q, const PatternTable& pt, int64_t t, bool user,
+                    std::vector<int32_t>& out, std::vector<int32_t>& tmp) {
+  Rng r(mix64(q.seed * 0x9E3779B97F4A7C15ull + (uint64_t)t + (user ? 0x7777777ull : 0)));
+  out.clear();
+  int64_t target = std::max<int64_t>(1, poisson(r, q.avg_len));
+  for (int guard = 0; (int64_t)out.size() < target && guard < 64; ++guard) {
+    const auto& pat = pt.pats[pt.pick(r)];
+    tmp.assign(pat.begin(), pat.end());
+    double c = pt.corrupt[&pat - &pt.pats[0]];
+    while (!tmp.empty() && r.uniform() < c) {
+      size_t j = (size_t)r.below(tmp.size());
+      tmp[j] = tmp.back();
+      tmp.pop_back();
+    }
+    if (tmp.empty()) continue;
+    if ((int64_t)(out.size() + tmp.size()) > target && !out.empty()) {
+      if (r.uniform() < 0.5) break;
+    }
+    for (int32_t x : tmp)
+      if (std::find(out.begin(), out.end(), x) == out.end()) out.push_back(x);
+  }
+  std::sort(out.begin(), out.end());
+  if (user && !out.empty()) {
+    // a user basket: a random non-empty subset of up to 4 items of a transaction
+    size_t keep = 1 + (size_t)r.below(std::min<size_t>(4, out.size()));
+    for (size_t i = 0; i < keep; ++i) {
+      size_t j = i + (size_t)r.below(out.size() - i);
+      std::swap(out[i], out[j]);
+    }
+    out.resize(keep);
+    std::sort(out.begin(), out.end());
+  }
+}
+
+}  // namespace fa
+
+using namespace fa;
+
+static QuestParams make_params(double avg_len, double avg_pat_len, int64_t n_patterns,
+                               int64_t n_items, uint64_t seed) {
+  QuestParams q;
+  q.avg_len = avg_len; q.avg_pat_len = avg_pat_len;
+  q.n_patterns = std::max<int64_t>(1, n_patterns);
+  q.n_items = std::max<int64_t>(1, n_items);
+  q.seed = seed;
+  return q;
+}
+
+// Generates transactions [txn_begin, txn_end) as a numeric-mode TxnDB
+// (id = item value + 1, matching the parser's numeric id space).
+FA_API TxnDB* fa_quest_generate(int64_t txn_begin, int64_t txn_end, double avg_len,
+                                double avg_pat_len, int64_t n_patterns, int64_t n_items,
+                                uint64_t seed, int user_mode, int nthreads) {
+  QuestParams q = make_params(avg_len, avg_pat_len, n_patterns, n_items, seed);
+  PatternTable pt(q);
+  auto* db = new TxnDB();
+  db->numeric = true;
+  db->vocab = q.n_items + 2;
+  int64_t n = std::max<int64_t>(0, txn_end - txn_begin);
+  int nt = std::max(1, nthreads);
+  if (n < (int64_t)nt * 1024) nt = 1;
+  db->chunks.assign(nt, TxnChunk());
+  parallel_for_threads(nt, [&](int t) {
+    int64_t lo = txn_begin + n * t / nt, hi = txn_begin + n * (t + 1) / nt;
+    TxnChunk& ch = db->chunks[t];
+    ch.lens.reserve(hi - lo);
+    ch.items.reserve((size_t)((hi - lo) * (avg_len + 1)));
+    std::vector<int32_t> out, tmp;
+    for (int64_t i = lo; i < hi; ++i) {
+      gen_txn(q, pt, i, user_mode != 0, out, tmp);
+      for (int32_t x : out) ch.items.push_back(x + 1);
+      ch.lens.push_back((int64_t)ch.items.size());
+    }
+  });
+  return db;
+}
+
+// Writes transactions [0, n_txn) as text ("v1 v2 ...\n" per line).
+FA_API int fa_quest_write(const char* path, int64_t n_txn, double avg_len, double avg_pat_len,
+                          int64_t n_patterns, int64_t n_items, uint64_t seed, int user_mode,
+                          int nthreads) {
+  QuestParams q = make_params(avg_len, avg_pat_len, n_patterns, n_items, seed);
+  PatternTable pt(q);
+  FILE* f = std::fopen(path, "wb");
+  if (!f) return 1;
+  const int64_t block = 1 << 16;
+  int nt = std::max(1, nthreads);
+  std::vector<std::string> bufs(nt);
+  for (int64_t b0 = 0; b0 < n_txn; b0 += block * nt) {
+    parallel_for_threads(nt, [&](int t) {
+      std::string& s = bufs[t];
+      s.clear();
+      std::vector<int32_t> out, tmp;
+      char num[16];
+      int64_t lo = b0 + block * t, hi = std::min(n_txn, lo + block);
+      for (int64_t i = lo; i < hi; ++i) {
+        gen_txn(q, pt, i, user_mode != 0, out, tmp);
+        for (size_t j = 0; j < out.size(); ++j) {
+          int len = std::snprintf(num, sizeof num, "%d", out[j]);
+          if (j) s.push_back(' ');
+          s.append(num, len);
+        }
+        s.push_back('\n');
+      }
+    });
+    for (auto& s : bufs) std::fwrite(s.data(), 1, s.size(), f);
+  }
+  return std::fclose(f) == 0 ? 0 : 2;
+}

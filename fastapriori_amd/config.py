@@ -1,0 +1,72 @@
+"""Job configuration: CLI > environment (FA_*) > defaults.
+
+Positional arguments keep the reference's semantics (Main.scala:24-25,
+Utils.scala:21-23,39,48): ``input`` and ``output`` are string PREFIXES —
+``input + "D.dat"``, ``output + "freqItemset"`` — so directories need a
+trailing slash; ``temp`` is the checkpoint location (ignored by the reference).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+from dataclasses import dataclass, field
+
+
+def _env(name: str, default):
+    v = os.environ.get(name)
+    if v is None:
+        return default
+    if isinstance(default, bool):
+        return v.lower() in ("1", "true", "yes", "on")
+    return type(default)(v)
+
+
+@dataclass
+class JobConfig:
+    input: str = ""
+    output: str = ""
+    temp: str = ""
+    min_support: float = 0.092                  # Main.scala:23
+    device: str = "auto"                        # auto | cuda | cpu
+    dedup: str = "auto"
+    pair_strategy: str = "auto"
+    with_counts: bool = False                   # also write <out>freqItems ("a b[cnt]", Utils.scala:51-63)
+    resume: bool = False
+    rules_only: bool = False
+    checkpoint: bool = True
+    overwrite: bool = False
+    profile: bool = False
+    metrics_path: str | None = None
+    max_level: int = 0
+    extra: dict = field(default_factory=dict)
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(
+        prog="python -m fastapriori_amd",
+        description="MI355X-native FastApriori: frequent itemsets + association-rule recommendations")
+    p.add_argument("input", help="input prefix: reads <input>D.dat and <input>U.dat")
+    p.add_argument("output", help="output prefix: writes <output>freqItemset/ and <output>recommends/")
+    p.add_argument("temp", nargs="?", default="", help="temporary path (per-level checkpoints)")
+    p.add_argument("--min-support", type=float, default=_env("FA_MIN_SUPPORT", 0.092))
+    p.add_argument("--device", choices=["auto", "cuda", "cpu"], default=_env("FA_DEVICE", "auto"))
+    p.add_argument("--dedup", choices=["auto", "on", "off"], default=_env("FA_DEDUP", "auto"))
+    p.add_argument("--pair-strategy", choices=["auto", "horizontal", "gram"],
+                   default=_env("FA_PAIR_STRATEGY", "auto"))
+    p.add_argument("--with-counts", action="store_true", default=_env("FA_WITH_COUNTS", False))
+    p.add_argument("--resume", action="store_true", default=_env("FA_RESUME", False))
+    p.add_argument("--rules-only", action="store_true", default=_env("FA_RULES_ONLY", False))
+    p.add_argument("--no-checkpoint", dest="checkpoint", action="store_false", default=True)
+    p.add_argument("--overwrite", action="store_true", default=_env("FA_OVERWRITE", False))
+    p.add_argument("--profile", action="store_true", default=_env("FA_PROFILE", False))
+    p.add_argument("--metrics", dest="metrics_path", default=os.environ.get("FA_METRICS"))
+    p.add_argument("--max-level", type=int, default=_env("FA_MAX_LEVEL", 0))
+    return p
+
+
+def parse_args(argv=None) -> JobConfig:
+    a = build_parser().parse_args(argv)
+    return JobConfig(input=a.input, output=a.output, temp=a.temp, min_support=a.min_support, device=a.device,
+                     dedup=a.dedup, pair_strategy=a.pair_strategy, with_counts=a.with_counts, resume=a.resume,
+                     rules_only=a.rules_only, checkpoint=a.checkpoint, overwrite=a.overwrite,
+                     profile=a.profile, metrics_path=a.metrics_path, max_level=a.max_level)

@@ -1,0 +1,357 @@
+"""FastApriori: level-wise frequent-itemset mining, count-distributed over GPUs.
+
+Reference: FastApriori.scala (class FastApriori, :18-248).  Same observable
+result — every itemset with support >= ceil(minSupport * N), F1 counted over
+token occurrences, k >= 2 over distinct sets of transactions keeping >= 2
+frequent items — computed the MI355X way:
+
+  reference (Spark)                               here (per rank, then RCCL)
+  ---------------------------------------------   --------------------------------------------
+  flatMap/reduceByKey histogram (:55-58)          HIP LDS histogram + all_reduce(int64[V])
+  rank by count (:60-62)                          identical host sort on every rank
+  map->set->filter(size>1)->reduceByKey (:66-79)  HIP compress to sorted rank rows (+ optional
+                                                  hash dedup into weight classes)
+  F1 Spark jobs -> Boolean[T] per item (:195-210) HIP LDS-tiled build of uint64 bitmaps [F1][W]
+  broadcast bitmaps, pairs parallelize (:212-241) HIP pair kernel (sparse: LDS pair tile from
+                                                  rank rows; dense: bit-matrix Gram) +
+                                                  all_reduce of the pair counts
+  genCandidates (:167-193)                        C++ apriori_gen (identical on all ranks)
+  genNextFreqItemsets (:132-160)                  HIP prefix-shared AND+popcount per group +
+                                                  all_reduce(int64[C_k])
+
+Transactions are sharded (count distribution); candidate lists and results
+are replicated, so the only traffic is one count vector per level.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..ops.host import apriori_gen
+from ..parallel.comm import Comm
+from ..utils.jvm import java_string_key, min_count
+from ..utils.metrics import Logger, roctx_range
+from .data import MiningResult, TransactionShard
+
+# Cost-model constants for choosing the k = 2 kernel (calibrated on MI355X; see
+# docs/PERF.md).  Work units: pair increments for the horizontal kernel, 64-bit
+# word pairs for the Gram kernel.
+HORIZONTAL_PAIRS_PER_S = 2.0e11
+GRAM_WORDPAIRS_PER_S = 1.2e13
+
+
+@dataclass
+class MinerConfig:
+    min_support: float = 0.092
+    dedup: str = "auto"             # auto | on | off
+    pair_strategy: str = "auto"     # auto | horizontal | gram
+    dedup_threshold: float = 0.8    # dedup when distinct/T below this (auto)
+    max_level: int = 0              # 0 = unlimited
+
+
+class FastApriori:
+    """Level-wise miner.  ``run(shard)`` on every rank returns the same MiningResult."""
+
+    def __init__(self, min_support: float = 0.092, comm: Comm | None = None, config: MinerConfig | None = None,
+                 logger: Logger | None = None, checkpoint=None):
+        self.cfg = config or MinerConfig(min_support=min_support)
+        self.cfg.min_support = min_support if config is None else self.cfg.min_support
+        self.comm = comm or Comm()
+        self.log = logger or Logger(self.comm.rank)
+        self.ckpt = checkpoint
+        self.stats: dict = {}
+
+    # fluent setters of the reference (FastApriori.scala:21-29)
+    def set_min_support(self, v: float) -> "FastApriori":
+        self.cfg.min_support = float(v)
+        return self
+
+    # ------------------------------------------------------------------
+    def run(self, shard: TransactionShard, resume: MiningResult | None = None) -> MiningResult:
+        t_start = time.perf_counter()
+        comm, dev = self.comm, shard.items.device
+        n_global = comm.allreduce_int(shard.n_lines)
+        mc = min_count(self.cfg.min_support, n_global)
+        self.stats = {"n_lines": n_global, "min_count": mc}
+
+        with roctx_range("F1"):
+            items, counts1, lut = self._frequent_items(shard, mc)
+        F1 = len(items)
+        self.log.line(f"1 freq items {F1}")
+        levels = [np.arange(F1, dtype=np.int32).reshape(-1, 1)]
+        counts = [counts1]
+        result = MiningResult(items, levels, counts, mc, n_global, self.stats)
+        if resume is not None:
+            self._check_resume(resume, result)
+        if self.ckpt is not None:
+            self.ckpt.save_level(result, 1)
+        if F1 < 2:
+            return self._finish(result, t_start)
+
+        with roctx_range("compress"):
+            db = self._compress(shard, lut, F1)
+        self.stats.update(T=db["T_global"], distinct=db["ncols_global"])
+
+        # ---- k = 2 -----------------------------------------------------
+        t0 = time.perf_counter()
+        if resume is not None and len(resume.levels) >= 2:
+            levels.append(resume.levels[1]); counts.append(resume.counts[1])
+        else:
+            with roctx_range("pairs"):
+                rows2, cnt2 = self._pairs(db, F1, mc)
+            levels.append(rows2); counts.append(cnt2)
+            if self.ckpt is not None:
+                self.ckpt.save_level(result, 2)
+        self.log.line(f"2 candidates items {F1 * (F1 - 1) // 2}")
+        self.log.line(f"2 freq items {len(levels[1])}")
+        self.log.line(f"Use Time 2 items {int((time.perf_counter() - t0) * 1000)}")
+        self.log.metric(phase="level", k=2, candidates=F1 * (F1 - 1) // 2, frequent=len(levels[1]),
+                        ms=(time.perf_counter() - t0) * 1e3, strategy=self.stats.get("pair_strategy"))
+
+        # ---- k >= 3 ----------------------------------------------------
+        k = 3
+        while len(levels[-1]) >= k and (self.cfg.max_level == 0 or k <= self.cfg.max_level):
+            t0 = time.perf_counter()
+            if resume is not None and len(resume.levels) >= k:
+                levels.append(resume.levels[k - 1]); counts.append(resume.counts[k - 1])
+                k += 1
+                continue
+            with roctx_range(f"level{k}"):
+                prefix_idx, ext_off, ext = apriori_gen(levels[-1])
+                C = int(ext.size)
+                self.log.line(f"{k} candidate items {C}")
+                if C == 0:
+                    levels.append(np.zeros((0, k), np.int32)); counts.append(np.zeros(0, np.int64))
+                    self.log.line(f"{k} freq items 0")
+                    break
+                cnt = self._count_level(db, levels[-1], prefix_idx, ext_off, ext)
+                keep = cnt >= mc
+                g_of_e = np.repeat(np.arange(prefix_idx.size), np.diff(ext_off))
+                rows = np.concatenate([levels[-1][prefix_idx[g_of_e[keep]]], ext[keep, None]], axis=1)
+                levels.append(np.ascontiguousarray(rows, dtype=np.int32))
+                counts.append(cnt[keep].astype(np.int64))
+            ms = (time.perf_counter() - t0) * 1e3
+            self.log.line(f"{k} freq items {len(levels[-1])}")
+            self.log.line(f"Use Time {k} items {int(ms)}")
+            self.log.metric(phase="level", k=k, candidates=C, frequent=len(levels[-1]), ms=ms,
+                            groups=int(prefix_idx.size))
+            if self.ckpt is not None:
+                self.ckpt.save_level(result, k)
+            k += 1
+        # drop a trailing empty level (the reference never emits empty levels)
+        while len(levels) > 1 and len(levels[-1]) == 0:
+            levels.pop(); counts.pop()
+        return self._finish(result, t_start)
+
+    def _finish(self, result: MiningResult, t_start: float) -> MiningResult:
+        total_k2 = sum(len(c) for c in result.counts[1:])
+        self.log.line(f"Total freq items sets {total_k2}")
+        self.stats["mine_ms"] = (time.perf_counter() - t_start) * 1e3
+        self.stats["n_itemsets"] = result.n_itemsets
+        self.stats["bytes_reduced"] = self.comm.bytes_reduced
+        return result
+
+    def _check_resume(self, resume: MiningResult, fresh: MiningResult) -> None:
+        if resume.items != fresh.items or not np.array_equal(resume.counts[0], fresh.counts[0]):
+            raise ValueError("checkpoint does not match the input data (different F1)")
+
+    # ------------------------------------------------------------------
+    # F1: histogram, all-reduce, ranking (FastApriori.scala:46-62)
+    # ------------------------------------------------------------------
+    def _frequent_items(self, shard: TransactionShard, mc: int):
+        comm, vocab, dev = self.comm, shard.vocab, shard.items.device
+        thr = max(mc, 1)   # only tokens that occur can be frequent (even at minSupport 0)
+        if vocab.numeric:
+            V = comm.allreduce_int(vocab.size, "max")
+            hist = ops.histogram(shard.items, V)
+            if shard.extras.size:
+                hist += torch.bincount(torch.from_numpy(shard.extras.astype(np.int64)), minlength=V).to(dev)
+            comm.all_reduce_(hist)
+            fid = torch.nonzero(hist >= thr).flatten()
+            fcnt = hist[fid].cpu().numpy()
+            fid = fid.cpu().numpy()
+            tokens = [vocab.token(int(i)) for i in fid]
+            order = sorted(range(len(fid)), key=lambda j: (-int(fcnt[j]), java_string_key(tokens[j])))
+            items = [tokens[j] for j in order]
+            counts1 = fcnt[order].astype(np.int64)
+            lut = torch.full((max(V, 1),), -1, dtype=torch.int32)
+            if len(order):
+                lut[torch.from_numpy(fid[order].astype(np.int64))] = torch.arange(len(order), dtype=torch.int32)
+            return items, counts1, lut.to(dev)
+        # dictionary mode: agree on identity through 64-bit token hashes
+        Vl = vocab.size
+        hist = ops.histogram(shard.items, max(Vl, 1)).cpu().numpy()[:Vl]
+        if shard.extras.size:
+            hist = hist + np.bincount(shard.extras, minlength=Vl)[:Vl]
+        hashes = vocab.hashes.astype(np.uint64)
+        if np.unique(hashes).size != Vl:
+            raise RuntimeError("64-bit token hash collision inside one shard")
+        if comm.distributed:
+            owner = (hashes % np.uint64(comm.world_size)).astype(np.int64)
+            send_h = [hashes[owner == r].view(np.int64) for r in range(comm.world_size)]
+            send_c = [hist[owner == r].astype(np.int64) for r in range(comm.world_size)]
+            rh = np.concatenate(comm.all_to_all_varlen(send_h))
+            rc = np.concatenate(comm.all_to_all_varlen(send_c))
+            uh, inv = np.unique(rh, return_inverse=True)
+            tot = np.bincount(inv, weights=rc, minlength=uh.size).astype(np.int64)
+            mine = uh[tot >= thr], tot[tot >= thr]
+            gathered = comm.all_gather_object((mine[0].tolist(), mine[1].tolist()))
+            freq = {}
+            for hs, cs in gathered:
+                freq.update(zip(hs, cs))
+            local_idx = {int(h): i for i, h in enumerate(hashes.view(np.int64).tolist())}
+            strs = {h: vocab.strings[local_idx[h]] for h in freq if h in local_idx}
+            allstrs = {}
+            for d in comm.all_gather_object(strs):
+                allstrs.update(d)
+            entries = [(h, c, allstrs[h]) for h, c in freq.items()]
+        else:
+            sel = np.nonzero(hist >= thr)[0]
+            entries = [(int(hashes.view(np.int64)[i]), int(hist[i]), vocab.strings[i]) for i in sel]
+        entries.sort(key=lambda e: (-e[1], java_string_key(e[2])))
+        items = [e[2] for e in entries]
+        counts1 = np.array([e[1] for e in entries], dtype=np.int64)
+        rank_of_hash = {e[0]: r for r, e in enumerate(entries)}
+        lut_np = np.full(max(Vl, 1), -1, dtype=np.int32)
+        for i, h in enumerate(hashes.view(np.int64).tolist()):
+            r = rank_of_hash.get(h)
+            if r is not None:
+                lut_np[i] = r
+        return items, counts1, torch.from_numpy(lut_np).to(dev)
+
+    # ------------------------------------------------------------------
+    # Compression (FastApriori.scala:66-79) and the vertical layout
+    # ------------------------------------------------------------------
+    def _compress(self, shard: TransactionShard, lut: torch.Tensor, F1: int) -> dict:
+        dev = shard.items.device
+        cnt = ops.txn_freq_count(shard.offsets, shard.items, lut)
+        kept = torch.nonzero(cnt >= 2).flatten().to(torch.int32)
+        T = kept.numel()
+        roff = torch.zeros(T + 1, dtype=torch.int64, device=dev)
+        if T:
+            torch.cumsum(cnt[kept.to(torch.int64)].to(torch.int64), 0, out=roff[1:])
+        ranks = ops.compress(shard.offsets, shard.items, lut, kept, roff)
+        db = {"roff": roff, "ranks": ranks, "T": T, "src": None, "ncols": T, "wword": None, "wrow": None,
+              "bm": None, "W": 0, "F1": F1}
+        pair_work = 0
+        if T:
+            lens = roff[1:] - roff[:-1]
+            pair_work = int((lens * (lens - 1) // 2).sum().item())
+        db["pair_work"] = pair_work
+        if self._want_dedup(db):
+            self._dedup(db)
+        db["T_global"] = self.comm.allreduce_int(T)
+        db["ncols_global"] = self.comm.allreduce_int(db["ncols"] if db["src"] is None else db["n_distinct"])
+        self.log.metric(phase="compress", T=T, distinct=db.get("n_distinct", T), nnz=int(ranks.numel()))
+        return db
+
+    def _want_dedup(self, db) -> bool:
+        mode = self.cfg.dedup
+        if mode == "off" or db["T"] < 2:
+            decision = False
+        elif mode == "on":
+            decision = True
+        else:
+            # estimate the distinct fraction on a prefix sample of the rows
+            n = min(db["T"], 1 << 20)
+            sub_off = db["roff"][: n + 1]
+            h1, _ = ops.row_hash(sub_off, db["ranks"][: int(sub_off[-1].item())])
+            frac = torch.unique(h1).numel() / max(n, 1)
+            decision = frac < self.cfg.dedup_threshold
+        # every rank must take the same decision (the layout differs)
+        return bool(self.comm.allreduce_int(int(decision), "max"))
+
+    def _dedup(self, db) -> None:
+        """Merge identical compressed rows into weight classes (FastApriori.scala:71-79).
+
+        Columns are ordered by weight (unit weight first) and every class is padded
+        to a multiple of 64 columns, so each bitmap word carries exactly one weight.
+        """
+        roff, ranks, T = db["roff"], db["ranks"], db["T"]
+        dev = ranks.device
+        h1, h2 = ops.row_hash(roff, ranks)
+        o = torch.argsort(h2, stable=True)
+        o = o[torch.argsort(h1[o], stable=True)]
+        a1, a2 = h1[o], h2[o]
+        new = torch.ones(T, dtype=torch.bool, device=dev)
+        new[1:] = (a1[1:] != a1[:-1]) | (a2[1:] != a2[:-1])
+        run = torch.cumsum(new.to(torch.int64), 0) - 1
+        nd = int(run[-1].item()) + 1
+        weight = torch.bincount(run, minlength=nd)
+        rep = o[new]                                   # one representative kept row per run
+        wo = torch.argsort(weight, stable=True)
+        w_sorted, rep_sorted = weight[wo], rep[wo]
+        cls_w, cls_n = torch.unique_consecutive(w_sorted, return_counts=True)
+        padded = (cls_n + 63) // 64 * 64
+        cls_col0 = torch.cumsum(padded, 0) - padded
+        cls_first = torch.cumsum(cls_n, 0) - cls_n
+        cls_of = torch.repeat_interleave(torch.arange(cls_n.numel(), device=dev), cls_n)
+        col = cls_col0[cls_of] + (torch.arange(nd, device=dev) - cls_first[cls_of])
+        ncols = int(padded.sum().item())
+        src = torch.full((ncols,), -1, dtype=torch.int32, device=dev)
+        src[col] = rep_sorted.to(torch.int32)
+        wword = torch.repeat_interleave(cls_w.to(torch.int32), padded // 64)
+        wrow = torch.zeros(T, dtype=torch.int32, device=dev)
+        wrow[rep] = weight.to(torch.int32)
+        db.update(src=src, ncols=ncols, wword=wword, wrow=wrow, n_distinct=nd)
+
+    def _bitmaps(self, db) -> None:
+        if db["bm"] is None:
+            with roctx_range("bitmaps"):
+                bm, W = ops.build_bitmaps(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"])
+            db["bm"], db["W"] = bm, W
+
+    # ------------------------------------------------------------------
+    # k = 2 (FastApriori.scala:212-241)
+    # ------------------------------------------------------------------
+    def _pick_pair_strategy(self, db, F1: int) -> str:
+        s = self.cfg.pair_strategy
+        if s != "auto":
+            return s
+        W = (db["ncols"] + 63) // 64
+        t_h = db["pair_work"] / HORIZONTAL_PAIRS_PER_S
+        t_g = (F1 * (F1 - 1) / 2) * W / GRAM_WORDPAIRS_PER_S
+        # ranks must agree: decide on the global work
+        pick_gram = t_g < t_h
+        return "gram" if self.comm.allreduce_int(int(pick_gram), "max") else "horizontal"
+
+    def _pairs(self, db, F1: int, mc: int):
+        strat = self._pick_pair_strategy(db, F1)
+        self.stats["pair_strategy"] = strat
+        if strat == "gram":
+            self._bitmaps(db)
+            pc = ops.pair_counts_gram(db["bm"], db["W"], db["wword"])
+        else:
+            pc = ops.pair_counts_horizontal(db["roff"], db["ranks"], db["wrow"], F1)
+        iu = torch.triu_indices(F1, F1, 1, device=pc.device)
+        flat = pc[iu[0], iu[1]].contiguous()
+        self.comm.all_reduce_(flat)
+        keep = torch.nonzero(flat >= mc).flatten()
+        rows = torch.stack([iu[0][keep], iu[1][keep]], 1).to(torch.int32).cpu().numpy()
+        cnt = flat[keep].cpu().numpy().astype(np.int64)
+        return np.ascontiguousarray(rows), cnt
+
+    # ------------------------------------------------------------------
+    # k >= 3 (FastApriori.scala:132-160)
+    # ------------------------------------------------------------------
+    def _count_level(self, db, prev: np.ndarray, prefix_idx, ext_off, ext) -> np.ndarray:
+        self._bitmaps(db)
+        dev = db["ranks"].device
+        prefix = torch.from_numpy(np.ascontiguousarray(prev[prefix_idx], dtype=np.int32)).to(dev)
+        ext_t = torch.from_numpy(np.ascontiguousarray(ext, dtype=np.int32)).to(dev)
+        cnt = ops.count_candidates(db["bm"], db["W"], prefix, ext_off, ext_t, db["wword"])
+        self.comm.all_reduce_(cnt)
+        return cnt.cpu().numpy()
+
+
+def mine(shard: TransactionShard, min_support: float = 0.092, comm: Comm | None = None, **kw) -> MiningResult:
+    cfg = MinerConfig(min_support=min_support, **kw)
+    return FastApriori(min_support, comm, cfg).run(shard)
+
+
+__all__ = ["FastApriori", "MinerConfig", "mine", "math"]

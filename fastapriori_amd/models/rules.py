@@ -1,0 +1,110 @@
+"""AssociationRules: rule generation, redundancy cut, ordering, recommendation.
+
+Reference: AssociationRules.scala (class AssociationRules, :17-190).
+
+  reference (Spark)                                  here
+  -------------------------------------------------  -----------------------------------------------
+  removeRedundancy: zipWithIndex, map to rank sets,  native parse of this rank's U.dat byte range,
+    reduceByKey dedup, collectAsMap (:33-64)         LUT to ranks on the device (empty -> "0")
+  genRules: linear scan for S - {s} (:122-145)       C++ subset index by binary search
+  cut, level by level (:147-182)                     C++ hash lookups of the kept lower level
+  sortWith(conf desc, token.toInt) (:74, :116-120)   C++ stable sort with precomputed tie positions
+  per-basket first-match scan (:80-106)              HIP: one wave per basket, 64 rules per step,
+                                                     __ballot + ffs for the earliest match
+  collect to driver + saveRecommends                 gather of rank ids to rank 0
+
+Divergences (documented): when there are no rules at all the reference throws
+on ``rules.keys.min`` (:147); we recommend "0" for every user.  Non-integer
+consequent tokens in a confidence tie would throw NumberFormatException there;
+we order them after the integers by Java string order.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..ops.host import RuleTable, rules_build
+from ..parallel.comm import Comm
+from ..utils.jvm import rule_tiebreak_key
+from ..utils.metrics import Logger
+from .data import MiningResult, TransactionShard, Vocabulary
+
+
+class AssociationRules:
+    def __init__(self, result: MiningResult, comm: Comm | None = None, logger: Logger | None = None):
+        self.result = result
+        self.comm = comm or Comm()
+        self.log = logger or Logger(self.comm.rank)
+        self._rules: RuleTable | None = None
+        self._rules_dev = None
+
+    # ------------------------------------------------------------------
+    def rules(self) -> RuleTable:
+        if self._rules is None:
+            items = self.result.items
+            order = sorted(range(len(items)), key=lambda r: rule_tiebreak_key(items[r]))
+            tie_pos = np.empty(len(items), dtype=np.int64)
+            tie_pos[np.asarray(order, dtype=np.int64)] = np.arange(len(items), dtype=np.int64)
+            self._rules = rules_build(self.result.levels, self.result.counts, tie_pos)
+            for size, before, after in self._rules.level_stats[1:]:
+                self.log.line(f"Before cut level {size} Nums: {before}")
+                self.log.line(f"After cut level {size} Nums: {after}")
+            self.log.line(f"Size association rules {self._rules.n_rules}")
+        return self._rules
+
+    def rule_list(self) -> list[tuple[tuple[int, ...], int, float]]:
+        rt = self.rules()
+        return [(tuple(rt.antecedent(i).tolist()), int(rt.cons[i]), float(rt.conf[i]))
+                for i in range(rt.n_rules)]
+
+    # ------------------------------------------------------------------
+    def _rank_lut(self, vocab: Vocabulary) -> np.ndarray:
+        """User-shard id -> rank (-1 when the token is not a frequent item)."""
+        lut = np.full(max(vocab.size, 1), -1, dtype=np.int32)
+        if vocab.numeric:
+            for r, t in enumerate(self.result.items):
+                i = Vocabulary.numeric_id(t)
+                if 0 <= i < vocab.size:
+                    lut[i] = r
+        else:
+            rank = {t: r for r, t in enumerate(self.result.items)}
+            for i, s in enumerate(vocab.strings):
+                r = rank.get(s)
+                if r is not None:
+                    lut[i] = r
+        return lut
+
+    def recommend_shard(self, users: TransactionShard) -> torch.Tensor:
+        """Recommended rank per local U.dat line (-1 = "0"), on the users' device."""
+        rt = self.rules()
+        dev = users.items.device
+        lut = torch.from_numpy(self._rank_lut(users.vocab)).to(dev)
+        n = users.n_lines
+        if n == 0:
+            return torch.zeros(0, dtype=torch.int32, device=dev)
+        r = lut[users.items.to(torch.int64)] if users.items.numel() else users.items
+        keep = r >= 0
+        lens = users.offsets[1:] - users.offsets[:-1]
+        row = torch.repeat_interleave(torch.arange(n, device=dev), lens)
+        bcnt = torch.bincount(row[keep], minlength=n)
+        boff = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(bcnt, 0, out=boff[1:])
+        bask = r[keep].to(torch.int32).contiguous()
+        if self._rules_dev is None or self._rules_dev[0] != dev:
+            self._rules_dev = (dev, torch.from_numpy(rt.ante_off).to(dev), torch.from_numpy(rt.ante).to(dev),
+                               torch.from_numpy(rt.cons).to(dev))
+        _, a_off, ante, cons = self._rules_dev
+        return ops.recommend(a_off, ante, cons, len(self.result.items), boff, bask)
+
+    def run(self, users: TransactionShard) -> list[str] | None:
+        """Recommendations for every U.dat line, in file order, on rank 0 (None elsewhere)."""
+        rec = self.recommend_shard(users)
+        parts = self.comm.gather_varlen(rec)
+        if parts is None:
+            return None
+        items = self.result.items
+        out = []
+        for p in parts:
+            out.extend("0" if v < 0 else items[v] for v in p.tolist())
+        return out

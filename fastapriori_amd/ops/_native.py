@@ -1,0 +1,108 @@
+"""ctypes bindings for libfa_host.so (C++ runtime) and libfa_hip.so (CDNA4 kernels).
+
+The HIP library links ``libamdhip64.so.7``; torch ships a runtime with the same
+SONAME, so ``torch`` is imported (and its HIP runtime loaded) before the kernel
+library is dlopen'ed — both then share one runtime and torch's streams are valid
+handles for our launchers.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+from . import build as _build
+
+_lock = threading.Lock()
+_host = None
+_hip = None
+
+i32, i64, u64, dbl = C.c_int32, C.c_int64, C.c_uint64, C.c_double
+vp, cp = C.c_void_p, C.c_char_p
+I64P = C.POINTER(C.c_int64)
+IP = C.POINTER(C.c_int)
+
+_HOST_SIGS = {
+    "fa_parse_file": (vp, [cp, i64, i64, C.c_int, C.c_int, IP]),
+    "fa_parse_buffer": (vp, [cp, i64, C.c_int, C.c_int]),
+    "fa_file_size": (i64, [cp]),
+    "fa_next_line_start": (i64, [cp, i64, i64]),
+    "fa_txndb_info": (None, [vp, vp]),
+    "fa_txndb_export": (None, [vp, vp, vp, vp, C.c_int]),
+    "fa_txndb_export_dict": (None, [vp, vp, vp, vp]),
+    "fa_txndb_free": (None, [vp]),
+    "fa_hash_bytes": (u64, [cp, i64]),
+    "fa_quest_generate": (vp, [i64, i64, dbl, dbl, i64, i64, u64, C.c_int, C.c_int]),
+    "fa_quest_write": (C.c_int, [cp, i64, dbl, dbl, i64, i64, u64, C.c_int, C.c_int]),
+    "fa_apriori_gen": (vp, [vp, i64, C.c_int, C.c_int, vp]),
+    "fa_cands_export": (None, [vp, vp, vp, vp]),
+    "fa_cands_free": (None, [vp]),
+    "fa_rules_build": (vp, [vp, vp, vp, C.c_int, vp, C.c_int, vp]),
+    "fa_rules_nante": (i64, [vp]),
+    "fa_rules_nstats": (i64, [vp]),
+    "fa_rules_export": (None, [vp, vp, vp, vp, vp, vp]),
+    "fa_rules_free": (None, [vp]),
+    "fa_recommend_cpu": (None, [vp, vp, vp, i64, i32, vp, vp, i64, vp, C.c_int]),
+    "fa_write_freq_itemsets": (C.c_int, [cp, vp, vp, i32, vp, vp, vp, C.c_int, C.c_int, C.c_int]),
+    "fa_cpu_histogram": (None, [vp, i64, i64, vp, C.c_int]),
+    "fa_cpu_txn_freq_count": (None, [vp, vp, i64, vp, vp, C.c_int]),
+    "fa_cpu_build_bitmaps": (None, [vp, vp, vp, i64, i64, vp, C.c_int]),
+    "fa_cpu_row_hash": (None, [vp, vp, i64, vp, vp, C.c_int]),
+    "fa_cpu_pair_gram": (None, [vp, i32, i64, i64, vp, vp, C.c_int]),
+    "fa_cpu_pair_horizontal": (None, [vp, vp, i64, vp, i32, vp, C.c_int]),
+    "fa_cpu_count_candidates": (None, [vp, i64, i64, vp, i32, vp, vp, i64, vp, vp, C.c_int]),
+}
+
+_HIP_SIGS = {
+    "fa_hip_histogram": (C.c_int, [vp, i64, i32, vp, vp]),
+    "fa_hip_txn_freq_count": (C.c_int, [vp, vp, i64, vp, vp, vp]),
+    "fa_hip_compress_regs": (C.c_int, [C.c_int, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp]),
+    "fa_hip_compress_lds": (C.c_int, [vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp]),
+    "fa_hip_row_hash": (C.c_int, [vp, vp, i64, vp, vp, vp]),
+    "fa_hip_build_bitmaps": (C.c_int, [vp, vp, vp, i64, i32, i64, C.c_int, C.c_int, vp, vp]),
+    "fa_hip_pair_horizontal": (C.c_int, [vp, vp, i64, vp, i32, vp, C.c_int, vp]),
+    "fa_hip_pair_gram_popc": (C.c_int, [vp, i32, i64, i64, vp, vp, C.c_int, vp]),
+    "fa_hip_count_candidates": (C.c_int, [vp, i64, i64, vp, C.c_int, vp, vp, vp, C.c_int, vp, vp, vp]),
+    "fa_hip_recommend": (C.c_int, [vp, vp, vp, i64, i32, vp, vp, i64, vp, vp]),
+}
+
+
+def _declare(lib, sigs):
+    for name, (res, args) in sigs.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+def host():
+    global _host
+    if _host is None:
+        with _lock:
+            if _host is None:
+                path = _build.HOST_LIB
+                if not os.path.exists(path):
+                    _build.build_host()
+                _host = _declare(C.CDLL(path), _HOST_SIGS)
+    return _host
+
+
+def hip():
+    """The kernel library.  Raises loudly when it is missing: there is no fallback."""
+    global _hip
+    if _hip is None:
+        with _lock:
+            if _hip is None:
+                import torch  # noqa: F401  (load torch's HIP runtime first; see module doc)
+                path = _build.HIP_LIB
+                if not os.path.exists(path):
+                    raise RuntimeError(
+                        f"{path} is missing: build it with `python -m fastapriori_amd.ops.build` "
+                        "(the GPU path has no non-native fallback)")
+                _hip = _declare(C.CDLL(path), _HIP_SIGS)
+    return _hip
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with HIP error code {rc}")

@@ -1,0 +1,262 @@
+"""Typed wrappers over the mining primitives.
+
+Every op takes torch tensors and runs where they live:
+  * CUDA (= HIP on ROCm) tensors -> the hand-written CDNA4 kernels in libfa_hip.so,
+    launched on torch's current stream.  There is no silent fallback: a missing
+    library raises.
+  * CPU tensors -> the C++ reference implementations in libfa_host.so (used by
+    the gloo multi-process tests and the CPU plumbing config).
+
+Conventions: bitmaps are int64 tensors [F1, Wp] holding raw 64-bit words
+(column c = bit c&63 of word c>>6); counts come back as int64.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..utils.env import num_threads
+from . import _native
+
+_I32, _I64 = torch.int32, torch.int64
+
+
+def _p(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _hip_call(name: str, *args) -> None:
+    rc = getattr(_native.hip(), name)(*args)
+    _native.check(rc, name)
+
+
+# ---------------------------------------------------------------------------
+def histogram(items: torch.Tensor, V: int) -> torch.Tensor:
+    """Occurrences of each id in ``items`` (int32) -> int64 [V]."""
+    assert items.dtype == _I32 and items.is_contiguous()
+    if items.is_cuda:
+        out = torch.zeros(V, dtype=_I32, device=items.device)
+        if items.numel():
+            _hip_call("fa_hip_histogram", _p(items), items.numel(), V, _p(out), _stream(items))
+        return out.to(_I64)
+    out = torch.zeros(V, dtype=_I64)
+    _native.host().fa_cpu_histogram(_p(items), items.numel(), V, _p(out), num_threads())
+    return out
+
+
+def txn_freq_count(offsets: torch.Tensor, items: torch.Tensor, lut: torch.Tensor) -> torch.Tensor:
+    """Number of frequent ids (``lut[id] >= 0``) per transaction -> int32 [n]."""
+    n = offsets.numel() - 1
+    out = torch.empty(n, dtype=_I32, device=items.device)
+    if n <= 0:
+        return out
+    if items.is_cuda:
+        _hip_call("fa_hip_txn_freq_count", _p(offsets), _p(items), n, _p(lut), _p(out), _stream(items))
+    else:
+        _native.host().fa_cpu_txn_freq_count(_p(offsets), _p(items), n, _p(lut), _p(out), num_threads())
+    return out
+
+
+def compress(offsets, items, lut, kept, roff) -> torch.Tensor:
+    """Kept transaction x -> its frequent ranks sorted ascending, CSR by ``roff``."""
+    T = kept.numel()
+    nnz = int(roff[-1].item()) if T else 0
+    ranks = torch.empty(max(nnz, 1), dtype=_I32, device=items.device)
+    if T == 0:
+        return ranks[:0]
+    if not items.is_cuda:
+        return _compress_torch(offsets, items, lut, kept, roff, ranks, None)[:nnz]
+    st = _stream(items)
+    over = torch.empty(T, dtype=_I32, device=items.device)
+    n_over = torch.zeros(1, dtype=_I32, device=items.device)
+    _hip_call("fa_hip_compress_regs", 16, _p(offsets), _p(items), _p(lut), None, T, _p(kept), _p(roff),
+              _p(ranks), _p(over), _p(n_over), st)
+    n1 = int(n_over.item())
+    if n1:
+        over2 = torch.empty(n1, dtype=_I32, device=items.device)
+        n_over2 = torch.zeros(1, dtype=_I32, device=items.device)
+        _hip_call("fa_hip_compress_regs", 64, _p(offsets), _p(items), _p(lut), _p(over), n1, _p(kept),
+                  _p(roff), _p(ranks), _p(over2), _p(n_over2), st)
+        n2 = int(n_over2.item())
+        if n2:
+            over3 = torch.empty(n2, dtype=_I32, device=items.device)
+            n_over3 = torch.zeros(1, dtype=_I32, device=items.device)
+            _hip_call("fa_hip_compress_lds", _p(offsets), _p(items), _p(lut), _p(over2), n2, _p(kept),
+                      _p(roff), _p(ranks), _p(over3), _p(n_over3), st)
+            n3 = int(n_over3.item())
+            if n3:   # rows longer than 16384 tokens: sorted by torch, row by row
+                _compress_torch(offsets, items, lut, kept, roff, ranks, over3[:n3])
+    return ranks[:nnz]
+
+
+def _compress_torch(offsets, items, lut, kept, roff, ranks, rows):
+    """Torch implementation: all rows vectorised (rows=None) or the listed rows."""
+    if rows is not None:
+        for x in rows.tolist():
+            t = int(kept[x].item())
+            r = lut[items[offsets[t]:offsets[t + 1]].to(_I64)]
+            r = torch.sort(r[r >= 0]).values
+            ranks[int(roff[x].item()): int(roff[x + 1].item())] = r.to(_I32)
+        return ranks
+    dev = items.device
+    t = kept.to(_I64)
+    starts = offsets[t]
+    lens = offsets[t + 1] - starts
+    total = int(lens.sum().item())
+    rowid = torch.repeat_interleave(torch.arange(t.numel(), device=dev), lens)
+    seg0 = torch.repeat_interleave(torch.cumsum(lens, 0) - lens, lens)
+    pos = torch.arange(total, device=dev) - seg0 + torch.repeat_interleave(starts, lens)
+    r = lut[items[pos].to(_I64)].to(_I64)
+    keep = r >= 0
+    base = int(lut.max().item()) + 1
+    key, _ = torch.sort(rowid[keep] * base + r[keep])
+    ranks[: key.numel()] = (key % base).to(_I32)
+    return ranks[: key.numel()]
+
+
+def row_hash(roff: torch.Tensor, ranks: torch.Tensor):
+    T = roff.numel() - 1
+    h1 = torch.empty(T, dtype=_I64, device=ranks.device)
+    h2 = torch.empty(T, dtype=_I64, device=ranks.device)
+    if T <= 0:
+        return h1, h2
+    if ranks.is_cuda:
+        _hip_call("fa_hip_row_hash", _p(roff), _p(ranks), T, _p(h1), _p(h2), _stream(ranks))
+    else:
+        _native.host().fa_cpu_row_hash(_p(roff), _p(ranks), T, _p(h1), _p(h2), num_threads())
+    return h1, h2
+
+
+def bitmap_geometry(F1: int, ncols: int) -> tuple[int, int, int, int]:
+    """(W, Wp, WT, R): valid words, padded row stride, LDS tile words, ranks per pass."""
+    W = (ncols + 63) // 64
+    WT = 8
+    if F1 > 0:
+        WT = 1 << max(2, min(5, int(np.floor(np.log2(max(1, 8192 // max(F1, 1)))))))
+    R = max(1, min(F1, 8192 // WT)) if F1 > 0 else 1
+    Wp = max(64, (W + 63) // 64 * 64)
+    return W, Wp, WT, R
+
+
+def build_bitmaps(roff, ranks, src, ncols: int, F1: int) -> tuple[torch.Tensor, int]:
+    """Item-major bitmaps [F1, Wp] (int64 words) and the valid word count W."""
+    W, Wp, WT, R = bitmap_geometry(F1, ncols)
+    dev = ranks.device
+    if ranks.is_cuda:
+        bm = torch.empty((max(F1, 1), Wp), dtype=_I64, device=dev)
+        if F1 > 0:
+            _hip_call("fa_hip_build_bitmaps", _p(roff), _p(ranks), _p(src), ncols, F1, Wp, WT, R, _p(bm),
+                      _stream(ranks))
+    else:
+        bm = torch.zeros((max(F1, 1), Wp), dtype=_I64)
+        if F1 > 0:
+            _native.host().fa_cpu_build_bitmaps(_p(roff), _p(ranks), _p(src), ncols, Wp, _p(bm), num_threads())
+    return bm[:F1], W
+
+
+def pair_counts_horizontal(roff, ranks, wrow, F1: int) -> torch.Tensor:
+    T = roff.numel() - 1
+    dev = ranks.device
+    if ranks.is_cuda:
+        out = torch.zeros((F1, F1), dtype=_I32, device=dev)
+        if T > 0 and F1 >= 2:
+            _hip_call("fa_hip_pair_horizontal", _p(roff), _p(ranks), T, _p(wrow), F1, _p(out), 4096,
+                      _stream(ranks))
+        return out.to(_I64)
+    out = torch.zeros((F1, F1), dtype=_I64)
+    if T > 0 and F1 >= 2:
+        _native.host().fa_cpu_pair_horizontal(_p(roff), _p(ranks), T, _p(wrow), F1, _p(out), num_threads())
+    return out
+
+
+def pair_counts_gram(bm: torch.Tensor, W: int, wword) -> torch.Tensor:
+    F1, Wp = bm.shape[0], bm.stride(0)
+    if bm.is_cuda:
+        out = torch.zeros((F1, F1), dtype=_I32, device=bm.device)
+        if W > 0 and F1 >= 2:
+            _hip_call("fa_hip_pair_gram_popc", _p(bm), F1, Wp, W, _p(wword), _p(out), 4096, _stream(bm))
+        return out.to(_I64)
+    out = torch.zeros((F1, F1), dtype=_I64)
+    if W > 0 and F1 >= 2:
+        _native.host().fa_cpu_pair_gram(_p(bm), F1, Wp, W, _p(wword), _p(out), num_threads())
+    return out
+
+
+def _split_groups(ext_off: np.ndarray, per_block: int, max_block_ext: int = 1024):
+    """Host-side work split for the candidate kernel.
+
+    Groups with more than ``max_block_ext`` extensions are cut into several
+    groups sharing a prefix; then consecutive groups are packed into blocks
+    of about ``per_block`` extensions (never more than ``max_block_ext``).
+    Returns (group index per new group, new ext_off, block starts).
+    """
+    G = ext_off.size - 1
+    sizes = np.diff(ext_off)
+    pieces = np.maximum(1, (sizes + max_block_ext - 1) // max_block_ext)
+    gidx = np.repeat(np.arange(G, dtype=np.int64), pieces)
+    first = np.repeat(np.cumsum(pieces) - pieces, pieces)
+    k = np.arange(gidx.size) - first
+    new_off = np.minimum(ext_off[gidx] + k * max_block_ext, ext_off[gidx + 1])
+    new_off = np.append(new_off, ext_off[-1]).astype(np.int64)
+    # greedy packing by extension count
+    starts = [0]
+    acc = 0
+    nsz = np.diff(new_off)
+    lim = max(1, min(per_block, max_block_ext))
+    for i, s in enumerate(nsz.tolist()):
+        if acc + s > lim and acc > 0:
+            starts.append(i)
+            acc = 0
+        acc += s
+    starts.append(nsz.size)
+    return gidx, new_off, np.asarray(starts, dtype=np.int32)
+
+
+def count_candidates(bm: torch.Tensor, W: int, prefix: torch.Tensor, ext_off: np.ndarray,
+                     ext: torch.Tensor, wword) -> torch.Tensor:
+    """Support of every candidate prefix[g] + ext[e] (e in group g) -> int64 [C]."""
+    C = ext.numel()
+    dev = bm.device
+    m = prefix.shape[1] if prefix.dim() == 2 else 0
+    if C == 0:
+        return torch.zeros(0, dtype=_I64, device=dev)
+    if bm.is_cuda:
+        nsc = max(1, (W + 2047) // 2048)
+        per_block = int(np.clip(C * nsc // 4096, 16, 1024))
+        gidx, new_off, starts = _split_groups(ext_off, per_block)
+        pre = prefix[torch.from_numpy(gidx).to(dev)].contiguous() if gidx.size != prefix.shape[0] else prefix
+        off_t = torch.from_numpy(new_off).to(dev)
+        st_t = torch.from_numpy(starts).to(dev)
+        out = torch.zeros(C, dtype=_I32, device=dev)
+        _hip_call("fa_hip_count_candidates", _p(bm), bm.stride(0), W, _p(pre), m, _p(off_t), _p(ext),
+                  _p(st_t), starts.size - 1, _p(wword), _p(out), _stream(bm))
+        return out.to(_I64)
+    out = torch.zeros(C, dtype=_I64)
+    off_t = torch.from_numpy(np.ascontiguousarray(ext_off, dtype=np.int64))
+    _native.host().fa_cpu_count_candidates(_p(bm), bm.stride(0), W, _p(prefix), m, _p(off_t), _p(ext),
+                                           prefix.shape[0], _p(wword), _p(out), num_threads())
+    return out
+
+
+def recommend(ante_off, ante, cons, F1: int, boff, bask) -> torch.Tensor:
+    """First-match recommendation per basket -> int32 rank (or -1 for "0")."""
+    M = boff.numel() - 1
+    R = cons.numel()
+    dev = bask.device
+    out = torch.full((max(M, 0),), -1, dtype=_I32, device=dev)
+    if M <= 0 or R == 0:
+        return out
+    if bask.is_cuda:
+        rc = _native.hip().fa_hip_recommend(_p(ante_off), _p(ante), _p(cons), R, F1, _p(boff), _p(bask), M,
+                                            _p(out), _stream(bask))
+        if rc == 2:  # vocabulary too wide for an LDS bitset: host path
+            return recommend(ante_off.cpu(), ante.cpu(), cons.cpu(), F1, boff.cpu(), bask.cpu()).to(dev)
+        _native.check(rc, "fa_hip_recommend")
+        return out
+    _native.host().fa_recommend_cpu(_p(ante_off), _p(ante), _p(cons), R, F1, _p(boff), _p(bask), M, _p(out),
+                                    num_threads())
+    return out

@@ -1,0 +1,186 @@
+"""Collective communication for count distribution (one process per GPU).
+
+Every rank owns a contiguous shard of the transactions; all ranks hold the
+identical candidate lists and only count vectors move (SURVEY §2.4 plan):
+
+  X3/X8   line / transaction totals          -> all_reduce(int64[1])
+  X4      F1 token histogram                  -> all_reduce(int64[V])
+  X12     pair supports                       -> all_reduce(int64[F1*(F1-1)/2])
+  X15     level-k candidate supports          -> all_reduce(int64[C_k])
+  X17     U.dat line offsets                  -> all_gather(int64[1])
+  X24     recommendations                     -> gather to rank 0
+
+On ROCm the ``nccl`` backend is RCCL, riding xGMI between the GPUs of a node;
+``gloo`` serves CPU-only runs and tests.  Large vectors are reduced in buckets
+sized for xGMI: 7 point-to-point links per GPU mean one ring uses ~2 of them,
+so buckets are a multiple of world_size * 7 chunks and small enough that RCCL
+can pipeline them (``FA_BUCKET_MB``, default 64 MiB).
+"""
+from __future__ import annotations
+
+import os
+import pickle
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class Comm:
+    rank: int = 0
+    world_size: int = 1
+    device: torch.device = torch.device("cpu")
+    backend: str = "none"
+    bytes_reduced: int = 0
+
+    @property
+    def distributed(self) -> bool:
+        return self.world_size > 1
+
+    @property
+    def is_root(self) -> bool:
+        return self.rank == 0
+
+    # -- tensors ------------------------------------------------------------
+    def _comm_device(self) -> torch.device:
+        return self.device if self.backend == "nccl" else torch.device("cpu")
+
+    def all_reduce_(self, t: torch.Tensor, op=None) -> torch.Tensor:
+        """In-place sum (or ``op``) across ranks; returns the tensor on its own device."""
+        if not self.distributed:
+            return t
+        op = op or dist.ReduceOp.SUM
+        dev = self._comm_device()
+        x = t if t.device == dev else t.to(dev)
+        flat = x.view(-1)
+        nbytes = flat.numel() * flat.element_size()
+        self.bytes_reduced += nbytes
+        bucket = self.bucket_elems(flat.element_size())
+        if flat.numel() <= bucket:
+            dist.all_reduce(flat, op=op)
+        else:
+            for s in range(0, flat.numel(), bucket):
+                dist.all_reduce(flat[s:s + bucket], op=op)
+        if x is not t:
+            t.copy_(x)
+        return t
+
+    def bucket_elems(self, elem_size: int) -> int:
+        mb = float(os.environ.get("FA_BUCKET_MB", "64"))
+        n = int(mb * (1 << 20)) // elem_size
+        q = max(1, self.world_size * 7 * 64)
+        return max(q, n // q * q)
+
+    def allreduce_int(self, v: int, op: str = "sum") -> int:
+        if not self.distributed:
+            return int(v)
+        t = torch.tensor([int(v)], dtype=torch.int64, device=self._comm_device())
+        dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+        return int(t.item())
+
+    def all_gather_int(self, v: int) -> list[int]:
+        if not self.distributed:
+            return [int(v)]
+        t = torch.tensor([int(v)], dtype=torch.int64, device=self._comm_device())
+        out = [torch.zeros_like(t) for _ in range(self.world_size)]
+        dist.all_gather(out, t)
+        return [int(x.item()) for x in out]
+
+    def all_gather_object(self, obj) -> list:
+        if not self.distributed:
+            return [obj]
+        out = [None] * self.world_size
+        dist.all_gather_object(out, obj)
+        return out
+
+    def broadcast_object(self, obj, src: int = 0):
+        if not self.distributed:
+            return obj
+        box = [obj]
+        dist.broadcast_object_list(box, src=src)
+        return box[0]
+
+    def gather_varlen(self, t: torch.Tensor) -> list[torch.Tensor] | None:
+        """Gather 1-D tensors of different lengths to rank 0 (None elsewhere)."""
+        if not self.distributed:
+            return [t.cpu()]
+        dev = self._comm_device()
+        sizes = self.all_gather_int(t.numel())
+        mx = max(sizes) if sizes else 0
+        buf = torch.zeros(max(mx, 1), dtype=t.dtype, device=dev)
+        buf[: t.numel()] = t.to(dev)
+        outs = [torch.zeros_like(buf) for _ in range(self.world_size)]
+        dist.all_gather(outs, buf)
+        if not self.is_root:
+            return None
+        return [o[:s].cpu() for o, s in zip(outs, sizes)]
+
+    def all_to_all_varlen(self, parts: list[np.ndarray], dtype=np.int64) -> list[np.ndarray]:
+        """Exchange variable-length int arrays: parts[r] goes to rank r."""
+        if not self.distributed:
+            return [parts[0]]
+        dev = self._comm_device()
+        send_sizes = torch.tensor([p.size for p in parts], dtype=torch.int64, device=dev)
+        recv_sizes = torch.empty_like(send_sizes)
+        dist.all_to_all_single(recv_sizes, send_sizes)
+        rs = recv_sizes.cpu().tolist()
+        send = torch.from_numpy(np.concatenate(parts).astype(dtype)).to(dev) if sum(p.size for p in parts) \
+            else torch.zeros(0, dtype=torch.int64, device=dev)
+        recv = torch.empty(sum(rs), dtype=send.dtype, device=dev)
+        dist.all_to_all_single(recv, send, output_split_sizes=rs,
+                               input_split_sizes=[p.size for p in parts])
+        out = recv.cpu().numpy()
+        res, o = [], 0
+        for s in rs:
+            res.append(out[o:o + s])
+            o += s
+        return res
+
+    def barrier(self) -> None:
+        if self.distributed:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.device.index])
+            else:
+                dist.barrier()
+
+
+def init_comm(device: str | None = None, backend: str | None = None, timeout_s: float = 1800) -> Comm:
+    """Create the communicator from torchrun's env (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*).
+
+    ``device``: "cuda", "cpu" or None (cuda when available).  The backend is
+    RCCL ("nccl") for GPU runs, gloo for CPU runs.
+    """
+    from datetime import timedelta
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if device is None:
+        device = "cuda" if torch.cuda.is_available() else "cpu"
+    if device == "cuda":
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
+    if world <= 1:
+        return Comm(0, 1, dev, "none")
+    be = backend or ("nccl" if dev.type == "cuda" else "gloo")
+    if not dist.is_initialized():
+        kw = dict(backend=be, timeout=timedelta(seconds=timeout_s))
+        if be == "nccl":
+            kw["device_id"] = dev
+        dist.init_process_group(**kw)
+    return Comm(dist.get_rank(), dist.get_world_size(), dev, be)
+
+
+def shutdown_comm(comm: Comm) -> None:
+    if comm.distributed and dist.is_initialized():
+        try:
+            comm.barrier()
+        finally:
+            dist.destroy_process_group()
+
+
+__all__ = ["Comm", "init_comm", "shutdown_comm", "pickle"]

@@ -1,0 +1,217 @@
+"""Input shards and output files (reference formats).
+
+Reading (Utils.scala:19-27): each rank parses the lines that start inside its
+byte range [size*r/W, size*(r+1)/W) of the file with the native mmap parser.
+Writing (Utils.scala:29-49): rank 0 writes Spark-style output directories with
+a single ``part-00000`` plus an empty ``_SUCCESS`` marker.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+import torch
+
+from ..models.data import MiningResult, TransactionShard, Vocabulary
+from ..ops import _native
+from .env import num_threads
+
+
+def _pinned(n: int, dtype, pin: bool) -> torch.Tensor:
+    n = max(n, 1)
+    if pin:
+        try:
+            return torch.empty(n, dtype=dtype, pin_memory=True)
+        except RuntimeError:
+            pass
+    return torch.empty(n, dtype=dtype)
+
+
+def txndb_to_shard(h, device: torch.device, line_base: int = 0) -> TransactionShard:
+    """Export a native TxnDB handle into torch tensors (frees the handle)."""
+    lib = _native.host()
+    info = np.zeros(6, dtype=np.int64)
+    lib.fa_txndb_info(h, info.ctypes.data)
+    n, nnz, nx, numeric, vocab, dbytes = (int(v) for v in info)
+    pin = device.type == "cuda"
+    off = _pinned(n + 1, torch.int64, pin)
+    items = _pinned(nnz, torch.int32, pin)
+    extras = np.zeros(max(nx, 1), dtype=np.int32)
+    lib.fa_txndb_export(h, off.data_ptr(), items.data_ptr(), extras.ctypes.data, num_threads())
+    strings = hashes = None
+    if not numeric:
+        buf = np.zeros(max(dbytes, 1), dtype=np.uint8)
+        soff = np.zeros(vocab + 1, dtype=np.int64)
+        hashes = np.zeros(max(vocab, 1), dtype=np.uint64)
+        lib.fa_txndb_export_dict(h, buf.ctypes.data, soff.ctypes.data, hashes.ctypes.data)
+        raw = buf.tobytes()
+        strings = [raw[soff[i]:soff[i + 1]].decode("utf-8", "replace") for i in range(vocab)]
+        hashes = hashes[:vocab]
+    lib.fa_txndb_free(h)
+    off = off[: n + 1]
+    if n == 0:
+        off.zero_()
+    items = items[:nnz]
+    shard = TransactionShard(off.to(device, non_blocking=True), items.to(device, non_blocking=True),
+                             extras[:nx], Vocabulary(bool(numeric), vocab, strings, hashes), line_base)
+    return shard
+
+
+def parse_file(path: str, byte_begin: int = 0, byte_end: int = -1, mode: int = 0,
+               device: torch.device | str = "cpu", line_base: int = 0) -> TransactionShard:
+    err = C.c_int(0)
+    h = _native.host().fa_parse_file(path.encode(), byte_begin, byte_end, mode, num_threads(), C.byref(err))
+    if not h:
+        raise FileNotFoundError(f"cannot read {path} (error {err.value})")
+    return txndb_to_shard(h, torch.device(device), line_base)
+
+
+def parse_bytes(data: bytes, mode: int = 0, device="cpu") -> TransactionShard:
+    h = _native.host().fa_parse_buffer(data, len(data), mode, num_threads())
+    return txndb_to_shard(h, torch.device(device))
+
+
+def read_shard(path: str, comm, device: torch.device | str | None = None) -> TransactionShard:
+    """This rank's shard of ``path``; all ranks agree on numeric vs dict ids."""
+    device = torch.device(device or comm.device)
+    size = _native.host().fa_file_size(path.encode())
+    if size < 0:
+        raise FileNotFoundError(path)
+    b = size * comm.rank // comm.world_size
+    e = size * (comm.rank + 1) // comm.world_size
+    shard = parse_file(path, b, e, 0, "cpu")
+    need_dict = comm.allreduce_int(0 if shard.vocab.numeric else 1, "max")
+    if need_dict and shard.vocab.numeric:
+        shard = parse_file(path, b, e, 1, "cpu")
+    counts = comm.all_gather_int(shard.n_lines)
+    shard.line_base = int(sum(counts[: comm.rank]))
+    return shard.to(device)
+
+
+def generate_shard(n_txn: int, comm, device=None, avg_len: float = 10.0, avg_pat: float = 4.0,
+                   n_patterns: int = 2000, n_items: int = 1000, seed: int = 1, users: bool = False
+                   ) -> TransactionShard:
+    """This rank's slice of a synthetic Quest database (see csrc/host/quest.cpp)."""
+    device = torch.device(device or comm.device)
+    b = n_txn * comm.rank // comm.world_size
+    e = n_txn * (comm.rank + 1) // comm.world_size
+    h = _native.host().fa_quest_generate(b, e, avg_len, avg_pat, n_patterns, n_items, seed,
+                                         1 if users else 0, num_threads())
+    return txndb_to_shard(h, device, b)
+
+
+def write_quest_file(path: str, n_txn: int, avg_len=10.0, avg_pat=4.0, n_patterns=2000, n_items=1000,
+                     seed=1, users=False) -> None:
+    rc = _native.host().fa_quest_write(path.encode(), n_txn, avg_len, avg_pat, n_patterns, n_items, seed,
+                                       1 if users else 0, num_threads())
+    if rc:
+        raise OSError(f"failed to write {path}")
+
+
+# ---------------------------------------------------------------------------
+# Writers
+# ---------------------------------------------------------------------------
+class OutputExistsError(FileExistsError):
+    pass
+
+
+def _prepare_dir(path: str, overwrite: bool) -> None:
+    if os.path.exists(path):
+        if not overwrite:
+            # Spark's saveAsTextFile refuses an existing output directory.
+            raise OutputExistsError(f"Output directory {path} already exists")
+        for f in os.listdir(path):
+            os.remove(os.path.join(path, f))
+    else:
+        os.makedirs(path, exist_ok=True)
+
+
+def _tokens_blob(items: list[str]):
+    enc = [t.encode("utf-8") for t in items]
+    off = np.zeros(len(enc) + 1, dtype=np.int64)
+    if enc:
+        off[1:] = np.cumsum([len(e) for e in enc])
+    blob = b"".join(enc) or b"\0"
+    return blob, off
+
+
+def write_freq_itemsets(result: MiningResult, out_dir: str, with_counts: bool = False,
+                        overwrite: bool = False) -> str:
+    """``<output>freqItemset/part-00000`` (or ``freqItems`` with counts, Utils.scala:61)."""
+    _prepare_dir(out_dir, overwrite)
+    blob, off = _tokens_blob(result.items)
+    levels = [np.ascontiguousarray(l, dtype=np.int32) for l in result.levels]
+    counts = [np.ascontiguousarray(c, dtype=np.int64) for c in result.counts]
+    K = len(levels)
+    rows_p = (C.c_void_p * max(K, 1))(*[l.ctypes.data for l in levels])
+    cnt_p = (C.c_void_p * max(K, 1))(*[c.ctypes.data for c in counts])
+    sizes = np.array([l.shape[0] for l in levels] or [0], dtype=np.int64)
+    part = os.path.join(out_dir, "part-00000")
+    rc = _native.host().fa_write_freq_itemsets(part.encode(), blob, off.ctypes.data, len(result.items),
+                                               C.cast(rows_p, C.c_void_p), C.cast(cnt_p, C.c_void_p),
+                                               sizes.ctypes.data, K, 1 if with_counts else 0, num_threads())
+    if rc:
+        raise OSError(f"failed to write {part}")
+    open(os.path.join(out_dir, "_SUCCESS"), "wb").close()
+    return part
+
+
+def write_lines(lines: list[str], out_dir: str, overwrite: bool = False) -> str:
+    """``<output>recommends/part-00000``: one token per U.dat line (Utils.scala:43-49)."""
+    _prepare_dir(out_dir, overwrite)
+    part = os.path.join(out_dir, "part-00000")
+    with open(part, "wb") as f:
+        if lines:
+            f.write(("\n".join(lines) + "\n").encode("utf-8"))
+    open(os.path.join(out_dir, "_SUCCESS"), "wb").close()
+    return part
+
+
+def write_items_to_rank(result: MiningResult, path: str) -> None:
+    """``ItemsToRank`` ("item rank" lines) and ``FreqItems`` companions read by getAll (Utils.scala:65-81)."""
+    with open(path, "w", encoding="utf-8") as f:
+        for r, t in enumerate(result.items):
+            f.write(f"{t} {r}\n")
+
+
+def write_freq_items(result: MiningResult, path: str) -> None:
+    with open(path, "w", encoding="utf-8") as f:
+        for t in result.items:
+            f.write(t + "\n")
+
+
+def load_saved_results(freq_with_counts: str, items_to_rank: str, min_count: int = 0,
+                       n_lines: int = 0) -> MiningResult:
+    """Rebuild a MiningResult from saved files — the reference's ``Utils.getAll``
+    (Utils.scala:65-81): "item rank" lines + "a b c[cnt]" itemset lines."""
+    rank: dict[str, int] = {}
+    with open(items_to_rank, encoding="utf-8") as f:
+        for line in f:
+            line = line.rstrip("\n")
+            if not line:
+                continue
+            tok, r = line.rsplit(" ", 1)
+            rank[tok] = int(r)
+    items = [None] * len(rank)
+    for t, r in rank.items():
+        items[r] = t
+    by_k: dict[int, list[tuple[list[int], int]]] = {}
+    part = freq_with_counts
+    if os.path.isdir(part):
+        part = os.path.join(part, "part-00000")
+    with open(part, encoding="utf-8") as f:
+        for line in f:
+            line = line.rstrip("\n")
+            if not line:
+                continue
+            body, cnt = line[:-1].rsplit("[", 1)
+            ranks = sorted(rank[t] for t in body.split(" "))
+            by_k.setdefault(len(ranks), []).append((ranks, int(cnt)))
+    K = max(by_k) if by_k else 0
+    levels, counts = [], []
+    for k in range(1, K + 1):
+        rows = sorted(by_k.get(k, []))
+        levels.append(np.array([r for r, _ in rows], dtype=np.int32).reshape(-1, k))
+        counts.append(np.array([c for _, c in rows], dtype=np.int64))
+    return MiningResult(items=items, levels=levels, counts=counts, min_count=min_count, n_lines=n_lines)
