@@ -64,7 +64,7 @@ FA_API int fa_hip_recommend(const int64_t* ante_off, const int32_t* ante, const 
   if (M <= 0) return 0;
   const size_t words = (size_t)((F1 + 31) / 32);
   const size_t lds = std::max<size_t>(4, words * 4 * kRecWaves);
-  if (lds > 160 * 1024) return 2;   // caller falls back to the host path
+  if (lds > 64 * 1024) return 2;   // caller falls back to the host path
   dim3 g((unsigned)((M + kRecWaves - 1) / kRecWaves));
   hipLaunchKernelGGL(k_recommend, g, dim3(256), lds, st, ante_off, ante, cons, R, F1, boff, bask, M, out);
   FA_LAUNCH_RET();

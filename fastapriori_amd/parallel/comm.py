@@ -80,6 +80,13 @@ class Comm:
         dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
         return int(t.item())
 
+    def allreduce_float_max(self, v: float) -> float:
+        if not self.distributed:
+            return float(v)
+        t = torch.tensor([float(v)], dtype=torch.float64, device=self._comm_device())
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
     def all_gather_int(self, v: int) -> list[int]:
         if not self.distributed:
             return [int(v)]

@@ -1,0 +1,148 @@
+"""HIP kernel numerics: every device op against its CPU reference on the same inputs.
+
+All counts are integers, so the comparison is exact.  Shapes deliberately hit
+the edges: T not a multiple of 64, W not a multiple of the kernel tiles,
+F1 not a multiple of the 64/128 item tiles, long transactions (>64 items,
+which take the LDS-sort tier), and dedup weight classes.
+"""
+import numpy as np
+import pytest
+import torch
+
+from fastapriori_amd import ops
+from fastapriori_amd.models.apriori import FastApriori, MinerConfig
+from fastapriori_amd.ops import _native
+from fastapriori_amd.ops.host import apriori_gen
+from fastapriori_amd.parallel.comm import Comm
+from fastapriori_amd.utils.io import generate_shard, parse_bytes
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def test_native_library_is_loaded():
+    lib = _native.hip()
+    assert lib is not None
+    import os
+    maps = open(f"/proc/{os.getpid()}/maps").read()
+    assert "libfa_hip.so" in maps
+
+
+def _random_db(n, V, max_len, seed, long_rows=0):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, max_len + 1, n)
+    if long_rows:
+        lens[rng.choice(n, long_rows, replace=False)] = rng.integers(65, 300, long_rows)
+    rows = [rng.choice(V, size=min(l, V), replace=False).astype(np.int32) for l in lens]
+    off = np.zeros(n + 1, np.int64)
+    off[1:] = np.cumsum([r.size for r in rows])
+    items = np.concatenate(rows) if rows else np.zeros(0, np.int32)
+    return torch.from_numpy(off), torch.from_numpy(items.astype(np.int32))
+
+
+@pytest.mark.parametrize("V", [37, 1000, 20000])
+def test_histogram(V):
+    _, items = _random_db(5000, V, 30, 1)
+    ref = ops.histogram(items, V)
+    got = ops.histogram(items.to(DEV), V).cpu()
+    assert torch.equal(ref, got)
+    # unaligned view
+    got2 = ops.histogram(items[1:].contiguous().to(DEV)[0:], V).cpu()
+    assert torch.equal(ops.histogram(items[1:].contiguous(), V), got2)
+
+
+def _prep(n=3000, V=400, max_len=25, seed=0, long_rows=5, F1_frac=0.6):
+    off, items = _random_db(n, V, max_len, seed, long_rows)
+    rng = np.random.default_rng(seed + 1)
+    F1 = int(V * F1_frac)
+    perm = rng.permutation(V)
+    lut = np.full(V, -1, np.int32)
+    lut[perm[:F1]] = np.arange(F1, dtype=np.int32)
+    return off, items, torch.from_numpy(lut), F1
+
+
+def _compress_inputs(off, items, lut):
+    cnt = ops.txn_freq_count(off, items, lut)
+    kept = torch.nonzero(cnt >= 2).flatten().to(torch.int32)
+    roff = torch.zeros(kept.numel() + 1, dtype=torch.int64)
+    roff[1:] = torch.cumsum(cnt[kept.long()].long(), 0)
+    return cnt, kept, roff
+
+
+def test_txn_count_and_compress():
+    off, items, lut, F1 = _prep()
+    cnt, kept, roff = _compress_inputs(off, items, lut)
+    gcnt = ops.txn_freq_count(off.to(DEV), items.to(DEV), lut.to(DEV)).cpu()
+    assert torch.equal(cnt, gcnt)
+    ref = ops.compress(off, items, lut, kept, roff)
+    got = ops.compress(off.to(DEV), items.to(DEV), lut.to(DEV), kept.to(DEV), roff.to(DEV)).cpu()
+    assert torch.equal(ref, got)
+
+
+def test_row_hash_matches_host():
+    off, items, lut, F1 = _prep(seed=3)
+    _, kept, roff = _compress_inputs(off, items, lut)
+    ranks = ops.compress(off, items, lut, kept, roff)
+    h1, h2 = ops.row_hash(roff, ranks)
+    g1, g2 = ops.row_hash(roff.to(DEV), ranks.to(DEV))
+    assert torch.equal(h1, g1.cpu()) and torch.equal(h2, g2.cpu())
+
+
+@pytest.mark.parametrize("F1_frac", [0.05, 0.6, 1.0])
+def test_bitmaps_pairs_candidates(F1_frac):
+    off, items, lut, F1 = _prep(n=5000, V=700, seed=5, F1_frac=F1_frac)
+    _, kept, roff = _compress_inputs(off, items, lut)
+    ranks = ops.compress(off, items, lut, kept, roff)
+    T = kept.numel()
+    bm, W = ops.build_bitmaps(roff, ranks, None, T, F1)
+    gbm, gW = ops.build_bitmaps(roff.to(DEV), ranks.to(DEV), None, T, F1)
+    assert W == gW
+    assert torch.equal(bm[:, :W], gbm[:, :W].cpu())
+    # horizontal vs gram vs host
+    ph = ops.pair_counts_horizontal(roff, ranks, None, F1)
+    gph = ops.pair_counts_horizontal(roff.to(DEV), ranks.to(DEV), None, F1).cpu()
+    gpg = ops.pair_counts_gram(gbm, gW, None).cpu()
+    assert torch.equal(ph, gph)
+    assert torch.equal(torch.triu(ph, 1), torch.triu(gpg, 1))
+    # level-3 candidates from the frequent pairs
+    iu = torch.triu_indices(F1, F1, 1)
+    pc = ph[iu[0], iu[1]]
+    sel = torch.nonzero(pc >= max(1, int(pc.float().quantile(0.7).item()))).flatten()
+    prev = torch.stack([iu[0][sel], iu[1][sel]], 1).numpy().astype(np.int32)
+    if prev.shape[0] < 3:
+        return
+    pidx, eoff, ext = apriori_gen(prev)
+    if ext.size == 0:
+        return
+    prefix = torch.from_numpy(prev[pidx].copy())
+    ext_t = torch.from_numpy(ext.copy())
+    ref = ops.count_candidates(bm, W, prefix, eoff, ext_t, None)
+    got = ops.count_candidates(gbm, gW, prefix.to(DEV), eoff, ext_t.to(DEV), None).cpu()
+    assert torch.equal(ref, got)
+
+
+def test_weighted_dedup_paths_match():
+    # many duplicate rows -> dedup on; compare full mining cuda vs cpu, both strategies
+    sh = generate_shard(20000, Comm(), "cpu", 6.0, 3.0, 50, 60, seed=7)
+    res_cpu = FastApriori(0.01, config=MinerConfig(min_support=0.01, dedup="off")).run(sh)
+    shg = sh.to(DEV)
+    for strat in ("horizontal", "gram"):
+        for dd in ("on", "off"):
+            r = FastApriori(0.01, config=MinerConfig(min_support=0.01, dedup=dd, pair_strategy=strat)).run(shg)
+            assert r.as_dict() == res_cpu.as_dict(), (strat, dd)
+
+
+def test_recommend_kernel():
+    sh = generate_shard(20000, Comm(), "cpu", 8.0, 3.0, 80, 100, seed=9)
+    res = FastApriori(0.01, config=MinerConfig(min_support=0.01)).run(sh)
+    from fastapriori_amd.models.rules import AssociationRules
+    users = generate_shard(3000, Comm(), "cpu", 8.0, 3.0, 80, 100, seed=9, users=True)
+    ar = AssociationRules(res)
+    ref = ar.recommend_shard(users)
+    got = ar.recommend_shard(users.to(DEV)).cpu()
+    assert torch.equal(ref, got)
+
+
+def test_parse_to_device_roundtrip():
+    sh = parse_bytes(b"1 2 3\n\n4 4 5\n", device=DEV)
+    assert sh.items.is_cuda and sh.n_lines == 3
