@@ -38,38 +38,122 @@ __device__ __forceinline__ int64_t lower_bound_i32(const int32_t* __restrict__ a
   return lo;
 }
 
-__global__ __launch_bounds__(256) void k_pair_horizontal(
+// Each workgroup owns one 128x128 tile (bi, bj) of the pair matrix (u32 in LDS)
+// and a chunk of rows.  Its 8 wavefronts run fully decoupled: each takes
+// 64-row batches of the chunk, stages the batch's sorted ranks into a
+// wave-private LDS span (u16), and every lane scans its row for the bi / bj
+// segments and scatters the pairs into the shared tile with ds_add_u32.  There
+// is no workgroup barrier in the main loop; global-load latency is hidden by a
+// two-deep register pipeline (row offsets two batches ahead, ranks one ahead)
+// and by the 16 resident waves per CU.  The logical block id is XCD-remapped so
+// the nbp tiles of one chunk run on one XCD and re-read the chunk from its L2.
+constexpr int kPW = 16;                // waves per workgroup (1024 threads)
+constexpr int kWSpan = 1024;           // ranks staged per wave batch
+constexpr int kWPer = kWSpan / 64;     // per lane
+
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Per-row block table: bt[x*(nb+1) + b] = offset (within row x) of its first
+// rank >= b*kPB; bt[x*(nb+1) + nb] = row length.  Built once per mining run so
+// tile visits find their segments with two byte loads instead of a scan.
+template <typename BT>
+__global__ __launch_bounds__(256) void k_block_table(const int64_t* __restrict__ roff,
+                                                     const int32_t* __restrict__ ranks, int64_t T, int nb,
+                                                     BT* __restrict__ bt) {
+  const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= T) return;
+  const int64_t s = roff[x], e = roff[x + 1];
+  BT* out = bt + x * (nb + 1);
+  int64_t i = s;
+  for (int b = 0; b < nb; ++b) {
+    const int edge = b * kPB;
+    while (i < e && ranks[i] < edge) ++i;
+    out[b] = (BT)(i - s);
+  }
+  out[nb] = (BT)(e - s);
+}
+
+template <typename BT>
+__global__ __launch_bounds__(1024) void k_pair_horizontal(
     const int64_t* __restrict__ roff, const int32_t* __restrict__ ranks, int64_t T,
-    const int32_t* __restrict__ wrow, int32_t F1, int nb, int nbp, int64_t chunk,
+    const int32_t* __restrict__ wrow, const BT* __restrict__ bt, int32_t F1, int nb, int nbp, int64_t chunk,
     uint32_t* __restrict__ out) {
   __shared__ uint32_t tile[kPB * kPB];
-  const int pid = blockIdx.x % nbp;
-  const int64_t ch = blockIdx.x / nbp;
+  __shared__ int32_t wmeta[kPW][4][64];           // per lane: pair prefix, i-start, weight, (j0-i0)|nj<<24
+  const uint32_t logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int pid = logical % nbp;
+  const int64_t ch = logical / nbp;
   int bi, bj;
   tri_index(pid, nb, bi, bj);
   const int rb0 = bi * kPB, cb0 = bj * kPB;
   const bool diag = bi == bj;
   for (int i = threadIdx.x; i < kPB * kPB; i += blockDim.x) tile[i] = 0;
   __syncthreads();
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  int32_t* mpre = wmeta[wv][0];
+  int32_t* mist = wmeta[wv][1];
+  int32_t* mwt = wmeta[wv][2];
+  int32_t* mjn = wmeta[wv][3];
   const int64_t x0 = ch * chunk, x1 = min(T, x0 + chunk);
-  for (int64_t x = x0 + threadIdx.x; x < x1; x += blockDim.x) {
-    const int64_t s = roff[x], e = roff[x + 1];
-    if (e - s < 2) continue;
-    const uint32_t w = wrow ? (uint32_t)wrow[x] : 1u;
-    if (w == 0) continue;   // dedup: non-representative row
-    const int64_t i0 = lower_bound_i32(ranks, s, e, rb0);
-    const int64_t i1 = lower_bound_i32(ranks, i0, e, rb0 + kPB);
-    if (i0 == i1) continue;
-    int64_t j0, j1;
-    if (diag) { j0 = i0; j1 = i1; }
-    else {
-      j0 = lower_bound_i32(ranks, i1, e, cb0);
-      j1 = lower_bound_i32(ranks, j0, e, cb0 + kPB);
+  const int64_t nbatch = x1 > x0 ? (x1 - x0 + 63) / 64 : 0;
+  const int nbp1 = nb + 1;
+  struct Ro { int64_t ro; uint32_t w; int si0, si1, sj0, sj1; };
+  Ro A{}, B{};
+  auto load_ro = [&](int64_t q, Ro& r) {
+    const int64_t xb = x0 + q * 64, xe = min(x1, xb + 64), x = xb + lane;
+    const bool valid = x < xe;
+    r.ro = roff[valid ? x : xe];
+    r.w = valid ? (wrow ? (uint32_t)wrow[x] : 1u) : 0u;
+    const BT* row = bt + (valid ? x : 0) * nbp1;
+    r.si0 = row[bi]; r.si1 = row[bi + 1];
+    if (diag) { r.sj0 = r.si0; r.sj1 = r.si1; }
+    else { r.sj0 = row[bj]; r.sj1 = row[bj + 1]; }
+  };
+  int64_t q = wv;
+  if (q < nbatch) load_ro(q, A);
+  for (; q < nbatch; q += kPW) {
+    if (q + kPW < nbatch) load_ro(q + kPW, B);     // prefetch: lands while this batch scatters
+    const int ni = A.w ? A.si1 - A.si0 : 0;
+    const int nj = A.w ? A.sj1 - A.sj0 : 0;
+    const int P = (ni > 0 && nj > 0) ? ni * nj : 0;
+    int incl = P;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
     }
-    for (int64_t i = i0; i < i1; ++i) {
-      const int a = (ranks[i] - rb0) * kPB - cb0;
-      for (int64_t j = diag ? i + 1 : j0; j < j1; ++j) atomicAdd(&tile[a + ranks[j]], w);
+    const int total = __shfl(incl, 63, 64);
+    if (total > 0) {
+      // row-local pair rectangle, addressed relative to this batch's first row
+      const int64_t base = __shfl(A.ro, 0, 64);
+      mpre[lane] = incl - P;
+      mist[lane] = (int)(A.ro - base + A.si0);                  // i-segment start within the batch
+      mwt[lane] = (int)A.w;
+      mjn[lane] = (A.sj0 - A.si0) | (nj << 24);                 // j-segment offset | nj (<= 128)
+      wave_lds_fence();
+      for (int f = lane; f < total; f += 64) {
+        int owner = 0;
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1)
+          if (mpre[owner + step] <= f) owner += step;
+        const int loc = f - mpre[owner];
+        const int packed = mjn[owner];
+        const int cols = (int)((uint32_t)packed >> 24);
+        const int ii = (int)(((float)loc + 0.5f) * __builtin_amdgcn_rcpf((float)cols));
+        const int jj = loc - ii * cols;
+        if (diag && jj <= ii) continue;
+        const int64_t ia = base + mist[owner] + ii;
+        const int64_t jb = ia - ii + (packed & 0xFFFFFF) + jj;
+        const int ra = ranks[ia], rb = ranks[jb];
+        atomicAdd(&tile[(ra - rb0) * kPB + (rb - cb0)], (uint32_t)mwt[owner]);
+      }
+      wave_lds_fence();
     }
+    A = B;
   }
   __syncthreads();
   for (int i = threadIdx.x; i < kPB * kPB; i += blockDim.x) {
@@ -210,22 +294,146 @@ __global__ __launch_bounds__(256) void k_count_candidates(
     if (acc[i]) atomicAdd(&out[e_base + i], acc[i]);
 }
 
+// ---------------------------------------------------------------------------
+// k >= 3, slab-stationary counting (the default path).
+//
+// A slab = SW consecutive bitmap words (64*SW columns).  Each workgroup walks
+// slabs b = blockIdx.x, +gridDim.x, ...: it builds the slab of every item used
+// by this level's candidates directly in LDS from the compressed rows
+// (ds_or_b64), then every thread takes candidate groups, ANDs the group's
+// prefix rows once into registers and popcounts each extension row against it,
+// adding into a per-candidate LDS accumulator that lives across all slabs.
+// One pass reads the compressed rows once and touches HBM for nothing else;
+// the global bitmap is never materialised.  One coalesced atomic per candidate
+// per workgroup at the end.
+// ---------------------------------------------------------------------------
+template <int SW, bool kWeighted>
+__global__ __launch_bounds__(512) void k_count_slab(
+    const int64_t* __restrict__ roff, const int32_t* __restrict__ ranks, const int32_t* __restrict__ src,
+    int64_t ncols, const int32_t* __restrict__ item_map, int n_used, const int32_t* __restrict__ gpre, int m,
+    const int32_t* __restrict__ gext_off, const int32_t* __restrict__ gext, int G, int C,
+    const int32_t* __restrict__ wword, uint32_t* __restrict__ out) {
+  extern __shared__ uint64_t lds[];
+  constexpr int SWP = SW + 1;                       // padded row stride (bank spread)
+  constexpr int CPT = SW * 64 / 512 > 0 ? SW * 64 / 512 : 1;   // columns per thread
+  constexpr int RPC = 32 / CPT;                     // ranks per column prefetched in registers
+  uint64_t* slab = lds;
+  uint32_t* acc = reinterpret_cast<uint32_t*>(lds + (size_t)n_used * SWP);
+  for (int i = threadIdx.x; i < C; i += blockDim.x) acc[i] = 0;
+  const int64_t W = (ncols + 63) >> 6;
+  const int64_t nslabs = (W + SW - 1) / SW;
+
+  // register prefetch of the next slab's columns: row start, length, first RPC ranks
+  int64_t pbeg[CPT], plen[CPT];
+  int32_t pv[CPT][RPC];
+  auto prefetch = [&](int64_t sb) {
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      const int j = threadIdx.x + c * 512;
+      const int64_t col = sb * SW * 64 + j;
+      int64_t row = -1;
+      if (sb < nslabs && j < SW * 64 && col < ncols) row = src ? (int64_t)src[col] : col;
+      pbeg[c] = row >= 0 ? roff[row] : 0;
+      plen[c] = row >= 0 ? roff[row + 1] - pbeg[c] : 0;
+#pragma unroll
+      for (int r = 0; r < RPC; ++r) pv[c][r] = r < plen[c] ? ranks[pbeg[c] + r] : 0;
+    }
+  };
+  prefetch(blockIdx.x);
+  for (int64_t sb = blockIdx.x; sb < nslabs; sb += gridDim.x) {
+    const int64_t w0 = sb * SW;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n_used * SWP; i += blockDim.x) slab[i] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      const int j = threadIdx.x + c * 512;
+      const unsigned long long bit = 1ull << (j & 63);
+      uint64_t* base = slab + (j >> 6);
+      int32_t u[RPC];
+#pragma unroll
+      for (int r = 0; r < RPC; ++r) u[r] = r < plen[c] ? item_map[pv[c][r]] : -1;
+#pragma unroll
+      for (int r = 0; r < RPC; ++r)
+        if (u[r] >= 0) atomicOr((unsigned long long*)(base + (size_t)u[r] * SWP), bit);
+      for (int64_t r = RPC; r < plen[c]; ++r) {   // long rows: rest straight from global
+        const int uu = item_map[ranks[pbeg[c] + r]];
+        if (uu >= 0) atomicOr((unsigned long long*)(base + (size_t)uu * SWP), bit);
+      }
+    }
+    __syncthreads();
+    prefetch(sb + gridDim.x);                       // overlaps the counting below
+    int32_t wt[SW];
+#pragma unroll
+    for (int q = 0; q < SW; ++q) wt[q] = kWeighted ? ((w0 + q < W) ? wword[w0 + q] : 0) : 1;
+    for (int g = threadIdx.x; g < G; g += blockDim.x) {
+      uint64_t p[SW];
+      const int32_t* pr = gpre + (size_t)g * m;
+      {
+        const uint64_t* r0 = slab + (size_t)pr[0] * SWP;
+#pragma unroll
+        for (int q = 0; q < SW; ++q) p[q] = r0[q];
+      }
+      for (int j = 1; j < m; ++j) {
+        const uint64_t* rj = slab + (size_t)pr[j] * SWP;
+#pragma unroll
+        for (int q = 0; q < SW; ++q) p[q] &= rj[q];
+      }
+      uint64_t any = 0;
+#pragma unroll
+      for (int q = 0; q < SW; ++q) any |= p[q];
+      if (!any) continue;
+      for (int e = gext_off[g], e1 = gext_off[g + 1]; e < e1; ++e) {
+        const uint64_t* re = slab + (size_t)gext[e] * SWP;
+        uint32_t s = 0;
+#pragma unroll
+        for (int q = 0; q < SW; ++q) {
+          if (kWeighted) s += popc64_acc(p[q] & re[q], 0) * (uint32_t)wt[q];
+          else s = popc64_acc(p[q] & re[q], s);
+        }
+        acc[e] += s;
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < C; i += blockDim.x)
+    if (acc[i]) atomicAdd(&out[i], acc[i]);
+}
+
 }  // namespace fa
 
 using namespace fa;
 
+// bt: per-row block table built by fa_hip_block_table (u8 when every row has
+// <= 255 frequent items, else u16 — bt_bytes says which).
+FA_API int fa_hip_block_table(const int64_t* roff, const int32_t* ranks, int64_t T, int32_t F1, void* bt,
+                              int bt_bytes, hipStream_t st) {
+  if (T <= 0) return 0;
+  const int nb = (F1 + kPB - 1) / kPB;
+  dim3 g((unsigned)((T + 255) / 256));
+  if (bt_bytes == 1) hipLaunchKernelGGL(k_block_table<uint8_t>, g, dim3(256), 0, st, roff, ranks, T, nb, (uint8_t*)bt);
+  else hipLaunchKernelGGL(k_block_table<uint16_t>, g, dim3(256), 0, st, roff, ranks, T, nb, (uint16_t*)bt);
+  FA_LAUNCH_RET();
+}
+
 FA_API int fa_hip_pair_horizontal(const int64_t* roff, const int32_t* ranks, int64_t T,
-                                  const int32_t* wrow, int32_t F1, uint32_t* out, int target_wgs,
-                                  hipStream_t st) {
+                                  const int32_t* wrow, const void* bt, int bt_bytes, int32_t F1, uint32_t* out,
+                                  int target_wgs, hipStream_t st) {
   if (T <= 0 || F1 < 2) return 0;
+  if (F1 > 65535) return 4;   // u16 staging
   const int nb = (F1 + kPB - 1) / kPB;
   const int nbp = nb * (nb + 1) / 2;
   int64_t nch = std::max<int64_t>(1, (target_wgs + nbp - 1) / nbp);
   nch = std::min<int64_t>(nch, std::max<int64_t>(1, T / 512));
   const int64_t chunk = (T + nch - 1) / nch;
   nch = (T + chunk - 1) / chunk;
-  hipLaunchKernelGGL(k_pair_horizontal, dim3((unsigned)(nch * nbp)), dim3(256), 0, st, roff, ranks,
-                     T, wrow, F1, nb, nbp, chunk, out);
+  dim3 g((unsigned)(nch * nbp)), b(64 * kPW);
+  if (bt_bytes == 1)
+    hipLaunchKernelGGL(k_pair_horizontal<uint8_t>, g, b, 0, st, roff, ranks, T, wrow, (const uint8_t*)bt, F1, nb,
+                       nbp, chunk, out);
+  else
+    hipLaunchKernelGGL(k_pair_horizontal<uint16_t>, g, b, 0, st, roff, ranks, T, wrow, (const uint16_t*)bt, F1, nb,
+                       nbp, chunk, out);
   FA_LAUNCH_RET();
 }
 
@@ -259,4 +467,34 @@ FA_API int fa_hip_count_candidates(const uint64_t* bm, int64_t Wp, int64_t W, co
   else
     hipLaunchKernelGGL(k_count_candidates<false>, g, dim3(256), 0, st, bm, Wp, W, prefix, m, ext_off, ext, gb_start, ngb, wword, out);
   FA_LAUNCH_RET();
+}
+
+// Slab-stationary level counting.  gpre/gext hold slab-row ids (item_map
+// applied); C <= cap of the LDS accumulator.  Returns 3 when the LDS budget
+// cannot hold the slab + accumulator (the caller splits the candidates).
+FA_API int fa_hip_count_slab(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
+                             const int32_t* item_map, int n_used, const int32_t* gpre, int m,
+                             const int32_t* gext_off, const int32_t* gext, int G, int C, const int32_t* wword,
+                             uint32_t* out, int sw, int n_wg, hipStream_t st) {
+  if (G <= 0 || C <= 0 || ncols <= 0) return 0;
+  const size_t lds = (size_t)n_used * (sw + 1) * 8 + (size_t)C * 4;
+  if (lds > 160 * 1024) return 3;
+  dim3 g((unsigned)n_wg), b(512);
+#define FA_SLAB_CASE(S)                                                                                   \
+  if (sw == S) {                                                                                          \
+    auto kern = wword ? (void (*)(const int64_t*, const int32_t*, const int32_t*, int64_t, const int32_t*, \
+                                  int, const int32_t*, int, const int32_t*, const int32_t*, int, int,      \
+                                  const int32_t*, uint32_t*))k_count_slab<S, true>                         \
+                      : k_count_slab<S, false>;                                                            \
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);          \
+    hipLaunchKernelGGL(kern, g, b, lds, st, roff, ranks, src, ncols, item_map, n_used, gpre, m, gext_off,  \
+                       gext, G, C, wword, out);                                                            \
+    FA_LAUNCH_RET();                                                                                       \
+  }
+  FA_SLAB_CASE(4)
+  FA_SLAB_CASE(8)
+  FA_SLAB_CASE(16)
+  FA_SLAB_CASE(32)
+#undef FA_SLAB_CASE
+  return 1;
 }

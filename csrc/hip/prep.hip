@@ -85,18 +85,15 @@ template <int N>
 __global__ __launch_bounds__(256) void k_compress_regs(
     const int64_t* __restrict__ off, const int32_t* __restrict__ items, const int32_t* __restrict__ lut,
     const int32_t* __restrict__ rows, int64_t nrows, const int32_t* __restrict__ kept,
-    const int64_t* __restrict__ roff, int32_t* __restrict__ ranks, int32_t* __restrict__ overflow,
-    int32_t* __restrict__ n_overflow) {
+    const int64_t* __restrict__ roff, int32_t* __restrict__ ranks, int8_t* __restrict__ over_flag) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nrows) return;
   const int32_t x = rows ? rows[i] : (int32_t)i;
   const int64_t t = kept[x];
   const int64_t s = off[t];
   const int64_t L = off[t + 1] - s;
-  if (L > N) {
-    overflow[atomicAdd(n_overflow, 1)] = x;
-    return;
-  }
+  over_flag[i] = L > N ? 1 : 0;
+  if (L > N) return;
   uint32_t a[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) {
@@ -109,6 +106,84 @@ __global__ __launch_bounds__(256) void k_compress_regs(
 #pragma unroll
   for (int j = 0; j < N; ++j)
     if (j < c) ranks[o + j] = (int32_t)a[j];
+}
+
+// Tier 1 with LDS staging: a workgroup's 256 kept rows usually come from one
+// contiguous span of the input CSR, so the span is loaded coalesced (and
+// mapped through the LUT) into LDS, each thread sorts its row from LDS, and the
+// sorted output span is written back coalesced.  Rows longer than N go to the
+// overflow list; their (garbage) slots in the output span are rewritten by the
+// next tier, which runs later on the same stream.
+constexpr int kCSpan = 8192;
+constexpr int kCPer = kCSpan / 256;   // span elements per thread, loaded with full ILP
+
+template <int N>
+__global__ __launch_bounds__(256) void k_compress_staged(
+    const int64_t* __restrict__ off, const int32_t* __restrict__ items, const int32_t* __restrict__ lut,
+    int64_t T, const int32_t* __restrict__ kept, const int64_t* __restrict__ roff,
+    int32_t* __restrict__ ranks, int8_t* __restrict__ over_flag) {
+  __shared__ uint32_t buf[kCSpan];
+  const int64_t x0 = (int64_t)blockIdx.x * blockDim.x;
+  const int64_t x1 = min(T, x0 + (int64_t)blockDim.x);
+  const int64_t x = x0 + threadIdx.x;
+  // independent loads first: this row's bounds and the span bounds
+  const int64_t t = x < x1 ? (int64_t)kept[x] : 0;
+  const int64_t tf = kept[x0], tl = kept[x1 - 1];
+  const int64_t s = off[t], e_row = off[t + 1];
+  const int64_t base = off[tf];
+  const int64_t n_in = off[tl + 1] - base;
+  const int64_t obase = roff[x0];
+  const int64_t n_out = roff[x1] - obase;
+  const int64_t o_row = x < x1 ? roff[x] : 0, o_end = x < x1 ? roff[x + 1] : 0;
+  const bool staged = n_in <= kCSpan;
+  if (staged) {
+    int32_t v[kCPer];
+#pragma unroll
+    for (int k = 0; k < kCPer; ++k) {
+      const int64_t i = threadIdx.x + k * 256;
+      v[k] = i < n_in ? items[base + i] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kCPer; ++k) {
+      const int64_t i = threadIdx.x + k * 256;
+      if (i < n_in) v[k] = lut[v[k]];
+    }
+#pragma unroll
+    for (int k = 0; k < kCPer; ++k) {
+      const int64_t i = threadIdx.x + k * 256;
+      if (i < n_in) buf[i] = v[k] < 0 ? 0xFFFFFFFFu : (uint32_t)v[k];
+    }
+  }
+  __syncthreads();
+  uint32_t a[N];
+  const int64_t L = e_row - s;
+  const bool mine = x < x1 && L <= N;
+  if (x < x1) over_flag[x] = L > N ? 1 : 0;
+  if (mine) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      uint32_t v = 0xFFFFFFFFu;
+      if (j < L) {
+        if (staged) v = buf[s - base + j];
+        else { const int32_t r = lut[items[s + j]]; v = r < 0 ? 0xFFFFFFFFu : (uint32_t)r; }
+      }
+      a[j] = v;
+    }
+    bitonic_regs<N>(a);
+  }
+  __syncthreads();   // everyone is done reading the input span
+  const int64_t o = o_row - obase, c = o_end - o_row;
+  if (mine) {
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+      if (j < c) {
+        if (staged) buf[o + j] = a[j];
+        else ranks[obase + o + j] = (int32_t)a[j];
+      }
+  }
+  __syncthreads();
+  if (staged)
+    for (int64_t i = threadIdx.x; i < n_out; i += blockDim.x) ranks[obase + i] = (int32_t)buf[i];
 }
 
 // Long rows: one 256-thread workgroup per row, bitonic sort in LDS (<= 16384).
@@ -228,6 +303,90 @@ __global__ __launch_bounds__(256) void k_build_bitmaps(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Transaction trimming before level k: an item can only matter if it occurs in
+// some level-k candidate, and a row only if it keeps >= k such items.  Pass 1
+// counts surviving items per row; pass 2 compacts the kept rows.  Both stage a
+// 256-row span through LDS with all loads issued back to back.
+// ---------------------------------------------------------------------------
+constexpr int kTSpan = 8192;
+constexpr int kTPer = kTSpan / 256;
+
+__global__ __launch_bounds__(256) void k_trim_count(const int64_t* __restrict__ roff,
+                                                    const int32_t* __restrict__ ranks, int64_t T,
+                                                    const int8_t* __restrict__ alive, int32_t* __restrict__ cnt) {
+  __shared__ uint8_t buf[kTSpan];
+  const int64_t x0 = (int64_t)blockIdx.x * blockDim.x;
+  const int64_t x1 = min(T, x0 + (int64_t)blockDim.x);
+  const int64_t x = x0 + threadIdx.x;
+  const int64_t base = roff[x0], n = roff[x1] - base;
+  const int64_t s = x < x1 ? roff[x] : 0, e = x < x1 ? roff[x + 1] : 0;
+  const bool staged = n <= kTSpan;
+  if (staged) {
+    int32_t v[kTPer];
+#pragma unroll
+    for (int k = 0; k < kTPer; ++k) {
+      const int64_t i = threadIdx.x + k * 256;
+      v[k] = i < n ? ranks[base + i] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kTPer; ++k) {
+      const int64_t i = threadIdx.x + k * 256;
+      if (i < n) buf[i] = (uint8_t)alive[v[k]];
+    }
+  }
+  __syncthreads();
+  if (x >= x1) return;
+  int32_t c = 0;
+  if (staged) for (int64_t i = s; i < e; ++i) c += buf[i - base];
+  else for (int64_t i = s; i < e; ++i) c += alive[ranks[i]];
+  cnt[x] = c;
+}
+
+__global__ __launch_bounds__(256) void k_trim_write(const int64_t* __restrict__ roff,
+                                                    const int32_t* __restrict__ ranks,
+                                                    const int8_t* __restrict__ alive,
+                                                    const int32_t* __restrict__ kept, int64_t K,
+                                                    const int64_t* __restrict__ nroff, int32_t* __restrict__ nranks) {
+  __shared__ int32_t bin[kTSpan];
+  __shared__ int32_t bout[kTSpan];
+  const int64_t y0 = (int64_t)blockIdx.x * blockDim.x;
+  const int64_t y1 = min(K, y0 + (int64_t)blockDim.x);
+  const int64_t y = y0 + threadIdx.x;
+  const int64_t t = y < y1 ? (int64_t)kept[y] : 0;
+  const int64_t base = roff[kept[y0]], n = roff[(int64_t)kept[y1 - 1] + 1] - base;
+  const int64_t s = roff[t], e = roff[t + 1];
+  const int64_t obase = nroff[y0], n_out = nroff[y1] - obase;
+  const int64_t o = y < y1 ? nroff[y] - obase : 0;
+  const bool staged = n <= kTSpan;
+  if (staged) {
+    int32_t v[kTPer];
+#pragma unroll
+    for (int k = 0; k < kTPer; ++k) {
+      const int64_t i = threadIdx.x + k * 256;
+      v[k] = i < n ? ranks[base + i] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kTPer; ++k) {
+      const int64_t i = threadIdx.x + k * 256;
+      if (i < n) bin[i] = alive[v[k]] ? v[k] : -1;
+    }
+  }
+  __syncthreads();
+  if (y < y1) {
+    if (staged) {
+      int64_t w = o;
+      for (int64_t i = s; i < e; ++i) { const int32_t r = bin[i - base]; if (r >= 0) bout[w++] = r; }
+    } else {
+      int64_t w = obase + o;
+      for (int64_t i = s; i < e; ++i) { const int32_t r = ranks[i]; if (alive[r]) nranks[w++] = r; }
+    }
+  }
+  __syncthreads();
+  if (staged)
+    for (int64_t i = threadIdx.x; i < n_out; i += blockDim.x) nranks[obase + i] = bout[i];
+}
+
 }  // namespace fa
 
 using namespace fa;
@@ -258,16 +417,24 @@ FA_API int fa_hip_txn_freq_count(const int64_t* off, const int32_t* items, int64
 // tier: 16 / 64 register networks over `rows` (nullptr = all kept rows 0..nrows)
 FA_API int fa_hip_compress_regs(int tier, const int64_t* off, const int32_t* items, const int32_t* lut,
                                 const int32_t* rows, int64_t nrows, const int32_t* kept,
-                                const int64_t* roff, int32_t* ranks, int32_t* overflow,
-                                int32_t* n_overflow, hipStream_t st) {
+                                const int64_t* roff, int32_t* ranks, int8_t* over_flag, hipStream_t st) {
   if (nrows <= 0) return 0;
   dim3 g((unsigned)((nrows + 255) / 256));
   if (tier == 16)
-    hipLaunchKernelGGL(k_compress_regs<16>, g, dim3(256), 0, st, off, items, lut, rows, nrows, kept, roff, ranks, overflow, n_overflow);
+    hipLaunchKernelGGL(k_compress_regs<16>, g, dim3(256), 0, st, off, items, lut, rows, nrows, kept, roff, ranks, over_flag);
   else if (tier == 64)
-    hipLaunchKernelGGL(k_compress_regs<64>, g, dim3(256), 0, st, off, items, lut, rows, nrows, kept, roff, ranks, overflow, n_overflow);
+    hipLaunchKernelGGL(k_compress_regs<64>, g, dim3(256), 0, st, off, items, lut, rows, nrows, kept, roff, ranks, over_flag);
   else
     return 1;
+  FA_LAUNCH_RET();
+}
+
+FA_API int fa_hip_compress_staged(const int64_t* off, const int32_t* items, const int32_t* lut, int64_t T,
+                                  const int32_t* kept, const int64_t* roff, int32_t* ranks, int8_t* over_flag,
+                                  hipStream_t st) {
+  if (T <= 0) return 0;
+  hipLaunchKernelGGL(k_compress_staged<16>, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, st, off, items, lut,
+                     T, kept, roff, ranks, over_flag);
   FA_LAUNCH_RET();
 }
 
@@ -296,5 +463,20 @@ FA_API int fa_hip_build_bitmaps(const int64_t* roff, const int32_t* ranks, const
   dim3 g((unsigned)(Wp / WT), (unsigned)((F1 + R - 1) / R));
   size_t lds = (size_t)R * 2 * WT * 4;
   hipLaunchKernelGGL(k_build_bitmaps, g, dim3(256), lds, st, roff, ranks, src, ncols, F1, Wp, WT, R, bm);
+  FA_LAUNCH_RET();
+}
+
+FA_API int fa_hip_trim_count(const int64_t* roff, const int32_t* ranks, int64_t T, const int8_t* alive,
+                             int32_t* cnt, hipStream_t st) {
+  if (T <= 0) return 0;
+  hipLaunchKernelGGL(k_trim_count, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, st, roff, ranks, T, alive, cnt);
+  FA_LAUNCH_RET();
+}
+
+FA_API int fa_hip_trim_write(const int64_t* roff, const int32_t* ranks, const int8_t* alive, const int32_t* kept,
+                             int64_t K, const int64_t* nroff, int32_t* nranks, hipStream_t st) {
+  if (K <= 0) return 0;
+  hipLaunchKernelGGL(k_trim_write, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, st, roff, ranks, alive, kept, K,
+                     nroff, nranks);
   FA_LAUNCH_RET();
 }

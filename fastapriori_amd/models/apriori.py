@@ -25,6 +25,7 @@ are replicated, so the only traffic is one count vector per level.
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass
 
@@ -35,7 +36,7 @@ from .. import ops
 from ..ops.host import apriori_gen
 from ..parallel.comm import Comm
 from ..utils.jvm import java_string_key, min_count
-from ..utils.metrics import Logger, roctx_range
+from ..utils.metrics import Logger, Timer, roctx_range
 from .data import MiningResult, TransactionShard
 
 # Cost-model constants for choosing the k = 2 kernel (calibrated on MI355X; see
@@ -52,6 +53,8 @@ class MinerConfig:
     pair_strategy: str = "auto"     # auto | horizontal | gram
     dedup_threshold: float = 0.8    # dedup when distinct/T below this (auto)
     max_level: int = 0              # 0 = unlimited
+    level_kernel: str = "auto"      # auto | slab | bitmap  (k >= 3 counting kernel)
+    trim: bool = True               # transaction trimming before every level k >= 3
 
 
 class FastApriori:
@@ -78,8 +81,10 @@ class FastApriori:
         n_global = comm.allreduce_int(shard.n_lines)
         mc = min_count(self.cfg.min_support, n_global)
         self.stats = {"n_lines": n_global, "min_count": mc}
+        tm = Timer(dev, sync=os.environ.get("FA_PHASE_TIMING") == "1")
+        self._timer = tm
 
-        with roctx_range("F1"):
+        with roctx_range("F1"), tm.phase("f1"):
             items, counts1, lut = self._frequent_items(shard, mc)
         F1 = len(items)
         self.log.line(f"1 freq items {F1}")
@@ -93,7 +98,7 @@ class FastApriori:
         if F1 < 2:
             return self._finish(result, t_start)
 
-        with roctx_range("compress"):
+        with roctx_range("compress"), tm.phase("compress"):
             db = self._compress(shard, lut, F1)
         self.stats.update(T=db["T_global"], distinct=db["ncols_global"])
 
@@ -102,7 +107,7 @@ class FastApriori:
         if resume is not None and len(resume.levels) >= 2:
             levels.append(resume.levels[1]); counts.append(resume.counts[1])
         else:
-            with roctx_range("pairs"):
+            with roctx_range("pairs"), tm.phase("pairs"):
                 rows2, cnt2 = self._pairs(db, F1, mc)
             levels.append(rows2); counts.append(cnt2)
             if self.ckpt is not None:
@@ -121,14 +126,16 @@ class FastApriori:
                 levels.append(resume.levels[k - 1]); counts.append(resume.counts[k - 1])
                 k += 1
                 continue
-            with roctx_range(f"level{k}"):
-                prefix_idx, ext_off, ext = apriori_gen(levels[-1])
+            with roctx_range(f"level{k}"), tm.phase(f"level{k}"):
+                with tm.phase("apriori_gen"):
+                    prefix_idx, ext_off, ext = apriori_gen(levels[-1])
                 C = int(ext.size)
                 self.log.line(f"{k} candidate items {C}")
                 if C == 0:
                     levels.append(np.zeros((0, k), np.int32)); counts.append(np.zeros(0, np.int64))
                     self.log.line(f"{k} freq items 0")
                     break
+                self._trim(db, np.unique(np.concatenate([levels[-1][prefix_idx].ravel(), ext])), k)
                 cnt = self._count_level(db, levels[-1], prefix_idx, ext_off, ext)
                 keep = cnt >= mc
                 g_of_e = np.repeat(np.arange(prefix_idx.size), np.diff(ext_off))
@@ -154,6 +161,8 @@ class FastApriori:
         self.stats["mine_ms"] = (time.perf_counter() - t_start) * 1e3
         self.stats["n_itemsets"] = result.n_itemsets
         self.stats["bytes_reduced"] = self.comm.bytes_reduced
+        if getattr(self, "_timer", None) is not None and self._timer.sync:
+            self.stats["phase_ms"] = {k: round(v, 3) for k, v in self._timer.t.items()}
         return result
 
     def _check_resume(self, resume: MiningResult, fresh: MiningResult) -> None:
@@ -284,6 +293,24 @@ class FastApriori:
         nd = int(run[-1].item()) + 1
         weight = torch.bincount(run, minlength=nd)
         rep = o[new]                                   # one representative kept row per run
+        wrow = torch.zeros(T, dtype=torch.int32, device=dev)
+        wrow[rep] = weight.to(torch.int32)
+        db.update(wrow=wrow, n_distinct=nd)
+        self._layout_weighted(db)
+
+    @staticmethod
+    def _layout_weighted(db) -> None:
+        """Columns = rows with weight > 0, grouped by weight (unit weight first), each
+        class padded to 64 so every bitmap word carries one weight."""
+        wrow = db["wrow"]
+        dev = wrow.device
+        rep = torch.nonzero(wrow > 0).flatten()
+        weight = wrow[rep].to(torch.int64)
+        nd = rep.numel()
+        if nd == 0:
+            db.update(src=torch.full((64,), -1, dtype=torch.int32, device=dev), ncols=64,
+                      wword=torch.ones(1, dtype=torch.int32, device=dev))
+            return
         wo = torch.argsort(weight, stable=True)
         w_sorted, rep_sorted = weight[wo], rep[wo]
         cls_w, cls_n = torch.unique_consecutive(w_sorted, return_counts=True)
@@ -296,9 +323,26 @@ class FastApriori:
         src = torch.full((ncols,), -1, dtype=torch.int32, device=dev)
         src[col] = rep_sorted.to(torch.int32)
         wword = torch.repeat_interleave(cls_w.to(torch.int32), padded // 64)
-        wrow = torch.zeros(T, dtype=torch.int32, device=dev)
-        wrow[rep] = weight.to(torch.int32)
-        db.update(src=src, ncols=ncols, wword=wword, wrow=wrow, n_distinct=nd)
+        db.update(src=src, ncols=ncols, wword=wword)
+
+    def _trim(self, db, used: np.ndarray, k: int) -> None:
+        """Transaction trimming before level k (items outside C_k, rows with < k of them)."""
+        if not self.cfg.trim or db["T"] == 0:
+            return
+        dev = db["ranks"].device
+        alive = torch.zeros(db["F1"], dtype=torch.int8)
+        alive[torch.from_numpy(used.astype(np.int64))] = 1
+        kept, nroff, nranks, nw = ops.trim_rows(db["roff"], db["ranks"], alive.to(dev), k, db["wrow"])
+        K = kept.numel()
+        if K > 0.9 * db["T"] and nranks.numel() > 0.9 * db["ranks"].numel():
+            return   # not worth re-laying out
+        db.update(roff=nroff, ranks=nranks, T=K, bm=None, W=0)
+        if db["wrow"] is not None:
+            db["wrow"] = nw
+            self._layout_weighted(db)
+        else:
+            db.update(src=None, ncols=K)
+        self.log.metric(phase="trim", k=k, rows=K, nnz=int(nranks.numel()))
 
     def _bitmaps(self, db) -> None:
         if db["bm"] is None:
@@ -340,8 +384,14 @@ class FastApriori:
     # k >= 3 (FastApriori.scala:132-160)
     # ------------------------------------------------------------------
     def _count_level(self, db, prev: np.ndarray, prefix_idx, ext_off, ext) -> np.ndarray:
-        self._bitmaps(db)
         dev = db["ranks"].device
+        if dev.type == "cuda" and self.cfg.level_kernel in ("auto", "slab"):
+            cnt = ops.count_level_slab(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"],
+                                       prev[prefix_idx], ext_off, ext, db["wword"])
+            if cnt is not None:
+                self.comm.all_reduce_(cnt)
+                return cnt.cpu().numpy()
+        self._bitmaps(db)
         prefix = torch.from_numpy(np.ascontiguousarray(prev[prefix_idx], dtype=np.int32)).to(dev)
         ext_t = torch.from_numpy(np.ascontiguousarray(ext, dtype=np.int32)).to(dev)
         cnt = ops.count_candidates(db["bm"], db["W"], prefix, ext_off, ext_t, db["wword"])

@@ -56,11 +56,17 @@ _HOST_SIGS = {
 _HIP_SIGS = {
     "fa_hip_histogram": (C.c_int, [vp, i64, i32, vp, vp]),
     "fa_hip_txn_freq_count": (C.c_int, [vp, vp, i64, vp, vp, vp]),
-    "fa_hip_compress_regs": (C.c_int, [C.c_int, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp]),
+    "fa_hip_compress_regs": (C.c_int, [C.c_int, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp]),
+    "fa_hip_compress_staged": (C.c_int, [vp, vp, vp, i64, vp, vp, vp, vp, vp]),
+    "fa_hip_count_slab": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, vp,
+                                    C.c_int, C.c_int, vp]),
+    "fa_hip_trim_count": (C.c_int, [vp, vp, i64, vp, vp, vp]),
+    "fa_hip_trim_write": (C.c_int, [vp, vp, vp, vp, i64, vp, vp, vp]),
     "fa_hip_compress_lds": (C.c_int, [vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp]),
     "fa_hip_row_hash": (C.c_int, [vp, vp, i64, vp, vp, vp]),
     "fa_hip_build_bitmaps": (C.c_int, [vp, vp, vp, i64, i32, i64, C.c_int, C.c_int, vp, vp]),
-    "fa_hip_pair_horizontal": (C.c_int, [vp, vp, i64, vp, i32, vp, C.c_int, vp]),
+    "fa_hip_block_table": (C.c_int, [vp, vp, i64, i32, vp, C.c_int, vp]),
+    "fa_hip_pair_horizontal": (C.c_int, [vp, vp, i64, vp, vp, C.c_int, i32, vp, C.c_int, vp]),
     "fa_hip_pair_gram_popc": (C.c_int, [vp, i32, i64, i64, vp, vp, C.c_int, vp]),
     "fa_hip_count_candidates": (C.c_int, [vp, i64, i64, vp, C.c_int, vp, vp, vp, C.c_int, vp, vp, vp]),
     "fa_hip_recommend": (C.c_int, [vp, vp, vp, i64, i32, vp, vp, i64, vp, vp]),

@@ -71,17 +71,17 @@ def compress(offsets, items, lut, kept, roff) -> torch.Tensor:
     if not items.is_cuda:
         return _compress_torch(offsets, items, lut, kept, roff, ranks, None)[:nnz]
     st = _stream(items)
-    over = torch.empty(T, dtype=_I32, device=items.device)
-    n_over = torch.zeros(1, dtype=_I32, device=items.device)
-    _hip_call("fa_hip_compress_regs", 16, _p(offsets), _p(items), _p(lut), None, T, _p(kept), _p(roff),
-              _p(ranks), _p(over), _p(n_over), st)
-    n1 = int(n_over.item())
+    flag = torch.empty(T, dtype=torch.int8, device=items.device)
+    _hip_call("fa_hip_compress_staged", _p(offsets), _p(items), _p(lut), T, _p(kept), _p(roff), _p(ranks),
+              _p(flag), st)
+    over = torch.nonzero(flag).flatten().to(_I32)
+    n1 = over.numel()
     if n1:
-        over2 = torch.empty(n1, dtype=_I32, device=items.device)
-        n_over2 = torch.zeros(1, dtype=_I32, device=items.device)
+        flag2 = torch.empty(n1, dtype=torch.int8, device=items.device)
         _hip_call("fa_hip_compress_regs", 64, _p(offsets), _p(items), _p(lut), _p(over), n1, _p(kept),
-                  _p(roff), _p(ranks), _p(over2), _p(n_over2), st)
-        n2 = int(n_over2.item())
+                  _p(roff), _p(ranks), _p(flag2), st)
+        over2 = over[torch.nonzero(flag2).flatten()].contiguous()
+        n2 = over2.numel()
         if n2:
             over3 = torch.empty(n2, dtype=_I32, device=items.device)
             n_over3 = torch.zeros(1, dtype=_I32, device=items.device)
@@ -164,8 +164,14 @@ def pair_counts_horizontal(roff, ranks, wrow, F1: int) -> torch.Tensor:
     if ranks.is_cuda:
         out = torch.zeros((F1, F1), dtype=_I32, device=dev)
         if T > 0 and F1 >= 2:
-            _hip_call("fa_hip_pair_horizontal", _p(roff), _p(ranks), T, _p(wrow), F1, _p(out), 4096,
-                      _stream(ranks))
+            nb = (F1 + 127) // 128
+            maxlen = int((roff[1:] - roff[:-1]).max().item())
+            bt_bytes = 1 if maxlen <= 255 else 2
+            bt = torch.empty(T * (nb + 1) * bt_bytes, dtype=torch.uint8, device=dev)
+            st = _stream(ranks)
+            _hip_call("fa_hip_block_table", _p(roff), _p(ranks), T, F1, _p(bt), bt_bytes, st)
+            _hip_call("fa_hip_pair_horizontal", _p(roff), _p(ranks), T, _p(wrow), _p(bt), bt_bytes, F1, _p(out),
+                      1024, st)
         return out.to(_I64)
     out = torch.zeros((F1, F1), dtype=_I64)
     if T > 0 and F1 >= 2:
@@ -240,6 +246,108 @@ def count_candidates(bm: torch.Tensor, W: int, prefix: torch.Tensor, ext_off: np
     _native.host().fa_cpu_count_candidates(_p(bm), bm.stride(0), W, _p(prefix), m, _p(off_t), _p(ext),
                                            prefix.shape[0], _p(wword), _p(out), num_threads())
     return out
+
+
+def trim_rows(roff, ranks, alive: torch.Tensor, min_len: int, wrow=None):
+    """Keep rows with >= min_len alive items, dropping the dead items.
+
+    alive: int8 [F1] on the rows' device.  Returns (kept row ids int32, new roff,
+    new ranks, new wrow) — ranks stay sorted within each row.
+    """
+    T = roff.numel() - 1
+    dev = ranks.device
+    cnt = torch.empty(max(T, 0), dtype=_I32, device=dev)
+    if T == 0:
+        return (torch.zeros(0, dtype=_I32, device=dev), roff, ranks, wrow)
+    if ranks.is_cuda:
+        _hip_call("fa_hip_trim_count", _p(roff), _p(ranks), T, _p(alive), _p(cnt), _stream(ranks))
+    else:
+        a = alive[ranks.to(_I64)].to(_I64)
+        cs = torch.zeros(ranks.numel() + 1, dtype=_I64)
+        torch.cumsum(a, 0, out=cs[1:])
+        cnt = (cs[roff[1:]] - cs[roff[:-1]]).to(_I32)
+    keep = cnt >= min_len
+    if wrow is not None:
+        keep &= wrow > 0
+    kept = torch.nonzero(keep).flatten().to(_I32)
+    K = kept.numel()
+    nroff = torch.zeros(K + 1, dtype=_I64, device=dev)
+    if K:
+        torch.cumsum(cnt[kept.to(_I64)].to(_I64), 0, out=nroff[1:])
+    nnz = int(nroff[-1].item())
+    nranks = torch.empty(max(nnz, 1), dtype=_I32, device=dev)
+    if K and ranks.is_cuda:
+        _hip_call("fa_hip_trim_write", _p(roff), _p(ranks), _p(alive), _p(kept), K, _p(nroff), _p(nranks),
+                  _stream(ranks))
+    elif K:
+        lens = roff[1:] - roff[:-1]
+        rowmask = torch.zeros(T, dtype=torch.bool)
+        rowmask[kept.to(_I64)] = True
+        em = torch.repeat_interleave(rowmask, lens) & (alive[ranks.to(_I64)] > 0)
+        nranks[:nnz] = ranks[em]
+    nw = wrow[kept.to(_I64)].contiguous() if wrow is not None else None
+    return kept, nroff, nranks[:nnz], nw
+
+
+_LDS_BYTES = 160 * 1024
+
+
+def slab_plan(n_used: int, C: int):
+    """Pick the slab width SW (words) and the accumulator capacity for k_count_slab."""
+    for sw in (32, 16, 8, 4):
+        slab = n_used * (sw + 1) * 8
+        cap = (_LDS_BYTES - slab) // 4
+        if cap >= min(C, 8192) or (sw == 4 and cap >= 1024):
+            return sw, int(cap)
+    return 0, 0
+
+
+def count_level_slab(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_off: np.ndarray,
+                     ext: np.ndarray, wword) -> torch.Tensor | None:
+    """Slab-stationary support counting for one level (device only).
+
+    prefix: int32 [G, m] rank ids; ext_off int64 [G+1]; ext int32 [C].
+    Returns int64 counts [C], or None when the items do not fit the LDS slab
+    (the caller then uses the bitmap kernel).
+    """
+    dev = ranks.device
+    C = int(ext.size)
+    if C == 0:
+        return torch.zeros(0, dtype=_I64, device=dev)
+    used = np.unique(np.concatenate([prefix.ravel(), ext]))
+    sw, cap = slab_plan(used.size, C)
+    if sw == 0:
+        return None
+    item_map = np.full(max(F1, 1), -1, dtype=np.int32)
+    item_map[used] = np.arange(used.size, dtype=np.int32)
+    gpre = item_map[prefix]
+    gext = item_map[ext]
+    # split groups into passes of <= cap extensions (big groups into pieces)
+    gidx, new_off, starts = _split_groups(ext_off, cap, max_block_ext=cap)
+    gpre = np.ascontiguousarray(gpre[gidx], dtype=np.int32)
+    m = gpre.shape[1]
+    out = torch.zeros(C, dtype=_I32, device=dev)
+    imap_t = torch.from_numpy(item_map).to(dev)
+    gext_t = torch.from_numpy(np.ascontiguousarray(gext, dtype=np.int32)).to(dev)
+    W = (ncols + 63) // 64
+    nslabs = (W + sw - 1) // sw
+    st = _stream(ranks)
+    keep = []
+    for pi in range(starts.size - 1):
+        g0, g1 = int(starts[pi]), int(starts[pi + 1])
+        e0, e1 = int(new_off[g0]), int(new_off[g1])
+        loc_off = torch.from_numpy((new_off[g0:g1 + 1] - e0).astype(np.int32)).to(dev)
+        pre_t = torch.from_numpy(gpre[g0:g1]).to(dev)
+        keep += [loc_off, pre_t]
+        lds = used.size * (sw + 1) * 8 + (e1 - e0) * 4
+        per_cu = max(1, _LDS_BYTES // max(lds, 1))
+        n_wg = int(max(1, min(nslabs, 256 * min(per_cu, 2))))
+        _hip_call("fa_hip_count_slab", _p(roff), _p(ranks), _p(src), ncols, _p(imap_t), int(used.size), _p(pre_t),
+                  m, _p(loc_off), gext_t.data_ptr() + 4 * e0, g1 - g0, e1 - e0, _p(wword),
+                  out.data_ptr() + 4 * e0, sw, n_wg, st)
+    res = out.to(_I64)
+    del keep
+    return res
 
 
 def recommend(ante_off, ante, cons, F1: int, boff, bask) -> torch.Tensor:

@@ -119,6 +119,18 @@ def test_bitmaps_pairs_candidates(F1_frac):
     ref = ops.count_candidates(bm, W, prefix, eoff, ext_t, None)
     got = ops.count_candidates(gbm, gW, prefix.to(DEV), eoff, ext_t.to(DEV), None).cpu()
     assert torch.equal(ref, got)
+    slab = ops.count_level_slab(roff.to(DEV), ranks.to(DEV), None, T, F1, prev[pidx], eoff, ext, None)
+    assert slab is not None and torch.equal(ref, slab.cpu())
+
+
+def test_slab_many_passes_and_levels():
+    # a deep-level database: many candidates force several accumulator passes
+    sh = generate_shard(60000, Comm(), "cpu", 14.0, 6.0, 300, 120, seed=11)
+    cfg = dict(min_support=0.004, dedup="off")
+    ref = FastApriori(0.004, config=MinerConfig(level_kernel="bitmap", **cfg)).run(sh)
+    got = FastApriori(0.004, config=MinerConfig(level_kernel="slab", **cfg)).run(sh.to(DEV))
+    assert len(ref.levels) >= 4
+    assert ref.as_dict() == got.as_dict()
 
 
 def test_weighted_dedup_paths_match():
