@@ -83,6 +83,7 @@ __global__ __launch_bounds__(1024) void k_pair_horizontal(
     const int32_t* __restrict__ wrow, const BT* __restrict__ bt, int32_t F1, int nb, int nbp, int64_t chunk,
     uint32_t* __restrict__ out) {
   __shared__ uint32_t tile[kPB * kPB];
+  __shared__ uint16_t wspan[kPW][kWSpan];
   __shared__ int32_t wmeta[kPW][4][64];           // per lane: pair prefix, i-start, weight, (j0-i0)|nj<<24
   const uint32_t logical = xcd_remap(blockIdx.x, gridDim.x);
   const int pid = logical % nbp;
@@ -101,12 +102,13 @@ __global__ __launch_bounds__(1024) void k_pair_horizontal(
   const int64_t x0 = ch * chunk, x1 = min(T, x0 + chunk);
   const int64_t nbatch = x1 > x0 ? (x1 - x0 + 63) / 64 : 0;
   const int nbp1 = nb + 1;
-  struct Ro { int64_t ro; uint32_t w; int si0, si1, sj0, sj1; };
+  struct Ro { int64_t ro, end; uint32_t w; int si0, si1, sj0, sj1; };
   Ro A{}, B{};
   auto load_ro = [&](int64_t q, Ro& r) {
     const int64_t xb = x0 + q * 64, xe = min(x1, xb + 64), x = xb + lane;
     const bool valid = x < xe;
     r.ro = roff[valid ? x : xe];
+    r.end = roff[xe];
     r.w = valid ? (wrow ? (uint32_t)wrow[x] : 1u) : 0u;
     const BT* row = bt + (valid ? x : 0) * nbp1;
     r.si0 = row[bi]; r.si1 = row[bi + 1];
@@ -130,6 +132,23 @@ __global__ __launch_bounds__(1024) void k_pair_horizontal(
     if (total > 0) {
       // row-local pair rectangle, addressed relative to this batch's first row
       const int64_t base = __shfl(A.ro, 0, 64);
+      // lazily stage this batch's ranks (coalesced) — only batches with pairs in the tile
+      const int64_t n = A.end - base;
+      const bool staged = n <= kWSpan;
+      uint16_t* sp = wspan[wv];
+      if (staged) {
+        int32_t v[kWPer];
+#pragma unroll
+        for (int k = 0; k < kWPer; ++k) {
+          const int64_t i = lane + 64 * k;
+          v[k] = i < n ? ranks[base + i] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < kWPer; ++k) {
+          const int64_t i = lane + 64 * k;
+          if (i < n) sp[i] = (uint16_t)v[k];
+        }
+      }
       mpre[lane] = incl - P;
       mist[lane] = (int)(A.ro - base + A.si0);                  // i-segment start within the batch
       mwt[lane] = (int)A.w;
@@ -146,9 +165,10 @@ __global__ __launch_bounds__(1024) void k_pair_horizontal(
         const int ii = (int)(((float)loc + 0.5f) * __builtin_amdgcn_rcpf((float)cols));
         const int jj = loc - ii * cols;
         if (diag && jj <= ii) continue;
-        const int64_t ia = base + mist[owner] + ii;
+        const int64_t ia = mist[owner] + ii;
         const int64_t jb = ia - ii + (packed & 0xFFFFFF) + jj;
-        const int ra = ranks[ia], rb = ranks[jb];
+        const int ra = staged ? (int)sp[ia] : ranks[base + ia];
+        const int rb = staged ? (int)sp[jb] : ranks[base + jb];
         atomicAdd(&tile[(ra - rb0) * kPB + (rb - cb0)], (uint32_t)mwt[owner]);
       }
       wave_lds_fence();
@@ -313,12 +333,12 @@ __global__ __launch_bounds__(512) void k_count_slab(
     int64_t ncols, const int32_t* __restrict__ item_map, int n_used, const int32_t* __restrict__ gpre, int m,
     const int32_t* __restrict__ gext_off, const int32_t* __restrict__ gext, int G, int C,
     const int32_t* __restrict__ wword, uint32_t* __restrict__ out) {
-  extern __shared__ uint64_t lds[];
-  constexpr int SWP = SW + 1;                       // padded row stride (bank spread)
+  extern __shared__ uint4 lds4[];                  // 16-B aligned base
+  constexpr int SWP = SW + 2;                       // row stride: 16-B aligned, odd number of 16-B slots
   constexpr int CPT = SW * 64 / 512 > 0 ? SW * 64 / 512 : 1;   // columns per thread
   constexpr int RPC = 32 / CPT;                     // ranks per column prefetched in registers
-  uint64_t* slab = lds;
-  uint32_t* acc = reinterpret_cast<uint32_t*>(lds + (size_t)n_used * SWP);
+  uint64_t* slab = reinterpret_cast<uint64_t*>(lds4);
+  uint32_t* acc = reinterpret_cast<uint32_t*>(slab + (size_t)n_used * SWP);
   for (int i = threadIdx.x; i < C; i += blockDim.x) acc[i] = 0;
   const int64_t W = (ncols + 63) >> 6;
   const int64_t nslabs = (W + SW - 1) / SW;
@@ -343,7 +363,11 @@ __global__ __launch_bounds__(512) void k_count_slab(
   for (int64_t sb = blockIdx.x; sb < nslabs; sb += gridDim.x) {
     const int64_t w0 = sb * SW;
     __syncthreads();
-    for (int i = threadIdx.x; i < n_used * SWP; i += blockDim.x) slab[i] = 0;
+    {
+      uint4* s4 = lds4;
+      const uint4 z = make_uint4(0, 0, 0, 0);
+      for (int i = threadIdx.x; i < n_used * SWP / 2; i += blockDim.x) s4[i] = z;
+    }
     __syncthreads();
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
@@ -366,30 +390,39 @@ __global__ __launch_bounds__(512) void k_count_slab(
     int32_t wt[SW];
 #pragma unroll
     for (int q = 0; q < SW; ++q) wt[q] = kWeighted ? ((w0 + q < W) ? wword[w0 + q] : 0) : 1;
+    // work pieces: a prefix with <= 8 extensions (host-split), so lanes stay balanced
     for (int g = threadIdx.x; g < G; g += blockDim.x) {
-      uint64_t p[SW];
+      uint4 p[SW / 2];
       const int32_t* pr = gpre + (size_t)g * m;
       {
-        const uint64_t* r0 = slab + (size_t)pr[0] * SWP;
+        const uint4* r0 = lds4 + (size_t)pr[0] * (SWP / 2);
 #pragma unroll
-        for (int q = 0; q < SW; ++q) p[q] = r0[q];
+        for (int q = 0; q < SW / 2; ++q) p[q] = r0[q];
       }
       for (int j = 1; j < m; ++j) {
-        const uint64_t* rj = slab + (size_t)pr[j] * SWP;
+        const uint4* rj = lds4 + (size_t)pr[j] * (SWP / 2);
 #pragma unroll
-        for (int q = 0; q < SW; ++q) p[q] &= rj[q];
+        for (int q = 0; q < SW / 2; ++q) {
+          const uint4 v = rj[q];
+          p[q].x &= v.x; p[q].y &= v.y; p[q].z &= v.z; p[q].w &= v.w;
+        }
       }
-      uint64_t any = 0;
+      uint32_t any = 0;
 #pragma unroll
-      for (int q = 0; q < SW; ++q) any |= p[q];
+      for (int q = 0; q < SW / 2; ++q) any |= p[q].x | p[q].y | p[q].z | p[q].w;
       if (!any) continue;
       for (int e = gext_off[g], e1 = gext_off[g + 1]; e < e1; ++e) {
-        const uint64_t* re = slab + (size_t)gext[e] * SWP;
+        const uint4* re = lds4 + (size_t)gext[e] * (SWP / 2);
         uint32_t s = 0;
 #pragma unroll
-        for (int q = 0; q < SW; ++q) {
-          if (kWeighted) s += popc64_acc(p[q] & re[q], 0) * (uint32_t)wt[q];
-          else s = popc64_acc(p[q] & re[q], s);
+        for (int q = 0; q < SW / 2; ++q) {
+          const uint4 v = re[q];
+          if (kWeighted) {
+            s += (uint32_t)(__popc(p[q].x & v.x) + __popc(p[q].y & v.y)) * (uint32_t)wt[2 * q] +
+                 (uint32_t)(__popc(p[q].z & v.z) + __popc(p[q].w & v.w)) * (uint32_t)wt[2 * q + 1];
+          } else {
+            s += __popc(p[q].x & v.x) + __popc(p[q].y & v.y) + __popc(p[q].z & v.z) + __popc(p[q].w & v.w);
+          }
         }
         acc[e] += s;
       }
@@ -423,8 +456,15 @@ FA_API int fa_hip_pair_horizontal(const int64_t* roff, const int32_t* ranks, int
   if (F1 > 65535) return 4;   // u16 staging
   const int nb = (F1 + kPB - 1) / kPB;
   const int nbp = nb * (nb + 1) / 2;
-  int64_t nch = std::max<int64_t>(1, (target_wgs + nbp - 1) / nbp);
-  nch = std::min<int64_t>(nch, std::max<int64_t>(1, T / 512));
+  // target_wgs <= 0: |target_wgs| rows per chunk (locality mode: the nbp tiles of a
+  // chunk run together and share it through L2 / Infinity Cache)
+  int64_t nch;
+  if (target_wgs > 0) {
+    nch = std::max<int64_t>(1, (target_wgs + nbp - 1) / nbp);
+    nch = std::min<int64_t>(nch, std::max<int64_t>(1, T / 512));
+  } else {
+    nch = std::max<int64_t>(1, (T + (-target_wgs) - 1) / (-target_wgs));
+  }
   const int64_t chunk = (T + nch - 1) / nch;
   nch = (T + chunk - 1) / chunk;
   dim3 g((unsigned)(nch * nbp)), b(64 * kPW);
@@ -477,7 +517,7 @@ FA_API int fa_hip_count_slab(const int64_t* roff, const int32_t* ranks, const in
                              const int32_t* gext_off, const int32_t* gext, int G, int C, const int32_t* wword,
                              uint32_t* out, int sw, int n_wg, hipStream_t st) {
   if (G <= 0 || C <= 0 || ncols <= 0) return 0;
-  const size_t lds = (size_t)n_used * (sw + 1) * 8 + (size_t)C * 4;
+  const size_t lds = (size_t)n_used * (sw + 2) * 8 + (size_t)C * 4;
   if (lds > 160 * 1024) return 3;
   dim3 g((unsigned)n_wg), b(512);
 #define FA_SLAB_CASE(S)                                                                                   \

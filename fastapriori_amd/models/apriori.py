@@ -87,6 +87,7 @@ class FastApriori:
         with roctx_range("F1"), tm.phase("f1"):
             items, counts1, lut = self._frequent_items(shard, mc)
         F1 = len(items)
+        self._counts1 = counts1
         self.log.line(f"1 freq items {F1}")
         levels = [np.arange(F1, dtype=np.int32).reshape(-1, 1)]
         counts = [counts1]
@@ -246,7 +247,7 @@ class FastApriori:
             torch.cumsum(cnt[kept.to(torch.int64)].to(torch.int64), 0, out=roff[1:])
         ranks = ops.compress(shard.offsets, shard.items, lut, kept, roff)
         db = {"roff": roff, "ranks": ranks, "T": T, "src": None, "ncols": T, "wword": None, "wrow": None,
-              "bm": None, "W": 0, "F1": F1}
+              "bm": None, "W": 0, "F1": F1, "alive": np.ones(F1, dtype=bool), "c1": self._counts1}
         pair_work = 0
         if T:
             lens = roff[1:] - roff[:-1]
@@ -325,9 +326,38 @@ class FastApriori:
         wword = torch.repeat_interleave(cls_w.to(torch.int32), padded // 64)
         db.update(src=src, ncols=ncols, wword=wword)
 
+    def _trim_worth_it(self, db, used: np.ndarray, k: int) -> bool:
+        """Binomial estimate of the rows that would survive trimming.
+
+        Item occurrences survive with probability p = (occurrences of the level's
+        candidate items) / (occurrences of the items still in the rows); a row of
+        length L keeps >= k of them with probability P[Binom(L, p) >= k].  Trimming
+        costs two passes over the rows, so it runs only when it removes a lot.
+        """
+        from scipy.stats import binom
+        c1 = db["c1"]
+        alive = db["alive"]
+        denom = float(c1[alive].sum())
+        if denom <= 0:
+            return False
+        p = float(c1[used].sum()) / denom
+        hist = db["len_hist"]
+        L = np.arange(hist.size)
+        est_rows = float((hist * binom.sf(k - 1, L, p)).sum())
+        est_nnz = float((hist * L * p).sum())
+        return est_rows < 0.75 * max(db["T"], 1) or est_nnz < 0.6 * max(int(db["ranks"].numel()), 1)
+
+    def _len_hist(self, db) -> np.ndarray:
+        lens = db["roff"][1:] - db["roff"][:-1]
+        return torch.bincount(lens).cpu().numpy() if lens.numel() else np.zeros(1, np.int64)
+
     def _trim(self, db, used: np.ndarray, k: int) -> None:
         """Transaction trimming before level k (items outside C_k, rows with < k of them)."""
         if not self.cfg.trim or db["T"] == 0:
+            return
+        if "len_hist" not in db:
+            db["len_hist"] = self._len_hist(db)
+        if not self._trim_worth_it(db, used, k):
             return
         dev = db["ranks"].device
         alive = torch.zeros(db["F1"], dtype=torch.int8)
@@ -337,6 +367,9 @@ class FastApriori:
         if K > 0.9 * db["T"] and nranks.numel() > 0.9 * db["ranks"].numel():
             return   # not worth re-laying out
         db.update(roff=nroff, ranks=nranks, T=K, bm=None, W=0)
+        db["alive"] = np.zeros_like(db["alive"])
+        db["alive"][used] = True
+        db["len_hist"] = self._len_hist(db)
         if db["wrow"] is not None:
             db["wrow"] = nw
             self._layout_weighted(db)

@@ -19,6 +19,7 @@ from ..utils.env import num_threads
 from . import _native
 
 _I32, _I64 = torch.int32, torch.int64
+PAIR_CHUNK_ROWS = 1 << 18   # rows per pair-kernel chunk (working set ~10 MB: L2 / Infinity Cache resident)
 
 
 def _p(t: torch.Tensor | None) -> int | None:
@@ -171,7 +172,7 @@ def pair_counts_horizontal(roff, ranks, wrow, F1: int) -> torch.Tensor:
             st = _stream(ranks)
             _hip_call("fa_hip_block_table", _p(roff), _p(ranks), T, F1, _p(bt), bt_bytes, st)
             _hip_call("fa_hip_pair_horizontal", _p(roff), _p(ranks), T, _p(wrow), _p(bt), bt_bytes, F1, _p(out),
-                      1024, st)
+                      -PAIR_CHUNK_ROWS, st)
         return out.to(_I64)
     out = torch.zeros((F1, F1), dtype=_I64)
     if T > 0 and F1 >= 2:
@@ -208,17 +209,18 @@ def _split_groups(ext_off: np.ndarray, per_block: int, max_block_ext: int = 1024
     k = np.arange(gidx.size) - first
     new_off = np.minimum(ext_off[gidx] + k * max_block_ext, ext_off[gidx + 1])
     new_off = np.append(new_off, ext_off[-1]).astype(np.int64)
-    # greedy packing by extension count
-    starts = [0]
-    acc = 0
+    # pack consecutive pieces into blocks of <= lim extensions: a piece goes to the
+    # block its first extension falls in, with blocks sized lim - max_piece so the
+    # straddling piece still fits (vectorised; no Python loop over pieces)
     nsz = np.diff(new_off)
     lim = max(1, min(per_block, max_block_ext))
-    for i, s in enumerate(nsz.tolist()):
-        if acc + s > lim and acc > 0:
-            starts.append(i)
-            acc = 0
-        acc += s
-    starts.append(nsz.size)
+    step = max(1, lim - int(nsz.max(initial=0)) + 1) if nsz.size and nsz.max() < lim else 1
+    before = new_off[:-1] - new_off[0]
+    blk = before // step
+    starts = np.flatnonzero(np.diff(blk, prepend=-1) > 0) if nsz.size else np.zeros(0, np.int64)
+    starts = np.append(starts, nsz.size)
+    if starts[0] != 0:
+        starts = np.insert(starts, 0, 0)
     return gidx, new_off, np.asarray(starts, dtype=np.int32)
 
 
@@ -295,7 +297,7 @@ _LDS_BYTES = 160 * 1024
 def slab_plan(n_used: int, C: int):
     """Pick the slab width SW (words) and the accumulator capacity for k_count_slab."""
     for sw in (32, 16, 8, 4):
-        slab = n_used * (sw + 1) * 8
+        slab = n_used * (sw + 2) * 8
         cap = (_LDS_BYTES - slab) // 4
         if cap >= min(C, 8192) or (sw == 4 and cap >= 1024):
             return sw, int(cap)
@@ -323,8 +325,10 @@ def count_level_slab(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, 
     gpre = item_map[prefix]
     gext = item_map[ext]
     # split groups into passes of <= cap extensions (big groups into pieces)
-    gidx, new_off, starts = _split_groups(ext_off, cap, max_block_ext=cap)
-    gpre = np.ascontiguousarray(gpre[gidx], dtype=np.int32)
+    # pieces of <= 8 extensions per prefix keep the lanes of a wave balanced
+    gidx8, off8, _ = _split_groups(ext_off, 8, max_block_ext=8)
+    gidx, new_off, starts = _split_groups(off8, cap, max_block_ext=cap)
+    gpre = np.ascontiguousarray(gpre[gidx8[gidx]], dtype=np.int32)
     m = gpre.shape[1]
     out = torch.zeros(C, dtype=_I32, device=dev)
     imap_t = torch.from_numpy(item_map).to(dev)
@@ -339,7 +343,7 @@ def count_level_slab(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, 
         loc_off = torch.from_numpy((new_off[g0:g1 + 1] - e0).astype(np.int32)).to(dev)
         pre_t = torch.from_numpy(gpre[g0:g1]).to(dev)
         keep += [loc_off, pre_t]
-        lds = used.size * (sw + 1) * 8 + (e1 - e0) * 4
+        lds = used.size * (sw + 2) * 8 + (e1 - e0) * 4
         per_cu = max(1, _LDS_BYTES // max(lds, 1))
         n_wg = int(max(1, min(nslabs, 256 * min(per_cu, 2))))
         _hip_call("fa_hip_count_slab", _p(roff), _p(ranks), _p(src), ncols, _p(imap_t), int(used.size), _p(pre_t),
