@@ -132,7 +132,10 @@ def gen_rules(res: OracleResult) -> list[tuple[frozenset, int, float]]:
 
 
 def sort_rules(rules, items: list[str]):
-    return sorted(rules, key=lambda t: (-t[2], rule_tiebreak_key(items[t[1]]),
+    """conf desc, then consequent as Int (AssociationRules.scala:116-120).  Remaining ties
+    (same conf and consequent) are Spark collect order in the reference; they cannot change a
+    recommendation, and we fix them as (antecedent size, antecedent ranks) for determinism."""
+    return sorted(rules, key=lambda t: (-t[2], rule_tiebreak_key(items[t[1]]), len(t[0]),
                                         tuple(sorted(t[0]))))
 
 

@@ -167,13 +167,16 @@ def init_comm(device: str | None = None, backend: str | None = None, timeout_s: 
     if device is None:
         device = "cuda" if torch.cuda.is_available() else "cpu"
     if device == "cuda":
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
     else:
         dev = torch.device("cpu")
     if world <= 1:
         return Comm(0, 1, dev, "none")
-    be = backend or ("nccl" if dev.type == "cuda" else "gloo")
+    # FA_DIST_BACKEND=gloo lets several ranks share one GPU (tests on a 1-GPU box);
+    # production GPU runs use RCCL ("nccl"), one process per GPU.
+    be = backend or os.environ.get("FA_DIST_BACKEND") or ("nccl" if dev.type == "cuda" else "gloo")
     if not dist.is_initialized():
         kw = dict(backend=be, timeout=timedelta(seconds=timeout_s))
         if be == "nccl":

@@ -33,8 +33,10 @@ def run_job(cfg: JobConfig, comm=None) -> dict:
     summary: dict = {}
     try:
         ckpt = None
-        if cfg.temp and cfg.checkpoint:
-            ckpt = Checkpointer(cfg.temp, comm.rank, input_fingerprint(d_path, cfg.min_support))
+        if cfg.temp and (cfg.checkpoint or cfg.rules_only):
+            # rules-only needs no D.dat: it reloads the mined itemsets (Utils.getAll's use case)
+            fp = None if cfg.rules_only else input_fingerprint(d_path, cfg.min_support)
+            ckpt = Checkpointer(cfg.temp, comm.rank, fp)
         comm.barrier()
 
         t1 = time.time()

@@ -1,0 +1,101 @@
+"""Count distribution across ranks (gloo, CPU): results must be bit-identical to world size 1.
+
+Exercises everything that crosses ranks: the line total (X3),
+the F1 histogram all-reduce (X4), the dictionary-mode hash exchange
+(all_to_all + all_gather, X4 arbitrary vocab), pair and level all-reduces
+(X12, X15), the identical-decision collectives (dedup / kernel choice), the U.dat
+line offsets (X17) and the recommendation gather (X24).
+"""
+import os
+
+import pytest
+
+from fastapriori_amd.parallel.launch import spawn_local
+
+
+def _mine_file(path_prefix: str, ms: float, dedup: str, strategy: str):
+    from fastapriori_amd.models.apriori import FastApriori, MinerConfig
+    from fastapriori_amd.models.rules import AssociationRules
+    from fastapriori_amd.parallel.comm import init_comm, shutdown_comm
+    from fastapriori_amd.utils.io import read_shard
+    from fastapriori_amd.utils.metrics import Logger
+
+    comm = init_comm("cpu")
+    try:
+        shard = read_shard(path_prefix + "D.dat", comm)
+        cfg = MinerConfig(min_support=ms, dedup=dedup, pair_strategy=strategy)
+        res = FastApriori(ms, comm, cfg, Logger(comm.rank, enabled=False)).run(shard)
+        users = read_shard(path_prefix + "U.dat", comm)
+        recs = AssociationRules(res, comm, Logger(comm.rank, enabled=False)).run(users)
+        return {"items": res.items, "sets": res.as_dict(), "recs": recs, "rank": comm.rank,
+                "lines": shard.n_lines, "base": shard.line_base}
+    finally:
+        shutdown_comm(comm)
+
+
+def _mine_generated(n: int, ms: float):
+    from fastapriori_amd.models.apriori import FastApriori, MinerConfig
+    from fastapriori_amd.parallel.comm import init_comm, shutdown_comm
+    from fastapriori_amd.utils.io import generate_shard
+    from fastapriori_amd.utils.metrics import Logger
+
+    comm = init_comm("cpu")
+    try:
+        shard = generate_shard(n, comm, "cpu", 8.0, 3.0, 100, 80, seed=5)
+        res = FastApriori(ms, comm, MinerConfig(min_support=ms), Logger(comm.rank, enabled=False)).run(shard)
+        return res.as_dict(), res.items
+    finally:
+        shutdown_comm(comm)
+
+
+@pytest.fixture(scope="module")
+def numeric_db(tmp_path_factory):
+    from fastapriori_amd.utils.io import write_quest_file
+    d = tmp_path_factory.mktemp("num")
+    write_quest_file(str(d / "D.dat"), 4000, 8.0, 3.0, 60, 50, seed=2)
+    write_quest_file(str(d / "U.dat"), 700, 8.0, 3.0, 60, 50, seed=2, users=True)
+    return str(d) + "/"
+
+
+@pytest.fixture(scope="module")
+def dict_db(tmp_path_factory):
+    import random
+    rng = random.Random(4)
+    words = [f"w{i}" for i in range(30)] + ["é", "ß", "x y"[0]]
+    d = tmp_path_factory.mktemp("dict")
+    with open(d / "D.dat", "w", encoding="utf-8") as f:
+        for _ in range(1500):
+            f.write(" ".join(rng.sample(words, rng.randint(0, 7))) + ("\r\n" if rng.random() < 0.2 else "\n"))
+    with open(d / "U.dat", "w", encoding="utf-8") as f:
+        for _ in range(300):
+            f.write(" ".join(rng.sample(words, rng.randint(0, 3))) + "\n")
+    return str(d) + "/"
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("dedup,strategy", [("off", "horizontal"), ("on", "gram")])
+def test_numeric_file_matches_single_rank(numeric_db, world, dedup, strategy):
+    ref = spawn_local(_mine_file, 1, numeric_db, 0.02, dedup, strategy)[0]
+    outs = spawn_local(_mine_file, world, numeric_db, 0.02, dedup, strategy)
+    for o in outs:
+        assert o["items"] == ref["items"]
+        assert o["sets"] == ref["sets"]
+    assert outs[0]["recs"] == ref["recs"]
+    assert all(o["recs"] is None for o in outs[1:])
+    assert sum(o["lines"] for o in outs) == ref["lines"]
+    assert [o["base"] for o in outs] == sorted(o["base"] for o in outs)
+
+
+def test_dictionary_vocab_across_ranks(dict_db):
+    ref = spawn_local(_mine_file, 1, dict_db, 0.008, "auto", "auto")[0]
+    outs = spawn_local(_mine_file, 3, dict_db, 0.008, "auto", "auto")
+    assert outs[0]["items"] == ref["items"] and outs[0]["sets"] == ref["sets"]
+    assert outs[0]["recs"] == ref["recs"]
+    assert len(ref["sets"]) > 40
+
+
+def test_generated_shards_are_world_size_invariant():
+    ref = spawn_local(_mine_generated, 1, 6000, 0.02)[0]
+    for world in (2, 3):
+        outs = spawn_local(_mine_generated, world, 6000, 0.02)
+        assert all(o == ref for o in outs)
