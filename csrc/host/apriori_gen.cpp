@@ -29,16 +29,69 @@ static inline int cmp_row(const int32_t* a, const int32_t* b, int m) {
   return 0;
 }
 
-static inline bool contains_row(const int32_t* rows, int64_t n, int m, const int32_t* key) {
-  int64_t lo = 0, hi = n;
-  while (lo < hi) {
-    int64_t mid = (lo + hi) >> 1;
-    int c = cmp_row(rows + mid * m, key, m);
-    if (c == 0) return true;
-    if (c < 0) lo = mid + 1; else hi = mid;
-  }
-  return false;
+static inline uint64_t row_hash(const int32_t* r, int m) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)m;
+  for (int i = 0; i < m; ++i) h = mix64(h ^ (uint32_t)r[i]);
+  return h;
 }
+
+// Open-addressing set of the rows of F_{k-1} (indices into `rows`), probed by
+// content: O(1) subset checks instead of a binary search per check.  The table
+// is split into nthreads partitions by the top hash bits, so it is built in
+// parallel with no synchronisation (each thread owns one partition).
+struct RowSet {
+  const int32_t* rows;
+  int m;
+  std::vector<int64_t> slot;   // -1 = empty
+  int pbits = 0;
+  uint64_t pmask;              // slots per partition - 1
+  size_t index(uint64_t h, uint64_t probe) const {
+    const uint64_t part = pbits ? (h >> (64 - pbits)) : 0;
+    return (size_t)((part * (pmask + 1)) + ((h + probe) & pmask));
+  }
+  RowSet(const int32_t* r, int64_t n, int m_, int nthreads) : rows(r), m(m_) {
+    int P = 1;
+    while (P * 2 <= std::max(1, nthreads) && P < 64) { P *= 2; ++pbits; }
+    size_t per = 16;
+    while (per * P < (size_t)n * 2) per <<= 1;
+    pmask = per - 1;
+    slot.assign(per * P, -1);
+    std::vector<uint64_t> h(n);
+    parallel_for(n, nthreads, 1 << 14, [&](int64_t b, int64_t e, int) {
+      for (int64_t i = b; i < e; ++i) h[i] = row_hash(rows + i * m, m);
+    });
+    parallel_for_threads(P, [&](int t) {
+      for (int64_t i = 0; i < n; ++i) {
+        if (pbits && (int)(h[i] >> (64 - pbits)) != t) continue;
+        uint64_t probe = 0;
+        while (slot[index(h[i], probe)] != -1) ++probe;
+        slot[index(h[i], probe)] = i;
+      }
+    });
+  }
+  template <class Eq>
+  bool find(uint64_t h, Eq&& eq) const {
+    for (uint64_t probe = 0;; ++probe) {
+      const int64_t i = slot[index(h, probe)];
+      if (i < 0) return false;
+      if (eq(rows + i * m)) return true;
+    }
+  }
+  bool contains(const int32_t* key) const {
+    return find(row_hash(key, m), [&](const int32_t* r) { return cmp_row(r, key, m) == 0; });
+  }
+  // Membership of (x without x[skip]) + y, given the hash state of its first m-1 ranks.
+  bool contains_drop(uint64_t state, const int32_t* x, int skip, int32_t y) const {
+    return find(mix64(state ^ (uint32_t)y), [&](const int32_t* r) {
+      if (r[m - 1] != y) return false;
+      for (int q = 0, w = 0; q < m; ++q) {
+        if (q == skip) continue;
+        if (r[w++] != x[q]) return false;
+      }
+      return true;
+    });
+  }
+};
 
 }  // namespace fa
 
@@ -49,36 +102,50 @@ FA_API Cands* fa_apriori_gen(const int32_t* prev, int64_t n, int m, int nthreads
   auto* out = new Cands();
   // class end for every row: first row index whose first m-1 ranks differ
   std::vector<int64_t> cls_end(n);
+  std::vector<char> starts(n + 1, 1);
+  parallel_for(n, nthreads, 1 << 14, [&](int64_t b, int64_t e, int) {
+    for (int64_t i = std::max<int64_t>(b, 1); i < e; ++i)
+      starts[i] = cmp_row(prev + i * m, prev + (i - 1) * m, m - 1) != 0;
+  });
   {
-    int64_t i = 0;
-    while (i < n) {
-      int64_t j = i + 1;
-      while (j < n && cmp_row(prev + j * m, prev + i * m, m - 1) == 0) ++j;
-      for (int64_t t = i; t < j; ++t) cls_end[t] = j;
-      i = j;
+    int64_t end = n;
+    for (int64_t i = n - 1; i >= 0; --i) {
+      cls_end[i] = end;
+      if (starts[i]) end = i;
     }
   }
+  bool any_join = false;
+  for (int64_t i = 0; i + 1 < n && !any_join; ++i) any_join = cls_end[i] > i + 1;
+  if (!any_join) {
+    out->ext_off.push_back(0);
+    sizes[0] = sizes[1] = 0;
+    return out;
+  }
+  RowSet set(prev, n, m, nthreads);
   const int64_t grain = 256;
   const int64_t nblocks = (n + grain - 1) / grain;
   std::vector<Cands> parts(nblocks);
   parallel_for(nblocks, nthreads, 1, [&](int64_t b0, int64_t b1, int) {
-    std::vector<int32_t> key(m);
+    std::vector<uint64_t> st(m);
     for (int64_t b = b0; b < b1; ++b) {
       Cands& pc = parts[b];
       pc.ext_off.push_back(0);
       for (int64_t i = b * grain; i < std::min(n, (b + 1) * grain); ++i) {
         const int32_t* x = prev + i * m;
         size_t before = pc.ext.size();
-        for (int64_t j = i + 1; j < cls_end[i]; ++j) {
-          int32_t y = prev[j * m + m - 1];
-          bool ok = true;
-          // drop x[p] for p < m-1 : key = x without p, then y  (ascending)
-          for (int p = 0; p < m - 1 && ok; ++p) {
-            int w = 0;
-            for (int q = 0; q < m; ++q) if (q != p) key[w++] = x[q];
-            key[w] = y;
-            ok = contains_row(prev, n, m, key.data());
+        if (cls_end[i] > i + 1) {
+          // hash state of (x without x[p]) for every p < m-1, shared by all y of the class
+          for (int p = 0; p < m - 1; ++p) {
+            uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)m;
+            for (int q = 0; q < m; ++q) if (q != p) h = mix64(h ^ (uint32_t)x[q]);
+            st[p] = h;
           }
+        }
+        for (int64_t j = i + 1; j < cls_end[i]; ++j) {
+          const int32_t y = prev[j * m + m - 1];
+          bool ok = true;
+          // drop x[p] for p < m-1: (x without x[p]) + y must be frequent
+          for (int p = 0; p < m - 1 && ok; ++p) ok = set.contains_drop(st[p], x, p, y);
           if (ok) pc.ext.push_back(y);
         }
         if (pc.ext.size() > before) {
