@@ -327,15 +327,18 @@ __global__ __launch_bounds__(256) void k_count_candidates(
 // the global bitmap is never materialised.  One coalesced atomic per candidate
 // per workgroup at the end.
 // ---------------------------------------------------------------------------
-template <int SW, bool kWeighted>
-__global__ __launch_bounds__(512) void k_count_slab(
+constexpr int kSlabThreads = 1024;
+
+template <int SW, bool kWeighted, bool kFromBM>
+__global__ __launch_bounds__(kSlabThreads) void k_count_slab(
     const int64_t* __restrict__ roff, const int32_t* __restrict__ ranks, const int32_t* __restrict__ src,
     int64_t ncols, const int32_t* __restrict__ item_map, int n_used, const int32_t* __restrict__ gpre, int m,
     const int32_t* __restrict__ gext_off, const int32_t* __restrict__ gext, int G, int C,
-    const int32_t* __restrict__ wword, uint32_t* __restrict__ out) {
+    const int32_t* __restrict__ wword, uint32_t* __restrict__ out, const uint64_t* __restrict__ bm,
+    int64_t Wp) {
   extern __shared__ uint4 lds4[];                  // 16-B aligned base
   constexpr int SWP = SW + 2;                       // row stride: 16-B aligned, odd number of 16-B slots
-  constexpr int CPT = SW * 64 / 512 > 0 ? SW * 64 / 512 : 1;   // columns per thread
+  constexpr int CPT = SW * 64 / kSlabThreads > 0 ? SW * 64 / kSlabThreads : 1;   // columns per thread
   constexpr int RPC = 32 / CPT;                     // ranks per column prefetched in registers
   uint64_t* slab = reinterpret_cast<uint64_t*>(lds4);
   uint32_t* acc = reinterpret_cast<uint32_t*>(slab + (size_t)n_used * SWP);
@@ -347,9 +350,10 @@ __global__ __launch_bounds__(512) void k_count_slab(
   int64_t pbeg[CPT], plen[CPT];
   int32_t pv[CPT][RPC];
   auto prefetch = [&](int64_t sb) {
+    if (kFromBM) return;
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
-      const int j = threadIdx.x + c * 512;
+      const int j = threadIdx.x + c * kSlabThreads;
       const int64_t col = sb * SW * 64 + j;
       int64_t row = -1;
       if (sb < nslabs && j < SW * 64 && col < ncols) row = src ? (int64_t)src[col] : col;
@@ -363,26 +367,34 @@ __global__ __launch_bounds__(512) void k_count_slab(
   for (int64_t sb = blockIdx.x; sb < nslabs; sb += gridDim.x) {
     const int64_t w0 = sb * SW;
     __syncthreads();
-    {
-      uint4* s4 = lds4;
-      const uint4 z = make_uint4(0, 0, 0, 0);
-      for (int i = threadIdx.x; i < n_used * SWP / 2; i += blockDim.x) s4[i] = z;
-    }
-    __syncthreads();
+    if (kFromBM) {
+      // multi-pass level: the used-item bitmap is materialised once; copy the slab tile
+      for (int i = threadIdx.x; i < n_used * SW; i += blockDim.x) {
+        const int u = i / SW, q = i - u * SW;
+        slab[(size_t)u * SWP + q] = (w0 + q < W) ? bm[(size_t)u * Wp + w0 + q] : 0ull;
+      }
+    } else {
+      {
+        uint4* s4 = lds4;
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        for (int i = threadIdx.x; i < n_used * SWP / 2; i += blockDim.x) s4[i] = z;
+      }
+      __syncthreads();
 #pragma unroll
-    for (int c = 0; c < CPT; ++c) {
-      const int j = threadIdx.x + c * 512;
-      const unsigned long long bit = 1ull << (j & 63);
-      uint64_t* base = slab + (j >> 6);
-      int32_t u[RPC];
+      for (int c = 0; c < CPT; ++c) {
+        const int j = threadIdx.x + c * kSlabThreads;
+        const unsigned long long bit = 1ull << (j & 63);
+        uint64_t* base = slab + (j >> 6);
+        int32_t u[RPC];
 #pragma unroll
-      for (int r = 0; r < RPC; ++r) u[r] = r < plen[c] ? item_map[pv[c][r]] : -1;
+        for (int r = 0; r < RPC; ++r) u[r] = r < plen[c] ? item_map[pv[c][r]] : -1;
 #pragma unroll
-      for (int r = 0; r < RPC; ++r)
-        if (u[r] >= 0) atomicOr((unsigned long long*)(base + (size_t)u[r] * SWP), bit);
-      for (int64_t r = RPC; r < plen[c]; ++r) {   // long rows: rest straight from global
-        const int uu = item_map[ranks[pbeg[c] + r]];
-        if (uu >= 0) atomicOr((unsigned long long*)(base + (size_t)uu * SWP), bit);
+        for (int r = 0; r < RPC; ++r)
+          if (u[r] >= 0) atomicOr((unsigned long long*)(base + (size_t)u[r] * SWP), bit);
+        for (int64_t r = RPC; r < plen[c]; ++r) {   // long rows: rest straight from global
+          const int uu = item_map[ranks[pbeg[c] + r]];
+          if (uu >= 0) atomicOr((unsigned long long*)(base + (size_t)uu * SWP), bit);
+        }
       }
     }
     __syncthreads();
@@ -390,7 +402,8 @@ __global__ __launch_bounds__(512) void k_count_slab(
     int32_t wt[SW];
 #pragma unroll
     for (int q = 0; q < SW; ++q) wt[q] = kWeighted ? ((w0 + q < W) ? wword[w0 + q] : 0) : 1;
-    // work pieces: a prefix with <= 8 extensions (host-split), so lanes stay balanced
+    // work pieces: a prefix with <= 8 extensions, host-sorted by size so the lanes of
+    // a wave run loops of (nearly) equal length
     for (int g = threadIdx.x; g < G; g += blockDim.x) {
       uint4 p[SW / 2];
       const int32_t* pr = gpre + (size_t)g * m;
@@ -411,7 +424,7 @@ __global__ __launch_bounds__(512) void k_count_slab(
 #pragma unroll
       for (int q = 0; q < SW / 2; ++q) any |= p[q].x | p[q].y | p[q].z | p[q].w;
       if (!any) continue;
-      for (int e = gext_off[g], e1 = gext_off[g + 1]; e < e1; ++e) {
+      for (int e = gext_off[2 * g], e1 = gext_off[2 * g + 1]; e < e1; ++e) {
         const uint4* re = lds4 + (size_t)gext[e] * (SWP / 2);
         uint32_t s = 0;
 #pragma unroll
@@ -515,26 +528,28 @@ FA_API int fa_hip_count_candidates(const uint64_t* bm, int64_t Wp, int64_t W, co
 FA_API int fa_hip_count_slab(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
                              const int32_t* item_map, int n_used, const int32_t* gpre, int m,
                              const int32_t* gext_off, const int32_t* gext, int G, int C, const int32_t* wword,
-                             uint32_t* out, int sw, int n_wg, hipStream_t st) {
+                             uint32_t* out, int sw, int n_wg, const uint64_t* bm, int64_t Wp, hipStream_t st) {
   if (G <= 0 || C <= 0 || ncols <= 0) return 0;
   const size_t lds = (size_t)n_used * (sw + 2) * 8 + (size_t)C * 4;
   if (lds > 160 * 1024) return 3;
-  dim3 g((unsigned)n_wg), b(512);
-#define FA_SLAB_CASE(S)                                                                                   \
-  if (sw == S) {                                                                                          \
-    auto kern = wword ? (void (*)(const int64_t*, const int32_t*, const int32_t*, int64_t, const int32_t*, \
-                                  int, const int32_t*, int, const int32_t*, const int32_t*, int, int,      \
-                                  const int32_t*, uint32_t*))k_count_slab<S, true>                         \
-                      : k_count_slab<S, false>;                                                            \
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);          \
-    hipLaunchKernelGGL(kern, g, b, lds, st, roff, ranks, src, ncols, item_map, n_used, gpre, m, gext_off,  \
-                       gext, G, C, wword, out);                                                            \
-    FA_LAUNCH_RET();                                                                                       \
+  dim3 g((unsigned)n_wg), b(kSlabThreads);
+  using KernT = void (*)(const int64_t*, const int32_t*, const int32_t*, int64_t, const int32_t*, int,
+                         const int32_t*, int, const int32_t*, const int32_t*, int, int, const int32_t*,
+                         uint32_t*, const uint64_t*, int64_t);
+  KernT kern = nullptr;
+#define FA_SLAB_CASE(S)                                                                              \
+  if (sw == S) {                                                                                     \
+    if (bm) kern = wword ? (KernT)k_count_slab<S, true, true> : (KernT)k_count_slab<S, false, true>;  \
+    else kern = wword ? (KernT)k_count_slab<S, true, false> : (KernT)k_count_slab<S, false, false>;   \
   }
   FA_SLAB_CASE(4)
   FA_SLAB_CASE(8)
   FA_SLAB_CASE(16)
   FA_SLAB_CASE(32)
 #undef FA_SLAB_CASE
-  return 1;
+  if (!kern) return 1;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(kern, g, b, lds, st, roff, ranks, src, ncols, item_map, n_used, gpre, m, gext_off, gext, G, C,
+                     wword, out, bm, Wp);
+  FA_LAUNCH_RET();
 }

@@ -264,12 +264,17 @@ __global__ __launch_bounds__(256) void k_row_hash(const int64_t* __restrict__ ro
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_build_bitmaps(
     const int64_t* __restrict__ roff, const int32_t* __restrict__ ranks, const int32_t* __restrict__ src,
-    int64_t ncols, int32_t F1, int64_t Wp, int WT, int R, uint64_t* __restrict__ bm) {
+    int64_t ncols, int32_t F1, int64_t Wp, int WT, int R, uint64_t* __restrict__ bm,
+    const int32_t* __restrict__ item_map, const int32_t* __restrict__ used) {
   extern __shared__ uint32_t tile[];   // [R][2*WT]
   const int hw = 2 * WT;
-  const int r0 = blockIdx.y * R;
-  const int r1 = min(F1, r0 + R);
-  const int nr = r1 - r0;
+  // output rows [u0, u1); with an item map (u = item_map[rank], used[] = sorted ranks of
+  // the mapped items) the rank window is [used[u0], used[u1]) and rows are u - u0
+  const int u0 = blockIdx.y * R;
+  const int u1 = min(F1, u0 + R);
+  const int nr = u1 - u0;
+  const int r0 = item_map ? used[u0] : u0;
+  const int r1 = item_map ? (u1 < F1 ? used[u1] : 0x7FFFFFFF) : u1;
   for (int i = threadIdx.x; i < nr * hw; i += blockDim.x) tile[i] = 0;
   __syncthreads();
   const int64_t c0 = (int64_t)blockIdx.x * WT * 64;
@@ -291,7 +296,8 @@ __global__ __launch_bounds__(256) void k_build_bitmaps(
     for (int64_t i = lo; i < e; ++i) {
       const int r = ranks[i];
       if (r >= r1) break;
-      atomicOr(&tile[(r - r0) * hw + word], bit);
+      const int u = item_map ? item_map[r] : r;
+      if (u >= 0) atomicOr(&tile[(u - u0) * hw + word], bit);
     }
   }
   __syncthreads();
@@ -299,7 +305,7 @@ __global__ __launch_bounds__(256) void k_build_bitmaps(
   const int64_t base = c0 >> 5;
   for (int i = threadIdx.x; i < nr * hw; i += blockDim.x) {
     const int r = i / hw, w = i - r * hw;
-    out[(int64_t)(r0 + r) * (2 * Wp) + base + w] = tile[i];
+    out[(int64_t)(u0 + r) * (2 * Wp) + base + w] = tile[i];
   }
 }
 
@@ -457,12 +463,13 @@ FA_API int fa_hip_row_hash(const int64_t* roff, const int32_t* ranks, int64_t T,
 // Wp must be a multiple of WT.  LDS = R * 2 * WT * 4 bytes.
 FA_API int fa_hip_build_bitmaps(const int64_t* roff, const int32_t* ranks, const int32_t* src,
                                 int64_t ncols, int32_t F1, int64_t Wp, int WT, int R, uint64_t* bm,
-                                hipStream_t st) {
+                                const int32_t* item_map, const int32_t* used, hipStream_t st) {
   if (F1 <= 0 || Wp <= 0) return 0;
   if (Wp % WT) return 1;
   dim3 g((unsigned)(Wp / WT), (unsigned)((F1 + R - 1) / R));
   size_t lds = (size_t)R * 2 * WT * 4;
-  hipLaunchKernelGGL(k_build_bitmaps, g, dim3(256), lds, st, roff, ranks, src, ncols, F1, Wp, WT, R, bm);
+  hipLaunchKernelGGL(k_build_bitmaps, g, dim3(256), lds, st, roff, ranks, src, ncols, F1, Wp, WT, R, bm, item_map,
+                     used);
   FA_LAUNCH_RET();
 }
 

@@ -100,6 +100,8 @@ using namespace fa;
 // prev: n rows of m = k-1 ranks, each row ascending, rows lexicographically sorted.
 FA_API Cands* fa_apriori_gen(const int32_t* prev, int64_t n, int m, int nthreads, int64_t* sizes) {
   auto* out = new Cands();
+  // thread start-up costs ~50 us each: small levels run on the calling thread
+  nthreads = std::max(1, std::min<int>(nthreads, (int)(n / 4096)));
   // class end for every row: first row index whose first m-1 ranks differ
   std::vector<int64_t> cls_end(n);
   std::vector<char> starts(n + 1, 1);

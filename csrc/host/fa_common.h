@@ -4,8 +4,12 @@
 // consumed through ctypes by fastapriori_amd/ops/_native.py.
 #pragma once
 
+#include <unistd.h>
+
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <mutex>
 #include <cstdint>
 #include <cstring>
 #include <functional>
@@ -18,14 +22,65 @@
 
 namespace fa {
 
-// Run f(tid) on nthreads std::threads (tid 0 runs on the caller).
+// Persistent worker pool: thread start-up (~50 us per std::thread) would dominate
+// the small per-level host steps.  Recreated after fork().
+class ThreadPool {
+ public:
+  static ThreadPool& get() {
+    static ThreadPool* pool = nullptr;
+    static pid_t owner = 0;
+    static std::mutex m;
+    std::lock_guard<std::mutex> g(m);
+    if (!pool || owner != getpid()) { pool = new ThreadPool(); owner = getpid(); }  // old one leaks after fork
+    return *pool;
+  }
+  // Runs f(0..n-1); f(0) on the caller.  Calls are serialised.
+  void run(int n, const std::function<void(int)>& f) {
+    std::lock_guard<std::mutex> call(call_mu_);
+    ensure(n - 1);
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      job_ = &f; njob_ = n; next_ = 1; remaining_ = n - 1; ++gen_;
+    }
+    cv_.notify_all();
+    f(0);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [&] { return remaining_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void ensure(int k) {
+    while ((int)th_.size() < k) th_.emplace_back([this] { loop(); });
+  }
+  void loop() {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return gen_ != seen && next_ < njob_; });
+      seen = gen_;
+      while (next_ < njob_) {
+        const int id = next_++;
+        const std::function<void(int)>* f = job_;
+        lk.unlock();
+        (*f)(id);
+        lk.lock();
+        if (--remaining_ == 0) done_.notify_all();
+      }
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_, call_mu_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int)>* job_ = nullptr;
+  int njob_ = 0, next_ = 0, remaining_ = 0;
+  uint64_t gen_ = 0;
+};
+
+// Run f(tid) for tid in [0, nthreads) on the pool (tid 0 runs on the caller).
 inline void parallel_for_threads(int nthreads, const std::function<void(int)>& f) {
   if (nthreads <= 1) { f(0); return; }
-  std::vector<std::thread> ts;
-  ts.reserve(nthreads - 1);
-  for (int t = 1; t < nthreads; ++t) ts.emplace_back(f, t);
-  f(0);
-  for (auto& t : ts) t.join();
+  ThreadPool::get().run(nthreads, f);
 }
 
 // Dynamic chunked parallel loop over [0, n).

@@ -59,12 +59,12 @@ _HIP_SIGS = {
     "fa_hip_compress_regs": (C.c_int, [C.c_int, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp]),
     "fa_hip_compress_staged": (C.c_int, [vp, vp, vp, i64, vp, vp, vp, vp, vp]),
     "fa_hip_count_slab": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, vp,
-                                    C.c_int, C.c_int, vp]),
+                                    C.c_int, C.c_int, vp, i64, vp]),
     "fa_hip_trim_count": (C.c_int, [vp, vp, i64, vp, vp, vp]),
     "fa_hip_trim_write": (C.c_int, [vp, vp, vp, vp, i64, vp, vp, vp]),
     "fa_hip_compress_lds": (C.c_int, [vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp]),
     "fa_hip_row_hash": (C.c_int, [vp, vp, i64, vp, vp, vp]),
-    "fa_hip_build_bitmaps": (C.c_int, [vp, vp, vp, i64, i32, i64, C.c_int, C.c_int, vp, vp]),
+    "fa_hip_build_bitmaps": (C.c_int, [vp, vp, vp, i64, i32, i64, C.c_int, C.c_int, vp, vp, vp, vp]),
     "fa_hip_block_table": (C.c_int, [vp, vp, i64, i32, vp, C.c_int, vp]),
     "fa_hip_pair_horizontal": (C.c_int, [vp, vp, i64, vp, vp, C.c_int, i32, vp, C.c_int, vp]),
     "fa_hip_pair_gram_popc": (C.c_int, [vp, i32, i64, i64, vp, vp, C.c_int, vp]),

@@ -143,15 +143,19 @@ def bitmap_geometry(F1: int, ncols: int) -> tuple[int, int, int, int]:
     return W, Wp, WT, R
 
 
-def build_bitmaps(roff, ranks, src, ncols: int, F1: int) -> tuple[torch.Tensor, int]:
-    """Item-major bitmaps [F1, Wp] (int64 words) and the valid word count W."""
+def build_bitmaps(roff, ranks, src, ncols: int, F1: int, item_map=None, used=None) -> tuple[torch.Tensor, int]:
+    """Item-major bitmaps [F1, Wp] (int64 words) and the valid word count W.
+
+    With ``item_map`` (rank -> row, -1 = skip; device) and ``used`` (sorted ranks of
+    the mapped items; device) only those F1 = len(used) rows are built (device only).
+    """
     W, Wp, WT, R = bitmap_geometry(F1, ncols)
     dev = ranks.device
     if ranks.is_cuda:
         bm = torch.empty((max(F1, 1), Wp), dtype=_I64, device=dev)
         if F1 > 0:
             _hip_call("fa_hip_build_bitmaps", _p(roff), _p(ranks), _p(src), ncols, F1, Wp, WT, R, _p(bm),
-                      _stream(ranks))
+                      _p(item_map), _p(used), _stream(ranks))
     else:
         bm = torch.zeros((max(F1, 1), Wp), dtype=_I64)
         if F1 > 0:
@@ -329,6 +333,9 @@ def count_level_slab(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, 
     gidx8, off8, _ = _split_groups(ext_off, 8, max_block_ext=8)
     gidx, new_off, starts = _split_groups(off8, cap, max_block_ext=cap)
     gpre = np.ascontiguousarray(gpre[gidx8[gidx]], dtype=np.int32)
+    # within each pass, order pieces by extension count (desc): neighbouring lanes then
+    # loop equally long.  Pieces are (start, end) ranges, so reordering them is free.
+    piece_lo, piece_hi = new_off[:-1].copy(), new_off[1:].copy()
     m = gpre.shape[1]
     out = torch.zeros(C, dtype=_I32, device=dev)
     imap_t = torch.from_numpy(item_map).to(dev)
@@ -337,18 +344,27 @@ def count_level_slab(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, 
     nslabs = (W + sw - 1) // sw
     st = _stream(ranks)
     keep = []
+    bm = None
+    if starts.size - 1 > 1:
+        # several accumulator passes: build the used-item bitmap once, stream tiles from it
+        bm, _ = build_bitmaps(roff, ranks, src, ncols, int(used.size), imap_t,
+                              torch.from_numpy(used.astype(np.int32)).to(dev))
     for pi in range(starts.size - 1):
         g0, g1 = int(starts[pi]), int(starts[pi + 1])
         e0, e1 = int(new_off[g0]), int(new_off[g1])
-        loc_off = torch.from_numpy((new_off[g0:g1 + 1] - e0).astype(np.int32)).to(dev)
-        pre_t = torch.from_numpy(gpre[g0:g1]).to(dev)
+        sz = piece_hi[g0:g1] - piece_lo[g0:g1]
+        order = np.argsort(-sz, kind="stable")
+        lo = (piece_lo[g0:g1][order] - e0).astype(np.int32)
+        hi = (piece_hi[g0:g1][order] - e0).astype(np.int32)
+        loc_off = torch.from_numpy(np.stack([lo, hi], 1).reshape(-1)).to(dev)   # (begin, end) pairs
+        pre_t = torch.from_numpy(np.ascontiguousarray(gpre[g0:g1][order])).to(dev)
         keep += [loc_off, pre_t]
         lds = used.size * (sw + 2) * 8 + (e1 - e0) * 4
         per_cu = max(1, _LDS_BYTES // max(lds, 1))
         n_wg = int(max(1, min(nslabs, 256 * min(per_cu, 2))))
         _hip_call("fa_hip_count_slab", _p(roff), _p(ranks), _p(src), ncols, _p(imap_t), int(used.size), _p(pre_t),
                   m, _p(loc_off), gext_t.data_ptr() + 4 * e0, g1 - g0, e1 - e0, _p(wword),
-                  out.data_ptr() + 4 * e0, sw, n_wg, st)
+                  out.data_ptr() + 4 * e0, sw, n_wg, _p(bm), bm.stride(0) if bm is not None else 0, st)
     res = out.to(_I64)
     del keep
     return res

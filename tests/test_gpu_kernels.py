@@ -158,3 +158,16 @@ def test_recommend_kernel():
 def test_parse_to_device_roundtrip():
     sh = parse_bytes(b"1 2 3\n\n4 4 5\n", device=DEV)
     assert sh.items.is_cuda and sh.n_lines == 3
+
+
+def test_slab_multipass_from_bitmap(monkeypatch):
+    # shrink the LDS budget so the accumulator needs several passes -> bitmap-tile path
+    import fastapriori_amd.ops.primitives as prim
+    sh = generate_shard(30000, Comm(), "cpu", 12.0, 5.0, 200, 100, seed=13)
+    cfg = dict(min_support=0.005, dedup="off")
+    ref = FastApriori(0.005, config=MinerConfig(level_kernel="bitmap", **cfg)).run(sh)
+    monkeypatch.setattr(prim, "_LDS_BYTES", 24 * 1024)
+    got = FastApriori(0.005, config=MinerConfig(level_kernel="slab", **cfg)).run(sh.to(DEV))
+    assert ref.as_dict() == got.as_dict()
+    got_w = FastApriori(0.005, config=MinerConfig(level_kernel="slab", min_support=0.005, dedup="on")).run(sh.to(DEV))
+    assert ref.as_dict() == got_w.as_dict()
