@@ -185,6 +185,238 @@ __global__ __launch_bounds__(1024) void k_pair_horizontal(
 }
 
 // ---------------------------------------------------------------------------
+// k = 2, blocked layout.  Rows are re-laid out per 128-rank block:
+//   cnt[b][x]   u8   number of ranks of row x in block b
+//   base[b][q]  i64  where block b's data of 64-row batch q starts in lr
+//   lr[...]     u8   local ranks (rank - 128*b), block-major, batch-major, row order
+// A tile (bi, bj) then reads two bytes per row and only its two blocks' segments.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+  (void)lane;
+  return wave_scan_incl_dpp(v);
+}
+
+// one wave per 64-row batch; lane = row
+__global__ __launch_bounds__(256) void k_block_counts(const int64_t* __restrict__ roff,
+                                                      const int32_t* __restrict__ ranks, int64_t T, int nb,
+                                                      uint8_t* __restrict__ cnt, int64_t* __restrict__ bsum,
+                                                      int64_t nbatch, int pb) {
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= nbatch) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t x = q * 64 + lane;
+  const bool valid = x < T;
+  int64_t i = valid ? roff[x] : 0;
+  const int64_t e = valid ? roff[x + 1] : 0;
+  for (int b = 0; b < nb; ++b) {
+    const int edge = (b + 1) * pb;
+    int c = 0;
+    while (i < e && ranks[i] < edge) { ++i; ++c; }
+    if (valid) cnt[(int64_t)b * T + x] = (uint8_t)c;
+    int tot = c;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+    if (lane == 0) bsum[(int64_t)b * nbatch + q] = tot;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_block_scatter(const int64_t* __restrict__ roff,
+                                                       const int32_t* __restrict__ ranks, int64_t T, int nb,
+                                                       const uint8_t* __restrict__ cnt,
+                                                       const int64_t* __restrict__ base, int64_t nbatch,
+                                                       uint8_t* __restrict__ lr, int pb) {
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= nbatch) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t x = q * 64 + lane;
+  const bool valid = x < T;
+  int64_t i = valid ? roff[x] : 0;
+  for (int b = 0; b < nb; ++b) {
+    const int c = valid ? cnt[(int64_t)b * T + x] : 0;
+    const int incl = wave_incl_scan(c, lane);
+    int64_t o = base[(int64_t)b * nbatch + q] + (incl - c);
+    for (int k = 0; k < c; ++k) lr[o + k] = (uint8_t)(ranks[i + k] - b * pb);
+    i += c;
+  }
+}
+
+constexpr int kBSpan = 1024;   // staged bytes per block segment per wave batch
+
+__global__ __launch_bounds__(1024) void k_pair_blocked(
+    const uint8_t* __restrict__ cnt, const int64_t* __restrict__ base, const uint8_t* __restrict__ lr,
+    int64_t T, int64_t nbatch, const int32_t* __restrict__ wrow, int32_t F1, int nb, int nbp, int64_t chunk_b,
+    uint32_t* __restrict__ out) {
+  __shared__ uint32_t tile[kPB * kPB];
+  __shared__ uint8_t wsi[kPW][kBSpan];
+  __shared__ uint8_t wsj[kPW][kBSpan];
+  __shared__ int32_t wmeta[kPW][4][64];   // pair prefix, i-start, j-start, nj | weight<<8 (weight < 2^23) ...
+  const uint32_t logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int pid = logical % nbp;
+  const int64_t ch = logical / nbp;
+  int bi, bj;
+  tri_index(pid, nb, bi, bj);
+  const int rb0 = bi * kPB, cb0 = bj * kPB;
+  const bool diag = bi == bj;
+  for (int i = threadIdx.x; i < kPB * kPB; i += blockDim.x) tile[i] = 0;
+  __syncthreads();
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint8_t* si = wsi[wv];
+  uint8_t* sj = diag ? wsi[wv] : wsj[wv];
+  int32_t* mpre = wmeta[wv][0];
+  int32_t* mist = wmeta[wv][1];
+  int32_t* mjst = wmeta[wv][2];
+  int32_t* mnw = wmeta[wv][3];
+  const int64_t q0 = ch * chunk_b, q1 = min(nbatch, q0 + chunk_b);
+  const uint8_t* ci_row = cnt + (int64_t)bi * T;
+  const uint8_t* cj_row = cnt + (int64_t)bj * T;
+  // pipeline: counts of the next batch are loaded while this one scatters
+  auto load = [&](int64_t q, int& ci, int& cj, uint32_t& w) {
+    const int64_t x = q * 64 + lane;
+    const bool valid = x < T;
+    ci = valid ? ci_row[x] : 0;
+    cj = diag ? ci : (valid ? cj_row[x] : 0);
+    w = valid ? (wrow ? (uint32_t)wrow[x] : 1u) : 0u;
+  };
+  int ci = 0, cj = 0, ci_n = 0, cj_n = 0;
+  uint32_t w = 0, w_n = 0;
+  int64_t q = q0 + wv;
+  if (q < q1) load(q, ci, cj, w);
+  for (; q < q1; q += kPW) {
+    if (q + kPW < q1) load(q + kPW, ci_n, cj_n, w_n);
+    const int ni = w ? ci : 0, nj = w ? cj : 0;
+    const int P = (ni > 0 && nj > 0) ? ni * nj : 0;
+    const int incl = wave_incl_scan(P, lane);
+    const int total = wave_last(incl);
+    if (total > 0) {
+      const int inci = wave_incl_scan(ci, lane);
+      const int incj = diag ? inci : wave_incl_scan(cj, lane);
+      const int tot_i = wave_last(inci), tot_j = wave_last(incj);
+      const int64_t bsi = base[(int64_t)bi * nbatch + q];
+      const int64_t bsj = base[(int64_t)bj * nbatch + q];
+      const bool staged = tot_i <= kBSpan && tot_j <= kBSpan;
+      if (staged) {
+        for (int k = lane; k < tot_i; k += 64) si[k] = lr[bsi + k];
+        if (!diag)
+          for (int k = lane; k < tot_j; k += 64) sj[k] = lr[bsj + k];
+      }
+      mpre[lane] = incl - P;
+      mist[lane] = inci - ci;
+      mjst[lane] = incj - cj;
+      mnw[lane] = nj;
+      wave_lds_fence();
+      auto scatter = [&](const uint8_t* __restrict__ A, const uint8_t* __restrict__ B) {
+        for (int f = lane; f < total; f += 64) {
+          int owner = 0;
+#pragma unroll
+          for (int step = 32; step > 0; step >>= 1)
+            if (mpre[owner + step] <= f) owner += step;
+          const int loc = f - mpre[owner];
+          const int cols = mnw[owner];
+          const int ii = (int)(((float)loc + 0.5f) * __builtin_amdgcn_rcpf((float)cols));
+          const int jj = loc - ii * cols;
+          if (diag && jj <= ii) continue;
+          const int ra = A[mist[owner] + ii];
+          const int rb = B[mjst[owner] + jj];
+          const uint32_t wt = wrow ? (uint32_t)wrow[q * 64 + owner] : 1u;
+          atomicAdd(&tile[ra * kPB + rb], wt);
+        }
+      };
+      if (staged) scatter(si, sj);
+      else scatter(lr + bsi, lr + bsj);
+      wave_lds_fence();
+    }
+    ci = ci_n; cj = cj_n; w = w_n;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kPB * kPB; i += blockDim.x) {
+    const uint32_t v = tile[i];
+    if (!v) continue;
+    const int r = rb0 + i / kPB, c = cb0 + i % kPB;
+    if (r < F1 && c < F1) atomicAdd(&out[(int64_t)r * F1 + c], v);
+  }
+}
+
+// 256x256 tile of packed 16-bit counters (128 KB of LDS, 10 tiles for F1 <= 1024
+// instead of 36): two counters per u32 word, incremented with ds_add_u32 of
+// 1 or 1<<16.  A workgroup's chunk is <= 65535 unit-weight rows, so no counter
+// can carry into its neighbour before the flush.
+constexpr int kPB16 = 256;
+
+__global__ __launch_bounds__(1024) void k_pair_blocked16(
+    const uint8_t* __restrict__ cnt, const int64_t* __restrict__ base, const uint8_t* __restrict__ lr,
+    int64_t T, int64_t nbatch, int32_t F1, int nb, int nbp, int64_t chunk_b, uint32_t* __restrict__ out) {
+  __shared__ uint32_t tile[kPB16 * kPB16 / 2];
+  __shared__ int32_t wmeta[kPW][4][64];
+  const uint32_t logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int pid = logical % nbp;
+  const int64_t ch = logical / nbp;
+  int bi, bj;
+  tri_index(pid, nb, bi, bj);
+  const int rb0 = bi * kPB16, cb0 = bj * kPB16;
+  const bool diag = bi == bj;
+  for (int i = threadIdx.x; i < kPB16 * kPB16 / 2; i += blockDim.x) tile[i] = 0;
+  __syncthreads();
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  int32_t* mpre = wmeta[wv][0];
+  int32_t* mist = wmeta[wv][1];
+  int32_t* mjst = wmeta[wv][2];
+  int32_t* mnj = wmeta[wv][3];
+  const int64_t q0 = ch * chunk_b, q1 = min(nbatch, q0 + chunk_b);
+  const uint8_t* ci_row = cnt + (int64_t)bi * T;
+  const uint8_t* cj_row = cnt + (int64_t)bj * T;
+  int ci = 0, cj = 0, ci_n = 0, cj_n = 0;
+  auto load = [&](int64_t q, int& a, int& b) {
+    const int64_t x = q * 64 + lane;
+    a = x < T ? ci_row[x] : 0;
+    b = diag ? a : (x < T ? cj_row[x] : 0);
+  };
+  int64_t q = q0 + wv;
+  if (q < q1) load(q, ci, cj);
+  for (; q < q1; q += kPW) {
+    if (q + kPW < q1) load(q + kPW, ci_n, cj_n);
+    const int P = (ci > 0 && cj > 0) ? ci * cj : 0;
+    const int incl = wave_scan_incl_dpp(P);
+    const int total = wave_last(incl);
+    if (total > 0) {
+      const int inci = wave_scan_incl_dpp(ci);
+      const int incj = diag ? inci : wave_scan_incl_dpp(cj);
+      const uint8_t* A = lr + base[(int64_t)bi * nbatch + q];
+      const uint8_t* B = lr + base[(int64_t)bj * nbatch + q];
+      mpre[lane] = incl - P;
+      mist[lane] = inci - ci;
+      mjst[lane] = incj - cj;
+      mnj[lane] = cj;
+      wave_lds_fence();
+      for (int f = lane; f < total; f += 64) {
+        int owner = 0;
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1)
+          if (mpre[owner + step] <= f) owner += step;
+        const int loc = f - mpre[owner];
+        const int cols = mnj[owner];
+        const int ii = (int)(((float)loc + 0.5f) * __builtin_amdgcn_rcpf((float)cols));
+        const int jj = loc - ii * cols;
+        if (diag && jj <= ii) continue;
+        const int idx = (int)A[mist[owner] + ii] * kPB16 + (int)B[mjst[owner] + jj];
+        atomicAdd(&tile[idx >> 1], (idx & 1) ? 0x10000u : 1u);
+      }
+      wave_lds_fence();
+    }
+    ci = ci_n; cj = cj_n;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kPB16 * kPB16 / 2; i += blockDim.x) {
+    const uint32_t v = tile[i];
+    if (!v) continue;
+    const int idx = 2 * i;
+    const int r = rb0 + idx / kPB16, c = cb0 + idx % kPB16;
+    if (r >= F1) continue;
+    if ((v & 0xFFFF) && c < F1) atomicAdd(&out[(int64_t)r * F1 + c], v & 0xFFFF);
+    if ((v >> 16) && c + 1 < F1) atomicAdd(&out[(int64_t)r * F1 + c + 1], v >> 16);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k = 2, dense bit-matrix Gram with popcounts.  Tile 64x64 items, K-step 32 words.
 // ---------------------------------------------------------------------------
 constexpr int kGT = 64, kGK = 32, kGS = kGT + 1;   // LDS row stride (u64) breaks bank aliasing
@@ -551,5 +783,52 @@ FA_API int fa_hip_count_slab(const int64_t* roff, const int32_t* ranks, const in
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, g, b, lds, st, roff, ranks, src, ncols, item_map, n_used, gpre, m, gext_off, gext, G, C,
                      wword, out, bm, Wp);
+  FA_LAUNCH_RET();
+}
+
+FA_API int fa_hip_block_counts(const int64_t* roff, const int32_t* ranks, int64_t T, int32_t F1, uint8_t* cnt,
+                               int64_t* bsum, int pb, hipStream_t st) {
+  if (T <= 0) return 0;
+  const int nb = (F1 + pb - 1) / pb;
+  const int64_t nbatch = (T + 63) / 64;
+  hipLaunchKernelGGL(k_block_counts, dim3((unsigned)((nbatch + 3) / 4)), dim3(256), 0, st, roff, ranks, T, nb, cnt,
+                     bsum, nbatch, pb);
+  FA_LAUNCH_RET();
+}
+
+FA_API int fa_hip_block_scatter(const int64_t* roff, const int32_t* ranks, int64_t T, int32_t F1,
+                                const uint8_t* cnt, const int64_t* base, uint8_t* lr, int pb, hipStream_t st) {
+  if (T <= 0) return 0;
+  const int nb = (F1 + pb - 1) / pb;
+  const int64_t nbatch = (T + 63) / 64;
+  hipLaunchKernelGGL(k_block_scatter, dim3((unsigned)((nbatch + 3) / 4)), dim3(256), 0, st, roff, ranks, T, nb, cnt,
+                     base, nbatch, lr, pb);
+  FA_LAUNCH_RET();
+}
+
+FA_API int fa_hip_pair_blocked(const uint8_t* cnt, const int64_t* base, const uint8_t* lr, int64_t T,
+                               const int32_t* wrow, int32_t F1, uint32_t* out, int64_t chunk_rows, hipStream_t st) {
+  if (T <= 0 || F1 < 2) return 0;
+  const int nb = (F1 + kPB - 1) / kPB;
+  const int nbp = nb * (nb + 1) / 2;
+  const int64_t nbatch = (T + 63) / 64;
+  const int64_t chunk_b = std::max<int64_t>(kPW, (chunk_rows + 63) / 64);
+  const int64_t nch = (nbatch + chunk_b - 1) / chunk_b;
+  hipLaunchKernelGGL(k_pair_blocked, dim3((unsigned)(nch * nbp)), dim3(64 * kPW), 0, st, cnt, base, lr, T, nbatch,
+                     wrow, F1, nb, nbp, chunk_b, out);
+  FA_LAUNCH_RET();
+}
+
+// unit-weight rows only (chunks of <= 65535 rows keep the 16-bit counters exact)
+FA_API int fa_hip_pair_blocked16(const uint8_t* cnt, const int64_t* base, const uint8_t* lr, int64_t T, int32_t F1,
+                                 uint32_t* out, hipStream_t st) {
+  if (T <= 0 || F1 < 2) return 0;
+  const int nb = (F1 + kPB16 - 1) / kPB16;
+  const int nbp = nb * (nb + 1) / 2;
+  const int64_t nbatch = (T + 63) / 64;
+  const int64_t chunk_b = 65535 / 64;   // 1023 batches = 65472 rows
+  const int64_t nch = (nbatch + chunk_b - 1) / chunk_b;
+  hipLaunchKernelGGL(k_pair_blocked16, dim3((unsigned)(nch * nbp)), dim3(64 * kPW), 0, st, cnt, base, lr, T, nbatch,
+                     F1, nb, nbp, chunk_b, out);
   FA_LAUNCH_RET();
 }

@@ -22,6 +22,24 @@ __device__ __forceinline__ uint32_t popc64_acc(uint64_t x, uint32_t acc) {
   return acc + (uint32_t)__popc((uint32_t)x) + (uint32_t)__popc((uint32_t)(x >> 32));
 }
 
+// Inclusive wave64 prefix sum on the VALU with DPP (no LDS traffic, unlike
+// __shfl_up which lowers to ds_bpermute): row_shr 1/2/4/8 inside each 16-lane
+// row, then row_bcast:15 and row_bcast:31 across rows (GFX9-family DPP).
+__device__ __forceinline__ int wave_scan_incl_dpp(int v) {
+  const int lane = (int)(threadIdx.x & 63);
+  const int r = lane & 15;
+  int t;
+  t = __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false); if (r >= 1) v += t;   // row_shr:1
+  t = __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false); if (r >= 2) v += t;   // row_shr:2
+  t = __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false); if (r >= 4) v += t;   // row_shr:4
+  t = __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false); if (r >= 8) v += t;   // row_shr:8
+  t = __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false); if ((lane & 31) >= 16) v += t;  // row_bcast:15
+  t = __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false); if (lane >= 32) v += t;          // row_bcast:31
+  return v;
+}
+
+__device__ __forceinline__ int wave_last(int v) { return __builtin_amdgcn_readlane(v, 63); }
+
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -12,6 +12,8 @@ Conventions: bitmaps are int64 tensors [F1, Wp] holding raw 64-bit words
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -166,6 +168,27 @@ def build_bitmaps(roff, ranks, src, ncols: int, F1: int, item_map=None, used=Non
 def pair_counts_horizontal(roff, ranks, wrow, F1: int) -> torch.Tensor:
     T = roff.numel() - 1
     dev = ranks.device
+    if ranks.is_cuda and os.environ.get("FA_PAIR_KERNEL", "blocked") == "blocked":
+        out = torch.zeros((F1, F1), dtype=_I32, device=dev)
+        if T > 0 and F1 >= 2:
+            st = _stream(ranks)
+            pb = 128 if wrow is not None else 256       # u16 tiles need unit weights
+            nb = (F1 + pb - 1) // pb
+            nbatch = (T + 63) // 64
+            cnt = torch.empty(nb * T, dtype=torch.uint8, device=dev)
+            bsum = torch.empty(nb * nbatch, dtype=_I64, device=dev)
+            _hip_call("fa_hip_block_counts", _p(roff), _p(ranks), T, F1, _p(cnt), _p(bsum), pb, st)
+            base = torch.cumsum(bsum, 0)
+            total = int(base[-1].item())
+            base -= bsum
+            lr = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
+            _hip_call("fa_hip_block_scatter", _p(roff), _p(ranks), T, F1, _p(cnt), _p(base), _p(lr), pb, st)
+            if wrow is None:
+                _hip_call("fa_hip_pair_blocked16", _p(cnt), _p(base), _p(lr), T, F1, _p(out), st)
+            else:
+                _hip_call("fa_hip_pair_blocked", _p(cnt), _p(base), _p(lr), T, _p(wrow), F1, _p(out),
+                          PAIR_CHUNK_ROWS, st)
+        return out.to(_I64)
     if ranks.is_cuda:
         out = torch.zeros((F1, F1), dtype=_I32, device=dev)
         if T > 0 and F1 >= 2:

@@ -171,3 +171,18 @@ def test_slab_multipass_from_bitmap(monkeypatch):
     assert ref.as_dict() == got.as_dict()
     got_w = FastApriori(0.005, config=MinerConfig(level_kernel="slab", min_support=0.005, dedup="on")).run(sh.to(DEV))
     assert ref.as_dict() == got_w.as_dict()
+
+
+@pytest.mark.parametrize("kernel", ["blocked", "tile"])
+def test_pair_kernels_agree(monkeypatch, kernel):
+    monkeypatch.setenv("FA_PAIR_KERNEL", kernel)
+    off, items, lut, F1 = _prep(n=20000, V=900, seed=21, long_rows=30, F1_frac=0.9)
+    _, kept, roff = _compress_inputs(off, items, lut)
+    ranks = ops.compress(off, items, lut, kept, roff)
+    ref = ops.pair_counts_horizontal(roff, ranks, None, F1)
+    got = ops.pair_counts_horizontal(roff.to(DEV), ranks.to(DEV), None, F1).cpu()
+    assert torch.equal(ref, got)
+    w = torch.randint(0, 4, (kept.numel(),), dtype=torch.int32)
+    refw = ops.pair_counts_horizontal(roff, ranks, w, F1)
+    gotw = ops.pair_counts_horizontal(roff.to(DEV), ranks.to(DEV), w.to(DEV), F1).cpu()
+    assert torch.equal(refw, gotw)
