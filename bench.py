@@ -32,6 +32,10 @@ CONFIGS = {
     "T10I4D1K": (1_000, 10.0, 4.0, 200, 50, 0.1),
     "T40I10D100M": (100_000_000, 40.0, 10.0, 2000, 1000, 0.005),
     "T40I10D10M": (10_000_000, 40.0, 10.0, 2000, 1000, 0.005),
+    # wide vocabulary (Zipf-Mandelbrot words + topics, utils/io.generate_zipf_shard):
+    # avg_len is the mean document length, avg_pat_len unused, n_patterns = topics
+    "webdocs": (1_700_000, 177.0, 0.0, 2000, 5_267_656, 0.05),
+    "webdocs100K": (100_000, 177.0, 0.0, 2000, 5_267_656, 0.05),
 }
 HEADLINE = "T10I4D100M"
 
@@ -53,7 +57,7 @@ def main() -> int:
     import torch
     from fastapriori_amd.models.apriori import FastApriori, MinerConfig
     from fastapriori_amd.parallel.comm import init_comm, shutdown_comm
-    from fastapriori_amd.utils.io import generate_shard
+    from fastapriori_amd.utils.io import generate_shard, generate_zipf_shard
     from fastapriori_amd.utils.metrics import Logger
 
     dev = args.device if (args.device != "cuda" or torch.cuda.is_available()) else "cpu"
@@ -64,7 +68,11 @@ def main() -> int:
     world = comm.world_size
 
     t_gen = time.perf_counter()
-    shard = generate_shard(n_txn, comm, comm.device, avg_len, avg_pat, n_pat, n_items, args.seed)
+    if args.config.startswith("webdocs"):
+        shard = generate_zipf_shard(n_txn, comm, comm.device, mean_len=avg_len, n_items=n_items,
+                                    n_topics=n_pat, seed=args.seed)
+    else:
+        shard = generate_shard(n_txn, comm, comm.device, avg_len, avg_pat, n_pat, n_items, args.seed)
     if comm.device.type == "cuda":
         torch.cuda.synchronize()
     t_gen = time.perf_counter() - t_gen
@@ -103,7 +111,8 @@ def main() -> int:
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "int32/uint64-bitmap (exact integer counts)",
-            "data": f"synthetic Quest {args.config} (n={n_txn}, seed={args.seed}), generated in-process",
+            "data": (f"synthetic {'Zipf-topic' if args.config.startswith('webdocs') else 'Quest'} {args.config} "
+                     f"(n={n_txn}, seed={args.seed}), generated in-process"),
             "config": {"model": args.config, "global_batch": n_txn, "seq_len": avg_len,
                        "parallelism": f"dp{world}", "min_support": min_sup,
                        "n_itemsets": n_sets, "levels": [len(c) for c in res.counts],

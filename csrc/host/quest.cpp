@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdio>
 
+
 #include "fa_common.h"
 #include "txndb.h"
 
@@ -200,4 +201,86 @@ FA_API int fa_quest_write(const char* path, int64_t n_txn, double avg_len, doubl
     for (auto& s : bufs) std::fwrite(s.data(), 1, s.size(), f);
   }
   return std::fclose(f) == 0 ? 0 : 2;
+}
+
+// ---------------------------------------------------------------------------
+// Wide-vocabulary documents (webdocs-scale config; no real webdocs file can be
+// fetched).  A document is
+//   * a background bag: length ~ lognormal(mean_len, sigma), words drawn without
+//     replacement from a Zipf-Mandelbrot law p(k) ~ 1/(k+q)^s over n_items ids
+//     (q bounds the head's document frequency like stop-word filtering does), and
+//   * one topic (Zipf(1) over n_topics topics); each of the topic's 5-15 core
+//     words (drawn from ranks [100, 20100)) joins the document with probability
+//     0.8 — the correlated structure that makes deeper itemsets frequent.
+// Counter-based per document like the Quest generator.
+// ---------------------------------------------------------------------------
+namespace fa {
+struct ZipfTable {
+  std::vector<double> cdf;
+  ZipfTable(int64_t n, double s, double q) : cdf((size_t)n) {
+    double acc = 0;
+    for (int64_t k = 0; k < n; ++k) { acc += 1.0 / std::pow((double)(k + 1) + q, s); cdf[k] = acc; }
+    for (auto& c : cdf) c /= acc;
+  }
+  int64_t sample(Rng& r) const {
+    const double u = r.uniform();
+    return std::min<int64_t>((int64_t)(std::lower_bound(cdf.begin(), cdf.end(), u) - cdf.begin()),
+                             (int64_t)cdf.size() - 1);
+  }
+};
+}  // namespace fa
+
+FA_API TxnDB* fa_zipf_generate(int64_t txn_begin, int64_t txn_end, double mean_len, double sigma, int64_t n_items,
+                               double s, double q, int64_t n_topics, uint64_t seed, int nthreads) {
+  n_items = std::max<int64_t>(1, n_items);
+  ZipfTable words(n_items, s, q);
+  n_topics = std::max<int64_t>(1, n_topics);
+  ZipfTable topic_law(n_topics, 1.0, 0.0);
+  std::vector<std::vector<int64_t>> topics((size_t)n_topics);
+  {
+    Rng r(mix64(seed ^ 0x70F1C5ull));
+    const int64_t lo = std::min<int64_t>(100, n_items - 1), span = std::max<int64_t>(1, std::min<int64_t>(20000, n_items - lo));
+    for (auto& t : topics) {
+      const int64_t c = 5 + (int64_t)r.below(11);
+      for (int64_t j = 0; j < c; ++j) t.push_back(lo + (int64_t)r.below((uint64_t)span));
+    }
+  }
+  auto* db = new TxnDB();
+  db->numeric = true;
+  db->vocab = n_items + 2;
+  const int64_t n = std::max<int64_t>(0, txn_end - txn_begin);
+  int nt = std::max(1, nthreads);
+  if (n < (int64_t)nt * 256) nt = 1;
+  db->chunks.assign(nt, TxnChunk());
+  const double mu = std::log(std::max(1.0, mean_len)) - 0.5 * sigma * sigma;
+  parallel_for_threads(nt, [&](int t) {
+    const int64_t lo = txn_begin + n * t / nt, hi = txn_begin + n * (t + 1) / nt;
+    TxnChunk& ch = db->chunks[t];
+    ch.lens.reserve(hi - lo);
+    std::vector<int64_t> row;
+    std::vector<int64_t> table;
+    for (int64_t i = lo; i < hi; ++i) {
+      Rng r(mix64(seed * 0xD1B54A32D192ED03ull + (uint64_t)i));
+      const double g = std::sqrt(-2 * std::log(std::max(r.uniform(), 1e-300))) * std::cos(6.283185307179586 * r.uniform());
+      int64_t L = (int64_t)std::llround(std::exp(mu + sigma * g));
+      L = std::max<int64_t>(1, std::min<int64_t>({L, 20000, n_items}));
+      row.clear();
+      size_t cap = 64;
+      while (cap < (size_t)L * 2 + 64) cap <<= 1;
+      table.assign(cap, -1);
+      auto add = [&](int64_t it) {
+        size_t h = (size_t)mix64((uint64_t)it) & (cap - 1);
+        while (table[h] != -1) { if (table[h] == it) return; h = (h + 1) & (cap - 1); }
+        table[h] = it;
+        row.push_back(it);
+      };
+      for (int64_t w : topics[(size_t)topic_law.sample(r)])
+        if (r.uniform() < 0.8) add(w);
+      for (int64_t guard = 0; (int64_t)row.size() < L && guard < L * 8; ++guard) add(words.sample(r));
+      std::sort(row.begin(), row.end());
+      for (int64_t x : row) ch.items.push_back((int32_t)(x + 2));   // value x+1, numeric id value+1
+      ch.lens.push_back((int64_t)ch.items.size());
+    }
+  });
+  return db;
 }

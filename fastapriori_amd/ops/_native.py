@@ -33,6 +33,7 @@ _HOST_SIGS = {
     "fa_txndb_free": (None, [vp]),
     "fa_hash_bytes": (u64, [cp, i64]),
     "fa_quest_generate": (vp, [i64, i64, dbl, dbl, i64, i64, u64, C.c_int, C.c_int]),
+    "fa_zipf_generate": (vp, [i64, i64, dbl, dbl, i64, dbl, dbl, i64, u64, C.c_int]),
     "fa_quest_write": (C.c_int, [cp, i64, dbl, dbl, i64, i64, u64, C.c_int, C.c_int]),
     "fa_apriori_gen": (vp, [vp, i64, C.c_int, C.c_int, vp]),
     "fa_cands_export": (None, [vp, vp, vp, vp]),

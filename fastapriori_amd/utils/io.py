@@ -101,6 +101,18 @@ def generate_shard(n_txn: int, comm, device=None, avg_len: float = 10.0, avg_pat
     return txndb_to_shard(h, device, b)
 
 
+def generate_zipf_shard(n_txn: int, comm, device=None, mean_len: float = 177.0, sigma: float = 0.5,
+                        n_items: int = 5_267_656, s: float = 1.05, q: float = 50.0, n_topics: int = 2000,
+                        seed: int = 1) -> TransactionShard:
+    """This rank's slice of a wide-vocabulary (webdocs-like) synthetic database
+    (Zipf-Mandelbrot background words + topic cores, see csrc/host/quest.cpp)."""
+    device = torch.device(device or comm.device)
+    b = n_txn * comm.rank // comm.world_size
+    e = n_txn * (comm.rank + 1) // comm.world_size
+    h = _native.host().fa_zipf_generate(b, e, mean_len, sigma, n_items, s, q, n_topics, seed, num_threads())
+    return txndb_to_shard(h, device, b)
+
+
 def write_quest_file(path: str, n_txn: int, avg_len=10.0, avg_pat=4.0, n_patterns=2000, n_items=1000,
                      seed=1, users=False) -> None:
     rc = _native.host().fa_quest_write(path.encode(), n_txn, avg_len, avg_pat, n_patterns, n_items, seed,
