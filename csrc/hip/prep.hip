@@ -43,6 +43,68 @@ __global__ __launch_bounds__(256) void k_histogram(const int32_t* __restrict__ i
 }
 
 // ---------------------------------------------------------------------------
+// Heavy-hitter F1 for wide vocabularies (webdocs-scale: millions of ids, where
+// a V-bin histogram means one global atomic per token plus a V-sized
+// all-reduce).  Pass 1: a 2-row count-min sketch (2 x 16K u32 bins = 128 KB of
+// LDS per workgroup, one workgroup per CU), each workgroup storing its private
+// sketch to partial[wg] (summed by the caller).  Pass 2: exact counts for the
+// sketch's candidates only, through an LDS open-addressing table (keys -1 =
+// empty, linear probing).  Both hashes are multiplicative; the host mirrors
+// them (fastapriori_amd/ops/primitives.py: _sk_hash) to build the table.
+// ---------------------------------------------------------------------------
+constexpr int kSkLog = 14, kSkW = 1 << kSkLog;
+constexpr uint32_t kSkA0 = 0x9E3779B1u, kSkA1 = 0x85EBCA77u;
+
+template <bool kVec, class F>
+__device__ __forceinline__ void for_each_item(const int32_t* __restrict__ items, int64_t nnz, F&& f) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n4 = kVec ? (nnz >> 2) : 0;
+  const int4* it4 = reinterpret_cast<const int4*>(items);
+  for (int64_t i = gid; i < n4; i += stride) {
+    const int4 v = it4[i];
+    f(v.x); f(v.y); f(v.z); f(v.w);
+  }
+  for (int64_t i = (n4 << 2) + gid; i < nnz; i += stride) f(items[i]);
+}
+
+template <bool kVec>
+__global__ __launch_bounds__(1024) void k_f1_sketch(const int32_t* __restrict__ items, int64_t nnz,
+                                                    uint32_t* __restrict__ partial) {
+  __shared__ uint32_t sh[2 * kSkW];
+  for (int i = threadIdx.x; i < 2 * kSkW; i += blockDim.x) sh[i] = 0;
+  __syncthreads();
+  for_each_item<kVec>(items, nnz, [&](int32_t v) {
+    atomicAdd(&sh[((uint32_t)v * kSkA0) >> (32 - kSkLog)], 1u);
+    atomicAdd(&sh[kSkW + (((uint32_t)v * kSkA1) >> (32 - kSkLog))], 1u);
+  });
+  __syncthreads();
+  uint32_t* out = partial + (size_t)blockIdx.x * 2 * kSkW;
+  for (int i = threadIdx.x; i < 2 * kSkW; i += blockDim.x) out[i] = sh[i];
+}
+
+template <bool kVec>
+__global__ __launch_bounds__(1024) void k_f1_exact(const int32_t* __restrict__ items, int64_t nnz,
+                                                   const int32_t* __restrict__ keys, int log_s,
+                                                   uint32_t* __restrict__ counts) {
+  __shared__ int32_t sk[kSkW];
+  __shared__ uint32_t sc[kSkW];
+  const int S = 1 << log_s;
+  for (int i = threadIdx.x; i < S; i += blockDim.x) { sk[i] = keys[i]; sc[i] = 0; }
+  __syncthreads();
+  for_each_item<kVec>(items, nnz, [&](int32_t v) {
+    for (uint32_t h = ((uint32_t)v * kSkA0) >> (32 - log_s);; h = (h + 1) & (S - 1)) {
+      const int32_t k = sk[h];
+      if (k == v) { atomicAdd(&sc[h], 1u); break; }
+      if (k < 0) break;
+    }
+  });
+  __syncthreads();
+  for (int i = threadIdx.x; i < S; i += blockDim.x)
+    if (sc[i]) atomicAdd(&counts[i], sc[i]);
+}
+
+// ---------------------------------------------------------------------------
 // Number of frequent ids in every transaction (ids are distinct per line).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_txn_freq_count(const int64_t* __restrict__ off,
@@ -224,6 +286,65 @@ __global__ __launch_bounds__(256) void k_compress_lds(
   const int64_t o = roff[x];
   const int64_t c = roff[x + 1] - o;
   for (int j = threadIdx.x; j < c; j += blockDim.x) ranks[o + j] = (int32_t)sh[j];
+}
+
+// Long rows, F1 <= 65536: one wave per row and no sort.  The row's tokens are
+// read coalesced 256 at a time, mapped through the LUT, and each frequent rank
+// sets its bit in a per-wave LDS bitmap (ds_or_b64).  Lane l owns words
+// l + 64m; a popcount + DPP prefix scan over the words gives every lane its
+// output position, so ranks come out ascending.  Lanes clear their own words.
+constexpr int kCwMaxWords = 16;   // words per lane -> F1 <= 16 * 64 * 64
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ __launch_bounds__(256) void k_compress_wave(
+    const int64_t* __restrict__ off, const int32_t* __restrict__ items, const int32_t* __restrict__ lut,
+    const int32_t* __restrict__ rows, int64_t nrows, const int32_t* __restrict__ kept,
+    const int64_t* __restrict__ roff, int32_t* __restrict__ ranks, int M) {
+  __shared__ unsigned long long bm[4][kCwMaxWords * 64];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  unsigned long long* b = bm[w];
+  for (int m = 0; m < M; ++m) b[lane + 64 * m] = 0;
+  wave_lds_sync();
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t i = (int64_t)blockIdx.x * 4 + w; i < nrows; i += nw) {
+    const int32_t x = rows ? rows[i] : (int32_t)i;
+    const int64_t t = kept[x];
+    const int64_t s = off[t], L = off[t + 1] - s;
+    const int64_t o = roff[x];
+    for (int64_t j0 = 0; j0 < L; j0 += 256) {
+      int32_t v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int64_t j = j0 + lane + 64 * k;
+        v[k] = j < L ? items[s + j] : -1;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = v[k] >= 0 ? lut[v[k]] : -1;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (v[k] >= 0) atomicOr(&b[v[k] >> 6], 1ull << (v[k] & 63));
+    }
+    wave_lds_sync();
+    int base = 0;
+    for (int m = 0; m < M; ++m) {
+      const int widx = lane + 64 * m;
+      unsigned long long word = b[widx];
+      b[widx] = 0;
+      const int c = __popcll(word);
+      const int incl = wave_scan_incl_dpp(c);
+      int64_t pos = o + base + incl - c;
+      base += wave_last(incl);
+      while (word) {
+        ranks[pos++] = widx * 64 + (__ffsll((long long)word) - 1);
+        word &= word - 1;
+      }
+    }
+    wave_lds_sync();
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -413,10 +534,64 @@ FA_API int fa_hip_histogram(const int32_t* items, int64_t nnz, int32_t V, uint32
   FA_LAUNCH_RET();
 }
 
-FA_API int fa_hip_txn_freq_count(const int64_t* off, const int32_t* items, int64_t n,
+// Long documents: one wave per row, a ballot per 64 tokens.
+__global__ __launch_bounds__(256) void k_txn_freq_count_wave(const int64_t* __restrict__ off,
+                                                             const int32_t* __restrict__ items, int64_t n,
+                                                             const int32_t* __restrict__ lut,
+                                                             int32_t* __restrict__ cnt) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t t = (int64_t)blockIdx.x * 4 + w; t < n; t += nw) {
+    const int64_t s = off[t], L = off[t + 1] - s;
+    int32_t c = 0;
+    for (int64_t j0 = 0; j0 < L; j0 += 256) {
+      int32_t v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int64_t j = j0 + lane + 64 * k;
+        v[k] = j < L ? items[s + j] : -1;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) c += __popcll(__ballot(v[k] >= 0 && lut[v[k]] >= 0));
+    }
+    if (lane == 0) cnt[t] = c;
+  }
+}
+
+static int f1_grid(int64_t nnz) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>(256, (nnz + 1024 * 64 - 1) / (1024 * 64)));
+}
+
+// partial: [f1_grid(nnz)][2 * 16384] u32; returns the number of partial sketches via *nwg.
+FA_API int fa_hip_f1_sketch(const int32_t* items, int64_t nnz, uint32_t* partial, int* nwg, hipStream_t st) {
+  const int g = f1_grid(nnz);
+  *nwg = g;
+  if (nnz <= 0) return 0;
+  if (((uintptr_t)items & 15) == 0) hipLaunchKernelGGL(k_f1_sketch<true>, dim3(g), dim3(1024), 0, st, items, nnz, partial);
+  else hipLaunchKernelGGL(k_f1_sketch<false>, dim3(g), dim3(1024), 0, st, items, nnz, partial);
+  FA_LAUNCH_RET();
+}
+
+FA_API int fa_hip_f1_exact(const int32_t* items, int64_t nnz, const int32_t* keys, int log_s, uint32_t* counts,
+                           hipStream_t st) {
+  if (nnz <= 0) return 0;
+  if (log_s < 6 || log_s > kSkLog) return 1;
+  const int g = f1_grid(nnz);
+  if (((uintptr_t)items & 15) == 0)
+    hipLaunchKernelGGL(k_f1_exact<true>, dim3(g), dim3(1024), 0, st, items, nnz, keys, log_s, counts);
+  else
+    hipLaunchKernelGGL(k_f1_exact<false>, dim3(g), dim3(1024), 0, st, items, nnz, keys, log_s, counts);
+  FA_LAUNCH_RET();
+}
+
+FA_API int fa_hip_txn_freq_count(const int64_t* off, const int32_t* items, int64_t n, int64_t nnz,
                                  const int32_t* lut, int32_t* cnt, hipStream_t st) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(k_txn_freq_count, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, off, items, n, lut, cnt);
+  if (nnz > 48 * n)
+    hipLaunchKernelGGL(k_txn_freq_count_wave, dim3((unsigned)std::min<int64_t>((n + 3) / 4, 8192)), dim3(256), 0, st,
+                       off, items, n, lut, cnt);
+  else
+    hipLaunchKernelGGL(k_txn_freq_count, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, off, items, n, lut, cnt);
   FA_LAUNCH_RET();
 }
 
@@ -450,6 +625,19 @@ FA_API int fa_hip_compress_lds(const int64_t* off, const int32_t* items, const i
                                int32_t* n_too_long, hipStream_t st) {
   if (nrows <= 0) return 0;
   hipLaunchKernelGGL(k_compress_lds, dim3((unsigned)nrows), dim3(256), 0, st, off, items, lut, rows, kept, roff, ranks, too_long, n_too_long);
+  FA_LAUNCH_RET();
+}
+
+// rows == nullptr: kept rows 0..nrows-1.  Requires F1 <= 65536.
+FA_API int fa_hip_compress_wave(const int64_t* off, const int32_t* items, const int32_t* lut, const int32_t* rows,
+                                int64_t nrows, const int32_t* kept, const int64_t* roff, int32_t* ranks, int F1,
+                                hipStream_t st) {
+  if (nrows <= 0) return 0;
+  const int M = (F1 + 4095) / 4096;
+  if (M > kCwMaxWords) return 1;
+  const int64_t g = std::min<int64_t>((nrows + 3) / 4, 8192);
+  hipLaunchKernelGGL(k_compress_wave, dim3((unsigned)g), dim3(256), 0, st, off, items, lut, rows, nrows, kept, roff,
+                     ranks, std::max(M, 1));
   FA_LAUNCH_RET();
 }
 

@@ -145,3 +145,19 @@ FA_API void fa_cpu_count_candidates(const uint64_t* bm, int64_t Wp, int64_t W,
     }
   });
 }
+
+// Open-addressing probe table for the heavy-hitter F1 exact pass
+// (csrc/hip/prep.hip k_f1_exact): keys[S] = -1 or a candidate id, linear
+// probing from the multiplicative hash (id * a) >> (32 - log_s).  slot[i]
+// receives the position of ids[i].
+FA_API void fa_build_probe_table(const int64_t* ids, int64_t n, int log_s, uint32_t a, int32_t* keys,
+                                 int64_t* slot) {
+  const uint32_t S = 1u << log_s;
+  for (uint32_t i = 0; i < S; ++i) keys[i] = -1;
+  for (int64_t i = 0; i < n; ++i) {
+    uint32_t h = ((uint32_t)ids[i] * a) >> (32 - log_s);
+    while (keys[h] != -1 && keys[h] != (int32_t)ids[i]) h = (h + 1) & (S - 1);
+    keys[h] = (int32_t)ids[i];
+    slot[i] = h;
+  }
+}

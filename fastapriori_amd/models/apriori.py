@@ -44,6 +44,9 @@ from .data import MiningResult, TransactionShard
 # word pairs for the Gram kernel.
 HORIZONTAL_PAIRS_PER_S = 2.0e11
 GRAM_WORDPAIRS_PER_S = 1.2e13
+# numeric vocabularies at least this wide count F1 with the sketch + exact pass
+F1_SKETCH_MIN_VOCAB = 1 << 20
+F1_MAX_CANDIDATES = ops.primitives.F1_MAX_CANDIDATES
 
 
 @dataclass
@@ -55,6 +58,7 @@ class MinerConfig:
     max_level: int = 0              # 0 = unlimited
     level_kernel: str = "auto"      # auto | slab | bitmap  (k >= 3 counting kernel)
     trim: bool = True               # transaction trimming before every level k >= 3
+    f1: str = "auto"                # auto | sketch | histogram  (frequent-item counting)
 
 
 class FastApriori:
@@ -178,21 +182,27 @@ class FastApriori:
         thr = max(mc, 1)   # only tokens that occur can be frequent (even at minSupport 0)
         if vocab.numeric:
             V = comm.allreduce_int(vocab.size, "max")
-            hist = ops.histogram(shard.items, V)
-            if shard.extras.size:
-                hist += torch.bincount(torch.from_numpy(shard.extras.astype(np.int64)), minlength=V).to(dev)
-            comm.all_reduce_(hist)
-            fid = torch.nonzero(hist >= thr).flatten()
-            fcnt = hist[fid].cpu().numpy()
-            fid = fid.cpu().numpy()
+            got = None
+            if self.cfg.f1 == "sketch" or (self.cfg.f1 == "auto" and dev.type == "cuda"
+                                              and V >= F1_SKETCH_MIN_VOCAB):
+                got = self._f1_heavy_hitters(shard, V, thr)
+            if got is None:
+                hist = ops.histogram(shard.items, V)
+                if shard.extras.size:
+                    hist += torch.bincount(torch.from_numpy(shard.extras.astype(np.int64)), minlength=V).to(dev)
+                comm.all_reduce_(hist)
+                fid = torch.nonzero(hist >= thr).flatten()
+                got = fid.cpu().numpy(), hist[fid].cpu().numpy()
+            fid, fcnt = got
             tokens = [vocab.token(int(i)) for i in fid]
             order = sorted(range(len(fid)), key=lambda j: (-int(fcnt[j]), java_string_key(tokens[j])))
             items = [tokens[j] for j in order]
             counts1 = fcnt[order].astype(np.int64)
-            lut = torch.full((max(V, 1),), -1, dtype=torch.int32)
+            lut = torch.full((max(V, 1),), -1, dtype=torch.int32, device=dev)
             if len(order):
-                lut[torch.from_numpy(fid[order].astype(np.int64))] = torch.arange(len(order), dtype=torch.int32)
-            return items, counts1, lut.to(dev)
+                lut[torch.from_numpy(fid[order].astype(np.int64)).to(dev)] = torch.arange(
+                    len(order), dtype=torch.int32, device=dev)
+            return items, counts1, lut
         # dictionary mode: agree on identity through 64-bit token hashes
         Vl = vocab.size
         hist = ops.histogram(shard.items, max(Vl, 1)).cpu().numpy()[:Vl]
@@ -234,6 +244,31 @@ class FastApriori:
                 lut_np[i] = r
         return items, counts1, torch.from_numpy(lut_np).to(dev)
 
+    def _f1_heavy_hitters(self, shard: TransactionShard, V: int, thr: int):
+        """Numeric-mode F1 for wide vocabularies without a V-bin histogram.
+
+        A count-min sketch never under-estimates, so every id with support >=
+        thr is a candidate; exact counts of the candidates then decide.  The
+        sketch (2 x 16K int64) and the candidate counts are the only all-reduces
+        (instead of V int64).  Returns None (-> plain histogram) when the sketch
+        is too crowded to leave at most ops.F1_MAX_CANDIDATES candidates; the
+        decision is identical on every rank since the reduced sketch is."""
+        comm, dev = self.comm, shard.items.device
+        sk = ops.f1_sketch(shard.items)
+        ex = torch.from_numpy(shard.extras.astype(np.int64)) if shard.extras.size else None
+        if ex is not None:
+            sk += ops.f1_sketch(ex).to(dev)
+        comm.all_reduce_(sk)
+        cand = torch.nonzero(ops.sketch_estimate(sk, torch.arange(V, device=dev)) >= thr).flatten()
+        if cand.numel() > F1_MAX_CANDIDATES:
+            return None
+        cnt = ops.f1_exact(shard.items, cand)
+        if ex is not None:
+            cnt += ops.f1_exact(ex, cand.cpu()).to(dev)
+        comm.all_reduce_(cnt)
+        keep = cnt >= thr
+        return cand[keep].cpu().numpy(), cnt[keep].cpu().numpy()
+
     # ------------------------------------------------------------------
     # Compression (FastApriori.scala:66-79) and the vertical layout
     # ------------------------------------------------------------------
@@ -245,7 +280,7 @@ class FastApriori:
         roff = torch.zeros(T + 1, dtype=torch.int64, device=dev)
         if T:
             torch.cumsum(cnt[kept.to(torch.int64)].to(torch.int64), 0, out=roff[1:])
-        ranks = ops.compress(shard.offsets, shard.items, lut, kept, roff)
+        ranks = ops.compress(shard.offsets, shard.items, lut, kept, roff, F1)
         db = {"roff": roff, "ranks": ranks, "T": T, "src": None, "ncols": T, "wword": None, "wrow": None,
               "bm": None, "W": 0, "F1": F1, "alive": np.ones(F1, dtype=bool), "c1": self._counts1}
         pair_work = 0

@@ -46,6 +46,7 @@ _HOST_SIGS = {
     "fa_recommend_cpu": (None, [vp, vp, vp, i64, i32, vp, vp, i64, vp, C.c_int]),
     "fa_write_freq_itemsets": (C.c_int, [cp, vp, vp, i32, vp, vp, vp, C.c_int, C.c_int, C.c_int]),
     "fa_cpu_histogram": (None, [vp, i64, i64, vp, C.c_int]),
+    "fa_build_probe_table": (None, [vp, i64, C.c_int, C.c_uint32, vp, vp]),
     "fa_cpu_txn_freq_count": (None, [vp, vp, i64, vp, vp, C.c_int]),
     "fa_cpu_build_bitmaps": (None, [vp, vp, vp, i64, i64, vp, C.c_int]),
     "fa_cpu_row_hash": (None, [vp, vp, i64, vp, vp, C.c_int]),
@@ -56,13 +57,16 @@ _HOST_SIGS = {
 
 _HIP_SIGS = {
     "fa_hip_histogram": (C.c_int, [vp, i64, i32, vp, vp]),
-    "fa_hip_txn_freq_count": (C.c_int, [vp, vp, i64, vp, vp, vp]),
+    "fa_hip_f1_sketch": (C.c_int, [vp, i64, vp, vp, vp]),
+    "fa_hip_f1_exact": (C.c_int, [vp, i64, vp, C.c_int, vp, vp]),
+    "fa_hip_txn_freq_count": (C.c_int, [vp, vp, i64, i64, vp, vp, vp]),
     "fa_hip_compress_regs": (C.c_int, [C.c_int, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp]),
     "fa_hip_compress_staged": (C.c_int, [vp, vp, vp, i64, vp, vp, vp, vp, vp]),
     "fa_hip_count_slab": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, vp,
                                     C.c_int, C.c_int, vp, i64, vp]),
     "fa_hip_trim_count": (C.c_int, [vp, vp, i64, vp, vp, vp]),
     "fa_hip_trim_write": (C.c_int, [vp, vp, vp, vp, i64, vp, vp, vp]),
+    "fa_hip_compress_wave": (C.c_int, [vp, vp, vp, vp, i64, vp, vp, vp, C.c_int, vp]),
     "fa_hip_compress_lds": (C.c_int, [vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp]),
     "fa_hip_row_hash": (C.c_int, [vp, vp, i64, vp, vp, vp]),
     "fa_hip_build_bitmaps": (C.c_int, [vp, vp, vp, i64, i32, i64, C.c_int, C.c_int, vp, vp, vp, vp]),

@@ -12,6 +12,7 @@ Conventions: bitmaps are int64 tensors [F1, Wp] holding raw 64-bit words
 """
 from __future__ import annotations
 
+import ctypes as C
 import os
 
 import numpy as np
@@ -51,6 +52,60 @@ def histogram(items: torch.Tensor, V: int) -> torch.Tensor:
     return out
 
 
+# ---------------------------------------------------------------------------
+# Heavy-hitter F1 (wide vocabularies; csrc/hip/prep.hip k_f1_sketch/k_f1_exact)
+# ---------------------------------------------------------------------------
+SK_LOG = 14                      # sketch bins per row (2 rows)
+SK_A = (0x9E3779B1, 0x85EBCA77)  # multiplicative hash constants (mirrored in prep.hip)
+F1_MAX_CANDIDATES = 1 << 13      # exact-pass LDS table: 16K slots at load <= 0.5
+
+
+def sk_hash(ids: torch.Tensor, a: int, log: int = SK_LOG) -> torch.Tensor:
+    """(uint32(id) * a) >> (32 - log), as int64."""
+    return ((ids.to(_I64) * a) & 0xFFFFFFFF) >> (32 - log)
+
+
+def f1_sketch(items: torch.Tensor) -> torch.Tensor:
+    """2-row count-min sketch of the ids in ``items`` -> int64 [2, 2**SK_LOG]."""
+    W = 1 << SK_LOG
+    if items.is_cuda:
+        nwg = C.c_int(0)
+        partial = torch.empty(256 * 2 * W, dtype=_I32, device=items.device)
+        _hip_call("fa_hip_f1_sketch", _p(items), items.numel(), _p(partial), C.addressof(nwg), _stream(items))
+        # per-workgroup counts < 2^31 (a workgroup sees at most nnz/nwg tokens)
+        return partial[: nwg.value * 2 * W].view(max(nwg.value, 1), 2, W).sum(0, dtype=_I64) if nwg.value else \
+            torch.zeros(2, W, dtype=_I64, device=items.device)
+    return torch.stack([torch.bincount(sk_hash(items, a), minlength=W) for a in SK_A])
+
+
+def sketch_estimate(sk: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
+    return torch.minimum(sk[0][sk_hash(ids, SK_A[0])], sk[1][sk_hash(ids, SK_A[1])])
+
+
+def f1_exact(items: torch.Tensor, cand: torch.Tensor) -> torch.Tensor:
+    """Exact occurrence counts of the (distinct) ids ``cand`` in ``items`` -> int64 [len(cand)]."""
+    n = cand.numel()
+    assert n <= F1_MAX_CANDIDATES
+    if n == 0:
+        return torch.zeros(0, dtype=_I64, device=items.device)
+    if items.is_cuda:
+        log_s = max(6, (2 * n - 1).bit_length())
+        ids = cand.to(_I64).cpu().contiguous()
+        keys = torch.empty(1 << log_s, dtype=_I32)
+        slot = torch.empty(n, dtype=_I64)
+        _native.host().fa_build_probe_table(_p(ids), n, log_s, SK_A[0], _p(keys), _p(slot))
+        counts = torch.zeros(1 << log_s, dtype=_I32, device=items.device)
+        _hip_call("fa_hip_f1_exact", _p(items), items.numel(), _p(keys.to(items.device)), log_s, _p(counts),
+                  _stream(items))
+        return counts[slot.to(items.device)].to(_I64)
+    srt, order = torch.sort(cand.to(_I64))
+    pos = torch.searchsorted(srt, items.to(_I64)).clamp_(max=n - 1)
+    hit = srt[pos] == items.to(_I64)
+    out = torch.zeros(n, dtype=_I64)
+    out[order] = torch.bincount(pos[hit], minlength=n)
+    return out
+
+
 def txn_freq_count(offsets: torch.Tensor, items: torch.Tensor, lut: torch.Tensor) -> torch.Tensor:
     """Number of frequent ids (``lut[id] >= 0``) per transaction -> int32 [n]."""
     n = offsets.numel() - 1
@@ -58,14 +113,25 @@ def txn_freq_count(offsets: torch.Tensor, items: torch.Tensor, lut: torch.Tensor
     if n <= 0:
         return out
     if items.is_cuda:
-        _hip_call("fa_hip_txn_freq_count", _p(offsets), _p(items), n, _p(lut), _p(out), _stream(items))
+        _hip_call("fa_hip_txn_freq_count", _p(offsets), _p(items), n, items.numel(), _p(lut), _p(out),
+                  _stream(items))
     else:
         _native.host().fa_cpu_txn_freq_count(_p(offsets), _p(items), n, _p(lut), _p(out), num_threads())
     return out
 
 
-def compress(offsets, items, lut, kept, roff) -> torch.Tensor:
-    """Kept transaction x -> its frequent ranks sorted ascending, CSR by ``roff``."""
+COMPRESS_WAVE_MAX_F1 = 65536
+COMPRESS_WAVE_MEAN_LEN = 48    # mean row length above which every row goes to the wave kernel
+
+
+def compress(offsets, items, lut, kept, roff, F1: int | None = None) -> torch.Tensor:
+    """Kept transaction x -> its frequent ranks sorted ascending, CSR by ``roff``.
+
+    Device tiers (csrc/hip/prep.hip), chosen by row length L: L <= 16 LDS-staged
+    register sort; L <= 64 register bitonic network; longer rows one wave per
+    row with an LDS rank bitmap (no sort; F1 <= 65536) or, for wider F1, a
+    workgroup LDS bitonic sort.  Long-document data (mean L large) skips the
+    first two tiers."""
     T = kept.numel()
     nnz = int(roff[-1].item()) if T else 0
     ranks = torch.empty(max(nnz, 1), dtype=_I32, device=items.device)
@@ -74,6 +140,11 @@ def compress(offsets, items, lut, kept, roff) -> torch.Tensor:
     if not items.is_cuda:
         return _compress_torch(offsets, items, lut, kept, roff, ranks, None)[:nnz]
     st = _stream(items)
+    wave_ok = F1 is not None and F1 <= COMPRESS_WAVE_MAX_F1
+    if wave_ok and items.numel() > COMPRESS_WAVE_MEAN_LEN * max(offsets.numel() - 1, 1):
+        _hip_call("fa_hip_compress_wave", _p(offsets), _p(items), _p(lut), None, T, _p(kept), _p(roff),
+                  _p(ranks), F1, st)
+        return ranks[:nnz]
     flag = torch.empty(T, dtype=torch.int8, device=items.device)
     _hip_call("fa_hip_compress_staged", _p(offsets), _p(items), _p(lut), T, _p(kept), _p(roff), _p(ranks),
               _p(flag), st)
@@ -85,7 +156,10 @@ def compress(offsets, items, lut, kept, roff) -> torch.Tensor:
                   _p(roff), _p(ranks), _p(flag2), st)
         over2 = over[torch.nonzero(flag2).flatten()].contiguous()
         n2 = over2.numel()
-        if n2:
+        if n2 and wave_ok:
+            _hip_call("fa_hip_compress_wave", _p(offsets), _p(items), _p(lut), _p(over2), n2, _p(kept), _p(roff),
+                      _p(ranks), F1, st)
+        elif n2:
             over3 = torch.empty(n2, dtype=_I32, device=items.device)
             n_over3 = torch.zeros(1, dtype=_I32, device=items.device)
             _hip_call("fa_hip_compress_lds", _p(offsets), _p(items), _p(lut), _p(over2), n2, _p(kept),

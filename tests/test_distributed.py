@@ -33,6 +33,21 @@ def _mine_file(path_prefix: str, ms: float, dedup: str, strategy: str):
         shutdown_comm(comm)
 
 
+def _mine_zipf(n: int, ms: float, f1: str):
+    from fastapriori_amd.models.apriori import FastApriori, MinerConfig
+    from fastapriori_amd.parallel.comm import init_comm, shutdown_comm
+    from fastapriori_amd.utils.io import generate_zipf_shard
+    from fastapriori_amd.utils.metrics import Logger
+
+    comm = init_comm("cpu")
+    try:
+        shard = generate_zipf_shard(n, comm, "cpu", mean_len=40.0, n_items=1_500_000, n_topics=40, seed=3)
+        res = FastApriori(ms, comm, MinerConfig(min_support=ms, f1=f1), Logger(comm.rank, enabled=False)).run(shard)
+        return res.as_dict(), res.items
+    finally:
+        shutdown_comm(comm)
+
+
 def _mine_generated(n: int, ms: float):
     from fastapriori_amd.models.apriori import FastApriori, MinerConfig
     from fastapriori_amd.parallel.comm import init_comm, shutdown_comm
@@ -99,3 +114,10 @@ def test_generated_shards_are_world_size_invariant():
     for world in (2, 3):
         outs = spawn_local(_mine_generated, world, 6000, 0.02)
         assert all(o == ref for o in outs)
+
+
+def test_heavy_hitter_f1_across_ranks():
+    # sketch all-reduce -> identical candidates on every rank -> exact all-reduce
+    ref = spawn_local(_mine_zipf, 1, 3000, 0.03, "histogram")[0]
+    outs = spawn_local(_mine_zipf, 2, 3000, 0.03, "sketch")
+    assert all(o == ref for o in outs) and len(ref[0]) > 20

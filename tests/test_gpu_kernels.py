@@ -77,6 +77,20 @@ def test_txn_count_and_compress():
     ref = ops.compress(off, items, lut, kept, roff)
     got = ops.compress(off.to(DEV), items.to(DEV), lut.to(DEV), kept.to(DEV), roff.to(DEV)).cpu()
     assert torch.equal(ref, got)
+    # long-row tier: wave-per-row rank bitmap instead of the LDS sort
+    got = ops.compress(off.to(DEV), items.to(DEV), lut.to(DEV), kept.to(DEV), roff.to(DEV), F1).cpu()
+    assert torch.equal(ref, got)
+
+
+@pytest.mark.parametrize("V,frac", [(900, 0.5), (9000, 0.7)])
+def test_compress_long_documents(V, frac):
+    # mean row length > 48 -> every row through the wave kernel (F1 > 4096 -> 2 words per lane)
+    off, items, lut, F1 = _prep(n=1500, V=V, max_len=400, seed=3, long_rows=0, F1_frac=frac)
+    cnt, kept, roff = _compress_inputs(off, items, lut)
+    assert torch.equal(cnt, ops.txn_freq_count(off.to(DEV), items.to(DEV), lut.to(DEV)).cpu())
+    ref = ops.compress(off, items, lut, kept, roff)
+    got = ops.compress(off.to(DEV), items.to(DEV), lut.to(DEV), kept.to(DEV), roff.to(DEV), F1).cpu()
+    assert torch.equal(ref, got)
 
 
 def test_row_hash_matches_host():
@@ -186,3 +200,24 @@ def test_pair_kernels_agree(monkeypatch, kernel):
     refw = ops.pair_counts_horizontal(roff, ranks, w, F1)
     gotw = ops.pair_counts_horizontal(roff.to(DEV), ranks.to(DEV), w.to(DEV), F1).cpu()
     assert torch.equal(refw, gotw)
+
+
+@pytest.mark.parametrize("offset", [0, 1])
+def test_f1_sketch_and_exact(offset):
+    rng = np.random.default_rng(7)
+    ids = (rng.zipf(1.3, 2_000_003) % 3_000_000).astype(np.int32)
+    items = torch.from_numpy(ids)[offset:]
+    sk_cpu = ops.f1_sketch(items)
+    sk_gpu = ops.f1_sketch(items.to(DEV)).cpu()
+    assert torch.equal(sk_cpu, sk_gpu)
+    cand = torch.from_numpy(np.unique(ids[:5000])[:3000].astype(np.int64))
+    assert torch.equal(ops.f1_exact(items, cand), ops.f1_exact(items.to(DEV), cand.to(DEV)).cpu())
+
+
+def test_wide_vocab_miner_matches_cpu():
+    from fastapriori_amd.utils.io import generate_zipf_shard
+    sh = generate_zipf_shard(20000, Comm(), "cpu", mean_len=80.0, n_items=3_000_000, n_topics=100)
+    cfg = MinerConfig(min_support=0.02)
+    ref = FastApriori(0.02, config=MinerConfig(min_support=0.02, f1="histogram")).run(sh)
+    got = FastApriori(0.02, config=cfg).run(sh.to(DEV))
+    assert got.items == ref.items and got.as_dict() == ref.as_dict() and ref.n_itemsets > 100

@@ -110,3 +110,23 @@ def test_min_count_rounding():
     assert min_count(0.07, 100) == 8                   # 0.07*100 = 7.000000000000001 in IEEE double
     assert min_count(0.25, 7) == 2
     assert min_count(0.0, 5) == 0
+
+
+@pytest.mark.parametrize("data", [b"1 1 1 2\n3\n3\n", b"5 5 6\n5 6 7\n5 6\n\n6 6 6 6\n"])
+def test_heavy_hitter_f1_matches_histogram(data):
+    # sketch + exact pass (wide-vocabulary F1) must equal the plain histogram,
+    # including duplicate-token "extras" and the empty-line token
+    out = []
+    for f1 in ("sketch", "histogram"):
+        res = FastApriori(0.3, config=MinerConfig(min_support=0.3, f1=f1)).run(parse_bytes(data))
+        out.append((res.items, res.as_dict()))
+    assert out[0] == out[1]
+
+
+def test_heavy_hitter_f1_wide_vocab():
+    from fastapriori_amd.parallel.comm import Comm
+    from fastapriori_amd.utils.io import generate_zipf_shard
+    sh = generate_zipf_shard(3000, Comm(), "cpu", mean_len=60.0, n_items=2_000_000, n_topics=50)
+    a = FastApriori(0.03, config=MinerConfig(min_support=0.03, f1="sketch")).run(sh)
+    b = FastApriori(0.03, config=MinerConfig(min_support=0.03, f1="histogram")).run(sh)
+    assert a.items == b.items and a.as_dict() == b.as_dict() and a.n_itemsets > 50
