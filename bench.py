@@ -118,7 +118,8 @@ def main() -> int:
                        "n_itemsets": n_sets, "levels": [len(c) for c in res.counts],
                        "pair_strategy": miner.stats.get("pair_strategy"),
                        "min_count": res.min_count, "gen_s": round(t_gen, 2),
-                       **({"phase_ms": miner.stats["phase_ms"]} if "phase_ms" in miner.stats else {})},
+                       **({"phase_ms": miner.stats["phase_ms"]} if "phase_ms" in miner.stats else {}),
+                       **({"level_info": miner.stats["level_info"]} if "level_info" in miner.stats else {})},
         }
         print(json.dumps(line), flush=True)
     shutdown_comm(comm)

@@ -13,6 +13,8 @@
 //     candidates over a super-chunk of bitmap words; wave reductions into an
 //     LDS accumulator, one coalesced global atomic per candidate per chunk.
 // All accumulation is integer, so results are exact and order-independent.
+#include <cstdlib>
+
 #include "fa_hip.h"
 
 namespace fa {
@@ -561,14 +563,62 @@ __global__ __launch_bounds__(256) void k_count_candidates(
 // ---------------------------------------------------------------------------
 constexpr int kSlabThreads = 1024;
 
-template <int SW, bool kWeighted, bool kFromBM>
+// Slab build modes: per-column rank prefetch (dedup: columns gather rows through
+// src), wave-cooperative coalesced build (columns = rows, contiguous ranks), or
+// a copy from the materialised used-item bitmap (multi-pass levels).
+enum { kBuildCols = 0, kBuildContig = 1, kBuildBM = 2 };
+
+// Coalesced slab build for one 64-column word q of the tile: the 64 rows'
+// ranks are one contiguous span, read 2 x 64 at a time; a rank's column is the
+// last row whose start is <= its position (6-step binary search over the row
+// starts held one per lane, __shfl).  Empty rows are skipped by the search.
+// nsub waves share one word: wave h of them takes window groups h, h + nsub, ...
+// A rank's column (bit) is the row owning its position: rows are non-empty, so
+// it is (row starts before the window) + popc(start mask & lanes <= me) - 1.
+__device__ __forceinline__ void slab_build_word(uint64_t* __restrict__ slab, int swp, int q, int64_t col0,
+                                                int64_t ncols, const int64_t* __restrict__ roff,
+                                                const int32_t* __restrict__ ranks,
+                                                const int32_t* __restrict__ item_map, int h, int nsub,
+                                                unsigned long long* words) {
+  const int lane = threadIdx.x & 63;
+  const int64_t st = roff[min(col0 + lane, ncols)];
+  const int64_t base = roff[col0];
+  const int64_t end = roff[min(col0 + 64, ncols)];
+  const int srel = (int)(st - base);
+  const int n = (int)(end - base);
+  const unsigned long long le = lanes_le_mask();
+  constexpr int U = 2;                                // windows in flight per wave (4 measured slower)
+  for (int p0 = 64 * U * h; p0 < n; p0 += 64 * U * nsub) {
+    int r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int p = p0 + 64 * u + lane;
+      r[u] = p < n ? ranks[base + p] : -1;
+    }
+    // starts before p0: rows with srel < p0 (ballot over the row owners)
+    const int cs0 = __popcll(__ballot(srel < p0));
+    unsigned long long S[U];
+    window_starts<U>(words, srel, p0, S);
+    int cs = cs0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int l = cs + __popcll(S[u] & le) - 1;
+      const int uu = r[u] >= 0 ? item_map[r[u]] : -1;
+      if (uu >= 0) atomicOr((unsigned long long*)(slab + (size_t)uu * swp + q), 1ull << l);
+      cs += __popcll(S[u]);
+    }
+  }
+}
+
+template <int SW, bool kWeighted, int kBuild>
 __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
     const int64_t* __restrict__ roff, const int32_t* __restrict__ ranks, const int32_t* __restrict__ src,
     int64_t ncols, const int32_t* __restrict__ item_map, int n_used, const int32_t* __restrict__ gpre, int m,
     const int32_t* __restrict__ gext_off, const int32_t* __restrict__ gext, int G, int C,
     const int32_t* __restrict__ wword, uint32_t* __restrict__ out, const uint64_t* __restrict__ bm,
-    int64_t Wp) {
+    int64_t Wp, int dbg) {
   extern __shared__ uint4 lds4[];                  // 16-B aligned base
+  __shared__ unsigned long long build_words[kSlabThreads / 64 * 2];   // window_starts scratch
   constexpr int SWP = SW + 2;                       // row stride: 16-B aligned, odd number of 16-B slots
   constexpr int CPT = SW * 64 / kSlabThreads > 0 ? SW * 64 / kSlabThreads : 1;   // columns per thread
   constexpr int RPC = 32 / CPT;                     // ranks per column prefetched in registers
@@ -582,7 +632,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
   int64_t pbeg[CPT], plen[CPT];
   int32_t pv[CPT][RPC];
   auto prefetch = [&](int64_t sb) {
-    if (kFromBM) return;
+    if (kBuild != kBuildCols) return;
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
       const int j = threadIdx.x + c * kSlabThreads;
@@ -599,7 +649,9 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
   for (int64_t sb = blockIdx.x; sb < nslabs; sb += gridDim.x) {
     const int64_t w0 = sb * SW;
     __syncthreads();
-    if (kFromBM) {
+    if (dbg & 1) {
+      // profiling split (FA_SLAB_DEBUG=1): no slab build
+    } else if (kBuild == kBuildBM) {
       // multi-pass level: the used-item bitmap is materialised once; copy the slab tile
       for (int i = threadIdx.x; i < n_used * SW; i += blockDim.x) {
         const int u = i / SW, q = i - u * SW;
@@ -612,6 +664,15 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
         for (int i = threadIdx.x; i < n_used * SWP / 2; i += blockDim.x) s4[i] = z;
       }
       __syncthreads();
+      if (kBuild == kBuildContig) {
+        constexpr int NW = kSlabThreads / 64;                 // waves
+        constexpr int NSUB = NW > SW ? NW / SW : 1;           // waves per word
+        const int wv = threadIdx.x >> 6;
+        for (int q = wv / NSUB; q < SW; q += NW / NSUB)
+          if ((w0 + q) * 64 < ncols)
+            slab_build_word(slab, SWP, q, (w0 + q) * 64, ncols, roff, ranks, item_map, wv % NSUB, NSUB,
+                            build_words + wv * 2);
+      } else {
 #pragma unroll
       for (int c = 0; c < CPT; ++c) {
         const int j = threadIdx.x + c * kSlabThreads;
@@ -628,6 +689,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
           if (uu >= 0) atomicOr((unsigned long long*)(base + (size_t)uu * SWP), bit);
         }
       }
+      }
     }
     __syncthreads();
     prefetch(sb + gridDim.x);                       // overlaps the counting below
@@ -635,8 +697,8 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
 #pragma unroll
     for (int q = 0; q < SW; ++q) wt[q] = kWeighted ? ((w0 + q < W) ? wword[w0 + q] : 0) : 1;
     // work pieces: a prefix with <= 8 extensions, host-sorted by size so the lanes of
-    // a wave run loops of (nearly) equal length
-    for (int g = threadIdx.x; g < G; g += blockDim.x) {
+    // a wave run loops of (nearly) equal length (FA_SLAB_DEBUG=2: no counting)
+    for (int g = threadIdx.x; g < ((dbg & 2) ? 0 : G); g += blockDim.x) {
       uint4 p[SW / 2];
       const int32_t* pr = gpre + (size_t)g * m;
       {
@@ -763,26 +825,30 @@ FA_API int fa_hip_count_slab(const int64_t* roff, const int32_t* ranks, const in
                              uint32_t* out, int sw, int n_wg, const uint64_t* bm, int64_t Wp, hipStream_t st) {
   if (G <= 0 || C <= 0 || ncols <= 0) return 0;
   const size_t lds = (size_t)n_used * (sw + 2) * 8 + (size_t)C * 4;
-  if (lds > 160 * 1024) return 3;
+  if (lds > 160 * 1024 - 512) return 3;   // static build_words scratch
   dim3 g((unsigned)n_wg), b(kSlabThreads);
   using KernT = void (*)(const int64_t*, const int32_t*, const int32_t*, int64_t, const int32_t*, int,
                          const int32_t*, int, const int32_t*, const int32_t*, int, int, const int32_t*,
-                         uint32_t*, const uint64_t*, int64_t);
+                         uint32_t*, const uint64_t*, int64_t, int);
   KernT kern = nullptr;
-#define FA_SLAB_CASE(S)                                                                              \
-  if (sw == S) {                                                                                     \
-    if (bm) kern = wword ? (KernT)k_count_slab<S, true, true> : (KernT)k_count_slab<S, false, true>;  \
-    else kern = wword ? (KernT)k_count_slab<S, true, false> : (KernT)k_count_slab<S, false, false>;   \
+#define FA_SLAB_MODE(S, B) kern = wword ? (KernT)k_count_slab<S, true, B> : (KernT)k_count_slab<S, false, B>;
+#define FA_SLAB_CASE(S)                                   \
+  if (sw == S) {                                          \
+    if (bm) { FA_SLAB_MODE(S, kBuildBM) }                 \
+    else if (src) { FA_SLAB_MODE(S, kBuildCols) }         \
+    else { FA_SLAB_MODE(S, kBuildContig) }                \
   }
   FA_SLAB_CASE(4)
   FA_SLAB_CASE(8)
   FA_SLAB_CASE(16)
   FA_SLAB_CASE(32)
 #undef FA_SLAB_CASE
+#undef FA_SLAB_MODE
   if (!kern) return 1;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const int dbg = getenv("FA_SLAB_DEBUG") ? atoi(getenv("FA_SLAB_DEBUG")) : 0;
   hipLaunchKernelGGL(kern, g, b, lds, st, roff, ranks, src, ncols, item_map, n_used, gpre, m, gext_off, gext, G, C,
-                     wword, out, bm, Wp);
+                     wword, out, bm, Wp, dbg);
   FA_LAUNCH_RET();
 }
 

@@ -52,6 +52,38 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
   return v;
 }
 
+// Orders this wave's LDS accesses (a wave's LDS ops execute in issue order;
+// this keeps the compiler from reordering them and waits for completion).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Row-start masks for U consecutive 64-position windows of a wave's CSR span.
+// Lane l owns row l = [srel, ...) (rows non-empty, so starts are distinct);
+// bit j of S[u] is set when a row starts at position q0 + 64u + j.  words: U
+// per-wave LDS scratch words.  The owner row of position q0 + 64u + lane is then
+// (starts before the window) + popc(S[u] & lanes <= lane) - 1.
+template <int U>
+__device__ __forceinline__ void window_starts(unsigned long long* words, int srel, int q0,
+                                              unsigned long long (&S)[U]) {
+  const int lane = (int)(threadIdx.x & 63);
+  if (lane < U) words[lane] = 0ull;
+  wave_lds_sync();
+  const int b = srel - q0;
+  if (b >= 0 && b < 64 * U) atomicOr(&words[b >> 6], 1ull << (b & 63));
+  wave_lds_sync();
+#pragma unroll
+  for (int u = 0; u < U; ++u) S[u] = words[u];
+  wave_lds_sync();
+}
+
+__device__ __forceinline__ unsigned long long lanes_le_mask() {
+  const int lane = (int)(threadIdx.x & 63);
+  return lane == 63 ? ~0ull : ((2ull << lane) - 1);
+}
+
 // Bijective XCD-aware remap (cdna_hip_programming.md §5 "XCD swizzle must be
 // bijective"): consecutive logical ids land on the same XCD's L2.
 __device__ __forceinline__ uint32_t xcd_remap(uint32_t orig, uint32_t nwg) {

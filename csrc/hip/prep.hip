@@ -294,11 +294,6 @@ __global__ __launch_bounds__(256) void k_compress_lds(
 // l + 64m; a popcount + DPP prefix scan over the words gives every lane its
 // output position, so ranks come out ascending.  Lanes clear their own words.
 constexpr int kCwMaxWords = 16;   // words per lane -> F1 <= 16 * 64 * 64
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 __global__ __launch_bounds__(256) void k_compress_wave(
     const int64_t* __restrict__ off, const int32_t* __restrict__ items, const int32_t* __restrict__ lut,
@@ -431,87 +426,167 @@ __global__ __launch_bounds__(256) void k_build_bitmaps(
 }
 
 // ---------------------------------------------------------------------------
-// Transaction trimming before level k: an item can only matter if it occurs in
-// some level-k candidate, and a row only if it keeps >= k such items.  Pass 1
-// counts surviving items per row; pass 2 compacts the kept rows.  Both stage a
-// 256-row span through LDS with all loads issued back to back.
+// Transaction trimming before level k (an item matters only if it occurs in a
+// level-k candidate, a row only if it keeps >= k such items), as count -> scan
+// of block sums -> emit, wave-cooperative: a wave owns
+// 64 consecutive rows and streams their (contiguous) ranks 64 at a time,
+// coalesced; lane l also owns row l.  The alive table is in LDS.
+//   count: row l's alive count = sum over windows of popc(ballot(alive) & the
+//          window lanes inside row l);
+//   emit:  a rank's slot in its new row = the row's alive ranks in earlier
+//          windows (carried by the row's owner lane) + alive lanes of the same
+//          row below it in this window (ballot prefix), so the new CSR is
+//          written without any staging buffer.
+// Rows are dropped when they keep < min_len items (or weight 0).
 // ---------------------------------------------------------------------------
-constexpr int kTSpan = 8192;
-constexpr int kTPer = kTSpan / 256;
-
-__global__ __launch_bounds__(256) void k_trim_count(const int64_t* __restrict__ roff,
-                                                    const int32_t* __restrict__ ranks, int64_t T,
-                                                    const int8_t* __restrict__ alive, int32_t* __restrict__ cnt) {
-  __shared__ uint8_t buf[kTSpan];
-  const int64_t x0 = (int64_t)blockIdx.x * blockDim.x;
-  const int64_t x1 = min(T, x0 + (int64_t)blockDim.x);
-  const int64_t x = x0 + threadIdx.x;
-  const int64_t base = roff[x0], n = roff[x1] - base;
-  const int64_t s = x < x1 ? roff[x] : 0, e = x < x1 ? roff[x + 1] : 0;
-  const bool staged = n <= kTSpan;
-  if (staged) {
-    int32_t v[kTPer];
-#pragma unroll
-    for (int k = 0; k < kTPer; ++k) {
-      const int64_t i = threadIdx.x + k * 256;
-      v[k] = i < n ? ranks[base + i] : 0;
-    }
-#pragma unroll
-    for (int k = 0; k < kTPer; ++k) {
-      const int64_t i = threadIdx.x + k * 256;
-      if (i < n) buf[i] = (uint8_t)alive[v[k]];
-    }
-  }
+__device__ __forceinline__ int block_excl_scan256(int v, int* wtot, int* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int incl = wave_scan_incl_dpp(v);
+  if (lane == 63) wtot[w] = incl;
   __syncthreads();
-  if (x >= x1) return;
-  int32_t c = 0;
-  if (staged) for (int64_t i = s; i < e; ++i) c += buf[i - base];
-  else for (int64_t i = s; i < e; ++i) c += alive[ranks[i]];
-  cnt[x] = c;
+  int before = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) { before += k < w ? wtot[k] : 0; tot += wtot[k]; }
+  __syncthreads();
+  *total = tot;
+  return before + incl - v;
 }
 
-__global__ __launch_bounds__(256) void k_trim_write(const int64_t* __restrict__ roff,
-                                                    const int32_t* __restrict__ ranks,
-                                                    const int8_t* __restrict__ alive,
-                                                    const int32_t* __restrict__ kept, int64_t K,
-                                                    const int64_t* __restrict__ nroff, int32_t* __restrict__ nranks) {
-  __shared__ int32_t bin[kTSpan];
-  __shared__ int32_t bout[kTSpan];
-  const int64_t y0 = (int64_t)blockIdx.x * blockDim.x;
-  const int64_t y1 = min(K, y0 + (int64_t)blockDim.x);
-  const int64_t y = y0 + threadIdx.x;
-  const int64_t t = y < y1 ? (int64_t)kept[y] : 0;
-  const int64_t base = roff[kept[y0]], n = roff[(int64_t)kept[y1 - 1] + 1] - base;
-  const int64_t s = roff[t], e = roff[t + 1];
-  const int64_t obase = nroff[y0], n_out = nroff[y1] - obase;
-  const int64_t o = y < y1 ? nroff[y] - obase : 0;
-  const bool staged = n <= kTSpan;
-  if (staged) {
-    int32_t v[kTPer];
+__device__ __forceinline__ unsigned long long lane_range(int lo, int hi) {   // bits [lo, hi), 0 <= lo, hi <= 64
+  const unsigned long long h = hi >= 64 ? ~0ull : ((1ull << hi) - 1);
+  const unsigned long long l = lo >= 64 ? ~0ull : ((1ull << lo) - 1);
+  return hi > lo ? (h & ~l) : 0ull;
+}
+
+constexpr int kTrimAliveLds = 32768;
+
+struct TrimWave {
+  int64_t base;   // first rank position of the wave's rows
+  int n;          // ranks in the wave's rows
+  int srel, erel; // this lane's row [srel, erel) relative to base
+};
+
+__device__ __forceinline__ TrimWave trim_wave_setup(const int64_t* __restrict__ roff, int64_t row0, int64_t T) {
+  const int lane = threadIdx.x & 63;
+  TrimWave tw;
+  tw.base = roff[row0];
+  const int64_t end = roff[min(row0 + 64, T)];
+  tw.n = (int)(end - tw.base);
+  tw.srel = (int)(roff[min(row0 + lane, T)] - tw.base);
+  tw.erel = (int)(roff[min(row0 + lane + 1, T)] - tw.base);
+  return tw;
+}
+
+template <bool kLdsAlive>
+__global__ __launch_bounds__(256) void k_trim_scan_count(const int64_t* __restrict__ roff,
+                                                         const int32_t* __restrict__ ranks, int64_t T,
+                                                         const int8_t* __restrict__ alive, int F1, int min_len,
+                                                         const int32_t* __restrict__ wrow, int32_t* __restrict__ cnt,
+                                                         int32_t* __restrict__ bk_rows, int32_t* __restrict__ bk_nnz) {
+  extern __shared__ int8_t al[];                 // F1 bytes when kLdsAlive
+  __shared__ int wtot[4];
+  if (kLdsAlive)
+    for (int i = threadIdx.x; i < F1; i += blockDim.x) al[i] = alive[i];
+  __syncthreads();
+  const int8_t* A = kLdsAlive ? al : alive;
+  const int lane = threadIdx.x & 63;
+  const int64_t row0 = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63);
+  const int64_t row = row0 + lane;
+  int c = 0;
+  if (row0 < T) {
+    const TrimWave tw = trim_wave_setup(roff, row0, T);
+    constexpr int U = 8;                           // windows in flight per wave (memory-level parallelism)
+    for (int p0 = 0; p0 < tw.n; p0 += 64 * U) {
+      int32_t r[U];
 #pragma unroll
-    for (int k = 0; k < kTPer; ++k) {
-      const int64_t i = threadIdx.x + k * 256;
-      v[k] = i < n ? ranks[base + i] : 0;
+      for (int u = 0; u < U; ++u) {
+        const int p = p0 + 64 * u + lane;
+        r[u] = p < tw.n ? ranks[tw.base + p] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int q0 = p0 + 64 * u;
+        const unsigned long long b = __ballot(q0 + lane < tw.n && A[r[u]] != 0);
+        c += __popcll(b & lane_range(max(tw.srel - q0, 0), min(max(tw.erel - q0, 0), 64)));
+      }
     }
+  }
+  const bool keep = row < T && c >= min_len && (!wrow || wrow[row] > 0);
+  if (row < T) cnt[row] = keep ? c : -1;
+  int tr, tn;
+  (void)block_excl_scan256(keep ? 1 : 0, wtot, &tr);
+  (void)block_excl_scan256(keep ? c : 0, wtot, &tn);
+  if (threadIdx.x == 0) { bk_rows[blockIdx.x] = tr; bk_nnz[blockIdx.x] = tn; }
+}
+
+constexpr int kTrimHist = 256;
+
+template <bool kLdsAlive>
+__global__ __launch_bounds__(256) void k_trim_emit(const int64_t* __restrict__ roff, const int32_t* __restrict__ ranks,
+                                                   const int8_t* __restrict__ alive, int F1, int64_t T,
+                                                   const int32_t* __restrict__ cnt, const int64_t* __restrict__ base_rows,
+                                                   const int64_t* __restrict__ base_nnz, int64_t* __restrict__ nroff,
+                                                   int32_t* __restrict__ nranks, int32_t* __restrict__ kept,
+                                                   int64_t* __restrict__ hist) {
+  extern __shared__ int8_t al[];                 // F1 bytes when kLdsAlive
+  __shared__ uint32_t hs[kTrimHist];
+  __shared__ unsigned long long sw[4 * 4];        // per-wave window_starts scratch
+  __shared__ int wtot[4];
+  if (kLdsAlive)
+    for (int i = threadIdx.x; i < F1; i += blockDim.x) al[i] = alive[i];
+  hs[threadIdx.x] = 0;
+  const int8_t* A = kLdsAlive ? al : alive;
+  const int lane = threadIdx.x & 63;
+  const int64_t row0 = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63);
+  const int64_t row = row0 + lane;
+  const int32_t c = row < T ? cnt[row] : -1;
+  const bool keep = c >= 0;
+  int nk, nn;
+  const int rk = block_excl_scan256(keep ? 1 : 0, wtot, &nk);     // (contains __syncthreads)
+  const int ok = block_excl_scan256(keep ? c : 0, wtot, &nn);
+  const int64_t obase = base_nnz[blockIdx.x] + ok;                 // this row's first new slot
+  if (keep) {
+    nroff[base_rows[blockIdx.x] + rk] = obase;
+    kept[base_rows[blockIdx.x] + rk] = (int32_t)row;
+    atomicAdd(&hs[min(c, kTrimHist - 1)], 1u);
+  }
+  if (row0 < T && __ballot(keep) != 0ull) {
+    const TrimWave tw = trim_wave_setup(roff, row0, T);
+    // next output slot of my row (row owner view), -1 when the row is dropped
+    int64_t nxt = keep ? obase : -1;
+    unsigned long long* words = sw + (threadIdx.x >> 6) * 4;
+    const unsigned long long le = lanes_le_mask();
+    int cs = 0;                                                    // row starts before the window
+    constexpr int U = 4;
+    for (int p0 = 0; p0 < tw.n; p0 += 64 * U) {
+      int32_t r[U];
 #pragma unroll
-    for (int k = 0; k < kTPer; ++k) {
-      const int64_t i = threadIdx.x + k * 256;
-      if (i < n) bin[i] = alive[v[k]] ? v[k] : -1;
+      for (int u = 0; u < U; ++u) {
+        const int p = p0 + 64 * u + lane;
+        r[u] = p < tw.n ? ranks[tw.base + p] : 0;
+      }
+      unsigned long long S[U];
+      window_starts<U>(words, tw.srel, p0, S);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int q0 = p0 + 64 * u, p = q0 + lane;
+        const bool a = p < tw.n && A[r[u]] != 0;
+        const unsigned long long B = __ballot(a);
+        const unsigned long long sle = S[u] & le;
+        const int owner = cs + __popcll(sle) - 1;
+        const int rs = sle ? 63 - __clzll(sle) : 0;                // my row's first lane in this window
+        const int64_t dst = __shfl(nxt, owner & 63, 64);
+        if (a && dst >= 0) nranks[dst + __popcll(B & lane_range(rs, lane))] = r[u];
+        if (nxt >= 0) nxt += __popcll(B & lane_range(max(tw.srel - q0, 0), min(max(tw.erel - q0, 0), 64)));
+        cs += __popcll(S[u]);
+      }
     }
   }
   __syncthreads();
-  if (y < y1) {
-    if (staged) {
-      int64_t w = o;
-      for (int64_t i = s; i < e; ++i) { const int32_t r = bin[i - base]; if (r >= 0) bout[w++] = r; }
-    } else {
-      int64_t w = obase + o;
-      for (int64_t i = s; i < e; ++i) { const int32_t r = ranks[i]; if (alive[r]) nranks[w++] = r; }
-    }
-  }
-  __syncthreads();
-  if (staged)
-    for (int64_t i = threadIdx.x; i < n_out; i += blockDim.x) nranks[obase + i] = bout[i];
+  // 64 striped copies (summed by the caller): one shared copy would serialise
+  // ~10 bins x every block on a few L2 lines
+  if (hist && hs[threadIdx.x])
+    atomicAdd((unsigned long long*)&hist[(blockIdx.x & 63) * kTrimHist + threadIdx.x], (unsigned long long)hs[threadIdx.x]);
 }
 
 }  // namespace fa
@@ -661,17 +736,29 @@ FA_API int fa_hip_build_bitmaps(const int64_t* roff, const int32_t* ranks, const
   FA_LAUNCH_RET();
 }
 
-FA_API int fa_hip_trim_count(const int64_t* roff, const int32_t* ranks, int64_t T, const int8_t* alive,
-                             int32_t* cnt, hipStream_t st) {
+FA_API int fa_hip_trim_scan_count(const int64_t* roff, const int32_t* ranks, int64_t T, const int8_t* alive, int F1,
+                                  int min_len, const int32_t* wrow, int32_t* cnt, int32_t* bk_rows, int32_t* bk_nnz,
+                                  hipStream_t st) {
   if (T <= 0) return 0;
-  hipLaunchKernelGGL(k_trim_count, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, st, roff, ranks, T, alive, cnt);
+  const dim3 g((unsigned)((T + 255) / 256)), b(256);
+  if (F1 <= kTrimAliveLds)
+    hipLaunchKernelGGL(k_trim_scan_count<true>, g, b, F1, st, roff, ranks, T, alive, F1, min_len, wrow, cnt, bk_rows, bk_nnz);
+  else
+    hipLaunchKernelGGL(k_trim_scan_count<false>, g, b, 0, st, roff, ranks, T, alive, F1, min_len, wrow, cnt, bk_rows, bk_nnz);
   FA_LAUNCH_RET();
 }
 
-FA_API int fa_hip_trim_write(const int64_t* roff, const int32_t* ranks, const int8_t* alive, const int32_t* kept,
-                             int64_t K, const int64_t* nroff, int32_t* nranks, hipStream_t st) {
-  if (K <= 0) return 0;
-  hipLaunchKernelGGL(k_trim_write, dim3((unsigned)((K + 255) / 256)), dim3(256), 0, st, roff, ranks, alive, kept, K,
-                     nroff, nranks);
+// hist: int64 [64][256] striped row-length histogram (length clamped to 255) or nullptr.
+FA_API int fa_hip_trim_emit(const int64_t* roff, const int32_t* ranks, const int8_t* alive, int F1, int64_t T,
+                            const int32_t* cnt, const int64_t* base_rows, const int64_t* base_nnz, int64_t* nroff,
+                            int32_t* nranks, int32_t* kept, int64_t* hist, hipStream_t st) {
+  if (T <= 0) return 0;
+  const dim3 g((unsigned)((T + 255) / 256)), b(256);
+  if (F1 <= kTrimAliveLds)
+    hipLaunchKernelGGL(k_trim_emit<true>, g, b, F1, st, roff, ranks, alive, F1, T, cnt, base_rows, base_nnz, nroff,
+                       nranks, kept, hist);
+  else
+    hipLaunchKernelGGL(k_trim_emit<false>, g, b, 0, st, roff, ranks, alive, F1, T, cnt, base_rows, base_nnz, nroff,
+                       nranks, kept, hist);
   FA_LAUNCH_RET();
 }

@@ -140,8 +140,13 @@ class FastApriori:
                     levels.append(np.zeros((0, k), np.int32)); counts.append(np.zeros(0, np.int64))
                     self.log.line(f"{k} freq items 0")
                     break
-                self._trim(db, np.unique(np.concatenate([levels[-1][prefix_idx].ravel(), ext])), k)
-                cnt = self._count_level(db, levels[-1], prefix_idx, ext_off, ext)
+                with tm.phase(f"trim{k}"):
+                    self._trim(db, np.unique(np.concatenate([levels[-1][prefix_idx].ravel(), ext])), k)
+                with tm.phase("count"):
+                    cnt = self._count_level(db, levels[-1], prefix_idx, ext_off, ext)
+                if tm.sync:
+                    self.stats.setdefault("level_info", {})[k] = dict(
+                        ops.primitives.LAST_SLAB_PLAN, groups=int(prefix_idx.size))
                 keep = cnt >= mc
                 g_of_e = np.repeat(np.arange(prefix_idx.size), np.diff(ext_off))
                 rows = np.concatenate([levels[-1][prefix_idx[g_of_e[keep]]], ext[keep, None]], axis=1)
@@ -397,14 +402,14 @@ class FastApriori:
         dev = db["ranks"].device
         alive = torch.zeros(db["F1"], dtype=torch.int8)
         alive[torch.from_numpy(used.astype(np.int64))] = 1
-        kept, nroff, nranks, nw = ops.trim_rows(db["roff"], db["ranks"], alive.to(dev), k, db["wrow"])
+        kept, nroff, nranks, nw, hist = ops.trim_rows(db["roff"], db["ranks"], alive.to(dev), k, db["wrow"])
         K = kept.numel()
         if K > 0.9 * db["T"] and nranks.numel() > 0.9 * db["ranks"].numel():
             return   # not worth re-laying out
         db.update(roff=nroff, ranks=nranks, T=K, bm=None, W=0)
         db["alive"] = np.zeros_like(db["alive"])
         db["alive"][used] = True
-        db["len_hist"] = self._len_hist(db)
+        db["len_hist"] = hist.cpu().numpy()
         if db["wrow"] is not None:
             db["wrow"] = nw
             self._layout_weighted(db)

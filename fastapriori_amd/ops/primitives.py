@@ -351,24 +351,50 @@ def count_candidates(bm: torch.Tensor, W: int, prefix: torch.Tensor, ext_off: np
     return out
 
 
+TRIM_HIST_BINS = 256   # csrc/hip/prep.hip kTrimHist
+
+
 def trim_rows(roff, ranks, alive: torch.Tensor, min_len: int, wrow=None):
     """Keep rows with >= min_len alive items, dropping the dead items.
 
     alive: int8 [F1] on the rows' device.  Returns (kept row ids int32, new roff,
-    new ranks, new wrow) — ranks stay sorted within each row.
+    new ranks, new wrow, histogram of new row lengths int64 [256], lengths >= 255
+    in the last bin) — ranks stay sorted within each row.  Device path: count ->
+    scan of 256-row block sums -> emit (csrc/hip/prep.hip k_trim_scan_count /
+    k_trim_emit), one host sync for the output sizes.
     """
     T = roff.numel() - 1
     dev = ranks.device
-    cnt = torch.empty(max(T, 0), dtype=_I32, device=dev)
     if T == 0:
-        return (torch.zeros(0, dtype=_I32, device=dev), roff, ranks, wrow)
+        return (torch.zeros(0, dtype=_I32, device=dev), roff, ranks, wrow,
+                torch.zeros(TRIM_HIST_BINS, dtype=_I64, device=dev))
     if ranks.is_cuda:
-        _hip_call("fa_hip_trim_count", _p(roff), _p(ranks), T, _p(alive), _p(cnt), _stream(ranks))
-    else:
-        a = alive[ranks.to(_I64)].to(_I64)
-        cs = torch.zeros(ranks.numel() + 1, dtype=_I64)
-        torch.cumsum(a, 0, out=cs[1:])
-        cnt = (cs[roff[1:]] - cs[roff[:-1]]).to(_I32)
+        st = _stream(ranks)
+        nb = (T + 255) // 256
+        cnt = torch.empty(T, dtype=_I32, device=dev)
+        bk = torch.empty(2, nb, dtype=_I32, device=dev)
+        F1 = alive.numel()
+        _hip_call("fa_hip_trim_scan_count", _p(roff), _p(ranks), T, _p(alive), F1, int(min_len), _p(wrow), _p(cnt),
+                  _p(bk[0]), _p(bk[1]), st)
+        bases = torch.zeros(2, nb + 1, dtype=_I64, device=dev)
+        torch.cumsum(bk[0], 0, dtype=_I64, out=bases[0, 1:])    # two 1-D scans: the [2, nb] scan
+        torch.cumsum(bk[1], 0, dtype=_I64, out=bases[1, 1:])    # along dim 1 runs on 2 threads' worth
+        K, nnz = (int(v) for v in bases[:, -1].tolist())
+        nroff = torch.empty(K + 1, dtype=_I64, device=dev)
+        nroff[K:] = nnz
+        nranks = torch.empty(max(nnz, 1), dtype=_I32, device=dev)
+        kept = torch.empty(max(K, 1), dtype=_I32, device=dev)
+        hist = torch.zeros(64, TRIM_HIST_BINS, dtype=_I64, device=dev)
+        if K:
+            _hip_call("fa_hip_trim_emit", _p(roff), _p(ranks), _p(alive), F1, T, _p(cnt), _p(bases[0]), _p(bases[1]),
+                      _p(nroff), _p(nranks), _p(kept), _p(hist), st)
+        kept = kept[:K]
+        nw = wrow[kept.to(_I64)].contiguous() if wrow is not None else None
+        return kept, nroff, nranks[:nnz], nw, hist.sum(0)
+    a = alive[ranks.to(_I64)].to(_I64)
+    cs = torch.zeros(ranks.numel() + 1, dtype=_I64)
+    torch.cumsum(a, 0, out=cs[1:])
+    cnt = (cs[roff[1:]] - cs[roff[:-1]]).to(_I32)
     keep = cnt >= min_len
     if wrow is not None:
         keep &= wrow > 0
@@ -379,20 +405,19 @@ def trim_rows(roff, ranks, alive: torch.Tensor, min_len: int, wrow=None):
         torch.cumsum(cnt[kept.to(_I64)].to(_I64), 0, out=nroff[1:])
     nnz = int(nroff[-1].item())
     nranks = torch.empty(max(nnz, 1), dtype=_I32, device=dev)
-    if K and ranks.is_cuda:
-        _hip_call("fa_hip_trim_write", _p(roff), _p(ranks), _p(alive), _p(kept), K, _p(nroff), _p(nranks),
-                  _stream(ranks))
-    elif K:
+    if K:
         lens = roff[1:] - roff[:-1]
         rowmask = torch.zeros(T, dtype=torch.bool)
         rowmask[kept.to(_I64)] = True
         em = torch.repeat_interleave(rowmask, lens) & (alive[ranks.to(_I64)] > 0)
         nranks[:nnz] = ranks[em]
     nw = wrow[kept.to(_I64)].contiguous() if wrow is not None else None
-    return kept, nroff, nranks[:nnz], nw
+    hist = torch.bincount(cnt[kept.to(_I64)].to(_I64).clamp_(max=TRIM_HIST_BINS - 1),
+                          minlength=TRIM_HIST_BINS) if K else torch.zeros(TRIM_HIST_BINS, dtype=_I64)
+    return kept, nroff, nranks[:nnz], nw, hist
 
 
-_LDS_BYTES = 160 * 1024
+_LDS_BYTES = 160 * 1024 - 512   # minus the slab kernel's static scratch (build_words)
 
 
 def slab_plan(n_used: int, C: int):
@@ -403,6 +428,9 @@ def slab_plan(n_used: int, C: int):
         if cap >= min(C, 8192) or (sw == 4 and cap >= 1024):
             return sw, int(cap)
     return 0, 0
+
+
+LAST_SLAB_PLAN: dict = {}   # shape of the last count_level_slab call (diagnostics)
 
 
 def count_level_slab(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_off: np.ndarray,
@@ -464,6 +492,9 @@ def count_level_slab(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, 
                   out.data_ptr() + 4 * e0, sw, n_wg, _p(bm), bm.stride(0) if bm is not None else 0, st)
     res = out.to(_I64)
     del keep
+    LAST_SLAB_PLAN.clear()
+    LAST_SLAB_PLAN.update(rows=int(roff.numel() - 1), ncols=int(ncols), used=int(used.size), sw=sw, cap=cap,
+                          passes=int(starts.size - 1), pieces=int(gpre.shape[0]), m=m, C=C)
     return res
 
 

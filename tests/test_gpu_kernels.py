@@ -221,3 +221,20 @@ def test_wide_vocab_miner_matches_cpu():
     ref = FastApriori(0.02, config=MinerConfig(min_support=0.02, f1="histogram")).run(sh)
     got = FastApriori(0.02, config=cfg).run(sh.to(DEV))
     assert got.items == ref.items and got.as_dict() == ref.as_dict() and ref.n_itemsets > 100
+
+
+@pytest.mark.parametrize("weighted", [False, True])
+def test_trim_rows_matches_cpu(weighted):
+    off, items, lut, F1 = _prep(n=5000, V=300, max_len=40, seed=11, long_rows=20)
+    cnt, kept, roff = _compress_inputs(off, items, lut)
+    ranks = ops.compress(off, items, lut, kept, roff)
+    rng = np.random.default_rng(3)
+    alive = torch.from_numpy((rng.random(F1) < 0.6).astype(np.int8))
+    wrow = torch.from_numpy(rng.integers(0, 3, kept.numel()).astype(np.int32)) if weighted else None
+    ref = ops.trim_rows(roff, ranks, alive, 3, wrow)
+    got = ops.trim_rows(roff.to(DEV), ranks.to(DEV), alive.to(DEV), 3, wrow.to(DEV) if weighted else None)
+    for a, b in zip(ref, got):
+        if a is None:
+            assert b is None
+        else:
+            assert torch.equal(a, b.cpu())
