@@ -242,6 +242,124 @@ __global__ __launch_bounds__(256) void k_block_scatter(const int64_t* __restrict
   }
 }
 
+// Wave-cooperative versions (nb <= kWBMaxNB): a wave owns batch q (64 rows =
+// lanes) and streams the rows' contiguous ranks 64 at a time, coalesced.
+//   counts : row l's block-b count = sum over windows of popc(ballot(block == b)
+//            & the window lanes inside row l);
+//   scatter: row owners put (block base + rows-before prefix - row start -
+//            earlier-block items of the row) per block in an LDS table; a rank
+//            at position p of row r in block b goes to table[r][b] + p (ranks
+//            are sorted, so a row's block-b items are contiguous).
+// Rows are non-empty (compress keeps rows with >= 2 frequent items).
+constexpr int kWBMaxNB = 8;
+
+struct BatchSpan {
+  int64_t base;
+  int n, srel, erel;
+};
+
+__device__ __forceinline__ BatchSpan batch_span(const int64_t* __restrict__ roff, int64_t x0, int64_t T) {
+  const int lane = threadIdx.x & 63;
+  BatchSpan b;
+  b.base = roff[x0];
+  b.n = (int)(roff[min(x0 + 64, T)] - b.base);
+  b.srel = (int)(roff[min(x0 + lane, T)] - b.base);
+  b.erel = (int)(roff[min(x0 + lane + 1, T)] - b.base);
+  return b;
+}
+
+__device__ __forceinline__ unsigned long long lane_span(int lo, int hi) {   // bits [lo, hi) clamped to [0, 64]
+  lo = max(lo, 0); hi = min(hi, 64);
+  if (hi <= lo) return 0ull;
+  const unsigned long long h = hi >= 64 ? ~0ull : ((1ull << hi) - 1);
+  return h & ~((1ull << lo) - 1);
+}
+
+__global__ __launch_bounds__(256) void k_block_counts_w(const int64_t* __restrict__ roff,
+                                                        const int32_t* __restrict__ ranks, int64_t T, int nb,
+                                                        uint8_t* __restrict__ cnt, int64_t* __restrict__ bsum,
+                                                        int64_t nbatch, int lpb) {
+  const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= nbatch) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t x = q * 64 + lane;
+  const BatchSpan bs = batch_span(roff, q * 64, T);
+  int c[kWBMaxNB];
+#pragma unroll
+  for (int b = 0; b < kWBMaxNB; ++b) c[b] = 0;
+  constexpr int U = 4;
+  for (int p0 = 0; p0 < bs.n; p0 += 64 * U) {
+    int r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int p = p0 + 64 * u + lane;
+      r[u] = p < bs.n ? ranks[bs.base + p] >> lpb : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q0 = p0 + 64 * u;
+      const unsigned long long rm = lane_span(bs.srel - q0, bs.erel - q0);
+#pragma unroll
+      for (int b = 0; b < kWBMaxNB; ++b)
+        if (b < nb) c[b] += __popcll(__ballot(r[u] == b) & rm);
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < kWBMaxNB; ++b) {
+    if (b >= nb) break;
+    if (x < T) cnt[(int64_t)b * T + x] = (uint8_t)c[b];
+    const int tot = wave_last(wave_scan_incl_dpp(x < T ? c[b] : 0));
+    if (lane == 0) bsum[(int64_t)b * nbatch + q] = tot;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_block_scatter_w(const int64_t* __restrict__ roff,
+                                                         const int32_t* __restrict__ ranks, int64_t T, int nb,
+                                                         const uint8_t* __restrict__ cnt,
+                                                         const int64_t* __restrict__ base, int64_t nbatch,
+                                                         uint8_t* __restrict__ lr, int lpb) {
+  __shared__ int64_t offt[4][64 * kWBMaxNB];
+  __shared__ unsigned long long swords[4][4];
+  const int wv = threadIdx.x >> 6;
+  const int64_t q = (int64_t)blockIdx.x * 4 + wv;
+  if (q >= nbatch) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t x = q * 64 + lane;
+  const BatchSpan bs = batch_span(roff, q * 64, T);
+  int before = 0;
+#pragma unroll
+  for (int b = 0; b < kWBMaxNB; ++b) {
+    if (b >= nb) break;
+    const int c = x < T ? cnt[(int64_t)b * T + x] : 0;
+    const int pre = wave_scan_incl_dpp(c) - c;
+    offt[wv][lane * kWBMaxNB + b] = base[(int64_t)b * nbatch + q] + pre - bs.srel - before;
+    before += c;
+  }
+  const unsigned long long le = lanes_le_mask();
+  constexpr int U = 4;
+  for (int p0 = 0; p0 < bs.n; p0 += 64 * U) {
+    int r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int p = p0 + 64 * u + lane;
+      r[u] = p < bs.n ? ranks[bs.base + p] : -1;
+    }
+    const int cs0 = __popcll(__ballot(x < T && bs.srel < p0));
+    unsigned long long S[U];
+    window_starts<U>(swords[wv], x < T ? bs.srel : -(1 << 30), p0, S);   // (also orders the offt writes)
+    int cs = cs0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int row = cs + __popcll(S[u] & le) - 1;
+      cs += __popcll(S[u]);
+      if (r[u] >= 0) {
+        const int b = r[u] >> lpb;
+        lr[offt[wv][(row & 63) * kWBMaxNB + b] + p0 + 64 * u + lane] = (uint8_t)(r[u] - (b << lpb));
+      }
+    }
+  }
+}
+
 constexpr int kBSpan = 1024;   // staged bytes per block segment per wave batch
 
 __global__ __launch_bounds__(1024) void k_pair_blocked(
@@ -403,6 +521,119 @@ __global__ __launch_bounds__(1024) void k_pair_blocked16(
         atomicAdd(&tile[idx >> 1], (idx & 1) ? 0x10000u : 1u);
       }
       wave_lds_fence();
+    }
+    ci = ci_n; cj = cj_n;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kPB16 * kPB16 / 2; i += blockDim.x) {
+    const uint32_t v = tile[i];
+    if (!v) continue;
+    const int idx = 2 * i;
+    const int r = rb0 + idx / kPB16, c = cb0 + idx % kPB16;
+    if (r >= F1) continue;
+    if ((v & 0xFFFF) && c < F1) atomicAdd(&out[(int64_t)r * F1 + c], v & 0xFFFF);
+    if ((v >> 16) && c + 1 < F1) atomicAdd(&out[(int64_t)r * F1 + c + 1], v >> 16);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k = 2, unit-weight rows: one lane per (row, item-in-block-bi) position.
+//
+// Same blocked layout and 256x256 packed-u16 LDS tile as k_pair_blocked16, but
+// instead of flattening pairs (a 6-step dependent LDS binary search per pair),
+// a lane takes one position p of the batch's block-bi local ranks and loops
+// over its row's block-bj ranks.  The batch's local-rank bytes are staged in
+// per-wave LDS (coalesced loads); the row of position p comes from the
+// row-start mask of the window (window_starts over non-empty rows) and a
+// compaction table of the non-empty rows, so the dependency chain per pair is
+// one LDS byte read and one LDS atomic.
+// ---------------------------------------------------------------------------
+constexpr int kRowsStage = 512;     // staged local-rank bytes per wave and block
+
+__global__ __launch_bounds__(1024) void k_pair_rows16(
+    const uint8_t* __restrict__ cnt, const int64_t* __restrict__ base, const uint8_t* __restrict__ lr,
+    int64_t T, int64_t nbatch, int32_t F1, int nb, int nbp, int64_t chunk_b, uint32_t* __restrict__ out) {
+  __shared__ uint32_t tile[kPB16 * kPB16 / 2];
+  __shared__ uint8_t sa[kPW][kRowsStage];
+  __shared__ uint8_t sb[kPW][kRowsStage];
+  __shared__ uint8_t rowtab[kPW][64];
+  __shared__ unsigned long long swd[kPW][kRowsStage / 64];
+  const uint32_t logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int pid = logical % nbp;
+  const int64_t ch = logical / nbp;
+  int bi, bj;
+  tri_index(pid, nb, bi, bj);
+  const int rb0 = bi * kPB16, cb0 = bj * kPB16;
+  const bool diag = bi == bj;
+  for (int i = threadIdx.x; i < kPB16 * kPB16 / 2; i += blockDim.x) tile[i] = 0;
+  __syncthreads();
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const unsigned long long le = lanes_le_mask(), lt = le >> 1;
+  const int64_t q0 = ch * chunk_b, q1 = min(nbatch, q0 + chunk_b);
+  const uint8_t* ci_row = cnt + (int64_t)bi * T;
+  const uint8_t* cj_row = cnt + (int64_t)bj * T;
+  int ci = 0, cj = 0, ci_n = 0, cj_n = 0;
+  auto load = [&](int64_t q, int& a, int& b) {
+    const int64_t x = q * 64 + lane;
+    a = x < T ? ci_row[x] : 0;
+    b = diag ? a : (x < T ? cj_row[x] : 0);
+  };
+  int64_t q = q0 + wv;
+  if (q < q1) load(q, ci, cj);
+  for (; q < q1; q += kPW) {
+    if (q + kPW < q1) load(q + kPW, ci_n, cj_n);
+    const int inci = wave_scan_incl_dpp(ci);
+    const int SA = wave_last(inci);
+    const int incj = diag ? inci : wave_scan_incl_dpp(cj);
+    const int SB = diag ? SA : wave_last(incj);
+    // any pair at all in this batch? (diag: a row with >= 2 items; else a row with both)
+    const bool has = diag ? ci >= 2 : (ci > 0 && cj > 0);
+    if (__ballot(has) != 0ull) {
+      const uint8_t* gA = lr + base[(int64_t)bi * nbatch + q];
+      const uint8_t* gB = lr + base[(int64_t)bj * nbatch + q];
+      const bool stA = SA <= kRowsStage, stB = SB <= kRowsStage;
+      if (stA) for (int p = lane; p < SA; p += 64) sa[wv][p] = gA[p];
+      if (!diag && stB) for (int p = lane; p < SB; p += 64) sb[wv][p] = gB[p];
+      const unsigned long long M = __ballot(ci > 0);
+      if (ci > 0) rowtab[wv][__popcll(M & lt)] = (uint8_t)lane;
+      wave_lds_sync();
+      const uint8_t* A = stA ? sa[wv] : gA;
+      const uint8_t* B = diag ? A : (stB ? sb[wv] : gB);
+      const int jbeg = diag ? 0 : incj - cj;          // row owner view: my row's block-bj span
+      const int jend = diag ? inci : incj;
+      const int srow = ci > 0 ? inci - ci : -(1 << 30);
+      auto scatter = [&](int p0, unsigned long long Sw, int& cs) {
+        const int k = cs + __popcll(Sw & le) - 1;
+        cs += __popcll(Sw);
+        const int row = rowtab[wv][k & 63];
+        const int p = p0 + lane;
+        int j0 = __shfl(jbeg, row, 64);
+        const int j1 = __shfl(jend, row, 64);
+        if (diag) j0 = p + 1;
+        if (p < SA) {
+          const int i = (int)A[p] * kPB16;
+          for (int j = j0; j < j1; ++j) {
+            const int idx = i + (int)B[j];
+            atomicAdd(&tile[idx >> 1], (idx & 1) ? 0x10000u : 1u);
+          }
+        }
+      };
+      int cs = 0;                                      // non-empty rows started before the window
+      if (stA) {
+        // all (<= 8) windows' row-start masks in one LDS round trip
+        unsigned long long S[kRowsStage / 64];
+        window_starts<kRowsStage / 64>(swd[wv], srow, 0, S);
+#pragma unroll
+        for (int w = 0; w < kRowsStage / 64; ++w)
+          if (64 * w < SA) scatter(64 * w, S[w], cs);
+      } else {
+        for (int p0 = 0; p0 < SA; p0 += 64) {
+          unsigned long long S[1];
+          window_starts<1>(swd[wv], srow, p0, S);
+          scatter(p0, S[0], cs);
+        }
+      }
+      wave_lds_sync();
     }
     ci = ci_n; cj = cj_n;
   }
@@ -857,8 +1088,13 @@ FA_API int fa_hip_block_counts(const int64_t* roff, const int32_t* ranks, int64_
   if (T <= 0) return 0;
   const int nb = (F1 + pb - 1) / pb;
   const int64_t nbatch = (T + 63) / 64;
-  hipLaunchKernelGGL(k_block_counts, dim3((unsigned)((nbatch + 3) / 4)), dim3(256), 0, st, roff, ranks, T, nb, cnt,
-                     bsum, nbatch, pb);
+  const int lpb = __builtin_ctz((unsigned)pb);
+  if (nb <= kWBMaxNB && (1 << lpb) == pb)
+    hipLaunchKernelGGL(k_block_counts_w, dim3((unsigned)((nbatch + 3) / 4)), dim3(256), 0, st, roff, ranks, T, nb,
+                       cnt, bsum, nbatch, lpb);
+  else
+    hipLaunchKernelGGL(k_block_counts, dim3((unsigned)((nbatch + 3) / 4)), dim3(256), 0, st, roff, ranks, T, nb, cnt,
+                       bsum, nbatch, pb);
   FA_LAUNCH_RET();
 }
 
@@ -867,8 +1103,13 @@ FA_API int fa_hip_block_scatter(const int64_t* roff, const int32_t* ranks, int64
   if (T <= 0) return 0;
   const int nb = (F1 + pb - 1) / pb;
   const int64_t nbatch = (T + 63) / 64;
-  hipLaunchKernelGGL(k_block_scatter, dim3((unsigned)((nbatch + 3) / 4)), dim3(256), 0, st, roff, ranks, T, nb, cnt,
-                     base, nbatch, lr, pb);
+  const int lpb = __builtin_ctz((unsigned)pb);
+  if (nb <= kWBMaxNB && (1 << lpb) == pb)
+    hipLaunchKernelGGL(k_block_scatter_w, dim3((unsigned)((nbatch + 3) / 4)), dim3(256), 0, st, roff, ranks, T, nb,
+                       cnt, base, nbatch, lr, lpb);
+  else
+    hipLaunchKernelGGL(k_block_scatter, dim3((unsigned)((nbatch + 3) / 4)), dim3(256), 0, st, roff, ranks, T, nb, cnt,
+                       base, nbatch, lr, pb);
   FA_LAUNCH_RET();
 }
 
@@ -895,6 +1136,19 @@ FA_API int fa_hip_pair_blocked16(const uint8_t* cnt, const int64_t* base, const 
   const int64_t chunk_b = 65535 / 64;   // 1023 batches = 65472 rows
   const int64_t nch = (nbatch + chunk_b - 1) / chunk_b;
   hipLaunchKernelGGL(k_pair_blocked16, dim3((unsigned)(nch * nbp)), dim3(64 * kPW), 0, st, cnt, base, lr, T, nbatch,
+                     F1, nb, nbp, chunk_b, out);
+  FA_LAUNCH_RET();
+}
+
+FA_API int fa_hip_pair_rows16(const uint8_t* cnt, const int64_t* base, const uint8_t* lr, int64_t T, int32_t F1,
+                              uint32_t* out, hipStream_t st) {
+  if (T <= 0 || F1 < 2) return 0;
+  const int nb = (F1 + kPB16 - 1) / kPB16;
+  const int nbp = nb * (nb + 1) / 2;
+  const int64_t nbatch = (T + 63) / 64;
+  const int64_t chunk_b = 65535 / 64;   // 1023 batches = 65472 rows: 16-bit counters stay exact
+  const int64_t nch = (nbatch + chunk_b - 1) / chunk_b;
+  hipLaunchKernelGGL(k_pair_rows16, dim3((unsigned)(nch * nbp)), dim3(64 * kPW), 0, st, cnt, base, lr, T, nbatch,
                      F1, nb, nbp, chunk_b, out);
   FA_LAUNCH_RET();
 }

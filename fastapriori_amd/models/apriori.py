@@ -288,13 +288,17 @@ class FastApriori:
         ranks = ops.compress(shard.offsets, shard.items, lut, kept, roff, F1)
         db = {"roff": roff, "ranks": ranks, "T": T, "src": None, "ncols": T, "wword": None, "wrow": None,
               "bm": None, "W": 0, "F1": F1, "alive": np.ones(F1, dtype=bool), "c1": self._counts1}
-        pair_work = 0
-        if T:
-            lens = roff[1:] - roff[:-1]
-            pair_work = int((lens * (lens - 1) // 2).sum().item())
-        db["pair_work"] = pair_work
+        # row-length histogram (lengths >= 255 share the last bin): drives the pair
+        # cost model, the trimming model and the u8 per-block count guard
+        hist = ops.histogram(torch.clamp(cnt, max=255), 256).cpu().numpy() if cnt.numel() else np.zeros(256, np.int64)
+        hist[:2] = 0                         # rows with < 2 frequent items are not kept
+        L = np.arange(256, dtype=np.int64)
+        db["pair_work"] = int((hist * (L * (L - 1) // 2)).sum())
+        db["len_hist"] = hist
+        db["long_rows"] = bool(self.comm.allreduce_int(int(hist[255] > 0), "max"))
         if self._want_dedup(db):
             self._dedup(db)
+            db.pop("len_hist", None)
         db["T_global"] = self.comm.allreduce_int(T)
         db["ncols_global"] = self.comm.allreduce_int(db["ncols"] if db["src"] is None else db["n_distinct"])
         self.log.metric(phase="compress", T=T, distinct=db.get("n_distinct", T), nnz=int(ranks.numel()))
@@ -444,7 +448,7 @@ class FastApriori:
             self._bitmaps(db)
             pc = ops.pair_counts_gram(db["bm"], db["W"], db["wword"])
         else:
-            pc = ops.pair_counts_horizontal(db["roff"], db["ranks"], db["wrow"], F1)
+            pc = ops.pair_counts_horizontal(db["roff"], db["ranks"], db["wrow"], F1, db.get("long_rows", True))
         iu = torch.triu_indices(F1, F1, 1, device=pc.device)
         flat = pc[iu[0], iu[1]].contiguous()
         self.comm.all_reduce_(flat)

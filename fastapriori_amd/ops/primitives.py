@@ -239,14 +239,21 @@ def build_bitmaps(roff, ranks, src, ncols: int, F1: int, item_map=None, used=Non
     return bm[:F1], W
 
 
-def pair_counts_horizontal(roff, ranks, wrow, F1: int) -> torch.Tensor:
+def pair_counts_horizontal(roff, ranks, wrow, F1: int, long_rows: bool = True) -> torch.Tensor:
+    """Pair supports from the compressed rows -> int64 [F1, F1] (upper triangle).
+
+    Device path: per-row block counts + local-rank bytes (blocked layout), then
+    the 256 x 256 packed-u16 tile kernel for unit-weight rows, or 128 x 128 u32
+    tiles with row weights.  long_rows: some row may hold >= 256 items, which
+    would overflow a u8 count of a 256-item block -> 128-item blocks.
+    """
     T = roff.numel() - 1
     dev = ranks.device
     if ranks.is_cuda and os.environ.get("FA_PAIR_KERNEL", "blocked") == "blocked":
         out = torch.zeros((F1, F1), dtype=_I32, device=dev)
         if T > 0 and F1 >= 2:
             st = _stream(ranks)
-            pb = 128 if wrow is not None else 256       # u16 tiles need unit weights
+            pb = 128 if (wrow is not None or long_rows) else 256       # u16 tiles need unit weights
             nb = (F1 + pb - 1) // pb
             nbatch = (T + 63) // 64
             cnt = torch.empty(nb * T, dtype=torch.uint8, device=dev)
@@ -257,8 +264,9 @@ def pair_counts_horizontal(roff, ranks, wrow, F1: int) -> torch.Tensor:
             base -= bsum
             lr = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
             _hip_call("fa_hip_block_scatter", _p(roff), _p(ranks), T, F1, _p(cnt), _p(base), _p(lr), pb, st)
-            if wrow is None:
-                _hip_call("fa_hip_pair_blocked16", _p(cnt), _p(base), _p(lr), T, F1, _p(out), st)
+            if pb == 256:
+                k16 = "fa_hip_pair_blocked16" if os.environ.get("FA_PAIR_ROWS", "1") == "0" else "fa_hip_pair_rows16"
+                _hip_call(k16, _p(cnt), _p(base), _p(lr), T, F1, _p(out), st)
             else:
                 _hip_call("fa_hip_pair_blocked", _p(cnt), _p(base), _p(lr), T, _p(wrow), F1, _p(out),
                           PAIR_CHUNK_ROWS, st)

@@ -114,7 +114,7 @@ def test_bitmaps_pairs_candidates(F1_frac):
     assert torch.equal(bm[:, :W], gbm[:, :W].cpu())
     # horizontal vs gram vs host
     ph = ops.pair_counts_horizontal(roff, ranks, None, F1)
-    gph = ops.pair_counts_horizontal(roff.to(DEV), ranks.to(DEV), None, F1).cpu()
+    gph = ops.pair_counts_horizontal(roff.to(DEV), ranks.to(DEV), None, F1, long_rows=False).cpu()
     gpg = ops.pair_counts_gram(gbm, gW, None).cpu()
     assert torch.equal(ph, gph)
     assert torch.equal(torch.triu(ph, 1), torch.triu(gpg, 1))
@@ -187,14 +187,16 @@ def test_slab_multipass_from_bitmap(monkeypatch):
     assert ref.as_dict() == got_w.as_dict()
 
 
-@pytest.mark.parametrize("kernel", ["blocked", "tile"])
-def test_pair_kernels_agree(monkeypatch, kernel):
+@pytest.mark.parametrize("kernel,rows16", [("blocked", "1"), ("blocked", "0"), ("tile", "1")])
+@pytest.mark.parametrize("long_rows", [False, True])
+def test_pair_kernels_agree(monkeypatch, kernel, rows16, long_rows):
     monkeypatch.setenv("FA_PAIR_KERNEL", kernel)
+    monkeypatch.setenv("FA_PAIR_ROWS", rows16)
     off, items, lut, F1 = _prep(n=20000, V=900, seed=21, long_rows=30, F1_frac=0.9)
     _, kept, roff = _compress_inputs(off, items, lut)
     ranks = ops.compress(off, items, lut, kept, roff)
     ref = ops.pair_counts_horizontal(roff, ranks, None, F1)
-    got = ops.pair_counts_horizontal(roff.to(DEV), ranks.to(DEV), None, F1).cpu()
+    got = ops.pair_counts_horizontal(roff.to(DEV), ranks.to(DEV), None, F1, long_rows).cpu()
     assert torch.equal(ref, got)
     w = torch.randint(0, 4, (kept.numel(),), dtype=torch.int32)
     refw = ops.pair_counts_horizontal(roff, ranks, w, F1)
