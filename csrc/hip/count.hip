@@ -548,18 +548,23 @@ __global__ __launch_bounds__(1024) void k_pair_blocked16(
 // compaction table of the non-empty rows, so the dependency chain per pair is
 // one LDS byte read and one LDS atomic.
 // ---------------------------------------------------------------------------
-constexpr int kRowsStage = 512;     // staged local-rank bytes per wave and block
+constexpr int kRowsDw = 3;                  // staged dwords per lane and block
+constexpr int kRowsStage = 64 * kRowsDw * 4; // 768 staged local-rank bytes per wave and block
+constexpr int kRowsWin = kRowsStage / 64;    // 12 windows
 
 __global__ __launch_bounds__(1024) void k_pair_rows16(
     const uint8_t* __restrict__ cnt, const int64_t* __restrict__ base, const uint8_t* __restrict__ lr,
     int64_t T, int64_t nbatch, int32_t F1, int nb, int nbp, int64_t chunk_b, uint32_t* __restrict__ out) {
   __shared__ uint32_t tile[kPB16 * kPB16 / 2];
-  __shared__ uint8_t sa[kPW][kRowsStage];
-  __shared__ uint8_t sb[kPW][kRowsStage];
+  __shared__ uint32_t sa[kPW][kRowsStage / 4];
+  __shared__ uint32_t sb[kPW][kRowsStage / 4];
   __shared__ uint8_t rowtab[kPW][64];
-  __shared__ unsigned long long swd[kPW][kRowsStage / 64];
+  __shared__ unsigned long long swd[kPW][kRowsWin];
   const uint32_t logical = xcd_remap(blockIdx.x, gridDim.x);
   const int pid = logical % nbp;
+  // one chunk of <= 65472 rows per workgroup keeps the 16-bit counters exact.
+  // (Folding many chunks into u32 register accumulators instead, to cut the
+  // flush atomics, measured slower: 64 more VGPRs spill at 16 waves/CU.)
   const int64_t ch = logical / nbp;
   int bi, bj;
   tri_index(pid, nb, bi, bj);
@@ -572,33 +577,54 @@ __global__ __launch_bounds__(1024) void k_pair_rows16(
   const int64_t q0 = ch * chunk_b, q1 = min(nbatch, q0 + chunk_b);
   const uint8_t* ci_row = cnt + (int64_t)bi * T;
   const uint8_t* cj_row = cnt + (int64_t)bj * T;
-  int ci = 0, cj = 0, ci_n = 0, cj_n = 0;
-  auto load = [&](int64_t q, int& a, int& b) {
-    const int64_t x = q * 64 + lane;
-    a = x < T ? ci_row[x] : 0;
-    b = diag ? a : (x < T ? cj_row[x] : 0);
+  const int64_t* base_i = base + (int64_t)bi * nbatch;
+  const int64_t* base_j = base + (int64_t)bj * nbatch;
+  // Software pipeline over this wave's batches q, q + kPW, ...: block bases two
+  // batches ahead, counts and the aligned local-rank dwords one batch ahead.
+  auto ld_counts = [&](int64_t qq, int& a, int& b) {
+    const int64_t x = qq * 64 + lane;
+    a = (qq < q1 && x < T) ? ci_row[x] : 0;
+    b = diag ? a : ((qq < q1 && x < T) ? cj_row[x] : 0);
+  };
+  auto ld_bytes = [&](int64_t off, uint32_t (&d)[kRowsDw]) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(lr + (off & ~(int64_t)3));
+#pragma unroll
+    for (int k = 0; k < kRowsDw; ++k) d[k] = p[lane + 64 * k];    // lr is padded by >= 1 KiB
   };
   int64_t q = q0 + wv;
-  if (q < q1) load(q, ci, cj);
+  int ci, cj, ci_n, cj_n;
+  ld_counts(q, ci, cj);
+  ld_counts(q + kPW, ci_n, cj_n);
+  int64_t oa = q < q1 ? base_i[q] : 0, ob = q < q1 ? base_j[q] : 0;
+  int64_t oa_n = q + kPW < q1 ? base_i[q + kPW] : 0, ob_n = q + kPW < q1 ? base_j[q + kPW] : 0;
+  uint32_t da[kRowsDw], db[kRowsDw], da_n[kRowsDw], db_n[kRowsDw];
+  if (q < q1) { ld_bytes(oa, da); if (!diag) ld_bytes(ob, db); }
   for (; q < q1; q += kPW) {
-    if (q + kPW < q1) load(q + kPW, ci_n, cj_n);
+    // issue the next batches' loads first
+    int ci_nn, cj_nn;
+    ld_counts(q + 2 * kPW, ci_nn, cj_nn);
+    const int64_t oa_nn = q + 2 * kPW < q1 ? base_i[q + 2 * kPW] : 0;
+    const int64_t ob_nn = q + 2 * kPW < q1 ? base_j[q + 2 * kPW] : 0;
+    if (q + kPW < q1) { ld_bytes(oa_n, da_n); if (!diag) ld_bytes(ob_n, db_n); }
+
     const int inci = wave_scan_incl_dpp(ci);
     const int SA = wave_last(inci);
     const int incj = diag ? inci : wave_scan_incl_dpp(cj);
     const int SB = diag ? SA : wave_last(incj);
-    // any pair at all in this batch? (diag: a row with >= 2 items; else a row with both)
     const bool has = diag ? ci >= 2 : (ci > 0 && cj > 0);
     if (__ballot(has) != 0ull) {
-      const uint8_t* gA = lr + base[(int64_t)bi * nbatch + q];
-      const uint8_t* gB = lr + base[(int64_t)bj * nbatch + q];
-      const bool stA = SA <= kRowsStage, stB = SB <= kRowsStage;
-      if (stA) for (int p = lane; p < SA; p += 64) sa[wv][p] = gA[p];
-      if (!diag && stB) for (int p = lane; p < SB; p += 64) sb[wv][p] = gB[p];
+      const int sha = (int)(oa & 3), shb = (int)(ob & 3);
+      const bool stA = SA + sha <= kRowsStage, stB = diag || SB + shb <= kRowsStage;
+#pragma unroll
+      for (int k = 0; k < kRowsDw; ++k) {
+        sa[wv][lane + 64 * k] = da[k];
+        if (!diag) sb[wv][lane + 64 * k] = db[k];
+      }
       const unsigned long long M = __ballot(ci > 0);
       if (ci > 0) rowtab[wv][__popcll(M & lt)] = (uint8_t)lane;
       wave_lds_sync();
-      const uint8_t* A = stA ? sa[wv] : gA;
-      const uint8_t* B = diag ? A : (stB ? sb[wv] : gB);
+      const uint8_t* A = stA ? reinterpret_cast<const uint8_t*>(sa[wv]) + sha : lr + oa;
+      const uint8_t* B = diag ? A : (stB ? reinterpret_cast<const uint8_t*>(sb[wv]) + shb : lr + ob);
       const int jbeg = diag ? 0 : incj - cj;          // row owner view: my row's block-bj span
       const int jend = diag ? inci : incj;
       const int srow = ci > 0 ? inci - ci : -(1 << 30);
@@ -619,13 +645,17 @@ __global__ __launch_bounds__(1024) void k_pair_rows16(
         }
       };
       int cs = 0;                                      // non-empty rows started before the window
-      if (stA) {
-        // all (<= 8) windows' row-start masks in one LDS round trip
-        unsigned long long S[kRowsStage / 64];
-        window_starts<kRowsStage / 64>(swd[wv], srow, 0, S);
+      if (SA <= kRowsStage) {
+        // row-start masks, 4 windows per LDS round trip
 #pragma unroll
-        for (int w = 0; w < kRowsStage / 64; ++w)
-          if (64 * w < SA) scatter(64 * w, S[w], cs);
+        for (int w0 = 0; w0 < kRowsWin; w0 += 4) {
+          if (64 * w0 >= SA) break;
+          unsigned long long S[4];
+          window_starts<4>(swd[wv], srow, 64 * w0, S);
+#pragma unroll
+          for (int w = 0; w < 4; ++w)
+            if (64 * (w0 + w) < SA) scatter(64 * (w0 + w), S[w], cs);
+        }
       } else {
         for (int p0 = 0; p0 < SA; p0 += 64) {
           unsigned long long S[1];
@@ -635,7 +665,10 @@ __global__ __launch_bounds__(1024) void k_pair_rows16(
       }
       wave_lds_sync();
     }
-    ci = ci_n; cj = cj_n;
+    ci = ci_n; cj = cj_n; ci_n = ci_nn; cj_n = cj_nn;
+    oa = oa_n; ob = ob_n; oa_n = oa_nn; ob_n = ob_nn;
+#pragma unroll
+    for (int k = 0; k < kRowsDw; ++k) { da[k] = da_n[k]; db[k] = db_n[k]; }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < kPB16 * kPB16 / 2; i += blockDim.x) {

@@ -262,7 +262,7 @@ def pair_counts_horizontal(roff, ranks, wrow, F1: int, long_rows: bool = True) -
             base = torch.cumsum(bsum, 0)
             total = int(base[-1].item())
             base -= bsum
-            lr = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
+            lr = torch.empty(total + 1024, dtype=torch.uint8, device=dev)   # pad: aligned dword staging reads
             _hip_call("fa_hip_block_scatter", _p(roff), _p(ranks), T, F1, _p(cnt), _p(base), _p(lr), pb, st)
             if pb == 256:
                 k16 = "fa_hip_pair_blocked16" if os.environ.get("FA_PAIR_ROWS", "1") == "0" else "fa_hip_pair_rows16"
