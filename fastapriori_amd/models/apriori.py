@@ -59,6 +59,7 @@ class MinerConfig:
     level_kernel: str = "auto"      # auto | slab | bitmap  (k >= 3 counting kernel)
     trim: bool = True               # transaction trimming before every level k >= 3
     f1: str = "auto"                # auto | sketch | histogram  (frequent-item counting)
+    trim_min_rows: int = 1 << 20    # no trimming below this many rows (fixed cost > gain)
 
 
 class FastApriori:
@@ -378,6 +379,8 @@ class FastApriori:
         length L keeps >= k of them with probability P[Binom(L, p) >= k].  Trimming
         costs two passes over the rows, so it runs only when it removes a lot.
         """
+        if db["T"] < self.cfg.trim_min_rows:   # a trim's fixed cost (2 launches + a host sync) dominates
+            return False
         from scipy.stats import binom
         c1 = db["c1"]
         alive = db["alive"]

@@ -23,7 +23,7 @@ def _mine_file(path_prefix: str, ms: float, dedup: str, strategy: str):
     comm = init_comm("cpu")
     try:
         shard = read_shard(path_prefix + "D.dat", comm)
-        cfg = MinerConfig(min_support=ms, dedup=dedup, pair_strategy=strategy)
+        cfg = MinerConfig(trim_min_rows=0, min_support=ms, dedup=dedup, pair_strategy=strategy)
         res = FastApriori(ms, comm, cfg, Logger(comm.rank, enabled=False)).run(shard)
         users = read_shard(path_prefix + "U.dat", comm)
         recs = AssociationRules(res, comm, Logger(comm.rank, enabled=False)).run(users)
@@ -57,7 +57,7 @@ def _mine_generated(n: int, ms: float):
     comm = init_comm("cpu")
     try:
         shard = generate_shard(n, comm, "cpu", 8.0, 3.0, 100, 80, seed=5)
-        res = FastApriori(ms, comm, MinerConfig(min_support=ms), Logger(comm.rank, enabled=False)).run(shard)
+        res = FastApriori(ms, comm, MinerConfig(trim_min_rows=0, min_support=ms), Logger(comm.rank, enabled=False)).run(shard)
         return res.as_dict(), res.items
     finally:
         shutdown_comm(comm)

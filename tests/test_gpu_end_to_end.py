@@ -40,7 +40,7 @@ def _gpu_rank(n, ms):
     comm = init_comm("cuda")
     try:
         sh = generate_shard(n, comm, comm.device, 10.0, 4.0, 200, 200, seed=3)
-        res = FastApriori(ms, comm, MinerConfig(min_support=ms), Logger(comm.rank, enabled=False)).run(sh)
+        res = FastApriori(ms, comm, MinerConfig(trim_min_rows=0, min_support=ms), Logger(comm.rank, enabled=False)).run(sh)
         return res.as_dict()
     finally:
         shutdown_comm(comm)

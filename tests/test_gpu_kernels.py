@@ -141,8 +141,8 @@ def test_slab_many_passes_and_levels():
     # a deep-level database: many candidates force several accumulator passes
     sh = generate_shard(60000, Comm(), "cpu", 14.0, 6.0, 300, 120, seed=11)
     cfg = dict(min_support=0.004, dedup="off")
-    ref = FastApriori(0.004, config=MinerConfig(level_kernel="bitmap", **cfg)).run(sh)
-    got = FastApriori(0.004, config=MinerConfig(level_kernel="slab", **cfg)).run(sh.to(DEV))
+    ref = FastApriori(0.004, config=MinerConfig(trim_min_rows=0, level_kernel="bitmap", **cfg)).run(sh)
+    got = FastApriori(0.004, config=MinerConfig(trim_min_rows=0, level_kernel="slab", **cfg)).run(sh.to(DEV))
     assert len(ref.levels) >= 4
     assert ref.as_dict() == got.as_dict()
 
@@ -179,11 +179,11 @@ def test_slab_multipass_from_bitmap(monkeypatch):
     import fastapriori_amd.ops.primitives as prim
     sh = generate_shard(30000, Comm(), "cpu", 12.0, 5.0, 200, 100, seed=13)
     cfg = dict(min_support=0.005, dedup="off")
-    ref = FastApriori(0.005, config=MinerConfig(level_kernel="bitmap", **cfg)).run(sh)
+    ref = FastApriori(0.005, config=MinerConfig(trim_min_rows=0, level_kernel="bitmap", **cfg)).run(sh)
     monkeypatch.setattr(prim, "_LDS_BYTES", 24 * 1024)
-    got = FastApriori(0.005, config=MinerConfig(level_kernel="slab", **cfg)).run(sh.to(DEV))
+    got = FastApriori(0.005, config=MinerConfig(trim_min_rows=0, level_kernel="slab", **cfg)).run(sh.to(DEV))
     assert ref.as_dict() == got.as_dict()
-    got_w = FastApriori(0.005, config=MinerConfig(level_kernel="slab", min_support=0.005, dedup="on")).run(sh.to(DEV))
+    got_w = FastApriori(0.005, config=MinerConfig(trim_min_rows=0, level_kernel="slab", min_support=0.005, dedup="on")).run(sh.to(DEV))
     assert ref.as_dict() == got_w.as_dict()
 
 

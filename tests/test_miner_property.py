@@ -38,7 +38,7 @@ def test_miner_matches_oracle(rows, ms, strategy, dedup, trim):
     text = _db_text(rows)
     lines = text.splitlines()
     exp = oracle_mine([java_split_ws(l) for l in lines], ms)
-    res = FastApriori(ms, config=MinerConfig(min_support=ms, pair_strategy=strategy, dedup=dedup, trim=trim),
+    res = FastApriori(ms, config=MinerConfig(min_support=ms, pair_strategy=strategy, dedup=dedup, trim=trim, trim_min_rows=0),
                       logger=Logger(enabled=False)).run(parse_bytes(text.encode()))
     assert res.min_count == exp.min_count
     assert res.items == exp.items                      # same rank order (count desc, Java string asc)
@@ -55,7 +55,7 @@ def test_deep_levels_long_rows():
     text = _db_text(rows)
     exp = oracle_mine([java_split_ws(l) for l in text.splitlines()], 0.05)
     for strat in ("horizontal", "gram"):
-        res = FastApriori(0.05, config=MinerConfig(min_support=0.05, pair_strategy=strat),
+        res = FastApriori(0.05, config=MinerConfig(trim_min_rows=0, min_support=0.05, pair_strategy=strat),
                           logger=Logger(enabled=False)).run(parse_bytes(text.encode()))
         assert token_sets(res.items, res.as_dict()) == token_sets(exp.items, exp.itemsets)
         assert len(res.levels) >= 5
