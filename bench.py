@@ -52,11 +52,13 @@ def main() -> int:
     ap.add_argument("--dedup", default="auto")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--strategy", choices=["count", "candidate"], default="count",
+                    help="count: each rank generates its row shard; candidate: every rank holds all rows")
     args = ap.parse_args()
 
     import torch
     from fastapriori_amd.models.apriori import FastApriori, MinerConfig
-    from fastapriori_amd.parallel.comm import init_comm, shutdown_comm
+    from fastapriori_amd.parallel.comm import Comm, init_comm, shutdown_comm
     from fastapriori_amd.utils.io import generate_shard, generate_zipf_shard
     from fastapriori_amd.utils.metrics import Logger
 
@@ -68,16 +70,18 @@ def main() -> int:
     world = comm.world_size
 
     t_gen = time.perf_counter()
+    data_comm = comm if args.strategy == "count" else Comm(device=comm.device)
     if args.config.startswith("webdocs"):
-        shard = generate_zipf_shard(n_txn, comm, comm.device, mean_len=avg_len, n_items=n_items,
+        shard = generate_zipf_shard(n_txn, data_comm, comm.device, mean_len=avg_len, n_items=n_items,
                                     n_topics=n_pat, seed=args.seed)
     else:
-        shard = generate_shard(n_txn, comm, comm.device, avg_len, avg_pat, n_pat, n_items, args.seed)
+        shard = generate_shard(n_txn, data_comm, comm.device, avg_len, avg_pat, n_pat, n_items, args.seed)
     if comm.device.type == "cuda":
         torch.cuda.synchronize()
     t_gen = time.perf_counter() - t_gen
 
-    cfg = MinerConfig(min_support=min_sup, dedup=args.dedup, pair_strategy=args.pair_strategy)
+    cfg = MinerConfig(min_support=min_sup, dedup=args.dedup, pair_strategy=args.pair_strategy,
+                      parallelism=args.strategy)
     quiet = Logger(comm.rank, enabled=False)
 
     def sync():
@@ -114,7 +118,8 @@ def main() -> int:
             "data": (f"synthetic {'Zipf-topic' if args.config.startswith('webdocs') else 'Quest'} {args.config} "
                      f"(n={n_txn}, seed={args.seed}), generated in-process"),
             "config": {"model": args.config, "global_batch": n_txn, "seq_len": avg_len,
-                       "parallelism": f"dp{world}", "min_support": min_sup,
+                       "parallelism": f"{'dp' if args.strategy == 'count' else 'cp'}{world}",
+                       "min_support": min_sup,
                        "n_itemsets": n_sets, "levels": [len(c) for c in res.counts],
                        "pair_strategy": miner.stats.get("pair_strategy"),
                        "min_count": res.min_count, "gen_s": round(t_gen, 2),

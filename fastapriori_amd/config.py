@@ -38,6 +38,7 @@ class JobConfig:
     profile: bool = False
     metrics_path: str | None = None
     max_level: int = 0
+    strategy: str = "count"                     # count | candidate distribution
     extra: dict = field(default_factory=dict)
 
 
@@ -61,6 +62,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--profile", action="store_true", default=_env("FA_PROFILE", False))
     p.add_argument("--metrics", dest="metrics_path", default=os.environ.get("FA_METRICS"))
     p.add_argument("--max-level", type=int, default=_env("FA_MAX_LEVEL", 0))
+    p.add_argument("--strategy", choices=["count", "candidate"], default=_env("FA_STRATEGY", "count"),
+                   help="count: shard transactions, all-reduce counts; candidate: replicate the DB on every "
+                        "rank and split pairs by rows, level candidates by rank")
     return p
 
 
@@ -69,4 +73,5 @@ def parse_args(argv=None) -> JobConfig:
     return JobConfig(input=a.input, output=a.output, temp=a.temp, min_support=a.min_support, device=a.device,
                      dedup=a.dedup, pair_strategy=a.pair_strategy, with_counts=a.with_counts, resume=a.resume,
                      rules_only=a.rules_only, checkpoint=a.checkpoint, overwrite=a.overwrite,
-                     profile=a.profile, metrics_path=a.metrics_path, max_level=a.max_level)
+                     profile=a.profile, metrics_path=a.metrics_path, max_level=a.max_level,
+                     strategy=a.strategy)

@@ -60,6 +60,9 @@ class MinerConfig:
     trim: bool = True               # transaction trimming before every level k >= 3
     f1: str = "auto"                # auto | sketch | histogram  (frequent-item counting)
     trim_min_rows: int = 1 << 20    # no trimming below this many rows (fixed cost > gain)
+    parallelism: str = "count"      # count: rows sharded, counts all-reduced (default)
+                                    # candidate: every rank holds the whole DB; pairs split by rows,
+                                    #   level candidates split by rank (FastApriori.scala:98-100,140)
 
 
 class FastApriori:
@@ -82,7 +85,12 @@ class FastApriori:
     # ------------------------------------------------------------------
     def run(self, shard: TransactionShard, resume: MiningResult | None = None) -> MiningResult:
         t_start = time.perf_counter()
-        comm, dev = self.comm, shard.items.device
+        dev = shard.items.device
+        # candidate parallelism: the data is replicated, so data-side collectives
+        # (line count, F1, layout decisions) are local; only count vectors move
+        self.cand_par = self.cfg.parallelism == "candidate" and self.comm.distributed
+        self.dcomm = Comm(device=self.comm.device) if self.cand_par else self.comm
+        comm = self.dcomm
         n_global = comm.allreduce_int(shard.n_lines)
         mc = min_count(self.cfg.min_support, n_global)
         self.stats = {"n_lines": n_global, "min_count": mc}
@@ -184,7 +192,7 @@ class FastApriori:
     # F1: histogram, all-reduce, ranking (FastApriori.scala:46-62)
     # ------------------------------------------------------------------
     def _frequent_items(self, shard: TransactionShard, mc: int):
-        comm, vocab, dev = self.comm, shard.vocab, shard.items.device
+        comm, vocab, dev = self.dcomm, shard.vocab, shard.items.device
         thr = max(mc, 1)   # only tokens that occur can be frequent (even at minSupport 0)
         if vocab.numeric:
             V = comm.allreduce_int(vocab.size, "max")
@@ -259,7 +267,7 @@ class FastApriori:
         (instead of V int64).  Returns None (-> plain histogram) when the sketch
         is too crowded to leave at most ops.F1_MAX_CANDIDATES candidates; the
         decision is identical on every rank since the reduced sketch is."""
-        comm, dev = self.comm, shard.items.device
+        comm, dev = self.dcomm, shard.items.device
         sk = ops.f1_sketch(shard.items)
         ex = torch.from_numpy(shard.extras.astype(np.int64)) if shard.extras.size else None
         if ex is not None:
@@ -296,12 +304,12 @@ class FastApriori:
         L = np.arange(256, dtype=np.int64)
         db["pair_work"] = int((hist * (L * (L - 1) // 2)).sum())
         db["len_hist"] = hist
-        db["long_rows"] = bool(self.comm.allreduce_int(int(hist[255] > 0), "max"))
+        db["long_rows"] = bool(self.dcomm.allreduce_int(int(hist[255] > 0), "max"))
         if self._want_dedup(db):
             self._dedup(db)
             db.pop("len_hist", None)
-        db["T_global"] = self.comm.allreduce_int(T)
-        db["ncols_global"] = self.comm.allreduce_int(db["ncols"] if db["src"] is None else db["n_distinct"])
+        db["T_global"] = self.dcomm.allreduce_int(T)
+        db["ncols_global"] = self.dcomm.allreduce_int(db["ncols"] if db["src"] is None else db["n_distinct"])
         self.log.metric(phase="compress", T=T, distinct=db.get("n_distinct", T), nnz=int(ranks.numel()))
         return db
 
@@ -319,7 +327,7 @@ class FastApriori:
             frac = torch.unique(h1).numel() / max(n, 1)
             decision = frac < self.cfg.dedup_threshold
         # every rank must take the same decision (the layout differs)
-        return bool(self.comm.allreduce_int(int(decision), "max"))
+        return bool(self.dcomm.allreduce_int(int(decision), "max"))
 
     def _dedup(self, db) -> None:
         """Merge identical compressed rows into weight classes (FastApriori.scala:71-79).
@@ -442,16 +450,28 @@ class FastApriori:
         t_g = (F1 * (F1 - 1) / 2) * W / GRAM_WORDPAIRS_PER_S
         # ranks must agree: decide on the global work
         pick_gram = t_g < t_h
-        return "gram" if self.comm.allreduce_int(int(pick_gram), "max") else "horizontal"
+        return "gram" if self.dcomm.allreduce_int(int(pick_gram), "max") else "horizontal"
 
     def _pairs(self, db, F1: int, mc: int):
         strat = self._pick_pair_strategy(db, F1)
         self.stats["pair_strategy"] = strat
+        r, nr = (self.comm.rank, self.comm.world_size) if self.cand_par else (0, 1)
         if strat == "gram":
             self._bitmaps(db)
-            pc = ops.pair_counts_gram(db["bm"], db["W"], db["wword"])
+            # candidate parallelism: each rank takes a 32-word-aligned slice of the columns
+            W = db["W"]
+            w0, w1 = (W * r // nr) // 32 * 32, (W if r == nr - 1 else (W * (r + 1) // nr) // 32 * 32)
+            wword = db["wword"][w0:w1] if db["wword"] is not None else None
+            pc = ops.pair_counts_gram(db["bm"][:, w0:], max(w1 - w0, 0), wword)
         else:
-            pc = ops.pair_counts_horizontal(db["roff"], db["ranks"], db["wrow"], F1, db.get("long_rows", True))
+            roff, ranks, wrow = db["roff"], db["ranks"], db["wrow"]
+            if nr > 1:   # candidate parallelism: each rank takes a slice of the rows
+                T = db["T"]
+                a, b = T * r // nr, T * (r + 1) // nr
+                ra, rb = int(roff[a].item()), int(roff[b].item())
+                roff, ranks = roff[a:b + 1] - ra, ranks[ra:rb]
+                wrow = wrow[a:b] if wrow is not None else None
+            pc = ops.pair_counts_horizontal(roff, ranks, wrow, F1, db.get("long_rows", True))
         iu = torch.triu_indices(F1, F1, 1, device=pc.device)
         flat = pc[iu[0], iu[1]].contiguous()
         self.comm.all_reduce_(flat)
@@ -464,18 +484,39 @@ class FastApriori:
     # k >= 3 (FastApriori.scala:132-160)
     # ------------------------------------------------------------------
     def _count_level(self, db, prev: np.ndarray, prefix_idx, ext_off, ext) -> np.ndarray:
+        if self.cand_par:
+            # candidate parallelism: this rank counts a contiguous, extension-balanced
+            # range of prefix groups over all rows; the other entries stay 0, so the
+            # all-reduce assembles the full vector (FastApriori.scala:140-157)
+            C, r, nr = int(ext.size), self.comm.rank, self.comm.world_size
+            g0, g1 = (int(np.searchsorted(ext_off, C * q // nr, side="left")) for q in (r, r + 1))
+            g1 = prefix_idx.size if r == nr - 1 else g1
+            e0, e1 = int(ext_off[g0]), int(ext_off[g1])
+            part = np.zeros(0, np.int64)
+            if g1 > g0:
+                part = self._count_groups(db, prev, prefix_idx[g0:g1], ext_off[g0:g1 + 1] - e0, ext[e0:e1])
+            full = torch.zeros(C, dtype=torch.int64, device=self.comm.device)
+            full[e0:e1] = torch.from_numpy(part).to(full.device)
+            self.comm.all_reduce_(full)
+            return full.cpu().numpy()
+        cnt = self._count_groups(db, prev, prefix_idx, ext_off, ext)
+        return cnt
+
+    def _count_groups(self, db, prev: np.ndarray, prefix_idx, ext_off, ext) -> np.ndarray:
+        """Local support counts of the groups (prefix_idx, ext_off, ext), all-reduced over
+        the row shards in count parallelism (a no-op collective in candidate mode)."""
         dev = db["ranks"].device
         if dev.type == "cuda" and self.cfg.level_kernel in ("auto", "slab"):
             cnt = ops.count_level_slab(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"],
                                        prev[prefix_idx], ext_off, ext, db["wword"])
             if cnt is not None:
-                self.comm.all_reduce_(cnt)
+                self.dcomm.all_reduce_(cnt)
                 return cnt.cpu().numpy()
         self._bitmaps(db)
         prefix = torch.from_numpy(np.ascontiguousarray(prev[prefix_idx], dtype=np.int32)).to(dev)
         ext_t = torch.from_numpy(np.ascontiguousarray(ext, dtype=np.int32)).to(dev)
         cnt = ops.count_candidates(db["bm"], db["W"], prefix, ext_off, ext_t, db["wword"])
-        self.comm.all_reduce_(cnt)
+        self.dcomm.all_reduce_(cnt)
         return cnt.cpu().numpy()
 
 

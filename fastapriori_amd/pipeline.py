@@ -16,7 +16,7 @@ import time
 from .config import JobConfig
 from .models.apriori import FastApriori, MinerConfig
 from .models.rules import AssociationRules
-from .parallel.comm import init_comm, shutdown_comm
+from .parallel.comm import Comm, init_comm, shutdown_comm
 from .utils import io
 from .utils.checkpoint import Checkpointer, input_fingerprint
 from .utils.metrics import Logger
@@ -49,9 +49,10 @@ def run_job(cfg: JobConfig, comm=None) -> dict:
                 raise FileNotFoundError(f"no complete checkpoint under {ckpt.dir}")
         else:
             resume = ckpt.load() if (ckpt is not None and cfg.resume) else None
-            shard = io.read_shard(d_path, comm)
+            # candidate distribution: every rank holds the whole DB
+            shard = io.read_shard(d_path, comm if cfg.strategy == "count" else Comm(device=comm.device))
             mcfg = MinerConfig(min_support=cfg.min_support, dedup=cfg.dedup, pair_strategy=cfg.pair_strategy,
-                               max_level=cfg.max_level)
+                               max_level=cfg.max_level, parallelism=cfg.strategy)
             miner = FastApriori(cfg.min_support, comm, mcfg, log, ckpt)
             result = miner.run(shard, resume=resume)
             summary["miner"] = dict(miner.stats)

@@ -13,7 +13,7 @@ import pytest
 from fastapriori_amd.parallel.launch import spawn_local
 
 
-def _mine_file(path_prefix: str, ms: float, dedup: str, strategy: str):
+def _mine_file(path_prefix: str, ms: float, dedup: str, strategy: str, par: str = "count"):
     from fastapriori_amd.models.apriori import FastApriori, MinerConfig
     from fastapriori_amd.models.rules import AssociationRules
     from fastapriori_amd.parallel.comm import init_comm, shutdown_comm
@@ -22,8 +22,9 @@ def _mine_file(path_prefix: str, ms: float, dedup: str, strategy: str):
 
     comm = init_comm("cpu")
     try:
-        shard = read_shard(path_prefix + "D.dat", comm)
-        cfg = MinerConfig(trim_min_rows=0, min_support=ms, dedup=dedup, pair_strategy=strategy)
+        from fastapriori_amd.parallel.comm import Comm
+        shard = read_shard(path_prefix + "D.dat", comm if par == "count" else Comm())
+        cfg = MinerConfig(trim_min_rows=0, min_support=ms, dedup=dedup, pair_strategy=strategy, parallelism=par)
         res = FastApriori(ms, comm, cfg, Logger(comm.rank, enabled=False)).run(shard)
         users = read_shard(path_prefix + "U.dat", comm)
         recs = AssociationRules(res, comm, Logger(comm.rank, enabled=False)).run(users)
@@ -43,6 +44,24 @@ def _mine_zipf(n: int, ms: float, f1: str):
     try:
         shard = generate_zipf_shard(n, comm, "cpu", mean_len=40.0, n_items=1_500_000, n_topics=40, seed=3)
         res = FastApriori(ms, comm, MinerConfig(min_support=ms, f1=f1), Logger(comm.rank, enabled=False)).run(shard)
+        return res.as_dict(), res.items
+    finally:
+        shutdown_comm(comm)
+
+
+def _mine_candidate(n: int, ms: float, strategy: str, dedup: str):
+    """Candidate distribution: every rank generates the WHOLE DB (local Comm)."""
+    from fastapriori_amd.models.apriori import FastApriori, MinerConfig
+    from fastapriori_amd.parallel.comm import Comm, init_comm, shutdown_comm
+    from fastapriori_amd.utils.io import generate_shard
+    from fastapriori_amd.utils.metrics import Logger
+
+    comm = init_comm("cpu")
+    try:
+        shard = generate_shard(n, Comm(), "cpu", 12.0, 4.0, 100, 80, seed=7)
+        cfg = MinerConfig(trim_min_rows=0, min_support=ms, parallelism="candidate", pair_strategy=strategy,
+                          dedup=dedup)
+        res = FastApriori(ms, comm, cfg, Logger(comm.rank, enabled=False)).run(shard)
         return res.as_dict(), res.items
     finally:
         shutdown_comm(comm)
@@ -121,3 +140,20 @@ def test_heavy_hitter_f1_across_ranks():
     ref = spawn_local(_mine_zipf, 1, 3000, 0.03, "histogram")[0]
     outs = spawn_local(_mine_zipf, 2, 3000, 0.03, "sketch")
     assert all(o == ref for o in outs) and len(ref[0]) > 20
+
+
+@pytest.mark.parametrize("strategy,dedup", [("horizontal", "off"), ("gram", "on")])
+def test_candidate_distribution_matches_single_rank(strategy, dedup):
+    # replicated DB; pair counts split by rows / bitmap words, level candidates split by rank
+    ref = spawn_local(_mine_candidate, 1, 5000, 0.01, strategy, dedup)[0]
+    for world in (2, 3):
+        outs = spawn_local(_mine_candidate, world, 5000, 0.01, strategy, dedup)
+        assert all(o == ref for o in outs)
+    assert len(ref[0]) > 200 and max(len(k) for k in ref[0]) >= 4
+
+
+def test_candidate_distribution_file_and_rules(numeric_db):
+    ref = spawn_local(_mine_file, 1, numeric_db, 0.02, "auto", "auto")[0]
+    outs = spawn_local(_mine_file, 2, numeric_db, 0.02, "auto", "auto", "candidate")
+    assert all(o["sets"] == ref["sets"] and o["items"] == ref["items"] for o in outs)
+    assert outs[0]["recs"] == ref["recs"]
