@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--config", default="T10I4D100M")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--modes", default="0,1,2,3")
+    ap.add_argument("--sw", default="", help="comma list of FA_SLAB_SW values to replay (default: planner)")
     a = ap.parse_args()
     n, L, I, P, N, ms = bench.CONFIGS[a.config]
     shard = generate_shard(n, Comm(), "cuda", L, I, P, N, 1)
@@ -44,21 +45,24 @@ def main():
     apriori.ops.count_level_slab = real
     out = []
     for i, (args, kw) in enumerate(calls):
-        row = {"k": args[5].shape[1] + 1, "C": int(args[7].size)}
-        for mode in a.modes.split(","):
-            os.environ["FA_SLAB_DEBUG"] = mode
-            ts = []
-            for _ in range(a.reps):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                real(*args, **kw)
-                e1.record()
-                torch.cuda.synchronize()
-                ts.append(e0.elapsed_time(e1))
-            row[f"mode{mode}_ms"] = round(sorted(ts)[len(ts) // 2], 3)
-        row.update(ops.primitives.LAST_SLAB_PLAN)
-        out.append(row)
-        print(json.dumps(row), flush=True)
+        for sw in (a.sw.split(",") if a.sw else [""]):
+            os.environ["FA_SLAB_SW"] = sw or "0"
+            row = {"k": args[5].shape[1] + 1, "C": int(args[7].size), "force_sw": sw}
+            for mode in a.modes.split(","):
+                os.environ["FA_SLAB_DEBUG"] = mode
+                ts = []
+                for _ in range(a.reps):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    real(*args, **kw)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    ts.append(e0.elapsed_time(e1))
+                row[f"mode{mode}_ms"] = round(sorted(ts)[len(ts) // 2], 3)
+            row.update(ops.primitives.LAST_SLAB_PLAN)
+            out.append(row)
+            print(json.dumps(row), flush=True)
+        os.environ["FA_SLAB_SW"] = "0"
     os.environ["FA_SLAB_DEBUG"] = "0"
 
 

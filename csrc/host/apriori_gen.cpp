@@ -130,7 +130,10 @@ FA_API Cands* fa_apriori_gen(const int32_t* prev, int64_t n, int m, int nthreads
   parallel_for(nblocks, nthreads, 1, [&](int64_t b0, int64_t b1, int) {
     std::vector<uint64_t> st(m);
     for (int64_t b = b0; b < b1; ++b) {
-      Cands& pc = parts[b];
+      // built locally and moved: neighbouring blocks run on other threads, and
+      // appending through adjacent parts[] headers would false-share
+      struct Local { Cands c; Cands& dst; ~Local() { dst = std::move(c); } } L{Cands(), parts[b]};
+      Cands& pc = L.c;
       pc.ext_off.push_back(0);
       for (int64_t i = b * grain; i < std::min(n, (b + 1) * grain); ++i) {
         const int32_t* x = prev + i * m;

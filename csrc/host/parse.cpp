@@ -135,6 +135,53 @@ struct ThreadDict {
   }
 };
 
+// Numeric fast path for one line starting at p: a single pass in which digits
+// accumulate into the value and separators emit it; ids go straight into
+// `items` (duplicates of the line to `extras`).  Returns the position of the
+// line terminator, or -1 when the line needs the exact slow path (a byte that
+// is neither a digit, a separator nor a terminator: e.g. a trimmed control
+// character, or a non-numeric / non-canonical token) -- then nothing was emitted.
+static inline int64_t fast_numeric_line(const uint8_t* d, int64_t size, int64_t p, std::vector<int32_t>& items,
+                                        std::vector<int32_t>& extras, int32_t& mx) {
+  const size_t base = items.size();
+  uint64_t v = 0;
+  int nd = 0;                 // digits of the current token (0 = not in a token)
+  bool lead0 = false;
+  auto emit = [&]() -> bool {
+    if (nd > 10 || (lead0 && nd > 1) || v > 2147483646ull) return false;
+    const int32_t id = (int32_t)(v + 1);
+    for (size_t j = base; j < items.size(); ++j)
+      if (items[j] == id) { extras.push_back(id); return true; }
+    items.push_back(id);
+    mx = std::max(mx, id);
+    return true;
+  };
+  int64_t q = p;
+  for (; q < size; ++q) {
+    const uint8_t c = d[q];
+    const uint8_t dg = (uint8_t)(c - '0');
+    if (dg <= 9) {
+      if (nd == 0) { v = 0; lead0 = dg == 0; }
+      v = v * 10 + dg;
+      ++nd;
+      continue;
+    }
+    if (c == ' ' || c == '\t' || c == 0x0B || c == '\f') {
+      if (nd) { if (!emit()) { items.resize(base); return -1; } nd = 0; }
+      continue;
+    }
+    if (c == '\n' || c == '\r') break;
+    items.resize(base);
+    return -1;
+  }
+  if (nd && !emit()) { items.resize(base); return -1; }
+  if (items.size() == base) {          // blank line (after trim): the single token ""
+    items.push_back(0);
+    mx = std::max(mx, 0);
+  }
+  return q;
+}
+
 // Parse lines starting in [b, e) of an in-memory buffer.
 static int parse_buffer(const char* d, int64_t size, int64_t b, int64_t e, int mode, int nthreads,
                         TxnDB* db) {
@@ -149,16 +196,40 @@ static int parse_buffer(const char* d, int64_t size, int64_t b, int64_t e, int m
   db->chunks.assign(nt, TxnChunk());
   std::vector<std::vector<int32_t>> extras(nt);
   std::vector<ThreadDict> dicts(mode == 1 ? nt : 0);
+  std::vector<int32_t> tmax(nt, -1);
   std::atomic<bool> non_numeric{false};
 
   parallel_for_threads(nt, [&](int t) {
     int64_t lo = (t == 0) ? first : next_line_start(d, size, cuts[t]);
     int64_t hi = cuts[t + 1];
-    TxnChunk& ch = db->chunks[t];
+    // Everything a thread appends to lives on its own stack and is moved into
+    // the shared arrays at the end: the vector headers of db->chunks[] and
+    // extras[] sit side by side, and updating them per token false-shares
+    // (measured 4x slower than serial on a 16-thread EPYC box).
+    struct Local {
+      TxnChunk ch;
+      std::vector<int32_t> ex;
+      int32_t mx = -1;
+      TxnChunk& dst_ch;
+      std::vector<int32_t>& dst_ex;
+      int32_t& dst_mx;
+      ~Local() { dst_ch = std::move(ch); dst_ex = std::move(ex); dst_mx = mx; }
+    } L{TxnChunk(), {}, -1, db->chunks[t], extras[t], tmax[t]};
+    TxnChunk& ch = L.ch;
+    int32_t& mx = L.mx;
     std::vector<int32_t> line, table;
+    ch.items.reserve((size_t)std::max<int64_t>(0, (hi - lo) / 3));
+    ch.lens.reserve((size_t)std::max<int64_t>(0, (hi - lo) / 24));
     int64_t p = lo;
     while (p < hi && p < size) {
-      int64_t q = p;
+      int64_t q;
+      if (mode == 0 && (q = fast_numeric_line((const uint8_t*)d, size, p, ch.items, L.ex, mx)) >= 0) {
+        ch.lens.push_back((int64_t)(ch.items.size()));
+        if (q >= size) { p = size; break; }
+        p = (d[q] == '\r' && q + 1 < size && d[q + 1] == '\n') ? q + 2 : q + 1;
+        continue;
+      }
+      q = p;
       while (q < size && d[q] != '\n' && d[q] != '\r') ++q;
       line.clear();
       if (mode == 0) {
@@ -174,7 +245,9 @@ static int parse_buffer(const char* d, int64_t size, int64_t b, int64_t e, int m
           line.push_back(td.get(std::string_view(s, (size_t)n)));
         });
       }
-      emit_distinct(line, ch.items, extras[t], table);
+      if (mode == 0)
+        for (int32_t v : line) mx = std::max(mx, v);
+      emit_distinct(line, ch.items, L.ex, table);
       ch.lens.push_back((int64_t)(ch.items.size()));  // cumulative end within chunk
       if (q >= size) { p = size; break; }
       p = (d[q] == '\r' && q + 1 < size && d[q + 1] == '\n') ? q + 2 : q + 1;
@@ -186,8 +259,7 @@ static int parse_buffer(const char* d, int64_t size, int64_t b, int64_t e, int m
   db->numeric = (mode == 0);
   if (mode == 0) {
     int32_t mx = -1;
-    for (auto& ch : db->chunks) for (int32_t v : ch.items) mx = std::max(mx, v);
-    for (auto& ex : extras) for (int32_t v : ex) mx = std::max(mx, v);
+    for (int32_t m : tmax) mx = std::max(mx, m);
     db->vocab = (int64_t)mx + 1;
   } else {
     // merge thread dictionaries into one shard dictionary, remap ids

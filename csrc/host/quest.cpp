@@ -157,7 +157,10 @@ FA_API TxnDB* fa_quest_generate(int64_t txn_begin, int64_t txn_end, double avg_l
   db->chunks.assign(nt, TxnChunk());
   parallel_for_threads(nt, [&](int t) {
     int64_t lo = txn_begin + n * t / nt, hi = txn_begin + n * (t + 1) / nt;
-    TxnChunk& ch = db->chunks[t];
+    // appended on this thread's stack, moved into the shared array at the end
+    // (adjacent TxnChunk headers false-share when appended to in place)
+    struct Local { TxnChunk ch; TxnChunk& dst; ~Local() { dst = std::move(ch); } } L{TxnChunk(), db->chunks[t]};
+    TxnChunk& ch = L.ch;
     ch.lens.reserve(hi - lo);
     ch.items.reserve((size_t)((hi - lo) * (avg_len + 1)));
     std::vector<int32_t> out, tmp;
@@ -255,7 +258,10 @@ FA_API TxnDB* fa_zipf_generate(int64_t txn_begin, int64_t txn_end, double mean_l
   const double mu = std::log(std::max(1.0, mean_len)) - 0.5 * sigma * sigma;
   parallel_for_threads(nt, [&](int t) {
     const int64_t lo = txn_begin + n * t / nt, hi = txn_begin + n * (t + 1) / nt;
-    TxnChunk& ch = db->chunks[t];
+    // appended on this thread's stack, moved into the shared array at the end
+    // (adjacent TxnChunk headers false-share when appended to in place)
+    struct Local { TxnChunk ch; TxnChunk& dst; ~Local() { dst = std::move(ch); } } L{TxnChunk(), db->chunks[t]};
+    TxnChunk& ch = L.ch;
     ch.lens.reserve(hi - lo);
     std::vector<int64_t> row;
     std::vector<int64_t> table;

@@ -430,6 +430,9 @@ _LDS_BYTES = 160 * 1024 - 512   # minus the slab kernel's static scratch (build_
 
 def slab_plan(n_used: int, C: int):
     """Pick the slab width SW (words) and the accumulator capacity for k_count_slab."""
+    force = int(os.environ.get("FA_SLAB_SW", "0"))
+    if force:
+        return force, int((_LDS_BYTES - n_used * (force + 2) * 8) // 4)
     for sw in (32, 16, 8, 4):
         slab = n_used * (sw + 2) * 8
         cap = (_LDS_BYTES - slab) // 4

@@ -50,7 +50,9 @@ def run_job(cfg: JobConfig, comm=None) -> dict:
         else:
             resume = ckpt.load() if (ckpt is not None and cfg.resume) else None
             # candidate distribution: every rank holds the whole DB
+            t_read = time.time()
             shard = io.read_shard(d_path, comm if cfg.strategy == "count" else Comm(device=comm.device))
+            summary["read_ms"] = round((time.time() - t_read) * 1000, 1)
             mcfg = MinerConfig(min_support=cfg.min_support, dedup=cfg.dedup, pair_strategy=cfg.pair_strategy,
                                max_level=cfg.max_level, parallelism=cfg.strategy)
             miner = FastApriori(cfg.min_support, comm, mcfg, log, ckpt)
@@ -59,6 +61,7 @@ def run_job(cfg: JobConfig, comm=None) -> dict:
             del shard
             if ckpt is not None:
                 ckpt.mark_complete(result)
+            t_write = time.time()
             if comm.is_root:
                 io.write_freq_itemsets(result, out_freq, overwrite=cfg.overwrite)
                 if cfg.with_counts:
@@ -67,6 +70,8 @@ def run_job(cfg: JobConfig, comm=None) -> dict:
                     io.write_items_to_rank(result, cfg.output + "ItemsToRank")
                     io.write_freq_items(result, cfg.output + "FreqItems")
         comm.barrier()
+        if not cfg.rules_only:
+            summary["write_ms"] = round((time.time() - t_write) * 1000, 1)
         t_mine = int((time.time() - t1) * 1000)
         log.line(f"Total time for get freqItemsets {t_mine}")
 
