@@ -843,7 +843,7 @@ __device__ __forceinline__ void slab_build_word(uint64_t* __restrict__ slab, int
                                                 int64_t ncols, const int64_t* __restrict__ roff,
                                                 const int32_t* __restrict__ ranks,
                                                 const int32_t* __restrict__ item_map, int h, int nsub,
-                                                unsigned long long* words) {
+                                                unsigned long long* words, int swz = 0) {
   const int lane = threadIdx.x & 63;
   const int64_t st = roff[min(col0 + lane, ncols)];
   const int64_t base = roff[col0];
@@ -868,7 +868,7 @@ __device__ __forceinline__ void slab_build_word(uint64_t* __restrict__ slab, int
     for (int u = 0; u < U; ++u) {
       const int l = cs + __popcll(S[u] & le) - 1;
       const int uu = r[u] >= 0 ? item_map[r[u]] : -1;
-      if (uu >= 0) atomicOr((unsigned long long*)(slab + (size_t)uu * swp + q), 1ull << l);
+      if (uu >= 0) atomicOr((unsigned long long*)(slab + (size_t)uu * swp + (q ^ ((uu << 2) & swz))), 1ull << l);
       cs += __popcll(S[u]);
     }
   }
@@ -1004,6 +1004,218 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
     if (acc[i]) atomicAdd(&out[i], acc[i]);
 }
 
+// ---------------------------------------------------------------------------
+// k >= 3, trie-shared slab counting (the default level kernel).
+//
+// Same slab-stationary structure as k_count_slab (one LDS slab of the used
+// items per tile, per-candidate LDS accumulators across tiles), with two
+// changes measured to matter on MI355X:
+//
+//  * Prefix sharing along the candidate trie (FastApriori.scala:143-145 ANDs a
+//    group's prefix once; here the sharing extends across groups).  The
+//    active (k-1)-prefixes are visited in lexicographic order inside a work
+//    item; the AND of the first D1 items (P1), of the first D2 items (P2) and
+//    of the whole prefix (p) are kept in registers and recomputed only when
+//    the prefix changes at that depth (piece flags).  On T40I10 levels 8-11
+//    this reads 2.1-2.4x fewer slab rows than recomputing every prefix.
+//  * SW/4 lanes per work item (4 words each) with a per-item slot rotation:
+//    at SW = 32 the 16 lanes of every ds_read_b128 lane group
+//    ({0-3,12-15,20-27}, ...) cover 16 distinct 16-byte slots of the 256-byte
+//    rows, so slab reads are bank-conflict free (thread-per-group reads of
+//    random rows were ~3.5-way conflicted).  Partial popcounts are summed
+//    over the item's lanes with DPP (quad_perm, row_half_mirror).
+//
+// Work item w = pieces [witems[w].x, witems[w].y); piece = (gpre offset of its
+// prefix row, ext begin, ext end, flags): bit 1 = recompute P2 from P1, bit 0 =
+// recompute p from P2.  The first piece of a work item recomputes everything.
+// ---------------------------------------------------------------------------
+template <int SW, bool kWeighted, int kBuild>
+__global__ __launch_bounds__(kSlabThreads) void k_count_trie(
+    const int64_t* __restrict__ roff, const int32_t* __restrict__ ranks, const int32_t* __restrict__ src,
+    int64_t ncols, const int32_t* __restrict__ item_map, int n_used, const int32_t* __restrict__ gpre, int m,
+    int D1, int D2, const int4* __restrict__ pieces, const int2* __restrict__ witems, int NW,
+    const int32_t* __restrict__ gext, int C, const int32_t* __restrict__ wword, uint32_t* __restrict__ out,
+    const uint64_t* __restrict__ bm, int64_t Wp) {
+  constexpr int NQ = 2;                        // uint4 (4 words) per lane: ~90 VGPRs at 1024 threads
+  constexpr int RS = SW / 2;                   // uint4 slots per slab row
+  constexpr int LPP = RS / NQ;                 // lanes per work item: 2 / 4 / 8 for SW = 8 / 16 / 32
+  static_assert(LPP == 2 || LPP == 4 || LPP == 8, "SW in {8, 16, 32}");
+  // Row u stores logical 16-B slot L at physical slot L ^ (2u mod RS) (word q at
+  // q ^ (4u mod SW)).  The XOR is even, so a read's slot parity is kept and the
+  // rotation below stays conflict-free, while the slab build's atomicOr of one
+  // word q over random items u spreads over 8 slots instead of one bank pair.
+  constexpr int SWZ = SW - 4;                  // word-index XOR mask applied to (u << 2)
+  extern __shared__ uint4 lds4[];
+  __shared__ unsigned long long build_words[kSlabThreads / 64 * 2];
+  uint64_t* slab = reinterpret_cast<uint64_t*>(lds4);
+  uint32_t* acc = reinterpret_cast<uint32_t*>(slab + (size_t)n_used * SW);
+  for (int i = threadIdx.x; i < C; i += blockDim.x) acc[i] = 0;
+  const int64_t W = (ncols + 63) >> 6;
+  const int64_t nslabs = (W + SW - 1) / SW;
+
+  const int lane = threadIdx.x & 63;
+  const int t = lane & (LPP - 1);
+  const int grp = threadIdx.x / LPP;           // work-item slot in the workgroup
+  constexpr int NGRP = kSlabThreads / LPP;
+  const int rot = (lane / LPP) % NQ;
+  int off[NQ];                                 // rotated slot of step q (conflict-free lane groups)
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) off[q] = t * NQ + (q + rot) % NQ;
+
+  for (int64_t sb = blockIdx.x; sb < nslabs; sb += gridDim.x) {
+    const int64_t w0 = sb * SW;
+    __syncthreads();
+    if (kBuild == kBuildBM) {
+      for (int i = threadIdx.x; i < n_used * SW; i += blockDim.x) {
+        const int u = i / SW, q = i - u * SW;
+        slab[(size_t)u * SW + (q ^ ((u << 2) & SWZ))] = (w0 + q < W) ? bm[(size_t)u * Wp + w0 + q] : 0ull;
+      }
+    } else {
+      {
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        for (int i = threadIdx.x; i < n_used * RS; i += blockDim.x) lds4[i] = z;
+      }
+      __syncthreads();
+      if (kBuild == kBuildContig) {
+        constexpr int NWV = kSlabThreads / 64;
+        constexpr int NSUB = NWV > SW ? NWV / SW : 1;
+        const int wv = threadIdx.x >> 6;
+        for (int q = wv / NSUB; q < SW; q += NWV / NSUB)
+          if ((w0 + q) * 64 < ncols)
+            slab_build_word(slab, SW, q, (w0 + q) * 64, ncols, roff, ranks, item_map, wv % NSUB, NSUB,
+                            build_words + wv * 2, SWZ);
+      } else {
+        // dedup layout: column j of the tile gathers row src[col]
+        for (int j = threadIdx.x; j < SW * 64; j += blockDim.x) {
+          const int64_t col = w0 * 64 + j;
+          if (col >= ncols) break;
+          const int64_t row = src ? (int64_t)src[col] : col;
+          if (row < 0) continue;
+          const unsigned long long bit = 1ull << (j & 63);
+          const int qw = j >> 6;
+          for (int64_t r = roff[row], r1 = roff[row + 1]; r < r1; ++r) {
+            const int uu = item_map[ranks[r]];
+            if (uu >= 0) atomicOr((unsigned long long*)(slab + (size_t)uu * SW + (qw ^ ((uu << 2) & SWZ))), bit);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    uint32_t wt[2 * NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int64_t wa = w0 + 2 * off[q];
+      wt[2 * q] = kWeighted ? ((wa < W) ? (uint32_t)wword[wa] : 0u) : 1u;
+      wt[2 * q + 1] = kWeighted ? ((wa + 1 < W) ? (uint32_t)wword[wa + 1] : 0u) : 1u;
+    }
+    // AND of slab rows it[j0..j1) into a[]; two rows per step keep 2*NQ reads in flight
+    auto and_rows = [&](uint4 (&a)[NQ], const int32_t* it, int j0, int j1) {
+      int j = j0;
+      for (; j + 2 <= j1; j += 2) {
+        const int ua = it[j], ub = it[j + 1];
+        const int xa = (ua << 1) & (RS - 1), xb = (ub << 1) & (RS - 1);
+        const uint4* ra = lds4 + (size_t)ua * RS;
+        const uint4* rb = lds4 + (size_t)ub * RS;
+        uint4 va[NQ], vb[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) { va[q] = ra[off[q] ^ xa]; vb[q] = rb[off[q] ^ xb]; }
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          a[q].x &= va[q].x & vb[q].x; a[q].y &= va[q].y & vb[q].y;
+          a[q].z &= va[q].z & vb[q].z; a[q].w &= va[q].w & vb[q].w;
+        }
+      }
+      if (j < j1) {
+        const int ua = it[j], xa = (ua << 1) & (RS - 1);
+        const uint4* ra = lds4 + (size_t)ua * RS;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const uint4 v = ra[off[q] ^ xa];
+          a[q].x &= v.x; a[q].y &= v.y; a[q].z &= v.z; a[q].w &= v.w;
+        }
+      }
+    };
+    auto dot = [&](const uint4 (&p)[NQ], const uint4 (&v)[NQ]) -> uint32_t {
+      uint32_t s = 0;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        if (kWeighted) {
+          s += (uint32_t)(__popc(p[q].x & v[q].x) + __popc(p[q].y & v[q].y)) * wt[2 * q] +
+               (uint32_t)(__popc(p[q].z & v[q].z) + __popc(p[q].w & v[q].w)) * wt[2 * q + 1];
+        } else {
+          s += __popc(p[q].x & v[q].x) + __popc(p[q].y & v[q].y) + __popc(p[q].z & v[q].z) +
+               __popc(p[q].w & v[q].w);
+        }
+      }
+      return s;
+    };
+    // sum over the work item's LPP consecutive lanes (DPP: quad_perm, row_half_mirror)
+    auto lanes_sum = [&](uint32_t s) -> uint32_t {
+      s += (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0xB1, 0xf, 0xf, false);                   // [1,0,3,2]
+      if (LPP >= 4) s += (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0x4E, 0xf, 0xf, false);     // [2,3,0,1]
+      if (LPP >= 8) s += (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0x141, 0xf, 0xf, false);    // half mirror
+      return s;
+    };
+    for (int w = grp; w < NW; w += NGRP) {
+      const int2 wi = witems[w];
+      uint4 P1[NQ], P2[NQ], p[NQ];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) P1[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
+      and_rows(P1, gpre + pieces[wi.x].x, 0, D1);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) { P2[q] = P1[q]; p[q] = P1[q]; }
+      for (int pi = wi.x; pi < wi.y; ++pi) {
+        const int4 d = pieces[pi];
+        const int32_t* it = gpre + d.x;
+        if (d.w & 2) {
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) P2[q] = P1[q];
+          and_rows(P2, it, D1, D2);
+        }
+        if (d.w & 1) {
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) p[q] = P2[q];
+          and_rows(p, it, D2, m);
+        }
+        int e = d.y;
+        // four extension rows per step: 4*NQ independent slab reads in flight per lane
+        for (; e + 4 <= d.z; e += 4) {
+          const int u0 = gext[e], u1 = gext[e + 1], u2 = gext[e + 2], u3 = gext[e + 3];
+          const int x0 = (u0 << 1) & (RS - 1), x1 = (u1 << 1) & (RS - 1);
+          const int x2 = (u2 << 1) & (RS - 1), x3 = (u3 << 1) & (RS - 1);
+          const uint4* r0 = lds4 + (size_t)u0 * RS;
+          const uint4* r1 = lds4 + (size_t)u1 * RS;
+          const uint4* r2 = lds4 + (size_t)u2 * RS;
+          const uint4* r3 = lds4 + (size_t)u3 * RS;
+          uint4 v0[NQ], v1[NQ], v2[NQ], v3[NQ];
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) {
+            v0[q] = r0[off[q] ^ x0]; v1[q] = r1[off[q] ^ x1]; v2[q] = r2[off[q] ^ x2]; v3[q] = r3[off[q] ^ x3];
+          }
+          const uint32_t s0 = lanes_sum(dot(p, v0)), s1 = lanes_sum(dot(p, v1));
+          const uint32_t s2 = lanes_sum(dot(p, v2)), s3 = lanes_sum(dot(p, v3));
+          if (t == 0) {
+            atomicAdd(&acc[e], s0); atomicAdd(&acc[e + 1], s1);
+            atomicAdd(&acc[e + 2], s2); atomicAdd(&acc[e + 3], s3);
+          }
+        }
+        for (; e < d.z; ++e) {
+          const int u0 = gext[e], x0 = (u0 << 1) & (RS - 1);
+          const uint4* r0 = lds4 + (size_t)u0 * RS;
+          uint4 v0[NQ];
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) v0[q] = r0[off[q] ^ x0];
+          const uint32_t s0 = lanes_sum(dot(p, v0));
+          if (t == 0) atomicAdd(&acc[e], s0);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < C; i += blockDim.x)
+    if (acc[i]) atomicAdd(&out[i], acc[i]);
+}
+
 }  // namespace fa
 
 using namespace fa;
@@ -1113,6 +1325,42 @@ FA_API int fa_hip_count_slab(const int64_t* roff, const int32_t* ranks, const in
   const int dbg = getenv("FA_SLAB_DEBUG") ? atoi(getenv("FA_SLAB_DEBUG")) : 0;
   hipLaunchKernelGGL(kern, g, b, lds, st, roff, ranks, src, ncols, item_map, n_used, gpre, m, gext_off, gext, G, C,
                      wword, out, bm, Wp, dbg);
+  FA_LAUNCH_RET();
+}
+
+// Trie-shared slab counting (k_count_trie).  pieces: int4 [NP], witems: int2 [NW]
+// (see the kernel); gext/out are pass-local (C <= LDS accumulator capacity).
+// Returns 3 when the slab + accumulator exceed the LDS budget.
+FA_API int fa_hip_count_trie(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
+                             const int32_t* item_map, int n_used, const int32_t* gpre, int m, int D1, int D2,
+                             const void* pieces, const void* witems, int NW, const int32_t* gext, int C,
+                             const int32_t* wword, uint32_t* out, int sw, int n_wg, const uint64_t* bm, int64_t Wp,
+                             hipStream_t st) {
+  if (NW <= 0 || C <= 0 || ncols <= 0) return 0;
+  if (!(0 <= D1 && D1 <= D2 && D2 <= m)) return 2;
+  const size_t lds = (size_t)n_used * sw * 8 + (size_t)C * 4;
+  if (lds > 160 * 1024 - 512) return 3;
+  using KernT = void (*)(const int64_t*, const int32_t*, const int32_t*, int64_t, const int32_t*, int,
+                         const int32_t*, int, int, int, const int4*, const int2*, int, const int32_t*, int,
+                         const int32_t*, uint32_t*, const uint64_t*, int64_t);
+  KernT kern = nullptr;
+#define FA_TRIE_MODE(S, B) kern = wword ? (KernT)k_count_trie<S, true, B> : (KernT)k_count_trie<S, false, B>;
+#define FA_TRIE_CASE(S)                                   \
+  if (sw == S) {                                          \
+    if (bm) { FA_TRIE_MODE(S, kBuildBM) }                 \
+    else if (src) { FA_TRIE_MODE(S, kBuildCols) }         \
+    else { FA_TRIE_MODE(S, kBuildContig) }                \
+  }
+  FA_TRIE_CASE(8)
+  FA_TRIE_CASE(16)
+  FA_TRIE_CASE(32)
+#undef FA_TRIE_CASE
+#undef FA_TRIE_MODE
+  if (!kern) return 1;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(kern, dim3((unsigned)n_wg), dim3(kSlabThreads), lds, st, roff, ranks, src, ncols, item_map,
+                     n_used, gpre, m, D1, D2, (const int4*)pieces, (const int2*)witems, NW, gext, C, wword, out, bm,
+                     Wp);
   FA_LAUNCH_RET();
 }
 

@@ -47,6 +47,9 @@ GRAM_WORDPAIRS_PER_S = 1.2e13
 # numeric vocabularies at least this wide count F1 with the sketch + exact pass
 F1_SKETCH_MIN_VOCAB = 1 << 20
 F1_MAX_CANDIDATES = ops.primitives.F1_MAX_CANDIDATES
+# auto level kernel: trie-shared counting when its slab-row reads are below this
+# fraction of the slab kernel's (measured break-even on T10I4 / T40I10, MI355X)
+TRIE_MIN_SAVING = float(os.environ.get("FA_TRIE_MIN_SAVING", "0.53"))
 
 
 @dataclass
@@ -56,7 +59,7 @@ class MinerConfig:
     pair_strategy: str = "auto"     # auto | horizontal | gram
     dedup_threshold: float = 0.8    # dedup when distinct/T below this (auto)
     max_level: int = 0              # 0 = unlimited
-    level_kernel: str = "auto"      # auto | slab | bitmap  (k >= 3 counting kernel)
+    level_kernel: str = os.environ.get("FA_LEVEL_KERNEL", "auto")   # auto (= trie) | trie | slab | bitmap
     trim: bool = True               # transaction trimming before every level k >= 3
     f1: str = "auto"                # auto | sketch | histogram  (frequent-item counting)
     trim_min_rows: int = 1 << 20    # no trimming below this many rows (fixed cost > gain)
@@ -152,10 +155,13 @@ class FastApriori:
                 with tm.phase(f"trim{k}"):
                     self._trim(db, np.unique(np.concatenate([levels[-1][prefix_idx].ravel(), ext])), k)
                 with tm.phase("count"):
+                    self._level_kernel_used = "slab"
                     cnt = self._count_level(db, levels[-1], prefix_idx, ext_off, ext)
                 if tm.sync:
-                    self.stats.setdefault("level_info", {})[k] = dict(
-                        ops.primitives.LAST_SLAB_PLAN, groups=int(prefix_idx.size))
+                    plan = ops.primitives.LAST_TRIE_PLAN if getattr(self, "_level_kernel_used", "") == "trie" \
+                        else ops.primitives.LAST_SLAB_PLAN
+                    plan = dict(plan, kernel=getattr(self, "_level_kernel_used", "slab"))
+                    self.stats.setdefault("level_info", {})[k] = dict(plan, groups=int(prefix_idx.size))
                 keep = cnt >= mc
                 g_of_e = np.repeat(np.arange(prefix_idx.size), np.diff(ext_off))
                 rows = np.concatenate([levels[-1][prefix_idx[g_of_e[keep]]], ext[keep, None]], axis=1)
@@ -506,7 +512,18 @@ class FastApriori:
         """Local support counts of the groups (prefix_idx, ext_off, ext), all-reduced over
         the row shards in count parallelism (a no-op collective in candidate mode)."""
         dev = db["ranks"].device
-        if dev.type == "cuda" and self.cfg.level_kernel in ("auto", "slab"):
+        lk = self.cfg.level_kernel
+        if dev.type == "cuda" and lk in ("auto", "trie"):
+            # auto: the trie kernel where prefix sharing removes enough slab reads
+            # (deep levels); the thread-per-group slab kernel is faster per read
+            cnt = ops.count_level_trie(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"],
+                                       prev[prefix_idx], ext_off, ext, db["wword"],
+                                       min_saving=TRIE_MIN_SAVING if lk == "auto" else 0.0)
+            if cnt is not None:
+                self._level_kernel_used = "trie"
+                self.dcomm.all_reduce_(cnt)
+                return cnt.cpu().numpy()
+        if dev.type == "cuda" and lk in ("auto", "slab"):
             cnt = ops.count_level_slab(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"],
                                        prev[prefix_idx], ext_off, ext, db["wword"])
             if cnt is not None:

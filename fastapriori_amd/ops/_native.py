@@ -38,6 +38,7 @@ _HOST_SIGS = {
     "fa_apriori_gen": (vp, [vp, i64, C.c_int, C.c_int, vp]),
     "fa_cands_export": (None, [vp, vp, vp, vp]),
     "fa_cands_free": (None, [vp]),
+    "fa_plan_trie": (C.c_int, [vp, i64, C.c_int, vp, i64, i64, C.c_int, C.c_int, vp, vp, vp, i64, vp]),
     "fa_rules_build": (vp, [vp, vp, vp, C.c_int, vp, C.c_int, vp]),
     "fa_rules_nante": (i64, [vp]),
     "fa_rules_nstats": (i64, [vp]),
@@ -62,6 +63,8 @@ _HIP_SIGS = {
     "fa_hip_txn_freq_count": (C.c_int, [vp, vp, i64, i64, vp, vp, vp]),
     "fa_hip_compress_regs": (C.c_int, [C.c_int, vp, vp, vp, vp, i64, vp, vp, vp, vp, vp]),
     "fa_hip_compress_staged": (C.c_int, [vp, vp, vp, i64, vp, vp, vp, vp, vp]),
+    "fa_hip_count_trie": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, vp, C.c_int, C.c_int, C.c_int, vp, vp,
+                                    C.c_int, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, i64, vp]),
     "fa_hip_count_slab": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, vp,
                                     C.c_int, C.c_int, vp, i64, vp]),
     "fa_hip_trim_scan_count": (C.c_int, [vp, vp, i64, vp, C.c_int, C.c_int, vp, vp, vp, vp, vp]),

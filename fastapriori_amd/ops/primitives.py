@@ -509,6 +509,140 @@ def count_level_slab(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, 
     return res
 
 
+# ---------------------------------------------------------------------------
+# k >= 3, trie-shared slab counting (k_count_trie + csrc/host/plan.cpp)
+# ---------------------------------------------------------------------------
+# relative cost of one slab-row read at slab width SW (16-B slot conflicts of the
+# rotated 4-word lane layout: none at 256-B rows, ~1.6x at 128 B, ~2.2x at 64 B)
+_TRIE_CONFLICT = {32: 1.0, 16: 1.6, 8: 2.2}
+TRIE_EMAX = int(os.environ.get("FA_TRIE_EMAX", "24"))     # max extensions per work item
+TRIE_ROUNDS = int(os.environ.get("FA_TRIE_ROUNDS", "4"))   # work items per lane group and pass (target)
+TRIE_PASS_WEIGHT = float(os.environ.get("FA_TRIE_PASS_WEIGHT", "4"))
+
+
+def trie_slab_plan(n_used: int, C: int, W: int, reads_est: float) -> tuple[int, int]:
+    """Slab width SW and accumulator capacity for k_count_trie, by a time model:
+    slab-row reads x words x conflict factor, plus one used-item bitmap stream per
+    extra accumulator pass.  (0, 0) when no width fits the LDS."""
+    force = int(os.environ.get("FA_SLAB_SW", "0"))
+    best = None
+    for sw in ((force,) if force else (32, 16, 8)):
+        cap = (_LDS_BYTES - n_used * sw * 8) // 4
+        if cap < min(C, 1024):
+            continue
+        passes = -(-C // cap)
+        t = reads_est * W * 8 * _TRIE_CONFLICT.get(sw, 2.0) / 60e12
+        if passes > 1:   # a pass re-streams the used-item bitmap and re-runs every tile's skeleton
+            t += TRIE_PASS_WEIGHT * passes * n_used * W * 8 / 5e12
+        if best is None or t < best[0]:
+            best = (t, sw, int(cap))
+    return (best[1], best[2]) if best else (0, 0)
+
+
+def emulate_trie(bits: np.ndarray, gpre: np.ndarray, gext: np.ndarray, plan, weights=None) -> np.ndarray:
+    """CPU model of k_count_trie's plan semantics over a bool matrix bits [n_used, ncols]
+    (tests: any piece-flag or pass-offset error shows up as a wrong count)."""
+    m = gpre.shape[1]
+    flat = gpre.reshape(-1)
+    w = np.ones(bits.shape[1], np.int64) if weights is None else weights
+    out = np.zeros(gext.size, np.int64)
+    ones = np.ones(bits.shape[1], bool)
+    for w0, w1, base in plan.passes.tolist():
+        for wi in range(w0, w1):
+            pa, pb = plan.witems[wi]
+            g0 = plan.pieces[pa, 0]
+            P1 = ones.copy()
+            for j in range(plan.d1):
+                P1 &= bits[flat[g0 + j]]
+            P2 = P1.copy(); p = P1.copy()
+            for pi in range(pa, pb):
+                off, e0, e1, f = plan.pieces[pi]
+                if f & 2:
+                    P2 = P1.copy()
+                    for j in range(plan.d1, plan.d2):
+                        P2 &= bits[flat[off + j]]
+                if f & 1:
+                    p = P2.copy()
+                    for j in range(plan.d2, m):
+                        p &= bits[flat[off + j]]
+                for e in range(e0, e1):
+                    out[base + e] += int(((p & bits[gext[base + e]]) * w).sum())
+    return out
+
+
+LAST_TRIE_PLAN: dict = {}
+
+
+def count_level_trie(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_off: np.ndarray,
+                     ext: np.ndarray, wword, min_saving: float = 0.0) -> torch.Tensor | None:
+    """Trie-shared slab counting for one level (device only).
+
+    prefix: int32 [G, m] prefix rows (lexicographic); ext_off int64 [G+1]; ext int32 [C].
+    Returns int64 counts [C] in ext order, or None when the used items do not fit
+    any LDS slab, or (min_saving > 0) when the plan's slab-row reads exceed
+    min_saving x those of the thread-per-group slab kernel (pieces of <= 8).
+    """
+    from .host import plan_trie
+    dev = ranks.device
+    C = int(ext.size)
+    if C == 0:
+        return torch.zeros(0, dtype=_I64, device=dev)
+    G, m = prefix.shape
+    used = np.unique(np.concatenate([prefix.ravel(), ext]))
+    W = (ncols + 63) // 64
+    sw, cap = trie_slab_plan(int(used.size), C, W, C + 0.5 * G * m)
+    if sw == 0:
+        return None
+    # enough work items per pass for every lane group of the workgroup to have several
+    # (latency hiding): NGRP = 1024 threads / (SW/4 lanes per item)
+    ngrp = 4096 // sw
+    emax = int(max(2, min(TRIE_EMAX, min(C, cap) // (TRIE_ROUNDS * ngrp))))
+    plan = plan_trie(prefix, ext_off, emax, cap)
+    if min_saving > 0:
+        slab_reads = int(np.ceil(np.diff(ext_off) / 8).sum()) * m + C
+        if plan.reads > min_saving * slab_reads:
+            return None
+    item_map = np.full(max(F1, 1), -1, dtype=np.int32)
+    item_map[used] = np.arange(used.size, dtype=np.int32)
+    gpre = np.ascontiguousarray(item_map[prefix], dtype=np.int32)
+    gext = np.ascontiguousarray(item_map[ext], dtype=np.int32)
+    # one host->device copy of all int32 tables
+    nP, nW = plan.pieces.size, plan.witems.size
+    host = np.concatenate([gpre.ravel(), gext, plan.pieces.ravel(), plan.witems.ravel(), item_map])
+    buf = torch.from_numpy(host).pin_memory().to(dev, non_blocking=True) if dev.type == "cuda" else \
+        torch.from_numpy(host)
+    o_gext = gpre.size
+    o_pc = o_gext + gext.size
+    o_wi = o_pc + nP
+    o_im = o_wi + nW
+    base_ptr = buf.data_ptr()
+    out = torch.zeros(C, dtype=_I32, device=dev)
+    bm = None
+    if plan.passes.shape[0] > 1:
+        bm, _ = build_bitmaps(roff, ranks, src, ncols, int(used.size), buf[o_im:o_im + item_map.size],
+                              torch.from_numpy(used.astype(np.int32)).to(dev))
+    st = _stream(ranks)
+    bounds = list(plan.passes[:, 2].tolist()) + [int(ext_off[-1] - ext_off[0])]
+    nslabs = (W + sw - 1) // sw
+    for q, (w0, w1, e0) in enumerate(plan.passes.tolist()):
+        Cq = bounds[q + 1] - e0
+        lds = used.size * sw * 8 + Cq * 4
+        per_cu = max(1, _LDS_BYTES // max(lds, 1))
+        n_wg = int(max(1, min(nslabs, 256 * min(per_cu, 2))))
+        _hip_call("fa_hip_count_trie", _p(roff), _p(ranks), _p(src), ncols, base_ptr + 4 * o_im, int(used.size),
+                  base_ptr, m, plan.d1, plan.d2, base_ptr + 4 * o_pc, base_ptr + 4 * (o_wi + 2 * w0),
+                  w1 - w0, base_ptr + 4 * (o_gext + e0), Cq, _p(wword), out.data_ptr() + 4 * e0, sw, n_wg,
+                  _p(bm), bm.stride(0) if bm is not None else 0, st)
+    res = out.to(_I64)
+    LAST_TRIE_PLAN.clear()
+    LAST_TRIE_PLAN.update(rows=int(roff.numel() - 1), used=int(used.size), sw=sw, cap=cap,
+                          passes=int(plan.passes.shape[0]), pieces=int(plan.pieces.shape[0]),
+                          witems=int(plan.witems.shape[0]), emax=emax, m=m, C=C, d1=plan.d1, d2=plan.d2,
+                          reads=plan.reads, reads_unshared=plan.reads_unshared)
+    del buf
+    return res
+
+
 def recommend(ante_off, ante, cons, F1: int, boff, bask) -> torch.Tensor:
     """First-match recommendation per basket -> int32 rank (or -1 for "0")."""
     M = boff.numel() - 1

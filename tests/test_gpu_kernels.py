@@ -135,6 +135,8 @@ def test_bitmaps_pairs_candidates(F1_frac):
     assert torch.equal(ref, got)
     slab = ops.count_level_slab(roff.to(DEV), ranks.to(DEV), None, T, F1, prev[pidx], eoff, ext, None)
     assert slab is not None and torch.equal(ref, slab.cpu())
+    trie = ops.count_level_trie(roff.to(DEV), ranks.to(DEV), None, T, F1, prev[pidx], eoff, ext, None)
+    assert trie is not None and torch.equal(ref, trie.cpu())
 
 
 def test_slab_many_passes_and_levels():
@@ -240,3 +242,34 @@ def test_trim_rows_matches_cpu(weighted):
             assert b is None
         else:
             assert torch.equal(a, b.cpu())
+
+
+@pytest.mark.parametrize("sw", ["8", "16", "32"])
+@pytest.mark.parametrize("lds_kb", [0, 24])
+def test_trie_kernel_widths_and_passes(monkeypatch, sw, lds_kb):
+    # every slab width, single- and multi-pass (bitmap tiles), unit and dedup weights:
+    # whole-miner results must equal the CPU reference through the deep levels
+    import fastapriori_amd.ops.primitives as prim
+    sh = generate_shard(30000, Comm(), "cpu", 14.0, 6.0, 200, 120, seed=17)
+    cfg = dict(min_support=0.004)
+    ref = FastApriori(0.004, config=MinerConfig(trim_min_rows=0, level_kernel="bitmap", dedup="off", **cfg)).run(sh)
+    assert len(ref.levels) >= 5
+    monkeypatch.setenv("FA_SLAB_SW", sw)
+    if lds_kb:
+        monkeypatch.setattr(prim, "_LDS_BYTES", lds_kb * 1024)
+    for dd in ("off", "on"):
+        got = FastApriori(0.004, config=MinerConfig(trim_min_rows=0, level_kernel="trie", dedup=dd, **cfg)).run(
+            sh.to(DEV))
+        assert ref.as_dict() == got.as_dict(), (sw, lds_kb, dd)
+        if lds_kb:
+            assert prim.LAST_TRIE_PLAN["passes"] >= 1
+
+
+def test_trie_kernel_small_work_items(monkeypatch):
+    import fastapriori_amd.ops.primitives as prim
+    sh = generate_shard(20000, Comm(), "cpu", 12.0, 5.0, 150, 100, seed=19)
+    ref = FastApriori(0.005, config=MinerConfig(min_support=0.005, trim_min_rows=0, level_kernel="bitmap")).run(sh)
+    monkeypatch.setattr(prim, "TRIE_EMAX", 1)
+    got = FastApriori(0.005, config=MinerConfig(min_support=0.005, trim_min_rows=0, level_kernel="trie")).run(
+        sh.to(DEV))
+    assert ref.as_dict() == got.as_dict()

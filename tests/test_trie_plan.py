@@ -1,0 +1,82 @@
+"""Planner of the trie-shared level kernel (csrc/host/plan.cpp), checked on CPU.
+
+ops.emulate_trie executes a plan with the kernel's exact semantics (P1/P2/p
+registers, piece flags, pass-local extension offsets) over a bool bitmap; its
+counts must equal brute-force support counts for every split depth, work-item
+size and accumulator capacity (many passes included).
+"""
+import numpy as np
+import pytest
+
+from fastapriori_amd import ops
+from fastapriori_amd.ops.host import apriori_gen, plan_trie
+
+
+def _level(rng, n_items=14, n_rows=400, k=4, dens=0.45):
+    bits = rng.random((n_items, n_rows)) < dens
+    # frequent (k-1)-itemsets of this bitmap at a low threshold -> realistic sharing
+    from itertools import combinations
+    m = k - 1
+    prev = []
+    for c in combinations(range(n_items), m):
+        if np.logical_and.reduce(bits[list(c)]).sum() >= 6:
+            prev.append(c)
+    return bits, np.array(prev, dtype=np.int32).reshape(-1, m)
+
+
+@pytest.mark.parametrize("k", [3, 4, 5])
+@pytest.mark.parametrize("emax,cap", [(24, 1 << 20), (3, 1 << 20), (5, 7), (1, 2)])
+@pytest.mark.parametrize("depths", [None, (0, 0), (1, 1), "max"])
+def test_plan_counts_match_brute_force(k, emax, cap, depths):
+    rng = np.random.default_rng(k * 7 + emax)
+    bits, prev = _level(rng, k=k)
+    pidx, eoff, ext = apriori_gen(prev)
+    if ext.size == 0:
+        pytest.skip("no candidates")
+    P = prev[pidx]
+    m = P.shape[1]
+    d1, d2 = (-1, -1) if depths is None else ((m - 1, m - 1) if depths == "max" else depths)
+    plan = plan_trie(P, eoff, emax, cap, d1, d2)
+    g_of_e = np.repeat(np.arange(pidx.size), np.diff(eoff))
+    want = np.array([np.logical_and.reduce(bits[list(P[g]) + [e]]).sum() for g, e in zip(g_of_e, ext)])
+    got = ops.emulate_trie(bits, P, ext, plan)
+    assert np.array_equal(got, want)
+    # structure: pieces cover every extension once; passes respect the capacity
+    cover = np.zeros(ext.size, np.int64)
+    for w0, w1, base in plan.passes.tolist():
+        for a, b in plan.witems[w0:w1]:
+            for off, e0, e1, f in plan.pieces[a:b]:
+                assert e1 - e0 <= emax
+                cover[base + e0:base + e1] += 1
+    assert np.all(cover == 1)
+    nxt = list(plan.passes[1:, 2]) + [ext.size]
+    assert all(b - a <= cap for a, b in zip(plan.passes[:, 2], nxt))
+    assert plan.reads <= plan.reads_unshared
+
+
+def test_weighted_emulation():
+    rng = np.random.default_rng(5)
+    bits, prev = _level(rng, k=3)
+    pidx, eoff, ext = apriori_gen(prev)
+    P = prev[pidx]
+    w = rng.integers(0, 4, bits.shape[1])
+    plan = plan_trie(P, eoff, 8, 1 << 20)
+    g_of_e = np.repeat(np.arange(pidx.size), np.diff(eoff))
+    want = np.array([(np.logical_and.reduce(bits[list(P[g]) + [e]]) * w).sum() for g, e in zip(g_of_e, ext)])
+    assert np.array_equal(ops.emulate_trie(bits, P, ext, plan, w), want)
+
+
+def test_sharing_reduces_reads_on_deep_levels():
+    # downward-closed deep level: every 6-subset of three overlapping 11-itemsets
+    from itertools import combinations
+    rng = np.random.default_rng(1)
+    core = rng.choice(30, 6, replace=False)
+    rows = set()
+    for _ in range(3):
+        big = np.sort(np.concatenate([core, rng.choice(np.setdiff1d(np.arange(30), core), 5, replace=False)]))
+        rows.update(combinations(big.tolist(), 6))
+    prev = np.array(sorted(rows), np.int32)
+    pidx, eoff, ext = apriori_gen(prev)
+    plan = plan_trie(prev[pidx], eoff, 24, 1 << 20)
+    assert ext.size > 100
+    assert plan.reads * 1.5 < plan.reads_unshared
