@@ -554,7 +554,7 @@ constexpr int kRowsWin = kRowsStage / 64;    // 12 windows
 
 __global__ __launch_bounds__(1024) void k_pair_rows16(
     const uint8_t* __restrict__ cnt, const int64_t* __restrict__ base, const uint8_t* __restrict__ lr,
-    int64_t T, int64_t nbatch, int32_t F1, int nb, int nbp, int64_t chunk_b, uint32_t* __restrict__ out) {
+    int64_t T, int64_t nbatch, int32_t F1, int nb, int nbp, int64_t chunk_b, uint32_t* __restrict__ out, int dbg) {
   __shared__ uint32_t tile[kPB16 * kPB16 / 2];
   __shared__ uint32_t sa[kPW][kRowsStage / 4];
   __shared__ uint32_t sb[kPW][kRowsStage / 4];
@@ -638,10 +638,11 @@ __global__ __launch_bounds__(1024) void k_pair_rows16(
         if (diag) j0 = p + 1;
         if (p < SA) {
           const int i = (int)A[p] * kPB16;
-          for (int j = j0; j < j1; ++j) {
-            const int idx = i + (int)B[j];
-            atomicAdd(&tile[idx >> 1], (idx & 1) ? 0x10000u : 1u);
-          }
+          if (!(dbg & 1))
+            for (int j = j0; j < j1; ++j) {
+              const int idx = i + (int)B[j];
+              atomicAdd(&tile[idx >> 1], (idx & 1) ? 0x10000u : 1u);
+            }
         }
       };
       int cs = 0;                                      // non-empty rows started before the window
@@ -671,7 +672,7 @@ __global__ __launch_bounds__(1024) void k_pair_rows16(
     for (int k = 0; k < kRowsDw; ++k) { da[k] = da_n[k]; db[k] = db_n[k]; }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < kPB16 * kPB16 / 2; i += blockDim.x) {
+  for (int i = threadIdx.x; i < ((dbg & 2) ? 0 : kPB16 * kPB16 / 2); i += blockDim.x) {
     const uint32_t v = tile[i];
     if (!v) continue;
     const int idx = 2 * i;
@@ -880,7 +881,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
     int64_t ncols, const int32_t* __restrict__ item_map, int n_used, const int32_t* __restrict__ gpre, int m,
     const int32_t* __restrict__ gext_off, const int32_t* __restrict__ gext, int G, int C,
     const int32_t* __restrict__ wword, uint32_t* __restrict__ out, const uint64_t* __restrict__ bm,
-    int64_t Wp, int dbg) {
+    int64_t Wp, int dbg, const int32_t* __restrict__ gpm) {
   extern __shared__ uint4 lds4[];                  // 16-B aligned base
   __shared__ unsigned long long build_words[kSlabThreads / 64 * 2];   // window_starts scratch
   constexpr int SWP = SW + 2;                       // row stride: 16-B aligned, odd number of 16-B slots
@@ -964,13 +965,15 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
     // a wave run loops of (nearly) equal length (FA_SLAB_DEBUG=2: no counting)
     for (int g = threadIdx.x; g < ((dbg & 2) ? 0 : G); g += blockDim.x) {
       uint4 p[SW / 2];
-      const int32_t* pr = gpre + (size_t)g * m;
+      // gpm: per-piece (prefix offset, length) when levels of different k share a launch
+      const int32_t* pr = gpm ? gpre + gpm[2 * g] : gpre + (size_t)g * m;
+      const int mg = gpm ? gpm[2 * g + 1] : m;
       {
         const uint4* r0 = lds4 + (size_t)pr[0] * (SWP / 2);
 #pragma unroll
         for (int q = 0; q < SW / 2; ++q) p[q] = r0[q];
       }
-      for (int j = 1; j < m; ++j) {
+      for (int j = 1; j < mg; ++j) {
         const uint4* rj = lds4 + (size_t)pr[j] * (SWP / 2);
 #pragma unroll
         for (int q = 0; q < SW / 2; ++q) {
@@ -1298,14 +1301,15 @@ FA_API int fa_hip_count_candidates(const uint64_t* bm, int64_t Wp, int64_t W, co
 FA_API int fa_hip_count_slab(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
                              const int32_t* item_map, int n_used, const int32_t* gpre, int m,
                              const int32_t* gext_off, const int32_t* gext, int G, int C, const int32_t* wword,
-                             uint32_t* out, int sw, int n_wg, const uint64_t* bm, int64_t Wp, hipStream_t st) {
+                             uint32_t* out, int sw, int n_wg, const uint64_t* bm, int64_t Wp, hipStream_t st,
+                             const int32_t* gpm) {
   if (G <= 0 || C <= 0 || ncols <= 0) return 0;
   const size_t lds = (size_t)n_used * (sw + 2) * 8 + (size_t)C * 4;
   if (lds > 160 * 1024 - 512) return 3;   // static build_words scratch
   dim3 g((unsigned)n_wg), b(kSlabThreads);
   using KernT = void (*)(const int64_t*, const int32_t*, const int32_t*, int64_t, const int32_t*, int,
                          const int32_t*, int, const int32_t*, const int32_t*, int, int, const int32_t*,
-                         uint32_t*, const uint64_t*, int64_t, int);
+                         uint32_t*, const uint64_t*, int64_t, int, const int32_t*);
   KernT kern = nullptr;
 #define FA_SLAB_MODE(S, B) kern = wword ? (KernT)k_count_slab<S, true, B> : (KernT)k_count_slab<S, false, B>;
 #define FA_SLAB_CASE(S)                                   \
@@ -1324,7 +1328,7 @@ FA_API int fa_hip_count_slab(const int64_t* roff, const int32_t* ranks, const in
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const int dbg = getenv("FA_SLAB_DEBUG") ? atoi(getenv("FA_SLAB_DEBUG")) : 0;
   hipLaunchKernelGGL(kern, g, b, lds, st, roff, ranks, src, ncols, item_map, n_used, gpre, m, gext_off, gext, G, C,
-                     wword, out, bm, Wp, dbg);
+                     wword, out, bm, Wp, dbg, gpm);
   FA_LAUNCH_RET();
 }
 
@@ -1430,6 +1434,6 @@ FA_API int fa_hip_pair_rows16(const uint8_t* cnt, const int64_t* base, const uin
   const int64_t chunk_b = 65535 / 64;   // 1023 batches = 65472 rows: 16-bit counters stay exact
   const int64_t nch = (nbatch + chunk_b - 1) / chunk_b;
   hipLaunchKernelGGL(k_pair_rows16, dim3((unsigned)(nch * nbp)), dim3(64 * kPW), 0, st, cnt, base, lr, T, nbatch,
-                     F1, nb, nbp, chunk_b, out);
+                     F1, nb, nbp, chunk_b, out, getenv("FA_PAIR_DEBUG") ? atoi(getenv("FA_PAIR_DEBUG")) : 0);
   FA_LAUNCH_RET();
 }

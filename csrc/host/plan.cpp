@@ -15,6 +15,8 @@
 //   passes      (consecutive work items whose extensions fit the LDS accumulator)
 // and sorts the work items of a pass by estimated cost so the lanes of a wave
 // run loops of similar length.
+#include <cstring>
+
 #include "fa_common.h"
 
 namespace fa {
@@ -148,5 +150,174 @@ FA_API int fa_plan_trie(const int32_t* P, int64_t G, int m, const int64_t* ext_o
   }
   info[0] = np; info[1] = nw; info[2] = npass; info[3] = d1; info[4] = d2;
   info[5] = reads; info[6] = reads_unshared; info[7] = 0;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// One-call level planner: everything the level kernels need, computed in C++
+// and written into one (pinned) int32 buffer so the driver issues a single
+// host->device copy per level.
+//
+//   params (double[8]): lds_bytes, min_saving (0 = always trie, >1 = never),
+//                       conflict16, conflict8, pass_weight, rounds, emax_max, W
+//   info (int64[24]) out:
+//     0 kernel (0 slab, 1 trie)  1 sw  2 cap  3 n_used  4 n_pieces  5 n_witems
+//     6 n_passes  7 d1  8 d2  9 trie reads  10 slab reads  11 emax
+//     12 off item_map  13 off used  14 off gext  15 off gpre  16 off pieces/loc_off
+//     17 off witems  18 total int32 written
+//   passes (int64[3 * maxpass]): slab: (piece begin, piece end, ext base);
+//                                trie: (witem begin, witem end, ext base)
+// Returns 0, 3 (buffer too small), 4 (no slab width fits: use the bitmap kernel).
+// ---------------------------------------------------------------------------
+static int slab_width(int64_t n_used, int64_t C, double lds, int64_t* cap_out) {
+  for (int sw : {32, 16, 8, 4}) {
+    const int64_t cap = (int64_t)((lds - (double)n_used * (sw + 2) * 8) / 4);
+    if (cap >= std::min<int64_t>(C, 8192) || (sw == 4 && cap >= 1024)) { *cap_out = cap; return sw; }
+  }
+  return 0;
+}
+
+FA_API int fa_level_plan(const int32_t* Pf, const int64_t* poff, int64_t G, const int64_t* ext_off,
+                         const int32_t* ext, int32_t F1, const double* params, int32_t* buf, int64_t buf_cap,
+                         int64_t* passes, int64_t max_pass, int64_t* info) {
+  const double lds = params[0], min_saving = params[1], conf16 = params[2], conf8 = params[3];
+  const double pass_w = params[4], rounds = params[5];
+  const int64_t emax_max = (int64_t)params[6];
+  const double W = params[7];
+  const int64_t C = ext_off[G] - ext_off[0];
+  for (int i = 0; i < 24; ++i) info[i] = 0;
+  if (G <= 0 || C <= 0) return 1;
+  // prefix lengths: uniform for one level, mixed when several levels share a launch
+  const int m0 = (int)(poff[1] - poff[0]);
+  bool uniform = true;
+  int64_t sum_m = 0;
+  for (int64_t g = 0; g < G; ++g) {
+    const int mg = (int)(poff[g + 1] - poff[g]);
+    uniform = uniform && mg == m0;
+    sum_m += mg;
+  }
+  // used items and the rank -> slab-row map
+  std::vector<uint8_t> mark((size_t)std::max(F1, 1), 0);
+  for (int64_t i = poff[0]; i < poff[G]; ++i) mark[Pf[i]] = 1;
+  for (int64_t e = 0; e < C; ++e) mark[ext[ext_off[0] + e]] = 1;
+  int64_t pos = 0;
+  auto need = [&](int64_t n) { return pos + n <= buf_cap; };
+  if (!need(2 * (int64_t)F1 + C)) return 3;
+  int32_t* item_map = buf + pos; info[12] = pos; pos += F1;
+  int32_t* used = buf + pos; info[13] = pos;
+  int64_t n_used = 0;
+  for (int32_t r = 0; r < F1; ++r) {
+    if (mark[r]) { item_map[r] = (int32_t)n_used; used[n_used++] = r; } else item_map[r] = -1;
+  }
+  pos += n_used;
+  int32_t* gext = buf + pos; info[14] = pos; pos += C;
+  for (int64_t e = 0; e < C; ++e) gext[e] = item_map[ext[ext_off[0] + e]];
+  info[3] = n_used;
+
+  // slab-kernel reads: pieces of <= 8 extensions, each ANDs its whole prefix
+  int64_t pieces8 = 0, slab_reads = C;
+  for (int64_t g = 0; g < G; ++g) {
+    const int64_t np = std::max<int64_t>(1, (ext_off[g + 1] - ext_off[g] + 7) / 8);
+    pieces8 += np;
+    slab_reads += np * (poff[g + 1] - poff[g]);
+  }
+  info[10] = slab_reads;
+
+  // ---- trie kernel (one level: uniform prefix length): slab width by the time model, then the plan
+  if (uniform && min_saving <= 1.0) {
+    const int m = m0;
+    const int32_t* P = Pf + poff[0];
+    int best_sw = 0;
+    int64_t best_cap = 0;
+    double best_t = 0;
+    const double reads_est = (double)C + 0.5 * (double)G * m;
+    for (int sw : {32, 16, 8}) {
+      const int64_t cap = (int64_t)((lds - (double)n_used * sw * 8) / 4);
+      if (cap < std::min<int64_t>(C, 1024)) continue;
+      const int64_t passes_n = (C + cap - 1) / cap;
+      double t = reads_est * W * 8 * (sw == 32 ? 1.0 : sw == 16 ? conf16 : conf8) / 60e12;
+      if (passes_n > 1) t += pass_w * passes_n * (double)n_used * W * 8 / 5e12;
+      if (best_sw == 0 || t < best_t) { best_sw = sw; best_cap = cap; best_t = t; }
+    }
+    if (best_sw) {
+      const int64_t ngrp = 4096 / best_sw;
+      const int64_t emax = std::max<int64_t>(2, std::min<int64_t>(emax_max,
+                                             std::min<int64_t>(C, best_cap) / (int64_t)(rounds * ngrp)));
+      const int64_t maxp = G + C / emax + 2;
+      if (!need(G * m + 6 * maxp)) return 3;
+      int32_t* gpre = buf + pos;
+      const int64_t o_gpre = pos;
+      for (int64_t i = 0; i < G * m; ++i) gpre[i] = item_map[P[i]];
+      int32_t* pieces = buf + pos + G * m;
+      int32_t* witems = pieces + 4 * maxp;
+      std::vector<int64_t> pas(3 * (size_t)maxp);
+      int64_t tinfo[8];
+      const int rc = fa_plan_trie(P, G, m, ext_off, emax, best_cap, -1, -1, pieces, witems, pas.data(), maxp, tinfo);
+      if (rc != 0) return 10 + rc;
+      info[9] = tinfo[5];
+      if (min_saving <= 0.0 || (double)tinfo[5] <= min_saving * (double)slab_reads) {
+        if (tinfo[2] > max_pass) return 3;
+        const int64_t np = tinfo[0], nw = tinfo[1];
+        std::memmove(pieces + 4 * np, witems, sizeof(int32_t) * 2 * nw);
+        info[0] = 1; info[1] = best_sw; info[2] = best_cap; info[4] = np; info[5] = nw; info[6] = tinfo[2];
+        info[7] = tinfo[3]; info[8] = tinfo[4]; info[11] = emax;
+        info[15] = o_gpre; info[16] = o_gpre + G * m; info[17] = o_gpre + G * m + 4 * np;
+        pos = o_gpre + G * m + 4 * np + 2 * nw;
+        info[18] = pos;
+        for (int64_t q = 0; q < 3 * tinfo[2]; ++q) passes[q] = pas[q];
+        return 0;
+      }
+    }
+  }
+
+  // ---- slab kernel: pieces of <= 8 extensions, passes of <= cap, size-sorted per pass
+  int64_t cap = 0;
+  const int sw = slab_width(n_used, C, lds, &cap);
+  if (sw == 0) return 4;
+  struct Piece { int64_t g, lo, hi; };
+  std::vector<Piece> pcs;
+  pcs.reserve((size_t)pieces8);
+  int64_t pre_total = 0;
+  for (int64_t g = 0; g < G; ++g) {
+    const int64_t a = ext_off[g] - ext_off[0], b = ext_off[g + 1] - ext_off[0];
+    const int64_t mg = poff[g + 1] - poff[g];
+    if (a == b) { pcs.push_back({g, a, a}); pre_total += mg; continue; }
+    for (int64_t x = a; x < b; x += 8) { pcs.push_back({g, x, std::min(b, x + 8)}); pre_total += mg; }
+  }
+  const int64_t NP = (int64_t)pcs.size();
+  if (!need(pre_total + 4 * NP)) return 3;
+  int32_t* gpre = buf + pos;
+  int32_t* loc = gpre + pre_total;
+  int32_t* gpm = loc + 2 * NP;
+  info[15] = pos; info[16] = pos + pre_total; info[19] = pos + pre_total + 2 * NP;
+  int64_t npass = 0, i = 0, wpos = 0;
+  std::vector<int64_t> ord;
+  while (i < NP) {
+    // a pass takes pieces while their extensions fit the accumulator
+    const int64_t base = pcs[i].lo;
+    int64_t j = i;
+    while (j < NP && pcs[j].hi - base <= cap) ++j;
+    if (j == i) j = i + 1;   // a single piece always fits (<= 8 extensions)
+    if (npass >= max_pass) return 3;
+    ord.resize((size_t)(j - i));
+    for (int64_t k = 0; k < j - i; ++k) ord[k] = i + k;
+    std::stable_sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) {
+      return pcs[a].hi - pcs[a].lo > pcs[b].hi - pcs[b].lo;
+    });
+    for (int64_t k = 0; k < j - i; ++k) {
+      const Piece& pc = pcs[ord[k]];
+      const int64_t mg = poff[pc.g + 1] - poff[pc.g];
+      gpm[2 * (i + k)] = (int32_t)wpos;
+      gpm[2 * (i + k) + 1] = (int32_t)mg;
+      for (int64_t t = 0; t < mg; ++t) gpre[wpos++] = item_map[Pf[poff[pc.g] + t]];
+      loc[2 * (i + k)] = (int32_t)(pc.lo - base);
+      loc[2 * (i + k) + 1] = (int32_t)(pc.hi - base);
+    }
+    passes[3 * npass] = i; passes[3 * npass + 1] = j; passes[3 * npass + 2] = base;
+    ++npass;
+    i = j;
+  }
+  info[0] = 0; info[1] = sw; info[2] = cap; info[4] = NP; info[6] = npass;
+  info[18] = pos + pre_total + 4 * NP;
   return 0;
 }

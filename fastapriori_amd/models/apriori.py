@@ -47,9 +47,10 @@ GRAM_WORDPAIRS_PER_S = 1.2e13
 # numeric vocabularies at least this wide count F1 with the sketch + exact pass
 F1_SKETCH_MIN_VOCAB = 1 << 20
 F1_MAX_CANDIDATES = ops.primitives.F1_MAX_CANDIDATES
-# auto level kernel: trie-shared counting when its slab-row reads are below this
-# fraction of the slab kernel's (measured break-even on T10I4 / T40I10, MI355X)
-TRIE_MIN_SAVING = float(os.environ.get("FA_TRIE_MIN_SAVING", "0.53"))
+# level bundling (FastApriori._plan_bundle)
+BUNDLE_LEVELS = os.environ.get("FA_BUNDLE", "1") == "1"
+BUNDLE_GROWTH = float(os.environ.get("FA_BUNDLE_GROWTH", "1.5"))
+BUNDLE_MAX_PREFIX = int(os.environ.get("FA_BUNDLE_MAX_PREFIX", "9"))
 
 
 @dataclass
@@ -152,29 +153,39 @@ class FastApriori:
                     levels.append(np.zeros((0, k), np.int32)); counts.append(np.zeros(0, np.int64))
                     self.log.line(f"{k} freq items 0")
                     break
+                # level bundling: count the next levels' candidates, generated from this
+                # level's candidates, in the same launch (see _plan_bundle)
+                with tm.phase("apriori_gen"):
+                    bundle = self._plan_bundle(db, k, levels[-1], prefix_idx, ext_off, ext)
+                used = np.unique(np.concatenate([np.concatenate([pv[pi].ravel(), ex]) for _, pv, pi, _, ex in bundle]))
                 with tm.phase(f"trim{k}"):
-                    self._trim(db, np.unique(np.concatenate([levels[-1][prefix_idx].ravel(), ext])), k)
+                    self._trim(db, used, k)
                 with tm.phase("count"):
-                    self._level_kernel_used = "slab"
-                    cnt = self._count_level(db, levels[-1], prefix_idx, ext_off, ext)
+                    cnts = self._count_bundle(db, bundle)
                 if tm.sync:
-                    plan = ops.primitives.LAST_TRIE_PLAN if getattr(self, "_level_kernel_used", "") == "trie" \
-                        else ops.primitives.LAST_SLAB_PLAN
-                    plan = dict(plan, kernel=getattr(self, "_level_kernel_used", "slab"))
-                    self.stats.setdefault("level_info", {})[k] = dict(plan, groups=int(prefix_idx.size))
-                keep = cnt >= mc
-                g_of_e = np.repeat(np.arange(prefix_idx.size), np.diff(ext_off))
-                rows = np.concatenate([levels[-1][prefix_idx[g_of_e[keep]]], ext[keep, None]], axis=1)
-                levels.append(np.ascontiguousarray(rows, dtype=np.int32))
-                counts.append(cnt[keep].astype(np.int64))
+                    self.stats.setdefault("level_info", {})[k] = dict(ops.primitives.LAST_LEVEL_PLAN,
+                                                                      groups=int(prefix_idx.size),
+                                                                      bundled=len(bundle))
+                for (kk, pv, pi, eo, ex), cnt in zip(bundle, cnts):
+                    keep = cnt >= mc
+                    g_of_e = np.repeat(np.arange(pi.size), np.diff(eo))
+                    rows = np.concatenate([pv[pi[g_of_e[keep]]], ex[keep, None]], axis=1)
+                    levels.append(np.ascontiguousarray(rows, dtype=np.int32))
+                    counts.append(cnt[keep].astype(np.int64))
             ms = (time.perf_counter() - t0) * 1e3
-            self.log.line(f"{k} freq items {len(levels[-1])}")
-            self.log.line(f"Use Time {k} items {int(ms)}")
-            self.log.metric(phase="level", k=k, candidates=C, frequent=len(levels[-1]), ms=ms,
-                            groups=int(prefix_idx.size))
-            if self.ckpt is not None:
-                self.ckpt.save_level(result, k)
-            k += 1
+            for j, (kk, pv, pi, eo, ex) in enumerate(bundle):
+                Fk = levels[kk - 1]
+                if kk > k and self.log.enabled:
+                    # the reference logs the candidates generated from F_{k-1}; a bundled
+                    # level counted a superset generated from C_{k-1}
+                    self.log.line(f"{kk} candidate items {int(apriori_gen(levels[kk - 2])[2].size)}")
+                self.log.line(f"{kk} freq items {len(Fk)}")
+                self.log.line(f"Use Time {kk} items {int(ms) if j == 0 else 0}")
+                self.log.metric(phase="level", k=kk, candidates=int(ex.size), frequent=len(Fk),
+                                ms=ms if j == 0 else 0.0, groups=int(pi.size), bundled_with=k)
+                if self.ckpt is not None:
+                    self.ckpt.save_level(result, kk)
+            k += len(bundle)
         # drop a trailing empty level (the reference never emits empty levels)
         while len(levels) > 1 and len(levels[-1]) == 0:
             levels.pop(); counts.pop()
@@ -489,6 +500,69 @@ class FastApriori:
     # ------------------------------------------------------------------
     # k >= 3 (FastApriori.scala:132-160)
     # ------------------------------------------------------------------
+    def _plan_bundle(self, db, k: int, prev: np.ndarray, prefix_idx, ext_off, ext) -> list:
+        """Levels counted in one launch, starting with level k.
+
+        Level k+1's candidates are generated from level k's *candidates* (not
+        its frequent sets): a superset of apriori_gen(F_k) with exact counts, so
+        thresholding it yields exactly F_{k+1} (every frequent (k+1)-itemset has
+        frequent, hence candidate, k-subsets).  On T10I4 data these supersets are
+        within 2-20 % of the real candidate sets, and one slab build + one launch
+        replaces several.  Levels are added while the total fits one LDS
+        accumulator pass, a level does not grow past BUNDLE_GROWTH x the previous
+        one, and prefixes stay short (deep levels prefer the trie kernel).
+        Returns [(k, prefix rows source, prefix_idx, ext_off, ext), ...]."""
+        bundle = [(k, prev, prefix_idx, ext_off, ext)]
+        if (not BUNDLE_LEVELS or self.cand_par or self.cfg.level_kernel not in ("auto", "slab")
+                or k - 1 > BUNDLE_MAX_PREFIX):
+            return bundle
+        C = int(ext.size)
+        items = np.zeros(db["F1"], dtype=bool)
+        items[prev[prefix_idx].ravel()] = True
+        items[ext] = True
+        total = C
+        if total > ops.primitives.slab_capacity(int(items.sum()), total):
+            return bundle
+        g_of_e = np.repeat(np.arange(prefix_idx.size), np.diff(ext_off))
+        cand = np.ascontiguousarray(np.concatenate([prev[prefix_idx[g_of_e]], ext[:, None]], axis=1), np.int32)
+        last = C
+        kk = k
+        while self.cfg.max_level == 0 or kk + 1 <= self.cfg.max_level:
+            pi, eo, ex = apriori_gen(cand)
+            C2 = int(ex.size)
+            if C2 == 0 or C2 > BUNDLE_GROWTH * last:
+                break
+            it2 = items.copy()
+            it2[cand[pi].ravel()] = True
+            it2[ex] = True
+            if total + C2 > ops.primitives.slab_capacity(int(it2.sum()), total + C2):
+                break
+            kk += 1
+            bundle.append((kk, cand, pi, eo, ex))
+            items, total, last = it2, total + C2, C2
+            g2 = np.repeat(np.arange(pi.size), np.diff(eo))
+            cand = np.ascontiguousarray(np.concatenate([cand[pi[g2]], ex[:, None]], axis=1), np.int32)
+        return bundle
+
+    def _count_bundle(self, db, bundle: list) -> list:
+        """Counts of every level of a bundle (one launch on the GPU)."""
+        if len(bundle) == 1 or db["ranks"].device.type != "cuda":
+            return [self._count_level(db, pv, pi, eo, ex) for _, pv, pi, eo, ex in bundle]
+        pre = [pv[pi] for _, pv, pi, _, _ in bundle]
+        poff = np.concatenate([[0], np.cumsum(np.concatenate([np.full(p.shape[0], p.shape[1]) for p in pre]))])
+        flat = np.concatenate([p.ravel() for p in pre]).astype(np.int32)
+        sizes = [int(ex.size) for *_, ex in bundle]
+        eoff = np.concatenate([[0], np.cumsum(np.concatenate([np.diff(eo) for _, _, _, eo, _ in bundle]))])
+        ext = np.concatenate([ex for *_, ex in bundle]).astype(np.int32)
+        cnt = ops.count_level(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"], flat, eoff, ext,
+                              db["wword"], kernel="slab", poff=poff)
+        if cnt is None:
+            return [self._count_level(db, pv, pi, eo, ex) for _, pv, pi, eo, ex in bundle]
+        self.dcomm.all_reduce_(cnt)
+        c = cnt.cpu().numpy()
+        return np.split(c, np.cumsum(sizes)[:-1])
+
+
     def _count_level(self, db, prev: np.ndarray, prefix_idx, ext_off, ext) -> np.ndarray:
         if self.cand_par:
             # candidate parallelism: this rank counts a contiguous, extension-balanced
@@ -513,19 +587,9 @@ class FastApriori:
         the row shards in count parallelism (a no-op collective in candidate mode)."""
         dev = db["ranks"].device
         lk = self.cfg.level_kernel
-        if dev.type == "cuda" and lk in ("auto", "trie"):
-            # auto: the trie kernel where prefix sharing removes enough slab reads
-            # (deep levels); the thread-per-group slab kernel is faster per read
-            cnt = ops.count_level_trie(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"],
-                                       prev[prefix_idx], ext_off, ext, db["wword"],
-                                       min_saving=TRIE_MIN_SAVING if lk == "auto" else 0.0)
-            if cnt is not None:
-                self._level_kernel_used = "trie"
-                self.dcomm.all_reduce_(cnt)
-                return cnt.cpu().numpy()
-        if dev.type == "cuda" and lk in ("auto", "slab"):
-            cnt = ops.count_level_slab(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"],
-                                       prev[prefix_idx], ext_off, ext, db["wword"])
+        if dev.type == "cuda" and lk in ("auto", "trie", "slab"):
+            cnt = ops.count_level(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"], prev[prefix_idx],
+                                  ext_off, ext, db["wword"], kernel=lk)
             if cnt is not None:
                 self.dcomm.all_reduce_(cnt)
                 return cnt.cpu().numpy()

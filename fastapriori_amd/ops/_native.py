@@ -38,6 +38,7 @@ _HOST_SIGS = {
     "fa_apriori_gen": (vp, [vp, i64, C.c_int, C.c_int, vp]),
     "fa_cands_export": (None, [vp, vp, vp, vp]),
     "fa_cands_free": (None, [vp]),
+    "fa_level_plan": (C.c_int, [vp, vp, i64, vp, vp, i32, vp, vp, i64, vp, i64, vp]),
     "fa_plan_trie": (C.c_int, [vp, i64, C.c_int, vp, i64, i64, C.c_int, C.c_int, vp, vp, vp, i64, vp]),
     "fa_rules_build": (vp, [vp, vp, vp, C.c_int, vp, C.c_int, vp]),
     "fa_rules_nante": (i64, [vp]),
@@ -66,7 +67,7 @@ _HIP_SIGS = {
     "fa_hip_count_trie": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, vp, C.c_int, C.c_int, C.c_int, vp, vp,
                                     C.c_int, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, i64, vp]),
     "fa_hip_count_slab": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, vp,
-                                    C.c_int, C.c_int, vp, i64, vp]),
+                                    C.c_int, C.c_int, vp, i64, vp, vp]),
     "fa_hip_trim_scan_count": (C.c_int, [vp, vp, i64, vp, C.c_int, C.c_int, vp, vp, vp, vp, vp]),
     "fa_hip_trim_emit": (C.c_int, [vp, vp, vp, C.c_int, i64, vp, vp, vp, vp, vp, vp, vp, vp]),
     "fa_hip_compress_wave": (C.c_int, [vp, vp, vp, vp, i64, vp, vp, vp, C.c_int, vp]),

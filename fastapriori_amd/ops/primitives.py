@@ -441,6 +441,16 @@ def slab_plan(n_used: int, C: int):
     return 0, 0
 
 
+def slab_capacity(n_used: int, C: int) -> int:
+    """Accumulator capacity (candidates per pass) of the slab kernel for n_used items
+    (csrc/host/plan.cpp slab_width); 0 when no width fits."""
+    for sw in (32, 16, 8, 4):
+        cap = int((_LDS_BYTES - n_used * (sw + 2) * 8) // 4)
+        if cap >= min(C, 8192) or (sw == 4 and cap >= 1024):
+            return cap
+    return 0
+
+
 LAST_SLAB_PLAN: dict = {}   # shape of the last count_level_slab call (diagnostics)
 
 
@@ -500,7 +510,7 @@ def count_level_slab(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, 
         n_wg = int(max(1, min(nslabs, 256 * min(per_cu, 2))))
         _hip_call("fa_hip_count_slab", _p(roff), _p(ranks), _p(src), ncols, _p(imap_t), int(used.size), _p(pre_t),
                   m, _p(loc_off), gext_t.data_ptr() + 4 * e0, g1 - g0, e1 - e0, _p(wword),
-                  out.data_ptr() + 4 * e0, sw, n_wg, _p(bm), bm.stride(0) if bm is not None else 0, st)
+                  out.data_ptr() + 4 * e0, sw, n_wg, _p(bm), bm.stride(0) if bm is not None else 0, st, None)
     res = out.to(_I64)
     del keep
     LAST_SLAB_PLAN.clear()
@@ -518,6 +528,9 @@ _TRIE_CONFLICT = {32: 1.0, 16: 1.6, 8: 2.2}
 TRIE_EMAX = int(os.environ.get("FA_TRIE_EMAX", "24"))     # max extensions per work item
 TRIE_ROUNDS = int(os.environ.get("FA_TRIE_ROUNDS", "4"))   # work items per lane group and pass (target)
 TRIE_PASS_WEIGHT = float(os.environ.get("FA_TRIE_PASS_WEIGHT", "4"))
+# auto level kernel: trie-shared counting when its slab-row reads are below this
+# fraction of the slab kernel's (measured break-even on T10I4 / T40I10, MI355X)
+_TRIE_MIN_SAVING = float(os.environ.get("FA_TRIE_MIN_SAVING", "0.53"))
 
 
 def trie_slab_plan(n_used: int, C: int, W: int, reads_est: float) -> tuple[int, int]:
@@ -641,6 +654,143 @@ def count_level_trie(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, 
                           reads=plan.reads, reads_unshared=plan.reads_unshared)
     del buf
     return res
+
+
+def level_plan_host(prefix: np.ndarray, ext_off: np.ndarray, ext: np.ndarray, F1: int, W: int,
+                    kernel: str = "auto", lds_bytes: int | None = None, poff: np.ndarray | None = None):
+    """fa_level_plan on host arrays (tests / diagnostics): (rc, info, passes, buf)."""
+    P, po, G, m = _flat_prefix(prefix, poff)
+    C = int(ext.size)
+    eo = np.ascontiguousarray(ext_off, dtype=np.int64)
+    ex = np.ascontiguousarray(ext, dtype=np.int32)
+    min_saving = {"auto": _TRIE_MIN_SAVING, "trie": 0.0, "slab": 2.0}[kernel]
+    params = np.array([lds_bytes or _LDS_BYTES, min_saving, _TRIE_CONFLICT[16], _TRIE_CONFLICT[8],
+                       TRIE_PASS_WEIGHT, TRIE_ROUNDS, TRIE_EMAX, W], dtype=np.float64)
+    bound = 2 * F1 + C + G * m + 6 * (G + C // 2 + 2) + (m + 4) * (G + C // 8 + 1) + 16
+    buf = np.zeros(bound, np.int32)
+    passes = np.zeros((G + C + 2, 3), np.int64)
+    info = np.zeros(24, np.int64)
+    rc = _native.host().fa_level_plan(P.ctypes.data, po.ctypes.data, G, eo.ctypes.data, ex.ctypes.data, F1,
+                                      params.ctypes.data, buf.ctypes.data, bound, passes.ctypes.data,
+                                      passes.shape[0], info.ctypes.data)
+    return rc, info, passes[:int(info[6])], buf[:int(info[18])]
+
+
+def emulate_level_plan(bits_by_rank: np.ndarray, info, passes, buf, m: int, C: int) -> np.ndarray:
+    """CPU model of both level kernels over the plan written by fa_level_plan;
+    bits_by_rank: bool [F1, ncols]."""
+    n_used = int(info[3])
+    used = buf[info[13]:info[13] + n_used]
+    bits = bits_by_rank[used]
+    gext = buf[info[14]:info[14] + C]
+    out = np.zeros(C, np.int64)
+    if info[0] == 1:
+        class _Plan:
+            pass
+        pl = _Plan()
+        npc, nw = int(info[4]), int(info[5])
+        pl.pieces = buf[info[16]:info[16] + 4 * npc].reshape(-1, 4)
+        pl.witems = buf[info[17]:info[17] + 2 * nw].reshape(-1, 2)
+        pl.passes = passes
+        pl.d1, pl.d2 = int(info[7]), int(info[8])
+        G = (int(info[16]) - int(info[15])) // m
+        gpre = buf[info[15]:info[15] + G * m].reshape(-1, m)
+        return emulate_trie(bits, gpre, gext, pl)
+    npc = int(info[4])
+    gpre = buf[info[15]:info[16]]
+    loc = buf[info[16]:info[16] + 2 * npc].reshape(-1, 2)
+    gpm = buf[info[19]:info[19] + 2 * npc].reshape(-1, 2)
+    for a, b, e0 in passes.tolist():
+        for pi in range(a, b):
+            p = np.logical_and.reduce(bits[gpre[gpm[pi, 0]:gpm[pi, 0] + gpm[pi, 1]]])
+            for e in range(loc[pi, 0], loc[pi, 1]):
+                out[e0 + e] += int((p & bits[gext[e0 + e]]).sum())
+    return out
+
+
+LAST_LEVEL_PLAN: dict = {}   # shape of the last count_level call (diagnostics)
+
+
+def _flat_prefix(prefix: np.ndarray, poff: np.ndarray | None):
+    if poff is None:
+        P = np.ascontiguousarray(prefix, dtype=np.int32)
+        G, m = P.shape
+        return P.reshape(-1), np.arange(G + 1, dtype=np.int64) * m, G, m
+    poff = np.ascontiguousarray(poff, dtype=np.int64)
+    G = poff.size - 1
+    return np.ascontiguousarray(prefix, dtype=np.int32).reshape(-1), poff, G, int(np.diff(poff).max(initial=0))
+
+
+def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_off: np.ndarray, ext: np.ndarray,
+                wword, kernel: str = "auto", poff: np.ndarray | None = None) -> torch.Tensor | None:
+    """Support counts of one level on the device: one native planning call
+    (csrc/host/plan.cpp fa_level_plan: used items, kernel choice, work items,
+    accumulator passes) into one pinned buffer, one host->device copy, then the
+    trie-shared (k_count_trie) or slab (k_count_slab) kernel per pass.
+
+    kernel: auto (trie where it saves enough slab-row reads) | trie | slab.
+    prefix: int32 [G, m], or (poff given) a flat int32 array with group g's
+    prefix at poff[g]:poff[g+1] — groups of several levels (k) in one launch.
+    Returns int64 counts [C] (ext order), or None when no LDS slab fits (the
+    caller then uses the bitmap kernel)."""
+    dev = ranks.device
+    C = int(ext.size)
+    if C == 0:
+        return torch.zeros(0, dtype=_I64, device=dev)
+    P, po, G, m = _flat_prefix(prefix, poff)
+    eo = np.ascontiguousarray(ext_off, dtype=np.int64)
+    ex = np.ascontiguousarray(ext, dtype=np.int32)
+    W = (ncols + 63) // 64
+    min_saving = {"auto": _TRIE_MIN_SAVING, "trie": 0.0, "slab": 2.0}[kernel]
+    params = np.array([_LDS_BYTES, min_saving, _TRIE_CONFLICT[16], _TRIE_CONFLICT[8], TRIE_PASS_WEIGHT,
+                       TRIE_ROUNDS, TRIE_EMAX, W], dtype=np.float64)
+    bound = 2 * F1 + C + G * m + 6 * (G + C // 2 + 2) + (m + 4) * (G + C // 8 + 1) + 16
+    on_gpu = dev.type == "cuda"
+    buf = torch.empty(bound, dtype=_I32, pin_memory=on_gpu)
+    max_pass = G + C + 2
+    passes = np.zeros((max_pass, 3), dtype=np.int64)
+    info = np.zeros(24, dtype=np.int64)
+    rc = _native.host().fa_level_plan(P.ctypes.data, po.ctypes.data, G, eo.ctypes.data, ex.ctypes.data, F1,
+                                      params.ctypes.data, buf.data_ptr(), bound, passes.ctypes.data, max_pass,
+                                      info.ctypes.data)
+    if rc == 4:
+        return None
+    if rc != 0:
+        raise RuntimeError(f"fa_level_plan failed ({rc})")
+    kern, sw, cap, n_used, npass = int(info[0]), int(info[1]), int(info[2]), int(info[3]), int(info[6])
+    total = int(info[18])
+    dbuf = buf[:total].to(dev, non_blocking=True)
+    base = dbuf.data_ptr()
+    passes = passes[:npass]
+    o_im, o_used, o_gext, o_gpre, o_pc, o_wi, o_gpm = (int(info[i]) for i in (12, 13, 14, 15, 16, 17, 19))
+    out = torch.zeros(C, dtype=_I32, device=dev)
+    bm = None
+    if npass > 1:
+        bm, _ = build_bitmaps(roff, ranks, src, ncols, n_used, dbuf[o_im:o_im + F1], dbuf[o_used:o_used + n_used])
+    st = _stream(ranks)
+    bounds = passes[:, 2].tolist() + [C]
+    nslabs = (W + sw - 1) // sw
+    for q, (a, b, e0) in enumerate(passes.tolist()):
+        Cq = bounds[q + 1] - e0
+        if kern == 1:
+            lds = n_used * sw * 8 + Cq * 4
+            n_wg = int(max(1, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2))))
+            _hip_call("fa_hip_count_trie", _p(roff), _p(ranks), _p(src), ncols, base + 4 * o_im, n_used,
+                      base + 4 * o_gpre, m, int(info[7]), int(info[8]), base + 4 * o_pc, base + 4 * (o_wi + 2 * a),
+                      b - a, base + 4 * (o_gext + e0), Cq, _p(wword), out.data_ptr() + 4 * e0, sw, n_wg, _p(bm),
+                      bm.stride(0) if bm is not None else 0, st)
+        else:
+            lds = n_used * (sw + 2) * 8 + Cq * 4
+            n_wg = int(max(1, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2))))
+            _hip_call("fa_hip_count_slab", _p(roff), _p(ranks), _p(src), ncols, base + 4 * o_im, n_used,
+                      base + 4 * o_gpre, m, base + 4 * (o_pc + 2 * a), base + 4 * (o_gext + e0), b - a, Cq,
+                      _p(wword), out.data_ptr() + 4 * e0, sw, n_wg, _p(bm), bm.stride(0) if bm is not None else 0,
+                      st, base + 4 * (o_gpm + 2 * a))
+    LAST_LEVEL_PLAN.clear()
+    LAST_LEVEL_PLAN.update(kernel="trie" if kern == 1 else "slab", rows=int(roff.numel() - 1), used=n_used, sw=sw,
+                           cap=cap, passes=npass, pieces=int(info[4]), witems=int(info[5]), d1=int(info[7]),
+                           d2=int(info[8]), trie_reads=int(info[9]), slab_reads=int(info[10]), m=m, C=C)
+    return out.to(_I64)
 
 
 def recommend(ante_off, ante, cons, F1: int, boff, bask) -> torch.Tensor:

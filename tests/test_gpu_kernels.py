@@ -273,3 +273,15 @@ def test_trie_kernel_small_work_items(monkeypatch):
     got = FastApriori(0.005, config=MinerConfig(min_support=0.005, trim_min_rows=0, level_kernel="trie")).run(
         sh.to(DEV))
     assert ref.as_dict() == got.as_dict()
+
+
+def test_bundled_levels_on_gpu(monkeypatch):
+    # several levels of different k counted in one slab launch (per-piece prefix lengths)
+    from fastapriori_amd.models import apriori as ap
+    sh = generate_shard(40000, Comm(), "cpu", 10.0, 4.0, 200, 100, seed=23)
+    ref = FastApriori(0.003, config=MinerConfig(min_support=0.003, level_kernel="bitmap")).run(sh)
+    got = FastApriori(0.003, config=MinerConfig(min_support=0.003)).run(sh.to(DEV))
+    assert ref.as_dict() == got.as_dict() and len(ref.levels) >= 5
+    monkeypatch.setattr(ap, "BUNDLE_LEVELS", False)
+    got2 = FastApriori(0.003, config=MinerConfig(min_support=0.003)).run(sh.to(DEV))
+    assert ref.as_dict() == got2.as_dict()

@@ -80,3 +80,78 @@ def test_sharing_reduces_reads_on_deep_levels():
     plan = plan_trie(prev[pidx], eoff, 24, 1 << 20)
     assert ext.size > 100
     assert plan.reads * 1.5 < plan.reads_unshared
+
+
+@pytest.mark.parametrize("kernel", ["slab", "trie", "auto"])
+@pytest.mark.parametrize("lds_kb", [160, 6, 3])
+@pytest.mark.parametrize("k", [3, 5])
+def test_level_plan_counts(kernel, lds_kb, k):
+    # fa_level_plan (one-call planner feeding the GPU level kernels) for both kernels,
+    # single- and multi-pass, must reproduce brute-force supports
+    from fastapriori_amd.ops.primitives import emulate_level_plan, level_plan_host
+    rng = np.random.default_rng(k)
+    bits, prev = _level(rng, n_items=16, k=k)
+    pidx, eoff, ext = apriori_gen(prev)
+    if ext.size == 0:
+        pytest.skip("no candidates")
+    P = prev[pidx]
+    rc, info, passes, buf = level_plan_host(P, eoff, ext, bits.shape[0], (bits.shape[1] + 63) // 64, kernel,
+                                            lds_bytes=lds_kb * 1024)
+    if rc == 4:                      # no slab fits this LDS budget: the caller uses the bitmap kernel
+        assert lds_kb < 8
+        return
+    assert rc == 0
+    if kernel != "auto" and lds_kb == 160:
+        assert info[0] == (1 if kernel == "trie" else 0)
+    assert info[6] >= 1 and (info[6] > 1) == (ext.size > info[2])
+    g_of_e = np.repeat(np.arange(pidx.size), np.diff(eoff))
+    want = np.array([np.logical_and.reduce(bits[list(P[g]) + [e]]).sum() for g, e in zip(g_of_e, ext)])
+    got = emulate_level_plan(bits, info, passes, buf, P.shape[1], ext.size)
+    assert np.array_equal(got, want)
+
+
+def test_level_plan_mixed_prefix_lengths():
+    # groups of several levels (different k) in one slab launch: flat prefixes + poff
+    from fastapriori_amd.ops.primitives import emulate_level_plan, level_plan_host
+    rng = np.random.default_rng(11)
+    bits, prev3 = _level(rng, n_items=16, k=4)
+    _, prev2 = _level(rng, n_items=16, k=3)
+    groups = []
+    for prev in (prev2, prev3):
+        pidx, eoff, ext = apriori_gen(prev)
+        groups.append((prev[pidx], eoff, ext))
+    flat = np.concatenate([g[0].ravel() for g in groups]).astype(np.int32)
+    poff = np.concatenate([[0], np.cumsum(np.concatenate([np.full(g[0].shape[0], g[0].shape[1]) for g in groups]))])
+    eoff = np.concatenate([[0], np.cumsum(np.concatenate([np.diff(g[1]) for g in groups]))])
+    ext = np.concatenate([g[2] for g in groups]).astype(np.int32)
+    rc, info, passes, buf = level_plan_host(flat, eoff, ext, bits.shape[0], 8, "auto", poff=poff)
+    assert rc == 0 and info[0] == 0          # mixed lengths always take the slab kernel
+    want = []
+    for P, eo, ex in groups:
+        g_of_e = np.repeat(np.arange(P.shape[0]), np.diff(eo))
+        want += [np.logical_and.reduce(bits[list(P[g]) + [e]]).sum() for g, e in zip(g_of_e, ex)]
+    got = emulate_level_plan(bits, info, passes, buf, 0, ext.size)
+    assert np.array_equal(got, np.array(want))
+
+
+def test_bundled_levels_match_unbundled(monkeypatch):
+    # counting later levels from the previous level's candidates must not change results
+    import torch
+    from fastapriori_amd.models import apriori as ap
+    from fastapriori_amd.models.apriori import FastApriori, MinerConfig
+    from fastapriori_amd.parallel.comm import Comm
+    from fastapriori_amd.utils.io import generate_shard
+    sh = generate_shard(20000, Comm(), torch.device("cpu"), 10.0, 4.0, 200, 100, seed=3)
+    seen = []
+    orig = FastApriori._plan_bundle
+
+    def spy(self, *a):
+        b = orig(self, *a)
+        seen.append(len(b))
+        return b
+    monkeypatch.setattr(FastApriori, "_plan_bundle", spy)
+    on = FastApriori(0.003, config=MinerConfig(min_support=0.003)).run(sh)
+    assert max(seen) > 1 and len(on.levels) >= 5
+    monkeypatch.setattr(ap, "BUNDLE_LEVELS", False)
+    off = FastApriori(0.003, config=MinerConfig(min_support=0.003)).run(sh)
+    assert on.as_dict() == off.as_dict() and on.items == off.items
