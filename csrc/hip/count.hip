@@ -636,13 +636,12 @@ __global__ __launch_bounds__(1024) void k_pair_rows16(
         int j0 = __shfl(jbeg, row, 64);
         const int j1 = __shfl(jend, row, 64);
         if (diag) j0 = p + 1;
-        if (p < SA) {
+        if (p < SA && !(dbg & 1)) {
           const int i = (int)A[p] * kPB16;
-          if (!(dbg & 1))
-            for (int j = j0; j < j1; ++j) {
-              const int idx = i + (int)B[j];
-              atomicAdd(&tile[idx >> 1], (idx & 1) ? 0x10000u : 1u);
-            }
+          for (int j = j0; j < j1; ++j) {
+            const int idx = i + (int)B[j];
+            atomicAdd(&tile[idx >> 1], (idx & 1) ? 0x10000u : 1u);
+          }
         }
       };
       int cs = 0;                                      // non-empty rows started before the window

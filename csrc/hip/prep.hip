@@ -589,6 +589,174 @@ __global__ __launch_bounds__(256) void k_trim_emit(const int64_t* __restrict__ r
     atomicAdd((unsigned long long*)&hist[(blockIdx.x & 63) * kTrimHist + threadIdx.x], (unsigned long long)hs[threadIdx.x]);
 }
 
+
+// ---------------------------------------------------------------------------
+// Two-pass fused compression (short rows).  Replaces per-row counts + a
+// 100M-entry nonzero/cumsum in torch: each workgroup owns 256 consecutive
+// input rows (one contiguous CSR span, loaded coalesced into LDS and mapped
+// through the LUT once per pass).
+//   pass 1 (k_cmp_agg):  per-workgroup (kept rows, kept items) + the kept-row
+//                        length histogram (clamped to 255);
+//   host:                exclusive scan of the 2 x nWG aggregates;
+//   pass 2 (k_cmp_emit): block scans give every kept row its index and output
+//                        offset; writes kept[], roff[], and the sorted ranks of
+//                        rows <= 16 tokens (register bitonic network), staged
+//                        through LDS for coalesced stores; longer rows are
+//                        appended to an overflow list for the next tiers.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void cmp_block_scan2(int a, int b, int& ea, int& eb, int& ta, int& tb, int* sh) {
+  // exclusive scans of a and b over the 256-thread workgroup (4 waves)
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int ia = wave_scan_incl_dpp(a), ib = wave_scan_incl_dpp(b);
+  if (lane == 63) { sh[w] = ia; sh[4 + w] = ib; }
+  __syncthreads();
+  int pa = 0, pb = 0;
+  for (int k = 0; k < w; ++k) { pa += sh[k]; pb += sh[4 + k]; }
+  ta = sh[0] + sh[1] + sh[2] + sh[3];
+  tb = sh[4] + sh[5] + sh[6] + sh[7];
+  ea = pa + ia - a;
+  eb = pb + ib - b;
+}
+
+// Loads the workgroup's span into LDS as mapped ranks (0xFFFFFFFF = not frequent).
+// 16 KB spans (4096 tokens per 256 rows: every T10I4 workgroup) keep 8
+// workgroups resident per CU, which hides the dependent offset -> token -> LUT
+// loads of these short-lived workgroups.
+constexpr int kCmpSpan = 4096;
+constexpr int kCmpPer = kCmpSpan / 256;
+__device__ __forceinline__ bool cmp_stage(uint32_t* buf, const int32_t* __restrict__ items,
+                                          const int32_t* __restrict__ lut, int64_t base, int64_t n_in) {
+  if (n_in > kCmpSpan) return false;
+  int32_t v[kCmpPer];
+#pragma unroll
+  for (int k = 0; k < kCmpPer; ++k) {
+    const int64_t i = threadIdx.x + k * 256;
+    v[k] = i < n_in ? items[base + i] : 0;
+  }
+#pragma unroll
+  for (int k = 0; k < kCmpPer; ++k) {
+    const int64_t i = threadIdx.x + k * 256;
+    if (i < n_in) v[k] = lut[v[k]];
+  }
+#pragma unroll
+  for (int k = 0; k < kCmpPer; ++k) {
+    const int64_t i = threadIdx.x + k * 256;
+    if (i < n_in) buf[i] = v[k] < 0 ? 0xFFFFFFFFu : (uint32_t)v[k];
+  }
+  return true;
+}
+
+constexpr int kCmpN = 16;          // rows of <= kCmpN tokens are sorted by k_cmp_emit
+constexpr int kCmpStripes = 64;    // histogram copies
+
+__global__ __launch_bounds__(256) void k_cmp_agg(const int64_t* __restrict__ off, const int32_t* __restrict__ items,
+                                                 const int32_t* __restrict__ lut, int64_t n,
+                                                 int32_t* __restrict__ agg, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t buf[kCmpSpan];
+  __shared__ uint32_t lh[256];
+  __shared__ int sh[8];
+  const int64_t r0 = (int64_t)blockIdx.x * 256, r1 = min(n, r0 + 256);
+  const int64_t r = r0 + threadIdx.x;
+  lh[threadIdx.x] = 0;
+  const int64_t base = off[r0], n_in = off[r1] - base;
+  const int64_t s = r < r1 ? off[r] : 0, e = r < r1 ? off[r + 1] : 0;
+  const bool staged = cmp_stage(buf, items, lut, base, n_in);
+  __syncthreads();
+  int c = 0;
+  for (int64_t i = s; i < e; ++i) {
+    const uint32_t v = staged ? buf[i - base] : (uint32_t)lut[items[i]];
+    c += v != 0xFFFFFFFFu;
+  }
+  const int kept = c >= 2;
+  int ea, eb, ta, tb;
+  cmp_block_scan2(kept, kept ? c : 0, ea, eb, ta, tb, sh);
+  if (kept) atomicAdd(&lh[min(c, 255)], 1u);
+  const unsigned long long ob = __ballot(kept && e - s > kCmpN);
+  __shared__ int ov_w[4];
+  if ((threadIdx.x & 63) == 0) ov_w[threadIdx.x >> 6] = __popcll(ob);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    agg[3 * blockIdx.x] = ta; agg[3 * blockIdx.x + 1] = tb;
+    agg[3 * blockIdx.x + 2] = ov_w[0] + ov_w[1] + ov_w[2] + ov_w[3];
+  }
+  // striped histogram copies: 390K workgroups adding into one 256-bin row would
+  // serialise on a few hot addresses (~10 distinct row lengths)
+  if (lh[threadIdx.x]) atomicAdd(&hist[(blockIdx.x & (kCmpStripes - 1)) * 256 + threadIdx.x], lh[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(256) void k_cmp_emit(const int64_t* __restrict__ off, const int32_t* __restrict__ items,
+                                                  const int32_t* __restrict__ lut, int64_t n,
+                                                  const int64_t* __restrict__ pre_rows,
+                                                  const int64_t* __restrict__ pre_items,
+                                                  const int64_t* __restrict__ pre_over,
+                                                  int32_t* __restrict__ kept_out, int64_t* __restrict__ roff,
+                                                  int32_t* __restrict__ ranks, int32_t* __restrict__ over) {
+  constexpr int N = kCmpN;
+  __shared__ uint32_t buf[kCmpSpan];
+  __shared__ int sh[8];
+  const int64_t r0 = (int64_t)blockIdx.x * 256, r1 = min(n, r0 + 256);
+  const int64_t r = r0 + threadIdx.x;
+  const int64_t base = off[r0], n_in = off[r1] - base;
+  const int64_t s = r < r1 ? off[r] : 0, e = r < r1 ? off[r + 1] : 0;
+  const int64_t xr0 = pre_rows[blockIdx.x], obase = pre_items[blockIdx.x];
+  const bool staged = cmp_stage(buf, items, lut, base, n_in);
+  __syncthreads();
+  const int64_t L = e - s;
+  uint32_t a[N];
+  int c = 0;
+  if (L <= N) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      uint32_t v = 0xFFFFFFFFu;
+      if (j < L) v = staged ? buf[s - base + j] : (uint32_t)lut[items[s + j]];
+      a[j] = v;
+      c += v != 0xFFFFFFFFu;
+    }
+  } else {
+    for (int64_t i = s; i < e; ++i) {
+      const uint32_t v = staged ? buf[i - base] : (uint32_t)lut[items[i]];
+      c += v != 0xFFFFFFFFu;
+    }
+  }
+  const int kept = c >= 2;
+  const int ov = kept && L > N;
+  int ea, eb, ta, tb;
+  cmp_block_scan2(kept, kept ? c : 0, ea, eb, ta, tb, sh);
+  // overflow rows go to their slot of the scanned per-workgroup counts (no atomics:
+  // a counter shared by every workgroup serialises), ballot ranks inside the waves
+  __shared__ int ov_w[4];
+  const int w = threadIdx.x >> 6;
+  const unsigned long long ob = __ballot(ov);
+  if ((threadIdx.x & 63) == 0) ov_w[w] = __popcll(ob);
+  __syncthreads();
+  const int64_t ov_base = pre_over[blockIdx.x];
+  const int64_t xk = xr0 + ea;
+  if (kept) {
+    kept_out[xk] = (int32_t)r;
+    roff[xk + 1] = obase + eb + c;
+    if (ov) {
+      int64_t before = ov_base;
+      for (int k = 0; k < w; ++k) before += ov_w[k];
+      over[before + __popcll(ob & (lanes_le_mask() >> 1))] = (int32_t)xk;
+    }
+  }
+  const bool mine = kept && L <= N;
+  if (mine) bitonic_regs<N>(a);
+  __syncthreads();   // everyone is done reading the input span
+  if (staged && tb <= kCmpSpan) {
+    if (mine) {
+#pragma unroll
+      for (int j = 0; j < N; ++j)
+        if (j < c) buf[eb + j] = a[j];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < tb; i += blockDim.x) ranks[obase + i] = (int32_t)buf[i];
+  } else if (mine) {
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+      if (j < c) ranks[obase + eb + j] = (int32_t)a[j];
+  }
+}
 }  // namespace fa
 
 using namespace fa;
@@ -760,5 +928,22 @@ FA_API int fa_hip_trim_emit(const int64_t* roff, const int32_t* ranks, const int
   else
     hipLaunchKernelGGL(k_trim_emit<false>, g, b, 0, st, roff, ranks, alive, F1, T, cnt, base_rows, base_nnz, nroff,
                        nranks, kept, hist);
+  FA_LAUNCH_RET();
+}
+
+// Two-pass fused compression: agg int32 [3 * nwg], hist u32 [64 * 256] striped copies (zeroed by the caller).
+FA_API int fa_hip_cmp_agg(const int64_t* off, const int32_t* items, const int32_t* lut, int64_t n, int32_t* agg,
+                          uint32_t* hist, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_cmp_agg, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, off, items, lut, n, agg, hist);
+  FA_LAUNCH_RET();
+}
+
+FA_API int fa_hip_cmp_emit(const int64_t* off, const int32_t* items, const int32_t* lut, int64_t n,
+                           const int64_t* pre_rows, const int64_t* pre_items, const int64_t* pre_over, int32_t* kept,
+                           int64_t* roff, int32_t* ranks, int32_t* over, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_cmp_emit, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, off, items, lut, n, pre_rows,
+                     pre_items, pre_over, kept, roff, ranks, over);
   FA_LAUNCH_RET();
 }

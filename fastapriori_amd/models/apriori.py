@@ -49,6 +49,7 @@ F1_SKETCH_MIN_VOCAB = 1 << 20
 F1_MAX_CANDIDATES = ops.primitives.F1_MAX_CANDIDATES
 # level bundling (FastApriori._plan_bundle)
 BUNDLE_LEVELS = os.environ.get("FA_BUNDLE", "1") == "1"
+FUSED_COMPRESS = os.environ.get("FA_FUSED_COMPRESS", "1") == "1"
 BUNDLE_GROWTH = float(os.environ.get("FA_BUNDLE_GROWTH", "1.5"))
 BUNDLE_MAX_PREFIX = int(os.environ.get("FA_BUNDLE_MAX_PREFIX", "9"))
 
@@ -305,18 +306,26 @@ class FastApriori:
     # ------------------------------------------------------------------
     def _compress(self, shard: TransactionShard, lut: torch.Tensor, F1: int) -> dict:
         dev = shard.items.device
-        cnt = ops.txn_freq_count(shard.offsets, shard.items, lut)
-        kept = torch.nonzero(cnt >= 2).flatten().to(torch.int32)
-        T = kept.numel()
-        roff = torch.zeros(T + 1, dtype=torch.int64, device=dev)
-        if T:
-            torch.cumsum(cnt[kept.to(torch.int64)].to(torch.int64), 0, out=roff[1:])
-        ranks = ops.compress(shard.offsets, shard.items, lut, kept, roff, F1)
+        n_rows = shard.offsets.numel() - 1
+        if (dev.type == "cuda" and n_rows > 0 and FUSED_COMPRESS
+                and shard.items.numel() <= ops.primitives.COMPRESS_WAVE_MEAN_LEN * n_rows):
+            # fused two-pass path: kept rows, offsets, sorted ranks and the length histogram
+            kept, roff, ranks, hist_t = ops.compress_rows(shard.offsets, shard.items, lut, F1)
+            T = kept.numel()
+            hist = hist_t.cpu().numpy()
+        else:
+            cnt = ops.txn_freq_count(shard.offsets, shard.items, lut)
+            kept = torch.nonzero(cnt >= 2).flatten().to(torch.int32)
+            T = kept.numel()
+            roff = torch.zeros(T + 1, dtype=torch.int64, device=dev)
+            if T:
+                torch.cumsum(cnt[kept.to(torch.int64)].to(torch.int64), 0, out=roff[1:])
+            ranks = ops.compress(shard.offsets, shard.items, lut, kept, roff, F1)
+            hist = ops.histogram(torch.clamp(cnt, max=255), 256).cpu().numpy() if cnt.numel() else np.zeros(256, np.int64)
         db = {"roff": roff, "ranks": ranks, "T": T, "src": None, "ncols": T, "wword": None, "wrow": None,
               "bm": None, "W": 0, "F1": F1, "alive": np.ones(F1, dtype=bool), "c1": self._counts1}
         # row-length histogram (lengths >= 255 share the last bin): drives the pair
         # cost model, the trimming model and the u8 per-block count guard
-        hist = ops.histogram(torch.clamp(cnt, max=255), 256).cpu().numpy() if cnt.numel() else np.zeros(256, np.int64)
         hist[:2] = 0                         # rows with < 2 frequent items are not kept
         L = np.arange(256, dtype=np.int64)
         db["pair_work"] = int((hist * (L * (L - 1) // 2)).sum())

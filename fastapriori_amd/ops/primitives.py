@@ -170,6 +170,53 @@ def compress(offsets, items, lut, kept, roff, F1: int | None = None) -> torch.Te
     return ranks[:nnz]
 
 
+def compress_rows(offsets, items, lut, F1: int):
+    """Fused two-pass compression (device, short rows; csrc/hip/prep.hip k_cmp_agg /
+    k_cmp_emit): returns (kept int32 [T], roff int64 [T+1], ranks int32 [nnz],
+    length histogram int64 [256]) with one host synchronisation.  Rows of more
+    than 16 tokens are finished by the register / wave tiers of ``compress``."""
+    dev = items.device
+    n = offsets.numel() - 1
+    nwg = (n + 255) // 256
+    st = _stream(items)
+    agg = torch.empty(3 * max(nwg, 1), dtype=_I32, device=dev)
+    hist = torch.zeros(64, 256, dtype=_I32, device=dev)
+    _hip_call("fa_hip_cmp_agg", _p(offsets), _p(items), _p(lut), n, _p(agg), _p(hist), st)
+    pre = torch.zeros(3, nwg + 1, dtype=_I64, device=dev)
+    a3 = agg.view(-1, 3).t().to(_I64).contiguous()
+    for q in range(3):   # 1-D scans (the batched innermost-dim scan is ~20x slower here)
+        torch.cumsum(a3[q], 0, out=pre[q, 1:])
+    kept = torch.empty(max(n, 1), dtype=_I32, device=dev)
+    roff = torch.empty(n + 1, dtype=_I64, device=dev)
+    roff[0] = 0
+    ranks = torch.empty(max(items.numel(), 1), dtype=_I32, device=dev)
+    over = torch.empty(max(n, 1), dtype=_I32, device=dev)
+    _hip_call("fa_hip_cmp_emit", _p(offsets), _p(items), _p(lut), n, _p(pre[0]), _p(pre[1]), _p(pre[2]), _p(kept),
+              _p(roff), _p(ranks), _p(over), st)
+    sizes = pre[:, -1].cpu().tolist()
+    T, nnz, no = int(sizes[0]), int(sizes[1]), int(sizes[2])
+    kept, roff, ranks = kept[:T], roff[:T + 1], ranks[:nnz]
+    if no:
+        over = over[:no]
+        flag2 = torch.empty(no, dtype=torch.int8, device=dev)
+        _hip_call("fa_hip_compress_regs", 64, _p(offsets), _p(items), _p(lut), _p(over), no, _p(kept), _p(roff),
+                  _p(ranks), _p(flag2), st)
+        over2 = over[torch.nonzero(flag2).flatten()].contiguous()
+        n2 = over2.numel()
+        if n2 and F1 <= COMPRESS_WAVE_MAX_F1:
+            _hip_call("fa_hip_compress_wave", _p(offsets), _p(items), _p(lut), _p(over2), n2, _p(kept), _p(roff),
+                      _p(ranks), F1, st)
+        elif n2:
+            over3 = torch.empty(n2, dtype=_I32, device=dev)
+            n_over3 = torch.zeros(1, dtype=_I32, device=dev)
+            _hip_call("fa_hip_compress_lds", _p(offsets), _p(items), _p(lut), _p(over2), n2, _p(kept), _p(roff),
+                      _p(ranks), _p(over3), _p(n_over3), st)
+            n3 = int(n_over3.item())
+            if n3:
+                _compress_torch(offsets, items, lut, kept, roff, ranks, over3[:n3])
+    return kept, roff, ranks, hist.sum(0, dtype=_I64)
+
+
 def _compress_torch(offsets, items, lut, kept, roff, ranks, rows):
     """Torch implementation: all rows vectorised (rows=None) or the listed rows."""
     if rows is not None:

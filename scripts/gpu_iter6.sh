@@ -1,0 +1,7 @@
+#!/bin/bash
+set -e
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -k "compress" > gpurun_out/iter_tests.log 2>&1
+timeout -k 10 200 python bench.py --steps 5 --warmup 1 > gpurun_out/it6_T10.json 2>/dev/null
+timeout -k 10 200 python bench.py --n-txn 12500000 --steps 10 --warmup 2 > gpurun_out/it6_12M.json 2>/dev/null
+TAG=T10c bash scripts/gpu_kt.sh

@@ -285,3 +285,16 @@ def test_bundled_levels_on_gpu(monkeypatch):
     monkeypatch.setattr(ap, "BUNDLE_LEVELS", False)
     got2 = FastApriori(0.003, config=MinerConfig(min_support=0.003)).run(sh.to(DEV))
     assert ref.as_dict() == got2.as_dict()
+
+
+@pytest.mark.parametrize("n,max_len,long_rows", [(5000, 25, 5), (70000, 14, 40), (3000, 60, 300)])
+def test_compress_rows_fused(n, max_len, long_rows):
+    # two-pass fused compression (kept rows, offsets, sorted ranks, length histogram) vs the CPU path;
+    # long rows go through the overflow tiers, wide spans through the unstaged path
+    off, items, lut, F1 = _prep(n=n, V=700, max_len=max_len, seed=n, long_rows=long_rows)
+    cnt, kept, roff = _compress_inputs(off, items, lut)
+    ref = ops.compress(off, items, lut, kept, roff)
+    gk, groff, granks, ghist = ops.compress_rows(off.to(DEV), items.to(DEV), lut.to(DEV), F1)
+    assert torch.equal(kept, gk.cpu()) and torch.equal(roff, groff.cpu()) and torch.equal(ref, granks.cpu())
+    h = torch.bincount(torch.clamp(cnt[cnt >= 2], max=255).long(), minlength=256)
+    assert torch.equal(h, ghist.cpu())
