@@ -1,0 +1,145 @@
+// Candidate generation (apriori-gen: join + full subset prune) on the GPU.
+//
+// Reference behaviour: FastApriori.scala:167-193 — for every frequent
+// (k-1)-itemset x the extensions are ranks y > max(x) such that (x - x_i) + y
+// is frequent for every x_i; groups with no extension are dropped.  Bitset
+// formulation (same as the host apriori_gen.cpp fast path): for every
+// (m-1)-prefix Q that starts a class of the sorted F_{k-1}, Ext(Q) = bitset of
+// the class's last items; then
+//     ext(x) = { y > x[m-1] } AND Ext(x[0..m-2]) AND  AND_{p < m-1} Ext(x - x[p]).
+// One wave per row, lane w owning bitset word w (ranks < 64 * 64 = 4096), so a
+// row's m-1 subset lookups are wave-uniform hash probes and its extensions come
+// out ascending from a popcount + DPP prefix scan over the lanes.
+#include "fa_hip.h"
+
+namespace fa {
+
+__device__ __forceinline__ uint64_t ag_mix(uint64_t x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
+  return x;
+}
+
+// hash of row r's items except position `skip` (skip = m-1: the row's (m-1)-prefix)
+__device__ __forceinline__ uint64_t ag_hash_drop(const int32_t* __restrict__ r, int m, int skip) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)(m - 1);
+  for (int q = 0; q < m; ++q)
+    if (q != skip) h = ag_mix(h ^ (uint32_t)r[q]);
+  return h;
+}
+
+// true when row a's first m-1 items equal row b's items except b[skip]
+__device__ __forceinline__ bool ag_eq_drop(const int32_t* __restrict__ a, const int32_t* __restrict__ b, int m,
+                                           int skip) {
+  for (int q = 0, t = 0; q < m; ++q) {
+    if (q == skip) continue;
+    if (a[t++] != b[q]) return false;
+  }
+  return true;
+}
+
+// insert the class starts: slot <- start row id (open addressing, linear probing)
+__global__ __launch_bounds__(256) void k_ag_insert(const int32_t* __restrict__ P, int64_t n, int m,
+                                                   int32_t* __restrict__ table, uint32_t mask) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t* r = P + i * m;
+  if (i > 0) {
+    const int32_t* pr = P + (i - 1) * m;
+    bool same = true;
+    for (int q = 0; q < m - 1; ++q) same = same && r[q] == pr[q];
+    if (same) return;                       // not a class start
+  }
+  uint32_t at = (uint32_t)ag_hash_drop(r, m, m - 1) & mask;
+  while (atomicCAS(&table[at], -1, (int32_t)i) != -1) at = (at + 1) & mask;
+}
+
+__device__ __forceinline__ int32_t ag_find(const int32_t* __restrict__ P, int m, const int32_t* __restrict__ table,
+                                           uint32_t mask, const int32_t* __restrict__ x, int skip) {
+  uint32_t at = (uint32_t)ag_hash_drop(x, m, skip) & mask;
+  for (;;) {
+    const int32_t s = table[at];
+    if (s < 0) return -1;
+    if (ag_eq_drop(P + (int64_t)s * m, x, m, skip)) return s;
+    at = (at + 1) & mask;
+  }
+}
+
+// Ext bitsets keyed by class start row: ext[s * nw + w]
+__global__ __launch_bounds__(256) void k_ag_ext(const int32_t* __restrict__ P, int64_t n, int m,
+                                                const int32_t* __restrict__ table, uint32_t mask, int nw,
+                                                unsigned long long* __restrict__ ext) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t* r = P + i * m;
+  const int32_t s = ag_find(P, m, table, mask, r, m - 1);
+  const int32_t y = r[m - 1];
+  atomicOr(&ext[(int64_t)s * nw + (y >> 6)], 1ull << (y & 63));
+}
+
+// pass 0: cnt[i] = number of extensions of row i;  pass 1: write them at off[i].
+template <bool kEmit>
+__global__ __launch_bounds__(256) void k_ag_rows(const int32_t* __restrict__ P, int64_t n, int m,
+                                                 const int32_t* __restrict__ table, uint32_t mask, int nw,
+                                                 const unsigned long long* __restrict__ ext,
+                                                 int32_t* __restrict__ cnt, const int64_t* __restrict__ off,
+                                                 int32_t* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nwave = (int64_t)gridDim.x * (blockDim.x / 64);
+  for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); i < n; i += nwave) {
+    const int32_t* x = P + i * m;
+    const int32_t last = x[m - 1];
+    // own class: Ext(x[0..m-2]) restricted to y > last
+    const int32_t s0 = ag_find(P, m, table, mask, x, m - 1);
+    unsigned long long a = 0;
+    if (lane < nw) {
+      a = ext[(int64_t)s0 * nw + lane];
+      const int lw = last >> 6;
+      if (lane < lw) a = 0;
+      else if (lane == lw) a &= (last & 63) == 63 ? 0ull : (~0ull << ((last & 63) + 1));
+    }
+    for (int p = 0; p < m - 1 && __ballot(a != 0) != 0ull; ++p) {
+      const int32_t sp = ag_find(P, m, table, mask, x, p);
+      if (sp < 0) { a = 0; break; }
+      if (lane < nw) a &= ext[(int64_t)sp * nw + lane];
+    }
+    const int c = __popcll(a);
+    if (!kEmit) {
+      const int tot = wave_last(wave_scan_incl_dpp(c));
+      if (lane == 0) cnt[i] = tot;
+    } else {
+      const int incl = wave_scan_incl_dpp(c);
+      int64_t o = off[i] + (incl - c);
+      for (unsigned long long v = a; v; v &= v - 1) out[o++] = lane * 64 + __builtin_ctzll(v);
+    }
+  }
+}
+
+}  // namespace fa
+
+using namespace fa;
+
+// Table: int32 [mask + 1] filled with -1 by the caller; ext: u64 [n * nw] zeroed.
+FA_API int fa_hip_ag_build(const int32_t* P, int64_t n, int m, int32_t* table, uint32_t mask, int nw, void* ext,
+                           hipStream_t st) {
+  if (n <= 0) return 0;
+  if (m < 2 || nw > 64) return 1;
+  dim3 g((unsigned)((n + 255) / 256));
+  hipLaunchKernelGGL(k_ag_insert, g, dim3(256), 0, st, P, n, m, table, mask);
+  hipLaunchKernelGGL(k_ag_ext, g, dim3(256), 0, st, P, n, m, table, mask, nw, (unsigned long long*)ext);
+  FA_LAUNCH_RET();
+}
+
+// emit = 0: cnt[n] = extensions per row;  emit = 1: out[off[i] ...] = row i's extensions.
+FA_API int fa_hip_ag_rows(const int32_t* P, int64_t n, int m, const int32_t* table, uint32_t mask, int nw,
+                          const void* ext, int32_t* cnt, const int64_t* off, int32_t* out, int emit, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (m < 2 || nw > 64) return 1;
+  const unsigned nwg = (unsigned)std::min<int64_t>((n + 3) / 4, 65536);
+  if (emit)
+    hipLaunchKernelGGL(k_ag_rows<true>, dim3(nwg), dim3(256), 0, st, P, n, m, table, mask, nw,
+                       (const unsigned long long*)ext, cnt, off, out);
+  else
+    hipLaunchKernelGGL(k_ag_rows<false>, dim3(nwg), dim3(256), 0, st, P, n, m, table, mask, nw,
+                       (const unsigned long long*)ext, cnt, off, out);
+  FA_LAUNCH_RET();
+}

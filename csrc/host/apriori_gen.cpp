@@ -163,7 +163,7 @@ static Cands* apriori_gen_bitset(const int32_t* prev, int64_t n, int m, int nthr
   const int64_t grain = 1024;
   const int64_t nblocks = (n + grain - 1) / grain;
   std::vector<Cands> parts(nblocks);
-  nthreads = std::max(1, std::min<int>(nthreads, (int)(n / 4096)));
+  nthreads = std::max(1, std::min<int>(nthreads, (int)(n / 1024)));
   parallel_for(nblocks, nthreads, 1, [&](int64_t b0, int64_t b1, int) {
     std::vector<uint64_t> acc((size_t)nw);
     std::vector<int32_t> key((size_t)std::max(1, m - 1));
@@ -226,7 +226,7 @@ FA_API Cands* fa_apriori_gen(const int32_t* prev, int64_t n, int m, int nthreads
   }
   auto* out = new Cands();
   // thread start-up costs ~50 us each: small levels run on the calling thread
-  nthreads = std::max(1, std::min<int>(nthreads, (int)(n / 4096)));
+  nthreads = std::max(1, std::min<int>(nthreads, (int)(n / 1024)));
   // class end for every row: first row index whose first m-1 ranks differ
   std::vector<int64_t> cls_end(n);
   std::vector<char> starts(n + 1, 1);

@@ -840,6 +840,38 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
     return out.to(_I64)
 
 
+AG_DEVICE_MAX_F1 = 4096   # bitset words per lane-wave: 64 x 64 bits
+
+
+def apriori_gen_device(prev: np.ndarray, F1: int, dev) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """apriori-gen on the GPU (csrc/hip/gen.hip): same output as ops.host.apriori_gen
+    (prefix_idx int32 [G], ext_off int64 [G+1], ext int32 [C]) with two host syncs."""
+    n, m = prev.shape
+    P = torch.from_numpy(np.ascontiguousarray(prev, dtype=np.int32)).to(dev, non_blocking=False)
+    cap = 16
+    while cap < 2 * n:
+        cap <<= 1
+    table = torch.full((cap,), -1, dtype=_I32, device=dev)
+    nw = (F1 + 63) // 64
+    ext = torch.zeros(n * nw, dtype=_I64, device=dev)
+    st = _stream(P)
+    _hip_call("fa_hip_ag_build", _p(P), n, m, _p(table), cap - 1, nw, _p(ext), st)
+    cnt = torch.empty(n, dtype=_I32, device=dev)
+    _hip_call("fa_hip_ag_rows", _p(P), n, m, _p(table), cap - 1, nw, _p(ext), _p(cnt), None, None, 0, st)
+    off = torch.zeros(n + 1, dtype=_I64, device=dev)
+    torch.cumsum(cnt, 0, out=off[1:])
+    C = int(off[-1].item())
+    out = torch.empty(max(C, 1), dtype=_I32, device=dev)
+    if C:
+        _hip_call("fa_hip_ag_rows", _p(P), n, m, _p(table), cap - 1, nw, _p(ext), None, _p(off), _p(out), 1, st)
+    both = torch.cat([cnt, out[:C]]).cpu().numpy()
+    cnt_h, ext_h = both[:n], both[n:]
+    prefix_idx = np.flatnonzero(cnt_h).astype(np.int32)
+    ext_off = np.zeros(prefix_idx.size + 1, dtype=np.int64)
+    np.cumsum(cnt_h[prefix_idx], out=ext_off[1:])
+    return prefix_idx, ext_off, ext_h.astype(np.int32, copy=False)
+
+
 def recommend(ante_off, ante, cons, F1: int, boff, bask) -> torch.Tensor:
     """First-match recommendation per basket -> int32 rank (or -1 for "0")."""
     M = boff.numel() - 1

@@ -298,3 +298,21 @@ def test_compress_rows_fused(n, max_len, long_rows):
     assert torch.equal(kept, gk.cpu()) and torch.equal(roff, groff.cpu()) and torch.equal(ref, granks.cpu())
     h = torch.bincount(torch.clamp(cnt[cnt >= 2], max=255).long(), minlength=256)
     assert torch.equal(h, ghist.cpu())
+
+
+@pytest.mark.parametrize("k", [3, 4, 6])
+def test_apriori_gen_device_matches_host(k):
+    # GPU bitset apriori-gen == host apriori-gen on real levels (and speculative candidate levels)
+    sh = generate_shard(30000, Comm(), "cpu", 12.0, 5.0, 150, 300, seed=29)
+    res = FastApriori(0.003, config=MinerConfig(min_support=0.003)).run(sh)
+    assert len(res.levels) >= k
+    prev = res.levels[k - 2]
+    want = apriori_gen(prev)
+    got = ops.apriori_gen_device(prev, len(res.items), DEV)
+    for a, b in zip(want, got):
+        assert np.array_equal(a, b)
+    pidx, eoff, ext = want
+    g = np.repeat(np.arange(pidx.size), np.diff(eoff))
+    cand = np.ascontiguousarray(np.concatenate([prev[pidx[g]], ext[:, None]], 1), np.int32)
+    for a, b in zip(apriori_gen(cand), ops.apriori_gen_device(cand, len(res.items), DEV)):
+        assert np.array_equal(a, b)
