@@ -50,6 +50,9 @@ F1_MAX_CANDIDATES = ops.primitives.F1_MAX_CANDIDATES
 # level bundling (FastApriori._plan_bundle)
 BUNDLE_LEVELS = os.environ.get("FA_BUNDLE", "1") == "1"
 FUSED_COMPRESS = os.environ.get("FA_FUSED_COMPRESS", "1") == "1"
+# short rows only: 256-row spans must fit the 4096-token LDS stage and most rows the
+# 16-token register sort (T40I10's 40-token rows are faster on the tiered path)
+FUSED_COMPRESS_MEAN_LEN = 12
 GEN_DEVICE = os.environ.get("FA_GEN_DEVICE", "1") == "1"
 GEN_DEVICE_MIN_ROWS = int(os.environ.get("FA_GEN_DEVICE_MIN_ROWS", "512"))
 BUNDLE_GROWTH = float(os.environ.get("FA_BUNDLE_GROWTH", "1.5"))
@@ -311,7 +314,7 @@ class FastApriori:
         dev = shard.items.device
         n_rows = shard.offsets.numel() - 1
         if (dev.type == "cuda" and n_rows > 0 and FUSED_COMPRESS
-                and shard.items.numel() <= ops.primitives.COMPRESS_WAVE_MEAN_LEN * n_rows):
+                and shard.items.numel() <= FUSED_COMPRESS_MEAN_LEN * n_rows):
             # fused two-pass path: kept rows, offsets, sorted ranks and the length histogram
             kept, roff, ranks, hist_t = ops.compress_rows(shard.offsets, shard.items, lut, F1)
             T = kept.numel()
