@@ -10,6 +10,8 @@
 // One wave per row, lane w owning bitset word w (ranks < 64 * 64 = 4096), so a
 // row's m-1 subset lookups are wave-uniform hash probes and its extensions come
 // out ascending from a popcount + DPP prefix scan over the lanes.
+#include <hipcub/hipcub.hpp>
+
 #include "fa_hip.h"
 
 namespace fa {
@@ -82,7 +84,7 @@ __global__ __launch_bounds__(256) void k_ag_rows(const int32_t* __restrict__ P, 
                                                  const int32_t* __restrict__ table, uint32_t mask, int nw,
                                                  const unsigned long long* __restrict__ ext,
                                                  int32_t* __restrict__ cnt, const int64_t* __restrict__ off,
-                                                 int32_t* __restrict__ out) {
+                                                 int32_t* __restrict__ out, int32_t* __restrict__ rows = nullptr) {
   const int lane = threadIdx.x & 63;
   const int64_t nwave = (int64_t)gridDim.x * (blockDim.x / 64);
   for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); i < n; i += nwave) {
@@ -109,7 +111,16 @@ __global__ __launch_bounds__(256) void k_ag_rows(const int32_t* __restrict__ P, 
     } else {
       const int incl = wave_scan_incl_dpp(c);
       int64_t o = off[i] + (incl - c);
-      for (unsigned long long v = a; v; v &= v - 1) out[o++] = lane * 64 + __builtin_ctzll(v);
+      for (unsigned long long v = a; v; v &= v - 1) {
+        const int32_t y = lane * 64 + __builtin_ctzll(v);
+        out[o] = y;
+        if (rows) {   // the full candidate row (x, y): the next speculative level's input
+          int32_t* r = rows + o * (m + 1);
+          for (int q = 0; q < m; ++q) r[q] = x[q];
+          r[m] = y;
+        }
+        ++o;
+      }
     }
   }
 }
@@ -141,5 +152,61 @@ FA_API int fa_hip_ag_rows(const int32_t* P, int64_t n, int m, const int32_t* tab
   else
     hipLaunchKernelGGL(k_ag_rows<false>, dim3(nwg), dim3(256), 0, st, P, n, m, table, mask, nw,
                        (const unsigned long long*)ext, cnt, off, out);
+  FA_LAUNCH_RET();
+}
+
+// One call: apriori-gen of P (device, [n][m], sorted) with every step on the
+// stream and two synchronisations, into the pinned host buffer
+//   host = cnt [n] | ext [C] | candidate rows [C][m+1].
+// ws: device workspace.  sizes[0] = C; on rc 5 / 6 sizes[1] = bytes of workspace /
+// int32 of host buffer needed (the caller grows its buffer and calls again).
+FA_API int fa_hip_ag_gen(const int32_t* P, int64_t n, int m, int F1, void* ws, int64_t ws_bytes, int32_t* host,
+                         int64_t host_cap, int64_t* sizes, hipStream_t st) {
+  sizes[0] = 0;
+  if (n <= 0) return 0;
+  if (m < 2 || F1 > 4096) return 1;
+  const int nw = (F1 + 63) / 64;
+  uint32_t cap = 16;
+  while (cap < 2 * (uint64_t)n) cap <<= 1;
+  auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
+  size_t cub_bytes = 0;
+  (void)hipcub::DeviceScan::InclusiveSum(nullptr, cub_bytes, (const int32_t*)nullptr, (int64_t*)nullptr, (int)n, st);
+  const int64_t fixed = al(4 * (int64_t)cap) + al(8 * n * nw) + al(4 * n) + al(8 * (n + 1)) + al((int64_t)cub_bytes);
+  if (fixed > ws_bytes) { sizes[1] = fixed; return 5; }
+  char* w = static_cast<char*>(ws);
+  int32_t* table = reinterpret_cast<int32_t*>(w); w += al(4 * (int64_t)cap);
+  unsigned long long* ext = reinterpret_cast<unsigned long long*>(w); w += al(8 * n * nw);
+  int32_t* cnt = reinterpret_cast<int32_t*>(w); w += al(4 * n);
+  int64_t* off = reinterpret_cast<int64_t*>(w); w += al(8 * (n + 1));
+  void* cub_tmp = w; w += al((int64_t)cub_bytes);
+  (void)hipMemsetAsync(table, 0xFF, 4 * (size_t)cap, st);
+  (void)hipMemsetAsync(ext, 0, 8 * (size_t)n * nw, st);
+  (void)hipMemsetAsync(off, 0, 8, st);
+  dim3 g((unsigned)((n + 255) / 256));
+  hipLaunchKernelGGL(k_ag_insert, g, dim3(256), 0, st, P, n, m, table, cap - 1);
+  hipLaunchKernelGGL(k_ag_ext, g, dim3(256), 0, st, P, n, m, table, cap - 1, nw, ext);
+  const unsigned nwg = (unsigned)std::min<int64_t>((n + 3) / 4, 65536);
+  hipLaunchKernelGGL(k_ag_rows<false>, dim3(nwg), dim3(256), 0, st, P, n, m, table, cap - 1, nw, ext, cnt, nullptr,
+                     nullptr, nullptr);
+  (void)hipcub::DeviceScan::InclusiveSum(cub_tmp, cub_bytes, cnt, off + 1, (int)n, st);
+  int64_t C = 0;
+  (void)hipMemcpyAsync(&C, off + n, 8, hipMemcpyDeviceToHost, st);
+  (void)hipStreamSynchronize(st);
+  const int64_t need_ws = fixed + al(4 * C) + al(4 * C * (m + 1));
+  if (need_ws > ws_bytes) { sizes[1] = need_ws; return 5; }
+  const int64_t need_host = n + C + C * (m + 1);
+  if (need_host > host_cap) { sizes[1] = need_host; return 6; }
+  int32_t* ext_out = reinterpret_cast<int32_t*>(w); w += al(4 * C);
+  int32_t* rows_out = reinterpret_cast<int32_t*>(w);
+  if (C)
+    hipLaunchKernelGGL(k_ag_rows<true>, dim3(nwg), dim3(256), 0, st, P, n, m, table, cap - 1, nw, ext, nullptr, off,
+                       ext_out, rows_out);
+  (void)hipMemcpyAsync(host, cnt, 4 * (size_t)n, hipMemcpyDeviceToHost, st);
+  if (C) {
+    (void)hipMemcpyAsync(host + n, ext_out, 4 * (size_t)C, hipMemcpyDeviceToHost, st);
+    (void)hipMemcpyAsync(host + n + C, rows_out, 4 * (size_t)C * (m + 1), hipMemcpyDeviceToHost, st);
+  }
+  (void)hipStreamSynchronize(st);
+  sizes[0] = C;
   FA_LAUNCH_RET();
 }

@@ -153,7 +153,7 @@ class FastApriori:
                 continue
             with roctx_range(f"level{k}"), tm.phase(f"level{k}"):
                 with tm.phase("apriori_gen"):
-                    prefix_idx, ext_off, ext = self._gen(levels[-1])
+                    prefix_idx, ext_off, ext, cand_rows = self._gen(levels[-1], want_rows=True)
                 C = int(ext.size)
                 self.log.line(f"{k} candidate items {C}")
                 if C == 0:
@@ -163,8 +163,12 @@ class FastApriori:
                 # level bundling: count the next levels' candidates, generated from this
                 # level's candidates, in the same launch (see _plan_bundle)
                 with tm.phase("apriori_gen"):
-                    bundle = self._plan_bundle(db, k, levels[-1], prefix_idx, ext_off, ext)
-                used = np.unique(np.concatenate([np.concatenate([pv[pi].ravel(), ex]) for _, pv, pi, _, ex in bundle]))
+                    bundle = self._plan_bundle(db, k, levels[-1], prefix_idx, ext_off, ext, cand_rows)
+                mark = np.zeros(max(db["F1"], 1), dtype=bool)
+                for _, pv, pi, _, ex in bundle:
+                    mark[pv[pi].ravel()] = True
+                    mark[ex] = True
+                used = np.flatnonzero(mark)
                 with tm.phase(f"trim{k}"):
                     self._trim(db, used, k)
                 with tm.phase("count"):
@@ -232,10 +236,14 @@ class FastApriori:
                 fid = torch.nonzero(hist >= thr).flatten()
                 got = fid.cpu().numpy(), hist[fid].cpu().numpy()
             fid, fcnt = got
-            tokens = [vocab.token(int(i)) for i in fid]
-            order = sorted(range(len(fid)), key=lambda j: (-int(fcnt[j]), java_string_key(tokens[j])))
-            items = [tokens[j] for j in order]
-            counts1 = fcnt[order].astype(np.int64)
+            # numeric tokens are ASCII decimal strings: Java String order == code-point
+            # order, so one vectorised lexsort replaces a Python sort with string keys
+            fid = np.asarray(fid, dtype=np.int64)
+            tok = (fid - 1).astype(str)
+            tok[fid == 0] = ""
+            order = np.lexsort((tok, -np.asarray(fcnt, dtype=np.int64))) if fid.size else np.zeros(0, np.int64)
+            items = tok[order].tolist()
+            counts1 = np.asarray(fcnt)[order].astype(np.int64)
             lut = torch.full((max(V, 1),), -1, dtype=torch.int32, device=dev)
             if len(order):
                 lut[torch.from_numpy(fid[order].astype(np.int64)).to(dev)] = torch.arange(
@@ -421,7 +429,7 @@ class FastApriori:
         """
         if db["T"] < self.cfg.trim_min_rows:   # a trim's fixed cost (2 launches + a host sync) dominates
             return False
-        from scipy.stats import binom
+        from scipy.special import betainc
         c1 = db["c1"]
         alive = db["alive"]
         denom = float(c1[alive].sum())
@@ -430,7 +438,12 @@ class FastApriori:
         p = float(c1[used].sum()) / denom
         hist = db["len_hist"]
         L = np.arange(hist.size)
-        est_rows = float((hist * binom.sf(k - 1, L, p)).sum())
+        # P[Binom(L, p) >= k] = I_p(k, L - k + 1) (regularised incomplete beta), 0 for L < k
+        sf = np.zeros(hist.size)
+        ok = L >= k
+        if p > 0:
+            sf[ok] = betainc(k, L[ok] - k + 1, min(p, 1.0))
+        est_rows = float((hist * sf).sum())
         est_nnz = float((hist * L * p).sum())
         return est_rows < 0.75 * max(db["T"], 1) or est_nnz < 0.6 * max(int(db["ranks"].numel()), 1)
 
@@ -515,18 +528,25 @@ class FastApriori:
     # ------------------------------------------------------------------
     # k >= 3 (FastApriori.scala:132-160)
     # ------------------------------------------------------------------
-    def _gen(self, prev: np.ndarray):
+    def _gen(self, prev: np.ndarray, want_rows: bool = False):
         """apriori-gen (FastApriori.scala:167-193): on the GPU for big levels (host
         call costs ~130 ns per candidate; the device path ~60 us per call), else the
-        C++ host path.  Both return identical (prefix_idx, ext_off, ext)."""
+        C++ host path.  Both return identical (prefix_idx, ext_off, ext) [+ the
+        candidate rows [C, m+1] when want_rows]."""
         dev = self._dev
         n = prev.shape[0]
         if (dev.type == "cuda" and GEN_DEVICE and n >= GEN_DEVICE_MIN_ROWS and prev.shape[1] >= 2
                 and self._F1 <= ops.primitives.AG_DEVICE_MAX_F1):
-            return ops.apriori_gen_device(prev, self._F1, dev)
-        return apriori_gen(prev)
+            return ops.apriori_gen_device(prev, self._F1, dev, want_rows)
+        pi, eo, ex = apriori_gen(prev)
+        if not want_rows:
+            return pi, eo, ex
+        g = np.repeat(np.arange(pi.size), np.diff(eo))
+        rows = np.concatenate([prev[pi[g]], ex[:, None]], axis=1) if ex.size else \
+            np.zeros((0, prev.shape[1] + 1), np.int32)
+        return pi, eo, ex, np.ascontiguousarray(rows, dtype=np.int32)
 
-    def _plan_bundle(self, db, k: int, prev: np.ndarray, prefix_idx, ext_off, ext) -> list:
+    def _plan_bundle(self, db, k: int, prev: np.ndarray, prefix_idx, ext_off, ext, cand_rows=None) -> list:
         """Levels counted in one launch, starting with level k.
 
         Level k+1's candidates are generated from level k's *candidates* (not
@@ -547,27 +567,27 @@ class FastApriori:
         items[prev[prefix_idx].ravel()] = True
         items[ext] = True
         total = C
-        if total > ops.primitives.slab_capacity(int(items.sum()), total):
+        n_used = int(items.sum())
+        if total > ops.primitives.slab_capacity(n_used, total):
             return bundle
-        g_of_e = np.repeat(np.arange(prefix_idx.size), np.diff(ext_off))
-        cand = np.ascontiguousarray(np.concatenate([prev[prefix_idx[g_of_e]], ext[:, None]], axis=1), np.int32)
+        if cand_rows is None:
+            g_of_e = np.repeat(np.arange(prefix_idx.size), np.diff(ext_off))
+            cand_rows = np.concatenate([prev[prefix_idx[g_of_e]], ext[:, None]], axis=1)
+        cand = np.ascontiguousarray(cand_rows, np.int32)
         last = C
         kk = k
         while self.cfg.max_level == 0 or kk + 1 <= self.cfg.max_level:
-            pi, eo, ex = self._gen(cand)
+            pi, eo, ex, nxt = self._gen(cand, want_rows=True)
             C2 = int(ex.size)
             if C2 == 0 or C2 > BUNDLE_GROWTH * last:
                 break
-            it2 = items.copy()
-            it2[cand[pi].ravel()] = True
-            it2[ex] = True
-            if total + C2 > ops.primitives.slab_capacity(int(it2.sum()), total + C2):
+            # later levels only use items of level k's candidates: n_used is fixed
+            if total + C2 > ops.primitives.slab_capacity(n_used, total + C2):
                 break
             kk += 1
             bundle.append((kk, cand, pi, eo, ex))
-            items, total, last = it2, total + C2, C2
-            g2 = np.repeat(np.arange(pi.size), np.diff(eo))
-            cand = np.ascontiguousarray(np.concatenate([cand[pi[g2]], ex[:, None]], axis=1), np.int32)
+            total, last = total + C2, C2
+            cand = nxt
         return bundle
 
     def _count_bundle(self, db, bundle: list) -> list:

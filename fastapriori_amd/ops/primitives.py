@@ -33,6 +33,54 @@ def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
+class _PinnedStage:
+    """Grow-only pinned host staging buffer for small per-level H2D copies.
+
+    Fresh pinned allocations of varying sizes (tensor.pin_memory(), torch.empty(...,
+    pin_memory=True)) each cost a host-allocator round trip of ~0.3-0.5 ms, which
+    showed up as the largest host gaps between kernels of the level loop.  An event
+    recorded after each copy guards the buffer against reuse while a copy from it
+    may still be in flight."""
+
+    def __init__(self):
+        self.buf = None
+        self.event = None
+
+    def get(self, nbytes: int) -> torch.Tensor:
+        if self.event is not None:
+            self.event.synchronize()
+            self.event = None
+        if self.buf is None or self.buf.numel() < nbytes:
+            self.buf = torch.empty(max(nbytes, 1 << 20, 2 * (self.buf.numel() if self.buf is not None else 0)),
+                                   dtype=torch.uint8, pin_memory=True)
+        return self.buf[:nbytes]
+
+    def h2d(self, host: np.ndarray, dev) -> torch.Tensor:
+        """Copy a host array to the device through the pinned stage (async)."""
+        host = np.ascontiguousarray(host)
+        st = self.get(host.nbytes)
+        st.numpy()[:] = host.reshape(-1).view(np.uint8)
+        out = st.to(dev, non_blocking=True).view(dtype=_np2torch(host.dtype)).reshape(host.shape)
+        self.event = torch.cuda.Event()
+        self.event.record()
+        return out
+
+
+def _np2torch(dt):
+    return {np.dtype(np.int32): torch.int32, np.dtype(np.int64): torch.int64, np.dtype(np.uint8): torch.uint8}[
+        np.dtype(dt)]
+
+
+_STAGES: dict = {}
+
+
+def pinned_stage(key: str) -> _PinnedStage:
+    st = _STAGES.get(key)
+    if st is None:
+        st = _STAGES[key] = _PinnedStage()
+    return st
+
+
 def _hip_call(name: str, *args) -> None:
     rc = getattr(_native.hip(), name)(*args)
     _native.check(rc, name)
@@ -793,7 +841,8 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
                        TRIE_ROUNDS, TRIE_EMAX, W], dtype=np.float64)
     bound = 2 * F1 + C + G * m + 6 * (G + C // 2 + 2) + (m + 4) * (G + C // 8 + 1) + 16
     on_gpu = dev.type == "cuda"
-    buf = torch.empty(bound, dtype=_I32, pin_memory=on_gpu)
+    stage = pinned_stage("level_plan") if on_gpu else None
+    buf = stage.get(4 * bound).view(dtype=_I32) if on_gpu else torch.empty(bound, dtype=_I32)
     max_pass = G + C + 2
     passes = np.zeros((max_pass, 3), dtype=np.int64)
     info = np.zeros(24, dtype=np.int64)
@@ -807,6 +856,9 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
     kern, sw, cap, n_used, npass = int(info[0]), int(info[1]), int(info[2]), int(info[3]), int(info[6])
     total = int(info[18])
     dbuf = buf[:total].to(dev, non_blocking=True)
+    if on_gpu:
+        stage.event = torch.cuda.Event()
+        stage.event.record()
     base = dbuf.data_ptr()
     passes = passes[:npass]
     o_im, o_used, o_gext, o_gpre, o_pc, o_wi, o_gpm = (int(info[i]) for i in (12, 13, 14, 15, 16, 17, 19))
@@ -843,33 +895,44 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
 AG_DEVICE_MAX_F1 = 4096   # bitset words per lane-wave: 64 x 64 bits
 
 
-def apriori_gen_device(prev: np.ndarray, F1: int, dev) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
-    """apriori-gen on the GPU (csrc/hip/gen.hip): same output as ops.host.apriori_gen
-    (prefix_idx int32 [G], ext_off int64 [G+1], ext int32 [C]) with two host syncs."""
+_GEN_WS: dict = {}
+
+
+def apriori_gen_device(prev: np.ndarray, F1: int, dev, want_rows: bool = False):
+    """apriori-gen on the GPU (csrc/hip/gen.hip fa_hip_ag_gen: one native call, two
+    stream syncs): (prefix_idx int32 [G], ext_off int64 [G+1], ext int32 [C]) as
+    ops.host.apriori_gen, plus the candidate rows int32 [C, m+1] when want_rows."""
     n, m = prev.shape
-    P = torch.from_numpy(np.ascontiguousarray(prev, dtype=np.int32)).to(dev, non_blocking=False)
-    cap = 16
-    while cap < 2 * n:
-        cap <<= 1
-    table = torch.full((cap,), -1, dtype=_I32, device=dev)
-    nw = (F1 + 63) // 64
-    ext = torch.zeros(n * nw, dtype=_I64, device=dev)
+    P = pinned_stage("gen").h2d(np.ascontiguousarray(prev, dtype=np.int32), dev)
     st = _stream(P)
-    _hip_call("fa_hip_ag_build", _p(P), n, m, _p(table), cap - 1, nw, _p(ext), st)
-    cnt = torch.empty(n, dtype=_I32, device=dev)
-    _hip_call("fa_hip_ag_rows", _p(P), n, m, _p(table), cap - 1, nw, _p(ext), _p(cnt), None, None, 0, st)
-    off = torch.zeros(n + 1, dtype=_I64, device=dev)
-    torch.cumsum(cnt, 0, out=off[1:])
-    C = int(off[-1].item())
-    out = torch.empty(max(C, 1), dtype=_I32, device=dev)
-    if C:
-        _hip_call("fa_hip_ag_rows", _p(P), n, m, _p(table), cap - 1, nw, _p(ext), None, _p(off), _p(out), 1, st)
-    both = torch.cat([cnt, out[:C]]).cpu().numpy()
-    cnt_h, ext_h = both[:n], both[n:]
+    sizes = np.zeros(2, dtype=np.int64)
+    host_stage = pinned_stage("gen_out")
+    need_host = n + 8 * n * (m + 2) + 1024
+    for _ in range(4):
+        ws = _GEN_WS.get(dev)
+        host = host_stage.get(4 * need_host).view(dtype=_I32)
+        rc = _native.hip().fa_hip_ag_gen(_p(P), n, m, F1, _p(ws), ws.numel() if ws is not None else 0,
+                                         host.data_ptr(), host.numel(), sizes.ctypes.data, st)
+        if rc == 5:
+            _GEN_WS[dev] = torch.empty(int(sizes[1] * 1.5) + (1 << 20), dtype=torch.uint8, device=dev)
+            continue
+        if rc == 6:
+            need_host = int(sizes[1] * 1.5) + 1024
+            continue
+        _native.check(rc, "fa_hip_ag_gen")
+        break
+    else:
+        raise RuntimeError("fa_hip_ag_gen: workspace sizing did not converge")
+    C = int(sizes[0])
+    h = host.numpy()
+    cnt_h = h[:n]
     prefix_idx = np.flatnonzero(cnt_h).astype(np.int32)
     ext_off = np.zeros(prefix_idx.size + 1, dtype=np.int64)
     np.cumsum(cnt_h[prefix_idx], out=ext_off[1:])
-    return prefix_idx, ext_off, ext_h.astype(np.int32, copy=False)
+    ext_h = h[n:n + C].copy()
+    if want_rows:
+        return prefix_idx, ext_off, ext_h, h[n + C:n + C + C * (m + 1)].reshape(C, m + 1).copy()
+    return prefix_idx, ext_off, ext_h
 
 
 def recommend(ante_off, ante, cons, F1: int, boff, bask) -> torch.Tensor:

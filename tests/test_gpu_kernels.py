@@ -314,5 +314,9 @@ def test_apriori_gen_device_matches_host(k):
     pidx, eoff, ext = want
     g = np.repeat(np.arange(pidx.size), np.diff(eoff))
     cand = np.ascontiguousarray(np.concatenate([prev[pidx[g]], ext[:, None]], 1), np.int32)
-    for a, b in zip(apriori_gen(cand), ops.apriori_gen_device(cand, len(res.items), DEV)):
+    got = ops.apriori_gen_device(cand, len(res.items), DEV, want_rows=True)
+    want = apriori_gen(cand)
+    for a, b in zip(want, got[:3]):
         assert np.array_equal(a, b)
+    g2 = np.repeat(np.arange(want[0].size), np.diff(want[1]))
+    assert np.array_equal(got[3], np.concatenate([cand[want[0][g2]], want[2][:, None]], 1))
