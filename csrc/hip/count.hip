@@ -750,6 +750,105 @@ __global__ __launch_bounds__(256) void k_pair_gram_popc(
 }
 
 // ---------------------------------------------------------------------------
+// k = 2, dense bit-matrix Gram on the matrix cores (unit weights).
+//
+// count[a][b] = sum_t bit_a(t) bit_b(t) = (B^T B)[a][b] with B the T x F1 0/1
+// matrix: a GEMM with K = transactions.  Bits are unpacked to int8 in registers
+// (a nibble n -> 4 bytes by (n * 0x204081) & 0x01010101, no carries) and fed
+// to v_mfma_i32_32x32x32_i8 with exact int32 accumulation.  A workgroup owns a
+// 128 x 128 item tile (4 waves x 64 x 64 = 2 x 2 MFMA tiles each) and a chunk
+// of bitmap words, staged through LDS 8 words (512 transactions) at a time
+// with coalesced 64-byte row reads; partial tiles are added with one atomic
+// per element.  Lane (r, h) supplies A[r][16h + j] and B[16h + j][c] from the
+// same 16 transactions, so the K pairing is exact whatever the hardware's
+// k-order inside a lane half is (the same for A and B).
+// ---------------------------------------------------------------------------
+typedef int fa_v4i __attribute__((ext_vector_type(4)));
+typedef int fa_v16i __attribute__((ext_vector_type(16)));
+constexpr int kMT = 128;     // items per tile side
+constexpr int kMW = 8;       // words staged per step
+constexpr int kMS = kMW + 1; // LDS row stride (words): 72 B rows -> conflict-free ds_read_b64
+
+__device__ __forceinline__ fa_v4i unpack16_i8(uint32_t b) {
+  fa_v4i r;
+  r.x = (int)(((b & 0xFu) * 0x00204081u) & 0x01010101u);
+  r.y = (int)((((b >> 4) & 0xFu) * 0x00204081u) & 0x01010101u);
+  r.z = (int)((((b >> 8) & 0xFu) * 0x00204081u) & 0x01010101u);
+  r.w = (int)((((b >> 12) & 0xFu) * 0x00204081u) & 0x01010101u);
+  return r;
+}
+
+__global__ __launch_bounds__(256) void k_pair_gram_mfma(const uint64_t* __restrict__ bm, int32_t F1, int64_t Wp,
+                                                        int64_t W, int nt, int ntp, int64_t kchunk,
+                                                        uint32_t* __restrict__ out) {
+  __shared__ uint64_t As[kMT * kMS];
+  __shared__ uint64_t Bs[kMT * kMS];
+  const int tp = blockIdx.x % ntp;
+  const int64_t kc = blockIdx.x / ntp;
+  int ti, tj;
+  tri_index(tp, nt, ti, tj);
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int wr = (wv >> 1) * 64, wc = (wv & 1) * 64;     // the wave's 64 x 64 sub-tile
+  fa_v16i acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = fa_v16i{0};
+  const int64_t k_begin = kc * kchunk, k_end = min(W, k_begin + kchunk);
+  for (int64_t k0 = k_begin; k0 < k_end; k0 += kMW) {
+    // stage 128 rows x 8 words of each operand: thread = (row, word), 4 per thread
+#pragma unroll
+    for (int it = 0; it < (kMT * kMW) / 256; ++it) {
+      const int idx = threadIdx.x + it * 256;
+      const int row = idx >> 3, w = idx & 7;
+      const int ra = ti * kMT + row, rb = tj * kMT + row;
+      const int64_t kk = k0 + w;
+      As[row * kMS + w] = (ra < F1 && kk < k_end) ? bm[(int64_t)ra * Wp + kk] : 0ull;
+      Bs[row * kMS + w] = (rb < F1 && kk < k_end) ? bm[(int64_t)rb * Wp + kk] : 0ull;
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int w = 0; w < kMW; ++w) {
+      uint64_t a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        a[i] = As[(wr + 32 * i + r) * kMS + w];
+        b[i] = Bs[(wc + 32 * i + r) * kMS + w];
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {                  // two 32-transaction k-steps per word
+        const int sh = 32 * s2 + 16 * h;
+        fa_v4i fa[2], fb[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          fa[i] = unpack16_i8((uint32_t)(a[i] >> sh) & 0xFFFFu);
+          fb[i] = unpack16_i8((uint32_t)(b[i] >> sh) & 0xFFFFu);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  // C/D layout (gfx950, 32x32): col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int row = ti * kMT + wr + 32 * i + (g & 3) + 8 * (g >> 2) + 4 * h;
+        const int col = tj * kMT + wc + 32 * j + r;
+        const int v = acc[i][j][g];
+        if (row < col && col < F1 && v) atomicAdd(&out[(int64_t)row * F1 + col], (uint32_t)v);
+      }
+}
+
+// ---------------------------------------------------------------------------
 // k >= 3: prefix-shared candidate counting.
 // Workgroup = (super-chunk sc of 256*kWPT words) x (group block gb).  Each thread
 // keeps its kWPT words of the prefix AND in registers, streams every
@@ -1259,6 +1358,21 @@ FA_API int fa_hip_pair_horizontal(const int64_t* roff, const int32_t* ranks, int
   else
     hipLaunchKernelGGL(k_pair_horizontal<uint16_t>, g, b, 0, st, roff, ranks, T, wrow, (const uint16_t*)bt, F1, nb,
                        nbp, chunk, out);
+  FA_LAUNCH_RET();
+}
+
+// Unit-weight Gram on the matrix cores (k_pair_gram_mfma); out: u32 [F1][F1] (upper triangle).
+FA_API int fa_hip_pair_gram_mfma(const uint64_t* bm, int32_t F1, int64_t Wp, int64_t W, uint32_t* out,
+                                 int target_wgs, hipStream_t st) {
+  if (W <= 0 || F1 < 2) return 0;
+  const int nt = (F1 + kMT - 1) / kMT;
+  const int ntp = nt * (nt + 1) / 2;
+  int64_t nk = std::max<int64_t>(1, (target_wgs + ntp - 1) / ntp);
+  int64_t kchunk = (W + nk - 1) / nk;
+  kchunk = std::max<int64_t>(kMW, (kchunk + kMW - 1) / kMW * kMW);
+  nk = (W + kchunk - 1) / kchunk;
+  hipLaunchKernelGGL(k_pair_gram_mfma, dim3((unsigned)(nk * ntp)), dim3(256), 0, st, bm, F1, Wp, W, nt, ntp, kchunk,
+                     out);
   FA_LAUNCH_RET();
 }
 

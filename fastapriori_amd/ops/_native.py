@@ -86,6 +86,7 @@ _HIP_SIGS = {
     "fa_hip_pair_rows16": (C.c_int, [vp, vp, vp, i64, C.c_int, vp, vp]),
     "fa_hip_pair_blocked16": (C.c_int, [vp, vp, vp, i64, i32, vp, vp]),
     "fa_hip_pair_blocked": (C.c_int, [vp, vp, vp, i64, vp, i32, vp, i64, vp]),
+    "fa_hip_pair_gram_mfma": (C.c_int, [vp, i32, i64, i64, vp, C.c_int, vp]),
     "fa_hip_pair_gram_popc": (C.c_int, [vp, i32, i64, i64, vp, vp, C.c_int, vp]),
     "fa_hip_count_candidates": (C.c_int, [vp, i64, i64, vp, C.c_int, vp, vp, vp, C.c_int, vp, vp, vp]),
     "fa_hip_recommend": (C.c_int, [vp, vp, vp, i64, i32, vp, vp, i64, vp, vp]),

@@ -389,7 +389,11 @@ def pair_counts_gram(bm: torch.Tensor, W: int, wword) -> torch.Tensor:
     if bm.is_cuda:
         out = torch.zeros((F1, F1), dtype=_I32, device=bm.device)
         if W > 0 and F1 >= 2:
-            _hip_call("fa_hip_pair_gram_popc", _p(bm), F1, Wp, W, _p(wword), _p(out), 4096, _stream(bm))
+            if wword is None and os.environ.get("FA_GRAM_KERNEL", "mfma") == "mfma":
+                # unit weights: int8 GEMM on the matrix cores (weights > 1 need the popcount form)
+                _hip_call("fa_hip_pair_gram_mfma", _p(bm), F1, Wp, W, _p(out), 4096, _stream(bm))
+            else:
+                _hip_call("fa_hip_pair_gram_popc", _p(bm), F1, Wp, W, _p(wword), _p(out), 4096, _stream(bm))
         return out.to(_I64)
     out = torch.zeros((F1, F1), dtype=_I64)
     if W > 0 and F1 >= 2:

@@ -320,3 +320,27 @@ def test_apriori_gen_device_matches_host(k):
         assert np.array_equal(a, b)
     g2 = np.repeat(np.arange(want[0].size), np.diff(want[1]))
     assert np.array_equal(got[3], np.concatenate([cand[want[0][g2]], want[2][:, None]], 1))
+
+
+@pytest.mark.parametrize("F1,T", [(37, 5000), (300, 70001), (1000, 9000)])
+def test_pair_gram_mfma_matches_popcount(monkeypatch, F1, T):
+    # i8 MFMA Gram (v_mfma_i32_32x32x32_i8) vs the popcount Gram and the CPU Gram on
+    # asymmetric random bitmaps (F1 not a multiple of the 128 tile, W of the 8-word step)
+    rng = np.random.default_rng(F1)
+    dens = rng.random(F1) * 0.6
+    bits = rng.random((F1, T)) < dens[:, None]
+    W = (T + 63) // 64
+    Wp = (W + 63) // 64 * 64
+    words = np.zeros((F1, Wp), dtype=np.uint64)
+    packed = np.packbits(bits, axis=1, bitorder="little")
+    pad = np.zeros((F1, W * 8), np.uint8)
+    pad[:, :packed.shape[1]] = packed
+    words[:, :W] = pad.view(np.uint64)
+    bm = torch.from_numpy(words.view(np.int64)).to(DEV)
+    got = ops.pair_counts_gram(bm, W, None).cpu()
+    monkeypatch.setenv("FA_GRAM_KERNEL", "popc")
+    ref = ops.pair_counts_gram(bm, W, None).cpu()
+    want = torch.from_numpy(bits.astype(np.int64) @ bits.astype(np.int64).T)
+    iu = torch.triu_indices(F1, F1, 1)
+    assert torch.equal(got[iu[0], iu[1]], want[iu[0], iu[1]])
+    assert torch.equal(ref[iu[0], iu[1]], want[iu[0], iu[1]])
