@@ -979,7 +979,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
     int64_t ncols, const int32_t* __restrict__ item_map, int n_used, const int32_t* __restrict__ gpre, int m,
     const int32_t* __restrict__ gext_off, const int32_t* __restrict__ gext, int G, int C,
     const int32_t* __restrict__ wword, uint32_t* __restrict__ out, const uint64_t* __restrict__ bm,
-    int64_t Wp, int dbg, const int32_t* __restrict__ gpm) {
+    int64_t Wp, int dbg, const int32_t* __restrict__ gpm, const int32_t* __restrict__ bm_rows) {
   extern __shared__ uint4 lds4[];                  // 16-B aligned base
   __shared__ unsigned long long build_words[kSlabThreads / 64 * 2];   // window_starts scratch
   constexpr int SWP = SW + 2;                       // row stride: 16-B aligned, odd number of 16-B slots
@@ -1018,7 +1018,9 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
       // multi-pass level: the used-item bitmap is materialised once; copy the slab tile
       for (int i = threadIdx.x; i < n_used * SW; i += blockDim.x) {
         const int u = i / SW, q = i - u * SW;
-        slab[(size_t)u * SWP + q] = (w0 + q < W) ? bm[(size_t)u * Wp + w0 + q] : 0ull;
+        // bm_rows: slab row -> bitmap row when the bitmap holds every item (built once per layout)
+        const int64_t br = bm_rows ? bm_rows[u] : u;
+        slab[(size_t)u * SWP + q] = (w0 + q < W) ? bm[(size_t)br * Wp + w0 + q] : 0ull;
       }
     } else {
       {
@@ -1136,7 +1138,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_trie(
     int64_t ncols, const int32_t* __restrict__ item_map, int n_used, const int32_t* __restrict__ gpre, int m,
     int D1, int D2, const int4* __restrict__ pieces, const int2* __restrict__ witems, int NW,
     const int32_t* __restrict__ gext, int C, const int32_t* __restrict__ wword, uint32_t* __restrict__ out,
-    const uint64_t* __restrict__ bm, int64_t Wp) {
+    const uint64_t* __restrict__ bm, int64_t Wp, const int32_t* __restrict__ bm_rows) {
   constexpr int NQ = 2;                        // uint4 (4 words) per lane: ~90 VGPRs at 1024 threads
   constexpr int RS = SW / 2;                   // uint4 slots per slab row
   constexpr int LPP = RS / NQ;                 // lanes per work item: 2 / 4 / 8 for SW = 8 / 16 / 32
@@ -1169,7 +1171,8 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_trie(
     if (kBuild == kBuildBM) {
       for (int i = threadIdx.x; i < n_used * SW; i += blockDim.x) {
         const int u = i / SW, q = i - u * SW;
-        slab[(size_t)u * SW + (q ^ ((u << 2) & SWZ))] = (w0 + q < W) ? bm[(size_t)u * Wp + w0 + q] : 0ull;
+        const int64_t br = bm_rows ? bm_rows[u] : u;
+        slab[(size_t)u * SW + (q ^ ((u << 2) & SWZ))] = (w0 + q < W) ? bm[(size_t)br * Wp + w0 + q] : 0ull;
       }
     } else {
       {
@@ -1415,14 +1418,14 @@ FA_API int fa_hip_count_slab(const int64_t* roff, const int32_t* ranks, const in
                              const int32_t* item_map, int n_used, const int32_t* gpre, int m,
                              const int32_t* gext_off, const int32_t* gext, int G, int C, const int32_t* wword,
                              uint32_t* out, int sw, int n_wg, const uint64_t* bm, int64_t Wp, hipStream_t st,
-                             const int32_t* gpm) {
+                             const int32_t* gpm, const int32_t* bm_rows) {
   if (G <= 0 || C <= 0 || ncols <= 0) return 0;
   const size_t lds = (size_t)n_used * (sw + 2) * 8 + (size_t)C * 4;
   if (lds > 160 * 1024 - 512) return 3;   // static build_words scratch
   dim3 g((unsigned)n_wg), b(kSlabThreads);
   using KernT = void (*)(const int64_t*, const int32_t*, const int32_t*, int64_t, const int32_t*, int,
                          const int32_t*, int, const int32_t*, const int32_t*, int, int, const int32_t*,
-                         uint32_t*, const uint64_t*, int64_t, int, const int32_t*);
+                         uint32_t*, const uint64_t*, int64_t, int, const int32_t*, const int32_t*);
   KernT kern = nullptr;
 #define FA_SLAB_MODE(S, B) kern = wword ? (KernT)k_count_slab<S, true, B> : (KernT)k_count_slab<S, false, B>;
 #define FA_SLAB_CASE(S)                                   \
@@ -1441,7 +1444,7 @@ FA_API int fa_hip_count_slab(const int64_t* roff, const int32_t* ranks, const in
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const int dbg = getenv("FA_SLAB_DEBUG") ? atoi(getenv("FA_SLAB_DEBUG")) : 0;
   hipLaunchKernelGGL(kern, g, b, lds, st, roff, ranks, src, ncols, item_map, n_used, gpre, m, gext_off, gext, G, C,
-                     wword, out, bm, Wp, dbg, gpm);
+                     wword, out, bm, Wp, dbg, gpm, bm_rows);
   FA_LAUNCH_RET();
 }
 
@@ -1452,14 +1455,14 @@ FA_API int fa_hip_count_trie(const int64_t* roff, const int32_t* ranks, const in
                              const int32_t* item_map, int n_used, const int32_t* gpre, int m, int D1, int D2,
                              const void* pieces, const void* witems, int NW, const int32_t* gext, int C,
                              const int32_t* wword, uint32_t* out, int sw, int n_wg, const uint64_t* bm, int64_t Wp,
-                             hipStream_t st) {
+                             hipStream_t st, const int32_t* bm_rows) {
   if (NW <= 0 || C <= 0 || ncols <= 0) return 0;
   if (!(0 <= D1 && D1 <= D2 && D2 <= m)) return 2;
   const size_t lds = (size_t)n_used * sw * 8 + (size_t)C * 4;
   if (lds > 160 * 1024 - 512) return 3;
   using KernT = void (*)(const int64_t*, const int32_t*, const int32_t*, int64_t, const int32_t*, int,
                          const int32_t*, int, int, int, const int4*, const int2*, int, const int32_t*, int,
-                         const int32_t*, uint32_t*, const uint64_t*, int64_t);
+                         const int32_t*, uint32_t*, const uint64_t*, int64_t, const int32_t*);
   KernT kern = nullptr;
 #define FA_TRIE_MODE(S, B) kern = wword ? (KernT)k_count_trie<S, true, B> : (KernT)k_count_trie<S, false, B>;
 #define FA_TRIE_CASE(S)                                   \
@@ -1477,7 +1480,7 @@ FA_API int fa_hip_count_trie(const int64_t* roff, const int32_t* ranks, const in
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, dim3((unsigned)n_wg), dim3(kSlabThreads), lds, st, roff, ranks, src, ncols, item_map,
                      n_used, gpre, m, D1, D2, (const int4*)pieces, (const int2*)witems, NW, gext, C, wword, out, bm,
-                     Wp);
+                     Wp, bm_rows);
   FA_LAUNCH_RET();
 }
 

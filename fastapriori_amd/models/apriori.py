@@ -477,11 +477,14 @@ class FastApriori:
             db.update(src=None, ncols=K)
         self.log.metric(phase="trim", k=k, rows=K, nnz=int(nranks.numel()))
 
-    def _bitmaps(self, db) -> None:
+    def _bitmaps(self, db):
+        """Item-major bitmaps of every item for the current row layout (built once,
+        reused by the Gram pair kernel and every multi-pass level until a trim)."""
         if db["bm"] is None:
             with roctx_range("bitmaps"):
                 bm, W = ops.build_bitmaps(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"])
             db["bm"], db["W"] = bm, W
+        return db["bm"]
 
     # ------------------------------------------------------------------
     # k = 2 (FastApriori.scala:212-241)
@@ -601,7 +604,7 @@ class FastApriori:
         eoff = np.concatenate([[0], np.cumsum(np.concatenate([np.diff(eo) for _, _, _, eo, _ in bundle]))])
         ext = np.concatenate([ex for *_, ex in bundle]).astype(np.int32)
         cnt = ops.count_level(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"], flat, eoff, ext,
-                              db["wword"], kernel="slab", poff=poff)
+                              db["wword"], kernel="slab", poff=poff, full_bm=lambda: self._bitmaps(db))
         if cnt is None:
             return [self._count_level(db, pv, pi, eo, ex) for _, pv, pi, eo, ex in bundle]
         self.dcomm.all_reduce_(cnt)
@@ -635,7 +638,7 @@ class FastApriori:
         lk = self.cfg.level_kernel
         if dev.type == "cuda" and lk in ("auto", "trie", "slab"):
             cnt = ops.count_level(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"], prev[prefix_idx],
-                                  ext_off, ext, db["wword"], kernel=lk)
+                                  ext_off, ext, db["wword"], kernel=lk, full_bm=lambda: self._bitmaps(db))
             if cnt is not None:
                 self.dcomm.all_reduce_(cnt)
                 return cnt.cpu().numpy()

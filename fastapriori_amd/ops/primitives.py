@@ -609,7 +609,7 @@ def count_level_slab(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, 
         n_wg = int(max(1, min(nslabs, 256 * min(per_cu, 2))))
         _hip_call("fa_hip_count_slab", _p(roff), _p(ranks), _p(src), ncols, _p(imap_t), int(used.size), _p(pre_t),
                   m, _p(loc_off), gext_t.data_ptr() + 4 * e0, g1 - g0, e1 - e0, _p(wword),
-                  out.data_ptr() + 4 * e0, sw, n_wg, _p(bm), bm.stride(0) if bm is not None else 0, st, None)
+                  out.data_ptr() + 4 * e0, sw, n_wg, _p(bm), bm.stride(0) if bm is not None else 0, st, None, None)
     res = out.to(_I64)
     del keep
     LAST_SLAB_PLAN.clear()
@@ -744,7 +744,7 @@ def count_level_trie(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, 
         _hip_call("fa_hip_count_trie", _p(roff), _p(ranks), _p(src), ncols, base_ptr + 4 * o_im, int(used.size),
                   base_ptr, m, plan.d1, plan.d2, base_ptr + 4 * o_pc, base_ptr + 4 * (o_wi + 2 * w0),
                   w1 - w0, base_ptr + 4 * (o_gext + e0), Cq, _p(wword), out.data_ptr() + 4 * e0, sw, n_wg,
-                  _p(bm), bm.stride(0) if bm is not None else 0, st)
+                  _p(bm), bm.stride(0) if bm is not None else 0, st, None)
     res = out.to(_I64)
     LAST_TRIE_PLAN.clear()
     LAST_TRIE_PLAN.update(rows=int(roff.numel() - 1), used=int(used.size), sw=sw, cap=cap,
@@ -821,7 +821,7 @@ def _flat_prefix(prefix: np.ndarray, poff: np.ndarray | None):
 
 
 def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_off: np.ndarray, ext: np.ndarray,
-                wword, kernel: str = "auto", poff: np.ndarray | None = None) -> torch.Tensor | None:
+                wword, kernel: str = "auto", poff: np.ndarray | None = None, full_bm=None) -> torch.Tensor | None:
     """Support counts of one level on the device: one native planning call
     (csrc/host/plan.cpp fa_level_plan: used items, kernel choice, work items,
     accumulator passes) into one pinned buffer, one host->device copy, then the
@@ -830,6 +830,9 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
     kernel: auto (trie where it saves enough slab-row reads) | trie | slab.
     prefix: int32 [G, m], or (poff given) a flat int32 array with group g's
     prefix at poff[g]:poff[g+1] — groups of several levels (k) in one launch.
+    full_bm: optional callable returning the bitmap of every item [F1, Wp] of the
+    current row layout (built once, shared by all multi-pass levels until the rows
+    change); without it a used-item bitmap is built for each multi-pass level.
     Returns int64 counts [C] (ext order), or None when no LDS slab fits (the
     caller then uses the bitmap kernel)."""
     dev = ranks.device
@@ -867,9 +870,14 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
     passes = passes[:npass]
     o_im, o_used, o_gext, o_gpre, o_pc, o_wi, o_gpm = (int(info[i]) for i in (12, 13, 14, 15, 16, 17, 19))
     out = torch.zeros(C, dtype=_I32, device=dev)
-    bm = None
+    bm, bm_rows = None, None
     if npass > 1:
-        bm, _ = build_bitmaps(roff, ranks, src, ncols, n_used, dbuf[o_im:o_im + F1], dbuf[o_used:o_used + n_used])
+        if full_bm is not None:
+            bm = full_bm()
+            bm_rows = base + 4 * o_used             # slab row u -> bitmap row used[u]
+        else:
+            bm, _ = build_bitmaps(roff, ranks, src, ncols, n_used, dbuf[o_im:o_im + F1],
+                                  dbuf[o_used:o_used + n_used])
     st = _stream(ranks)
     bounds = passes[:, 2].tolist() + [C]
     nslabs = (W + sw - 1) // sw
@@ -881,14 +889,14 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
             _hip_call("fa_hip_count_trie", _p(roff), _p(ranks), _p(src), ncols, base + 4 * o_im, n_used,
                       base + 4 * o_gpre, m, int(info[7]), int(info[8]), base + 4 * o_pc, base + 4 * (o_wi + 2 * a),
                       b - a, base + 4 * (o_gext + e0), Cq, _p(wword), out.data_ptr() + 4 * e0, sw, n_wg, _p(bm),
-                      bm.stride(0) if bm is not None else 0, st)
+                      bm.stride(0) if bm is not None else 0, st, bm_rows)
         else:
             lds = n_used * (sw + 2) * 8 + Cq * 4
             n_wg = int(max(1, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2))))
             _hip_call("fa_hip_count_slab", _p(roff), _p(ranks), _p(src), ncols, base + 4 * o_im, n_used,
                       base + 4 * o_gpre, m, base + 4 * (o_pc + 2 * a), base + 4 * (o_gext + e0), b - a, Cq,
                       _p(wword), out.data_ptr() + 4 * e0, sw, n_wg, _p(bm), bm.stride(0) if bm is not None else 0,
-                      st, base + 4 * (o_gpm + 2 * a))
+                      st, base + 4 * (o_gpm + 2 * a), bm_rows)
     LAST_LEVEL_PLAN.clear()
     LAST_LEVEL_PLAN.update(kernel="trie" if kern == 1 else "slab", rows=int(roff.numel() - 1), used=n_used, sw=sw,
                            cap=cap, passes=npass, pieces=int(info[4]), witems=int(info[5]), d1=int(info[7]),
