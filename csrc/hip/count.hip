@@ -979,7 +979,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
     int64_t ncols, const int32_t* __restrict__ item_map, int n_used, const int32_t* __restrict__ gpre, int m,
     const int32_t* __restrict__ gext_off, const int32_t* __restrict__ gext, int G, int C,
     const int32_t* __restrict__ wword, uint32_t* __restrict__ out, const uint64_t* __restrict__ bm,
-    int64_t Wp, int dbg, const int32_t* __restrict__ gpm, const int32_t* __restrict__ bm_rows) {
+    int64_t Wp, int dbg, const int32_t* __restrict__ gpm, const int32_t* __restrict__ bm_rows, int acc16) {
   extern __shared__ uint4 lds4[];                  // 16-B aligned base
   __shared__ unsigned long long build_words[kSlabThreads / 64 * 2];   // window_starts scratch
   constexpr int SWP = SW + 2;                       // row stride: 16-B aligned, odd number of 16-B slots
@@ -987,7 +987,10 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
   constexpr int RPC = 32 / CPT;                     // ranks per column prefetched in registers
   uint64_t* slab = reinterpret_cast<uint64_t*>(lds4);
   uint32_t* acc = reinterpret_cast<uint32_t*>(slab + (size_t)n_used * SWP);
-  for (int i = threadIdx.x; i < C; i += blockDim.x) acc[i] = 0;
+  // acc16: two 16-bit counters per word (unit weights, <= 65535 columns per
+  // workgroup, guaranteed by the launcher's grid): twice the candidates per pass
+  const int n_acc = acc16 ? (C + 1) >> 1 : C;
+  for (int i = threadIdx.x; i < n_acc; i += blockDim.x) acc[i] = 0;
   const int64_t W = (ncols + 63) >> 6;
   const int64_t nslabs = (W + SW - 1) / SW;
 
@@ -1098,13 +1101,16 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
             s += __popc(p[q].x & v.x) + __popc(p[q].y & v.y) + __popc(p[q].z & v.z) + __popc(p[q].w & v.w);
           }
         }
-        acc[e] += s;
+        if (acc16) atomicAdd(&acc[e >> 1], s << ((e & 1) << 4));
+        else acc[e] += s;
       }
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < C; i += blockDim.x)
-    if (acc[i]) atomicAdd(&out[i], acc[i]);
+  for (int i = threadIdx.x; i < C; i += blockDim.x) {
+    const uint32_t v = acc16 ? (acc[i >> 1] >> ((i & 1) << 4)) & 0xFFFFu : acc[i];
+    if (v) atomicAdd(&out[i], v);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1138,7 +1144,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_trie(
     int64_t ncols, const int32_t* __restrict__ item_map, int n_used, const int32_t* __restrict__ gpre, int m,
     int D1, int D2, const int4* __restrict__ pieces, const int2* __restrict__ witems, int NW,
     const int32_t* __restrict__ gext, int C, const int32_t* __restrict__ wword, uint32_t* __restrict__ out,
-    const uint64_t* __restrict__ bm, int64_t Wp, const int32_t* __restrict__ bm_rows) {
+    const uint64_t* __restrict__ bm, int64_t Wp, const int32_t* __restrict__ bm_rows, int acc16) {
   constexpr int NQ = 2;                        // uint4 (4 words) per lane: ~90 VGPRs at 1024 threads
   constexpr int RS = SW / 2;                   // uint4 slots per slab row
   constexpr int LPP = RS / NQ;                 // lanes per work item: 2 / 4 / 8 for SW = 8 / 16 / 32
@@ -1152,7 +1158,12 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_trie(
   __shared__ unsigned long long build_words[kSlabThreads / 64 * 2];
   uint64_t* slab = reinterpret_cast<uint64_t*>(lds4);
   uint32_t* acc = reinterpret_cast<uint32_t*>(slab + (size_t)n_used * SW);
-  for (int i = threadIdx.x; i < C; i += blockDim.x) acc[i] = 0;
+  const int n_acc = acc16 ? (C + 1) >> 1 : C;   // acc16: packed 16-bit counters (see k_count_slab)
+  for (int i = threadIdx.x; i < n_acc; i += blockDim.x) acc[i] = 0;
+  auto acc_add = [&](int e, uint32_t v) {
+    if (acc16) atomicAdd(&acc[e >> 1], v << ((e & 1) << 4));
+    else atomicAdd(&acc[e], v);
+  };
   const int64_t W = (ncols + 63) >> 6;
   const int64_t nslabs = (W + SW - 1) / SW;
 
@@ -1299,8 +1310,8 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_trie(
           const uint32_t s0 = lanes_sum(dot(p, v0)), s1 = lanes_sum(dot(p, v1));
           const uint32_t s2 = lanes_sum(dot(p, v2)), s3 = lanes_sum(dot(p, v3));
           if (t == 0) {
-            atomicAdd(&acc[e], s0); atomicAdd(&acc[e + 1], s1);
-            atomicAdd(&acc[e + 2], s2); atomicAdd(&acc[e + 3], s3);
+            acc_add(e, s0); acc_add(e + 1, s1);
+            acc_add(e + 2, s2); acc_add(e + 3, s3);
           }
         }
         for (; e < d.z; ++e) {
@@ -1310,14 +1321,16 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_trie(
 #pragma unroll
           for (int q = 0; q < NQ; ++q) v0[q] = r0[off[q] ^ x0];
           const uint32_t s0 = lanes_sum(dot(p, v0));
-          if (t == 0) atomicAdd(&acc[e], s0);
+          if (t == 0) acc_add(e, s0);
         }
       }
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < C; i += blockDim.x)
-    if (acc[i]) atomicAdd(&out[i], acc[i]);
+  for (int i = threadIdx.x; i < C; i += blockDim.x) {
+    const uint32_t v = acc16 ? (acc[i >> 1] >> ((i & 1) << 4)) & 0xFFFFu : acc[i];
+    if (v) atomicAdd(&out[i], v);
+  }
 }
 
 }  // namespace fa
@@ -1418,14 +1431,14 @@ FA_API int fa_hip_count_slab(const int64_t* roff, const int32_t* ranks, const in
                              const int32_t* item_map, int n_used, const int32_t* gpre, int m,
                              const int32_t* gext_off, const int32_t* gext, int G, int C, const int32_t* wword,
                              uint32_t* out, int sw, int n_wg, const uint64_t* bm, int64_t Wp, hipStream_t st,
-                             const int32_t* gpm, const int32_t* bm_rows) {
+                             const int32_t* gpm, const int32_t* bm_rows, int acc16) {
   if (G <= 0 || C <= 0 || ncols <= 0) return 0;
-  const size_t lds = (size_t)n_used * (sw + 2) * 8 + (size_t)C * 4;
+  const size_t lds = (size_t)n_used * (sw + 2) * 8 + (acc16 ? (size_t)((C + 1) / 2) * 4 : (size_t)C * 4);
   if (lds > 160 * 1024 - 512) return 3;   // static build_words scratch
   dim3 g((unsigned)n_wg), b(kSlabThreads);
   using KernT = void (*)(const int64_t*, const int32_t*, const int32_t*, int64_t, const int32_t*, int,
                          const int32_t*, int, const int32_t*, const int32_t*, int, int, const int32_t*,
-                         uint32_t*, const uint64_t*, int64_t, int, const int32_t*, const int32_t*);
+                         uint32_t*, const uint64_t*, int64_t, int, const int32_t*, const int32_t*, int);
   KernT kern = nullptr;
 #define FA_SLAB_MODE(S, B) kern = wword ? (KernT)k_count_slab<S, true, B> : (KernT)k_count_slab<S, false, B>;
 #define FA_SLAB_CASE(S)                                   \
@@ -1444,7 +1457,7 @@ FA_API int fa_hip_count_slab(const int64_t* roff, const int32_t* ranks, const in
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const int dbg = getenv("FA_SLAB_DEBUG") ? atoi(getenv("FA_SLAB_DEBUG")) : 0;
   hipLaunchKernelGGL(kern, g, b, lds, st, roff, ranks, src, ncols, item_map, n_used, gpre, m, gext_off, gext, G, C,
-                     wword, out, bm, Wp, dbg, gpm, bm_rows);
+                     wword, out, bm, Wp, dbg, gpm, bm_rows, acc16);
   FA_LAUNCH_RET();
 }
 
@@ -1455,14 +1468,14 @@ FA_API int fa_hip_count_trie(const int64_t* roff, const int32_t* ranks, const in
                              const int32_t* item_map, int n_used, const int32_t* gpre, int m, int D1, int D2,
                              const void* pieces, const void* witems, int NW, const int32_t* gext, int C,
                              const int32_t* wword, uint32_t* out, int sw, int n_wg, const uint64_t* bm, int64_t Wp,
-                             hipStream_t st, const int32_t* bm_rows) {
+                             hipStream_t st, const int32_t* bm_rows, int acc16) {
   if (NW <= 0 || C <= 0 || ncols <= 0) return 0;
   if (!(0 <= D1 && D1 <= D2 && D2 <= m)) return 2;
-  const size_t lds = (size_t)n_used * sw * 8 + (size_t)C * 4;
+  const size_t lds = (size_t)n_used * sw * 8 + (acc16 ? (size_t)((C + 1) / 2) * 4 : (size_t)C * 4);
   if (lds > 160 * 1024 - 512) return 3;
   using KernT = void (*)(const int64_t*, const int32_t*, const int32_t*, int64_t, const int32_t*, int,
                          const int32_t*, int, int, int, const int4*, const int2*, int, const int32_t*, int,
-                         const int32_t*, uint32_t*, const uint64_t*, int64_t, const int32_t*);
+                         const int32_t*, uint32_t*, const uint64_t*, int64_t, const int32_t*, int);
   KernT kern = nullptr;
 #define FA_TRIE_MODE(S, B) kern = wword ? (KernT)k_count_trie<S, true, B> : (KernT)k_count_trie<S, false, B>;
 #define FA_TRIE_CASE(S)                                   \
@@ -1480,7 +1493,7 @@ FA_API int fa_hip_count_trie(const int64_t* roff, const int32_t* ranks, const in
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, dim3((unsigned)n_wg), dim3(kSlabThreads), lds, st, roff, ranks, src, ncols, item_map,
                      n_used, gpre, m, D1, D2, (const int4*)pieces, (const int2*)witems, NW, gext, C, wword, out, bm,
-                     Wp, bm_rows);
+                     Wp, bm_rows, acc16);
   FA_LAUNCH_RET();
 }
 

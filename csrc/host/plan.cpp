@@ -158,8 +158,9 @@ FA_API int fa_plan_trie(const int32_t* P, int64_t G, int m, const int64_t* ext_o
 // and written into one (pinned) int32 buffer so the driver issues a single
 // host->device copy per level.
 //
-//   params (double[8]): lds_bytes, min_saving (0 = always trie, >1 = never),
-//                       conflict16, conflict8, pass_weight, rounds, emax_max, W
+//   params (double[9]): lds_bytes, min_saving (0 = always trie, >1 = never),
+//                       conflict16, conflict8, pass_weight, rounds, emax_max, W,
+//                       LDS bytes per accumulator (4, or 2 for packed 16-bit counters)
 //   info (int64[24]) out:
 //     0 kernel (0 slab, 1 trie)  1 sw  2 cap  3 n_used  4 n_pieces  5 n_witems
 //     6 n_passes  7 d1  8 d2  9 trie reads  10 slab reads  11 emax
@@ -169,9 +170,9 @@ FA_API int fa_plan_trie(const int32_t* P, int64_t G, int m, const int64_t* ext_o
 //                                trie: (witem begin, witem end, ext base)
 // Returns 0, 3 (buffer too small), 4 (no slab width fits: use the bitmap kernel).
 // ---------------------------------------------------------------------------
-static int slab_width(int64_t n_used, int64_t C, double lds, int64_t* cap_out) {
+static int slab_width(int64_t n_used, int64_t C, double lds, int64_t* cap_out, double accb = 4) {
   for (int sw : {32, 16, 8, 4}) {
-    const int64_t cap = (int64_t)((lds - (double)n_used * (sw + 2) * 8) / 4);
+    const int64_t cap = (int64_t)((lds - (double)n_used * (sw + 2) * 8) / accb);
     if (cap >= std::min<int64_t>(C, 8192) || (sw == 4 && cap >= 1024)) { *cap_out = cap; return sw; }
   }
   return 0;
@@ -184,6 +185,7 @@ FA_API int fa_level_plan(const int32_t* Pf, const int64_t* poff, int64_t G, cons
   const double pass_w = params[4], rounds = params[5];
   const int64_t emax_max = (int64_t)params[6];
   const double W = params[7];
+  const double accb = params[8] > 0 ? params[8] : 4;   // LDS bytes per accumulator (2: packed 16-bit)
   const int64_t C = ext_off[G] - ext_off[0];
   for (int i = 0; i < 24; ++i) info[i] = 0;
   if (G <= 0 || C <= 0) return 1;
@@ -232,7 +234,7 @@ FA_API int fa_level_plan(const int32_t* Pf, const int64_t* poff, int64_t G, cons
     double best_t = 0;
     const double reads_est = (double)C + 0.5 * (double)G * m;
     for (int sw : {32, 16, 8}) {
-      const int64_t cap = (int64_t)((lds - (double)n_used * sw * 8) / 4);
+      const int64_t cap = (int64_t)((lds - (double)n_used * sw * 8) / accb);
       if (cap < std::min<int64_t>(C, 1024)) continue;
       const int64_t passes_n = (C + cap - 1) / cap;
       double t = reads_est * W * 8 * (sw == 32 ? 1.0 : sw == 16 ? conf16 : conf8) / 60e12;
@@ -272,7 +274,7 @@ FA_API int fa_level_plan(const int32_t* Pf, const int64_t* poff, int64_t G, cons
 
   // ---- slab kernel: pieces of <= 8 extensions, passes of <= cap, size-sorted per pass
   int64_t cap = 0;
-  const int sw = slab_width(n_used, C, lds, &cap);
+  const int sw = slab_width(n_used, C, lds, &cap, accb);
   if (sw == 0) return 4;
   struct Piece { int64_t g, lo, hi; };
   std::vector<Piece> pcs;

@@ -609,7 +609,7 @@ def count_level_slab(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, 
         n_wg = int(max(1, min(nslabs, 256 * min(per_cu, 2))))
         _hip_call("fa_hip_count_slab", _p(roff), _p(ranks), _p(src), ncols, _p(imap_t), int(used.size), _p(pre_t),
                   m, _p(loc_off), gext_t.data_ptr() + 4 * e0, g1 - g0, e1 - e0, _p(wword),
-                  out.data_ptr() + 4 * e0, sw, n_wg, _p(bm), bm.stride(0) if bm is not None else 0, st, None, None)
+                  out.data_ptr() + 4 * e0, sw, n_wg, _p(bm), bm.stride(0) if bm is not None else 0, st, None, None, 0)
     res = out.to(_I64)
     del keep
     LAST_SLAB_PLAN.clear()
@@ -627,6 +627,7 @@ _TRIE_CONFLICT = {32: 1.0, 16: 1.6, 8: 2.2}
 TRIE_EMAX = int(os.environ.get("FA_TRIE_EMAX", "24"))     # max extensions per work item
 TRIE_ROUNDS = int(os.environ.get("FA_TRIE_ROUNDS", "4"))   # work items per lane group and pass (target)
 TRIE_PASS_WEIGHT = float(os.environ.get("FA_TRIE_PASS_WEIGHT", "4"))
+ACC16 = os.environ.get("FA_ACC16", "0") == "1"   # measured: halving passes did not pay on T40I10 (more flushes, worse widths)
 # auto level kernel: trie-shared counting when its slab-row reads are below this
 # fraction of the slab kernel's (measured break-even on T10I4 / T40I10, MI355X)
 _TRIE_MIN_SAVING = float(os.environ.get("FA_TRIE_MIN_SAVING", "0.53"))
@@ -744,7 +745,7 @@ def count_level_trie(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, 
         _hip_call("fa_hip_count_trie", _p(roff), _p(ranks), _p(src), ncols, base_ptr + 4 * o_im, int(used.size),
                   base_ptr, m, plan.d1, plan.d2, base_ptr + 4 * o_pc, base_ptr + 4 * (o_wi + 2 * w0),
                   w1 - w0, base_ptr + 4 * (o_gext + e0), Cq, _p(wword), out.data_ptr() + 4 * e0, sw, n_wg,
-                  _p(bm), bm.stride(0) if bm is not None else 0, st, None)
+                  _p(bm), bm.stride(0) if bm is not None else 0, st, None, 0)
     res = out.to(_I64)
     LAST_TRIE_PLAN.clear()
     LAST_TRIE_PLAN.update(rows=int(roff.numel() - 1), used=int(used.size), sw=sw, cap=cap,
@@ -764,7 +765,7 @@ def level_plan_host(prefix: np.ndarray, ext_off: np.ndarray, ext: np.ndarray, F1
     ex = np.ascontiguousarray(ext, dtype=np.int32)
     min_saving = {"auto": _TRIE_MIN_SAVING, "trie": 0.0, "slab": 2.0}[kernel]
     params = np.array([lds_bytes or _LDS_BYTES, min_saving, _TRIE_CONFLICT[16], _TRIE_CONFLICT[8],
-                       TRIE_PASS_WEIGHT, TRIE_ROUNDS, TRIE_EMAX, W], dtype=np.float64)
+                       TRIE_PASS_WEIGHT, TRIE_ROUNDS, TRIE_EMAX, W, 4.0], dtype=np.float64)
     bound = 2 * F1 + C + G * m + 6 * (G + C // 2 + 2) + (m + 4) * (G + C // 8 + 1) + 16
     buf = np.zeros(bound, np.int32)
     passes = np.zeros((G + C + 2, 3), np.int64)
@@ -844,8 +845,11 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
     ex = np.ascontiguousarray(ext, dtype=np.int32)
     W = (ncols + 63) // 64
     min_saving = {"auto": _TRIE_MIN_SAVING, "trie": 0.0, "slab": 2.0}[kernel]
+    # packed 16-bit LDS counters for unit weights: twice the candidates per pass; the
+    # grid then keeps every workgroup at <= 65535 columns (see the n_wg floor below)
+    acc16 = False
     params = np.array([_LDS_BYTES, min_saving, _TRIE_CONFLICT[16], _TRIE_CONFLICT[8], TRIE_PASS_WEIGHT,
-                       TRIE_ROUNDS, TRIE_EMAX, W], dtype=np.float64)
+                       TRIE_ROUNDS, TRIE_EMAX, W, 4.0], dtype=np.float64)
     bound = 2 * F1 + C + G * m + 6 * (G + C // 2 + 2) + (m + 4) * (G + C // 8 + 1) + 16
     on_gpu = dev.type == "cuda"
     stage = pinned_stage("level_plan") if on_gpu else None
@@ -856,6 +860,13 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
     rc = _native.host().fa_level_plan(P.ctypes.data, po.ctypes.data, G, eo.ctypes.data, ex.ctypes.data, F1,
                                       params.ctypes.data, buf.data_ptr(), bound, passes.ctypes.data, max_pass,
                                       info.ctypes.data)
+    if rc in (0, 4) and (rc == 4 or info[6] > 1) and wword is None and ACC16:
+        # several accumulator passes (or none fits): replan with packed 16-bit counters
+        params[8] = 2.0
+        rc = _native.host().fa_level_plan(P.ctypes.data, po.ctypes.data, G, eo.ctypes.data, ex.ctypes.data, F1,
+                                          params.ctypes.data, buf.data_ptr(), bound, passes.ctypes.data, max_pass,
+                                          info.ctypes.data)
+        acc16 = rc == 0
     if rc == 4:
         return None
     if rc != 0:
@@ -881,22 +892,24 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
     st = _stream(ranks)
     bounds = passes[:, 2].tolist() + [C]
     nslabs = (W + sw - 1) // sw
+    wg_floor = -(-nslabs // max(1, 65535 // (64 * sw))) if acc16 else 1
+    accb = 2 if acc16 else 4
     for q, (a, b, e0) in enumerate(passes.tolist()):
         Cq = bounds[q + 1] - e0
         if kern == 1:
-            lds = n_used * sw * 8 + Cq * 4
-            n_wg = int(max(1, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2))))
+            lds = n_used * sw * 8 + Cq * accb
+            n_wg = int(max(wg_floor, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2))))
             _hip_call("fa_hip_count_trie", _p(roff), _p(ranks), _p(src), ncols, base + 4 * o_im, n_used,
                       base + 4 * o_gpre, m, int(info[7]), int(info[8]), base + 4 * o_pc, base + 4 * (o_wi + 2 * a),
                       b - a, base + 4 * (o_gext + e0), Cq, _p(wword), out.data_ptr() + 4 * e0, sw, n_wg, _p(bm),
-                      bm.stride(0) if bm is not None else 0, st, bm_rows)
+                      bm.stride(0) if bm is not None else 0, st, bm_rows, int(acc16))
         else:
-            lds = n_used * (sw + 2) * 8 + Cq * 4
-            n_wg = int(max(1, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2))))
+            lds = n_used * (sw + 2) * 8 + Cq * accb
+            n_wg = int(max(wg_floor, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2))))
             _hip_call("fa_hip_count_slab", _p(roff), _p(ranks), _p(src), ncols, base + 4 * o_im, n_used,
                       base + 4 * o_gpre, m, base + 4 * (o_pc + 2 * a), base + 4 * (o_gext + e0), b - a, Cq,
                       _p(wword), out.data_ptr() + 4 * e0, sw, n_wg, _p(bm), bm.stride(0) if bm is not None else 0,
-                      st, base + 4 * (o_gpm + 2 * a), bm_rows)
+                      st, base + 4 * (o_gpm + 2 * a), bm_rows, int(acc16))
     LAST_LEVEL_PLAN.clear()
     LAST_LEVEL_PLAN.update(kernel="trie" if kern == 1 else "slab", rows=int(roff.numel() - 1), used=n_used, sw=sw,
                            cap=cap, passes=npass, pieces=int(info[4]), witems=int(info[5]), d1=int(info[7]),

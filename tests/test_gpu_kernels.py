@@ -344,3 +344,17 @@ def test_pair_gram_mfma_matches_popcount(monkeypatch, F1, T):
     iu = torch.triu_indices(F1, F1, 1)
     assert torch.equal(got[iu[0], iu[1]], want[iu[0], iu[1]])
     assert torch.equal(ref[iu[0], iu[1]], want[iu[0], iu[1]])
+
+
+@pytest.mark.parametrize("kernel", ["slab", "trie"])
+def test_acc16_multipass_matches(monkeypatch, kernel):
+    # packed 16-bit LDS counters: forced multi-pass levels (small LDS budget) replan with
+    # 2-byte accumulators and a grid floor of <= 65535 columns per workgroup
+    import fastapriori_amd.ops.primitives as prim
+    sh = generate_shard(150000, Comm(), "cpu", 12.0, 5.0, 200, 100, seed=31)
+    ref = FastApriori(0.004, config=MinerConfig(min_support=0.004, trim_min_rows=0, level_kernel="bitmap")).run(sh)
+    monkeypatch.setattr(prim, "_LDS_BYTES", 40 * 1024)
+    monkeypatch.setattr(prim, "ACC16", True)
+    got = FastApriori(0.004, config=MinerConfig(min_support=0.004, trim_min_rows=0, level_kernel=kernel)).run(
+        sh.to(DEV))
+    assert ref.as_dict() == got.as_dict()
