@@ -301,11 +301,12 @@ FA_API int fa_level_plan(const int32_t* Pf, const int64_t* poff, int64_t G, cons
     while (j < NP && pcs[j].hi - base <= cap) ++j;
     if (j == i) j = i + 1;   // a single piece always fits (<= 8 extensions)
     if (npass >= max_pass) return 3;
+    // stable order by extension count (8..0, descending): counting sort
+    int64_t bucket[10] = {0};
+    for (int64_t k = i; k < j; ++k) bucket[8 - (pcs[k].hi - pcs[k].lo) + 1] += 1;
+    for (int b = 1; b < 10; ++b) bucket[b] += bucket[b - 1];
     ord.resize((size_t)(j - i));
-    for (int64_t k = 0; k < j - i; ++k) ord[k] = i + k;
-    std::stable_sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) {
-      return pcs[a].hi - pcs[a].lo > pcs[b].hi - pcs[b].lo;
-    });
+    for (int64_t k = i; k < j; ++k) ord[bucket[8 - (pcs[k].hi - pcs[k].lo)]++] = k;
     for (int64_t k = 0; k < j - i; ++k) {
       const Piece& pc = pcs[ord[k]];
       const int64_t mg = poff[pc.g + 1] - poff[pc.g];
