@@ -522,7 +522,7 @@ class FastApriori:
             pc = ops.pair_counts_horizontal(roff, ranks, wrow, F1, db.get("long_rows", True))
         iu = torch.triu_indices(F1, F1, 1, device=pc.device)
         flat = pc[iu[0], iu[1]].contiguous()
-        self.comm.all_reduce_(flat)
+        self.comm.all_reduce_(flat, bound=self.stats["n_lines"])
         keep = torch.nonzero(flat >= mc).flatten()
         rows = torch.stack([iu[0][keep], iu[1][keep]], 1).to(torch.int32).cpu().numpy()
         cnt = flat[keep].cpu().numpy().astype(np.int64)
@@ -607,7 +607,7 @@ class FastApriori:
                               db["wword"], kernel="slab", poff=poff, full_bm=lambda: self._bitmaps(db))
         if cnt is None:
             return [self._count_level(db, pv, pi, eo, ex) for _, pv, pi, eo, ex in bundle]
-        self.dcomm.all_reduce_(cnt)
+        self.dcomm.all_reduce_(cnt, bound=self.stats["n_lines"])
         c = cnt.cpu().numpy()
         return np.split(c, np.cumsum(sizes)[:-1])
 
@@ -626,7 +626,7 @@ class FastApriori:
                 part = self._count_groups(db, prev, prefix_idx[g0:g1], ext_off[g0:g1 + 1] - e0, ext[e0:e1])
             full = torch.zeros(C, dtype=torch.int64, device=self.comm.device)
             full[e0:e1] = torch.from_numpy(part).to(full.device)
-            self.comm.all_reduce_(full)
+            self.comm.all_reduce_(full, bound=self.stats["n_lines"])
             return full.cpu().numpy()
         cnt = self._count_groups(db, prev, prefix_idx, ext_off, ext)
         return cnt
@@ -640,13 +640,13 @@ class FastApriori:
             cnt = ops.count_level(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"], prev[prefix_idx],
                                   ext_off, ext, db["wword"], kernel=lk, full_bm=lambda: self._bitmaps(db))
             if cnt is not None:
-                self.dcomm.all_reduce_(cnt)
+                self.dcomm.all_reduce_(cnt, bound=self.stats["n_lines"])
                 return cnt.cpu().numpy()
         self._bitmaps(db)
         prefix = torch.from_numpy(np.ascontiguousarray(prev[prefix_idx], dtype=np.int32)).to(dev)
         ext_t = torch.from_numpy(np.ascontiguousarray(ext, dtype=np.int32)).to(dev)
         cnt = ops.count_candidates(db["bm"], db["W"], prefix, ext_off, ext_t, db["wword"])
-        self.dcomm.all_reduce_(cnt)
+        self.dcomm.all_reduce_(cnt, bound=self.stats["n_lines"])
         return cnt.cpu().numpy()
 
 

@@ -6,9 +6,12 @@ Reference: AssociationRules.scala (class AssociationRules, :17-190).
   -------------------------------------------------  -----------------------------------------------
   removeRedundancy: zipWithIndex, map to rank sets,  native parse of this rank's U.dat byte range,
     reduceByKey dedup, collectAsMap (:33-64)         LUT to ranks on the device (empty -> "0")
-  genRules: linear scan for S - {s} (:122-145)       C++ subset index by binary search
-  cut, level by level (:147-182)                     C++ hash lookups of the kept lower level
-  sortWith(conf desc, token.toInt) (:74, :116-120)   C++ stable sort with precomputed tie positions
+  genRules: linear scan for S - {s} (:122-145)       HIP subset index: one thread per (S, position)
+                                                     binary-searches level k-1 (csrc/hip/rules.hip)
+  cut, level by level (:147-182)                     HIP dense lookup of the child rule through the
+                                                     subset index (no hash table, no broadcast)
+  sortWith(conf desc, token.toInt) (:74, :116-120)   device stable sorts on a packed key; HIP emit
+                                                     (CPU runs: the same in C++, csrc/host/rules.cpp)
   per-basket first-match scan (:80-106)              HIP: one wave per basket, 64 rules per step,
                                                      __ballot + ffs for the earliest match
   collect to driver + saveRecommends                 gather of rank ids to rank 0
@@ -32,10 +35,13 @@ from .data import MiningResult, TransactionShard, Vocabulary
 
 
 class AssociationRules:
-    def __init__(self, result: MiningResult, comm: Comm | None = None, logger: Logger | None = None):
+    def __init__(self, result: MiningResult, comm: Comm | None = None, logger: Logger | None = None,
+                 device: torch.device | str | None = None):
         self.result = result
         self.comm = comm or Comm()
         self.log = logger or Logger(self.comm.rank)
+        # rules are built where the job runs: the GPU kernels on a GPU rank, C++ on a CPU one
+        self.device = torch.device(device) if device is not None else self.comm.device
         self._rules: RuleTable | None = None
         self._rules_dev = None
 
@@ -46,7 +52,13 @@ class AssociationRules:
             order = sorted(range(len(items)), key=lambda r: rule_tiebreak_key(items[r]))
             tie_pos = np.empty(len(items), dtype=np.int64)
             tie_pos[np.asarray(order, dtype=np.int64)] = np.arange(len(items), dtype=np.int64)
-            self._rules = rules_build(self.result.levels, self.result.counts, tie_pos)
+            if self.device.type == "cuda":
+                d = ops.primitives.rules_build_device(self.result.levels, self.result.counts, tie_pos, self.device)
+                self._rules = RuleTable(d["ante_off"].cpu().numpy(), d["ante"].cpu().numpy(),
+                                        d["cons"].cpu().numpy(), d["conf"].cpu().numpy(), d["level_stats"])
+                self._rules_dev = (self.device, d["ante_off"], d["ante"], d["cons"])
+            else:
+                self._rules = rules_build(self.result.levels, self.result.counts, tie_pos)
             for size, before, after in self._rules.level_stats[1:]:
                 self.log.line(f"Before cut level {size} Nums: {before}")
                 self.log.line(f"After cut level {size} Nums: {after}")

@@ -978,3 +978,83 @@ def recommend(ante_off, ante, cons, F1: int, boff, bask) -> torch.Tensor:
     _native.host().fa_recommend_cpu(_p(ante_off), _p(ante), _p(cons), R, F1, _p(boff), _p(bask), M, _p(out),
                                     num_threads())
     return out
+
+
+def rules_build_device(levels: list, counts: list, tie_pos: np.ndarray, dev) -> dict:
+    """Association rules on the GPU (csrc/hip/rules.hip; AssociationRules.scala:116-182).
+
+    levels[k-1]: int32 [n_k, k] lexicographically sorted itemsets, counts[k-1] their
+    supports.  Returns device tensors ante_off int64 [R+1], ante int32, cons int32 [R],
+    conf float64 [R] in recommendation order, plus level_stats [(antecedent size,
+    before cut, after cut)] — the same table as the host builder (ops.host.rules_build).
+    """
+    K = len(levels)
+    empty = dict(ante_off=torch.zeros(1, dtype=_I64, device=dev), ante=torch.zeros(0, dtype=_I32, device=dev),
+                 cons=torch.zeros(0, dtype=_I32, device=dev), conf=torch.zeros(0, dtype=torch.float64, device=dev),
+                 level_stats=[])
+    if K < 2 or len(levels[1]) == 0:
+        return empty
+    lv = [np.ascontiguousarray(l, dtype=np.int32).reshape(-1) for l in levels]
+    base = np.zeros(K + 2, dtype=np.int64)            # base[m]: offset of the size-m level
+    np.cumsum([l.size for l in lv], out=base[2:K + 2])
+    rows_all = torch.from_numpy(np.concatenate(lv)).to(dev)
+    cbase = np.zeros(K + 1, dtype=np.int64)
+    np.cumsum([len(c) for c in counts], out=cbase[1:])
+    cnt_all = torch.from_numpy(np.concatenate([np.asarray(c, dtype=np.int64) for c in counts])).to(dev)
+    st = _stream(rows_all)
+    lib = _native.hip()
+
+    def rows(m):
+        return rows_all.data_ptr() + int(base[m]) * 4
+
+    def cnts(m):
+        return cnt_all.data_ptr() + int(cbase[m - 1]) * 8
+
+    kept_prev = conf_prev = None
+    parts = []          # per level: (flat rule ids kept, conf, sub)
+    stats = []
+    for k in range(2, K + 1):
+        nS, nA = len(levels[k - 1]), len(levels[k - 2])
+        if nS == 0:
+            break
+        sub = torch.empty(nS * k, dtype=_I32, device=dev)
+        conf = torch.empty(nS * k, dtype=torch.float64, device=dev)
+        _native.check(lib.fa_hip_rule_gen(rows(k), nS, k, rows(k - 1), nA, cnts(k), cnts(k - 1), _p(sub), _p(conf),
+                                          st), "fa_hip_rule_gen")
+        if k == 2:
+            kept = torch.ones(nS * k, dtype=torch.uint8, device=dev)
+        else:
+            kept = torch.empty(nS * k, dtype=torch.uint8, device=dev)
+            _native.check(lib.fa_hip_rule_cut(_p(sub), _p(conf), nS, k, _p(kept_prev), _p(conf_prev), _p(kept), st),
+                          "fa_hip_rule_cut")
+        ids = torch.nonzero(kept).flatten()
+        parts.append((k, ids, conf, sub))
+        stats.append((k - 1, nS * k, ids.numel()))
+        kept_prev, conf_prev = kept, conf
+    conf_r = torch.cat([c[i] for _, i, c, _ in parts])
+    R = conf_r.numel()
+    if R == 0:
+        return dict(empty, level_stats=stats)
+    cons_r = torch.cat([rows_all[int(base[k]):int(base[k + 1])][i] for k, i, _, _ in parts])
+    ante_idx = torch.cat([s[i] for _, i, _, s in parts])
+    msz = torch.cat([torch.full((i.numel(),), k - 1, dtype=_I32, device=dev) for k, i, _, _ in parts])
+    tie = torch.from_numpy(np.ascontiguousarray(tie_pos, dtype=np.int64)).to(dev)[cons_r.to(_I64)]
+    # total order: conf desc, consequent tie position, antecedent size, antecedent index
+    key = (msz.to(_I64) << 32) | ante_idx.to(_I64)
+    if len(tie_pos) < (1 << 24) and K < 128:
+        key = key | (tie << 39)
+        o = torch.argsort(key)
+    else:
+        o = torch.argsort(key)
+        o = o[torch.argsort(tie[o], stable=True)]
+    o = o[torch.sort(conf_r[o], descending=True, stable=True)[1]]
+    msz_s, idx_s = msz[o].contiguous(), ante_idx[o].contiguous()
+    ante_off = torch.zeros(R + 1, dtype=_I64, device=dev)
+    torch.cumsum(msz_s.to(_I64), 0, out=ante_off[1:])
+    nante = int(ante_off[-1].item())
+    ante = torch.empty(nante, dtype=_I32, device=dev)
+    base_t = torch.from_numpy(base).to(dev)
+    _native.check(lib.fa_hip_rule_emit(_p(rows_all), _p(base_t), _p(msz_s), _p(idx_s), _p(ante_off), R, _p(ante), st),
+                  "fa_hip_rule_emit")
+    return dict(ante_off=ante_off, ante=ante, cons=cons_r[o].contiguous(), conf=conf_r[o].contiguous(),
+                level_stats=stats)

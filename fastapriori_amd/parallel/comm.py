@@ -47,13 +47,20 @@ class Comm:
     def _comm_device(self) -> torch.device:
         return self.device if self.backend == "nccl" else torch.device("cpu")
 
-    def all_reduce_(self, t: torch.Tensor, op=None) -> torch.Tensor:
-        """In-place sum (or ``op``) across ranks; returns the tensor on its own device."""
+    def all_reduce_(self, t: torch.Tensor, op=None, bound: int | None = None) -> torch.Tensor:
+        """In-place sum (or ``op``) across ranks; returns the tensor on its own device.
+
+        ``bound``: an upper bound of every reduced value (support counts never exceed
+        the global number of lines).  Below 2**31 an int64 vector travels as int32,
+        halving the bytes on the xGMI links."""
         if not self.distributed:
             return t
         op = op or dist.ReduceOp.SUM
         dev = self._comm_device()
-        x = t if t.device == dev else t.to(dev)
+        if bound is not None and t.dtype == torch.int64 and 0 <= bound < (1 << 31):
+            x = t.to(device=dev, dtype=torch.int32)
+        else:
+            x = t if t.device == dev else t.to(dev)
         flat = x.view(-1)
         nbytes = flat.numel() * flat.element_size()
         self.bytes_reduced += nbytes

@@ -171,6 +171,28 @@ def test_recommend_kernel():
     assert torch.equal(ref, got)
 
 
+@pytest.mark.parametrize("seed,min_sup", [(9, 0.01), (11, 0.004)])
+def test_rules_device_matches_host(seed, min_sup):
+    # subset index, level-wise cut, ordering and antecedent emission on the GPU
+    # against the C++ builder, on a mined result with several levels
+    from fastapriori_amd.models.rules import AssociationRules
+    sh = generate_shard(30000, Comm(), "cpu", 10.0, 4.0, 60, 80, seed=seed)
+    res = FastApriori(min_sup, config=MinerConfig(min_support=min_sup)).run(sh)
+    assert len(res.levels) >= 4
+    host = AssociationRules(res).rules()
+    dev = AssociationRules(res, device=DEV)
+    got = dev.rules()
+    assert got.n_rules == host.n_rules > 0
+    assert np.array_equal(got.ante_off, host.ante_off)
+    assert np.array_equal(got.ante, host.ante)
+    assert np.array_equal(got.cons, host.cons)
+    assert np.array_equal(got.conf, host.conf)
+    assert got.level_stats == host.level_stats
+    users = generate_shard(3000, Comm(), "cpu", 8.0, 3.0, 60, 80, seed=seed, users=True)
+    ref = AssociationRules(res).recommend_shard(users)
+    assert torch.equal(dev.recommend_shard(users.to(DEV)).cpu(), ref)
+
+
 def test_parse_to_device_roundtrip():
     sh = parse_bytes(b"1 2 3\n\n4 4 5\n", device=DEV)
     assert sh.items.is_cuda and sh.n_lines == 3
