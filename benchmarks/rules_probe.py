@@ -42,6 +42,24 @@ def main():
         out[name + "_ms"] = round(best * 1e3, 2)
         out[name + "_rules"] = rt.n_rules
         out[name + "_sig"] = int(np.asarray(rt.cons, dtype=np.int64).sum() + rt.ante.astype(np.int64).sum())
+    users = generate_shard(max(n // 100, 1000), Comm(device=dev), dev, L, I, P, N, 1, users=True)
+    ar = AssociationRules(res, logger=Logger(enabled=False), device=dev)
+    ar.rules()
+    recs = {}
+    for name, idx in (("recommend_indexed", True), ("recommend_scan", False)):
+        ar.use_index = idx
+        best = 1e9
+        for _ in range(a.reps):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            r = ar.recommend_shard(users)
+            torch.cuda.synchronize()
+            best = min(best, time.perf_counter() - t)
+        out[name + "_ms"] = round(best * 1e3, 2)
+        recs[name] = r.cpu()
+    out["users"] = users.n_lines
+    out["recommend_agree"] = bool(torch.equal(recs["recommend_indexed"], recs["recommend_scan"]))
+    out["users_with_rec"] = int((recs["recommend_indexed"] >= 0).sum())
     print(json.dumps(out), flush=True)
 
 

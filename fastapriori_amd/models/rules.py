@@ -13,7 +13,9 @@ Reference: AssociationRules.scala (class AssociationRules, :17-190).
   sortWith(conf desc, token.toInt) (:74, :116-120)   device stable sorts on a packed key; HIP emit
                                                      (CPU runs: the same in C++, csrc/host/rules.cpp)
   per-basket first-match scan (:80-106)              HIP: one wave per basket, 64 rules per step,
-                                                     __ballot + ffs for the earliest match
+                                                     __ballot + ffs for the earliest match; big rule
+                                                     tables scan only the per-item rule lists of the
+                                                     basket's items (k_recommend_indexed)
   collect to driver + saveRecommends                 gather of rank ids to rank 0
 
 Divergences (documented): when there are no rules at all the reference throws
@@ -44,6 +46,7 @@ class AssociationRules:
         self.device = torch.device(device) if device is not None else self.comm.device
         self._rules: RuleTable | None = None
         self._rules_dev = None
+        self.use_index = True      # per-item rule lists for big rule tables (k_recommend_indexed)
 
     # ------------------------------------------------------------------
     def rules(self) -> RuleTable:
@@ -106,8 +109,13 @@ class AssociationRules:
         if self._rules_dev is None or self._rules_dev[0] != dev:
             self._rules_dev = (dev, torch.from_numpy(rt.ante_off).to(dev), torch.from_numpy(rt.ante).to(dev),
                                torch.from_numpy(rt.cons).to(dev))
-        _, a_off, ante, cons = self._rules_dev
-        return ops.recommend(a_off, ante, cons, len(self.result.items), boff, bask)
+        _, a_off, ante, cons = self._rules_dev[:4]
+        index = None
+        if dev.type == "cuda" and cons.numel() >= ops.primitives.RECOMMEND_INDEX_MIN_RULES and self.use_index:
+            if len(self._rules_dev) == 4:
+                self._rules_dev = self._rules_dev + (ops.primitives.recommend_index(a_off, ante, len(self.result.items)),)
+            index = self._rules_dev[4]
+        return ops.recommend(a_off, ante, cons, len(self.result.items), boff, bask, index=index)
 
     def run(self, users: TransactionShard) -> list[str] | None:
         """Recommendations for every U.dat line, in file order, on rank 0 (None elsewhere)."""

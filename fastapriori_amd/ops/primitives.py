@@ -960,8 +960,25 @@ def apriori_gen_device(prev: np.ndarray, F1: int, dev, want_rows: bool = False):
     return prefix_idx, ext_off, ext_h
 
 
-def recommend(ante_off, ante, cons, F1: int, boff, bask) -> torch.Tensor:
-    """First-match recommendation per basket -> int32 rank (or -1 for "0")."""
+RECOMMEND_INDEX_MIN_RULES = 2048
+
+
+def recommend_index(ante_off: torch.Tensor, ante: torch.Tensor, F1: int):
+    """Rule lists per item for k_recommend_indexed: rule r is listed under the last
+    (highest-rank) item of its antecedent, ids ascending.  -> (list_off int64 [F1+1],
+    list_rule int32 [R])."""
+    key = ante[ante_off[1:] - 1].to(_I64)
+    order = torch.argsort(key, stable=True).to(_I32)
+    list_off = torch.zeros(F1 + 1, dtype=_I64, device=ante.device)
+    torch.cumsum(torch.bincount(key, minlength=F1), 0, out=list_off[1:])
+    return list_off, order
+
+
+def recommend(ante_off, ante, cons, F1: int, boff, bask, index=None) -> torch.Tensor:
+    """First-match recommendation per basket -> int32 rank (or -1 for "0").
+
+    ``index``: (list_off, list_rule) from recommend_index — the per-item rule
+    lists that let a basket skip rules whose antecedent cannot be inside it."""
     M = boff.numel() - 1
     R = cons.numel()
     dev = bask.device
@@ -969,8 +986,13 @@ def recommend(ante_off, ante, cons, F1: int, boff, bask) -> torch.Tensor:
     if M <= 0 or R == 0:
         return out
     if bask.is_cuda:
-        rc = _native.hip().fa_hip_recommend(_p(ante_off), _p(ante), _p(cons), R, F1, _p(boff), _p(bask), M,
-                                            _p(out), _stream(bask))
+        if index is not None:
+            rc = _native.hip().fa_hip_recommend_indexed(_p(index[0]), _p(index[1]), _p(ante_off), _p(ante),
+                                                        _p(cons), R, F1, _p(boff), _p(bask), M, _p(out),
+                                                        _stream(bask))
+        else:
+            rc = _native.hip().fa_hip_recommend(_p(ante_off), _p(ante), _p(cons), R, F1, _p(boff), _p(bask), M,
+                                                _p(out), _stream(bask))
         if rc == 2:  # vocabulary too wide for an LDS bitset: host path
             return recommend(ante_off.cpu(), ante.cpu(), cons.cpu(), F1, boff.cpu(), bask.cpu()).to(dev)
         _native.check(rc, "fa_hip_recommend")

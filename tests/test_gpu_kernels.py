@@ -191,6 +191,20 @@ def test_rules_device_matches_host(seed, min_sup):
     users = generate_shard(3000, Comm(), "cpu", 8.0, 3.0, 60, 80, seed=seed, users=True)
     ref = AssociationRules(res).recommend_shard(users)
     assert torch.equal(dev.recommend_shard(users.to(DEV)).cpu(), ref)
+    # indexed (per-item rule lists) and plain ordered scans agree
+    import fastapriori_amd.ops.primitives as prim
+    ud = users.to(DEV)
+    old_min = prim.RECOMMEND_INDEX_MIN_RULES
+    try:
+        prim.RECOMMEND_INDEX_MIN_RULES = 1
+        dev.use_index = True
+        a = dev.recommend_shard(ud).cpu()
+        dev.use_index = False
+        b = dev.recommend_shard(ud).cpu()
+    finally:
+        prim.RECOMMEND_INDEX_MIN_RULES = old_min
+    assert torch.equal(a, ref) and torch.equal(b, ref)
+    assert (ref >= 0).any() and (ref < 0).any()
 
 
 def test_parse_to_device_roundtrip():
