@@ -91,6 +91,11 @@ _HIP_SIGS = {
     "fa_hip_count_candidates": (C.c_int, [vp, i64, i64, vp, C.c_int, vp, vp, vp, C.c_int, vp, vp, vp]),
     "fa_hip_recommend": (C.c_int, [vp, vp, vp, i64, i32, vp, vp, i64, vp, vp]),
     "fa_hip_recommend_indexed": (C.c_int, [vp, vp, vp, vp, vp, i64, i32, vp, vp, i64, vp, vp]),
+    "fa_hip_parse_tiles": (i64, [i64]),
+    "fa_hip_line_count": (C.c_int, [vp, i64, vp, vp]),
+    "fa_hip_line_ends": (C.c_int, [vp, i64, vp, vp, vp]),
+    "fa_hip_parse_lines": (C.c_int, [vp, vp, i64, vp, vp, vp, vp, vp, vp, vp]),
+    "fa_hip_compact_lines": (C.c_int, [vp, vp, vp, vp, vp, vp, vp, i64, vp, vp, vp]),
     "fa_hip_rule_gen": (C.c_int, [vp, i64, C.c_int, vp, i64, vp, vp, vp, vp, vp]),
     "fa_hip_rule_cut": (C.c_int, [vp, vp, i64, C.c_int, vp, vp, vp, vp]),
     "fa_hip_rule_emit": (C.c_int, [vp, vp, vp, vp, vp, i64, vp, vp]),

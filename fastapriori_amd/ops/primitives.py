@@ -1080,3 +1080,55 @@ def rules_build_device(levels: list, counts: list, tie_pos: np.ndarray, dev) -> 
                   "fa_hip_rule_emit")
     return dict(ante_off=ante_off, ante=ante, cons=cons_r[o].contiguous(), conf=conf_r[o].contiguous(),
                 level_stats=stats)
+
+
+def parse_numeric_device(buf: torch.Tensor, n: int, last_is_term: bool):
+    """Parse n file bytes already in HBM (csrc/hip/parse.hip).  ``buf`` is uint8,
+    padded with >= 64 zero bytes past a multiple of 64.  Returns (offsets int64
+    [nl+1], items int32, extras int32, vocab size), all on the device except the
+    vocab size, or None when a token is not canonical numeric (-> host parser)."""
+    dev = buf.device
+    st = _stream(buf)
+    lib = _native.hip()
+    if n <= 0:
+        return (torch.zeros(1, dtype=_I64, device=dev), torch.zeros(0, dtype=_I32, device=dev),
+                torch.zeros(0, dtype=_I32, device=dev), 0)
+    assert buf.numel() >= (n + 63) // 64 * 64 + 64 and buf.dtype == torch.uint8
+    tiles = int(lib.fa_hip_parse_tiles(n))
+    tile_cnt = torch.empty(tiles, dtype=_I32, device=dev)
+    _native.check(lib.fa_hip_line_count(_p(buf), n, _p(tile_cnt), st), "fa_hip_line_count")
+    tile_base = torch.zeros(tiles + 1, dtype=_I64, device=dev)
+    torch.cumsum(tile_cnt, 0, out=tile_base[1:])
+    n_term = int(tile_base[-1].item())
+    nl = n_term + (0 if last_is_term else 1)
+    ends = torch.empty(max(nl, 1), dtype=_I64, device=dev)
+    _native.check(lib.fa_hip_line_ends(_p(buf), n, _p(tile_base), _p(ends), st), "fa_hip_line_ends")
+    if not last_is_term:
+        ends[n_term] = n
+    ends = ends[:nl]
+    starts = torch.empty_like(ends)
+    starts[0] = 0
+    starts[1:] = ends[:-1] + 1
+    bound = torch.clamp((ends - starts + 1) // 2, min=1)
+    bound_off = torch.zeros(nl + 1, dtype=_I64, device=dev)
+    torch.cumsum(bound, 0, out=bound_off[1:])
+    nb = int(bound_off[-1].item())
+    scratch = torch.empty(nb, dtype=_I32, device=dev)
+    xscratch = torch.empty(nb, dtype=_I32, device=dev)
+    dcnt = torch.empty(nl, dtype=_I32, device=dev)
+    xcnt = torch.empty(nl, dtype=_I32, device=dev)
+    flags = torch.zeros(2, dtype=_I32, device=dev)
+    _native.check(lib.fa_hip_parse_lines(_p(buf), _p(ends), nl, _p(bound_off), _p(scratch), _p(xscratch), _p(dcnt),
+                                         _p(xcnt), _p(flags), st), "fa_hip_parse_lines")
+    off = torch.zeros(nl + 1, dtype=_I64, device=dev)
+    torch.cumsum(dcnt, 0, out=off[1:])
+    xoff = torch.zeros(nl + 1, dtype=_I64, device=dev)
+    torch.cumsum(xcnt, 0, out=xoff[1:])
+    info = torch.stack([flags[0].to(_I64), flags[1].to(_I64), off[-1], xoff[-1]]).cpu().tolist()
+    if info[0]:
+        return None
+    items = torch.empty(info[2], dtype=_I32, device=dev)
+    extras = torch.empty(info[3], dtype=_I32, device=dev)
+    _native.check(lib.fa_hip_compact_lines(_p(scratch), _p(xscratch), _p(bound_off), _p(dcnt), _p(xcnt), _p(off),
+                                           _p(xoff), nl, _p(items), _p(extras), st), "fa_hip_compact_lines")
+    return off, items, extras, int(info[1]) + 1

@@ -67,6 +67,110 @@ def parse_file(path: str, byte_begin: int = 0, byte_end: int = -1, mode: int = 0
     return txndb_to_shard(h, torch.device(device), line_base)
 
 
+# ---------------------------------------------------------------------------
+# Device parser path: the shard's bytes go to HBM (pread by host threads into a
+# ring of pinned slots, overlapped with the H2D copies) and are tokenised by
+# csrc/hip/parse.hip.  Numeric vocabularies only; anything else returns None and
+# the caller uses the host parser.
+GPU_PARSE = os.environ.get("FA_GPU_PARSE", "1") == "1"
+_RING_SLOT = 32 << 20
+_RING_SLOTS = 8
+_ring: list = []
+
+
+def _next_line_start(fd: int, size: int, pos: int) -> int:
+    """First line start >= pos (parse.cpp next_line_start): the byte after the first
+    terminator at or after pos - 1 ('\r\n' counts as one)."""
+    if pos <= 0:
+        return 0
+    i = pos - 1
+    while i < size:
+        blk = os.pread(fd, 1 << 16, i)
+        if not blk:
+            break
+        for k, c in enumerate(blk):
+            if c == 10:
+                return i + k + 1
+            if c == 13:
+                if i + k + 1 < size and os.pread(fd, 1, i + k + 1) == b"\n":
+                    return i + k + 2
+                return i + k + 1
+        i += len(blk)
+    return size
+
+
+def _file_to_device(fd: int, first: int, n: int, dev) -> torch.Tensor:
+    """Bytes [first, first + n) of the file -> uint8 device tensor padded with zeros
+    to a multiple of 64 plus 64."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    out = torch.empty((n + 63) // 64 * 64 + 64, dtype=torch.uint8, device=dev)
+    out[n:].zero_()
+    if n == 0:
+        return out
+    if not _ring:
+        _ring.extend(torch.empty(_RING_SLOT, dtype=torch.uint8, pin_memory=True) for _ in range(_RING_SLOTS))
+    nch = (n + _RING_SLOT - 1) // _RING_SLOT
+    events: list = [None] * _RING_SLOTS
+
+    def read_chunk(c: int) -> None:
+        ev = events[c % _RING_SLOTS]
+        if ev is not None:
+            ev.synchronize()          # the slot's previous H2D copy has finished
+        off = c * _RING_SLOT
+        m = min(_RING_SLOT, n - off)
+        mv = memoryview(_ring[c % _RING_SLOTS].numpy())
+        got = 0
+        while got < m:
+            r = os.preadv(fd, [mv[got:m]], first + off + got)
+            if r <= 0:
+                raise OSError(f"short read at {first + off + got}")
+            got += r
+
+    with ThreadPoolExecutor(min(num_threads(), _RING_SLOTS)) as ex:
+        fut = {c: ex.submit(read_chunk, c) for c in range(min(_RING_SLOTS, nch))}
+        for c in range(nch):
+            fut.pop(c).result()
+            s, off = c % _RING_SLOTS, c * _RING_SLOT
+            m = min(_RING_SLOT, n - off)
+            out[off:off + m].copy_(_ring[s][:m], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            events[s] = ev
+            if c + _RING_SLOTS < nch:
+                fut[c + _RING_SLOTS] = ex.submit(read_chunk, c + _RING_SLOTS)
+    return out
+
+
+def parse_file_device(path: str, byte_begin: int, byte_end: int, device, line_base: int = 0):
+    """Lines starting in [byte_begin, byte_end) parsed on the GPU, or None (non-numeric
+    tokens, or a CPU device)."""
+    from ..ops import primitives as prim
+
+    device = torch.device(device)
+    if device.type != "cuda":
+        return None
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        size = os.fstat(fd).st_size
+        b = max(0, min(byte_begin, size))
+        e = size if byte_end < 0 else max(b, min(byte_end, size))
+        first = _next_line_start(fd, size, b)
+        last = _next_line_start(fd, size, e) if e < size else size
+        last = max(last, first)
+        n = last - first
+        last_is_term = n == 0 or os.pread(fd, 1, last - 1) in (b"\n", b"\r")
+        buf = _file_to_device(fd, first, n, device)
+    finally:
+        os.close(fd)
+    got = prim.parse_numeric_device(buf, n, last_is_term)
+    del buf
+    if got is None:
+        return None
+    off, items, extras, vocab = got
+    return TransactionShard(off, items, extras.cpu().numpy(), Vocabulary(True, vocab), line_base)
+
+
 def parse_bytes(data: bytes, mode: int = 0, device="cpu") -> TransactionShard:
     h = _native.host().fa_parse_buffer(data, len(data), mode, num_threads())
     return txndb_to_shard(h, torch.device(device))
@@ -80,10 +184,13 @@ def read_shard(path: str, comm, device: torch.device | str | None = None) -> Tra
         raise FileNotFoundError(path)
     b = size * comm.rank // comm.world_size
     e = size * (comm.rank + 1) // comm.world_size
-    shard = parse_file(path, b, e, 0, "cpu")
+    shard = parse_file_device(path, b, e, device) if (GPU_PARSE and device.type == "cuda") else None
+    if shard is None:
+        # host parser, straight into pinned buffers when the shard goes to a GPU
+        shard = parse_file(path, b, e, 0, device)
     need_dict = comm.allreduce_int(0 if shard.vocab.numeric else 1, "max")
     if need_dict and shard.vocab.numeric:
-        shard = parse_file(path, b, e, 1, "cpu")
+        shard = parse_file(path, b, e, 1, device)
     counts = comm.all_gather_int(shard.n_lines)
     shard.line_base = int(sum(counts[: comm.rank]))
     return shard.to(device)

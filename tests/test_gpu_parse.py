@@ -1,0 +1,104 @@
+"""Device parser (csrc/hip/parse.hip) against the host parser (csrc/host/parse.cpp)
+on the same bytes and byte ranges: line splitting (\\n, \\r\\n, lone \\r, no final
+terminator), trim + split, blank lines, duplicate tokens (short lines and lines
+with more distinct tokens than the per-thread LDS column), and the fallback to
+the host parser for non-canonical or non-numeric tokens."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from fastapriori_amd.utils import io
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _same(path, b=0, e=-1):
+    got = io.parse_file_device(path, b, e, DEV)
+    ref = io.parse_file(path, b, e, 0, "cpu")
+    assert got is not None and ref.vocab.numeric
+    assert torch.equal(got.offsets.cpu(), ref.offsets)
+    assert torch.equal(got.items.cpu(), ref.items)
+    assert np.array_equal(got.extras, ref.extras)
+    assert got.vocab.size == ref.vocab.size
+    return got
+
+
+def _write(tmp_path, data: bytes, name="D.dat"):
+    p = os.path.join(tmp_path, name)
+    with open(p, "wb") as f:
+        f.write(data)
+    return p
+
+
+@pytest.mark.parametrize("data", [
+    b"1 2 3\n4 5\n",
+    b"1 2 3\n4 5",                       # no final terminator
+    b"1 2\r\n3 4\r\n\r\n5\r",              # CRLF, blank CRLF line, lone CR at EOF
+    b"1\r2\r\r3 3 3\n",                  # lone CRs, duplicates
+    b"\n\n  \t \n7\n",                   # blank and whitespace-only lines -> token ""
+    b"  9\t\t8 \x0b 7\x0c6  \n0 0 2147483646\n",
+    b"\x01 5 \x02\n",                    # control bytes trimmed at both ends
+    b"",
+    b"\n",
+])
+def test_device_parser_edge_cases(tmp_path, data):
+    p = _write(tmp_path, data)
+    if data:
+        _same(p)
+
+
+def test_long_lines_with_duplicates(tmp_path):
+    rng = np.random.default_rng(3)
+    lines = []
+    for L in (10, 63, 64, 65, 130, 400):
+        toks = rng.integers(0, 300, L)          # many repeats, > 64 distinct in the long ones
+        lines.append(" ".join(map(str, toks)))
+    p = _write(tmp_path, ("\n".join(lines) + "\n").encode())
+    g = _same(p)
+    assert g.extras.size > 0
+
+
+@pytest.mark.parametrize("data", [b"1 2\n007 3\n", b"1 2\nx y\n", b"1 2147483647\n", b"1 2\x013\n",
+                                  b"12345678901\n"])
+def test_non_numeric_falls_back(tmp_path, data):
+    p = _write(tmp_path, data)
+    assert io.parse_file_device(p, 0, -1, DEV) is None
+    assert not io.parse_file(p, 0, -1, 0, "cpu").vocab.numeric
+
+
+def test_random_files_and_byte_ranges(tmp_path):
+    rng = np.random.default_rng(11)
+    terms = [b"\n", b"\r\n", b"\r"]
+    seps = [b" ", b"\t", b"  ", b" \t "]
+    parts = []
+    for _ in range(3000):
+        L = int(rng.integers(0, 25))
+        toks = [str(int(v)).encode() for v in rng.integers(0, 50 if rng.random() < 0.5 else 5000, L)]
+        line = b""
+        for t in toks:
+            line += t + seps[int(rng.integers(0, len(seps)))]
+        if rng.random() < 0.2:
+            line = b" " + line
+        parts.append(line + terms[int(rng.integers(0, len(terms)))])
+    data = b"".join(parts)
+    p = _write(tmp_path, data)
+    _same(p)
+    size = len(data)
+    cuts = sorted(set([0, size] + [int(x) for x in rng.integers(0, size, 9)]))
+    total = 0
+    for b, e in zip(cuts[:-1], cuts[1:]):
+        total += _same(p, b, e).n_lines
+    assert total == io.parse_file(p, 0, -1, 0, "cpu").n_lines
+
+
+def test_read_shard_uses_device_parser(tmp_path, monkeypatch):
+    from fastapriori_amd.parallel.comm import Comm
+    p = _write(tmp_path, b"1 2 3\n2 3\n3 4 4\n" * 1000)
+    calls = []
+    orig = io.parse_file_device
+    monkeypatch.setattr(io, "parse_file_device", lambda *a, **k: calls.append(1) or orig(*a, **k))
+    sh = io.read_shard(p, Comm(device=DEV), DEV)
+    assert calls and sh.items.is_cuda and sh.n_lines == 3000 and sh.extras.size == 1000
