@@ -210,3 +210,82 @@ FA_API int fa_hip_ag_gen(const int32_t* P, int64_t n, int m, int F1, void* ws, i
   sizes[0] = C;
   FA_LAUNCH_RET();
 }
+
+// Speculative level chain for level bundling (fastapriori_amd FastApriori._plan_bundle):
+// starting from level k's candidate rows P0 [n0][m0] (device), generate level
+// k+1 from them, then k+2 from those, ... on the stream, with one 8-byte
+// readback per level (its candidate count) instead of a host round trip per
+// level.  A level is accepted while C > 0, C <= growth * C_prev, the bundle
+// total stays <= tmax (the slab accumulator capacity) and fewer than
+// max_levels were accepted; the first rejected level ends the chain.
+//   sizes[0] = accepted levels L; sizes[2 + l] = C_l;  rc 5 / 6: sizes[1] = bytes of
+//   workspace / int32 of host buffer to retry with.
+//   host, per accepted level l: cnt [n_l] | ext [C_l] | rows [C_l][m_l + 1]
+//   (n_{l+1} = C_l, m_{l+1} = m_l + 1).
+FA_API int fa_hip_ag_chain(const int32_t* P0, int64_t n0, int m0, int F1, void* ws, int64_t ws_bytes, int32_t* host,
+                           int64_t host_cap, int max_levels, double growth, int64_t total0, int64_t tmax,
+                           int64_t* sizes, hipStream_t st) {
+  sizes[0] = 0;
+  if (n0 <= 0 || max_levels <= 0) return 0;
+  if (m0 < 2 || F1 > 4096) return 1;
+  const int nw = (F1 + 63) / 64;
+  auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
+  char* const w0 = static_cast<char*>(ws);
+  char* w = w0;
+  const int32_t* P = P0;
+  int64_t n = n0, last = n0, total = total0, hoff = 0;
+  int m = m0, L = 0;
+  int64_t* Cdev = nullptr;
+  int64_t Ch = 0;
+  for (int l = 0; l < max_levels; ++l) {
+    uint32_t cap = 16;
+    while (cap < 2 * (uint64_t)n) cap <<= 1;
+    size_t cub_bytes = 0;
+    (void)hipcub::DeviceScan::InclusiveSum(nullptr, cub_bytes, (const int32_t*)nullptr, (int64_t*)nullptr, (int)n,
+                                           st);
+    const int64_t fixed = al(4 * (int64_t)cap) + al(8 * n * nw) + al(4 * n) + al(8 * (n + 1)) + al((int64_t)cub_bytes);
+    if ((w - w0) + fixed > ws_bytes) { (void)hipStreamSynchronize(st); sizes[1] = 2 * ((w - w0) + fixed); return 5; }
+    int32_t* table = reinterpret_cast<int32_t*>(w); w += al(4 * (int64_t)cap);
+    unsigned long long* ext = reinterpret_cast<unsigned long long*>(w); w += al(8 * n * nw);
+    int32_t* cnt = reinterpret_cast<int32_t*>(w); w += al(4 * n);
+    int64_t* off = reinterpret_cast<int64_t*>(w); w += al(8 * (n + 1));
+    void* cub_tmp = w; w += al((int64_t)cub_bytes);
+    (void)hipMemsetAsync(table, 0xFF, 4 * (size_t)cap, st);
+    (void)hipMemsetAsync(ext, 0, 8 * (size_t)n * nw, st);
+    (void)hipMemsetAsync(off, 0, 8, st);
+    dim3 g((unsigned)((n + 255) / 256));
+    hipLaunchKernelGGL(k_ag_insert, g, dim3(256), 0, st, P, n, m, table, cap - 1);
+    hipLaunchKernelGGL(k_ag_ext, g, dim3(256), 0, st, P, n, m, table, cap - 1, nw, ext);
+    const unsigned nwg = (unsigned)std::min<int64_t>((n + 3) / 4, 65536);
+    hipLaunchKernelGGL(k_ag_rows<false>, dim3(nwg), dim3(256), 0, st, P, n, m, table, cap - 1, nw, ext, cnt,
+                       nullptr, nullptr, nullptr);
+    (void)hipcub::DeviceScan::InclusiveSum(cub_tmp, cub_bytes, cnt, off + 1, (int)n, st);
+    Cdev = off + n;
+    (void)hipMemcpyAsync(&Ch, Cdev, 8, hipMemcpyDeviceToHost, st);
+    (void)hipStreamSynchronize(st);
+    const int64_t C = Ch;
+    if (C == 0 || (double)C > growth * (double)last || total + C > tmax) break;
+    const int64_t need_ws = (w - w0) + al(4 * C) + al(4 * C * (m + 1));
+    if (need_ws > ws_bytes) { sizes[1] = 2 * need_ws; return 5; }
+    const int64_t need_host = hoff + n + C + C * (m + 1);
+    if (need_host > host_cap) { (void)hipStreamSynchronize(st); sizes[1] = 2 * need_host; return 6; }
+    int32_t* ext_out = reinterpret_cast<int32_t*>(w); w += al(4 * C);
+    int32_t* rows_out = reinterpret_cast<int32_t*>(w); w += al(4 * C * (m + 1));
+    hipLaunchKernelGGL(k_ag_rows<true>, dim3(nwg), dim3(256), 0, st, P, n, m, table, cap - 1, nw, ext, nullptr, off,
+                       ext_out, rows_out);
+    (void)hipMemcpyAsync(host + hoff, cnt, 4 * (size_t)n, hipMemcpyDeviceToHost, st);
+    (void)hipMemcpyAsync(host + hoff + n, ext_out, 4 * (size_t)C, hipMemcpyDeviceToHost, st);
+    (void)hipMemcpyAsync(host + hoff + n + C, rows_out, 4 * (size_t)C * (m + 1), hipMemcpyDeviceToHost, st);
+    hoff = need_host;
+    sizes[2 + l] = C;
+    ++L;
+    total += C;
+    last = C;
+    P = rows_out;
+    n = C;
+    ++m;
+  }
+  (void)hipStreamSynchronize(st);
+  sizes[0] = L;
+  FA_LAUNCH_RET();
+}

@@ -54,6 +54,7 @@ FUSED_COMPRESS = os.environ.get("FA_FUSED_COMPRESS", "1") == "1"
 # 16-token register sort (T40I10's 40-token rows are faster on the tiered path)
 FUSED_COMPRESS_MEAN_LEN = 12
 GEN_DEVICE = os.environ.get("FA_GEN_DEVICE", "1") == "1"
+GEN_CHAIN = os.environ.get("FA_GEN_CHAIN", "1") == "1"
 GEN_DEVICE_MIN_ROWS = int(os.environ.get("FA_GEN_DEVICE_MIN_ROWS", "512"))
 BUNDLE_GROWTH = float(os.environ.get("FA_BUNDLE_GROWTH", "1.5"))
 BUNDLE_MAX_PREFIX = int(os.environ.get("FA_BUNDLE_MAX_PREFIX", "9"))
@@ -152,7 +153,7 @@ class FastApriori:
                 k += 1
                 continue
             with roctx_range(f"level{k}"), tm.phase(f"level{k}"):
-                with tm.phase("apriori_gen"):
+                with tm.phase("apriori_gen"), roctx_range("gen"):
                     prefix_idx, ext_off, ext, cand_rows = self._gen(levels[-1], want_rows=True)
                 C = int(ext.size)
                 self.log.line(f"{k} candidate items {C}")
@@ -162,16 +163,16 @@ class FastApriori:
                     break
                 # level bundling: count the next levels' candidates, generated from this
                 # level's candidates, in the same launch (see _plan_bundle)
-                with tm.phase("apriori_gen"):
+                with tm.phase("apriori_gen"), roctx_range("bundle"):
                     bundle = self._plan_bundle(db, k, levels[-1], prefix_idx, ext_off, ext, cand_rows)
                 mark = np.zeros(max(db["F1"], 1), dtype=bool)
                 for _, pv, pi, _, ex in bundle:
                     mark[pv[pi].ravel()] = True
                     mark[ex] = True
                 used = np.flatnonzero(mark)
-                with tm.phase(f"trim{k}"):
+                with tm.phase(f"trim{k}"), roctx_range("trim"):
                     self._trim(db, used, k)
-                with tm.phase("count"):
+                with tm.phase("count"), roctx_range("count"):
                     cnts = self._count_bundle(db, bundle)
                 if tm.sync:
                     self.stats.setdefault("level_info", {})[k] = dict(ops.primitives.LAST_LEVEL_PLAN,
@@ -579,6 +580,18 @@ class FastApriori:
         cand = np.ascontiguousarray(cand_rows, np.int32)
         last = C
         kk = k
+        dev = self._dev
+        if (dev.type == "cuda" and GEN_DEVICE and GEN_CHAIN and cand.shape[1] >= 2
+                and self._F1 <= ops.primitives.AG_DEVICE_MAX_F1):
+            # all speculative levels in one native call (one 8-byte readback per level)
+            max_lv = (self.cfg.max_level - k) if self.cfg.max_level else 64
+            tmax = ops.primitives.slab_total_limit(n_used)
+            for pi, eo, ex, nxt in ops.primitives.apriori_gen_chain(cand, self._F1, dev, max_lv, BUNDLE_GROWTH,
+                                                                    total, tmax):
+                kk += 1
+                bundle.append((kk, cand, pi, eo, ex))
+                cand = nxt
+            return bundle
         while self.cfg.max_level == 0 or kk + 1 <= self.cfg.max_level:
             pi, eo, ex, nxt = self._gen(cand, want_rows=True)
             C2 = int(ex.size)

@@ -960,6 +960,66 @@ def apriori_gen_device(prev: np.ndarray, F1: int, dev, want_rows: bool = False):
     return prefix_idx, ext_off, ext_h
 
 
+def apriori_gen_chain(rows: np.ndarray, F1: int, dev, max_levels: int, growth: float, total0: int,
+                      tmax: int) -> list:
+    """Speculative levels for bundling in one native call (csrc/hip/gen.hip fa_hip_ag_chain):
+    level m+1 candidates from ``rows`` (int32 [n, m], level k's candidate rows), then
+    m+2 from those, ... while each level is non-empty, grows at most ``growth`` x
+    and the bundle total stays <= ``tmax``.  Returns [(prefix_idx, ext_off, ext,
+    rows), ...] per accepted level, as apriori_gen_device."""
+    n, m = rows.shape
+    if n == 0 or max_levels <= 0:
+        return []
+    P = pinned_stage("gen").h2d(np.ascontiguousarray(rows, dtype=np.int32), dev)
+    st = _stream(P)
+    sizes = np.zeros(2 + max_levels, dtype=np.int64)
+    host_stage = pinned_stage("gen_out")
+    need_host = 1 << 20
+    for _ in range(32):
+        ws = _GEN_WS.get(dev)
+        if ws is None or ws.numel() < (64 << 20):
+            ws = _GEN_WS[dev] = torch.empty(64 << 20, dtype=torch.uint8, device=dev)
+        host = host_stage.get(4 * need_host).view(dtype=_I32)
+        rc = _native.hip().fa_hip_ag_chain(_p(P), n, m, F1, _p(ws), ws.numel(), host.data_ptr(), host.numel(),
+                                           max_levels, growth, total0, tmax, sizes.ctypes.data, st)
+        if rc == 5:
+            _GEN_WS[dev] = torch.empty(int(sizes[1]), dtype=torch.uint8, device=dev)
+            continue
+        if rc == 6:
+            need_host = int(sizes[1])
+            continue
+        _native.check(rc, "fa_hip_ag_chain")
+        break
+    else:
+        raise RuntimeError("fa_hip_ag_chain: buffer sizing did not converge")
+    h = host.numpy()
+    out, o = [], 0
+    for lv in range(int(sizes[0])):
+        C = int(sizes[2 + lv])
+        cnt_h = h[o:o + n]
+        prefix_idx = np.flatnonzero(cnt_h).astype(np.int32)
+        ext_off = np.zeros(prefix_idx.size + 1, dtype=np.int64)
+        np.cumsum(cnt_h[prefix_idx], out=ext_off[1:])
+        ext_h = h[o + n:o + n + C].copy()
+        nxt = h[o + n + C:o + n + C + C * (m + 1)].reshape(C, m + 1).copy()
+        out.append((prefix_idx, ext_off, ext_h, nxt))
+        o += n + C + C * (m + 1)
+        n, m = C, m + 1
+    return out
+
+
+def slab_total_limit(n_used: int) -> int:
+    """Largest bundle total t with t <= slab_capacity(n_used, t) (monotone in t)."""
+    lo, hi = 0, 1 << 31
+    while lo < hi:
+        mid = (lo + hi + 1) // 2
+        if mid <= slab_capacity(n_used, mid):
+            lo = mid
+        else:
+            hi = mid - 1
+    return lo
+
+
 RECOMMEND_INDEX_MIN_RULES = 2048
 
 

@@ -207,6 +207,45 @@ def test_rules_device_matches_host(seed, min_sup):
     assert (ref >= 0).any() and (ref < 0).any()
 
 
+def test_gen_chain_matches_iterated_gen():
+    # fa_hip_ag_chain == apriori_gen applied level after level (no growth / capacity stop)
+    sh = generate_shard(20000, Comm(), "cpu", 10.0, 4.0, 60, 80, seed=5)
+    res = FastApriori(0.004, config=MinerConfig(min_support=0.004)).run(sh)
+    prev = res.levels[2]
+    pi, eo, ex = apriori_gen(prev)
+    g = np.repeat(np.arange(pi.size), np.diff(eo))
+    cand = np.ascontiguousarray(np.concatenate([prev[pi[g]], ex[:, None]], axis=1), dtype=np.int32)
+    F1 = len(res.items)
+    # speculative chains from candidates can grow fast: cap the depth at 4 levels
+    got = ops.primitives.apriori_gen_chain(cand, F1, DEV, 4, 1e9, 0, 1 << 40)
+    assert len(got) >= 2
+    cur = cand
+    for gpi, geo, gex, grows in got:
+        pi, eo, ex = apriori_gen(cur)
+        assert np.array_equal(gpi, pi) and np.array_equal(geo, eo) and np.array_equal(gex, ex)
+        g = np.repeat(np.arange(pi.size), np.diff(eo))
+        cur = np.ascontiguousarray(np.concatenate([cur[pi[g]], ex[:, None]], axis=1), dtype=np.int32)
+        assert np.array_equal(grows, cur)
+    assert len(got) == 4 or apriori_gen(cur)[2].size == 0
+    # depth / capacity / growth stops
+    two = ops.primitives.apriori_gen_chain(cand, F1, DEV, 2, 1e9, 0, 1 << 40)
+    assert len(two) == min(2, len(got))
+    cap = ops.primitives.apriori_gen_chain(cand, F1, DEV, 4, 1e9, 0, got[0][2].size)
+    assert len(cap) == 1
+    c0 = got[0][2].size      # growth is measured against the previous level (the input for level 0)
+    assert len(ops.primitives.apriori_gen_chain(cand, F1, DEV, 4, (c0 - 0.5) / cand.shape[0], 0, 1 << 40)) == 0
+
+
+def test_bundling_chain_matches_python_loop(monkeypatch):
+    import fastapriori_amd.models.apriori as ap
+    sh = generate_shard(200000, Comm(), "cpu", 10.0, 4.0, 60, 80, seed=8).to(DEV)
+    cfg = MinerConfig(min_support=0.003)
+    a = FastApriori(0.003, config=cfg).run(sh)
+    monkeypatch.setattr(ap, "GEN_CHAIN", False)
+    b = FastApriori(0.003, config=MinerConfig(min_support=0.003)).run(sh)
+    assert a.as_dict() == b.as_dict()
+
+
 def test_parse_to_device_roundtrip():
     sh = parse_bytes(b"1 2 3\n\n4 4 5\n", device=DEV)
     assert sh.items.is_cuda and sh.n_lines == 3
