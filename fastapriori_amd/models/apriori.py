@@ -102,7 +102,9 @@ class FastApriori:
         self.cand_par = self.cfg.parallelism == "candidate" and self.comm.distributed
         self.dcomm = Comm(device=self.comm.device) if self.cand_par else self.comm
         comm = self.dcomm
-        n_global = comm.allreduce_int(shard.n_lines)
+        # line total and numeric vocabulary width in one collective
+        g = comm.all_gather_ints([shard.n_lines, shard.vocab.size if shard.vocab.numeric else 0])
+        n_global, self._V_max = int(g[:, 0].sum()), int(g[:, 1].max())
         mc = min_count(self.cfg.min_support, n_global)
         self.stats = {"n_lines": n_global, "min_count": mc}
         tm = Timer(dev, sync=os.environ.get("FA_PHASE_TIMING") == "1")
@@ -126,7 +128,7 @@ class FastApriori:
 
         with roctx_range("compress"), tm.phase("compress"):
             db = self._compress(shard, lut, F1)
-        self.stats.update(T=db["T_global"], distinct=db["ncols_global"])
+        self._db_local = db
 
         # ---- k = 2 -----------------------------------------------------
         t0 = time.perf_counter()
@@ -204,6 +206,12 @@ class FastApriori:
         return self._finish(result, t_start)
 
     def _finish(self, result: MiningResult, t_start: float) -> MiningResult:
+        db = getattr(self, "_db_local", None)
+        if db is not None:
+            # layout sizes for the metrics, one collective after the last level
+            g = self.dcomm.all_gather_ints([db["T0"], db["ncols0"]])
+            self.stats.update(T=int(g[:, 0].sum()), distinct=int(g[:, 1].sum()))
+            self._db_local = None
         total_k2 = sum(len(c) for c in result.counts[1:])
         self.log.line(f"Total freq items sets {total_k2}")
         self.stats["mine_ms"] = (time.perf_counter() - t_start) * 1e3
@@ -224,7 +232,7 @@ class FastApriori:
         comm, vocab, dev = self.dcomm, shard.vocab, shard.items.device
         thr = max(mc, 1)   # only tokens that occur can be frequent (even at minSupport 0)
         if vocab.numeric:
-            V = comm.allreduce_int(vocab.size, "max")
+            V = self._V_max
             got = None
             if self.cfg.f1 == "sketch" or (self.cfg.f1 == "auto" and dev.type == "cuda"
                                               and V >= F1_SKETCH_MIN_VOCAB):
@@ -345,12 +353,19 @@ class FastApriori:
         L = np.arange(256, dtype=np.int64)
         db["pair_work"] = int((hist * (L * (L - 1) // 2)).sum())
         db["len_hist"] = hist
-        db["long_rows"] = bool(self.dcomm.allreduce_int(int(hist[255] > 0), "max"))
-        if self._want_dedup(db):
+        # every rank must take the same layout decisions: long rows, dedup and (when the
+        # layout stays undeduplicated) the pair strategy, agreed in one collective
+        g = self.dcomm.all_gather_ints([int(hist[255] > 0), int(self._want_dedup(db)),
+                                        int(self._pick_gram_local(db, F1))])
+        db["long_rows"] = bool(g[:, 0].max())
+        db["pair_pick"] = None
+        if g[:, 1].max():
             self._dedup(db)
             db.pop("len_hist", None)
-        db["T_global"] = self.dcomm.allreduce_int(T)
-        db["ncols_global"] = self.dcomm.allreduce_int(db["ncols"] if db["src"] is None else db["n_distinct"])
+        else:
+            db["pair_pick"] = bool(g[:, 2].max())
+        db["T0"] = T
+        db["ncols0"] = db["ncols"] if db["src"] is None else db["n_distinct"]
         self.log.metric(phase="compress", T=T, distinct=db.get("n_distinct", T), nnz=int(ranks.numel()))
         return db
 
@@ -367,8 +382,8 @@ class FastApriori:
             h1, _ = ops.row_hash(sub_off, db["ranks"][: int(sub_off[-1].item())])
             frac = torch.unique(h1).numel() / max(n, 1)
             decision = frac < self.cfg.dedup_threshold
-        # every rank must take the same decision (the layout differs)
-        return bool(self.dcomm.allreduce_int(int(decision), "max"))
+        # local decision: the caller agrees on it across ranks (the layout differs)
+        return decision
 
     def _dedup(self, db) -> None:
         """Merge identical compressed rows into weight classes (FastApriori.scala:71-79).
@@ -494,12 +509,17 @@ class FastApriori:
         s = self.cfg.pair_strategy
         if s != "auto":
             return s
+        if db.get("pair_pick") is not None:     # agreed with the compress decisions
+            return "gram" if db["pair_pick"] else "horizontal"
+        # ranks must agree: any rank preferring the Gram kernel decides
+        return "gram" if self.dcomm.allreduce_int(int(self._pick_gram_local(db, F1)), "max") else "horizontal"
+
+    @staticmethod
+    def _pick_gram_local(db, F1: int) -> bool:
         W = (db["ncols"] + 63) // 64
         t_h = db["pair_work"] / HORIZONTAL_PAIRS_PER_S
         t_g = (F1 * (F1 - 1) / 2) * W / GRAM_WORDPAIRS_PER_S
-        # ranks must agree: decide on the global work
-        pick_gram = t_g < t_h
-        return "gram" if self.dcomm.allreduce_int(int(pick_gram), "max") else "horizontal"
+        return t_g < t_h
 
     def _pairs(self, db, F1: int, mc: int):
         strat = self._pick_pair_strategy(db, F1)

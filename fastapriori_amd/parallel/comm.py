@@ -34,10 +34,11 @@ class Comm:
     device: torch.device = torch.device("cpu")
     backend: str = "none"
     bytes_reduced: int = 0
+    force: bool = False     # run the collective code paths even at world size 1 (FA_FORCE_PG)
 
     @property
     def distributed(self) -> bool:
-        return self.world_size > 1
+        return self.world_size > 1 or self.force
 
     @property
     def is_root(self) -> bool:
@@ -101,6 +102,16 @@ class Comm:
         out = [torch.zeros_like(t) for _ in range(self.world_size)]
         dist.all_gather(out, t)
         return [int(x.item()) for x in out]
+
+    def all_gather_ints(self, values) -> np.ndarray:
+        """One collective for several small integers: int64 [world, len(values)]."""
+        v = np.asarray(values, dtype=np.int64).reshape(1, -1)
+        if not self.distributed:
+            return v
+        t = torch.from_numpy(v.ravel().copy()).to(self._comm_device())
+        out = torch.empty(self.world_size * t.numel(), dtype=torch.int64, device=t.device)
+        dist.all_gather_into_tensor(out, t)
+        return out.cpu().numpy().reshape(self.world_size, -1)
 
     def all_gather_object(self, obj) -> list:
         if not self.distributed:
@@ -179,8 +190,18 @@ def init_comm(device: str | None = None, backend: str | None = None, timeout_s: 
         dev = torch.device("cuda", local)
     else:
         dev = torch.device("cpu")
-    if world <= 1:
+    # FA_FORCE_PG=1 keeps a process group (and every collective) at world size 1, so a
+    # one-GPU box exercises the RCCL code paths of the multi-GPU run
+    force = world <= 1 and os.environ.get("FA_FORCE_PG") == "1"
+    if world <= 1 and not force:
         return Comm(0, 1, dev, "none")
+    if force:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:
+            from .launch import free_port
+            os.environ["MASTER_PORT"] = str(free_port())
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
     # FA_DIST_BACKEND=gloo lets several ranks share one GPU (tests on a 1-GPU box);
     # production GPU runs use RCCL ("nccl"), one process per GPU.
     be = backend or os.environ.get("FA_DIST_BACKEND") or ("nccl" if dev.type == "cuda" else "gloo")
@@ -189,7 +210,7 @@ def init_comm(device: str | None = None, backend: str | None = None, timeout_s: 
         if be == "nccl":
             kw["device_id"] = dev
         dist.init_process_group(**kw)
-    return Comm(dist.get_rank(), dist.get_world_size(), dev, be)
+    return Comm(dist.get_rank(), dist.get_world_size(), dev, be, force=force)
 
 
 def shutdown_comm(comm: Comm) -> None:

@@ -157,3 +157,11 @@ def test_candidate_distribution_file_and_rules(numeric_db):
     outs = spawn_local(_mine_file, 2, numeric_db, 0.02, "auto", "auto", "candidate")
     assert all(o["sets"] == ref["sets"] and o["items"] == ref["items"] for o in outs)
     assert outs[0]["recs"] == ref["recs"]
+
+
+def test_forced_process_group_at_world_one(numeric_db):
+    # FA_FORCE_PG=1: every collective runs at world size 1 (how a one-GPU box exercises
+    # the RCCL paths); results must equal the collective-free run
+    ref = spawn_local(_mine_file, 1, numeric_db, 0.02, "auto", "auto")[0]
+    got = spawn_local(_mine_file, 1, numeric_db, 0.02, "auto", "auto", env={"FA_FORCE_PG": "1"})[0]
+    assert got == ref

@@ -51,3 +51,39 @@ def test_two_ranks_share_gpu_match_one():
     outs = spawn_local(_gpu_rank, 2, 40000, 0.005, env={"FA_DIST_BACKEND": "gloo"})
     assert outs[0] == ref and outs[1] == ref
     assert len(ref) > 100
+
+
+def _rccl_rank(n, ms, strategy):
+    """Mining, rules and recommendations through the RCCL code paths (world size 1,
+    FA_FORCE_PG=1): every collective of the multi-GPU run executes on the device."""
+    import numpy as np
+    from fastapriori_amd.models.apriori import FastApriori, MinerConfig
+    from fastapriori_amd.models.rules import AssociationRules
+    from fastapriori_amd.parallel.comm import init_comm, shutdown_comm
+    from fastapriori_amd.utils.io import generate_shard, parse_bytes
+    from fastapriori_amd.utils.metrics import Logger
+    comm = init_comm("cuda")
+    try:
+        if os.environ.get("FA_FORCE_PG") == "1":
+            assert comm.backend == "nccl" and comm.distributed
+        log = Logger(comm.rank, enabled=False)
+        sh = generate_shard(n, comm, comm.device, 10.0, 4.0, 200, 200, seed=3)
+        res = FastApriori(ms, comm, MinerConfig(min_support=ms, parallelism=strategy), log).run(sh)
+        users = generate_shard(2000, comm, comm.device, 10.0, 4.0, 200, 200, seed=3, users=True)
+        recs = AssociationRules(res, comm, log).run(users)
+        # dictionary vocabulary: hash all-to-all + all_gather_object on RCCL
+        words = parse_bytes(b"a b c\nb c d\na c\nc d e a\n" * 50, device=comm.device)
+        dres = FastApriori(0.2, comm, MinerConfig(min_support=0.2), log).run(words)
+        comm.barrier()
+        t = comm.allreduce_float_max(1.5)
+        return res.as_dict(), recs, dres.as_dict(), dres.items, t, comm.bytes_reduced
+    finally:
+        shutdown_comm(comm)
+
+
+@pytest.mark.parametrize("strategy", ["count", "candidate"])
+def test_rccl_code_paths_match_single_process(strategy):
+    ref = spawn_local(_rccl_rank, 1, 60000, 0.004, strategy)[0]
+    got = spawn_local(_rccl_rank, 1, 60000, 0.004, strategy, env={"FA_FORCE_PG": "1"})[0]
+    assert got[0] == ref[0] and got[1] == ref[1] and got[2] == ref[2] and got[3] == ref[3]
+    assert got[4] == 1.5 and got[5] > 0 and ref[5] == 0
