@@ -167,10 +167,9 @@ class FastApriori:
                 # level's candidates, in the same launch (see _plan_bundle)
                 with tm.phase("apriori_gen"), roctx_range("bundle"):
                     bundle = self._plan_bundle(db, k, levels[-1], prefix_idx, ext_off, ext, cand_rows)
+                # later bundled levels only use items of level k's candidates
                 mark = np.zeros(max(db["F1"], 1), dtype=bool)
-                for _, pv, pi, _, ex in bundle:
-                    mark[pv[pi].ravel()] = True
-                    mark[ex] = True
+                mark[self._bundle_rows[0].ravel()] = True
                 used = np.flatnonzero(mark)
                 with tm.phase(f"trim{k}"), roctx_range("trim"):
                     self._trim(db, used, k)
@@ -180,11 +179,9 @@ class FastApriori:
                     self.stats.setdefault("level_info", {})[k] = dict(ops.primitives.LAST_LEVEL_PLAN,
                                                                       groups=int(prefix_idx.size),
                                                                       bundled=len(bundle))
-                for (kk, pv, pi, eo, ex), cnt in zip(bundle, cnts):
-                    keep = cnt >= mc
-                    g_of_e = np.repeat(np.arange(pi.size), np.diff(eo))
-                    rows = np.concatenate([pv[pi[g_of_e[keep]]], ex[keep, None]], axis=1)
-                    levels.append(np.ascontiguousarray(rows, dtype=np.int32))
+                for cand_k, cnt in zip(self._bundle_rows, cnts):
+                    keep = cnt >= mc          # candidate rows are in count order
+                    levels.append(np.ascontiguousarray(cand_k[keep], dtype=np.int32))
                     counts.append(cnt[keep].astype(np.int64))
             ms = (time.perf_counter() - t0) * 1e3
             for j, (kk, pv, pi, eo, ex) in enumerate(bundle):
@@ -583,21 +580,22 @@ class FastApriori:
         one, and prefixes stay short (deep levels prefer the trie kernel).
         Returns [(k, prefix rows source, prefix_idx, ext_off, ext), ...]."""
         bundle = [(k, prev, prefix_idx, ext_off, ext)]
+        if cand_rows is None:
+            g_of_e = np.repeat(np.arange(prefix_idx.size), np.diff(ext_off))
+            cand_rows = np.concatenate([prev[prefix_idx[g_of_e]], ext[:, None]], axis=1)
+        # candidate rows of every bundled level (result assembly: rows[count >= minCount])
+        self._bundle_rows = [np.ascontiguousarray(cand_rows, np.int32)]
         if (not BUNDLE_LEVELS or self.cand_par or self.cfg.level_kernel not in ("auto", "slab")
                 or k - 1 > BUNDLE_MAX_PREFIX):
             return bundle
         C = int(ext.size)
         items = np.zeros(db["F1"], dtype=bool)
-        items[prev[prefix_idx].ravel()] = True
-        items[ext] = True
+        items[self._bundle_rows[0].ravel()] = True
         total = C
         n_used = int(items.sum())
         if total > ops.primitives.slab_capacity(n_used, total):
             return bundle
-        if cand_rows is None:
-            g_of_e = np.repeat(np.arange(prefix_idx.size), np.diff(ext_off))
-            cand_rows = np.concatenate([prev[prefix_idx[g_of_e]], ext[:, None]], axis=1)
-        cand = np.ascontiguousarray(cand_rows, np.int32)
+        cand = self._bundle_rows[0]
         last = C
         kk = k
         dev = self._dev
@@ -610,6 +608,7 @@ class FastApriori:
                                                                     total, tmax):
                 kk += 1
                 bundle.append((kk, cand, pi, eo, ex))
+                self._bundle_rows.append(nxt)
                 cand = nxt
             return bundle
         while self.cfg.max_level == 0 or kk + 1 <= self.cfg.max_level:
@@ -622,6 +621,7 @@ class FastApriori:
                 break
             kk += 1
             bundle.append((kk, cand, pi, eo, ex))
+            self._bundle_rows.append(np.ascontiguousarray(nxt, np.int32))
             total, last = total + C2, C2
             cand = nxt
         return bundle
