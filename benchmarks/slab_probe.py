@@ -1,7 +1,7 @@
 """Time decomposition of the k >= 3 slab kernel on a real mining run.
 
-Mines a config once, recording the arguments of every ops.count_level_slab
-call, then replays each call under FA_SLAB_DEBUG = 0 (full), 1 (no slab build),
+Mines a config once, recording the arguments of every ops.count_level call
+(slab or trie kernel, bundles included), then replays each call under FA_SLAB_DEBUG = 0 (full), 1 (no slab build),
 2 (no counting), 3 (neither: launch + prefetch + final atomics) and prints the
 per-level times (CUDA events, median of --reps).
 
@@ -34,20 +34,20 @@ def main():
     n, L, I, P, N, ms = bench.CONFIGS[a.config]
     shard = generate_shard(n, Comm(), "cuda", L, I, P, N, 1)
     calls = []
-    real = ops.count_level_slab
+    real = ops.count_level
 
     def rec(*args, **kw):
         calls.append((args, kw))
         return real(*args, **kw)
 
-    apriori.ops.count_level_slab = rec
+    apriori.ops.count_level = rec
     FastApriori(ms, config=MinerConfig(min_support=ms)).run(shard)
-    apriori.ops.count_level_slab = real
+    apriori.ops.count_level = real
     out = []
     for i, (args, kw) in enumerate(calls):
         for sw in (a.sw.split(",") if a.sw else [""]):
             os.environ["FA_SLAB_SW"] = sw or "0"
-            row = {"k": args[5].shape[1] + 1, "C": int(args[7].size), "force_sw": sw}
+            row = {"call": i, "C": int(args[7].size), "force_sw": sw}
             for mode in a.modes.split(","):
                 os.environ["FA_SLAB_DEBUG"] = mode
                 ts = []
@@ -59,7 +59,7 @@ def main():
                     torch.cuda.synchronize()
                     ts.append(e0.elapsed_time(e1))
                 row[f"mode{mode}_ms"] = round(sorted(ts)[len(ts) // 2], 3)
-            row.update(ops.primitives.LAST_SLAB_PLAN)
+            row.update(ops.primitives.LAST_LEVEL_PLAN)
             out.append(row)
             print(json.dumps(row), flush=True)
         os.environ["FA_SLAB_SW"] = "0"

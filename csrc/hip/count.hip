@@ -973,13 +973,21 @@ __device__ __forceinline__ void slab_build_word(uint64_t* __restrict__ slab, int
   }
 }
 
-template <int SW, bool kWeighted, int kBuild>
+// kDfs (bundles of levels, unit weights): a work piece is a prefix plus up to 8
+// depth-1 nodes (candidates of level k) and, under each, its depth-2 nodes (the
+// level k+1 candidates whose prefix is that level-k candidate).  The AND of a
+// depth-1 node is counted and kept in registers for its children, so a level
+// k+1 candidate costs one slab-row read instead of its whole k-item prefix.
+//   gext_off[2g..2g+1]: node-1 range of piece g;  gext: int4 node-1 (slab row,
+//   output index, node-2 begin, node-2 end);  dfs2: int2 node-2 (slab row, output).
+template <int SW, bool kWeighted, int kBuild, bool kDfs = false>
 __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
     const int64_t* __restrict__ roff, const int32_t* __restrict__ ranks, const int32_t* __restrict__ src,
     int64_t ncols, const int32_t* __restrict__ item_map, int n_used, const int32_t* __restrict__ gpre, int m,
     const int32_t* __restrict__ gext_off, const int32_t* __restrict__ gext, int G, int C,
     const int32_t* __restrict__ wword, uint32_t* __restrict__ out, const uint64_t* __restrict__ bm,
-    int64_t Wp, int dbg, const int32_t* __restrict__ gpm, const int32_t* __restrict__ bm_rows, int acc16) {
+    int64_t Wp, int dbg, const int32_t* __restrict__ gpm, const int32_t* __restrict__ bm_rows, int acc16,
+    const int32_t* __restrict__ dfs2 = nullptr) {
   extern __shared__ uint4 lds4[];                  // 16-B aligned base
   __shared__ unsigned long long build_words[kSlabThreads / 64 * 2];   // window_starts scratch
   constexpr int SWP = SW + 2;                       // row stride: 16-B aligned, odd number of 16-B slots
@@ -1088,6 +1096,38 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
 #pragma unroll
       for (int q = 0; q < SW / 2; ++q) any |= p[q].x | p[q].y | p[q].z | p[q].w;
       if (!any) continue;
+      if constexpr (kDfs) {
+        const int4* n1 = reinterpret_cast<const int4*>(gext);
+        const int2* n2 = reinterpret_cast<const int2*>(dfs2);
+        for (int i = gext_off[2 * g], i1 = gext_off[2 * g + 1]; i < i1; ++i) {
+          const int4 nd = n1[i];
+          const uint4* re = lds4 + (size_t)nd.x * (SWP / 2);
+          uint4 v1[SW / 2];
+          uint32_t s = 0;
+#pragma unroll
+          for (int q = 0; q < SW / 2; ++q) {
+            const uint4 v = re[q];
+            v1[q].x = p[q].x & v.x; v1[q].y = p[q].y & v.y; v1[q].z = p[q].z & v.z; v1[q].w = p[q].w & v.w;
+            s += __popc(v1[q].x) + __popc(v1[q].y) + __popc(v1[q].z) + __popc(v1[q].w);
+          }
+          if (acc16) atomicAdd(&acc[nd.y >> 1], s << ((nd.y & 1) << 4));
+          else acc[nd.y] += s;
+          if (!s) continue;                          // no column holds the node: children are 0
+          for (int j = nd.z; j < nd.w; ++j) {
+            const int2 c2 = n2[j];
+            const uint4* r2 = lds4 + (size_t)c2.x * (SWP / 2);
+            uint32_t s2 = 0;
+#pragma unroll
+            for (int q = 0; q < SW / 2; ++q) {
+              const uint4 v = r2[q];
+              s2 += __popc(v1[q].x & v.x) + __popc(v1[q].y & v.y) + __popc(v1[q].z & v.z) + __popc(v1[q].w & v.w);
+            }
+            if (acc16) atomicAdd(&acc[c2.y >> 1], s2 << ((c2.y & 1) << 4));
+            else acc[c2.y] += s2;
+          }
+        }
+        continue;
+      }
       for (int e = gext_off[2 * g], e1 = gext_off[2 * g + 1]; e < e1; ++e) {
         const uint4* re = lds4 + (size_t)gext[e] * (SWP / 2);
         uint32_t s = 0;
@@ -1438,7 +1478,8 @@ FA_API int fa_hip_count_slab(const int64_t* roff, const int32_t* ranks, const in
   dim3 g((unsigned)n_wg), b(kSlabThreads);
   using KernT = void (*)(const int64_t*, const int32_t*, const int32_t*, int64_t, const int32_t*, int,
                          const int32_t*, int, const int32_t*, const int32_t*, int, int, const int32_t*,
-                         uint32_t*, const uint64_t*, int64_t, int, const int32_t*, const int32_t*, int);
+                         uint32_t*, const uint64_t*, int64_t, int, const int32_t*, const int32_t*, int,
+                         const int32_t*);
   KernT kern = nullptr;
 #define FA_SLAB_MODE(S, B) kern = wword ? (KernT)k_count_slab<S, true, B> : (KernT)k_count_slab<S, false, B>;
 #define FA_SLAB_CASE(S)                                   \
@@ -1457,7 +1498,40 @@ FA_API int fa_hip_count_slab(const int64_t* roff, const int32_t* ranks, const in
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const int dbg = getenv("FA_SLAB_DEBUG") ? atoi(getenv("FA_SLAB_DEBUG")) : 0;
   hipLaunchKernelGGL(kern, g, b, lds, st, roff, ranks, src, ncols, item_map, n_used, gpre, m, gext_off, gext, G, C,
-                     wword, out, bm, Wp, dbg, gpm, bm_rows, acc16);
+                     wword, out, bm, Wp, dbg, gpm, bm_rows, acc16, (const int32_t*)nullptr);
+  FA_LAUNCH_RET();
+}
+
+// Bundle counting with depth-2 prefix reuse (k_count_slab<.., kDfs = true>):
+// unit weights, one accumulator pass (C <= LDS capacity).  gpre/gpm: prefix slab
+// rows and per-piece (offset, length); prng: per-piece node-1 range; node1: int4,
+// node2: int2 (see the kernel).  Returns 3 when slab + accumulator exceed the LDS.
+FA_API int fa_hip_count_dfs(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
+                            const int32_t* item_map, int n_used, const int32_t* gpre, const int32_t* gpm,
+                            const int32_t* prng, const int32_t* node1, const int32_t* node2, int NP, int C,
+                            uint32_t* out, int sw, int n_wg, hipStream_t st) {
+  if (NP <= 0 || C <= 0 || ncols <= 0) return 0;
+  const size_t lds = (size_t)n_used * (sw + 2) * 8 + (size_t)C * 4;
+  if (lds > 160 * 1024 - 512) return 3;
+  using KernT = void (*)(const int64_t*, const int32_t*, const int32_t*, int64_t, const int32_t*, int,
+                         const int32_t*, int, const int32_t*, const int32_t*, int, int, const int32_t*,
+                         uint32_t*, const uint64_t*, int64_t, int, const int32_t*, const int32_t*, int,
+                         const int32_t*);
+  KernT kern = nullptr;
+#define FA_DFS_CASE(S)                                                              \
+  if (sw == S) kern = src ? (KernT)k_count_slab<S, false, kBuildCols, true>          \
+                          : (KernT)k_count_slab<S, false, kBuildContig, true>;
+  FA_DFS_CASE(4)
+  FA_DFS_CASE(8)
+  FA_DFS_CASE(16)
+  FA_DFS_CASE(32)
+#undef FA_DFS_CASE
+  if (!kern) return 1;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const int dbg = getenv("FA_SLAB_DEBUG") ? atoi(getenv("FA_SLAB_DEBUG")) : 0;
+  hipLaunchKernelGGL(kern, dim3((unsigned)n_wg), dim3(kSlabThreads), lds, st, roff, ranks, src, ncols, item_map,
+                     n_used, gpre, 0, prng, node1, NP, C, (const int32_t*)nullptr, out, (const uint64_t*)nullptr,
+                     (int64_t)0, dbg, gpm, (const int32_t*)nullptr, 0, node2);
   FA_LAUNCH_RET();
 }
 

@@ -56,6 +56,11 @@ FUSED_COMPRESS_MEAN_LEN = 12
 GEN_DEVICE = os.environ.get("FA_GEN_DEVICE", "1") == "1"
 GEN_CHAIN = os.environ.get("FA_GEN_CHAIN", "1") == "1"
 GEN_DEVICE_MIN_ROWS = int(os.environ.get("FA_GEN_DEVICE_MIN_ROWS", "512"))
+BUNDLE_DFS = os.environ.get("FA_BUNDLE_DFS", "1") == "1"
+# depth-2 reuse pays where prefixes are long; on short prefixes (k = 3: two items) the
+# lanes' uneven child loops cost more than the saved reads (T10I4D100M: bundle 3-4
+# 17.7 -> 21.0 ms with it, bundle 5-12 16.2 -> 14.6 ms)
+BUNDLE_DFS_MIN_M = int(os.environ.get("FA_BUNDLE_DFS_MIN_M", "4"))
 BUNDLE_GROWTH = float(os.environ.get("FA_BUNDLE_GROWTH", "1.5"))
 BUNDLE_MAX_PREFIX = int(os.environ.get("FA_BUNDLE_MAX_PREFIX", "9"))
 
@@ -630,6 +635,15 @@ class FastApriori:
         """Counts of every level of a bundle (one launch on the GPU)."""
         if len(bundle) == 1 or db["ranks"].device.type != "cuda":
             return [self._count_level(db, pv, pi, eo, ex) for _, pv, pi, eo, ex in bundle]
+        sizes = [int(ex.size) for *_, ex in bundle]
+        if BUNDLE_DFS and db["wword"] is None and bundle[0][1].shape[1] >= BUNDLE_DFS_MIN_M:
+            # depth-2 prefix reuse: level k+1 candidates read one slab row under their
+            # parent level-k candidate's AND (k_count_slab<kDfs>)
+            cnt = ops.primitives.count_bundle_dfs(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"],
+                                                  [(pv, pi, eo, ex) for _, pv, pi, eo, ex in bundle])
+            if cnt is not None:
+                self.dcomm.all_reduce_(cnt, bound=self.stats["n_lines"])
+                return np.split(cnt.cpu().numpy(), np.cumsum(sizes)[:-1])
         pre = [pv[pi] for _, pv, pi, _, _ in bundle]
         poff = np.concatenate([[0], np.cumsum(np.concatenate([np.full(p.shape[0], p.shape[1]) for p in pre]))])
         flat = np.concatenate([p.ravel() for p in pre]).astype(np.int32)

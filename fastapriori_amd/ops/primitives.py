@@ -1192,3 +1192,110 @@ def parse_numeric_device(buf: torch.Tensor, n: int, last_is_term: bool):
     _native.check(lib.fa_hip_compact_lines(_p(scratch), _p(xscratch), _p(bound_off), _p(dcnt), _p(xcnt), _p(off),
                                            _p(xoff), nl, _p(items), _p(extras), st), "fa_hip_compact_lines")
     return off, items, extras, int(info[1]) + 1
+
+
+DFS_PIECE_NODES = 8        # depth-1 nodes per work piece (as the slab kernel's extensions per piece)
+
+
+def plan_bundle_dfs(levels: list, F1: int):
+    """Work pieces of a level bundle for k_count_slab<kDfs> (see csrc/hip/count.hip).
+
+    levels[j] = (pv, pi, eo, ex) of bundle level j: groups' prefixes are pv[pi[g]],
+    candidates eo[g]..eo[g+1] extend them by ex.  Level j+1's prefix rows pv are
+    level j's candidate rows, so level j+1 group g is the child of level-j
+    candidate pi[g].  Even levels are roots (explicit prefix, depth-1 nodes); the
+    odd level after each is read as depth-2 nodes under its parent candidate.
+    Output index of level-j candidate c: sum(C_<j) + c.
+    Returns dict(used, item_map, gpre, gpm, prng, node1, node2, C) (numpy int32)."""
+    sizes = [int(lv[3].size) for lv in levels]
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    mark = np.zeros(max(F1, 1), dtype=bool)
+    mark[levels[0][0][levels[0][1]].ravel()] = True
+    mark[levels[0][3]] = True
+    used = np.flatnonzero(mark).astype(np.int32)
+    item_map = np.full(max(F1, 1), -1, dtype=np.int32)
+    item_map[used] = np.arange(used.size, dtype=np.int32)
+    gpre_l, gpm_l, prng_l, n1_l, n2_l = [], [], [], [], []
+    gpre_n = n1_n = n2_n = 0
+    for j in range(0, len(levels), 2):
+        pv, pi, eo, ex = levels[j]
+        G, Cj = int(pi.size), int(ex.size)
+        pre = item_map[pv[pi]]                                  # [G, m]
+        m = pre.shape[1]
+        gpre_l.append(pre.ravel())
+        # depth-2 ranges: the child group of every level-j candidate (if any)
+        n2b = np.zeros(Cj, dtype=np.int64)
+        n2e = np.zeros(Cj, dtype=np.int64)
+        if j + 1 < len(levels):
+            _, pi1, eo1, ex1 = levels[j + 1]
+            n2b[pi1] = n2_n + eo1[:-1]
+            n2e[pi1] = n2_n + eo1[1:]
+            n2_l.append(np.stack([item_map[ex1], (off[j + 1] + np.arange(ex1.size)).astype(np.int32)], 1))
+            n2_n += int(ex1.size)
+        n1_l.append(np.stack([item_map[ex], (off[j] + np.arange(Cj)).astype(np.int32),
+                              n2b.astype(np.int32), n2e.astype(np.int32)], 1))
+        # pieces: each group's candidates in chunks of DFS_PIECE_NODES, sharing the group's prefix
+        cnt = np.diff(eo)
+        npc = np.maximum(1, (cnt + DFS_PIECE_NODES - 1) // DFS_PIECE_NODES)
+        gi = np.repeat(np.arange(G), npc)
+        first = np.cumsum(npc) - npc
+        k_in = np.arange(gi.size) - np.repeat(first, npc)
+        b = eo[gi] + k_in * DFS_PIECE_NODES
+        e = np.minimum(eo[gi + 1], b + DFS_PIECE_NODES)
+        gpm_l.append(np.stack([gpre_n + gi * m, np.full(gi.size, m)], 1))
+        prng_l.append(np.stack([n1_n + b, n1_n + e], 1))
+        gpre_n += G * m
+        n1_n += Cj
+    gpm = np.concatenate(gpm_l).astype(np.int32)
+    prng = np.concatenate(prng_l).astype(np.int64)
+    node1 = np.concatenate(n1_l).astype(np.int32)
+    node2 = np.concatenate(n2_l).astype(np.int32) if n2_l else np.zeros((1, 2), np.int32)
+    # cost-sorted pieces (the lanes of a wave then run loops of similar length)
+    n2cnt = (node1[:, 3] - node1[:, 2]).astype(np.int64)
+    c2 = np.concatenate([[0], np.cumsum(n2cnt)])
+    cost = (prng[:, 1] - prng[:, 0]) + (c2[prng[:, 1]] - c2[prng[:, 0]]) + gpm[:, 1]
+    order = np.argsort(-cost, kind="stable")
+    return dict(used=used, item_map=item_map, gpre=np.concatenate(gpre_l).astype(np.int32),
+                gpm=np.ascontiguousarray(gpm[order]), prng=np.ascontiguousarray(prng[order].astype(np.int32)),
+                node1=node1, node2=node2, C=int(off[-1]))
+
+
+def count_bundle_dfs(roff, ranks, src, ncols: int, F1: int, levels: list) -> torch.Tensor | None:
+    """Counts of every level of a bundle (concatenated, level order) with depth-2
+    prefix reuse; None when the bundle does not fit one LDS accumulator pass."""
+    dev = ranks.device
+    plan = plan_bundle_dfs(levels, F1)
+    C, n_used = plan["C"], int(plan["used"].size)
+    sw = 0
+    for s in (32, 16, 8, 4):
+        cap = (_LDS_BYTES - n_used * (s + 2) * 8) // 4
+        if cap >= min(C, 8192) or (s == 4 and cap >= 1024):
+            sw = s
+            break
+    if sw == 0 or C > (_LDS_BYTES - n_used * (sw + 2) * 8) // 4:
+        return None
+    parts = [plan["item_map"], plan["used"], plan["gpre"], plan["gpm"].ravel(), plan["prng"].ravel(),
+             plan["node1"].ravel(), plan["node2"].ravel()]
+    offs = np.concatenate([[0], np.cumsum([(p.size + 3) // 4 * 4 for p in parts])])
+    host = np.zeros(int(offs[-1]), dtype=np.int32)
+    for p, o in zip(parts, offs[:-1]):
+        host[o:o + p.size] = p
+    dbuf = pinned_stage("level_plan").h2d(host, dev)
+    base = dbuf.data_ptr()
+    ptr = [base + 4 * int(o) for o in offs[:-1]]
+    out = torch.zeros(C, dtype=_I32, device=dev)
+    W = (ncols + 63) // 64
+    nslabs = (W + sw - 1) // sw
+    lds = n_used * (sw + 2) * 8 + C * 4
+    n_wg = int(min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2)))
+    NP = int(plan["gpm"].shape[0])
+    rc = _native.hip().fa_hip_count_dfs(_p(roff), _p(ranks), _p(src), ncols, ptr[0], n_used, ptr[2], ptr[3], ptr[4],
+                                        ptr[5], ptr[6], NP, C, out.data_ptr(), sw, n_wg, _stream(ranks))
+    if rc == 3:
+        return None
+    _native.check(rc, "fa_hip_count_dfs")
+    LAST_LEVEL_PLAN.clear()
+    LAST_LEVEL_PLAN.update(kernel="dfs", rows=int(roff.numel() - 1), used=n_used, sw=sw, cap=int(
+        (_LDS_BYTES - n_used * (sw + 2) * 8) // 4), passes=1, pieces=NP, witems=0, d1=0, d2=0, trie_reads=0,
+        slab_reads=int(plan["gpm"][:, 1].sum() + plan["node1"].shape[0] + plan["node2"].shape[0]), m=-1, C=C)
+    return out.to(_I64)

@@ -1,0 +1,12 @@
+#!/bin/bash
+set -e
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/iter_tests.log 2>&1
+export FA_PHASE_TIMING=1
+timeout -k 10 200 python bench.py --steps 3 --warmup 1 > gpurun_out/it23_T10.json 2>/dev/null
+FA_BUNDLE_DFS=0 timeout -k 10 200 python bench.py --steps 3 --warmup 1 > gpurun_out/it23_T10_nodfs.json 2>/dev/null
+unset FA_PHASE_TIMING
+timeout -k 10 200 python bench.py --steps 5 --warmup 1 > gpurun_out/it23_T10_ns.json 2>/dev/null
+FA_BUNDLE_DFS=0 timeout -k 10 200 python bench.py --steps 5 --warmup 1 > gpurun_out/it23_T10_nodfs_ns.json 2>/dev/null
+timeout -k 10 200 python bench.py --n-txn 12500000 --steps 20 --warmup 3 > gpurun_out/it23_12M.json 2>/dev/null
+FA_BUNDLE_DFS=0 timeout -k 10 200 python bench.py --n-txn 12500000 --steps 20 --warmup 3 > gpurun_out/it23_12M_nodfs.json 2>/dev/null

@@ -2,4 +2,3 @@
 set -e
 mkdir -p gpurun_out
 timeout -k 10 300 python benchmarks/slab_probe.py --config T10I4D100M > gpurun_out/slab_probe_T10.log 2>&1
-timeout -k 10 400 python benchmarks/slab_probe.py --config T40I10D10M --modes 0,1,2 > gpurun_out/slab_probe_T40_10M.log 2>&1

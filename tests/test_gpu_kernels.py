@@ -246,6 +246,25 @@ def test_bundling_chain_matches_python_loop(monkeypatch):
     assert a.as_dict() == b.as_dict()
 
 
+@pytest.mark.parametrize("n,ms", [(200000, 0.003), (60000, 0.002)])
+def test_bundle_dfs_matches_slab_and_cpu(monkeypatch, n, ms):
+    # depth-2 prefix reuse over bundled levels == the plain slab bundle == the CPU miner
+    import fastapriori_amd.models.apriori as ap
+    sh = generate_shard(n, Comm(), "cpu", 10.0, 4.0, 60, 80, seed=12)
+    ref = FastApriori(ms, config=MinerConfig(min_support=ms, dedup="off")).run(sh).as_dict()
+    shg = sh.to(DEV)
+    seen = []
+    real = ops.primitives.count_bundle_dfs
+    monkeypatch.setattr(ops.primitives, "count_bundle_dfs",
+                        lambda *a, **k: seen.append(1) or real(*a, **k))
+    monkeypatch.setattr(ap, "BUNDLE_DFS_MIN_M", 2)        # every bundle
+    a = FastApriori(ms, config=MinerConfig(min_support=ms, dedup="off")).run(shg).as_dict()
+    assert seen, "no bundle took the DFS kernel"
+    monkeypatch.setattr(ap, "BUNDLE_DFS", False)
+    b = FastApriori(ms, config=MinerConfig(min_support=ms, dedup="off")).run(shg).as_dict()
+    assert a == b == ref
+
+
 def test_parse_to_device_roundtrip():
     sh = parse_bytes(b"1 2 3\n\n4 4 5\n", device=DEV)
     assert sh.items.is_cuda and sh.n_lines == 3
