@@ -222,9 +222,39 @@ FA_API int fa_hip_ag_gen(const int32_t* P, int64_t n, int m, int F1, void* ws, i
 //   workspace / int32 of host buffer to retry with.
 //   host, per accepted level l: cnt [n_l] | ext [C_l] | rows [C_l][m_l + 1]
 //   (n_{l+1} = C_l, m_{l+1} = m_l + 1).
+// Bundle accumulator limit (fastapriori_amd ops.primitives.slab_capacity / slab_total_limit):
+// slab capacity for n_used items and C candidates, and the largest total t with
+// t <= capacity(t).
+static int64_t ag_slab_cap(int64_t n_used, int64_t C, double lds) {
+  for (int sw : {32, 16, 8, 4}) {
+    const int64_t cap = (int64_t)((lds - (double)n_used * (sw + 2) * 8) / 4);
+    if (cap >= std::min<int64_t>(C, 8192) || (sw == 4 && cap >= 1024)) return cap;
+  }
+  return 0;
+}
+static int64_t ag_total_limit(int64_t n_used, double lds) {
+  int64_t lo = 0, hi = (int64_t)1 << 31;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi + 1) / 2;
+    if (mid <= ag_slab_cap(n_used, mid, lds)) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void k_ag_mark(const int32_t* __restrict__ rows, int64_t n,
+                                                 uint32_t* __restrict__ bits) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    atomicOr(&bits[rows[i] >> 5], 1u << (rows[i] & 31));
+}
+
+// first_free = 1 (lds > 0): P0 is F_{k-1} itself; level 0 (= level k's candidates)
+// is always emitted, its used items (a device bitset, read back with level 1's
+// count) give n_used and the bundle limit tmax, and the chain continues only if
+// level k alone fits one accumulator pass.  host[0 .. 128) then holds that bitset
+// and the levels start at host[128].
 FA_API int fa_hip_ag_chain(const int32_t* P0, int64_t n0, int m0, int F1, void* ws, int64_t ws_bytes, int32_t* host,
                            int64_t host_cap, int max_levels, double growth, int64_t total0, int64_t tmax,
-                           int64_t* sizes, hipStream_t st) {
+                           int64_t* sizes, hipStream_t st, int first_free, double lds) {
   sizes[0] = 0;
   if (n0 <= 0 || max_levels <= 0) return 0;
   if (m0 < 2 || F1 > 4096) return 1;
@@ -233,8 +263,14 @@ FA_API int fa_hip_ag_chain(const int32_t* P0, int64_t n0, int m0, int F1, void* 
   char* const w0 = static_cast<char*>(ws);
   char* w = w0;
   const int32_t* P = P0;
-  int64_t n = n0, last = n0, total = total0, hoff = 0;
+  int64_t n = n0, last = n0, total = total0, hoff = first_free ? 128 : 0;
   int m = m0, L = 0;
+  uint32_t* mark = nullptr;
+  if (first_free) {
+    if (host_cap < 128) { sizes[1] = 1 << 20; return 6; }
+    mark = reinterpret_cast<uint32_t*>(w); w += al(512);
+    (void)hipMemsetAsync(mark, 0, 512, st);
+  }
   int64_t* Cdev = nullptr;
   int64_t Ch = 0;
   for (int l = 0; l < max_levels; ++l) {
@@ -264,7 +300,15 @@ FA_API int fa_hip_ag_chain(const int32_t* P0, int64_t n0, int m0, int F1, void* 
     (void)hipMemcpyAsync(&Ch, Cdev, 8, hipMemcpyDeviceToHost, st);
     (void)hipStreamSynchronize(st);
     const int64_t C = Ch;
-    if (C == 0 || (double)C > growth * (double)last || total + C > tmax) break;
+    if (first_free && l == 1) {
+      // level k's used items arrived with this sync: the bundle limit
+      int64_t n_used = 0;
+      for (int q = 0; q < 128; ++q) n_used += __builtin_popcount((uint32_t)host[q]);
+      tmax = ag_total_limit(n_used, lds);
+      if (total > ag_slab_cap(n_used, total, lds)) break;   // level k alone needs several passes
+    }
+    if (C == 0) break;
+    if (!(first_free && l == 0) && ((double)C > growth * (double)last || total + C > tmax)) break;
     const int64_t need_ws = (w - w0) + al(4 * C) + al(4 * C * (m + 1));
     if (need_ws > ws_bytes) { sizes[1] = 2 * need_ws; return 5; }
     const int64_t need_host = hoff + n + C + C * (m + 1);
@@ -276,6 +320,11 @@ FA_API int fa_hip_ag_chain(const int32_t* P0, int64_t n0, int m0, int F1, void* 
     (void)hipMemcpyAsync(host + hoff, cnt, 4 * (size_t)n, hipMemcpyDeviceToHost, st);
     (void)hipMemcpyAsync(host + hoff + n, ext_out, 4 * (size_t)C, hipMemcpyDeviceToHost, st);
     (void)hipMemcpyAsync(host + hoff + n + C, rows_out, 4 * (size_t)C * (m + 1), hipMemcpyDeviceToHost, st);
+    if (first_free && l == 0) {
+      hipLaunchKernelGGL(k_ag_mark, dim3((unsigned)std::min<int64_t>((C * (m + 1) + 255) / 256, 1024)), dim3(256), 0,
+                         st, rows_out, C * (m + 1), mark);
+      (void)hipMemcpyAsync(host, mark, 512, hipMemcpyDeviceToHost, st);
+    }
     hoff = need_host;
     sizes[2 + l] = C;
     ++L;

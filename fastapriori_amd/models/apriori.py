@@ -160,8 +160,13 @@ class FastApriori:
                 k += 1
                 continue
             with roctx_range(f"level{k}"), tm.phase(f"level{k}"):
-                with tm.phase("apriori_gen"), roctx_range("gen"):
-                    prefix_idx, ext_off, ext, cand_rows = self._gen(levels[-1], want_rows=True)
+                fused = self._gen_bundle_fused(k, levels[-1])
+                if fused is None:
+                    with tm.phase("apriori_gen"), roctx_range("gen"):
+                        prefix_idx, ext_off, ext, cand_rows = self._gen(levels[-1], want_rows=True)
+                else:
+                    prefix_idx, ext_off, ext, cand_rows = fused[0] if fused else (None, None, np.zeros(0, np.int32),
+                                                                                  None)
                 C = int(ext.size)
                 self.log.line(f"{k} candidate items {C}")
                 if C == 0:
@@ -170,8 +175,11 @@ class FastApriori:
                     break
                 # level bundling: count the next levels' candidates, generated from this
                 # level's candidates, in the same launch (see _plan_bundle)
-                with tm.phase("apriori_gen"), roctx_range("bundle"):
-                    bundle = self._plan_bundle(db, k, levels[-1], prefix_idx, ext_off, ext, cand_rows)
+                if fused is not None:
+                    bundle = self._bundle_from_chain(k, levels[-1], fused)
+                else:
+                    with tm.phase("apriori_gen"), roctx_range("bundle"):
+                        bundle = self._plan_bundle(db, k, levels[-1], prefix_idx, ext_off, ext, cand_rows)
                 # later bundled levels only use items of level k's candidates
                 mark = np.zeros(max(db["F1"], 1), dtype=bool)
                 mark[self._bundle_rows[0].ravel()] = True
@@ -571,6 +579,30 @@ class FastApriori:
         rows = np.concatenate([prev[pi[g]], ex[:, None]], axis=1) if ex.size else \
             np.zeros((0, prev.shape[1] + 1), np.int32)
         return pi, eo, ex, np.ascontiguousarray(rows, dtype=np.int32)
+
+    def _gen_bundle_fused(self, k: int, prev: np.ndarray):
+        """apriori-gen of level k and the speculative bundle levels in ONE native call
+        (fa_hip_ag_chain, first_free): the candidate count of each level is the only
+        readback.  None when the device chain does not apply (then _gen + _plan_bundle)."""
+        dev = self._dev
+        if not (dev.type == "cuda" and GEN_DEVICE and GEN_CHAIN and BUNDLE_LEVELS and not self.cand_par
+                and self.cfg.level_kernel in ("auto", "slab") and k - 1 <= BUNDLE_MAX_PREFIX
+                and prev.shape[0] >= GEN_DEVICE_MIN_ROWS and prev.shape[1] >= 2
+                and self._F1 <= ops.primitives.AG_DEVICE_MAX_F1):
+            return None
+        max_lv = (self.cfg.max_level - k + 1) if self.cfg.max_level else 64
+        with roctx_range("gen_bundle"), self._timer.phase("apriori_gen"):
+            return ops.primitives.apriori_gen_chain(prev, self._F1, dev, max_lv, BUNDLE_GROWTH, 0, 0,
+                                                    first_free=True)
+
+    def _bundle_from_chain(self, k: int, prev: np.ndarray, chain: list) -> list:
+        bundle, rows, src = [], [], prev
+        for j, (pi, eo, ex, nxt) in enumerate(chain):
+            bundle.append((k + j, src, pi, eo, ex))
+            rows.append(np.ascontiguousarray(nxt, np.int32))
+            src = nxt
+        self._bundle_rows = rows
+        return bundle
 
     def _plan_bundle(self, db, k: int, prev: np.ndarray, prefix_idx, ext_off, ext, cand_rows=None) -> list:
         """Levels counted in one launch, starting with level k.

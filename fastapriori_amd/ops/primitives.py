@@ -961,12 +961,16 @@ def apriori_gen_device(prev: np.ndarray, F1: int, dev, want_rows: bool = False):
 
 
 def apriori_gen_chain(rows: np.ndarray, F1: int, dev, max_levels: int, growth: float, total0: int,
-                      tmax: int) -> list:
+                      tmax: int, first_free: bool = False) -> list:
     """Speculative levels for bundling in one native call (csrc/hip/gen.hip fa_hip_ag_chain):
     level m+1 candidates from ``rows`` (int32 [n, m], level k's candidate rows), then
     m+2 from those, ... while each level is non-empty, grows at most ``growth`` x
     and the bundle total stays <= ``tmax``.  Returns [(prefix_idx, ext_off, ext,
-    rows), ...] per accepted level, as apriori_gen_device."""
+    rows), ...] per accepted level, as apriori_gen_device.
+
+    first_free: ``rows`` is F_{k-1}; the first level (level k's candidates) is always
+    returned, and the bundle limit comes from its used items on the device (the
+    whole of apriori-gen + bundle planning in one call)."""
     n, m = rows.shape
     if n == 0 or max_levels <= 0:
         return []
@@ -981,7 +985,8 @@ def apriori_gen_chain(rows: np.ndarray, F1: int, dev, max_levels: int, growth: f
             ws = _GEN_WS[dev] = torch.empty(64 << 20, dtype=torch.uint8, device=dev)
         host = host_stage.get(4 * need_host).view(dtype=_I32)
         rc = _native.hip().fa_hip_ag_chain(_p(P), n, m, F1, _p(ws), ws.numel(), host.data_ptr(), host.numel(),
-                                           max_levels, growth, total0, tmax, sizes.ctypes.data, st)
+                                           max_levels, growth, total0, tmax, sizes.ctypes.data, st,
+                                           int(first_free), float(_LDS_BYTES))
         if rc == 5:
             _GEN_WS[dev] = torch.empty(int(sizes[1]), dtype=torch.uint8, device=dev)
             continue
@@ -993,7 +998,7 @@ def apriori_gen_chain(rows: np.ndarray, F1: int, dev, max_levels: int, growth: f
     else:
         raise RuntimeError("fa_hip_ag_chain: buffer sizing did not converge")
     h = host.numpy()
-    out, o = [], 0
+    out, o = [], (128 if first_free else 0)
     for lv in range(int(sizes[0])):
         C = int(sizes[2 + lv])
         cnt_h = h[o:o + n]

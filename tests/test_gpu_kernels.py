@@ -232,6 +232,16 @@ def test_gen_chain_matches_iterated_gen():
     assert len(two) == min(2, len(got))
     cap = ops.primitives.apriori_gen_chain(cand, F1, DEV, 4, 1e9, 0, got[0][2].size)
     assert len(cap) == 1
+    # first_free: level k itself from F_{k-1} in the same call, limit from its used items
+    ff = ops.primitives.apriori_gen_chain(prev, F1, DEV, 4, 1e9, 0, 0, first_free=True)
+    pi, eo, ex = apriori_gen(prev)
+    assert np.array_equal(ff[0][0], pi) and np.array_equal(ff[0][1], eo) and np.array_equal(ff[0][2], ex)
+    assert np.array_equal(ff[0][3], cand)
+    for a, b in zip(ff[1:], got):
+        assert all(np.array_equal(x, y) for x, y in zip(a, b))
+    used = np.unique(cand)
+    lim = ops.primitives.slab_total_limit(used.size)
+    assert sum(l[2].size for l in ff) <= max(lim, ff[0][2].size)
     c0 = got[0][2].size      # growth is measured against the previous level (the input for level 0)
     assert len(ops.primitives.apriori_gen_chain(cand, F1, DEV, 4, (c0 - 0.5) / cand.shape[0], 0, 1 << 40)) == 0
 
