@@ -56,6 +56,7 @@ FUSED_COMPRESS_MEAN_LEN = 12
 GEN_DEVICE = os.environ.get("FA_GEN_DEVICE", "1") == "1"
 GEN_CHAIN = os.environ.get("FA_GEN_CHAIN", "1") == "1"
 GEN_DEVICE_MIN_ROWS = int(os.environ.get("FA_GEN_DEVICE_MIN_ROWS", "512"))
+_TRIU_CACHE: dict = {}
 BUNDLE_DFS = os.environ.get("FA_BUNDLE_DFS", "1") == "1"
 # depth-2 reuse pays where prefixes are long; on short prefixes (k = 3: two items) the
 # lanes' uneven child loops cost more than the saved reads (T10I4D100M: bundle 3-4
@@ -253,7 +254,8 @@ class FastApriori:
                     hist += torch.bincount(torch.from_numpy(shard.extras.astype(np.int64)), minlength=V).to(dev)
                 comm.all_reduce_(hist)
                 fid = torch.nonzero(hist >= thr).flatten()
-                got = fid.cpu().numpy(), hist[fid].cpu().numpy()
+                h = torch.stack([fid, hist[fid].to(torch.int64)]).cpu().numpy()     # one readback
+                got = h[0], h[1]
             fid, fcnt = got
             # numeric tokens are ASCII decimal strings: Java String order == code-point
             # order, so one vectorised lexsort replaces a Python sort with string keys
@@ -551,13 +553,19 @@ class FastApriori:
                 roff, ranks = roff[a:b + 1] - ra, ranks[ra:rb]
                 wrow = wrow[a:b] if wrow is not None else None
             pc = ops.pair_counts_horizontal(roff, ranks, wrow, F1, db.get("long_rows", True))
-        iu = torch.triu_indices(F1, F1, 1, device=pc.device)
-        flat = pc[iu[0], iu[1]].contiguous()
+        key = (F1, pc.device)
+        if key not in _TRIU_CACHE:
+            _TRIU_CACHE.clear()
+            # upper-triangle positions of the F1 x F1 pair matrix, and their flat offsets
+            iu = torch.triu_indices(F1, F1, 1, device=pc.device)
+            _TRIU_CACHE[key] = (iu, iu[0] * F1 + iu[1])
+        iu, fi = _TRIU_CACHE[key]
+        flat = pc.reshape(-1)[fi]
         self.comm.all_reduce_(flat, bound=self.stats["n_lines"])
         keep = torch.nonzero(flat >= mc).flatten()
-        rows = torch.stack([iu[0][keep], iu[1][keep]], 1).to(torch.int32).cpu().numpy()
-        cnt = flat[keep].cpu().numpy().astype(np.int64)
-        return np.ascontiguousarray(rows), cnt
+        # one readback: rows (a, b) and counts
+        h = torch.stack([iu[0][keep], iu[1][keep], flat[keep].to(torch.int64)]).cpu().numpy()
+        return np.ascontiguousarray(h[:2].T, dtype=np.int32), h[2].astype(np.int64)
 
     # ------------------------------------------------------------------
     # k >= 3 (FastApriori.scala:132-160)
