@@ -324,3 +324,102 @@ FA_API int fa_level_plan(const int32_t* Pf, const int64_t* poff, int64_t G, cons
   info[18] = pos + pre_total + 4 * NP;
   return 0;
 }
+
+// ---------------------------------------------------------------------------
+// Work plan of a level bundle for the depth-2 prefix-reuse kernel
+// (k_count_slab<.., kDfs>; Python reference: ops.primitives.plan_bundle_dfs).
+// Level j: groups g (prefix = row pi[j][g] of pv[j], m[j] items), candidates
+// eo[j][g] .. eo[j][g+1] extending them by ex[j][c].  Level j+1's prefix rows are
+// level j's candidates, so level j+1 group g' hangs under level-j candidate
+// pi[j+1][g'].  Even levels are roots; the odd level after each is read as
+// depth-2 nodes.  buf (int32) receives, at the offsets written to info:
+//   item_map [F1] | used [n_used] | gpre | gpm [NP][2] | prng [NP][2] | node1 [N1][4] | node2 [N2][2]
+// info: 0 n_used 1 NP 2 N1 3 N2 4 C 5..11 offsets of the seven arrays 12 total.
+// Returns 0, or 3 when buf is too small.
+// ---------------------------------------------------------------------------
+FA_API int fa_plan_dfs(int L, const int32_t* const* pv, const int32_t* m, const int32_t* const* pi,
+                       const int64_t* const* eo, const int32_t* const* ex, const int64_t* G, const int64_t* Cn,
+                       int32_t F1, int piece_nodes, int32_t* buf, int64_t buf_cap, int64_t* info) {
+  for (int i = 0; i < 16; ++i) info[i] = 0;
+  if (L <= 0) return 0;
+  std::vector<int64_t> off(L + 1, 0);
+  for (int j = 0; j < L; ++j) off[j + 1] = off[j] + Cn[j];
+  int64_t NP = 0, N1 = 0, N2 = 0, npre = 0;
+  for (int j = 0; j < L; j += 2) {
+    for (int64_t g = 0; g < G[j]; ++g)
+      NP += std::max<int64_t>(1, (eo[j][g + 1] - eo[j][g] + piece_nodes - 1) / piece_nodes);
+    N1 += Cn[j];
+    npre += G[j] * m[j];
+    if (j + 1 < L) N2 += Cn[j + 1];
+  }
+  const int64_t need = 2 * (int64_t)F1 + npre + 4 * NP + 4 * N1 + 2 * std::max<int64_t>(N2, 1) + 64;
+  if (need > buf_cap) return 3;
+  int64_t pos = 0;
+  int32_t* item_map = buf + pos; info[5] = pos; pos += F1;
+  int32_t* used = buf + pos; info[6] = pos;
+  std::vector<uint8_t> mark((size_t)std::max(F1, 1), 0);
+  for (int64_t g = 0; g < G[0]; ++g)
+    for (int t = 0; t < m[0]; ++t) mark[pv[0][(int64_t)pi[0][g] * m[0] + t]] = 1;
+  for (int64_t c = 0; c < Cn[0]; ++c) mark[ex[0][c]] = 1;
+  int64_t n_used = 0;
+  for (int32_t r = 0; r < F1; ++r) {
+    if (mark[r]) { item_map[r] = (int32_t)n_used; used[n_used++] = r; } else item_map[r] = -1;
+  }
+  pos += n_used;
+  int32_t* gpre = buf + pos; info[7] = pos; pos += npre;
+  int32_t* gpm = buf + pos; info[8] = pos; pos += 2 * NP;
+  int32_t* prng = buf + pos; info[9] = pos; pos += 2 * NP;
+  int32_t* node1 = buf + pos; info[10] = pos; pos += 4 * N1;
+  int32_t* node2 = buf + pos; info[11] = pos; pos += 2 * std::max<int64_t>(N2, 1);
+  struct Piece { int32_t po, pl, b, e; int64_t cost; };
+  std::vector<Piece> pcs;
+  pcs.reserve((size_t)NP);
+  int64_t gp = 0, n1 = 0, n2 = 0;
+  std::vector<int64_t> n2b, n2e;
+  for (int j = 0; j < L; j += 2) {
+    const int mj = m[j];
+    for (int64_t g = 0; g < G[j]; ++g)
+      for (int t = 0; t < mj; ++t) gpre[gp + g * mj + t] = item_map[pv[j][(int64_t)pi[j][g] * mj + t]];
+    n2b.assign((size_t)Cn[j], 0);
+    n2e.assign((size_t)Cn[j], 0);
+    if (j + 1 < L) {
+      for (int64_t g = 0; g < G[j + 1]; ++g) {
+        const int32_t c = pi[j + 1][g];
+        n2b[c] = n2 + eo[j + 1][g];
+        n2e[c] = n2 + eo[j + 1][g + 1];
+      }
+      for (int64_t c = 0; c < Cn[j + 1]; ++c) {
+        node2[2 * (n2 + c)] = item_map[ex[j + 1][c]];
+        node2[2 * (n2 + c) + 1] = (int32_t)(off[j + 1] + c);
+      }
+    }
+    for (int64_t c = 0; c < Cn[j]; ++c) {
+      int32_t* nd = node1 + 4 * (n1 + c);
+      nd[0] = item_map[ex[j][c]];
+      nd[1] = (int32_t)(off[j] + c);
+      nd[2] = (int32_t)n2b[c];
+      nd[3] = (int32_t)n2e[c];
+    }
+    for (int64_t g = 0; g < G[j]; ++g) {
+      const int64_t a = eo[j][g], b = eo[j][g + 1];
+      for (int64_t x = a; x < std::max(b, a + 1); x += piece_nodes) {
+        const int64_t y = std::min(b, x + piece_nodes);
+        int64_t cost = mj + (y - x);
+        for (int64_t c = x; c < y; ++c) cost += n2e[c] - n2b[c];
+        pcs.push_back({(int32_t)(gp + g * mj), (int32_t)mj, (int32_t)(n1 + x), (int32_t)(n1 + y), cost});
+      }
+    }
+    gp += G[j] * mj;
+    n1 += Cn[j];
+    if (j + 1 < L) n2 += Cn[j + 1];
+  }
+  // cost-sorted pieces (the lanes of a wave then run loops of similar length)
+  std::stable_sort(pcs.begin(), pcs.end(), [](const Piece& x, const Piece& y) { return x.cost > y.cost; });
+  for (size_t i = 0; i < pcs.size(); ++i) {
+    gpm[2 * i] = pcs[i].po; gpm[2 * i + 1] = pcs[i].pl;
+    prng[2 * i] = pcs[i].b; prng[2 * i + 1] = pcs[i].e;
+  }
+  info[0] = n_used; info[1] = (int64_t)pcs.size(); info[2] = N1; info[3] = N2; info[4] = off[L];
+  info[12] = pos;
+  return 0;
+}

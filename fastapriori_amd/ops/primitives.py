@@ -1265,9 +1265,76 @@ def plan_bundle_dfs(levels: list, F1: int):
                 node1=node1, node2=node2, C=int(off[-1]))
 
 
+def plan_bundle_dfs_native(levels: list, F1: int, out: torch.Tensor | None = None):
+    """plan_bundle_dfs in C++ (csrc/host/plan.cpp fa_plan_dfs), written into one int32
+    buffer (``out``, e.g. pinned, grown as needed).  Returns (buf, info) with info =
+    (n_used, NP, N1, N2, C, offsets of item_map, used, gpre, gpm, prng, node1, node2,
+    total)."""
+    L = len(levels)
+    pv = [np.ascontiguousarray(lv[0], dtype=np.int32) for lv in levels]
+    pi = [np.ascontiguousarray(lv[1], dtype=np.int32) for lv in levels]
+    eo = [np.ascontiguousarray(lv[2], dtype=np.int64) for lv in levels]
+    ex = [np.ascontiguousarray(lv[3], dtype=np.int32) for lv in levels]
+    arr = lambda xs: (C.c_void_p * L)(*[x.ctypes.data for x in xs])   # noqa: E731
+    m = np.array([x.shape[1] for x in pv], dtype=np.int32)
+    G = np.array([x.size for x in pi], dtype=np.int64)
+    Cn = np.array([x.size for x in ex], dtype=np.int64)
+    NP = sum(int(np.maximum(1, (np.diff(eo[j]) + DFS_PIECE_NODES - 1) // DFS_PIECE_NODES).sum())
+             for j in range(0, L, 2))
+    need = int(2 * F1 + (G * m)[::2].sum() + 4 * NP + 4 * Cn[::2].sum() + 2 * max(int(Cn[1::2].sum()), 1) + 64)
+    buf = out if out is not None and out.numel() >= need else torch.empty(need, dtype=_I32)
+    info = np.zeros(16, dtype=np.int64)
+    rc = _native.host().fa_plan_dfs(L, C.cast(arr(pv), C.c_void_p), m.ctypes.data, C.cast(arr(pi), C.c_void_p),
+                                    C.cast(arr(eo), C.c_void_p), C.cast(arr(ex), C.c_void_p), G.ctypes.data,
+                                    Cn.ctypes.data, F1, DFS_PIECE_NODES, buf.data_ptr(), buf.numel(),
+                                    info.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(f"fa_plan_dfs failed ({rc})")
+    return buf, info
+
+
 def count_bundle_dfs(roff, ranks, src, ncols: int, F1: int, levels: list) -> torch.Tensor | None:
     """Counts of every level of a bundle (concatenated, level order) with depth-2
     prefix reuse; None when the bundle does not fit one LDS accumulator pass."""
+    dev = ranks.device
+    stage = pinned_stage("level_plan")
+    est = 2 * F1 + 8 * sum(int(lv[3].size) + int(lv[1].size) * (lv[0].shape[1] + 2) for lv in levels) + 1024
+    buf, info = plan_bundle_dfs_native(levels, F1, stage.get(4 * est).view(dtype=_I32))
+    n_used, NP, C = int(info[0]), int(info[1]), int(info[4])
+    sw = 0
+    for s in (32, 16, 8, 4):
+        cap = (_LDS_BYTES - n_used * (s + 2) * 8) // 4
+        if cap >= min(C, 8192) or (s == 4 and cap >= 1024):
+            sw = s
+            break
+    if sw == 0 or C > (_LDS_BYTES - n_used * (sw + 2) * 8) // 4:
+        return None
+    total = int(info[12])
+    dbuf = buf[:total].to(dev, non_blocking=True)
+    if buf.is_pinned():
+        stage.event = torch.cuda.Event()
+        stage.event.record()
+    base = dbuf.data_ptr()
+    ptr = [base + 4 * int(info[i]) for i in range(5, 12)]
+    out = torch.zeros(C, dtype=_I32, device=dev)
+    W = (ncols + 63) // 64
+    nslabs = (W + sw - 1) // sw
+    lds = n_used * (sw + 2) * 8 + C * 4
+    n_wg = int(min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2)))
+    rc = _native.hip().fa_hip_count_dfs(_p(roff), _p(ranks), _p(src), ncols, ptr[0], n_used, ptr[2], ptr[3], ptr[4],
+                                        ptr[5], ptr[6], NP, C, out.data_ptr(), sw, n_wg, _stream(ranks))
+    if rc == 3:
+        return None
+    _native.check(rc, "fa_hip_count_dfs")
+    LAST_LEVEL_PLAN.clear()
+    LAST_LEVEL_PLAN.update(kernel="dfs", rows=int(roff.numel() - 1), used=n_used, sw=sw, cap=int(
+        (_LDS_BYTES - n_used * (sw + 2) * 8) // 4), passes=1, pieces=NP, witems=0, d1=0, d2=0, trie_reads=0,
+        slab_reads=0, m=-1, C=C)
+    return out.to(_I64)
+
+
+def _count_bundle_dfs_numpy(roff, ranks, src, ncols: int, F1: int, levels: list) -> torch.Tensor | None:
+    """The same with the numpy planner (reference; not on the hot path)."""
     dev = ranks.device
     plan = plan_bundle_dfs(levels, F1)
     C, n_used = plan["C"], int(plan["used"].size)

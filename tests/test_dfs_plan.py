@@ -54,3 +54,23 @@ def test_dfs_plan_counts_every_candidate_once():
     # every candidate is exactly one node: depth-1 nodes for even levels, depth-2 for odd ones
     assert plan["node1"].shape[0] + (plan["node2"].shape[0] if len(levels) > 1 else 0) == plan["C"]
     assert set(plan["node1"][:, 1]) | set(plan["node2"][:, 1]) == set(range(plan["C"]))
+
+
+def test_native_plan_matches_numpy_plan():
+    items = np.arange(3, 15)
+    rows = np.array([(a, b, c) for a in items for b in items if b > a for c in items if c > b], dtype=np.int32)
+    levels = _chain(rows, 5)
+    assert len(levels) >= 3
+    ref = prim.plan_bundle_dfs(levels, 30)
+    buf, info = prim.plan_bundle_dfs_native(levels, 30)
+    b = buf.numpy()
+    n_used, NP, N1, N2 = (int(x) for x in info[:4])
+    o = [int(x) for x in info[5:12]]
+    assert int(info[4]) == ref["C"]
+    assert np.array_equal(b[o[0]:o[0] + 30], ref["item_map"][:30])
+    assert np.array_equal(b[o[1]:o[1] + n_used], ref["used"])
+    assert np.array_equal(b[o[2]:o[2] + ref["gpre"].size], ref["gpre"])
+    assert np.array_equal(b[o[3]:o[3] + 2 * NP].reshape(-1, 2), ref["gpm"])
+    assert np.array_equal(b[o[4]:o[4] + 2 * NP].reshape(-1, 2), ref["prng"])
+    assert np.array_equal(b[o[5]:o[5] + 4 * N1].reshape(-1, 4), ref["node1"])
+    assert np.array_equal(b[o[6]:o[6] + 2 * N2].reshape(-1, 2), ref["node2"])
