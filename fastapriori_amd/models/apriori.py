@@ -57,6 +57,9 @@ GEN_DEVICE = os.environ.get("FA_GEN_DEVICE", "1") == "1"
 GEN_CHAIN = os.environ.get("FA_GEN_CHAIN", "1") == "1"
 GEN_DEVICE_MIN_ROWS = int(os.environ.get("FA_GEN_DEVICE_MIN_ROWS", "512"))
 _TRIU_CACHE: dict = {}
+_POW10 = 10 ** np.arange(1, 11, dtype=np.int64)           # numeric token order (_frequent_items)
+_POW10_PAD = 10 ** (10 - np.arange(0, 12).clip(max=10)).astype(np.int64)
+_TOKEN_POOL = __import__("concurrent.futures").futures.ThreadPoolExecutor(1)
 BUNDLE_DFS = os.environ.get("FA_BUNDLE_DFS", "1") == "1"
 # depth-2 reuse pays where prefixes are long; on short prefixes (k = 3: two items) the
 # lanes' uneven child loops cost more than the saved reads (T10I4D100M: bundle 3-4
@@ -118,13 +121,14 @@ class FastApriori:
 
         with roctx_range("F1"), tm.phase("f1"):
             items, counts1, lut = self._frequent_items(shard, mc)
-        F1 = len(items)
+        F1 = len(counts1)
         self._F1, self._dev = F1, dev
         self._counts1 = counts1
         self.log.line(f"1 freq items {F1}")
         levels = [np.arange(F1, dtype=np.int32).reshape(-1, 1)]
         counts = [counts1]
         result = MiningResult(items, levels, counts, mc, n_global, self.stats)
+        self._result_items(result, wait=resume is not None or self.ckpt is not None)
         if resume is not None:
             self._check_resume(resume, result)
         if self.ckpt is not None:
@@ -216,7 +220,15 @@ class FastApriori:
             levels.pop(); counts.pop()
         return self._finish(result, t_start)
 
+    @staticmethod
+    def _result_items(result: MiningResult, wait: bool = True) -> None:
+        """Numeric-mode tokens are formatted on a helper thread while the GPU runs
+        (the order is already fixed); this puts the finished list into the result."""
+        if wait and not isinstance(result.items, list):
+            result.items = result.items.result()
+
     def _finish(self, result: MiningResult, t_start: float) -> MiningResult:
+        self._result_items(result)
         db = getattr(self, "_db_local", None)
         if db is not None:
             # layout sizes for the metrics, one collective after the last level
@@ -257,13 +269,17 @@ class FastApriori:
                 h = torch.stack([fid, hist[fid].to(torch.int64)]).cpu().numpy()     # one readback
                 got = h[0], h[1]
             fid, fcnt = got
-            # numeric tokens are ASCII decimal strings: Java String order == code-point
-            # order, so one vectorised lexsort replaces a Python sort with string keys
+            # numeric tokens are ASCII decimal strings, and Java String order of decimals
+            # is the order of (digits left-aligned to 10 places, then length): ties of
+            # equal counts sort without building strings ("" = id 0 sorts first)
             fid = np.asarray(fid, dtype=np.int64)
-            tok = (fid - 1).astype(str)
-            tok[fid == 0] = ""
-            order = np.lexsort((tok, -np.asarray(fcnt, dtype=np.int64))) if fid.size else np.zeros(0, np.int64)
-            items = tok[order].tolist()
+            v = fid - 1
+            d = np.searchsorted(_POW10, v, side="right") + 1
+            key = v * _POW10_PAD[d]
+            key[fid == 0], d[fid == 0] = -1, 0
+            order = np.lexsort((d, key, -np.asarray(fcnt, dtype=np.int64))) if fid.size else np.zeros(0, np.int64)
+            ids = fid[order]
+            items = _TOKEN_POOL.submit(lambda: ["" if i == 0 else str(i - 1) for i in ids.tolist()])
             counts1 = np.asarray(fcnt)[order].astype(np.int64)
             lut = torch.full((max(V, 1),), -1, dtype=torch.int32, device=dev)
             if len(order):
@@ -390,9 +406,15 @@ class FastApriori:
         else:
             # estimate the distinct fraction on a prefix sample of the rows
             n = min(db["T"], 1 << 20)
-            sub_off = db["roff"][: n + 1]
-            h1, _ = ops.row_hash(sub_off, db["ranks"][: int(sub_off[-1].item())])
-            frac = torch.unique(h1).numel() / max(n, 1)
+            h1, _ = ops.row_hash(db["roff"][: n + 1], db["ranks"])
+            # distinct fraction by linear counting (occupied slots of a 4M-slot bitmap of
+            # the row hashes: one scatter + one sum, instead of sorting the sample)
+            m = 1 << 22
+            occ = torch.zeros(m, dtype=torch.uint8, device=h1.device)
+            occ[h1 & (m - 1)] = 1
+            filled = int(occ.sum().item())
+            est = -m * math.log(max(1.0 - filled / m, 1.0 / m))
+            frac = est / max(n, 1)
             decision = frac < self.cfg.dedup_threshold
         # local decision: the caller agrees on it across ranks (the layout differs)
         return decision

@@ -34,3 +34,14 @@ def test_split_lines():
     assert split_lines("a\n") == ["a"]
     assert split_lines("\n\n") == ["", ""]
     assert split_lines("a\r\r\nb") == ["a", "", "b"]
+
+
+def test_numeric_f1_ties_follow_java_string_order():
+    # equal counts everywhere: ranks must follow Java String order of the tokens
+    # (numeric keys in FastApriori._frequent_items, no strings built for the sort)
+    from fastapriori_amd.models.apriori import FastApriori, MinerConfig
+    from fastapriori_amd.utils.io import parse_bytes
+    toks = ["0", "1", "2", "10", "19", "100", "1000000000", "999", "2147483646", "21474836"]
+    data = ("\n".join([" ".join(toks)] * 5 + [""] * 5) + "\n").encode()
+    res = FastApriori(0.1, config=MinerConfig(min_support=0.1)).run(parse_bytes(data))
+    assert res.items == sorted(toks + [""])
