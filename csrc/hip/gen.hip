@@ -241,6 +241,16 @@ static int64_t ag_total_limit(int64_t n_used, double lds) {
   return lo;
 }
 
+// Per-level workspace init of the chain: hash table <- -1, Ext bitsets <- 0, off[0] <- 0.
+__global__ __launch_bounds__(256) void k_ag_init(int32_t* __restrict__ table, int64_t cap,
+                                                 unsigned long long* __restrict__ ext, int64_t n_ext,
+                                                 int64_t* __restrict__ off) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < cap; i += stride) table[i] = -1;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_ext; i += stride) ext[i] = 0ull;
+  if (blockIdx.x == 0 && threadIdx.x == 0) off[0] = 0;
+}
+
 __global__ __launch_bounds__(256) void k_ag_mark(const int32_t* __restrict__ rows, int64_t n,
                                                  uint32_t* __restrict__ bits) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
@@ -283,12 +293,12 @@ FA_API int fa_hip_ag_chain(const int32_t* P0, int64_t n0, int m0, int F1, void* 
     if ((w - w0) + fixed > ws_bytes) { (void)hipStreamSynchronize(st); sizes[1] = 2 * ((w - w0) + fixed); return 5; }
     int32_t* table = reinterpret_cast<int32_t*>(w); w += al(4 * (int64_t)cap);
     unsigned long long* ext = reinterpret_cast<unsigned long long*>(w); w += al(8 * n * nw);
-    int32_t* cnt = reinterpret_cast<int32_t*>(w); w += al(4 * n);
     int64_t* off = reinterpret_cast<int64_t*>(w); w += al(8 * (n + 1));
     void* cub_tmp = w; w += al((int64_t)cub_bytes);
-    (void)hipMemsetAsync(table, 0xFF, 4 * (size_t)cap, st);
-    (void)hipMemsetAsync(ext, 0, 8 * (size_t)n * nw, st);
-    (void)hipMemsetAsync(off, 0, 8, st);
+    // cnt | ext_out | rows_out contiguous (the host layout): one readback per level
+    int32_t* cnt = reinterpret_cast<int32_t*>(w);
+    hipLaunchKernelGGL(k_ag_init, dim3((unsigned)std::min<int64_t>((cap + 255) / 256, 4096)), dim3(256), 0, st,
+                       table, (int64_t)cap, ext, n * nw, off);
     dim3 g((unsigned)((n + 255) / 256));
     hipLaunchKernelGGL(k_ag_insert, g, dim3(256), 0, st, P, n, m, table, cap - 1);
     hipLaunchKernelGGL(k_ag_ext, g, dim3(256), 0, st, P, n, m, table, cap - 1, nw, ext);
@@ -309,17 +319,16 @@ FA_API int fa_hip_ag_chain(const int32_t* P0, int64_t n0, int m0, int F1, void* 
     }
     if (C == 0) break;
     if (!(first_free && l == 0) && ((double)C > growth * (double)last || total + C > tmax)) break;
-    const int64_t need_ws = (w - w0) + al(4 * C) + al(4 * C * (m + 1));
+    const int64_t need_ws = (w - w0) + al(4 * (n + C + C * (m + 1)));
     if (need_ws > ws_bytes) { sizes[1] = 2 * need_ws; return 5; }
     const int64_t need_host = hoff + n + C + C * (m + 1);
     if (need_host > host_cap) { (void)hipStreamSynchronize(st); sizes[1] = 2 * need_host; return 6; }
-    int32_t* ext_out = reinterpret_cast<int32_t*>(w); w += al(4 * C);
-    int32_t* rows_out = reinterpret_cast<int32_t*>(w); w += al(4 * C * (m + 1));
+    int32_t* ext_out = cnt + n;
+    int32_t* rows_out = ext_out + C;
+    w += al(4 * (n + C + C * (m + 1)));
     hipLaunchKernelGGL(k_ag_rows<true>, dim3(nwg), dim3(256), 0, st, P, n, m, table, cap - 1, nw, ext, nullptr, off,
                        ext_out, rows_out);
-    (void)hipMemcpyAsync(host + hoff, cnt, 4 * (size_t)n, hipMemcpyDeviceToHost, st);
-    (void)hipMemcpyAsync(host + hoff + n, ext_out, 4 * (size_t)C, hipMemcpyDeviceToHost, st);
-    (void)hipMemcpyAsync(host + hoff + n + C, rows_out, 4 * (size_t)C * (m + 1), hipMemcpyDeviceToHost, st);
+    (void)hipMemcpyAsync(host + hoff, cnt, 4 * (size_t)(n + C + C * (m + 1)), hipMemcpyDeviceToHost, st);
     if (first_free && l == 0) {
       hipLaunchKernelGGL(k_ag_mark, dim3((unsigned)std::min<int64_t>((C * (m + 1) + 255) / 256, 1024)), dim3(256), 0,
                          st, rows_out, C * (m + 1), mark);
