@@ -59,7 +59,19 @@ GEN_DEVICE_MIN_ROWS = int(os.environ.get("FA_GEN_DEVICE_MIN_ROWS", "512"))
 _TRIU_CACHE: dict = {}
 _POW10 = 10 ** np.arange(1, 11, dtype=np.int64)           # numeric token order (_frequent_items)
 _POW10_PAD = 10 ** (10 - np.arange(0, 12).clip(max=10)).astype(np.int64)
-_TOKEN_POOL = __import__("concurrent.futures").futures.ThreadPoolExecutor(1)
+
+
+class _Deferred:
+    """Host work whose result is needed only later: run while a long kernel is in
+    flight (FastApriori._run_deferred), or on first use."""
+
+    def __init__(self, fn):
+        self.fn, self.value, self.done = fn, None, False
+
+    def result(self):
+        if not self.done:
+            self.value, self.done = self.fn(), True
+        return self.value
 BUNDLE_DFS = os.environ.get("FA_BUNDLE_DFS", "1") == "1"
 # depth-2 reuse pays where prefixes are long; on short prefixes (k = 3: two items) the
 # lanes' uneven child loops cost more than the saved reads (T10I4D100M: bundle 3-4
@@ -109,6 +121,7 @@ class FastApriori:
         # candidate parallelism: the data is replicated, so data-side collectives
         # (line count, F1, layout decisions) are local; only count vectors move
         self.cand_par = self.cfg.parallelism == "candidate" and self.comm.distributed
+        self._deferred = []
         self.dcomm = Comm(device=self.comm.device) if self.cand_par else self.comm
         comm = self.dcomm
         # line total and numeric vocabulary width in one collective
@@ -220,10 +233,15 @@ class FastApriori:
             levels.pop(); counts.pop()
         return self._finish(result, t_start)
 
+    def _run_deferred(self) -> None:
+        for d in self._deferred:
+            d.result()
+        self._deferred = []
+
     @staticmethod
     def _result_items(result: MiningResult, wait: bool = True) -> None:
-        """Numeric-mode tokens are formatted on a helper thread while the GPU runs
-        (the order is already fixed); this puts the finished list into the result."""
+        """Numeric-mode tokens are formatted while the pair kernel runs (the order is
+        already fixed); this puts the finished list into the result."""
         if wait and not isinstance(result.items, list):
             result.items = result.items.result()
 
@@ -279,7 +297,8 @@ class FastApriori:
             key[fid == 0], d[fid == 0] = -1, 0
             order = np.lexsort((d, key, -np.asarray(fcnt, dtype=np.int64))) if fid.size else np.zeros(0, np.int64)
             ids = fid[order]
-            items = _TOKEN_POOL.submit(lambda: ["" if i == 0 else str(i - 1) for i in ids.tolist()])
+            items = _Deferred(lambda: ["" if i == 0 else str(i - 1) for i in ids.tolist()])
+            self._deferred.append(items)
             counts1 = np.asarray(fcnt)[order].astype(np.int64)
             lut = torch.full((max(V, 1),), -1, dtype=torch.int32, device=dev)
             if len(order):
@@ -575,6 +594,7 @@ class FastApriori:
                 roff, ranks = roff[a:b + 1] - ra, ranks[ra:rb]
                 wrow = wrow[a:b] if wrow is not None else None
             pc = ops.pair_counts_horizontal(roff, ranks, wrow, F1, db.get("long_rows", True))
+        self._run_deferred()      # host-only work while the pair kernel runs
         key = (F1, pc.device)
         if key not in _TRIU_CACHE:
             _TRIU_CACHE.clear()
