@@ -32,6 +32,24 @@ def test_cli_on_gpu_matches_oracle(tmp_path):
     assert open(tmp_path / "o_recommends/part-00000").read().splitlines() == recs
 
 
+def test_cli_under_torchrun_rccl_matches_oracle(tmp_path):
+    # the CLI job through torchrun with an RCCL process group (world size 1, every
+    # collective forced): shard reading, line offsets, gathers and rank-0 writes
+    write_quest_file(str(tmp_path / "D.dat"), 3000, 8.0, 3.0, 40, 40, seed=8)
+    write_quest_file(str(tmp_path / "U.dat"), 700, 8.0, 3.0, 40, 40, seed=8, users=True)
+    env = dict(os.environ, PYTHONPATH=ROOT, FA_FORCE_PG="1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                        "--master-addr", "127.0.0.1", "--master-port", "29561", "-m", "fastapriori_amd",
+                        f"{tmp_path}/", f"{tmp_path}/o_", f"{tmp_path}/t", "--min-support", "0.03",
+                        "--device", "cuda"], capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = open(tmp_path / "D.dat").read().splitlines()
+    u = open(tmp_path / "U.dat").read().splitlines()
+    lines, recs, _ = run_oracle(d, u, 0.03)
+    assert open(tmp_path / "o_freqItemset/part-00000").read().splitlines() == lines
+    assert open(tmp_path / "o_recommends/part-00000").read().splitlines() == recs
+
+
 def _gpu_rank(n, ms):
     from fastapriori_amd.models.apriori import FastApriori, MinerConfig
     from fastapriori_amd.parallel.comm import init_comm, shutdown_comm
