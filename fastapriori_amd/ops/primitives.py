@@ -1331,43 +1331,3 @@ def count_bundle_dfs(roff, ranks, src, ncols: int, F1: int, levels: list) -> tor
         (_LDS_BYTES - n_used * (sw + 2) * 8) // 4), passes=1, pieces=NP, witems=0, d1=0, d2=0, trie_reads=0,
         slab_reads=0, m=-1, C=C)
     return out.to(_I64)
-
-
-def _count_bundle_dfs_numpy(roff, ranks, src, ncols: int, F1: int, levels: list) -> torch.Tensor | None:
-    """The same with the numpy planner (reference; not on the hot path)."""
-    dev = ranks.device
-    plan = plan_bundle_dfs(levels, F1)
-    C, n_used = plan["C"], int(plan["used"].size)
-    sw = 0
-    for s in (32, 16, 8, 4):
-        cap = (_LDS_BYTES - n_used * (s + 2) * 8) // 4
-        if cap >= min(C, 8192) or (s == 4 and cap >= 1024):
-            sw = s
-            break
-    if sw == 0 or C > (_LDS_BYTES - n_used * (sw + 2) * 8) // 4:
-        return None
-    parts = [plan["item_map"], plan["used"], plan["gpre"], plan["gpm"].ravel(), plan["prng"].ravel(),
-             plan["node1"].ravel(), plan["node2"].ravel()]
-    offs = np.concatenate([[0], np.cumsum([(p.size + 3) // 4 * 4 for p in parts])])
-    host = np.zeros(int(offs[-1]), dtype=np.int32)
-    for p, o in zip(parts, offs[:-1]):
-        host[o:o + p.size] = p
-    dbuf = pinned_stage("level_plan").h2d(host, dev)
-    base = dbuf.data_ptr()
-    ptr = [base + 4 * int(o) for o in offs[:-1]]
-    out = torch.zeros(C, dtype=_I32, device=dev)
-    W = (ncols + 63) // 64
-    nslabs = (W + sw - 1) // sw
-    lds = n_used * (sw + 2) * 8 + C * 4
-    n_wg = int(min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2)))
-    NP = int(plan["gpm"].shape[0])
-    rc = _native.hip().fa_hip_count_dfs(_p(roff), _p(ranks), _p(src), ncols, ptr[0], n_used, ptr[2], ptr[3], ptr[4],
-                                        ptr[5], ptr[6], NP, C, out.data_ptr(), sw, n_wg, _stream(ranks))
-    if rc == 3:
-        return None
-    _native.check(rc, "fa_hip_count_dfs")
-    LAST_LEVEL_PLAN.clear()
-    LAST_LEVEL_PLAN.update(kernel="dfs", rows=int(roff.numel() - 1), used=n_used, sw=sw, cap=int(
-        (_LDS_BYTES - n_used * (sw + 2) * 8) // 4), passes=1, pieces=NP, witems=0, d1=0, d2=0, trie_reads=0,
-        slab_reads=int(plan["gpm"][:, 1].sum() + plan["node1"].shape[0] + plan["node2"].shape[0]), m=-1, C=C)
-    return out.to(_I64)
