@@ -6,18 +6,31 @@ database (F1 histogram + all-reduce, compression, vertical bitmaps, every
 level's candidate generation + counting + all-reduce, results replicated on
 every rank).  The database (100M Quest transactions, |T|=10, |I|=4, |L|=2000,
 N=1000 items) is generated deterministically per rank and kept resident in HBM
-before timing; parsing text is not part of the step (the CLI path parses with
-the native mmap parser, measured separately by benchmarks/run_bench.py).
-The total work is fixed as N grows, so scaling is "strong".
+before timing.  The total work is fixed as N grows, so scaling is "strong".
+
+After the timed steps the reference's own timing window (Main.scala:28-32:
+read + parse D.dat, mine, write freqItemset) is measured on the same database
+written to a D.dat file: once with the file's pages dropped from the page cache
+(posix_fadvise DONTNEED after fsync) and then warm.  Those numbers go into the
+JSON line's "e2e" record (``--e2e off`` skips them).
+
+``vs_baseline`` = this run's itemsets/s over the multi-threaded C++ CPU path of
+the same miner on the same config (BASELINE.md:27; profiles/cpu_<config>.json,
+measured by benchmarks/run_bench.py --mode cpu).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config T10I4D100M]
-    torchrun --nproc-per-node N bench.py --gpus N ...
+
+``--gpus N`` > 1 without a torchrun environment re-launches this script under
+``torch.distributed.run`` with N ranks (one per GPU, RCCL); under torchrun the
+world size must equal N or the run fails.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import shutil
+import subprocess
 import sys
 import time
 
@@ -40,9 +53,9 @@ CONFIGS = {
 HEADLINE = "T10I4D100M"
 
 
-def main() -> int:
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="number of ranks (one per GPU)")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default=HEADLINE, choices=sorted(CONFIGS))
@@ -54,7 +67,120 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--strategy", choices=["count", "candidate"], default="count",
                     help="count: each rank generates its row shard; candidate: every rank holds all rows")
-    args = ap.parse_args()
+    ap.add_argument("--e2e", choices=["auto", "on", "off"], default="auto",
+                    help="also time the reference window (read+parse+mine+write) on a D.dat file "
+                         "(auto: on for file-backed configs)")
+    ap.add_argument("--e2e-runs", type=int, default=2, help="warm-cache e2e runs after the cold one")
+    ap.add_argument("--workdir", default="", help="where the e2e D.dat is written (default $TMPDIR)")
+    return ap.parse_args(argv)
+
+
+def _relaunch(args) -> int:
+    """--gpus N from a plain `python bench.py`: start N ranks under torch.distributed.run.
+
+    This parent never touches the GPU; the children pick their device from LOCAL_RANK."""
+    from fastapriori_amd.parallel.launch import free_port
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__),
+           *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def cpu_baseline(config: str, min_sup: float, n_txn: int):
+    """itemsets/s of the C++ CPU path on the same config (profiles/cpu_<config>.json), or None."""
+    p = os.path.join(ROOT, "profiles", f"cpu_{config}.json")
+    if not os.path.exists(p):
+        return None
+    rec = None
+    with open(p) as f:
+        for line in f:
+            line = line.strip()
+            if line.startswith("{"):
+                rec = json.loads(line)
+    if not rec or rec.get("n_txn") != n_txn or abs(rec.get("min_support", min_sup) - min_sup) > 1e-12:
+        return None
+    return rec
+
+
+def _e2e_window(args, comm, n_txn, min_sup, cfgv, miner_cfg, sync):
+    """The reference's "Total time for get freqItemsets" window on a real D.dat."""
+    import torch
+    from fastapriori_amd.models.apriori import FastApriori
+    from fastapriori_amd.utils import io
+    from fastapriori_amd.utils.metrics import Logger
+    _, avg_len, avg_pat, n_pat, n_items, _ = cfgv
+    base = args.workdir or os.environ.get("TMPDIR") or "/tmp"
+    d = os.path.join(base, f"fa_bench_{args.config}_{n_txn}_{args.seed}")
+    path = os.path.join(d, "D.dat")
+    out = os.path.join(d, f"out_{os.getpid() if comm.is_root else 0}", "freqItemset")
+    t_w = time.perf_counter()
+    if comm.is_root:
+        os.makedirs(d, exist_ok=True)
+        if not os.path.exists(path):
+            tmp = path + ".tmp"
+            io.write_quest_file(tmp, n_txn, avg_len, avg_pat, n_pat, n_items, seed=args.seed)
+            os.replace(tmp, path)
+    comm.barrier()
+    write_s = time.perf_counter() - t_w
+    quiet = Logger(comm.rank, enabled=False)
+
+    def one_run():
+        sync()
+        t0 = time.perf_counter()
+        shard = io.read_shard(path, comm)
+        res = FastApriori(min_sup, comm, miner_cfg, quiet).run(shard)
+        if comm.is_root:
+            io.write_freq_itemsets(res, out, overwrite=True)
+        del shard
+        sync()
+        return comm.allreduce_float_max((time.perf_counter() - t0) * 1e3), res
+
+    # cold: the file's pages dropped from the page cache (every rank's local view)
+    dropped = False
+    if comm.is_root:
+        fd = os.open(path, os.O_RDONLY)
+        try:
+            os.fsync(fd)
+            os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+            dropped = True
+        except OSError:
+            dropped = False
+        finally:
+            os.close(fd)
+    comm.barrier()
+    cold_ms, res = one_run()
+    warm = [one_run()[0] for _ in range(max(args.e2e_runs, 1))]
+    warm_ms = min(warm)
+    if comm.is_root:
+        shutil.rmtree(os.path.dirname(out), ignore_errors=True)
+    if comm.device.type == "cuda":
+        torch.cuda.empty_cache()
+    return {
+        "window": "read+parse D.dat, mine, write freqItemset (Main.scala:28-32)",
+        "D_bytes": os.path.getsize(path), "file_write_s": round(write_s, 1),
+        "cold_ms": round(cold_ms, 1), "cold_cache_dropped": dropped,
+        "warm_ms": round(warm_ms, 1), "warm_runs": [round(x, 1) for x in warm],
+        "itemsets_per_s_cold": round(res.n_itemsets / (cold_ms / 1e3), 1),
+        "itemsets_per_s_warm": round(res.n_itemsets / (warm_ms / 1e3), 1),
+        "n_itemsets": res.n_itemsets,
+    }, path
+
+
+def main() -> int:
+    args = parse_args()
+    in_torchrun = "WORLD_SIZE" in os.environ and "RANK" in os.environ
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        return 2
+    if args.gpus > 1 and not in_torchrun:
+        return _relaunch(args)
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
+    if env_world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks",
+              file=sys.stderr)
+        return 2
 
     import torch
     from fastapriori_amd.models.apriori import FastApriori, MinerConfig
@@ -64,6 +190,9 @@ def main() -> int:
 
     dev = args.device if (args.device != "cuda" or torch.cuda.is_available()) else "cpu"
     comm = init_comm(dev)
+    if comm.world_size != args.gpus:
+        print(f"bench.py: process group has {comm.world_size} ranks, --gpus {args.gpus}", file=sys.stderr)
+        return 2
     n_txn, avg_len, avg_pat, n_pat, n_items, ms = CONFIGS[args.config]
     n_txn = args.n_txn or n_txn
     min_sup = args.min_support or ms
@@ -71,7 +200,8 @@ def main() -> int:
 
     t_gen = time.perf_counter()
     data_comm = comm if args.strategy == "count" else Comm(device=comm.device)
-    if args.config.startswith("webdocs"):
+    webdocs = args.config.startswith("webdocs")
+    if webdocs:
         shard = generate_zipf_shard(n_txn, data_comm, comm.device, mean_len=avg_len, n_items=n_items,
                                     n_topics=n_pat, seed=args.seed)
     else:
@@ -102,29 +232,49 @@ def main() -> int:
     ms_step = comm.allreduce_float_max(elapsed * 1e3 / max(args.steps, 1))
     n_sets = res.n_itemsets
     value = n_sets / (ms_step / 1e3)
+    stats = dict(miner.stats)
+
+    e2e = None
+    want_e2e = args.e2e == "on" or (args.e2e == "auto" and not webdocs and args.strategy == "count")
+    if want_e2e and args.steps > 0:
+        del shard
+        e2e, _ = _e2e_window(args, comm, n_txn, min_sup, CONFIGS[args.config], cfg, sync)
+        if e2e["n_itemsets"] != n_sets:
+            print(f"bench.py: e2e run found {e2e['n_itemsets']} itemsets, in-memory run {n_sets}",
+                  file=sys.stderr)
+            return 3
+
+    base = cpu_baseline(args.config, min_sup, n_txn)
     if comm.is_root:
         line = {
             "metric": f"itemsets/sec (mining wall-clock), {args.config} min_sup={min_sup:g}",
             "value": round(value, 2),
             "unit": "itemsets/s",
             "n_gpus": world if comm.device.type == "cuda" else 0,
+            "world_size": world,
+            "backend": comm.backend,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
             "scaling": "strong",
-            "vs_baseline": None,
+            "vs_baseline": round(value / base["itemsets_per_s"], 2) if base else None,
+            "baseline": ({"what": "C++ CPU path of the same miner, same config (BASELINE.md:27)",
+                          "itemsets_per_s": base["itemsets_per_s"], "ms": base["ms"],
+                          "threads": base.get("threads"), "source": f"profiles/cpu_{args.config}.json"}
+                         if base else None),
             "dtype": "int32/uint64-bitmap (exact integer counts)",
-            "data": (f"synthetic {'Zipf-topic' if args.config.startswith('webdocs') else 'Quest'} {args.config} "
+            "data": (f"synthetic {'Zipf-topic' if webdocs else 'Quest'} {args.config} "
                      f"(n={n_txn}, seed={args.seed}), generated in-process"),
             "config": {"model": args.config, "global_batch": n_txn, "seq_len": avg_len,
                        "parallelism": f"{'dp' if args.strategy == 'count' else 'cp'}{world}",
                        "min_support": min_sup,
                        "n_itemsets": n_sets, "levels": [len(c) for c in res.counts],
-                       "pair_strategy": miner.stats.get("pair_strategy"),
+                       "pair_strategy": stats.get("pair_strategy"),
                        "min_count": res.min_count, "gen_s": round(t_gen, 2),
-                       **({"phase_ms": miner.stats["phase_ms"]} if "phase_ms" in miner.stats else {}),
-                       **({"level_info": miner.stats["level_info"]} if "level_info" in miner.stats else {})},
+                       **({"phase_ms": stats["phase_ms"]} if "phase_ms" in stats else {}),
+                       **({"level_info": stats["level_info"]} if "level_info" in stats else {})},
+            "e2e": e2e,
         }
         print(json.dumps(line), flush=True)
     shutdown_comm(comm)

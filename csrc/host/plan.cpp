@@ -352,7 +352,9 @@ FA_API int fa_plan_dfs(int L, const int32_t* const* pv, const int32_t* m, const 
     npre += G[j] * m[j];
     if (j + 1 < L) N2 += Cn[j + 1];
   }
-  const int64_t need = 2 * (int64_t)F1 + npre + 4 * NP + 4 * N1 + 2 * std::max<int64_t>(N2, 1) + 64;
+  // + 8: node1 is read as int4 and node2 as int2 (count.hip), so their offsets are
+  // rounded up to 4 and 2 int32
+  const int64_t need = 2 * (int64_t)F1 + npre + 4 * NP + 4 * N1 + 2 * std::max<int64_t>(N2, 1) + 64 + 8;
   if (need > buf_cap) return 3;
   int64_t pos = 0;
   int32_t* item_map = buf + pos; info[5] = pos; pos += F1;
@@ -369,7 +371,9 @@ FA_API int fa_plan_dfs(int L, const int32_t* const* pv, const int32_t* m, const 
   int32_t* gpre = buf + pos; info[7] = pos; pos += npre;
   int32_t* gpm = buf + pos; info[8] = pos; pos += 2 * NP;
   int32_t* prng = buf + pos; info[9] = pos; pos += 2 * NP;
+  pos = (pos + 3) & ~(int64_t)3;
   int32_t* node1 = buf + pos; info[10] = pos; pos += 4 * N1;
+  pos = (pos + 1) & ~(int64_t)1;
   int32_t* node2 = buf + pos; info[11] = pos; pos += 2 * std::max<int64_t>(N2, 1);
   struct Piece { int32_t po, pl, b, e; int64_t cost; };
   std::vector<Piece> pcs;

@@ -39,6 +39,7 @@ class JobConfig:
     metrics_path: str | None = None
     max_level: int = 0
     strategy: str = "count"                     # count | candidate distribution
+    world_size: int = 0                         # 0: whatever torchrun started; N: launch / require N ranks
     extra: dict = field(default_factory=dict)
 
 
@@ -65,6 +66,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--strategy", choices=["count", "candidate"], default=_env("FA_STRATEGY", "count"),
                    help="count: shard transactions, all-reduce counts; candidate: replicate the DB on every "
                         "rank and split pairs by rows, level candidates by rank")
+    p.add_argument("--world-size", type=int, default=_env("FA_WORLD_SIZE", 0),
+                   help="number of ranks (one per GPU). Without a torchrun environment the job "
+                        "re-launches itself under torch.distributed.run; under torchrun the process "
+                        "group must have exactly this many ranks")
     return p
 
 
@@ -74,4 +79,4 @@ def parse_args(argv=None) -> JobConfig:
                      dedup=a.dedup, pair_strategy=a.pair_strategy, with_counts=a.with_counts, resume=a.resume,
                      rules_only=a.rules_only, checkpoint=a.checkpoint, overwrite=a.overwrite,
                      profile=a.profile, metrics_path=a.metrics_path, max_level=a.max_level,
-                     strategy=a.strategy)
+                     strategy=a.strategy, world_size=a.world_size)

@@ -446,6 +446,11 @@ class FastApriori:
         """
         roff, ranks, T = db["roff"], db["ranks"], db["T"]
         dev = ranks.device
+        if T == 0:
+            # a shard without kept rows still takes the agreed (weighted) layout
+            db.update(wrow=torch.zeros(0, dtype=torch.int32, device=dev), n_distinct=0)
+            self._layout_weighted(db)
+            return
         h1, h2 = ops.row_hash(roff, ranks)
         o = torch.argsort(h2, stable=True)
         o = o[torch.argsort(h1[o], stable=True)]

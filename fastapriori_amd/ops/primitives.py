@@ -1281,7 +1281,7 @@ def plan_bundle_dfs_native(levels: list, F1: int, out: torch.Tensor | None = Non
     Cn = np.array([x.size for x in ex], dtype=np.int64)
     NP = sum(int(np.maximum(1, (np.diff(eo[j]) + DFS_PIECE_NODES - 1) // DFS_PIECE_NODES).sum())
              for j in range(0, L, 2))
-    need = int(2 * F1 + (G * m)[::2].sum() + 4 * NP + 4 * Cn[::2].sum() + 2 * max(int(Cn[1::2].sum()), 1) + 64)
+    need = int(2 * F1 + (G * m)[::2].sum() + 4 * NP + 4 * Cn[::2].sum() + 2 * max(int(Cn[1::2].sum()), 1) + 64 + 8)
     buf = out if out is not None and out.numel() >= need else torch.empty(need, dtype=_I32)
     info = np.zeros(16, dtype=np.int64)
     rc = _native.host().fa_plan_dfs(L, C.cast(arr(pv), C.c_void_p), m.ctypes.data, C.cast(arr(pi), C.c_void_p),

@@ -205,6 +205,13 @@ def init_comm(device: str | None = None, backend: str | None = None, timeout_s: 
     # FA_DIST_BACKEND=gloo lets several ranks share one GPU (tests on a 1-GPU box);
     # production GPU runs use RCCL ("nccl"), one process per GPU.
     be = backend or os.environ.get("FA_DIST_BACKEND") or ("nccl" if dev.type == "cuda" else "gloo")
+    if be == "nccl":
+        # one process per GPU: RCCL cannot run two ranks of one communicator on one device
+        n_local = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+        n_dev = torch.cuda.device_count()
+        if n_local > n_dev:
+            raise RuntimeError(f"{n_local} local ranks but {n_dev} visible GPUs: RCCL needs one GPU per rank "
+                               "(FA_DIST_BACKEND=gloo lets ranks share a GPU for tests)")
     if not dist.is_initialized():
         kw = dict(backend=be, timeout=timedelta(seconds=timeout_s))
         if be == "nccl":
@@ -214,10 +221,23 @@ def init_comm(device: str | None = None, backend: str | None = None, timeout_s: 
 
 
 def shutdown_comm(comm: Comm) -> None:
+    """Leave the process group.  The closing barrier is skipped while an exception
+    propagates (called from a ``finally``): the peers may be blocked in another
+    collective, and a failed rank must exit rather than wait for them (fail fast)."""
+    import sys
     if comm.distributed and dist.is_initialized():
+        failing = sys.exc_info()[0] is not None
         try:
-            comm.barrier()
+            if not failing:
+                comm.barrier()
         finally:
+            if failing and comm.backend == "nccl":
+                # a clean destroy would wait for the peers' pending collectives
+                try:
+                    dist.distributed_c10d._abort_process_group()   # noqa: SLF001
+                    return
+                except Exception:
+                    pass
             dist.destroy_process_group()
 
 

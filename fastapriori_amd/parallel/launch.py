@@ -11,6 +11,7 @@ import os
 import pickle
 import socket
 import tempfile
+import time
 import traceback
 
 
@@ -44,13 +45,40 @@ def spawn_local(fn, world: int, *args, env: dict | None = None, timeout: float =
     with tempfile.TemporaryDirectory() as d:
         ctx = mp.start_processes(_worker, args=(world, free_port(), fn, args, d, env), nprocs=world,
                                  join=False, start_method="spawn")
-        ok = True
-        try:
-            ok = ctx.join(timeout)
-            while not ok:
-                ok = ctx.join(timeout)
-        except Exception:
-            ok = False
+        # fail fast: a rank that dies makes join() raise; a hang (ranks blocked in a
+        # collective their peer never reaches) runs into the deadline instead
+        deadline = time.monotonic() + timeout
+        timed_out = False
+        while True:
+            try:
+                if ctx.join(max(0.1, min(5.0, deadline - time.monotonic()))):
+                    break
+            except Exception:
+                break          # a rank failed: its result file says why
+            if time.monotonic() >= deadline:
+                timed_out = True
+                break
+        alive = [r for r, p in enumerate(ctx.processes) if p.is_alive()]
+        for p in ctx.processes:
+            if p.is_alive():
+                p.terminate()
+        for p in ctx.processes:
+            p.join(10)
+            if p.is_alive():
+                p.kill()
+                p.join(5)
+        if timed_out:
+            raise TimeoutError(f"spawn_local: ranks {alive} still running after {timeout:.0f} s")
+        errors = []
+        for r in range(world):
+            p = os.path.join(d, f"rank{r}.pkl")
+            if os.path.exists(p):
+                # our own file, written just above by our own worker
+                status, val = pickle.load(open(p, "rb"))
+                if status != "ok":
+                    errors.append(f"rank {r} failed:\n{val}")
+        if errors:
+            raise RuntimeError("\n".join(errors))
         out = []
         for r in range(world):
             p = os.path.join(d, f"rank{r}.pkl")

@@ -22,11 +22,31 @@ from .utils.checkpoint import Checkpointer, input_fingerprint
 from .utils.metrics import Logger
 
 
+def _load_checkpoint(ckpt: Checkpointer, comm, require_complete: bool = False):
+    """Rank 0 reads the checkpoint and sends it to every rank, so all ranks resume
+    from the same level (a per-rank read could race rank 0's rewrite of meta.json,
+    or miss a temp dir that is not shared, and then the ranks' collectives diverge)."""
+    res, err = None, None
+    if comm.is_root:
+        try:
+            res = ckpt.load(require_complete=require_complete)
+        except (OSError, ValueError, KeyError) as e:
+            err = f"{type(e).__name__}: {e}"
+    res, err = comm.broadcast_object((res, err))
+    if err:
+        raise ValueError(f"checkpoint load failed on rank 0: {err}")
+    return res
+
+
 def run_job(cfg: JobConfig, comm=None) -> dict:
     own_comm = comm is None
     if comm is None:
         dev = None if cfg.device == "auto" else cfg.device
         comm = init_comm(dev)
+    if cfg.world_size and comm.world_size != cfg.world_size:
+        if own_comm:
+            shutdown_comm(comm)
+        raise RuntimeError(f"--world-size {cfg.world_size} but the process group has {comm.world_size} ranks")
     log = Logger(comm.rank, metrics_path=cfg.metrics_path)
     d_path, u_path = cfg.input + "D.dat", cfg.input + "U.dat"
     out_freq, out_rec = cfg.output + "freqItemset", cfg.output + "recommends"
@@ -44,11 +64,11 @@ def run_job(cfg: JobConfig, comm=None) -> dict:
         if cfg.rules_only:
             if ckpt is None:
                 raise ValueError("--rules-only needs the temp path of a previous run")
-            result = ckpt.load(require_complete=True)
+            result = _load_checkpoint(ckpt, comm, require_complete=True)
             if result is None:
                 raise FileNotFoundError(f"no complete checkpoint under {ckpt.dir}")
         else:
-            resume = ckpt.load() if (ckpt is not None and cfg.resume) else None
+            resume = _load_checkpoint(ckpt, comm) if (ckpt is not None and cfg.resume) else None
             # candidate distribution: every rank holds the whole DB
             t_read = time.time()
             shard = io.read_shard(d_path, comm if cfg.strategy == "count" else Comm(device=comm.device))
@@ -93,9 +113,26 @@ def run_job(cfg: JobConfig, comm=None) -> dict:
             shutdown_comm(comm)
 
 
+def _relaunch(cfg: JobConfig, argv) -> int:
+    """``--world-size N`` from a plain ``python -m fastapriori_amd``: start N ranks (one per
+    GPU) under torch.distributed.run.  This parent process never touches the GPU."""
+    import subprocess
+    import sys
+
+    from .parallel.launch import free_port
+    argv = list(sys.argv[1:] if argv is None else argv)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={cfg.world_size}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}", "-m", "fastapriori_amd", *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def main(argv=None) -> int:
     from .config import parse_args
     cfg = parse_args(argv)
+    if cfg.world_size > 1 and "WORLD_SIZE" not in os.environ:
+        return _relaunch(cfg, argv)
     if cfg.profile:
         os.environ.setdefault("FA_METRICS", os.path.join(cfg.temp or ".", "fastapriori_metrics.jsonl"))
     run_job(cfg)

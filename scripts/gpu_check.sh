@@ -1,9 +1,14 @@
 #!/bin/bash
-# Quick GPU verification: kernel tests, smoke, headline bench, deep-k bench.
-set -e
+# Round check on one MI355X: GPU tests, the driver's bench command (with the e2e
+# window), and the C++ CPU baseline of the headline config (vs_baseline).
+# Every GPU step has its own time limit; the chain stops at the first failure.
+set -e -o pipefail
 mkdir -p gpurun_out
-export FA_PHASE_TIMING=1
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
-timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
-timeout -k 10 300 python bench.py --steps 5 --warmup 1 > gpurun_out/bench_T10I4D100M.json 2> gpurun_out/bench_T10I4D100M.err
-timeout -k 10 500 python bench.py --config T40I10D100M --steps 2 --warmup 1 > gpurun_out/bench_T40I10D100M.json 2> gpurun_out/bench_T40I10D100M.err
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+  > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 300 python bench.py --steps 10 --warmup 3 > gpurun_out/bench.json 2> gpurun_out/bench.err
+if [ "${FA_CPU_BASELINE:-0}" = "1" ]; then
+  timeout -k 10 600 python benchmarks/run_bench.py --mode cpu --device cpu --config T10I4D100M --steps 1 \
+    --warmup 0 > gpurun_out/cpu_T10I4D100M.json 2> gpurun_out/cpu_T10I4D100M.err
+fi
