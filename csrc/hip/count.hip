@@ -53,11 +53,7 @@ constexpr int kPW = 16;                // waves per workgroup (1024 threads)
 constexpr int kWSpan = 1024;           // ranks staged per wave batch
 constexpr int kWPer = kWSpan / 64;     // per lane
 
-__device__ __forceinline__ void wave_lds_fence() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
+__device__ __forceinline__ void wave_lds_fence() { wave_lds_sync(); }
 
 // Per-row block table: bt[x*(nb+1) + b] = offset (within row x) of its first
 // rank >= b*kPB; bt[x*(nb+1) + nb] = row length.  Built once per mining run so
@@ -552,82 +548,100 @@ constexpr int kRowsDw = 3;                  // staged dwords per lane and block
 constexpr int kRowsStage = 64 * kRowsDw * 4; // 768 staged local-rank bytes per wave and block
 constexpr int kRowsWin = kRowsStage / 64;    // 12 windows
 
-__global__ __launch_bounds__(1024) void k_pair_rows16(
-    const uint8_t* __restrict__ cnt, const int64_t* __restrict__ base, const uint8_t* __restrict__ lr,
-    int64_t T, int64_t nbatch, int32_t F1, int nb, int nbp, int64_t chunk_b, uint32_t* __restrict__ out, int dbg) {
-  __shared__ uint32_t tile[kPB16 * kPB16 / 2];
-  __shared__ uint32_t sa[kPW][kRowsStage / 4];
-  __shared__ uint32_t sb[kPW][kRowsStage / 4];
-  __shared__ uint8_t rowtab[kPW][64];
-  __shared__ unsigned long long swd[kPW][kRowsWin];
-  const uint32_t logical = xcd_remap(blockIdx.x, gridDim.x);
-  const int pid = logical % nbp;
-  // one chunk of <= 65472 rows per workgroup keeps the 16-bit counters exact.
-  // (Folding many chunks into u32 register accumulators instead, to cut the
-  // flush atomics, measured slower: 64 more VGPRs spill at 16 waves/CU.)
-  const int64_t ch = logical / nbp;
-  int bi, bj;
-  tri_index(pid, nb, bi, bj);
-  const int rb0 = bi * kPB16, cb0 = bj * kPB16;
-  const bool diag = bi == bj;
-  for (int i = threadIdx.x; i < kPB16 * kPB16 / 2; i += blockDim.x) tile[i] = 0;
-  __syncthreads();
+// Batches [q0, q1) of tile (bi, bj) into the packed-u16 LDS tile (no barriers).
+struct PairRowsLds {
+  uint32_t tile[kPB16 * kPB16 / 2];
+  uint32_t sa[kPW][kRowsStage / 4];
+  uint32_t sb[kPW][kRowsStage / 4];
+  uint8_t rowtab[kPW][64];
+  unsigned long long swd[kPW][kRowsWin];
+};
+
+// kDiag (bi == bj) is a template parameter: a runtime select between the two
+// count loads made the compiler wait for the prefetched load right after issue.
+//
+// Software pipeline with two register sets X / Y (the loop is unrolled twice, so
+// nothing is copied between iterations: a copy of a register that a load is
+// still filling would wait for it).  Per batch: "meta" = the rows' block counts
+// and the two segment bases, issued two batches ahead; "bytes" = the segments'
+// aligned dwords (addresses from meta), issued one batch ahead.  Every load is
+// unconditional -- cnt, base and lr are padded past their ends by the launcher
+// (batches past the chunk read real or padding data that is never processed) --
+// so the compiler's wait counts are exact and a wait never drains the loads
+// issued for later batches.
+struct PairBatch {
+  int ci, cj;            // this lane's row: items in block bi / bj
+  int64_t vb;            // lane 0: segment base in block bi, lane 1: in block bj
+  uint32_t da[kRowsDw], db[kRowsDw];
+};
+
+template <bool kDiag>
+__device__ __forceinline__ void pair_rows16_chunk_t(PairRowsLds& L, const uint8_t* __restrict__ cnt,
+                                                    const int64_t* __restrict__ base,
+                                                    const uint8_t* __restrict__ lr, int64_t T, int64_t nbatch,
+                                                    int bi, int bj, int64_t q0, int64_t q1, int dbg) {
+  uint32_t* tile = L.tile;
+  auto& sa = L.sa;
+  auto& sb = L.sb;
+  auto& rowtab = L.rowtab;
+  auto& swd = L.swd;
+  constexpr bool diag = kDiag;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const unsigned long long le = lanes_le_mask(), lt = le >> 1;
-  const int64_t q0 = ch * chunk_b, q1 = min(nbatch, q0 + chunk_b);
   const uint8_t* ci_row = cnt + (int64_t)bi * T;
   const uint8_t* cj_row = cnt + (int64_t)bj * T;
-  const int64_t* base_i = base + (int64_t)bi * nbatch;
-  const int64_t* base_j = base + (int64_t)bj * nbatch;
-  // Software pipeline over this wave's batches q, q + kPW, ...: block bases two
-  // batches ahead, counts and the aligned local-rank dwords one batch ahead.
-  auto ld_counts = [&](int64_t qq, int& a, int& b) {
+  const int64_t bsel = (lane & 1) ? (int64_t)bj * nbatch : (int64_t)bi * nbatch;
+  auto load_meta = [&](PairBatch& B, int64_t qq) {
     const int64_t x = qq * 64 + lane;
-    a = (qq < q1 && x < T) ? ci_row[x] : 0;
-    b = diag ? a : ((qq < q1 && x < T) ? cj_row[x] : 0);
+    B.ci = ci_row[x];
+    if (!kDiag) B.cj = cj_row[x];
+    B.vb = base[bsel + qq];            // lane-varying address: a vector load
   };
-  auto ld_bytes = [&](int64_t off, uint32_t (&d)[kRowsDw]) {
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(lr + (off & ~(int64_t)3));
+  auto load_bytes = [&](PairBatch& B) {
+    const int64_t oa = (int64_t)__builtin_amdgcn_readlane((int)B.vb, 0) |
+                       ((int64_t)__builtin_amdgcn_readlane((int)(B.vb >> 32), 0) << 32);
+    const uint32_t* pa = reinterpret_cast<const uint32_t*>(lr + (oa & ~(int64_t)3));
 #pragma unroll
-    for (int k = 0; k < kRowsDw; ++k) d[k] = p[lane + 64 * k];    // lr is padded by >= 1 KiB
+    for (int k = 0; k < kRowsDw; ++k) B.da[k] = pa[lane + 64 * k];   // lr is padded by >= 1 KiB
+    if (!kDiag) {
+      const int64_t ob = (int64_t)__builtin_amdgcn_readlane((int)B.vb, 1) |
+                         ((int64_t)__builtin_amdgcn_readlane((int)(B.vb >> 32), 1) << 32);
+      const uint32_t* pb = reinterpret_cast<const uint32_t*>(lr + (ob & ~(int64_t)3));
+#pragma unroll
+      for (int k = 0; k < kRowsDw; ++k) B.db[k] = pb[lane + 64 * k];
+    }
   };
-  int64_t q = q0 + wv;
-  int ci, cj, ci_n, cj_n;
-  ld_counts(q, ci, cj);
-  ld_counts(q + kPW, ci_n, cj_n);
-  int64_t oa = q < q1 ? base_i[q] : 0, ob = q < q1 ? base_j[q] : 0;
-  int64_t oa_n = q + kPW < q1 ? base_i[q + kPW] : 0, ob_n = q + kPW < q1 ? base_j[q + kPW] : 0;
-  uint32_t da[kRowsDw], db[kRowsDw], da_n[kRowsDw], db_n[kRowsDw];
-  if (q < q1) { ld_bytes(oa, da); if (!diag) ld_bytes(ob, db); }
-  for (; q < q1; q += kPW) {
-    // issue the next batches' loads first
-    int ci_nn, cj_nn;
-    ld_counts(q + 2 * kPW, ci_nn, cj_nn);
-    const int64_t oa_nn = q + 2 * kPW < q1 ? base_i[q + 2 * kPW] : 0;
-    const int64_t ob_nn = q + 2 * kPW < q1 ? base_j[q + 2 * kPW] : 0;
-    if (q + kPW < q1) { ld_bytes(oa_n, da_n); if (!diag) ld_bytes(ob_n, db_n); }
-
+  auto process = [&](PairBatch& X, int64_t qq) {
+    const int ci = (qq * 64 + lane < T) ? X.ci : 0;
+    const int cj = diag ? ci : ((qq * 64 + lane < T) ? X.cj : 0);
+    const int64_t oa = (int64_t)__builtin_amdgcn_readlane((int)X.vb, 0) |
+                       ((int64_t)__builtin_amdgcn_readlane((int)(X.vb >> 32), 0) << 32);
+    const int64_t ob = diag ? oa : ((int64_t)__builtin_amdgcn_readlane((int)X.vb, 1) |
+                                    ((int64_t)__builtin_amdgcn_readlane((int)(X.vb >> 32), 1) << 32));
     const int inci = wave_scan_incl_dpp(ci);
-    const int SA = wave_last(inci);
     const int incj = diag ? inci : wave_scan_incl_dpp(cj);
+    const int SA = wave_last(inci);
     const int SB = diag ? SA : wave_last(incj);
     const bool has = diag ? ci >= 2 : (ci > 0 && cj > 0);
-    if (__ballot(has) != 0ull) {
-      const int sha = (int)(oa & 3), shb = (int)(ob & 3);
-      const bool stA = SA + sha <= kRowsStage, stB = diag || SB + shb <= kRowsStage;
+    if (__ballot(has) == 0ull) return;
+    const int sha = (int)(oa & 3), shb = (int)(ob & 3);
+    const bool stA = SA + sha <= kRowsStage, stB = diag || SB + shb <= kRowsStage;
 #pragma unroll
-      for (int k = 0; k < kRowsDw; ++k) {
-        sa[wv][lane + 64 * k] = da[k];
-        if (!diag) sb[wv][lane + 64 * k] = db[k];
-      }
-      const unsigned long long M = __ballot(ci > 0);
-      if (ci > 0) rowtab[wv][__popcll(M & lt)] = (uint8_t)lane;
-      wave_lds_sync();
-      const uint8_t* A = stA ? reinterpret_cast<const uint8_t*>(sa[wv]) + sha : lr + oa;
-      const uint8_t* B = diag ? A : (stB ? reinterpret_cast<const uint8_t*>(sb[wv]) + shb : lr + ob);
-      const int jbeg = diag ? 0 : incj - cj;          // row owner view: my row's block-bj span
-      const int jend = diag ? inci : incj;
-      const int srow = ci > 0 ? inci - ci : -(1 << 30);
+    for (int k = 0; k < kRowsDw; ++k) {
+      sa[wv][lane + 64 * k] = X.da[k];
+      if (!diag) sb[wv][lane + 64 * k] = X.db[k];
+    }
+    const unsigned long long M = __ballot(ci > 0);
+    if (ci > 0) rowtab[wv][__popcll(M & lt)] = (uint8_t)lane;
+    wave_lds_sync();
+    const int jbeg = diag ? 0 : incj - cj;          // row owner view: my row's block-bj span
+    const int jend = diag ? inci : incj;
+    const int srow = ci > 0 ? inci - ci : -(1 << 30);
+    // A and B are either both LDS stages or both global: each call site then has
+    // one address space, so the byte reads are ds_read_u8 / global_load_ubyte
+    // (a pointer that may be either compiles to flat loads, whose waits also
+    // drain the prefetched global loads)
+    auto run_windows = [&](const uint8_t* __restrict__ A, const uint8_t* __restrict__ B) {
       auto scatter = [&](int p0, unsigned long long Sw, int& cs) {
         const int k = cs + __popcll(Sw & le) - 1;
         cs += __popcll(Sw);
@@ -637,15 +651,21 @@ __global__ __launch_bounds__(1024) void k_pair_rows16(
         const int j1 = __shfl(jend, row, 64);
         if (diag) j0 = p + 1;
         if (p < SA && !(dbg & 1)) {
-          const int i = (int)A[p] * kPB16;
+          // word of (a, b) = a * 128 + ((b >> 1) ^ (a & 31)): the bank (word mod 32)
+          // depends on a as well as b, so the lanes of one row (different a, same b
+          // in the off-diagonal tiles) hit different banks (pair_tile16_word)
+          const int a = (int)A[p];
+          const int rowb = a * (kPB16 / 2), xa = a & 31;
           for (int j = j0; j < j1; ++j) {
-            const int idx = i + (int)B[j];
-            atomicAdd(&tile[idx >> 1], (idx & 1) ? 0x10000u : 1u);
+            const int b = (int)B[j];
+            atomicAdd(&tile[rowb + ((b >> 1) ^ xa)], (b & 1) ? 0x10000u : 1u);
           }
         }
       };
-      int cs = 0;                                      // non-empty rows started before the window
-      if (SA <= kRowsStage) {
+      int cs = 0;                                    // non-empty rows started before the window
+      if (dbg & 8) {
+        // profiling split: batch-level work only (no windows)
+      } else if (SA <= kRowsStage) {
         // row-start masks, 4 windows per LDS round trip
 #pragma unroll
         for (int w0 = 0; w0 < kRowsWin; w0 += 4) {
@@ -663,22 +683,183 @@ __global__ __launch_bounds__(1024) void k_pair_rows16(
           scatter(p0, S[0], cs);
         }
       }
-      wave_lds_sync();
+    };
+    if (stA && stB) {
+      const uint8_t* As = reinterpret_cast<const uint8_t*>(sa[wv]) + sha;
+      run_windows(As, diag ? As : reinterpret_cast<const uint8_t*>(sb[wv]) + shb);
+    } else {
+      run_windows(lr + oa, diag ? lr + oa : lr + ob);
     }
-    ci = ci_n; cj = cj_n; ci_n = ci_nn; cj_n = cj_nn;
-    oa = oa_n; ob = ob_n; oa_n = oa_nn; ob_n = ob_nn;
-#pragma unroll
-    for (int k = 0; k < kRowsDw; ++k) { da[k] = da_n[k]; db[k] = db_n[k]; }
+    wave_lds_sync();
+  };
+  // batch t lives in set t % 3: its meta is issued two batches before its bytes'
+  // turn, its bytes one batch before it is processed
+  int64_t q = q0 + wv;
+  if (q >= q1) return;
+  PairBatch X, Y, Z;
+  load_meta(X, q);
+  load_meta(Y, q + kPW);
+  load_meta(Z, q + 2 * kPW);
+  load_bytes(X);
+  for (;;) {
+    load_bytes(Y);
+    process(X, q);
+    load_meta(X, q + 3 * kPW);
+    if ((q += kPW) >= q1) break;
+    load_bytes(Z);
+    process(Y, q);
+    load_meta(Y, q + 3 * kPW);
+    if ((q += kPW) >= q1) break;
+    load_bytes(X);
+    process(Z, q);
+    load_meta(Z, q + 3 * kPW);
+    if ((q += kPW) >= q1) break;
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < ((dbg & 2) ? 0 : kPB16 * kPB16 / 2); i += blockDim.x) {
+}
+
+__device__ __forceinline__ void pair_rows16_chunk(PairRowsLds& L, const uint8_t* __restrict__ cnt,
+                                                  const int64_t* __restrict__ base,
+                                                  const uint8_t* __restrict__ lr, int64_t T, int64_t nbatch,
+                                                  int bi, int bj, int64_t q0, int64_t q1, int dbg) {
+  if (bi == bj) pair_rows16_chunk_t<true>(L, cnt, base, lr, T, nbatch, bi, bj, q0, q1, dbg);
+  else pair_rows16_chunk_t<false>(L, cnt, base, lr, T, nbatch, bi, bj, q0, q1, dbg);
+}
+
+// Packed-u16 tile -> global counts.  With an even row stride (ld) the two
+// counters of a word go out as one 64-bit atomic (two adjacent u32 counts; a
+// u32 count never carries: it is bounded by the rows of the shard < 2^31).
+// (row, column) of word i of a swizzled rows16 tile (see pair_rows16_chunk)
+__device__ __forceinline__ void pair_tile16_word(int i, int rb0, int cb0, int& r, int& c) {
+  const int a = i >> 7;
+  r = rb0 + a;
+  c = cb0 + 2 * ((i & 127) ^ (a & 31));
+}
+
+__device__ __forceinline__ void pair_tile16_flush(const uint32_t* tile, int bi, int bj, int32_t F1, int64_t ld,
+                                                  uint32_t* __restrict__ out) {
+  const int rb0 = bi * kPB16, cb0 = bj * kPB16;
+  const bool pair64 = (ld & 1) == 0;
+  for (int i = threadIdx.x; i < kPB16 * kPB16 / 2; i += blockDim.x) {
     const uint32_t v = tile[i];
     if (!v) continue;
-    const int idx = 2 * i;
-    const int r = rb0 + idx / kPB16, c = cb0 + idx % kPB16;
+    int r, c;
+    pair_tile16_word(i, rb0, cb0, r, c);
     if (r >= F1) continue;
-    if ((v & 0xFFFF) && c < F1) atomicAdd(&out[(int64_t)r * F1 + c], v & 0xFFFF);
-    if ((v >> 16) && c + 1 < F1) atomicAdd(&out[(int64_t)r * F1 + c + 1], v >> 16);
+    uint32_t* o = out + (int64_t)r * ld + c;
+    if (pair64 && c + 1 < F1) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(o),
+                (unsigned long long)(v & 0xFFFFu) | ((unsigned long long)(v >> 16) << 32));
+    } else {
+      if ((v & 0xFFFF) && c < F1) atomicAdd(o, v & 0xFFFF);
+      if ((v >> 16) && c + 1 < F1) atomicAdd(o + 1, v >> 16);
+    }
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_pair_rows16(
+    const uint8_t* __restrict__ cnt, const int64_t* __restrict__ base, const uint8_t* __restrict__ lr,
+    int64_t T, int64_t nbatch, int32_t F1, int nb, int nbp, int64_t chunk_b, uint32_t* __restrict__ out, int dbg) {
+  __shared__ PairRowsLds L;
+  const uint32_t logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int pid = logical % nbp;
+  // one chunk of <= 65472 rows per workgroup keeps the 16-bit counters exact.
+  // (Folding many chunks into u32 register accumulators instead, to cut the
+  // flush atomics, measured slower: 64 more VGPRs spill at 16 waves/CU.)
+  const int64_t ch = logical / nbp;
+  int bi, bj;
+  tri_index(pid, nb, bi, bj);
+  for (int i = threadIdx.x; i < kPB16 * kPB16 / 2; i += blockDim.x) L.tile[i] = 0;
+  __syncthreads();
+  const int64_t q0 = ch * chunk_b, q1 = min(nbatch, q0 + chunk_b);
+  pair_rows16_chunk(L, cnt, base, lr, T, nbatch, bi, bj, q0, q1, dbg);
+  __syncthreads();
+  if (!(dbg & 2)) pair_tile16_flush(L.tile, bi, bj, F1, F1, out);
+}
+
+// Work-queue schedule of the same tiles: one persistent workgroup per CU, a
+// queue of sub-chunks (<= 32767 rows) per tile.  A workgroup starts on its home
+// tile (blockIdx % nbp) and keeps its LDS tile across sub-chunks: after each
+// one, counters with bit 15 set give 32768 to the global count ("drain"), so
+// every counter stays < 32768 + 32767 and a tile is flushed only when the
+// workgroup moves to another tile (then: the tile with the most sub-chunks
+// left) or ends.  The one-chunk-per-workgroup schedule (k_pair_rows16) flushes
+// a full 64K-counter tile per 65K rows: ~1e9 global atomics on T10I4D100M.
+// Every workgroup exits once all queues are exhausted (each grab increments a
+// queue counter, which never decreases).
+constexpr int64_t kQSubB = 511;   // batches per sub-chunk: 32704 rows
+
+__global__ __launch_bounds__(1024) void k_pair_queue16(
+    const uint8_t* __restrict__ cnt, const int64_t* __restrict__ base, const uint8_t* __restrict__ lr,
+    int64_t T, int64_t nbatch, int32_t F1, int64_t ld, int nb, int nbp, int* __restrict__ qctr, int nsub,
+    uint32_t* __restrict__ out, int dbg) {
+  __shared__ PairRowsLds L;
+  __shared__ int s_take[2];
+  int cur = -1;                                 // tile held in LDS
+  int t = (int)(blockIdx.x % (unsigned)nbp);    // tile to take work from
+  for (;;) {
+    if (threadIdx.x == 0) {
+      int got = -1, tt = t;
+      if (tt >= 0) {
+        const int g = atomicAdd(&qctr[tt], 1);
+        if (g < nsub) got = g;
+      }
+      if (got < 0) {
+        // this tile is exhausted: the tile with the most sub-chunks left, if any
+        int best = -1, left = 0;
+        for (int x = 0; x < nbp; ++x) {
+          const int l = nsub - __hip_atomic_load(&qctr[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (l > left) { left = l; best = x; }
+        }
+        tt = best;
+        if (tt >= 0) {
+          const int g = atomicAdd(&qctr[tt], 1);
+          got = g < nsub ? g : -2;              // -2: lost a race, look again
+        }
+      }
+      s_take[0] = tt;
+      s_take[1] = got;
+    }
+    __syncthreads();
+    const int tt = s_take[0], got = s_take[1];
+    __syncthreads();
+    if (got == -2) { t = -1; continue; }
+    if (tt < 0 || got < 0) break;
+    t = tt;
+    if (tt != cur) {
+      if (cur >= 0 && !(dbg & 2)) {
+        int bi, bj;
+        tri_index(cur, nb, bi, bj);
+        pair_tile16_flush(L.tile, bi, bj, F1, ld, out);
+      }
+      __syncthreads();
+      for (int i = threadIdx.x; i < kPB16 * kPB16 / 2; i += blockDim.x) L.tile[i] = 0;
+      __syncthreads();
+      cur = tt;
+    }
+    int bi, bj;
+    tri_index(cur, nb, bi, bj);
+    const int64_t q0 = (int64_t)got * kQSubB, q1 = min(nbatch, q0 + kQSubB);
+    pair_rows16_chunk(L, cnt, base, lr, T, nbatch, bi, bj, q0, q1, dbg);
+    __syncthreads();
+    // drain: bit 15 of either counter -> 32768 to the global count
+    const int rb0 = bi * kPB16, cb0 = bj * kPB16;
+    for (int i = threadIdx.x; i < kPB16 * kPB16 / 2; i += blockDim.x) {
+      const uint32_t v = L.tile[i];
+      const uint32_t hb = v & 0x80008000u;
+      if (!hb) continue;
+      L.tile[i] = v - hb;
+      int r, c;
+      pair_tile16_word(i, rb0, cb0, r, c);
+      if (r >= F1) continue;
+      if ((hb & 0x8000u) && c < F1 && !(dbg & 2)) atomicAdd(&out[(int64_t)r * ld + c], 32768u);
+      if ((hb >> 16) && c + 1 < F1 && !(dbg & 2)) atomicAdd(&out[(int64_t)r * ld + c + 1], 32768u);
+    }
+    __syncthreads();
+  }
+  if (cur >= 0 && !(dbg & 2)) {
+    int bi, bj;
+    tri_index(cur, nb, bi, bj);
+    pair_tile16_flush(L.tile, bi, bj, F1, ld, out);
   }
 }
 
@@ -1625,6 +1806,25 @@ FA_API int fa_hip_pair_blocked16(const uint8_t* cnt, const int64_t* base, const 
   const int64_t nch = (nbatch + chunk_b - 1) / chunk_b;
   hipLaunchKernelGGL(k_pair_blocked16, dim3((unsigned)(nch * nbp)), dim3(64 * kPW), 0, st, cnt, base, lr, T, nbatch,
                      F1, nb, nbp, chunk_b, out);
+  FA_LAUNCH_RET();
+}
+
+// Work-queue schedule (k_pair_queue16): qctr = nbp zeroed ints, out has row stride ld.
+FA_API int fa_hip_pair_queue16(const uint8_t* cnt, const int64_t* base, const uint8_t* lr, int64_t T, int32_t F1,
+                               int64_t ld, int* qctr, uint32_t* out, int n_wg, hipStream_t st) {
+  if (T <= 0 || F1 < 2) return 0;
+  const int nb = (F1 + kPB16 - 1) / kPB16;
+  const int nbp = nb * (nb + 1) / 2;
+  const int64_t nbatch = (T + 63) / 64;
+  const int nsub = (int)((nbatch + kQSubB - 1) / kQSubB);
+  if (n_wg <= 0) {
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    n_wg = ncu;
+  }
+  n_wg = (int)std::min<int64_t>(n_wg, (int64_t)nsub * nbp);
+  hipLaunchKernelGGL(k_pair_queue16, dim3((unsigned)n_wg), dim3(64 * kPW), 0, st, cnt, base, lr, T, nbatch, F1, ld,
+                     nb, nbp, qctr, nsub, out, getenv("FA_PAIR_DEBUG") ? atoi(getenv("FA_PAIR_DEBUG")) : 0);
   FA_LAUNCH_RET();
 }
 

@@ -52,12 +52,14 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
   return v;
 }
 
-// Orders this wave's LDS accesses (a wave's LDS ops execute in issue order;
-// this keeps the compiler from reordering them and waits for completion).
+// Orders this wave's LDS accesses across lanes.  The LDS executes one wave's DS
+// instructions in issue order, so a read issued after another lane's write sees
+// it: only the compiler must not reorder or cache them.  (A memory-model fence
+// would also emit s_waitcnt vmcnt(0), draining every prefetched global load of
+// a software-pipelined loop at each call: that cost the pair kernel ~7 ms.)
 __device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  __asm__ __volatile__("" ::: "memory");
 }
 
 // Row-start masks for U consecutive 64-position windows of a wave's CSR span.

@@ -89,6 +89,7 @@ _HIP_SIGS = {
     "fa_hip_block_counts": (C.c_int, [vp, vp, i64, i32, vp, vp, C.c_int, vp]),
     "fa_hip_block_scatter": (C.c_int, [vp, vp, i64, i32, vp, vp, vp, C.c_int, vp]),
     "fa_hip_pair_rows16": (C.c_int, [vp, vp, vp, i64, C.c_int, vp, vp]),
+    "fa_hip_pair_queue16": (C.c_int, [vp, vp, vp, i64, C.c_int, i64, vp, vp, C.c_int, vp]),
     "fa_hip_pair_blocked16": (C.c_int, [vp, vp, vp, i64, i32, vp, vp]),
     "fa_hip_pair_blocked": (C.c_int, [vp, vp, vp, i64, vp, i32, vp, i64, vp]),
     "fa_hip_pair_gram_mfma": (C.c_int, [vp, i32, i64, i64, vp, C.c_int, vp]),

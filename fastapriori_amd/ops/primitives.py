@@ -351,17 +351,37 @@ def pair_counts_horizontal(roff, ranks, wrow, F1: int, long_rows: bool = True) -
             pb = 128 if (wrow is not None or long_rows) else 256       # u16 tiles need unit weights
             nb = (F1 + pb - 1) // pb
             nbatch = (T + 63) // 64
-            cnt = torch.empty(nb * T, dtype=torch.uint8, device=dev)
+            # cnt / base are padded past their ends: the pair kernel's software
+            # pipeline loads up to 3 x 16 batches past a chunk unconditionally (those
+            # values are never processed; padded bases must be valid lr offsets)
+            pad_b = 3 * 16 + 2
+            cnt = torch.empty(nb * T + pad_b * 64, dtype=torch.uint8, device=dev)
+            cnt[nb * T:].zero_()
             bsum = torch.empty(nb * nbatch, dtype=_I64, device=dev)
             _hip_call("fa_hip_block_counts", _p(roff), _p(ranks), T, F1, _p(cnt), _p(bsum), pb, st)
-            base = torch.cumsum(bsum, 0)
-            total = int(base[-1].item())
-            base -= bsum
+            base = torch.zeros(nb * nbatch + pad_b, dtype=_I64, device=dev)
+            torch.cumsum(bsum, 0, out=base[:nb * nbatch])
+            total = int(base[nb * nbatch - 1].item())
+            base[:nb * nbatch] -= bsum
             lr = torch.empty(total + 1024, dtype=torch.uint8, device=dev)   # pad: aligned dword staging reads
             _hip_call("fa_hip_block_scatter", _p(roff), _p(ranks), T, F1, _p(cnt), _p(base), _p(lr), pb, st)
             if pb == 256:
-                k16 = "fa_hip_pair_blocked16" if os.environ.get("FA_PAIR_ROWS", "1") == "0" else "fa_hip_pair_rows16"
-                _hip_call(k16, _p(cnt), _p(base), _p(lr), T, F1, _p(out), st)
+                kern = os.environ.get("FA_PAIR_ROWS_KERNEL", "queue16")
+                if os.environ.get("FA_PAIR_DEBUG") == "4":
+                    pass        # profiling split (benchmarks/pair_probe.py): layout kernels only
+                elif kern == "queue16":
+                    # work-queue schedule: persistent workgroups keep their tile across
+                    # sub-chunks; even row stride -> two counters per 64-bit flush atomic
+                    ld = F1 + (F1 & 1)
+                    out = torch.zeros((F1, ld), dtype=_I32, device=dev)
+                    nbp = nb * (nb + 1) // 2
+                    qctr = torch.zeros(nbp, dtype=_I32, device=dev)
+                    _hip_call("fa_hip_pair_queue16", _p(cnt), _p(base), _p(lr), T, F1, ld, _p(qctr), _p(out),
+                              int(os.environ.get("FA_PAIR_WG", "0")), st)
+                    out = out[:, :F1]
+                else:
+                    k16 = "fa_hip_pair_blocked16" if kern == "blocked16" else "fa_hip_pair_rows16"
+                    _hip_call(k16, _p(cnt), _p(base), _p(lr), T, F1, _p(out), st)
             else:
                 _hip_call("fa_hip_pair_blocked", _p(cnt), _p(base), _p(lr), T, _p(wrow), F1, _p(out),
                           PAIR_CHUNK_ROWS, st)

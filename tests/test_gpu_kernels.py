@@ -293,11 +293,12 @@ def test_slab_multipass_from_bitmap(monkeypatch):
     assert ref.as_dict() == got_w.as_dict()
 
 
-@pytest.mark.parametrize("kernel,rows16", [("blocked", "1"), ("blocked", "0"), ("tile", "1")])
+@pytest.mark.parametrize("kernel,rows16", [("blocked", "rows16"), ("blocked", "blocked16"), ("blocked", "queue16"),
+                                           ("tile", "queue16")])
 @pytest.mark.parametrize("long_rows", [False, True])
 def test_pair_kernels_agree(monkeypatch, kernel, rows16, long_rows):
     monkeypatch.setenv("FA_PAIR_KERNEL", kernel)
-    monkeypatch.setenv("FA_PAIR_ROWS", rows16)
+    monkeypatch.setenv("FA_PAIR_ROWS_KERNEL", rows16)
     off, items, lut, F1 = _prep(n=20000, V=900, seed=21, long_rows=30, F1_frac=0.9)
     _, kept, roff = _compress_inputs(off, items, lut)
     ranks = ops.compress(off, items, lut, kept, roff)
@@ -308,6 +309,34 @@ def test_pair_kernels_agree(monkeypatch, kernel, rows16, long_rows):
     refw = ops.pair_counts_horizontal(roff, ranks, w, F1)
     gotw = ops.pair_counts_horizontal(roff.to(DEV), ranks.to(DEV), w.to(DEV), F1).cpu()
     assert torch.equal(refw, gotw)
+
+
+@pytest.mark.parametrize("F1,n_wg", [(600, 0), (601, 3), (257, 1)])
+def test_pair_queue_drain_and_stealing(monkeypatch, F1, n_wg):
+    """k_pair_queue16 over many sub-chunks: pair counts far above 2^16 (the u16 LDS
+    counters drain bit 15 into the global count), odd F1 (u32 flush path), and few
+    workgroups for many tiles (tile switches and stealing)."""
+    monkeypatch.setenv("FA_PAIR_ROWS_KERNEL", "queue16")
+    monkeypatch.setenv("FA_PAIR_WG", str(n_wg))
+    rng = np.random.default_rng(F1)
+    n = 150_000
+    lens = rng.integers(2, 9, n)
+    roff = np.zeros(n + 1, np.int64)
+    roff[1:] = np.cumsum(lens)
+    rows = []
+    for L in lens:
+        # ranks 0 and 1 in ~90 % of rows (counts ~135K: drained several times)
+        head = [r for r in (0, 1) if rng.random() < 0.9]
+        rest = rng.choice(np.arange(2, F1), size=max(int(L) - len(head), 0), replace=False)
+        rows.append(np.sort(np.concatenate([np.array(head, np.int64), rest]).astype(np.int32)))
+    lens = np.array([r.size for r in rows])
+    roff[1:] = np.cumsum(lens)
+    ranks = torch.from_numpy(np.concatenate(rows))
+    roff = torch.from_numpy(roff)
+    ref = ops.pair_counts_horizontal(roff, ranks, None, F1)
+    got = ops.pair_counts_horizontal(roff.to(DEV), ranks.to(DEV), None, F1, False).cpu()
+    assert int(ref[0, 1]) > 100_000
+    assert torch.equal(ref, got)
 
 
 @pytest.mark.parametrize("offset", [0, 1])
