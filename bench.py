@@ -15,7 +15,7 @@ written to a D.dat file: once with the file's pages dropped from the page cache
 JSON line's "e2e" record (``--e2e off`` skips them).
 
 ``vs_baseline`` = this run's itemsets/s over the multi-threaded C++ CPU path of
-the same miner on the same config (BASELINE.md:27; profiles/cpu_<config>.json,
+the same miner on the same config (BASELINE.md:27; benchmarks/cpu_baselines.json,
 measured by benchmarks/run_bench.py --mode cpu).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config T10I4D100M]
@@ -88,17 +88,16 @@ def _relaunch(args) -> int:
     return subprocess.call(cmd, env=env)
 
 
+BASELINES = os.path.join(ROOT, "benchmarks", "cpu_baselines.json")
+
+
 def cpu_baseline(config: str, min_sup: float, n_txn: int):
-    """itemsets/s of the C++ CPU path on the same config (profiles/cpu_<config>.json), or None."""
-    p = os.path.join(ROOT, "profiles", f"cpu_{config}.json")
-    if not os.path.exists(p):
+    """itemsets/s of the C++ CPU path on the same config (benchmarks/cpu_baselines.json,
+    written from benchmarks/run_bench.py --mode cpu runs), or None."""
+    if not os.path.exists(BASELINES):
         return None
-    rec = None
-    with open(p) as f:
-        for line in f:
-            line = line.strip()
-            if line.startswith("{"):
-                rec = json.loads(line)
+    with open(BASELINES) as f:
+        rec = json.load(f).get(config)
     if not rec or rec.get("n_txn") != n_txn or abs(rec.get("min_support", min_sup) - min_sup) > 1e-12:
         return None
     return rec
@@ -261,7 +260,7 @@ def main() -> int:
             "vs_baseline": round(value / base["itemsets_per_s"], 2) if base else None,
             "baseline": ({"what": "C++ CPU path of the same miner, same config (BASELINE.md:27)",
                           "itemsets_per_s": base["itemsets_per_s"], "ms": base["ms"],
-                          "threads": base.get("threads"), "source": f"profiles/cpu_{args.config}.json"}
+                          "threads": base.get("threads"), "source": "benchmarks/cpu_baselines.json"}
                          if base else None),
             "dtype": "int32/uint64-bitmap (exact integer counts)",
             "data": (f"synthetic {'Zipf-topic' if webdocs else 'Quest'} {args.config} "

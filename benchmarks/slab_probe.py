@@ -35,26 +35,33 @@ def main():
     shard = generate_shard(n, Comm(), "cuda", L, I, P, N, 1)
     calls = []
     real = ops.count_level
+    real_dfs = ops.primitives.count_bundle_dfs
 
     def rec(*args, **kw):
-        calls.append((args, kw))
+        calls.append((real, args, kw))
         return real(*args, **kw)
 
+    def rec_dfs(*args, **kw):
+        calls.append((real_dfs, args, kw))
+        return real_dfs(*args, **kw)
+
     apriori.ops.count_level = rec
+    ops.primitives.count_bundle_dfs = rec_dfs
     FastApriori(ms, config=MinerConfig(min_support=ms)).run(shard)
     apriori.ops.count_level = real
+    ops.primitives.count_bundle_dfs = real_dfs
     out = []
-    for i, (args, kw) in enumerate(calls):
+    for i, (fn, args, kw) in enumerate(calls):
         for sw in (a.sw.split(",") if a.sw else [""]):
             os.environ["FA_SLAB_SW"] = sw or "0"
-            row = {"call": i, "C": int(args[7].size), "force_sw": sw}
+            row = {"call": i, "fn": fn.__name__, "force_sw": sw}
             for mode in a.modes.split(","):
                 os.environ["FA_SLAB_DEBUG"] = mode
                 ts = []
                 for _ in range(a.reps):
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
-                    real(*args, **kw)
+                    fn(*args, **kw)
                     e1.record()
                     torch.cuda.synchronize()
                     ts.append(e0.elapsed_time(e1))

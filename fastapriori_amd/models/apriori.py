@@ -73,6 +73,9 @@ class _Deferred:
             self.value, self.done = self.fn(), True
         return self.value
 BUNDLE_DFS = os.environ.get("FA_BUNDLE_DFS", "1") == "1"
+# k = 2 across ranks: triangles of at least this many pairs are reduce-scattered and
+# thresholded per slice (Comm.reduce_scatter_select) instead of all-reduced
+PAIR_RS_MIN = int(os.environ.get("FA_PAIR_RS_MIN", str(1 << 15)))
 # depth-2 reuse pays where prefixes are long; on short prefixes (k = 3: two items) the
 # lanes' uneven child loops cost more than the saved reads (T10I4D100M: bundle 3-4
 # 17.7 -> 21.0 ms with it, bundle 5-12 16.2 -> 14.6 ms)
@@ -129,8 +132,11 @@ class FastApriori:
         n_global, self._V_max = int(g[:, 0].sum()), int(g[:, 1].max())
         mc = min_count(self.cfg.min_support, n_global)
         self.stats = {"n_lines": n_global, "min_count": mc}
-        tm = Timer(dev, sync=os.environ.get("FA_PHASE_TIMING") == "1")
+        # hipEvent phase timing (no synchronisation) whenever metrics are recorded
+        gpu_timing = os.environ.get("FA_GPU_TIMING") == "1" or bool(self.log.metrics_path)
+        tm = Timer(dev, sync=os.environ.get("FA_PHASE_TIMING") == "1", events=gpu_timing)
         self._timer = tm
+        self._level_recs = []     # per-level metric records, emitted by _finish with device times
 
         with roctx_range("F1"), tm.phase("f1"):
             items, counts1, lut = self._frequent_items(shard, mc)
@@ -155,6 +161,7 @@ class FastApriori:
 
         # ---- k = 2 -----------------------------------------------------
         t0 = time.perf_counter()
+        b0 = self._bytes_moved()
         if resume is not None and len(resume.levels) >= 2:
             levels.append(resume.levels[1]); counts.append(resume.counts[1])
         else:
@@ -166,13 +173,17 @@ class FastApriori:
         self.log.line(f"2 candidates items {F1 * (F1 - 1) // 2}")
         self.log.line(f"2 freq items {len(levels[1])}")
         self.log.line(f"Use Time 2 items {int((time.perf_counter() - t0) * 1000)}")
-        self.log.metric(phase="level", k=2, candidates=F1 * (F1 - 1) // 2, frequent=len(levels[1]),
-                        ms=(time.perf_counter() - t0) * 1e3, strategy=self.stats.get("pair_strategy"))
+        self._level_recs.append((dict(phase="level", k=2, candidates=F1 * (F1 - 1) // 2, frequent=len(levels[1]),
+                                      ms=(time.perf_counter() - t0) * 1e3, strategy=self.stats.get("pair_strategy"),
+                                      bytes_reduced=self._bytes_moved() - b0,
+                                      hbm_bytes_est=self.stats.get("pair_hbm_bytes_est", 0)),
+                                 "pairs"))
 
         # ---- k >= 3 ----------------------------------------------------
         k = 3
         while len(levels[-1]) >= k and (self.cfg.max_level == 0 or k <= self.cfg.max_level):
             t0 = time.perf_counter()
+            b0 = self._bytes_moved()
             if resume is not None and len(resume.levels) >= k:
                 levels.append(resume.levels[k - 1]); counts.append(resume.counts[k - 1])
                 k += 1
@@ -223,8 +234,13 @@ class FastApriori:
                     self.log.line(f"{kk} candidate items {int(apriori_gen(levels[kk - 2])[2].size)}")
                 self.log.line(f"{kk} freq items {len(Fk)}")
                 self.log.line(f"Use Time {kk} items {int(ms) if j == 0 else 0}")
-                self.log.metric(phase="level", k=kk, candidates=int(ex.size), frequent=len(Fk),
-                                ms=ms if j == 0 else 0.0, groups=int(pi.size), bundled_with=k)
+                plan = ops.primitives.LAST_LEVEL_PLAN
+                rec = dict(phase="level", k=kk, candidates=int(ex.size), frequent=len(Fk),
+                           ms=ms if j == 0 else 0.0, groups=int(pi.size), bundled_with=k,
+                           bytes_reduced=(self._bytes_moved() - b0) if j == 0 else 0,
+                           kernel=plan.get("kernel"),
+                           hbm_bytes_est=(self._level_hbm_bytes(db, plan) if j == 0 else 0))
+                self._level_recs.append((rec, f"level{k}" if j == 0 else None))
                 if self.ckpt is not None:
                     self.ckpt.save_level(result, kk)
             k += len(bundle)
@@ -245,6 +261,36 @@ class FastApriori:
         if wait and not isinstance(result.items, list):
             result.items = result.items.result()
 
+    def _bytes_moved(self) -> int:
+        b = self.comm.bytes_reduced
+        if getattr(self, "dcomm", self.comm) is not self.comm:
+            b += self.dcomm.bytes_reduced
+        return b
+
+    @staticmethod
+    def _level_hbm_bytes(db, plan: dict) -> int:
+        """HBM bytes a level's count kernel reads (estimate from its plan): every pass
+        rebuilds the slabs from the compressed rows (ranks + row offsets), or copies
+        the materialised bitmap of the used items."""
+        if not plan:
+            return 0
+        passes = int(plan.get("passes", 1) or 1)
+        rows = int(db["ranks"].numel()) * 4 + int(db["roff"].numel()) * 8
+        return passes * rows
+
+    def _emit_level_metrics(self) -> None:
+        tm = getattr(self, "_timer", None)
+        gpu = tm.finish() if (tm is not None and tm.events) else {}
+        if tm is not None and tm.events:
+            self.stats["gpu_phase_ms"] = {k: round(v, 3) for k, v in gpu.items()}
+        for rec, span in getattr(self, "_level_recs", []):
+            if span is not None and span in gpu:
+                rec["gpu_ms"] = round(gpu[span], 3)
+            self.log.metric(**rec)
+        self._level_recs = []
+        if os.environ.get("FA_TRACE") == "1" and tm is not None:
+            self.stats["trace"] = tm.trace(pid=self.comm.rank)
+
     def _finish(self, result: MiningResult, t_start: float) -> MiningResult:
         self._result_items(result)
         db = getattr(self, "_db_local", None)
@@ -258,6 +304,7 @@ class FastApriori:
         self.stats["mine_ms"] = (time.perf_counter() - t_start) * 1e3
         self.stats["n_itemsets"] = result.n_itemsets
         self.stats["bytes_reduced"] = self.comm.bytes_reduced
+        self._emit_level_metrics()
         if getattr(self, "_timer", None) is not None and self._timer.sync:
             self.stats["phase_ms"] = {k: round(v, 3) for k, v in self._timer.t.items()}
         return result
@@ -608,10 +655,23 @@ class FastApriori:
             _TRIU_CACHE[key] = (iu, iu[0] * F1 + iu[1])
         iu, fi = _TRIU_CACHE[key]
         flat = pc.reshape(-1)[fi]
-        self.comm.all_reduce_(flat, bound=self.stats["n_lines"])
-        keep = torch.nonzero(flat >= mc).flatten()
+        T, nnz = int(db["T"]), int(db["ranks"].numel())
+        if strat == "gram":
+            self.stats["pair_hbm_bytes_est"] = int(F1 * max(db["W"], 1) * 8 * ((F1 + 63) // 64))
+        else:
+            nb = (F1 + 255) // 256
+            self.stats["pair_hbm_bytes_est"] = int(2 * (4 * nnz + 8 * T) + nnz * (nb + 1) + T * nb * (nb + 1))
+        if self.comm.distributed and flat.numel() >= PAIR_RS_MIN:
+            # X12 as reduce-scatter + local threshold + all-gather of the survivors
+            # (F_2 << C_2): each rank thresholds its 1/world slice of the summed triangle
+            keep, vals = self.comm.reduce_scatter_select(flat, mc, bound=self.stats["n_lines"])
+        else:
+            self.comm.all_reduce_(flat, bound=self.stats["n_lines"])
+            keep = torch.nonzero(flat >= mc).flatten()
+            vals = flat[keep]
         # one readback: rows (a, b) and counts
-        h = torch.stack([iu[0][keep], iu[1][keep], flat[keep].to(torch.int64)]).cpu().numpy()
+        keep = keep.to(iu.device)
+        h = torch.stack([iu[0][keep], iu[1][keep], vals.to(device=iu.device, dtype=torch.int64)]).cpu().numpy()
         return np.ascontiguousarray(h[:2].T, dtype=np.int32), h[2].astype(np.int64)
 
     # ------------------------------------------------------------------

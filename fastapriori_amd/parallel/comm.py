@@ -5,7 +5,8 @@ identical candidate lists and only count vectors move (SURVEY §2.4 plan):
 
   X3/X8   line / transaction totals          -> all_reduce(int64[1])
   X4      F1 token histogram                  -> all_reduce(int64[V])
-  X12     pair supports                       -> all_reduce(int64[F1*(F1-1)/2])
+  X12     pair supports                       -> reduce_scatter + local threshold + all_gather of the
+                                                 survivors (big triangles), else all_reduce
   X15     level-k candidate supports          -> all_reduce(int64[C_k])
   X17     U.dat line offsets                  -> all_gather(int64[1])
   X24     recommendations                     -> gather to rank 0
@@ -74,6 +75,38 @@ class Comm:
         if x is not t:
             t.copy_(x)
         return t
+
+    def reduce_scatter_select(self, t: torch.Tensor, thr: int, bound: int | None = None):
+        """Entries of the cross-rank sum of ``t`` that are >= ``thr``: (indices, values),
+        identical on every rank and in index order.
+
+        reduce-scatter (each rank receives the sum of its 1/world slice) + a local
+        threshold + an all-gather of the survivors only.  An all-reduce moves
+        2(W-1)/W of the vector per rank; this moves (W-1)/W plus the survivors, which
+        for the k = 2 triangle are a few percent of it (the
+        FastApriori.scala:236-238 collect of F_2 without shipping C_2)."""
+        dev = self._comm_device()
+        narrow = bound is not None and t.dtype == torch.int64 and 0 <= bound < (1 << 31)
+        x = t.to(device=dev, dtype=torch.int32 if narrow else t.dtype).reshape(-1)
+        n, W = x.numel(), self.world_size
+        chunk = (n + W - 1) // W
+        if chunk * W != n:
+            x = torch.cat([x, torch.zeros(chunk * W - n, dtype=x.dtype, device=dev)])
+        part = torch.empty(chunk, dtype=x.dtype, device=dev)
+        dist.reduce_scatter_tensor(part, x)
+        self.bytes_reduced += chunk * (W - 1) * x.element_size()
+        loc = torch.nonzero(part >= thr).flatten()
+        mine = torch.stack([loc + self.rank * chunk, part[loc].to(torch.int64)]) if loc.numel() else \
+            torch.zeros((2, 0), dtype=torch.int64, device=dev)
+        sizes = self.all_gather_ints([int(mine.shape[1])])[:, 0]
+        mx = int(sizes.max())
+        buf = torch.zeros((2, max(mx, 1)), dtype=torch.int64, device=dev)
+        buf[:, :mine.shape[1]] = mine
+        out = torch.empty((W, 2, max(mx, 1)), dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(out, buf)
+        self.bytes_reduced += int(sizes.sum()) * 16
+        got = torch.cat([out[r, :, :int(sizes[r])] for r in range(W)], dim=1)
+        return got[0], got[1]
 
     def bucket_elems(self, elem_size: int) -> int:
         mb = float(os.environ.get("FA_BUCKET_MB", "64"))

@@ -10,6 +10,7 @@ RDD read makes it do.
 """
 from __future__ import annotations
 
+import json
 import os
 import time
 
@@ -78,6 +79,13 @@ def run_job(cfg: JobConfig, comm=None) -> dict:
             miner = FastApriori(cfg.min_support, comm, mcfg, log, ckpt)
             result = miner.run(shard, resume=resume)
             summary["miner"] = dict(miner.stats)
+            trace = summary["miner"].pop("trace", None)
+            if cfg.profile and trace is not None and comm.is_root:
+                # Chrome trace of the mining phases (host spans + hipEvent device spans)
+                tpath = os.path.join(cfg.temp or ".", "fastapriori_trace.json")
+                with open(tpath, "w") as f:
+                    json.dump({"traceEvents": trace, "displayTimeUnit": "ms"}, f)
+                summary["trace_path"] = tpath
             del shard
             if ckpt is not None:
                 ckpt.mark_complete(result)
@@ -134,6 +142,10 @@ def main(argv=None) -> int:
     if cfg.world_size > 1 and "WORLD_SIZE" not in os.environ:
         return _relaunch(cfg, argv)
     if cfg.profile:
+        # --profile: JSON-lines metrics (per-level device times, bytes reduced, HBM bytes
+        # estimates) and a Chrome trace of the phases, both under the temp path
         os.environ.setdefault("FA_METRICS", os.path.join(cfg.temp or ".", "fastapriori_metrics.jsonl"))
+        os.environ.setdefault("FA_TRACE", "1")
+        os.environ.setdefault("FA_GPU_TIMING", "1")
     run_job(cfg)
     return 0

@@ -85,6 +85,16 @@ def test_world8_matches_single_rank(quest_db, dedup, strategy):
     assert max(len(s) for s in ref["sets"]) >= 3
 
 
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_pair_reduce_scatter_select(quest_db, world):
+    # X12 as reduce-scatter + per-slice threshold + all-gather of the survivors
+    # (forced for every triangle size): bit-identical to the all-reduce path
+    ref = spawn_local(_mine_file, 1, quest_db, 0.02, "auto", "horizontal", timeout=TIMEOUT)[0]
+    outs = spawn_local(_mine_file, world, quest_db, 0.02, "auto", "horizontal", timeout=TIMEOUT,
+                       env={"FA_PAIR_RS_MIN": "0"})
+    _check(outs, ref)
+
+
 def test_world8_candidate_mode(quest_db):
     ref = spawn_local(_mine_file, 1, quest_db, 0.02, "auto", "auto", timeout=TIMEOUT)[0]
     outs = spawn_local(_mine_file, 8, quest_db, 0.02, "auto", "auto", "candidate", timeout=TIMEOUT)

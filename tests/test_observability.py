@@ -1,0 +1,64 @@
+"""Observability: ``--profile`` writes the JSON-lines metrics
+stream (per-level candidates / frequent / ms / bytes reduced / HBM-bytes estimate)
+and a Chrome trace of the mining phases; the "==== " lines of the reference
+(FastApriori.scala:103-127) are unchanged."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_profile_writes_metrics_and_trace(tmp_path):
+    from fastapriori_amd.utils.io import write_quest_file
+    d = str(tmp_path) + "/"
+    write_quest_file(d + "D.dat", 3000, 8.0, 3.0, 60, 50, seed=2)
+    write_quest_file(d + "U.dat", 200, 8.0, 3.0, 60, 50, seed=2, users=True)
+    tmp = tmp_path / "tmp"
+    tmp.mkdir()
+    env = {k: v for k, v in os.environ.items() if not k.startswith("FA_")}
+    env["PYTHONPATH"] = ROOT
+    r = subprocess.run([sys.executable, "-m", "fastapriori_amd", d, d + "out/", str(tmp), "--min-support", "0.02",
+                        "--device", "cpu", "--profile"], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "==== Total freq items sets" in r.stdout
+    recs = [json.loads(l) for l in open(tmp / "fastapriori_metrics.jsonl")]
+    levels = [x for x in recs if x.get("phase") == "level"]
+    assert [x["k"] for x in levels][:2] == [2, 3]
+    for x in levels:
+        for key in ("candidates", "frequent", "ms", "bytes_reduced", "hbm_bytes_est"):
+            assert key in x
+    assert any(x.get("phase") == "job" for x in recs)
+    trace = json.load(open(tmp / "fastapriori_trace.json"))
+    names = {e["name"] for e in trace["traceEvents"]}
+    assert {"f1", "compress", "pairs"} <= names
+
+
+def test_world_size_guard_refuses_mismatch(tmp_path):
+    from fastapriori_amd.utils.io import write_quest_file
+    d = str(tmp_path) + "/"
+    write_quest_file(d + "D.dat", 500, 8.0, 3.0, 60, 50, seed=2)
+    write_quest_file(d + "U.dat", 50, 8.0, 3.0, 60, 50, seed=2, users=True)
+    env = {k: v for k, v in os.environ.items() if not k.startswith("FA_")}
+    env.update(PYTHONPATH=ROOT, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "-m", "fastapriori_amd", d, d + "out/", "--device", "cpu",
+                        "--world-size", "2"], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode != 0 and "--world-size 2" in r.stderr
+
+
+def test_world_size_launches_ranks(tmp_path):
+    from fastapriori_amd.utils.io import write_quest_file
+    d = str(tmp_path) + "/"
+    write_quest_file(d + "D.dat", 2000, 8.0, 3.0, 60, 50, seed=2)
+    write_quest_file(d + "U.dat", 100, 8.0, 3.0, 60, 50, seed=2, users=True)
+    env = {k: v for k, v in os.environ.items() if not k.startswith("FA_") and k not in ("WORLD_SIZE", "RANK")}
+    env["PYTHONPATH"] = ROOT
+    r1 = subprocess.run([sys.executable, "-m", "fastapriori_amd", d, d + "o1/", "--device", "cpu",
+                         "--min-support", "0.02"], capture_output=True, text=True, env=env, timeout=300)
+    r2 = subprocess.run([sys.executable, "-m", "fastapriori_amd", d, d + "o2/", "--device", "cpu",
+                         "--min-support", "0.02", "--world-size", "3"], capture_output=True, text=True, env=env,
+                        timeout=300)
+    assert r1.returncode == 0 and r2.returncode == 0, r2.stderr[-3000:]
+    for part in ("freqItemset/part-00000", "recommends/part-00000"):
+        assert open(d + "o1/" + part).read() == open(d + "o2/" + part).read()
