@@ -30,29 +30,38 @@ import bench  # noqa: E402
 def _e2e(a, cfg):
     from fastapriori_amd.config import JobConfig
     from fastapriori_amd.pipeline import run_job
-    from fastapriori_amd.utils.io import write_quest_file
+    from fastapriori_amd.utils.io import write_quest_file, write_zipf_file
     n, L, I, P, N, ms = cfg
     n = a.n_txn or n
     ms = a.min_support or ms
-    d = os.path.join(a.workdir, f"{a.config}_{n}") + "/"
+    d = os.path.join(a.workdir, f"{a.config}_{n}_{a.tokens}") + "/"
     os.makedirs(d, exist_ok=True)
     t0 = time.time()
     if not os.path.exists(d + "D.dat"):
-        write_quest_file(d + "D.dat", n, L, I, P, N, seed=1)
-        write_quest_file(d + "U.dat", max(n // 100, 1000), L, I, P, N, seed=1, users=True)
+        if a.config.startswith("webdocs"):
+            # wide vocabulary: numeric ids or letter-string tokens (dictionary path)
+            write_zipf_file(d + "D.dat", n, mean_len=L, n_items=N, n_topics=P, seed=1,
+                            string_tokens=a.tokens == "str")
+            write_zipf_file(d + "U.dat", max(n // 100, 1000), mean_len=L / 4, n_items=N, n_topics=P, seed=2,
+                            string_tokens=a.tokens == "str")
+        else:
+            write_quest_file(d + "D.dat", n, L, I, P, N, seed=1)
+            write_quest_file(d + "U.dat", max(n // 100, 1000), L, I, P, N, seed=1, users=True)
     gen_s = time.time() - t0
     out = os.path.join(a.workdir, "out") + "/"
     runs = []
     for _ in range(a.warmup + a.steps):
         job = JobConfig(input=d, output=out, temp="", min_support=ms, device=a.device, overwrite=True,
                         checkpoint=False)
-        t = time.time()
+        t, c = time.time(), time.process_time()
         s = run_job(job)
         s["total_ms"] = round((time.time() - t) * 1000, 1)
+        s["host_cpu_s"] = time.process_time() - c      # host CPU time of this process (all threads)
         runs.append(s)
     best = min(runs[a.warmup:], key=lambda r: r["total_ms"])
     shutil.rmtree(out.rstrip("/") + "freqItemset", ignore_errors=True)
     return {"metric": f"end-to-end CLI job ms, {a.config} min_sup={ms}", "device": a.device, "n_txn": n,
+            "tokens": a.tokens, "host_cpu_s": round(best.get("host_cpu_s", 0.0), 2),
             "D_bytes": os.path.getsize(d + "D.dat"), "gen_s": round(gen_s, 1),
             **{k: best[k] for k in ("total_ms", "read_ms", "mine_ms", "write_ms", "recommend_ms", "n_itemsets",
                                    "n_rules") if k in best},
@@ -91,10 +100,12 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workdir", default=os.environ.get("TMPDIR", "/tmp") + "/fa_bench")
+    ap.add_argument("--tokens", choices=["num", "str"], default="num",
+                    help="webdocs e2e: numeric ids or letter-string tokens (dictionary path)")
     a = ap.parse_args()
     cfg = bench.CONFIGS[a.config]
-    if a.config.startswith("webdocs"):
-        raise SystemExit("webdocs configs are generated in-process only (bench.py)")
+    if a.config.startswith("webdocs") and a.mode == "cpu":
+        raise SystemExit("webdocs CPU baseline: not supported (bench.py generates it in-process)")
     line = _e2e(a, cfg) if a.mode == "e2e" else _cpu(a, cfg)
     print(json.dumps(line), flush=True)
 

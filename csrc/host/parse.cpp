@@ -21,6 +21,11 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <atomic>
 #include <unordered_map>
 
 #include "fa_common.h"
@@ -122,18 +127,136 @@ struct MappedFile {
   }
 };
 
+// Per-thread dictionary: open addressing on the 64-bit token hash (hash_bytes, the
+// identity the ranks agree on), verified by the bytes, so a 64-bit collision inside
+// a shard is reported (parse error 7) instead of merging two tokens.
 struct ThreadDict {
-  std::unordered_map<std::string_view, int32_t> map;
-  std::vector<std::string_view> strs;
+  struct Slot { uint64_t h; int32_t id; int32_t pad; };
+  std::vector<Slot> slot;               // id -1 = empty; the hash lives in the slot (one miss per probe)
+  std::vector<uint64_t> hash;           // per local id
+  std::vector<std::string_view> strs;   // per local id
+  bool collision = false;
+  ThreadDict() : slot(1 << 12, Slot{0, -1, 0}) {}
+  // Identity inside a thread is the 64-bit hash (as across ranks); equal hashes of
+  // different tokens are caught by merge_dicts' byte comparison across threads
+  // and by the length check here.
   int32_t get(std::string_view s) {
-    auto it = map.find(s);
-    if (it != map.end()) return it->second;
-    int32_t id = (int32_t)strs.size();
-    map.emplace(s, id);
+    const uint64_t h = hash_bytes(s.data(), s.size());
+    const size_t mask = slot.size() - 1;
+    size_t at = (size_t)h & mask;
+    for (;;) {
+      const Slot& e = slot[at];
+      if (e.id < 0) break;
+      if (e.h == h) {
+        if (strs[(size_t)e.id].size() != s.size()) collision = true;
+        return e.id;
+      }
+      at = (at + 1) & mask;
+    }
+    const int32_t id = (int32_t)strs.size();
+    slot[at] = Slot{h, id, 0};
+    hash.push_back(h);
     strs.push_back(s);
+    if (strs.size() * 2 > slot.size()) grow();
     return id;
   }
+  void grow() {
+    std::vector<Slot> ns(slot.size() * 2, Slot{0, -1, 0});
+    const size_t mask = ns.size() - 1;
+    for (size_t id = 0; id < strs.size(); ++id) {
+      size_t at = (size_t)hash[id] & mask;
+      while (ns[at].id >= 0) at = (at + 1) & mask;
+      ns[at] = Slot{hash[id], (int32_t)id, 0};
+    }
+    slot.swap(ns);
+  }
 };
+
+// Merge the thread dictionaries into one shard dictionary in parallel: entries are
+// partitioned by the top hash bits, each partition is sorted by hash and gets a
+// contiguous id range (ids in hash order: deterministic for any thread count).
+// remap[t][local id] = shard id.  Returns false on a 64-bit collision.
+static bool merge_dicts(std::vector<ThreadDict>& dicts, int nthreads, TxnDB* db,
+                        std::vector<std::vector<int32_t>>& remap) {
+  const int nt = (int)dicts.size();
+  constexpr int kBits = 8, kB = 1 << kBits;
+  struct Ent { uint64_t h; int32_t t, id; };
+  std::vector<std::vector<int64_t>> cnt(nt, std::vector<int64_t>(kB + 1, 0));
+  parallel_for_threads(std::max(1, std::min(nthreads, nt)), [&](int w) {
+    for (int t = w; t < nt; t += std::max(1, std::min(nthreads, nt)))
+      for (uint64_t h : dicts[t].hash) cnt[t][(h >> (64 - kBits)) + 1] += 1;
+  });
+  // bucket-major offsets: bucket b's entries of thread t start at off[b][t]
+  std::vector<int64_t> bstart(kB + 1, 0);
+  std::vector<std::vector<int64_t>> off(kB, std::vector<int64_t>(nt, 0));
+  int64_t o = 0;
+  for (int b = 0; b < kB; ++b) {
+    bstart[b] = o;
+    for (int t = 0; t < nt; ++t) { off[b][t] = o; o += cnt[t][b + 1]; }
+  }
+  bstart[kB] = o;
+  std::vector<Ent> ents((size_t)o);
+  parallel_for_threads(std::max(1, std::min(nthreads, nt)), [&](int w) {
+    for (int t = w; t < nt; t += std::max(1, std::min(nthreads, nt))) {
+      std::vector<int64_t> pos(kB);
+      for (int b = 0; b < kB; ++b) pos[b] = off[b][t];
+      const auto& H = dicts[t].hash;
+      for (size_t id = 0; id < H.size(); ++id) ents[(size_t)pos[H[id] >> (64 - kBits)]++] = {H[id], t, (int32_t)id};
+    }
+  });
+  // per bucket: sort by hash, distinct count
+  std::vector<int64_t> nd(kB + 1, 0);
+  std::atomic<bool> bad{false};
+  parallel_for_threads(std::max(1, nthreads), [&](int w) {
+    for (int b = w; b < kB; b += std::max(1, nthreads)) {
+      auto* a = ents.data() + bstart[b];
+      const int64_t n = bstart[b + 1] - bstart[b];
+      std::sort(a, a + n, [](const Ent& x, const Ent& y) { return x.h < y.h || (x.h == y.h && x.t < y.t); });
+      int64_t d = 0;
+      for (int64_t i = 0; i < n; ++i) {
+        if (i == 0 || a[i].h != a[i - 1].h) { ++d; continue; }
+        if (dicts[a[i].t].strs[(size_t)a[i].id] != dicts[a[i - 1].t].strs[(size_t)a[i - 1].id]) bad = true;
+      }
+      nd[b + 1] = d;
+    }
+  });
+  for (auto& td : dicts) if (td.collision) bad = true;
+  if (bad) return false;
+  for (int b = 0; b < kB; ++b) nd[b + 1] += nd[b];
+  const int64_t V = nd[kB];
+  remap.assign(nt, {});
+  for (int t = 0; t < nt; ++t) remap[t].assign(dicts[t].strs.size(), -1);
+  db->dict_off.assign((size_t)V + 1, 0);
+  db->dict_hash.assign((size_t)V, 0);
+  std::vector<std::string_view> first((size_t)V);
+  parallel_for_threads(std::max(1, nthreads), [&](int w) {
+    for (int b = w; b < kB; b += std::max(1, nthreads)) {
+      const auto* a = ents.data() + bstart[b];
+      const int64_t n = bstart[b + 1] - bstart[b];
+      int64_t g = nd[b] - 1;
+      for (int64_t i = 0; i < n; ++i) {
+        if (i == 0 || a[i].h != a[i - 1].h) {
+          ++g;
+          db->dict_hash[(size_t)g] = a[i].h;
+          first[(size_t)g] = dicts[a[i].t].strs[(size_t)a[i].id];
+        }
+        remap[a[i].t][(size_t)a[i].id] = (int32_t)g;
+      }
+    }
+  });
+  int64_t bytes = 0;
+  for (int64_t g = 0; g < V; ++g) { db->dict_off[(size_t)g] = bytes; bytes += (int64_t)first[(size_t)g].size(); }
+  db->dict_off[(size_t)V] = bytes;
+  db->dict_blob.resize((size_t)bytes);
+  parallel_for_threads(std::max(1, nthreads), [&](int w) {
+    const int nw = std::max(1, nthreads);
+    for (int64_t g = V * w / nw, e = V * (w + 1) / nw; g < e; ++g)
+      if (!first[(size_t)g].empty())
+        std::memcpy(&db->dict_blob[(size_t)db->dict_off[(size_t)g]], first[(size_t)g].data(), first[(size_t)g].size());
+  });
+  db->vocab = V;
+  return true;
+}
 
 // Numeric fast path for one line starting at p: a single pass in which digits
 // accumulate into the value and separators emit it; ids go straight into
@@ -199,6 +322,7 @@ static int parse_buffer(const char* d, int64_t size, int64_t b, int64_t e, int m
   std::vector<int32_t> tmax(nt, -1);
   std::atomic<bool> non_numeric{false};
 
+  const auto t_start = std::chrono::steady_clock::now();
   parallel_for_threads(nt, [&](int t) {
     int64_t lo = (t == 0) ? first : next_line_start(d, size, cuts[t]);
     int64_t hi = cuts[t + 1];
@@ -262,29 +386,20 @@ static int parse_buffer(const char* d, int64_t size, int64_t b, int64_t e, int m
     for (int32_t m : tmax) mx = std::max(mx, m);
     db->vocab = (int64_t)mx + 1;
   } else {
-    // merge thread dictionaries into one shard dictionary, remap ids
-    std::unordered_map<std::string_view, int32_t> global;
-    std::vector<std::string_view> gstrs;
-    for (int t = 0; t < nt; ++t) {
-      auto& td = dicts[t];
-      std::vector<int32_t> remap(td.strs.size());
-      for (size_t i = 0; i < td.strs.size(); ++i) {
-        auto it = global.find(td.strs[i]);
-        if (it == global.end()) {
-          int32_t id = (int32_t)gstrs.size();
-          global.emplace(td.strs[i], id);
-          gstrs.push_back(td.strs[i]);
-          remap[i] = id;
-        } else {
-          remap[i] = it->second;
-        }
+    // merge thread dictionaries into one shard dictionary, remap ids (parallel)
+    const auto t_tok = std::chrono::steady_clock::now();
+    std::vector<std::vector<int32_t>> remap;
+    if (!merge_dicts(dicts, nthreads, db, remap)) return 7;
+    if (getenv("FA_PARSE_TIMING"))
+      std::fprintf(stderr, "parse dict: tokenize %.1f ms, merge %.1f ms (%d threads)\n",
+                   std::chrono::duration<double, std::milli>(t_tok - t_start).count(),
+                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_tok).count(), nt);
+    parallel_for_threads(std::max(1, std::min(nthreads, nt)), [&](int w) {
+      for (int t = w; t < nt; t += std::max(1, std::min(nthreads, nt))) {
+        for (auto& v : db->chunks[t].items) v = remap[t][(size_t)v];
+        for (auto& v : extras[t]) v = remap[t][(size_t)v];
       }
-      for (auto& v : db->chunks[t].items) v = remap[v];
-      for (auto& v : extras[t]) v = remap[v];
-    }
-    db->dict.reserve(gstrs.size());
-    for (auto& s : gstrs) db->dict.emplace_back(s);
-    db->vocab = (int64_t)gstrs.size();
+    });
   }
   for (auto& ex : extras) db->extras.insert(db->extras.end(), ex.begin(), ex.end());
   return 0;
@@ -295,7 +410,8 @@ static int parse_buffer(const char* d, int64_t size, int64_t b, int64_t e, int m
 using namespace fa;
 
 // mode: 0 = auto (numeric if every token is canonical numeric, else dict), 1 = dict.
-// On failure returns nullptr and sets *err (1 = cannot open, 2 = mmap).
+// On failure returns nullptr and sets *err (1 = cannot open, 2 = mmap, 7 = 64-bit
+// token hash collision inside the shard).
 FA_API TxnDB* fa_parse_file(const char* path, int64_t byte_begin, int64_t byte_end, int mode,
                             int nthreads, int* err) {
   *err = 0;
@@ -308,7 +424,11 @@ FA_API TxnDB* fa_parse_file(const char* path, int64_t byte_begin, int64_t byte_e
     delete db;
     db = new TxnDB();
   }
-  parse_buffer(mf.data, mf.size, byte_begin, byte_end, 1, nthreads, db);
+  if (parse_buffer(mf.data, mf.size, byte_begin, byte_end, 1, nthreads, db) != 0) {
+    delete db;
+    *err = 7;          // two distinct tokens share a 64-bit hash
+    return nullptr;
+  }
   return db;
 }
 
@@ -319,7 +439,7 @@ FA_API TxnDB* fa_parse_buffer(const char* data, int64_t size, int mode, int nthr
     delete db;
     db = new TxnDB();
   }
-  parse_buffer(data, size, 0, size, 1, nthreads, db);
+  if (parse_buffer(data, size, 0, size, 1, nthreads, db) != 0) { delete db; return nullptr; }
   return db;
 }
 

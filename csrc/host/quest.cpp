@@ -233,14 +233,19 @@ struct ZipfTable {
 };
 }  // namespace fa
 
-FA_API TxnDB* fa_zipf_generate(int64_t txn_begin, int64_t txn_end, double mean_len, double sigma, int64_t n_items,
-                               double s, double q, int64_t n_topics, uint64_t seed, int nthreads) {
-  n_items = std::max<int64_t>(1, n_items);
-  ZipfTable words(n_items, s, q);
-  n_topics = std::max<int64_t>(1, n_topics);
-  ZipfTable topic_law(n_topics, 1.0, 0.0);
-  std::vector<std::vector<int64_t>> topics((size_t)n_topics);
-  {
+namespace fa {
+// The document model above, built once per call and shared by the threads.
+struct ZipfModel {
+  int64_t n_items, n_topics;
+  double mu, sigma;
+  uint64_t seed;
+  ZipfTable words, topic_law;
+  std::vector<std::vector<int64_t>> topics;
+  ZipfModel(double mean_len, double sigma_, int64_t n_items_, double s, double q, int64_t n_topics_, uint64_t seed_)
+      : n_items(std::max<int64_t>(1, n_items_)), n_topics(std::max<int64_t>(1, n_topics_)),
+        mu(std::log(std::max(1.0, mean_len)) - 0.5 * sigma_ * sigma_), sigma(sigma_), seed(seed_),
+        words(std::max<int64_t>(1, n_items_), s, q), topic_law(std::max<int64_t>(1, n_topics_), 1.0, 0.0),
+        topics((size_t)std::max<int64_t>(1, n_topics_)) {
     Rng r(mix64(seed ^ 0x70F1C5ull));
     const int64_t lo = std::min<int64_t>(100, n_items - 1), span = std::max<int64_t>(1, std::min<int64_t>(20000, n_items - lo));
     for (auto& t : topics) {
@@ -248,14 +253,52 @@ FA_API TxnDB* fa_zipf_generate(int64_t txn_begin, int64_t txn_end, double mean_l
       for (int64_t j = 0; j < c; ++j) t.push_back(lo + (int64_t)r.below((uint64_t)span));
     }
   }
+  // document i -> sorted distinct word ids (0-based) in row
+  void doc(int64_t i, std::vector<int64_t>& row, std::vector<int64_t>& table) const {
+    Rng r(mix64(seed * 0xD1B54A32D192ED03ull + (uint64_t)i));
+    const double g = std::sqrt(-2 * std::log(std::max(r.uniform(), 1e-300))) * std::cos(6.283185307179586 * r.uniform());
+    int64_t L = (int64_t)std::llround(std::exp(mu + sigma * g));
+    L = std::max<int64_t>(1, std::min<int64_t>({L, 20000, n_items}));
+    row.clear();
+    size_t cap = 64;
+    while (cap < (size_t)L * 2 + 64) cap <<= 1;
+    table.assign(cap, -1);
+    auto add = [&](int64_t it) {
+      size_t h = (size_t)mix64((uint64_t)it) & (cap - 1);
+      while (table[h] != -1) { if (table[h] == it) return; h = (h + 1) & (cap - 1); }
+      table[h] = it;
+      row.push_back(it);
+    };
+    for (int64_t w : topics[(size_t)topic_law.sample(r)])
+      if (r.uniform() < 0.8) add(w);
+    for (int64_t guard = 0; (int64_t)row.size() < L && guard < L * 8; ++guard) add(words.sample(r));
+    std::sort(row.begin(), row.end());
+  }
+};
+
+// String token of word id x for the string-vocabulary variant: "w" + base-26
+// letters of x + 1 (distinct for distinct ids, never a decimal number).
+inline int word_token(int64_t x, char* buf) {
+  char tmp[24];
+  int n = 0;
+  uint64_t v = (uint64_t)x + 1;
+  while (v) { tmp[n++] = (char)('a' + (v % 26)); v /= 26; }
+  buf[0] = 'w';
+  for (int j = 0; j < n; ++j) buf[1 + j] = tmp[n - 1 - j];
+  return n + 1;
+}
+}  // namespace fa
+
+FA_API TxnDB* fa_zipf_generate(int64_t txn_begin, int64_t txn_end, double mean_len, double sigma, int64_t n_items,
+                               double s, double q, int64_t n_topics, uint64_t seed, int nthreads) {
+  ZipfModel zm(mean_len, sigma, n_items, s, q, n_topics, seed);
   auto* db = new TxnDB();
   db->numeric = true;
-  db->vocab = n_items + 2;
+  db->vocab = zm.n_items + 2;
   const int64_t n = std::max<int64_t>(0, txn_end - txn_begin);
   int nt = std::max(1, nthreads);
   if (n < (int64_t)nt * 256) nt = 1;
   db->chunks.assign(nt, TxnChunk());
-  const double mu = std::log(std::max(1.0, mean_len)) - 0.5 * sigma * sigma;
   parallel_for_threads(nt, [&](int t) {
     const int64_t lo = txn_begin + n * t / nt, hi = txn_begin + n * (t + 1) / nt;
     // appended on this thread's stack, moved into the shared array at the end
@@ -263,30 +306,46 @@ FA_API TxnDB* fa_zipf_generate(int64_t txn_begin, int64_t txn_end, double mean_l
     struct Local { TxnChunk ch; TxnChunk& dst; ~Local() { dst = std::move(ch); } } L{TxnChunk(), db->chunks[t]};
     TxnChunk& ch = L.ch;
     ch.lens.reserve(hi - lo);
-    std::vector<int64_t> row;
-    std::vector<int64_t> table;
+    std::vector<int64_t> row, table;
     for (int64_t i = lo; i < hi; ++i) {
-      Rng r(mix64(seed * 0xD1B54A32D192ED03ull + (uint64_t)i));
-      const double g = std::sqrt(-2 * std::log(std::max(r.uniform(), 1e-300))) * std::cos(6.283185307179586 * r.uniform());
-      int64_t L = (int64_t)std::llround(std::exp(mu + sigma * g));
-      L = std::max<int64_t>(1, std::min<int64_t>({L, 20000, n_items}));
-      row.clear();
-      size_t cap = 64;
-      while (cap < (size_t)L * 2 + 64) cap <<= 1;
-      table.assign(cap, -1);
-      auto add = [&](int64_t it) {
-        size_t h = (size_t)mix64((uint64_t)it) & (cap - 1);
-        while (table[h] != -1) { if (table[h] == it) return; h = (h + 1) & (cap - 1); }
-        table[h] = it;
-        row.push_back(it);
-      };
-      for (int64_t w : topics[(size_t)topic_law.sample(r)])
-        if (r.uniform() < 0.8) add(w);
-      for (int64_t guard = 0; (int64_t)row.size() < L && guard < L * 8; ++guard) add(words.sample(r));
-      std::sort(row.begin(), row.end());
+      zm.doc(i, row, table);
       for (int64_t x : row) ch.items.push_back((int32_t)(x + 2));   // value x+1, numeric id value+1
       ch.lens.push_back((int64_t)ch.items.size());
     }
   });
   return db;
+}
+
+// The same documents written as a text file: numeric tokens (value x + 1, as the
+// in-memory generator) or, with string_tokens, word-like strings (word_token) so
+// the file exercises the dictionary (string-vocabulary) path of the parser/miner.
+FA_API int fa_zipf_write(const char* path, int64_t n_txn, double mean_len, double sigma, int64_t n_items, double s,
+                         double q, int64_t n_topics, uint64_t seed, int string_tokens, int nthreads) {
+  ZipfModel zm(mean_len, sigma, n_items, s, q, n_topics, seed);
+  FILE* f = std::fopen(path, "wb");
+  if (!f) return 1;
+  const int64_t block = 1 << 13;
+  int nt = std::max(1, nthreads);
+  std::vector<std::string> bufs(nt);
+  for (int64_t b0 = 0; b0 < n_txn; b0 += block * nt) {
+    parallel_for_threads(nt, [&](int t) {
+      std::string& out = bufs[t];
+      out.clear();
+      std::vector<int64_t> row, table;
+      char tok[32];
+      const int64_t lo = b0 + block * t, hi = std::min(n_txn, lo + block);
+      for (int64_t i = lo; i < hi; ++i) {
+        zm.doc(i, row, table);
+        for (size_t j = 0; j < row.size(); ++j) {
+          const int len = string_tokens ? word_token(row[j], tok)
+                                        : std::snprintf(tok, sizeof tok, "%lld", (long long)(row[j] + 1));
+          if (j) out.push_back(' ');
+          out.append(tok, (size_t)len);
+        }
+        out.push_back('\n');
+      }
+    });
+    for (auto& b : bufs) std::fwrite(b.data(), 1, b.size(), f);
+  }
+  return std::fclose(f) == 0 ? 0 : 2;
 }

@@ -8,7 +8,7 @@ using namespace fa;
 FA_API void fa_txndb_info(TxnDB* db, int64_t* info) {
   int64_t n = 0, nnz = 0, bytes = 0;
   for (auto& ch : db->chunks) { n += (int64_t)ch.lens.size(); nnz += (int64_t)ch.items.size(); }
-  for (auto& s : db->dict) bytes += (int64_t)s.size();
+  bytes = (int64_t)db->dict_blob.size();
   info[0] = n; info[1] = nnz; info[2] = (int64_t)db->extras.size();
   info[3] = db->numeric ? 1 : 0; info[4] = db->vocab; info[5] = bytes;
 }
@@ -39,16 +39,27 @@ FA_API void fa_txndb_export(TxnDB* db, int64_t* offsets, int32_t* items, int32_t
 }
 
 // Dictionary export: concatenated bytes + (n+1) offsets + 64-bit hash per entry.
-FA_API void fa_txndb_export_dict(TxnDB* db, char* buf, int64_t* str_off, uint64_t* hashes) {
-  int64_t o = 0;
-  for (size_t i = 0; i < db->dict.size(); ++i) {
-    const std::string& s = db->dict[i];
-    str_off[i] = o;
-    if (!s.empty()) std::memcpy(buf + o, s.data(), s.size());
-    hashes[i] = hash_bytes(s.data(), s.size());
-    o += (int64_t)s.size();
+FA_API void fa_txndb_export_dict(TxnDB* db, char* buf, int64_t* str_off, uint64_t* hashes, int nthreads) {
+  const int64_t n = db->vocab;
+  (void)nthreads;
+  if (!db->dict_blob.empty()) std::memcpy(buf, db->dict_blob.data(), db->dict_blob.size());
+  if (n > 0) {
+    std::memcpy(str_off, db->dict_off.data(), (size_t)(n + 1) * 8);
+    std::memcpy(hashes, db->dict_hash.data(), (size_t)n * 8);
+  } else {
+    str_off[0] = 0;
   }
-  str_off[db->dict.size()] = o;
+}
+
+// Hashes of n tokens given as one byte blob + (n+1) offsets (the same hash the
+// parser gives dictionary entries): maps token strings to shard ids without
+// Python loops over a vocabulary.
+FA_API void fa_hash_tokens(const char* blob, const int64_t* off, int64_t n, uint64_t* out, int nthreads) {
+  const int nt = std::max(1, std::min<int>(nthreads, (int)std::max<int64_t>(1, n / 4096)));
+  parallel_for_threads(nt, [&](int t) {
+    for (int64_t i = n * t / nt, e = n * (t + 1) / nt; i < e; ++i)
+      out[i] = hash_bytes(blob + off[i], (size_t)(off[i + 1] - off[i]));
+  });
 }
 
 FA_API void fa_txndb_free(TxnDB* db) { delete db; }

@@ -16,7 +16,11 @@ struct TxnDB {
   std::vector<int32_t> extras;     // one id per repeated occurrence inside a line
   bool numeric = true;
   int64_t vocab = 0;               // id space size
-  std::vector<std::string> dict;   // dict mode: id -> token bytes
+  // dict mode: id -> token bytes, as one blob + (vocab + 1) offsets, and the
+  // 64-bit hash of every entry (hash_bytes)
+  std::string dict_blob;
+  std::vector<int64_t> dict_off;
+  std::vector<uint64_t> dict_hash;
 };
 
 int64_t next_line_start(const char* d, int64_t size, int64_t pos);

@@ -304,6 +304,10 @@ class FastApriori:
         self.stats["mine_ms"] = (time.perf_counter() - t_start) * 1e3
         self.stats["n_itemsets"] = result.n_itemsets
         self.stats["bytes_reduced"] = self.comm.bytes_reduced
+        if ops.primitives.FALLBACKS:
+            self.stats["fallbacks"] = list(ops.primitives.FALLBACKS)
+            for f in ops.primitives.FALLBACKS:
+                self.log.metric(phase="fallback", what=f)
         self._emit_level_metrics()
         if getattr(self, "_timer", None) is not None and self._timer.sync:
             self.stats["phase_ms"] = {k: round(v, 3) for k, v in self._timer.t.items()}
@@ -352,45 +356,57 @@ class FastApriori:
                 lut[torch.from_numpy(fid[order].astype(np.int64)).to(dev)] = torch.arange(
                     len(order), dtype=torch.int32, device=dev)
             return items, counts1, lut
-        # dictionary mode: agree on identity through 64-bit token hashes
+        # dictionary mode: agree on identity through 64-bit token hashes.  Everything
+        # over the vocabulary is vectorised (a webdocs-scale shard has ~5M distinct
+        # strings); only the frequent items' strings are ever decoded.
         Vl = vocab.size
-        hist = ops.histogram(shard.items, max(Vl, 1)).cpu().numpy()[:Vl]
+        hist = ops.histogram(shard.items, max(Vl, 1)).cpu().numpy()[:Vl].astype(np.int64)
         if shard.extras.size:
             hist = hist + np.bincount(shard.extras, minlength=Vl)[:Vl]
         hashes = vocab.hashes.astype(np.uint64)
-        if np.unique(hashes).size != Vl:
+        h_order = np.argsort(hashes, kind="stable")
+        h_sorted = hashes[h_order]
+        if Vl > 1 and bool((h_sorted[1:] == h_sorted[:-1]).any()):
             raise RuntimeError("64-bit token hash collision inside one shard")
         if comm.distributed:
-            owner = (hashes % np.uint64(comm.world_size)).astype(np.int64)
-            send_h = [hashes[owner == r].view(np.int64) for r in range(comm.world_size)]
-            send_c = [hist[owner == r].astype(np.int64) for r in range(comm.world_size)]
+            # hash-partitioned counting (the reference's HashPartitioner shuffle,
+            # FastApriori.scala:55-58): owner = hash mod world
+            W = comm.world_size
+            owner = (hashes % np.uint64(W)).astype(np.int64)
+            by_owner = np.argsort(owner, kind="stable")
+            bounds = np.searchsorted(owner[by_owner], np.arange(W + 1))
+            send_h = [hashes[by_owner[bounds[r]:bounds[r + 1]]].view(np.int64) for r in range(W)]
+            send_c = [hist[by_owner[bounds[r]:bounds[r + 1]]] for r in range(W)]
             rh = np.concatenate(comm.all_to_all_varlen(send_h))
             rc = np.concatenate(comm.all_to_all_varlen(send_c))
             uh, inv = np.unique(rh, return_inverse=True)
             tot = np.bincount(inv, weights=rc, minlength=uh.size).astype(np.int64)
-            mine = uh[tot >= thr], tot[tot >= thr]
-            gathered = comm.all_gather_object((mine[0].tolist(), mine[1].tolist()))
-            freq = {}
-            for hs, cs in gathered:
-                freq.update(zip(hs, cs))
-            local_idx = {int(h): i for i, h in enumerate(hashes.view(np.int64).tolist())}
-            strs = {h: vocab.strings[local_idx[h]] for h in freq if h in local_idx}
+            ok = tot >= thr
+            parts = comm.all_gather_varlen_np(np.stack([uh[ok], tot[ok]]).ravel())
+            fh = np.concatenate([q.reshape(2, -1)[0] for q in parts]).view(np.uint64)
+            fc = np.concatenate([q.reshape(2, -1)[1] for q in parts])
+            # strings of the frequent tokens this shard has; every rank contributes its own
+            pos = np.minimum(np.searchsorted(h_sorted, fh), max(Vl - 1, 0))
+            have = (h_sorted[pos] == fh) if Vl else np.zeros(fh.size, bool)
+            mine = vocab.decode(h_order[pos[have]]) if have.any() else []
             allstrs = {}
-            for d in comm.all_gather_object(strs):
-                allstrs.update(d)
-            entries = [(h, c, allstrs[h]) for h, c in freq.items()]
+            for hs, ss in comm.all_gather_object((fh[have].view(np.int64).tolist(), mine)):
+                allstrs.update(zip(hs, ss))
+            fstr = [allstrs[h] for h in fh.view(np.int64).tolist()]
         else:
             sel = np.nonzero(hist >= thr)[0]
-            entries = [(int(hashes.view(np.int64)[i]), int(hist[i]), vocab.strings[i]) for i in sel]
-        entries.sort(key=lambda e: (-e[1], java_string_key(e[2])))
-        items = [e[2] for e in entries]
-        counts1 = np.array([e[1] for e in entries], dtype=np.int64)
-        rank_of_hash = {e[0]: r for r, e in enumerate(entries)}
+            fh, fc = hashes[sel], hist[sel]
+            fstr = vocab.decode(sel)
+        order = sorted(range(len(fstr)), key=lambda e: (-int(fc[e]), java_string_key(fstr[e])))
+        items = [fstr[e] for e in order]
+        counts1 = np.asarray(fc, dtype=np.int64)[order] if order else np.zeros(0, np.int64)
+        rank_h = np.asarray(fh, dtype=np.uint64)[order] if order else np.zeros(0, np.uint64)
         lut_np = np.full(max(Vl, 1), -1, dtype=np.int32)
-        for i, h in enumerate(hashes.view(np.int64).tolist()):
-            r = rank_of_hash.get(h)
-            if r is not None:
-                lut_np[i] = r
+        if rank_h.size and Vl:
+            ro = np.argsort(rank_h)
+            pos = np.minimum(np.searchsorted(rank_h[ro], hashes), rank_h.size - 1)
+            hit = rank_h[ro][pos] == hashes
+            lut_np[:Vl][hit] = ro[pos[hit]].astype(np.int32)
         return items, counts1, torch.from_numpy(lut_np).to(dev)
 
     def _f1_heavy_hitters(self, shard: TransactionShard, V: int, thr: int):
@@ -687,6 +703,9 @@ class FastApriori:
         if (dev.type == "cuda" and GEN_DEVICE and n >= GEN_DEVICE_MIN_ROWS and prev.shape[1] >= 2
                 and self._F1 <= ops.primitives.AG_DEVICE_MAX_F1):
             return ops.apriori_gen_device(prev, self._F1, dev, want_rows)
+        if dev.type == "cuda" and self._F1 > ops.primitives.AG_DEVICE_MAX_F1:
+            ops.primitives.note_fallback(f"apriori-gen on the host: F1 = {self._F1} frequent items exceed the "
+                                         f"device generator's {ops.primitives.AG_DEVICE_MAX_F1}-rank bitsets")
         pi, eo, ex = apriori_gen(prev)
         if not want_rows:
             return pi, eo, ex
@@ -700,7 +719,7 @@ class FastApriori:
         (fa_hip_ag_chain, first_free): the candidate count of each level is the only
         readback.  None when the device chain does not apply (then _gen + _plan_bundle)."""
         dev = self._dev
-        if not (dev.type == "cuda" and GEN_DEVICE and GEN_CHAIN and BUNDLE_LEVELS and not self.cand_par
+        if not (dev.type == "cuda" and GEN_DEVICE and GEN_CHAIN and BUNDLE_LEVELS
                 and self.cfg.level_kernel in ("auto", "slab") and k - 1 <= BUNDLE_MAX_PREFIX
                 and prev.shape[0] >= GEN_DEVICE_MIN_ROWS and prev.shape[1] >= 2
                 and self._F1 <= ops.primitives.AG_DEVICE_MAX_F1):
@@ -737,7 +756,7 @@ class FastApriori:
             cand_rows = np.concatenate([prev[prefix_idx[g_of_e]], ext[:, None]], axis=1)
         # candidate rows of every bundled level (result assembly: rows[count >= minCount])
         self._bundle_rows = [np.ascontiguousarray(cand_rows, np.int32)]
-        if (not BUNDLE_LEVELS or self.cand_par or self.cfg.level_kernel not in ("auto", "slab")
+        if (not BUNDLE_LEVELS or self.cfg.level_kernel not in ("auto", "slab")
                 or k - 1 > BUNDLE_MAX_PREFIX):
             return bundle
         C = int(ext.size)
@@ -778,10 +797,42 @@ class FastApriori:
             cand = nxt
         return bundle
 
+    def _cand_rows_view(self, db) -> dict:
+        """Candidate mode: this rank's 1/W slice of the replicated rows.
+
+        Bundled levels (one launch over many levels' candidates) are split by rows
+        like the k = 2 pairs, not by candidate groups: every rank holds the whole
+        DB, so any split is local, and the row split keeps the bundle/DFS kernels'
+        one-launch plans intact.  The all-reduce over the rank group sums the slices.
+        Unweighted rows: a row range (absolute offsets into the shared ranks);
+        weighted (dedup) layout: a range of 64-column words."""
+        key = (id(db["roff"]), db["T"], db["ncols"], id(db["src"]))
+        if getattr(self, "_cand_view_key", None) == key:
+            return self._cand_view
+        r, nr = self.comm.rank, self.comm.world_size
+        v = dict(db)
+        v.update(bm=None, W=0)
+        if db["src"] is None:
+            T = db["T"]
+            a, b = T * r // nr, T * (r + 1) // nr
+            v.update(roff=db["roff"][a:b + 1], T=b - a, ncols=b - a)
+        else:
+            W = (db["ncols"] + 63) // 64
+            w0, w1 = W * r // nr, W * (r + 1) // nr
+            v.update(src=db["src"][64 * w0:64 * w1].contiguous(), ncols=64 * (w1 - w0),
+                     wword=db["wword"][w0:w1].contiguous())
+        self._cand_view_key, self._cand_view = key, v
+        return v
+
     def _count_bundle(self, db, bundle: list) -> list:
-        """Counts of every level of a bundle (one launch on the GPU)."""
+        """Counts of every level of a bundle (one launch on the GPU).  The all-reduce is
+        over the rank group in both modes: row shards (count mode) or this rank's row
+        slice of the replicated DB (candidate mode, _cand_rows_view)."""
         if len(bundle) == 1 or db["ranks"].device.type != "cuda":
             return [self._count_level(db, pv, pi, eo, ex) for _, pv, pi, eo, ex in bundle]
+        full_db = db
+        if self.cand_par:
+            db = self._cand_rows_view(db)
         sizes = [int(ex.size) for *_, ex in bundle]
         if BUNDLE_DFS and db["wword"] is None and bundle[0][1].shape[1] >= BUNDLE_DFS_MIN_M:
             # depth-2 prefix reuse: level k+1 candidates read one slab row under their
@@ -789,7 +840,7 @@ class FastApriori:
             cnt = ops.primitives.count_bundle_dfs(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"],
                                                   [(pv, pi, eo, ex) for _, pv, pi, eo, ex in bundle])
             if cnt is not None:
-                self.dcomm.all_reduce_(cnt, bound=self.stats["n_lines"])
+                self.comm.all_reduce_(cnt, bound=self.stats["n_lines"])
                 return np.split(cnt.cpu().numpy(), np.cumsum(sizes)[:-1])
         pre = [pv[pi] for _, pv, pi, _, _ in bundle]
         poff = np.concatenate([[0], np.cumsum(np.concatenate([np.full(p.shape[0], p.shape[1]) for p in pre]))])
@@ -800,8 +851,8 @@ class FastApriori:
         cnt = ops.count_level(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"], flat, eoff, ext,
                               db["wword"], kernel="slab", poff=poff, full_bm=lambda: self._bitmaps(db))
         if cnt is None:
-            return [self._count_level(db, pv, pi, eo, ex) for _, pv, pi, eo, ex in bundle]
-        self.dcomm.all_reduce_(cnt, bound=self.stats["n_lines"])
+            return [self._count_level(full_db, pv, pi, eo, ex) for _, pv, pi, eo, ex in bundle]
+        self.comm.all_reduce_(cnt, bound=self.stats["n_lines"])
         c = cnt.cpu().numpy()
         return np.split(c, np.cumsum(sizes)[:-1])
 

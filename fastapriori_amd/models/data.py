@@ -7,24 +7,54 @@ import numpy as np
 import torch
 
 
-@dataclass
 class Vocabulary:
     """Token id space of one shard.
 
     numeric: id = int(token) + 1 for canonical decimal tokens, id 0 = the empty
              token "" (blank line).  Identical on every rank by construction.
-    dict:    shard-local ids with their strings and 64-bit hashes; ranks agree
-             on identity through the hashes (parallel/vocab_exchange in the miner).
+    dict:    shard-local ids with their 64-bit hashes; ranks agree on identity
+             through the hashes (FastApriori._frequent_items).  The strings stay
+             one UTF-8 byte blob + offsets (a 5M-entry vocabulary is never turned
+             into Python objects); ``decode(ids)`` materialises only the ones asked for.
     """
-    numeric: bool
-    size: int
-    strings: list[str] | None = None
-    hashes: np.ndarray | None = None
+
+    def __init__(self, numeric: bool, size: int, strings: list[str] | None = None,
+                 hashes: np.ndarray | None = None, blob: np.ndarray | None = None,
+                 offsets: np.ndarray | None = None):
+        self.numeric = bool(numeric)
+        self.size = int(size)
+        self.hashes = hashes
+        self.blob, self.offsets = blob, offsets
+        self._strings = strings
+        if strings is not None and blob is None and not numeric:
+            enc = [t.encode("utf-8") for t in strings]
+            self.offsets = np.zeros(len(enc) + 1, dtype=np.int64)
+            if enc:
+                self.offsets[1:] = np.cumsum([len(e) for e in enc])
+            self.blob = np.frombuffer(b"".join(enc) or b"\0", dtype=np.uint8)
+
+    @property
+    def strings(self) -> list[str] | None:
+        """Every string of the vocabulary (decoded on first use; avoid for wide ones)."""
+        if self._strings is None and self.blob is not None:
+            self._strings = self.decode(np.arange(self.size))
+        return self._strings
+
+    def decode(self, ids) -> list[str]:
+        ids = np.asarray(ids, dtype=np.int64).ravel()
+        if self._strings is not None:
+            return [self._strings[i] for i in ids.tolist()]
+        raw = self.blob.tobytes() if ids.size > 64 else None
+        out = []
+        for i in ids.tolist():
+            a, b = int(self.offsets[i]), int(self.offsets[i + 1])
+            out.append((raw[a:b] if raw is not None else self.blob[a:b].tobytes()).decode("utf-8", "replace"))
+        return out
 
     def token(self, i: int) -> str:
         if self.numeric:
             return "" if i == 0 else str(i - 1)
-        return self.strings[i]
+        return self.decode([i])[0]
 
     @staticmethod
     def numeric_id(token: str) -> int:
@@ -35,6 +65,20 @@ class Vocabulary:
             return -1
         v = int(token)
         return v + 1 if v <= 2147483646 else -1
+
+
+def hash_tokens(tokens: list[str]) -> np.ndarray:
+    """64-bit hashes of token strings, identical to the parser's dictionary hashes."""
+    from ..ops import _native
+    from ..utils.env import num_threads
+    enc = [t.encode("utf-8") for t in tokens]
+    off = np.zeros(len(enc) + 1, dtype=np.int64)
+    if enc:
+        off[1:] = np.cumsum([len(e) for e in enc])
+    blob = np.frombuffer(b"".join(enc) or b"\0", dtype=np.uint8).copy()
+    out = np.zeros(max(len(enc), 1), dtype=np.uint64)
+    _native.host().fa_hash_tokens(blob.ctypes.data, off.ctypes.data, len(enc), out.ctypes.data, num_threads())
+    return out[:len(enc)]
 
 
 @dataclass

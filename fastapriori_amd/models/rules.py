@@ -33,7 +33,7 @@ from ..ops.host import RuleTable, rules_build
 from ..parallel.comm import Comm
 from ..utils.jvm import rule_tiebreak_key
 from ..utils.metrics import Logger
-from .data import MiningResult, TransactionShard, Vocabulary
+from .data import MiningResult, TransactionShard, Vocabulary, hash_tokens
 
 
 class AssociationRules:
@@ -82,30 +82,43 @@ class AssociationRules:
                 i = Vocabulary.numeric_id(t)
                 if 0 <= i < vocab.size:
                     lut[i] = r
-        else:
-            rank = {t: r for r, t in enumerate(self.result.items)}
-            for i, s in enumerate(vocab.strings):
-                r = rank.get(s)
-                if r is not None:
-                    lut[i] = r
+        elif vocab.size and self.result.items:
+            # through the parser's 64-bit token hashes: no loop over the users' vocabulary
+            rh = hash_tokens(self.result.items)
+            ro = np.argsort(rh)
+            vh = vocab.hashes.astype(np.uint64)
+            pos = np.minimum(np.searchsorted(rh[ro], vh), rh.size - 1)
+            hit = rh[ro][pos] == vh
+            lut[:vocab.size][hit] = ro[pos[hit]].astype(np.int32)
         return lut
 
     def recommend_shard(self, users: TransactionShard) -> torch.Tensor:
-        """Recommended rank per local U.dat line (-1 = "0"), on the users' device."""
+        """Recommended rank per local U.dat line (-1 = "0"), on the users' device.
+
+        Identical baskets are recommended once (removeRedundancy's reduceByKey of the
+        rank sets, AssociationRules.scala:51-58): baskets are canonicalised (ranks
+        sorted), grouped by a 128-bit row hash, every group is verified equal to its
+        representative element by element, and the representatives' results fan out
+        to all lines of their group.  Cost O(distinct baskets) instead of O(lines) in
+        the first-match scan."""
         rt = self.rules()
         dev = users.items.device
         lut = torch.from_numpy(self._rank_lut(users.vocab)).to(dev)
         n = users.n_lines
         if n == 0:
             return torch.zeros(0, dtype=torch.int32, device=dev)
+        F1 = len(self.result.items)
         r = lut[users.items.to(torch.int64)] if users.items.numel() else users.items
         keep = r >= 0
         lens = users.offsets[1:] - users.offsets[:-1]
         row = torch.repeat_interleave(torch.arange(n, device=dev), lens)
-        bcnt = torch.bincount(row[keep], minlength=n)
+        rk, rr = row[keep], r[keep].to(torch.int64)
+        # canonical basket = its ranks ascending (the basket is a set)
+        key, _ = torch.sort(rk * max(F1, 1) + rr)
+        bask = (key % max(F1, 1)).to(torch.int32).contiguous()
+        bcnt = torch.bincount(rk, minlength=n)
         boff = torch.zeros(n + 1, dtype=torch.int64, device=dev)
         torch.cumsum(bcnt, 0, out=boff[1:])
-        bask = r[keep].to(torch.int32).contiguous()
         if self._rules_dev is None or self._rules_dev[0] != dev:
             self._rules_dev = (dev, torch.from_numpy(rt.ante_off).to(dev), torch.from_numpy(rt.ante).to(dev),
                                torch.from_numpy(rt.cons).to(dev))
@@ -113,9 +126,55 @@ class AssociationRules:
         index = None
         if dev.type == "cuda" and cons.numel() >= ops.primitives.RECOMMEND_INDEX_MIN_RULES and self.use_index:
             if len(self._rules_dev) == 4:
-                self._rules_dev = self._rules_dev + (ops.primitives.recommend_index(a_off, ante, len(self.result.items)),)
+                self._rules_dev = self._rules_dev + (ops.primitives.recommend_index(a_off, ante, F1),)
             index = self._rules_dev[4]
-        return ops.recommend(a_off, ante, cons, len(self.result.items), boff, bask, index=index)
+        groups = self._basket_groups(boff, bask, bcnt) if (self.dedup_baskets and n > 1) else None
+        if groups is None:
+            self.stats["distinct_baskets"] = n
+            return ops.recommend(a_off, ante, cons, F1, boff, bask, index=index)
+        rep, inv = groups
+        self.stats["distinct_baskets"] = int(rep.numel())
+        rcnt = bcnt[rep]
+        roff = torch.zeros(rep.numel() + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(rcnt, 0, out=roff[1:])
+        # gather the representatives' baskets into their own CSR
+        pos = torch.repeat_interleave(boff[rep] - roff[:-1], rcnt) + torch.arange(int(roff[-1]), device=dev)
+        rbask = bask[pos].contiguous()
+        rec = ops.recommend(a_off, ante, cons, F1, roff, rbask, index=index)
+        return rec[inv]
+
+    dedup_baskets = True
+
+    @property
+    def stats(self) -> dict:
+        if not hasattr(self, "_stats"):
+            self._stats = {}
+        return self._stats
+
+    @staticmethod
+    def _basket_groups(boff: torch.Tensor, bask: torch.Tensor, bcnt: torch.Tensor):
+        """(representative basket per group, group of every basket), or None when
+        dedup does not pay (few repeats) or a hash group fails the exact check."""
+        n = bcnt.numel()
+        h1, h2 = ops.row_hash(boff, bask)
+        # empty baskets hash alike: give them a key of their own (length is part of it)
+        key = torch.stack([h1, h2 ^ bcnt.to(torch.int64)], dim=1)
+        uk, inv = torch.unique(key, dim=0, return_inverse=True)
+        G = uk.shape[0]
+        if G > 0.9 * n:
+            return None
+        first = torch.full((G,), n, dtype=torch.int64, device=bask.device)
+        first.scatter_reduce_(0, inv, torch.arange(n, device=bask.device), reduce="amin")
+        # exact check: every basket equals its group's representative
+        rep_of = first[inv]
+        if not torch.equal(bcnt, bcnt[rep_of]):
+            return None
+        if bask.numel():
+            row = torch.repeat_interleave(torch.arange(n, device=bask.device), bcnt)
+            j = torch.arange(bask.numel(), device=bask.device) - boff[row]
+            if not torch.equal(bask, bask[boff[rep_of][row] + j]):
+                return None
+        return first, inv
 
     def run(self, users: TransactionShard) -> list[str] | None:
         """Recommendations for every U.dat line, in file order, on rank 0 (None elsewhere)."""

@@ -29,11 +29,13 @@ _HOST_SIGS = {
     "fa_next_line_start": (i64, [cp, i64, i64]),
     "fa_txndb_info": (None, [vp, vp]),
     "fa_txndb_export": (None, [vp, vp, vp, vp, C.c_int]),
-    "fa_txndb_export_dict": (None, [vp, vp, vp, vp]),
+    "fa_txndb_export_dict": (None, [vp, vp, vp, vp, C.c_int]),
+    "fa_hash_tokens": (None, [vp, vp, i64, vp, C.c_int]),
     "fa_txndb_free": (None, [vp]),
     "fa_hash_bytes": (u64, [cp, i64]),
     "fa_quest_generate": (vp, [i64, i64, dbl, dbl, i64, i64, u64, C.c_int, C.c_int]),
     "fa_zipf_generate": (vp, [i64, i64, dbl, dbl, i64, dbl, dbl, i64, u64, C.c_int]),
+    "fa_zipf_write": (C.c_int, [cp, i64, dbl, dbl, i64, dbl, dbl, i64, u64, C.c_int, C.c_int]),
     "fa_quest_write": (C.c_int, [cp, i64, dbl, dbl, i64, i64, u64, C.c_int, C.c_int]),
     "fa_apriori_gen": (vp, [vp, i64, C.c_int, C.c_int, vp]),
     "fa_cands_export": (None, [vp, vp, vp, vp]),

@@ -939,6 +939,17 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
 
 AG_DEVICE_MAX_F1 = 4096   # bitset words per lane-wave: 64 x 64 bits
 
+# Device -> host fallbacks taken in this process (each reported once on stderr and
+# recorded here; the miner copies new ones into its metrics stream).
+FALLBACKS: list = []
+
+
+def note_fallback(what: str) -> None:
+    if what not in FALLBACKS:
+        FALLBACKS.append(what)
+        import sys
+        print(f"fastapriori_amd: {what}", file=sys.stderr, flush=True)
+
 
 _GEN_WS: dict = {}
 
@@ -1079,6 +1090,8 @@ def recommend(ante_off, ante, cons, F1: int, boff, bask, index=None) -> torch.Te
             rc = _native.hip().fa_hip_recommend(_p(ante_off), _p(ante), _p(cons), R, F1, _p(boff), _p(bask), M,
                                                 _p(out), _stream(bask))
         if rc == 2:  # vocabulary too wide for an LDS bitset: host path
+            note_fallback(f"recommendation on the host: F1 = {F1} frequent items exceed the kernel's LDS basket "
+                          "bitset (64 KiB)")
             return recommend(ante_off.cpu(), ante.cpu(), cons.cpu(), F1, boff.cpu(), bask.cpu()).to(dev)
         _native.check(rc, "fa_hip_recommend")
         return out

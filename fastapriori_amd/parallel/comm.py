@@ -146,6 +146,23 @@ class Comm:
         dist.all_gather_into_tensor(out, t)
         return out.cpu().numpy().reshape(self.world_size, -1)
 
+    def all_gather_varlen_np(self, a: np.ndarray) -> list[np.ndarray]:
+        """All-gather 1-D int64 arrays of different lengths (sizes, then one padded
+        all_gather_into_tensor): rank order, on every rank."""
+        a = np.ascontiguousarray(a, dtype=np.int64).ravel()
+        if not self.distributed:
+            return [a]
+        sizes = self.all_gather_ints([a.size])[:, 0]
+        mx = max(int(sizes.max()), 1)
+        dev = self._comm_device()
+        buf = torch.zeros(mx, dtype=torch.int64, device=dev)
+        if a.size:
+            buf[:a.size] = torch.from_numpy(a).to(dev)
+        out = torch.empty(self.world_size * mx, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(out, buf)
+        o = out.cpu().numpy().reshape(self.world_size, mx)
+        return [o[r, :int(sizes[r])] for r in range(self.world_size)]
+
     def all_gather_object(self, obj) -> list:
         if not self.distributed:
             return [obj]

@@ -39,14 +39,13 @@ def txndb_to_shard(h, device: torch.device, line_base: int = 0) -> TransactionSh
     items = _pinned(nnz, torch.int32, pin)
     extras = np.zeros(max(nx, 1), dtype=np.int32)
     lib.fa_txndb_export(h, off.data_ptr(), items.data_ptr(), extras.ctypes.data, num_threads())
-    strings = hashes = None
+    buf = soff = hashes = None
     if not numeric:
+        # the dictionary stays a byte blob + offsets (Vocabulary.decode on demand)
         buf = np.zeros(max(dbytes, 1), dtype=np.uint8)
         soff = np.zeros(vocab + 1, dtype=np.int64)
         hashes = np.zeros(max(vocab, 1), dtype=np.uint64)
-        lib.fa_txndb_export_dict(h, buf.ctypes.data, soff.ctypes.data, hashes.ctypes.data)
-        raw = buf.tobytes()
-        strings = [raw[soff[i]:soff[i + 1]].decode("utf-8", "replace") for i in range(vocab)]
+        lib.fa_txndb_export_dict(h, buf.ctypes.data, soff.ctypes.data, hashes.ctypes.data, num_threads())
         hashes = hashes[:vocab]
     lib.fa_txndb_free(h)
     off = off[: n + 1]
@@ -54,7 +53,7 @@ def txndb_to_shard(h, device: torch.device, line_base: int = 0) -> TransactionSh
         off.zero_()
     items = items[:nnz]
     shard = TransactionShard(off.to(device, non_blocking=True), items.to(device, non_blocking=True),
-                             extras[:nx], Vocabulary(bool(numeric), vocab, strings, hashes), line_base)
+                             extras[:nx], Vocabulary(bool(numeric), vocab, None, hashes, buf, soff), line_base)
     return shard
 
 
@@ -63,6 +62,8 @@ def parse_file(path: str, byte_begin: int = 0, byte_end: int = -1, mode: int = 0
     err = C.c_int(0)
     h = _native.host().fa_parse_file(path.encode(), byte_begin, byte_end, mode, num_threads(), C.byref(err))
     if not h:
+        if err.value == 7:
+            raise RuntimeError(f"{path}: two distinct tokens share a 64-bit hash (dictionary mode)")
         raise FileNotFoundError(f"cannot read {path} (error {err.value})")
     return txndb_to_shard(h, torch.device(device), line_base)
 
@@ -173,6 +174,8 @@ def parse_file_device(path: str, byte_begin: int, byte_end: int, device, line_ba
 
 def parse_bytes(data: bytes, mode: int = 0, device="cpu") -> TransactionShard:
     h = _native.host().fa_parse_buffer(data, len(data), mode, num_threads())
+    if not h:
+        raise RuntimeError("two distinct tokens share a 64-bit hash (dictionary mode)")
     return txndb_to_shard(h, torch.device(device))
 
 
@@ -218,6 +221,18 @@ def generate_zipf_shard(n_txn: int, comm, device=None, mean_len: float = 177.0, 
     e = n_txn * (comm.rank + 1) // comm.world_size
     h = _native.host().fa_zipf_generate(b, e, mean_len, sigma, n_items, s, q, n_topics, seed, num_threads())
     return txndb_to_shard(h, device, b)
+
+
+def write_zipf_file(path: str, n_txn: int, mean_len: float = 177.0, sigma: float = 0.5, n_items: int = 5_267_656,
+                    s: float = 1.05, q: float = 50.0, n_topics: int = 2000, seed: int = 1,
+                    string_tokens: bool = False) -> None:
+    """Wide-vocabulary documents (generate_zipf_shard's model) as a text file; with
+    ``string_tokens`` every word is a letter string ("w" + base-26), so the file
+    takes the dictionary path of the parser and the miner."""
+    rc = _native.host().fa_zipf_write(path.encode(), n_txn, mean_len, sigma, n_items, s, q, n_topics, seed,
+                                      1 if string_tokens else 0, num_threads())
+    if rc:
+        raise OSError(f"failed to write {path}")
 
 
 def write_quest_file(path: str, n_txn: int, avg_len=10.0, avg_pat=4.0, n_patterns=2000, n_items=1000,

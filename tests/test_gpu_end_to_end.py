@@ -50,15 +50,18 @@ def test_cli_under_torchrun_rccl_matches_oracle(tmp_path):
     assert open(tmp_path / "o_recommends/part-00000").read().splitlines() == recs
 
 
-def _gpu_rank(n, ms):
+def _gpu_rank(n, ms, par="count", dedup="auto"):
     from fastapriori_amd.models.apriori import FastApriori, MinerConfig
-    from fastapriori_amd.parallel.comm import init_comm, shutdown_comm
+    from fastapriori_amd.parallel.comm import Comm, init_comm, shutdown_comm
     from fastapriori_amd.utils.io import generate_shard
     from fastapriori_amd.utils.metrics import Logger
     comm = init_comm("cuda")
     try:
-        sh = generate_shard(n, comm, comm.device, 10.0, 4.0, 200, 200, seed=3)
-        res = FastApriori(ms, comm, MinerConfig(trim_min_rows=0, min_support=ms), Logger(comm.rank, enabled=False)).run(sh)
+        # candidate mode: every rank holds the whole DB
+        sh = generate_shard(n, comm if par == "count" else Comm(device=comm.device), comm.device, 10.0, 4.0,
+                            200, 200, seed=3)
+        cfg = MinerConfig(trim_min_rows=0, min_support=ms, parallelism=par, dedup=dedup)
+        res = FastApriori(ms, comm, cfg, Logger(comm.rank, enabled=False)).run(sh)
         return res.as_dict()
     finally:
         shutdown_comm(comm)
@@ -71,6 +74,15 @@ def test_two_ranks_share_gpu_match_one():
     outs = spawn_local(_gpu_rank, 2, 40000, 0.005, env={"FA_DIST_BACKEND": "gloo", "FA_PAIR_RS_MIN": "0"})
     assert outs[0] == ref and outs[1] == ref
     assert len(ref) > 100
+
+
+@pytest.mark.parametrize("dedup", ["off", "on"])
+def test_two_ranks_share_gpu_candidate_mode(dedup):
+    # candidate distribution with level bundles counted on each rank's row slice of the
+    # replicated DB (FastApriori._cand_rows_view: row ranges, or word ranges when dedup)
+    ref = spawn_local(_gpu_rank, 1, 40000, 0.005, "count", dedup, env={"FA_DIST_BACKEND": "gloo"})[0]
+    outs = spawn_local(_gpu_rank, 2, 40000, 0.005, "candidate", dedup, env={"FA_DIST_BACKEND": "gloo"})
+    assert outs[0] == ref and outs[1] == ref
 
 
 def _rccl_rank(n, ms, strategy):

@@ -73,3 +73,26 @@ def test_rule_confidence_is_ieee_double():
         s = frozenset(ante) | {cons}
         d = res.as_dict()
         assert conf == d[s] / d[frozenset(ante)]
+
+
+def test_duplicate_baskets_recommended_once():
+    # removeRedundancy (AssociationRules.scala:51-58): identical baskets, in any token
+    # order and with repeats, are one distinct basket; results fan out to every line
+    rng = np.random.default_rng(5)
+    drows = [" ".join(map(str, rng.choice(12, size=rng.integers(1, 6), replace=False))) for _ in range(400)]
+    res = FastApriori(0.05, config=MinerConfig(min_support=0.05),
+                      logger=Logger(enabled=False)).run(parse_bytes(("\n".join(drows) + "\n").encode()))
+    pool = [[1, 2], [3], [2, 4, 5], [], [7, 1], [11, 10, 3]]
+    urows = []
+    for _ in range(300):
+        b = list(pool[rng.integers(len(pool))])
+        rng.shuffle(b)
+        urows.append(" ".join(map(str, b + b[:1])))      # shuffled, with a repeated token
+    users = parse_bytes(("\n".join(urows) + "\n").encode())
+    on = AssociationRules(res, logger=Logger(enabled=False))
+    got = on.run(users)
+    off = AssociationRules(res, logger=Logger(enabled=False))
+    off.dedup_baskets = False
+    assert got == off.run(users)
+    assert on.stats["distinct_baskets"] <= len(pool) < off.stats["distinct_baskets"] == 300
+    assert got == recommend(_oracle_from(res), [java_split_ws(r) for r in urows])
