@@ -1,4 +1,4 @@
-// Device-side parsing of a transaction file's bytes (numeric vocabularies).
+// Device-side parsing of a transaction file's bytes (numeric and dictionary vocabularies).
 //
 // Same input semantics as the host parser (csrc/host/parse.cpp, Utils.scala:19-27):
 //   * lines end at '\n', at '\r\n' or at a lone '\r' (Hadoop LineRecordReader);
@@ -180,9 +180,129 @@ __global__ __launch_bounds__(256) void k_compact_lines(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Dictionary (string) vocabularies on the device.  Same tokenisation; every token
+// gets the host parser's 64-bit identity hash (csrc/host/fa_common.h hash_bytes:
+// FNV-1a over the bytes, then the splitmix64 finaliser of h ^ length) and is
+// inserted into a global open-addressing table keyed by that hash (0 = empty; a
+// hash of 0 is stored as 1).  A token's id here is its table slot; k_slot_ids
+// turns occupied slots into dense ids (slot order, i.e. hash order) afterwards.
+// The slot's (byte offset, length) of one occurrence lets the host decode the
+// strings it needs (frequent items) without a dictionary of every token.
+// flags[0] |= 2 when a probe sequence exceeds kMaxProbe (table too full: the
+// caller falls back to the host parser).
+// ---------------------------------------------------------------------------
+constexpr int kMaxProbe = 256;
+
+__device__ __forceinline__ uint64_t dmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ int32_t dict_insert(unsigned long long* __restrict__ keys, int64_t* __restrict__ tpos,
+                                               int32_t* __restrict__ tlen, uint32_t mask, uint64_t h, int64_t pos,
+                                               int32_t len) {
+  if (h == 0) h = 1;
+  uint32_t at = (uint32_t)(h >> 20) & mask;
+  for (int p = 0; p < kMaxProbe; ++p) {
+    const unsigned long long k = keys[at];
+    if (k == h) return (int32_t)at;
+    if (k == 0) {
+      const unsigned long long old = atomicCAS(&keys[at], 0ull, (unsigned long long)h);
+      if (old == 0) {
+        tpos[at] = pos;
+        tlen[at] = len;
+        return (int32_t)at;
+      }
+      if (old == h) return (int32_t)at;
+    }
+    at = (at + 1) & mask;
+  }
+  return -1;
+}
+
+__global__ __launch_bounds__(kPT) void k_parse_lines_dict(
+    const uint8_t* __restrict__ buf, const int64_t* __restrict__ ends, int64_t nl,
+    const int64_t* __restrict__ bound_off, int32_t* __restrict__ scratch, int32_t* __restrict__ xscratch,
+    int32_t* __restrict__ dcnt, int32_t* __restrict__ xcnt, int32_t* __restrict__ flags,
+    unsigned long long* __restrict__ keys, int64_t* __restrict__ tpos, int32_t* __restrict__ tlen, uint32_t mask) {
+  __shared__ int32_t seen[kSeen * kPT];
+  const int tid = threadIdx.x;
+  const int64_t j = (int64_t)blockIdx.x * kPT + tid;
+  bool full = false;
+  if (j < nl) {
+    int64_t s = j ? ends[j - 1] + 1 : 0;
+    int64_t e = ends[j];
+    while (s < e && buf[s] <= 0x20) ++s;
+    while (e > s && buf[e - 1] <= 0x20) --e;
+    const int64_t bo = bound_off[j];
+    int D = 0, X = 0;
+    auto add = [&](int64_t ts, int64_t te, uint64_t h) {
+      const int32_t id = dict_insert(keys, tpos, tlen, mask, dmix64(h ^ (uint64_t)(te - ts)), ts, (int32_t)(te - ts));
+      if (id < 0) { full = true; return; }
+      bool dup = false;
+      const int lim = D < kSeen ? D : kSeen;
+      for (int q = 0; q < lim && !dup; ++q) dup = seen[q * kPT + tid] == id;
+      for (int q = kSeen; q < D && !dup; ++q) dup = scratch[bo + q] == id;
+      if (dup) {
+        xscratch[bo + X++] = id;
+      } else {
+        if (D < kSeen) seen[D * kPT + tid] = id;
+        scratch[bo + D++] = id;
+      }
+    };
+    if (s == e) {
+      add(s, s, 0xCBF29CE484222325ull);     // blank line: the single token ""
+    } else {
+      int64_t ts = -1;
+      uint64_t h = 0;
+      for (int64_t i = s; i <= e && !full; ++i) {
+        const uint32_t c = i < e ? buf[i] : (uint32_t)' ';
+        if (c == ' ' || c == '\t' || c == 0x0B || c == '\f') {
+          if (ts >= 0) { add(ts, i, h); ts = -1; }
+          continue;
+        }
+        if (ts < 0) { ts = i; h = 0xCBF29CE484222325ull; }
+        h = (h ^ c) * 0x100000001B3ull;
+      }
+    }
+    dcnt[j] = D;
+    xcnt[j] = X;
+  }
+  if (__ballot(full) != 0ull && lane_id() == 0) atomicOr(&flags[0], 2);
+}
+
+// dense id of every occupied slot (exclusive scan of occupancy done by the caller)
+__global__ __launch_bounds__(256) void k_slot_remap(int32_t* __restrict__ ids, int64_t n,
+                                                    const int32_t* __restrict__ slot_id) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    ids[i] = slot_id[ids[i]];
+}
+
 }  // namespace fa
 
 using namespace fa;
+
+FA_API int fa_hip_parse_lines_dict(const uint8_t* buf, const int64_t* ends, int64_t nl, const int64_t* bound_off,
+                                   int32_t* scratch, int32_t* xscratch, int32_t* dcnt, int32_t* xcnt,
+                                   int32_t* flags, void* keys, int64_t* tpos, int32_t* tlen, int64_t cap,
+                                   hipStream_t st) {
+  if (nl <= 0) return 0;
+  if (cap <= 0 || (cap & (cap - 1)) || cap > ((int64_t)1 << 31)) return 1;
+  hipLaunchKernelGGL(k_parse_lines_dict, dim3((unsigned)((nl + kPT - 1) / kPT)), dim3(kPT), 0, st, buf, ends, nl,
+                     bound_off, scratch, xscratch, dcnt, xcnt, flags, (unsigned long long*)keys, tpos, tlen,
+                     (uint32_t)(cap - 1));
+  FA_LAUNCH_RET();
+}
+
+FA_API int fa_hip_slot_remap(int32_t* ids, int64_t n, const int32_t* slot_id, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_slot_remap, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 65536)), dim3(256), 0, st, ids,
+                     n, slot_id);
+  FA_LAUNCH_RET();
+}
 
 FA_API int64_t fa_hip_parse_tiles(int64_t n) { return (n + kLTile - 1) / kLTile; }
 

@@ -357,57 +357,62 @@ class FastApriori:
                     len(order), dtype=torch.int32, device=dev)
             return items, counts1, lut
         # dictionary mode: agree on identity through 64-bit token hashes.  Everything
-        # over the vocabulary is vectorised (a webdocs-scale shard has ~5M distinct
-        # strings); only the frequent items' strings are ever decoded.
+        # over the vocabulary runs as tensor ops on the shard's device (a webdocs-scale
+        # shard has ~5M distinct strings); only the frequent items' strings are ever
+        # decoded.  Both parsers give every distinct token of a shard a distinct hash
+        # (a 64-bit collision is a parse error), so hashes identify ids.
         Vl = vocab.size
-        hist = ops.histogram(shard.items, max(Vl, 1)).cpu().numpy()[:Vl].astype(np.int64)
+        hist = ops.histogram(shard.items, max(Vl, 1))[:Vl].to(torch.int64)
         if shard.extras.size:
-            hist = hist + np.bincount(shard.extras, minlength=Vl)[:Vl]
-        hashes = vocab.hashes.astype(np.uint64)
-        h_order = np.argsort(hashes, kind="stable")
-        h_sorted = hashes[h_order]
-        if Vl > 1 and bool((h_sorted[1:] == h_sorted[:-1]).any()):
-            raise RuntimeError("64-bit token hash collision inside one shard")
+            hist += torch.bincount(torch.from_numpy(shard.extras.astype(np.int64)), minlength=Vl)[:Vl].to(dev)
+        hashes_t = torch.from_numpy(vocab.hashes.astype(np.uint64).view(np.int64)).to(dev)
         if comm.distributed:
             # hash-partitioned counting (the reference's HashPartitioner shuffle,
-            # FastApriori.scala:55-58): owner = hash mod world
+            # FastApriori.scala:55-58): owner = (hash >> 1) mod world
             W = comm.world_size
-            owner = (hashes % np.uint64(W)).astype(np.int64)
-            by_owner = np.argsort(owner, kind="stable")
-            bounds = np.searchsorted(owner[by_owner], np.arange(W + 1))
-            send_h = [hashes[by_owner[bounds[r]:bounds[r + 1]]].view(np.int64) for r in range(W)]
-            send_c = [hist[by_owner[bounds[r]:bounds[r + 1]]] for r in range(W)]
+            owner = torch.remainder(torch.bitwise_right_shift(hashes_t, 1) & ((1 << 62) - 1), W)
+            by_owner = torch.argsort(owner, stable=True)
+            bounds = torch.searchsorted(owner[by_owner], torch.arange(W + 1, device=dev)).cpu().numpy()
+            sh_np = hashes_t[by_owner].cpu().numpy()
+            sc_np = hist[by_owner].cpu().numpy()
+            send_h = [sh_np[bounds[r]:bounds[r + 1]] for r in range(W)]
+            send_c = [sc_np[bounds[r]:bounds[r + 1]] for r in range(W)]
             rh = np.concatenate(comm.all_to_all_varlen(send_h))
             rc = np.concatenate(comm.all_to_all_varlen(send_c))
             uh, inv = np.unique(rh, return_inverse=True)
             tot = np.bincount(inv, weights=rc, minlength=uh.size).astype(np.int64)
             ok = tot >= thr
             parts = comm.all_gather_varlen_np(np.stack([uh[ok], tot[ok]]).ravel())
-            fh = np.concatenate([q.reshape(2, -1)[0] for q in parts]).view(np.uint64)
+            fh = np.concatenate([q.reshape(2, -1)[0] for q in parts])
             fc = np.concatenate([q.reshape(2, -1)[1] for q in parts])
             # strings of the frequent tokens this shard has; every rank contributes its own
-            pos = np.minimum(np.searchsorted(h_sorted, fh), max(Vl - 1, 0))
-            have = (h_sorted[pos] == fh) if Vl else np.zeros(fh.size, bool)
-            mine = vocab.decode(h_order[pos[have]]) if have.any() else []
+            hs_sorted, hs_order = torch.sort(hashes_t)
+            fh_t = torch.from_numpy(fh).to(dev)
+            pos = torch.clamp(torch.searchsorted(hs_sorted, fh_t), max=max(Vl - 1, 0))
+            have = (hs_sorted[pos] == fh_t) if Vl else torch.zeros(fh_t.numel(), dtype=torch.bool, device=dev)
+            loc = hs_order[pos[have]].cpu().numpy()
+            have = have.cpu().numpy()
+            mine = vocab.decode(loc) if loc.size else []
             allstrs = {}
-            for hs, ss in comm.all_gather_object((fh[have].view(np.int64).tolist(), mine)):
+            for hs, ss in comm.all_gather_object((fh[have].tolist(), mine)):
                 allstrs.update(zip(hs, ss))
-            fstr = [allstrs[h] for h in fh.view(np.int64).tolist()]
+            fstr = [allstrs[h] for h in fh.tolist()]
         else:
-            sel = np.nonzero(hist >= thr)[0]
-            fh, fc = hashes[sel], hist[sel]
-            fstr = vocab.decode(sel)
+            sel = torch.nonzero(hist >= thr).flatten()
+            got = torch.stack([sel, hashes_t[sel], hist[sel]]).cpu().numpy()
+            sel_np, fh, fc = got[0], got[1], got[2]
+            fstr = vocab.decode(sel_np)
         order = sorted(range(len(fstr)), key=lambda e: (-int(fc[e]), java_string_key(fstr[e])))
         items = [fstr[e] for e in order]
         counts1 = np.asarray(fc, dtype=np.int64)[order] if order else np.zeros(0, np.int64)
-        rank_h = np.asarray(fh, dtype=np.uint64)[order] if order else np.zeros(0, np.uint64)
-        lut_np = np.full(max(Vl, 1), -1, dtype=np.int32)
-        if rank_h.size and Vl:
-            ro = np.argsort(rank_h)
-            pos = np.minimum(np.searchsorted(rank_h[ro], hashes), rank_h.size - 1)
-            hit = rank_h[ro][pos] == hashes
-            lut_np[:Vl][hit] = ro[pos[hit]].astype(np.int32)
-        return items, counts1, torch.from_numpy(lut_np).to(dev)
+        lut = torch.full((max(Vl, 1),), -1, dtype=torch.int32, device=dev)
+        if order and Vl:
+            rank_h = torch.from_numpy(np.asarray(fh, dtype=np.int64)[order]).to(dev)
+            rs, ro = torch.sort(rank_h)
+            pos = torch.clamp(torch.searchsorted(rs, hashes_t), max=rank_h.numel() - 1)
+            hit = rs[pos] == hashes_t
+            lut[:Vl][hit] = ro[pos[hit]].to(torch.int32)
+        return items, counts1, lut
 
     def _f1_heavy_hitters(self, shard: TransactionShard, V: int, thr: int):
         """Numeric-mode F1 for wide vocabularies without a V-bin histogram.

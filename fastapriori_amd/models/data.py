@@ -20,11 +20,14 @@ class Vocabulary:
 
     def __init__(self, numeric: bool, size: int, strings: list[str] | None = None,
                  hashes: np.ndarray | None = None, blob: np.ndarray | None = None,
-                 offsets: np.ndarray | None = None):
+                 offsets: np.ndarray | None = None, file_src: tuple | None = None):
         self.numeric = bool(numeric)
         self.size = int(size)
         self.hashes = hashes
         self.blob, self.offsets = blob, offsets
+        # device-parsed shards: (path, byte offset of the parsed range, first-occurrence
+        # offsets int64 [V], lengths int32 [V]) -- strings are read back from the file
+        self.file_src = file_src
         self._strings = strings
         if strings is not None and blob is None and not numeric:
             enc = [t.encode("utf-8") for t in strings]
@@ -36,7 +39,7 @@ class Vocabulary:
     @property
     def strings(self) -> list[str] | None:
         """Every string of the vocabulary (decoded on first use; avoid for wide ones)."""
-        if self._strings is None and self.blob is not None:
+        if self._strings is None and (self.blob is not None or self.file_src is not None):
             self._strings = self.decode(np.arange(self.size))
         return self._strings
 
@@ -44,6 +47,15 @@ class Vocabulary:
         ids = np.asarray(ids, dtype=np.int64).ravel()
         if self._strings is not None:
             return [self._strings[i] for i in ids.tolist()]
+        if self.file_src is not None:
+            import os
+            path, base, pos, lens = self.file_src
+            fd = os.open(path, os.O_RDONLY)
+            try:
+                return [os.pread(fd, int(lens[i]), base + int(pos[i])).decode("utf-8", "replace")
+                        for i in ids.tolist()]
+            finally:
+                os.close(fd)
         raw = self.blob.tobytes() if ids.size > 64 else None
         out = []
         for i in ids.tolist():

@@ -103,6 +103,8 @@ _HIP_SIGS = {
     "fa_hip_line_count": (C.c_int, [vp, i64, vp, vp]),
     "fa_hip_line_ends": (C.c_int, [vp, i64, vp, vp, vp]),
     "fa_hip_parse_lines": (C.c_int, [vp, vp, i64, vp, vp, vp, vp, vp, vp, vp]),
+    "fa_hip_parse_lines_dict": (C.c_int, [vp, vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, vp]),
+    "fa_hip_slot_remap": (C.c_int, [vp, i64, vp, vp]),
     "fa_hip_compact_lines": (C.c_int, [vp, vp, vp, vp, vp, vp, vp, i64, vp, vp, vp]),
     "fa_hip_rule_gen": (C.c_int, [vp, i64, C.c_int, vp, i64, vp, vp, vp, vp, vp]),
     "fa_hip_rule_cut": (C.c_int, [vp, vp, i64, C.c_int, vp, vp, vp, vp]),

@@ -1180,18 +1180,12 @@ def rules_build_device(levels: list, counts: list, tie_pos: np.ndarray, dev) -> 
                 level_stats=stats)
 
 
-def parse_numeric_device(buf: torch.Tensor, n: int, last_is_term: bool):
-    """Parse n file bytes already in HBM (csrc/hip/parse.hip).  ``buf`` is uint8,
-    padded with >= 64 zero bytes past a multiple of 64.  Returns (offsets int64
-    [nl+1], items int32, extras int32, vocab size), all on the device except the
-    vocab size, or None when a token is not canonical numeric (-> host parser)."""
+def _device_lines(buf: torch.Tensor, n: int, last_is_term: bool):
+    """Line ends of n file bytes in HBM and per-line upper-bound slots of (len + 1) / 2
+    ids: (ends int64 [nl], nl, bound_off int64 [nl + 1], total slots)."""
     dev = buf.device
     st = _stream(buf)
     lib = _native.hip()
-    if n <= 0:
-        return (torch.zeros(1, dtype=_I64, device=dev), torch.zeros(0, dtype=_I32, device=dev),
-                torch.zeros(0, dtype=_I32, device=dev), 0)
-    assert buf.numel() >= (n + 63) // 64 * 64 + 64 and buf.dtype == torch.uint8
     tiles = int(lib.fa_hip_parse_tiles(n))
     tile_cnt = torch.empty(tiles, dtype=_I32, device=dev)
     _native.check(lib.fa_hip_line_count(_p(buf), n, _p(tile_cnt), st), "fa_hip_line_count")
@@ -1210,7 +1204,37 @@ def parse_numeric_device(buf: torch.Tensor, n: int, last_is_term: bool):
     bound = torch.clamp((ends - starts + 1) // 2, min=1)
     bound_off = torch.zeros(nl + 1, dtype=_I64, device=dev)
     torch.cumsum(bound, 0, out=bound_off[1:])
-    nb = int(bound_off[-1].item())
+    return ends, nl, bound_off, int(bound_off[-1].item())
+
+
+def _compact_lines(scratch, xscratch, bound_off, dcnt, xcnt, nl, st):
+    dev = scratch.device
+    off = torch.zeros(nl + 1, dtype=_I64, device=dev)
+    torch.cumsum(dcnt, 0, out=off[1:])
+    xoff = torch.zeros(nl + 1, dtype=_I64, device=dev)
+    torch.cumsum(xcnt, 0, out=xoff[1:])
+    n_items, n_extras = (int(v) for v in torch.stack([off[-1], xoff[-1]]).cpu().tolist())
+    items = torch.empty(n_items, dtype=_I32, device=dev)
+    extras = torch.empty(n_extras, dtype=_I32, device=dev)
+    _native.check(_native.hip().fa_hip_compact_lines(_p(scratch), _p(xscratch), _p(bound_off), _p(dcnt), _p(xcnt),
+                                                     _p(off), _p(xoff), nl, _p(items), _p(extras), st),
+                  "fa_hip_compact_lines")
+    return off, items, extras
+
+
+def parse_numeric_device(buf: torch.Tensor, n: int, last_is_term: bool):
+    """Parse n file bytes already in HBM (csrc/hip/parse.hip).  ``buf`` is uint8,
+    padded with >= 64 zero bytes past a multiple of 64.  Returns (offsets int64
+    [nl+1], items int32, extras int32, vocab size), all on the device except the
+    vocab size, or None when a token is not canonical numeric (-> dictionary mode)."""
+    dev = buf.device
+    st = _stream(buf)
+    lib = _native.hip()
+    if n <= 0:
+        return (torch.zeros(1, dtype=_I64, device=dev), torch.zeros(0, dtype=_I32, device=dev),
+                torch.zeros(0, dtype=_I32, device=dev), 0)
+    assert buf.numel() >= (n + 63) // 64 * 64 + 64 and buf.dtype == torch.uint8
+    ends, nl, bound_off, nb = _device_lines(buf, n, last_is_term)
     scratch = torch.empty(nb, dtype=_I32, device=dev)
     xscratch = torch.empty(nb, dtype=_I32, device=dev)
     dcnt = torch.empty(nl, dtype=_I32, device=dev)
@@ -1218,18 +1242,51 @@ def parse_numeric_device(buf: torch.Tensor, n: int, last_is_term: bool):
     flags = torch.zeros(2, dtype=_I32, device=dev)
     _native.check(lib.fa_hip_parse_lines(_p(buf), _p(ends), nl, _p(bound_off), _p(scratch), _p(xscratch), _p(dcnt),
                                          _p(xcnt), _p(flags), st), "fa_hip_parse_lines")
-    off = torch.zeros(nl + 1, dtype=_I64, device=dev)
-    torch.cumsum(dcnt, 0, out=off[1:])
-    xoff = torch.zeros(nl + 1, dtype=_I64, device=dev)
-    torch.cumsum(xcnt, 0, out=xoff[1:])
-    info = torch.stack([flags[0].to(_I64), flags[1].to(_I64), off[-1], xoff[-1]]).cpu().tolist()
-    if info[0]:
+    fl = flags.cpu().tolist()
+    if fl[0]:
         return None
-    items = torch.empty(info[2], dtype=_I32, device=dev)
-    extras = torch.empty(info[3], dtype=_I32, device=dev)
-    _native.check(lib.fa_hip_compact_lines(_p(scratch), _p(xscratch), _p(bound_off), _p(dcnt), _p(xcnt), _p(off),
-                                           _p(xoff), nl, _p(items), _p(extras), st), "fa_hip_compact_lines")
-    return off, items, extras, int(info[1]) + 1
+    off, items, extras = _compact_lines(scratch, xscratch, bound_off, dcnt, xcnt, nl, st)
+    return off, items, extras, int(fl[1]) + 1
+
+
+def parse_dict_device(buf: torch.Tensor, n: int, last_is_term: bool):
+    """Dictionary-mode parse of n file bytes in HBM (k_parse_lines_dict): token ids
+    from a device hash table keyed by the parser's 64-bit token hash, then dense ids
+    in hash order.  Returns (offsets, items, extras, hashes uint64 np [V], first-
+    occurrence byte offsets int64 np [V], lengths int32 np [V]) or None when the
+    table overflows (-> host parser)."""
+    dev = buf.device
+    st = _stream(buf)
+    lib = _native.hip()
+    if n <= 0:
+        return None
+    ends, nl, bound_off, nb = _device_lines(buf, n, last_is_term)
+    # distinct tokens <= tokens <= n / 2; the table holds them at <= 50 % load
+    cap = 1 << 20
+    while cap < min(n, 1 << 30):
+        cap <<= 1
+    cap = min(cap, 1 << 28)
+    keys = torch.zeros(cap, dtype=_I64, device=dev)
+    tpos = torch.empty(cap, dtype=_I64, device=dev)
+    tlen = torch.empty(cap, dtype=_I32, device=dev)
+    scratch = torch.empty(nb, dtype=_I32, device=dev)
+    xscratch = torch.empty(nb, dtype=_I32, device=dev)
+    dcnt = torch.empty(nl, dtype=_I32, device=dev)
+    xcnt = torch.empty(nl, dtype=_I32, device=dev)
+    flags = torch.zeros(2, dtype=_I32, device=dev)
+    _native.check(lib.fa_hip_parse_lines_dict(_p(buf), _p(ends), nl, _p(bound_off), _p(scratch), _p(xscratch),
+                                              _p(dcnt), _p(xcnt), _p(flags), _p(keys), _p(tpos), _p(tlen), cap, st),
+                  "fa_hip_parse_lines_dict")
+    if int(flags[0].item()) & 2:
+        return None
+    off, items, extras = _compact_lines(scratch, xscratch, bound_off, dcnt, xcnt, nl, st)
+    occ = keys != 0
+    slot_id = (torch.cumsum(occ.to(_I32), 0, dtype=_I32) - 1).contiguous()
+    for t in (items, extras):
+        _native.check(lib.fa_hip_slot_remap(_p(t), t.numel(), _p(slot_id), st), "fa_hip_slot_remap")
+    sel = torch.nonzero(occ).flatten()
+    hashes = keys[sel].cpu().numpy().view(np.uint64)
+    return off, items, extras, hashes, tpos[sel].cpu().numpy(), tlen[sel].cpu().numpy()
 
 
 DFS_PIECE_NODES = 8        # depth-1 nodes per work piece (as the slab kernel's extensions per piece)

@@ -74,6 +74,7 @@ def parse_file(path: str, byte_begin: int = 0, byte_end: int = -1, mode: int = 0
 # csrc/hip/parse.hip.  Numeric vocabularies only; anything else returns None and
 # the caller uses the host parser.
 GPU_PARSE = os.environ.get("FA_GPU_PARSE", "1") == "1"
+DEVICE_DICT = os.environ.get("FA_GPU_PARSE_DICT", "1") == "1"
 _RING_SLOT = 32 << 20
 _RING_SLOTS = 8
 _ring: list = []
@@ -143,9 +144,12 @@ def _file_to_device(fd: int, first: int, n: int, dev) -> torch.Tensor:
     return out
 
 
-def parse_file_device(path: str, byte_begin: int, byte_end: int, device, line_base: int = 0):
-    """Lines starting in [byte_begin, byte_end) parsed on the GPU, or None (non-numeric
-    tokens, or a CPU device)."""
+def parse_file_device(path: str, byte_begin: int, byte_end: int, device, line_base: int = 0,
+                      force_dict: bool = False):
+    """Lines starting in [byte_begin, byte_end) parsed on the GPU, or None (a CPU device,
+    or a dictionary table overflow).  Numeric tokens take the numeric id space; any
+    other token the device dictionary path (hash-table ids, strings read back from the
+    file only for the ids decoded later)."""
     from ..ops import primitives as prim
 
     device = torch.device(device)
@@ -164,12 +168,18 @@ def parse_file_device(path: str, byte_begin: int, byte_end: int, device, line_ba
         buf = _file_to_device(fd, first, n, device)
     finally:
         os.close(fd)
-    got = prim.parse_numeric_device(buf, n, last_is_term)
+    got = None if force_dict else prim.parse_numeric_device(buf, n, last_is_term)
+    if got is not None:
+        del buf
+        off, items, extras, vocab = got
+        return TransactionShard(off, items, extras.cpu().numpy(), Vocabulary(True, vocab), line_base)
+    got = prim.parse_dict_device(buf, n, last_is_term) if DEVICE_DICT else None
     del buf
     if got is None:
         return None
-    off, items, extras, vocab = got
-    return TransactionShard(off, items, extras.cpu().numpy(), Vocabulary(True, vocab), line_base)
+    off, items, extras, hashes, pos, lens = got
+    voc = Vocabulary(False, int(hashes.size), hashes=hashes, file_src=(path, first, pos, lens))
+    return TransactionShard(off, items, extras.cpu().numpy(), voc, line_base)
 
 
 def parse_bytes(data: bytes, mode: int = 0, device="cpu") -> TransactionShard:
@@ -193,7 +203,10 @@ def read_shard(path: str, comm, device: torch.device | str | None = None) -> Tra
         shard = parse_file(path, b, e, 0, device)
     need_dict = comm.allreduce_int(0 if shard.vocab.numeric else 1, "max")
     if need_dict and shard.vocab.numeric:
-        shard = parse_file(path, b, e, 1, device)
+        # another rank saw non-numeric tokens: every rank takes dictionary ids
+        shard = (parse_file_device(path, b, e, device, force_dict=True)
+                 if (GPU_PARSE and DEVICE_DICT and device.type == "cuda") else None) or parse_file(path, b, e, 1,
+                                                                                                  device)
     counts = comm.all_gather_int(shard.n_lines)
     shard.line_base = int(sum(counts[: comm.rank]))
     return shard.to(device)

@@ -61,12 +61,47 @@ def test_long_lines_with_duplicates(tmp_path):
     assert g.extras.size > 0
 
 
+def _same_dict(path, b=0, e=-1):
+    """Device dictionary parse vs host dictionary parse: ids differ (slot order vs hash
+    order), so compare through the 64-bit token hashes and the decoded strings."""
+    got = io.parse_file_device(path, b, e, DEV, force_dict=True)
+    ref = io.parse_file(path, b, e, 1, "cpu")
+    assert got is not None and not got.vocab.numeric and not ref.vocab.numeric
+    assert torch.equal(got.offsets.cpu(), ref.offsets)
+    gh, rh = got.vocab.hashes, ref.vocab.hashes
+    assert np.array_equal(gh[got.items.cpu().numpy()], rh[ref.items.numpy()])
+    assert np.array_equal(gh[got.extras], rh[ref.extras])
+    assert got.vocab.size == ref.vocab.size
+    gs = dict(zip(gh.tolist(), got.vocab.decode(np.arange(got.vocab.size))))
+    rs = dict(zip(rh.tolist(), ref.vocab.decode(np.arange(ref.vocab.size))))
+    assert gs == rs
+    return got
+
+
 @pytest.mark.parametrize("data", [b"1 2\n007 3\n", b"1 2\nx y\n", b"1 2147483647\n", b"1 2\x013\n",
                                   b"12345678901\n"])
-def test_non_numeric_falls_back(tmp_path, data):
+def test_non_numeric_takes_device_dictionary(tmp_path, data):
     p = _write(tmp_path, data)
-    assert io.parse_file_device(p, 0, -1, DEV) is None
     assert not io.parse_file(p, 0, -1, 0, "cpu").vocab.numeric
+    got = io.parse_file_device(p, 0, -1, DEV)
+    assert got is not None and not got.vocab.numeric
+    _same_dict(p)
+
+
+def test_device_dictionary_random_words(tmp_path):
+    rng = np.random.default_rng(7)
+    words = [("w%x" % i).encode() for i in range(5000)] + ["é".encode(), "ß".encode(), b"a\x01b", b"0", b""]
+    parts = []
+    for _ in range(4000):
+        L = int(rng.integers(0, 90))
+        toks = [words[int(rng.integers(0, len(words) - 1))] for _ in range(L)]   # repeats included
+        parts.append(b" ".join(toks) + [b"\n", b"\r\n", b"\r"][int(rng.integers(0, 3))])
+    p = _write(tmp_path, b"".join(parts))
+    g = _same_dict(p)
+    assert g.extras.size > 0 and g.vocab.size > 4000
+    size = os.path.getsize(p)
+    for b, e in ((0, size // 3), (size // 3, size)):
+        _same_dict(p, b, e)
 
 
 def test_random_files_and_byte_ranges(tmp_path):
