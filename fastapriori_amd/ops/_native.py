@@ -69,6 +69,8 @@ _HIP_SIGS = {
     "fa_hip_ag_gen": (C.c_int, [vp, i64, C.c_int, C.c_int, vp, i64, vp, i64, vp, vp]),
     "fa_hip_ag_chain": (C.c_int, [vp, i64, C.c_int, C.c_int, vp, i64, vp, i64, C.c_int, dbl, i64, i64, vp, vp,
                                   C.c_int, dbl]),
+    "fa_hip_ag_chain_coop": (C.c_int, [vp, i64, C.c_int, C.c_int, vp, i64, vp, i64, C.c_int, dbl, i64, i64, vp,
+                                       C.c_int, dbl, C.c_int, vp]),
     "fa_hip_ag_build": (C.c_int, [vp, i64, C.c_int, vp, C.c_uint32, C.c_int, vp, vp]),
     "fa_hip_ag_rows": (C.c_int, [vp, i64, C.c_int, vp, C.c_uint32, C.c_int, vp, vp, vp, vp, C.c_int, vp]),
     "fa_hip_cmp_agg": (C.c_int, [vp, vp, vp, i64, vp, vp, vp]),

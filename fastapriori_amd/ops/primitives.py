@@ -1010,7 +1010,11 @@ def apriori_gen_chain(rows: np.ndarray, F1: int, dev, max_levels: int, growth: f
     sizes = np.zeros(2 + max_levels, dtype=np.int64)
     host_stage = pinned_stage("gen_out")
     need_host = 1 << 20
-    for _ in range(32):
+    got = _ag_chain_coop(P, n, m, F1, dev, max_levels, growth, total0, tmax, first_free, sizes) \
+        if (GEN_COOP and max_levels <= 60) else None
+    if got is not None:
+        h = got
+    for _ in range(0 if got is not None else 32):
         ws = _GEN_WS.get(dev)
         if ws is None or ws.numel() < (64 << 20):
             ws = _GEN_WS[dev] = torch.empty(64 << 20, dtype=torch.uint8, device=dev)
@@ -1027,8 +1031,10 @@ def apriori_gen_chain(rows: np.ndarray, F1: int, dev, max_levels: int, growth: f
         _native.check(rc, "fa_hip_ag_chain")
         break
     else:
-        raise RuntimeError("fa_hip_ag_chain: buffer sizing did not converge")
-    h = host.numpy()
+        if got is None:
+            raise RuntimeError("fa_hip_ag_chain: buffer sizing did not converge")
+    if got is None:
+        h = host.numpy()
     out, o = [], (128 if first_free else 0)
     for lv in range(int(sizes[0])):
         C = int(sizes[2 + lv])
@@ -1042,6 +1048,47 @@ def apriori_gen_chain(rows: np.ndarray, F1: int, dev, max_levels: int, growth: f
         o += n + C + C * (m + 1)
         n, m = C, m + 1
     return out
+
+
+GEN_COOP = os.environ.get("FA_GEN_COOP", "1") == "1"
+_COOP: dict = {}
+
+
+def _ag_chain_coop(P, n: int, m: int, F1: int, dev, max_levels: int, growth: float, total0: int, tmax: int,
+                   first_free: bool, sizes: np.ndarray):
+    """The chain as one cooperative kernel (k_ag_chain_coop): one launch, then two
+    small readbacks (control words, then the used part of the output area).  Returns
+    the host int32 array in fa_hip_ag_chain's layout and fills sizes, or None (launch
+    refused or an area too small: the caller runs the per-level chain)."""
+    st = _stream(P)
+    bufs = _COOP.get(dev)
+    if bufs is None:
+        props = torch.cuda.get_device_properties(dev)
+        bufs = _COOP[dev] = dict(work=torch.empty(64 << 20, dtype=torch.uint8, device=dev),
+                                 out=torch.empty(16 << 20, dtype=_I32, device=dev),
+                                 dctl=torch.zeros(72, dtype=_I64, device=dev),
+                                 ctl=torch.zeros(72, dtype=_I64, pin_memory=True),
+                                 n_wg=int(props.multi_processor_count))
+    rc = _native.hip().fa_hip_ag_chain_coop(_p(P), n, m, F1, _p(bufs["work"]), bufs["work"].numel(),
+                                            _p(bufs["out"]), bufs["out"].numel(), max_levels, growth, total0, tmax,
+                                            _p(bufs["dctl"]), int(first_free), float(_LDS_BYTES), bufs["n_wg"], st)
+    if rc != 0:
+        note_fallback(f"cooperative apriori-gen chain not launched (hip error {rc}): per-level chain")
+        return None
+    ctl = bufs["ctl"]
+    ctl.copy_(bufs["dctl"], non_blocking=True)
+    torch.cuda.current_stream(dev).synchronize()
+    c = ctl.numpy()
+    if int(c[1]) != 0:
+        return None
+    used = int(c[2])
+    host = pinned_stage("gen_out").get(4 * max(used, 1)).view(dtype=_I32)[:max(used, 1)]
+    if used:
+        host[:used].copy_(bufs["out"][:used], non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+    sizes[0] = int(c[0])
+    sizes[2:2 + int(c[0])] = c[4:4 + int(c[0])]
+    return host.numpy()
 
 
 def slab_total_limit(n_used: int) -> int:

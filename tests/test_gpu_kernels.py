@@ -246,6 +246,35 @@ def test_gen_chain_matches_iterated_gen():
     assert len(ops.primitives.apriori_gen_chain(cand, F1, DEV, 4, (c0 - 0.5) / cand.shape[0], 0, 1 << 40)) == 0
 
 
+@pytest.mark.parametrize("first_free", [True, False])
+def test_coop_chain_matches_per_level_chain(monkeypatch, first_free):
+    # k_ag_chain_coop (one cooperative launch, decisions on the device) == fa_hip_ag_chain
+    sh = generate_shard(200000, Comm(), "cpu", 10.0, 4.0, 60, 80, seed=8)
+    res = FastApriori(0.003, config=MinerConfig(min_support=0.003)).run(sh)
+    F1 = len(res.items)
+    n_levels = 0
+    for k in (2, 3, 4):
+        prev = res.levels[k - 1]
+        if first_free:
+            args = (prev, F1, DEV, 64, 1.5, 0, 0, True)
+        else:
+            pi, eo, ex = apriori_gen(prev)
+            g = np.repeat(np.arange(pi.size), np.diff(eo))
+            cand = np.ascontiguousarray(np.concatenate([prev[pi[g]], ex[:, None]], axis=1), dtype=np.int32)
+            args = (cand, F1, DEV, 64, 1.5, 0, 1 << 40, False)
+        monkeypatch.setattr(ops.primitives, "GEN_COOP", True)
+        a = ops.primitives.apriori_gen_chain(*args)
+        monkeypatch.setattr(ops.primitives, "GEN_COOP", False)
+        b = ops.primitives.apriori_gen_chain(*args)
+        assert len(a) == len(b)
+        n_levels += len(a)
+        for x, y in zip(a, b):
+            for u, v in zip(x, y):
+                assert np.array_equal(u, v)
+    assert n_levels >= 2
+    assert not any("cooperative" in f for f in ops.primitives.FALLBACKS)
+
+
 def test_bundling_chain_matches_python_loop(monkeypatch):
     import fastapriori_amd.models.apriori as ap
     sh = generate_shard(200000, Comm(), "cpu", 10.0, 4.0, 60, 80, seed=8).to(DEV)
