@@ -1010,8 +1010,9 @@ def apriori_gen_chain(rows: np.ndarray, F1: int, dev, max_levels: int, growth: f
     sizes = np.zeros(2 + max_levels, dtype=np.int64)
     host_stage = pinned_stage("gen_out")
     need_host = 1 << 20
-    got = _ag_chain_coop(P, n, m, F1, dev, max_levels, growth, total0, tmax, first_free, sizes) \
-        if (GEN_COOP and max_levels <= 60) else None
+    # (a chain capped at 60 levels only ends a bundle early: the miner goes on from there)
+    got = _ag_chain_coop(P, n, m, F1, dev, min(max_levels, 60), growth, total0, tmax, first_free, sizes) \
+        if GEN_COOP else None
     if got is not None:
         h = got
     for _ in range(0 if got is not None else 32):
@@ -1050,7 +1051,10 @@ def apriori_gen_chain(rows: np.ndarray, F1: int, dev, max_levels: int, growth: f
     return out
 
 
-GEN_COOP = os.environ.get("FA_GEN_COOP", "1") == "1"
+# Off by default: measured slower on MI355X (T10I4D100M 53.3 -> 56.8 ms, 12.5M-row shard
+# 9.9 -> 12.3 ms).  Eight grid barriers per level over 256 workgroups on 8 XCDs cost
+# more than the per-level host round trip they replace.
+GEN_COOP = os.environ.get("FA_GEN_COOP", "0") == "1"
 _COOP: dict = {}
 
 
@@ -1079,6 +1083,9 @@ def _ag_chain_coop(P, n: int, m: int, F1: int, dev, max_levels: int, growth: flo
     ctl.copy_(bufs["dctl"], non_blocking=True)
     torch.cuda.current_stream(dev).synchronize()
     c = ctl.numpy()
+    if os.environ.get("FA_DEBUG_COOP"):
+        import sys
+        print(f"ag_chain_coop: n={n} m={m} ctl={c[:8].tolist()} C={c[4:4 + int(c[0])].tolist()}", file=sys.stderr)
     if int(c[1]) != 0:
         return None
     used = int(c[2])

@@ -262,8 +262,13 @@ def test_coop_chain_matches_per_level_chain(monkeypatch, first_free):
             g = np.repeat(np.arange(pi.size), np.diff(eo))
             cand = np.ascontiguousarray(np.concatenate([prev[pi[g]], ex[:, None]], axis=1), dtype=np.int32)
             args = (cand, F1, DEV, 64, 1.5, 0, 1 << 40, False)
-        monkeypatch.setattr(ops.primitives, "GEN_COOP", True)
+        monkeypatch.setattr(ops.primitives, "GEN_COOP", True)      # opt-in path (FA_GEN_COOP=1)
+        calls = []
+        real = ops.primitives._ag_chain_coop
+        monkeypatch.setattr(ops.primitives, "_ag_chain_coop", lambda *a, **k: calls.append(1) or real(*a, **k))
         a = ops.primitives.apriori_gen_chain(*args)
+        monkeypatch.setattr(ops.primitives, "_ag_chain_coop", real)
+        assert calls
         monkeypatch.setattr(ops.primitives, "GEN_COOP", False)
         b = ops.primitives.apriori_gen_chain(*args)
         assert len(a) == len(b)
