@@ -115,13 +115,19 @@ def _e2e_window(args, comm, n_txn, min_sup, cfgv, miner_cfg, sync):
     path = os.path.join(d, "D.dat")
     out = os.path.join(d, f"out_{os.getpid() if comm.is_root else 0}", "freqItemset")
     t_w = time.perf_counter()
+    err = ""
     if comm.is_root:
-        os.makedirs(d, exist_ok=True)
-        if not os.path.exists(path):
-            tmp = path + ".tmp"
-            io.write_quest_file(tmp, n_txn, avg_len, avg_pat, n_pat, n_items, seed=args.seed)
-            os.replace(tmp, path)
-    comm.barrier()
+        try:
+            os.makedirs(d, exist_ok=True)
+            if not os.path.exists(path):
+                tmp = path + ".tmp"
+                io.write_quest_file(tmp, n_txn, avg_len, avg_pat, n_pat, n_items, seed=args.seed)
+                os.replace(tmp, path)
+        except OSError as e:           # e.g. no room for the file: skip the window, keep the bench
+            err = f"{type(e).__name__}: {e}"
+            shutil.rmtree(d, ignore_errors=True)
+    if comm.allreduce_int(1 if err else 0, "max"):
+        return {"window": "skipped", "error": err or "the D.dat file could not be written"}, None
     write_s = time.perf_counter() - t_w
     quiet = Logger(comm.rank, enabled=False)
 
@@ -238,7 +244,7 @@ def main() -> int:
     if want_e2e and args.steps > 0:
         del shard
         e2e, _ = _e2e_window(args, comm, n_txn, min_sup, CONFIGS[args.config], cfg, sync)
-        if e2e["n_itemsets"] != n_sets:
+        if "n_itemsets" in e2e and e2e["n_itemsets"] != n_sets:
             print(f"bench.py: e2e run found {e2e['n_itemsets']} itemsets, in-memory run {n_sets}",
                   file=sys.stderr)
             return 3

@@ -149,18 +149,31 @@ __global__ __launch_bounds__(256) void k_compress_regs(
     const int32_t* __restrict__ rows, int64_t nrows, const int32_t* __restrict__ kept,
     const int64_t* __restrict__ roff, int32_t* __restrict__ ranks, int8_t* __restrict__ over_flag) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nrows) return;
-  const int32_t x = rows ? rows[i] : (int32_t)i;
-  const int64_t t = kept[x];
-  const int64_t s = off[t];
-  const int64_t L = off[t + 1] - s;
-  over_flag[i] = L > N ? 1 : 0;
-  if (L > N) return;
+  const bool valid = i < nrows;
+  int64_t s = 0, L = 0, x = 0;
+  if (valid) {
+    x = rows ? rows[i] : (int32_t)i;
+    const int64_t t = kept[x];
+    s = off[t];
+    L = off[t + 1] - s;
+    over_flag[i] = L > N ? 1 : 0;
+  }
+  const bool mine = valid && L <= N;
+  // loads only up to the longest row of the wave (a wave-uniform bound: the slots past
+  // it are skipped by a scalar branch instead of issuing N mostly-masked loads)
+  int Lw = mine ? (int)L : 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { const int t = __shfl_xor(Lw, o, 64); Lw = t > Lw ? t : Lw; }
+  Lw = __builtin_amdgcn_readfirstlane(Lw);
+  if (!mine) return;
   uint32_t a[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) {
-    int32_t r = j < L ? lut[items[s + j]] : -1;
-    a[j] = r < 0 ? 0xFFFFFFFFu : (uint32_t)r;
+    a[j] = 0xFFFFFFFFu;
+    if (j < Lw) {
+      const int32_t r = j < L ? lut[items[s + j]] : -1;
+      a[j] = r < 0 ? 0xFFFFFFFFu : (uint32_t)r;
+    }
   }
   bitonic_regs<N>(a);
   const int64_t o = roff[x];
@@ -846,6 +859,8 @@ FA_API int fa_hip_compress_regs(int tier, const int64_t* off, const int32_t* ite
   dim3 g((unsigned)((nrows + 255) / 256));
   if (tier == 16)
     hipLaunchKernelGGL(k_compress_regs<16>, g, dim3(256), 0, st, off, items, lut, rows, nrows, kept, roff, ranks, over_flag);
+  else if (tier == 32)
+    hipLaunchKernelGGL(k_compress_regs<32>, g, dim3(256), 0, st, off, items, lut, rows, nrows, kept, roff, ranks, over_flag);
   else if (tier == 64)
     hipLaunchKernelGGL(k_compress_regs<64>, g, dim3(256), 0, st, off, items, lut, rows, nrows, kept, roff, ranks, over_flag);
   else
