@@ -1106,6 +1106,9 @@ __global__ __launch_bounds__(256) void k_count_candidates(
 // per workgroup at the end.
 // ---------------------------------------------------------------------------
 constexpr int kSlabThreads = 1024;
+#ifndef FA_TRIE_NQ
+#define FA_TRIE_NQ 2
+#endif
 
 // Slab build modes: per-column rank prefetch (dedup: columns gather rows through
 // src), wave-cooperative coalesced build (columns = rows, contiguous ranks), or
@@ -1359,14 +1362,14 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
 // prefix row, ext begin, ext end, flags): bit 1 = recompute P2 from P1, bit 0 =
 // recompute p from P2.  The first piece of a work item recomputes everything.
 // ---------------------------------------------------------------------------
-template <int SW, bool kWeighted, int kBuild>
+template <int SW, bool kWeighted, int kBuild, bool kAcc16 = false>
 __global__ __launch_bounds__(kSlabThreads) void k_count_trie(
     const int64_t* __restrict__ roff, const int32_t* __restrict__ ranks, const int32_t* __restrict__ src,
     int64_t ncols, const int32_t* __restrict__ item_map, int n_used, const int32_t* __restrict__ gpre, int m,
     int D1, int D2, const int4* __restrict__ pieces, const int2* __restrict__ witems, int NW,
     const int32_t* __restrict__ gext, int C, const int32_t* __restrict__ wword, uint32_t* __restrict__ out,
     const uint64_t* __restrict__ bm, int64_t Wp, const int32_t* __restrict__ bm_rows, int acc16) {
-  constexpr int NQ = 2;                        // uint4 (4 words) per lane: ~90 VGPRs at 1024 threads
+  constexpr int NQ = (SW / 2) / 2 < FA_TRIE_NQ ? (SW / 2) / 2 : FA_TRIE_NQ;   // uint4 per lane (NQ = 2: ~90 VGPRs)
   constexpr int RS = SW / 2;                   // uint4 slots per slab row
   constexpr int LPP = RS / NQ;                 // lanes per work item: 2 / 4 / 8 for SW = 8 / 16 / 32
   static_assert(LPP == 2 || LPP == 4 || LPP == 8, "SW in {8, 16, 32}");
@@ -1379,10 +1382,11 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_trie(
   __shared__ unsigned long long build_words[kSlabThreads / 64 * 2];
   uint64_t* slab = reinterpret_cast<uint64_t*>(lds4);
   uint32_t* acc = reinterpret_cast<uint32_t*>(slab + (size_t)n_used * SW);
-  const int n_acc = acc16 ? (C + 1) >> 1 : C;   // acc16: packed 16-bit counters (see k_count_slab)
+  (void)acc16;                                  // kAcc16: the launcher's choice as a template flag
+  const int n_acc = kAcc16 ? (C + 1) >> 1 : C;  // packed 16-bit counters (see k_count_slab)
   for (int i = threadIdx.x; i < n_acc; i += blockDim.x) acc[i] = 0;
   auto acc_add = [&](int e, uint32_t v) {
-    if (acc16) atomicAdd(&acc[e >> 1], v << ((e & 1) << 4));
+    if constexpr (kAcc16) atomicAdd(&acc[e >> 1], v << ((e & 1) << 4));
     else atomicAdd(&acc[e], v);
   };
   const int64_t W = (ncols + 63) >> 6;
@@ -1514,25 +1518,41 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_trie(
           and_rows(p, it, D2, m);
         }
         int e = d.y;
-        // four extension rows per step: 4*NQ independent slab reads in flight per lane
-        for (; e + 4 <= d.z; e += 4) {
-          const int u0 = gext[e], u1 = gext[e + 1], u2 = gext[e + 2], u3 = gext[e + 3];
-          const int x0 = (u0 << 1) & (RS - 1), x1 = (u1 << 1) & (RS - 1);
-          const int x2 = (u2 << 1) & (RS - 1), x3 = (u3 << 1) & (RS - 1);
-          const uint4* r0 = lds4 + (size_t)u0 * RS;
-          const uint4* r1 = lds4 + (size_t)u1 * RS;
-          const uint4* r2 = lds4 + (size_t)u2 * RS;
-          const uint4* r3 = lds4 + (size_t)u3 * RS;
-          uint4 v0[NQ], v1[NQ], v2[NQ], v3[NQ];
+        // UE extension rows per step (UE * NQ independent slab reads in flight per lane;
+        // UE = 4 at NQ = 2, 2 at NQ = 4 -- the same registers).  The next step's ids are
+        // loaded one step ahead (an unconditional load at a clamped index), so the
+        // global latency is not exposed at every step.
+        constexpr int UE = NQ >= 4 ? 2 : 4;
+        int nx[UE];
 #pragma unroll
-          for (int q = 0; q < NQ; ++q) {
-            v0[q] = r0[off[q] ^ x0]; v1[q] = r1[off[q] ^ x1]; v2[q] = r2[off[q] ^ x2]; v3[q] = r3[off[q] ^ x3];
+        for (int k = 0; k < UE; ++k) nx[k] = 0;
+        if (e + UE <= d.z) {
+#pragma unroll
+          for (int k = 0; k < UE; ++k) nx[k] = gext[e + k];
+        }
+        for (; e + UE <= d.z; e += UE) {
+          int u[UE];
+#pragma unroll
+          for (int k = 0; k < UE; ++k) u[k] = nx[k];
+          {
+            const int ep = min(e + UE, d.z - UE);
+#pragma unroll
+            for (int k = 0; k < UE; ++k) nx[k] = gext[ep + k];
           }
-          const uint32_t s0 = lanes_sum(dot(p, v0)), s1 = lanes_sum(dot(p, v1));
-          const uint32_t s2 = lanes_sum(dot(p, v2)), s3 = lanes_sum(dot(p, v3));
+          uint4 v[UE][NQ];
+#pragma unroll
+          for (int k = 0; k < UE; ++k) {
+            const int xk = (u[k] << 1) & (RS - 1);
+            const uint4* rk = lds4 + (size_t)u[k] * RS;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) v[k][q] = rk[off[q] ^ xk];
+          }
+          uint32_t sk[UE];
+#pragma unroll
+          for (int k = 0; k < UE; ++k) sk[k] = lanes_sum(dot(p, v[k]));
           if (t == 0) {
-            acc_add(e, s0); acc_add(e + 1, s1);
-            acc_add(e + 2, s2); acc_add(e + 3, s3);
+#pragma unroll
+            for (int k = 0; k < UE; ++k) acc_add(e + k, sk[k]);
           }
         }
         for (; e < d.z; ++e) {
@@ -1549,7 +1569,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_trie(
   }
   __syncthreads();
   for (int i = threadIdx.x; i < C; i += blockDim.x) {
-    const uint32_t v = acc16 ? (acc[i >> 1] >> ((i & 1) << 4)) & 0xFFFFu : acc[i];
+    const uint32_t v = kAcc16 ? (acc[i >> 1] >> ((i & 1) << 4)) & 0xFFFFu : acc[i];
     if (v) atomicAdd(&out[i], v);
   }
 }
@@ -1732,7 +1752,9 @@ FA_API int fa_hip_count_trie(const int64_t* roff, const int32_t* ranks, const in
                          const int32_t*, int, int, int, const int4*, const int2*, int, const int32_t*, int,
                          const int32_t*, uint32_t*, const uint64_t*, int64_t, const int32_t*, int);
   KernT kern = nullptr;
-#define FA_TRIE_MODE(S, B) kern = wword ? (KernT)k_count_trie<S, true, B> : (KernT)k_count_trie<S, false, B>;
+#define FA_TRIE_MODE(S, B)                                                                        \
+  kern = wword ? (KernT)k_count_trie<S, true, B>                                                  \
+               : (acc16 ? (KernT)k_count_trie<S, false, B, true> : (KernT)k_count_trie<S, false, B>);
 #define FA_TRIE_CASE(S)                                   \
   if (sw == S) {                                          \
     if (bm) { FA_TRIE_MODE(S, kBuildBM) }                 \

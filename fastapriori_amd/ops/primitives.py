@@ -169,7 +169,7 @@ def txn_freq_count(offsets: torch.Tensor, items: torch.Tensor, lut: torch.Tensor
 
 
 COMPRESS_WAVE_MAX_F1 = 65536
-COMPRESS_WAVE_MEAN_LEN = 48    # mean row length above which every row goes to the wave kernel
+COMPRESS_WAVE_MEAN_LEN = float(os.environ.get("FA_COMPRESS_WAVE_MEAN_LEN", "48"))   # mean row length above which every row goes to the wave kernel
 
 
 def compress(offsets, items, lut, kept, roff, F1: int | None = None) -> torch.Tensor:
