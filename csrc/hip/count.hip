@@ -1122,11 +1122,25 @@ enum { kBuildCols = 0, kBuildContig = 1, kBuildBM = 2 };
 // nsub waves share one word: wave h of them takes window groups h, h + nsub, ...
 // A rank's column (bit) is the row owning its position: rows are non-empty, so
 // it is (row starts before the window) + popc(start mask & lanes <= me) - 1.
-__device__ __forceinline__ void slab_build_word(uint64_t* __restrict__ slab, int swp, int q, int64_t col0,
-                                                int64_t ncols, const int64_t* __restrict__ roff,
-                                                const int32_t* __restrict__ ranks,
-                                                const int32_t* __restrict__ item_map, int h, int nsub,
-                                                unsigned long long* words, int swz = 0) {
+// rank -> slab row (-1: not used) from the global int32 map, or from the
+// workgroup's u16 copy in LDS (k_count_slab_rec; 0xFFFF = not used)
+struct MapGlobal {
+  const int32_t* __restrict__ p;
+  __device__ __forceinline__ int operator()(int r) const { return p[r]; }
+};
+struct MapLds {
+  const uint16_t* p;
+  __device__ __forceinline__ int operator()(int r) const {
+    const int v = p[r];
+    return v == 0xFFFF ? -1 : v;
+  }
+};
+
+template <class Map = MapGlobal>
+__device__ __forceinline__ void slab_build_word_m(uint64_t* __restrict__ slab, int swp, int q, int64_t col0,
+                                                  int64_t ncols, const int64_t* __restrict__ roff,
+                                                  const int32_t* __restrict__ ranks, Map item_map, int h,
+                                                  int nsub, unsigned long long* words, int swz = 0) {
   const int lane = threadIdx.x & 63;
   const int64_t st = roff[min(col0 + lane, ncols)];
   const int64_t base = roff[col0];
@@ -1150,9 +1164,58 @@ __device__ __forceinline__ void slab_build_word(uint64_t* __restrict__ slab, int
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int l = cs + __popcll(S[u] & le) - 1;
-      const int uu = r[u] >= 0 ? item_map[r[u]] : -1;
+      const int uu = r[u] >= 0 ? item_map(r[u]) : -1;
       if (uu >= 0) atomicOr((unsigned long long*)(slab + (size_t)uu * swp + (q ^ ((uu << 2) & swz))), 1ull << l);
       cs += __popcll(S[u]);
+    }
+  }
+}
+
+__device__ __forceinline__ void slab_build_word(uint64_t* __restrict__ slab, int swp, int q, int64_t col0,
+                                                int64_t ncols, const int64_t* __restrict__ roff,
+                                                const int32_t* __restrict__ ranks,
+                                                const int32_t* __restrict__ item_map, int h, int nsub,
+                                                unsigned long long* words, int swz = 0) {
+  slab_build_word_m(slab, swp, q, col0, ncols, roff, ranks, MapGlobal{item_map}, h, nsub, words, swz);
+}
+
+// Multi-pass levels copy the slab tile of every used item from the
+// materialised bitmap.  A plain strided loop (load, store, next) pays one global
+// round trip per 16 B a thread copies (~8-10 per slab at 1024 threads);
+// here every thread issues all its loads (after one batched load of the
+// bitmap row ids) before its first LDS store.  ROWW: LDS row stride in words;
+// kSwz: the trie kernel's word XOR ((u << 2) & (SW - 4)).
+template <int SW, int ROWW, bool kSwz>
+__device__ __forceinline__ void slab_copy_bm(uint4* lds4, int n_used, const uint64_t* __restrict__ bm, int64_t Wp,
+                                             const int32_t* __restrict__ bm_rows, int64_t w0, int64_t W) {
+  constexpr int QW = SW / 2;                 // uint4 per row
+  constexpr int KMAX = 4;                    // loads in flight per thread (more: the trie kernel spills)
+  const int total = n_used * QW;
+  for (int base = 0; base < total; base += KMAX * kSlabThreads) {
+    int32_t br[KMAX];
+    uint4 v[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const int i = base + (int)threadIdx.x + k * kSlabThreads;
+      br[k] = i < total ? (bm_rows ? bm_rows[i / QW] : i / QW) : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const int i = base + (int)threadIdx.x + k * kSlabThreads;
+      const int64_t w = w0 + 2 * (i % QW);
+      v[k] = make_uint4(0, 0, 0, 0);
+      // rows are Wp (a multiple of 64) words long and zero past W: a pair whose
+      // first word is valid may be read whole
+      if (i < total && w < W) v[k] = *reinterpret_cast<const uint4*>(bm + (size_t)br[k] * Wp + w);
+    }
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const int i = base + (int)threadIdx.x + k * kSlabThreads;
+      if (i < total) {
+        const int u = i / QW, q = i % QW;
+        const int qq = kSwz ? (q ^ (((u << 2) & (SW - 4)) >> 1)) : q;
+        lds4[(size_t)u * (ROWW / 2) + qq] = v[k];
+      }
     }
   }
 }
@@ -1211,12 +1274,8 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
       // profiling split (FA_SLAB_DEBUG=1): no slab build
     } else if (kBuild == kBuildBM) {
       // multi-pass level: the used-item bitmap is materialised once; copy the slab tile
-      for (int i = threadIdx.x; i < n_used * SW; i += blockDim.x) {
-        const int u = i / SW, q = i - u * SW;
-        // bm_rows: slab row -> bitmap row when the bitmap holds every item (built once per layout)
-        const int64_t br = bm_rows ? bm_rows[u] : u;
-        slab[(size_t)u * SWP + q] = (w0 + q < W) ? bm[(size_t)br * Wp + w0 + q] : 0ull;
-      }
+      // (bm_rows: slab row -> bitmap row when the bitmap holds every item)
+      slab_copy_bm<SW, SWP, false>(lds4, n_used, bm, Wp, bm_rows, w0, W);
     } else {
       {
         uint4* s4 = lds4;
@@ -1338,6 +1397,196 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
 }
 
 // ---------------------------------------------------------------------------
+// k >= 3, slab-stationary counting from piece records (the slab path of
+// fa_level_plan).
+//
+// Same slab build and thread-per-piece counting as k_count_slab, with the piece
+// metadata laid out for latency.  PMC of k_count_slab on the T10I4D100M level 3-4
+// bundle: waves wait ~64 % of their cycles, only ~3 % of it on LDS -- every piece
+// walked a chain of dependent global loads (gpm -> prefix ids -> slab rows,
+// gext_off -> each extension id).  Here a piece is one 48-B record (plan.cpp):
+//   a = {ext begin, n_ext | m << 8 | long-prefix flag << 16, prefix ids 0-3 (u16)}
+//   b = {extension ids 0-7 (u16)}
+//   c = {prefix ids 4-11 (u16)}, or c.x = gpre offset when m > 12
+// loaded one piece ahead.  A thread's pieces are the same on every slab, so the
+// load after its last piece fetches its first piece for the next slab.  The
+// rank -> slab-row map of the slab build is copied to LDS as u16 (one dependent
+// global load less per rank).
+// ---------------------------------------------------------------------------
+constexpr int kMapLdsMax = 8192;   // plan.cpp fa_slab_map_lds: F1 <= this keeps the map in LDS
+
+__device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
+  // popcount + add in one VALU op (the compiler otherwise splits the sum into
+  // v_bcnt(x, 0) + v_add3 trees: 25 % more VALU in the extension loop)
+  uint32_t r;
+  __asm__("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+  return r;
+}
+
+__device__ __forceinline__ int u16_at(const int4& v, int k) {
+  const int w = (k >> 1) == 0 ? v.x : (k >> 1) == 1 ? v.y : (k >> 1) == 2 ? v.z : v.w;
+  return (k & 1) ? (int)((uint32_t)w >> 16) : (w & 0xFFFF);
+}
+
+template <int SW, bool kWeighted, int kBuild, bool kAcc16>
+__global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
+    const int64_t* __restrict__ roff, const int32_t* __restrict__ ranks, const int32_t* __restrict__ src,
+    int64_t ncols, const int32_t* __restrict__ item_map, int F1, int n_used, const int32_t* __restrict__ gpre,
+    const int4* __restrict__ rec, int G, int C, const int32_t* __restrict__ wword, uint32_t* __restrict__ out,
+    const uint64_t* __restrict__ bm, int64_t Wp, const int32_t* __restrict__ bm_rows, int dbg) {
+  extern __shared__ uint4 lds4[];
+  __shared__ unsigned long long build_words[kSlabThreads / 64 * 2];
+  constexpr int SWP = SW + 2;                       // row stride: odd number of 16-B slots
+  constexpr int RS = SWP / 2;
+  uint64_t* slab = reinterpret_cast<uint64_t*>(lds4);
+  uint32_t* acc = reinterpret_cast<uint32_t*>(slab + (size_t)n_used * SWP);
+  const int n_acc = kAcc16 ? (C + 1) >> 1 : C;
+  uint16_t* smap = reinterpret_cast<uint16_t*>(acc + ((n_acc + 3) & ~3));
+  const bool map_lds = kBuild == kBuildContig && F1 <= kMapLdsMax;
+  for (int i = threadIdx.x; i < n_acc; i += blockDim.x) acc[i] = 0;
+  if (map_lds) {
+    for (int i = threadIdx.x; i < F1; i += blockDim.x) {
+      const int v = item_map[i];
+      smap[i] = v < 0 ? (uint16_t)0xFFFF : (uint16_t)v;
+    }
+  }
+  const int64_t W = (ncols + 63) >> 6;
+  const int64_t nslabs = (W + SW - 1) / SW;
+  const int4 z4 = make_int4(0, 0, 0, 0);
+  const int g0 = (int)threadIdx.x;
+  int4 ra = z4, rb = z4, rc = z4;
+  if (g0 < G) { ra = rec[3 * g0]; rb = rec[3 * g0 + 1]; rc = rec[3 * g0 + 2]; }
+
+  auto and_row = [&](uint4 (&p)[SW / 2], int u) {
+    const uint4* r = lds4 + (size_t)u * RS;
+#pragma unroll
+    for (int q = 0; q < SW / 2; ++q) {
+      const uint4 v = r[q];
+      p[q].x &= v.x; p[q].y &= v.y; p[q].z &= v.z; p[q].w &= v.w;
+    }
+  };
+  auto acc_add = [&](int e, uint32_t v) {
+    if constexpr (kAcc16) atomicAdd(&acc[e >> 1], v << ((e & 1) << 4));
+    else atomicAdd(&acc[e], v);
+  };
+
+  for (int64_t sb = blockIdx.x; sb < nslabs; sb += gridDim.x) {
+    const int64_t w0 = sb * SW;
+    __syncthreads();
+    if (dbg & 1) {
+      // profiling split (FA_SLAB_DEBUG=1): no slab build
+    } else if (kBuild == kBuildBM) {
+      slab_copy_bm<SW, SWP, false>(lds4, n_used, bm, Wp, bm_rows, w0, W);
+    } else {
+      {
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        for (int i = threadIdx.x; i < n_used * RS; i += blockDim.x) lds4[i] = z;
+      }
+      __syncthreads();
+      if (kBuild == kBuildContig) {
+        constexpr int NW = kSlabThreads / 64;
+        constexpr int NSUB = NW > SW ? NW / SW : 1;
+        const int wv = threadIdx.x >> 6;
+        for (int q = wv / NSUB; q < SW; q += NW / NSUB) {
+          if ((w0 + q) * 64 >= ncols) continue;
+          if (map_lds)
+            slab_build_word_m(slab, SWP, q, (w0 + q) * 64, ncols, roff, ranks, MapLds{smap}, wv % NSUB, NSUB,
+                              build_words + wv * 2);
+          else
+            slab_build_word_m(slab, SWP, q, (w0 + q) * 64, ncols, roff, ranks, MapGlobal{item_map}, wv % NSUB,
+                              NSUB, build_words + wv * 2);
+        }
+      } else {
+        // dedup layout: column j of the tile gathers row src[col]
+        for (int j = threadIdx.x; j < SW * 64; j += blockDim.x) {
+          const int64_t col = w0 * 64 + j;
+          if (col >= ncols) break;
+          const int64_t row = src ? (int64_t)src[col] : col;
+          if (row < 0) continue;
+          const unsigned long long bit = 1ull << (j & 63);
+          uint64_t* base = slab + (j >> 6);
+          for (int64_t r = roff[row], r1 = roff[row + 1]; r < r1; ++r) {
+            const int uu = item_map[ranks[r]];
+            if (uu >= 0) atomicOr((unsigned long long*)(base + (size_t)uu * SWP), bit);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    uint32_t wt[SW];
+#pragma unroll
+    for (int q = 0; q < SW; ++q) wt[q] = kWeighted ? ((w0 + q < W) ? (uint32_t)wword[w0 + q] : 0u) : 1u;
+    for (int g = g0; g < ((dbg & 2) ? 0 : G); g += kSlabThreads) {
+      // this thread's next piece (after its last one: its first, for the next slab)
+      const int gn = g + kSlabThreads < G ? g + kSlabThreads : g0;
+      const int4 na = rec[3 * gn], nb = rec[3 * gn + 1], nc = rec[3 * gn + 2];
+      const int n_ext = ra.y & 0xFF, m = (ra.y >> 8) & 0xFF;
+      uint4 p[SW / 2];
+      {
+        const uint4* r0 = lds4 + (size_t)(ra.z & 0xFFFF) * RS;
+#pragma unroll
+        for (int q = 0; q < SW / 2; ++q) p[q] = r0[q];
+      }
+      if (!((ra.y >> 16) & 1)) {
+#pragma unroll
+        for (int j = 1; j < 4; ++j)
+          if (j < m) and_row(p, u16_at(ra, 4 + j));
+        if (m > 4) {
+#pragma unroll
+          for (int j = 4; j < 12; ++j)
+            if (j < m) and_row(p, u16_at(rc, j - 4));
+        }
+      } else {
+        const int32_t* pr = gpre + rc.x;            // long prefixes (m > 12): ids from the plan's gpre
+        for (int j = 1; j < m; ++j) and_row(p, pr[j]);
+      }
+      uint32_t any = 0;
+#pragma unroll
+      for (int q = 0; q < SW / 2; ++q) any |= p[q].x | p[q].y | p[q].z | p[q].w;
+      if (any) {
+        const int e0 = ra.x;
+        // UE extension rows in flight per step (2 x 64 B at SW <= 8; wider rows one at a time)
+        constexpr int UE = SW <= 8 ? 2 : 1;
+#pragma unroll
+        for (int k = 0; k < 8; k += UE) {
+          if (k >= n_ext) break;
+          uint32_t s[UE];
+          const uint4* r[UE];
+#pragma unroll
+          for (int x = 0; x < UE; ++x) {
+            s[x] = 0;
+            r[x] = lds4 + (size_t)u16_at(rb, k + x < n_ext ? k + x : k) * RS;
+          }
+#pragma unroll
+          for (int q = 0; q < SW / 2; ++q) {
+#pragma unroll
+            for (int x = 0; x < UE; ++x) {
+              const uint4 v = r[x][q];
+              if (kWeighted) {
+                s[x] += (uint32_t)(__popc(p[q].x & v.x) + __popc(p[q].y & v.y)) * wt[2 * q] +
+                        (uint32_t)(__popc(p[q].z & v.z) + __popc(p[q].w & v.w)) * wt[2 * q + 1];
+              } else {
+                s[x] = bcnt_acc(p[q].x & v.x, s[x]); s[x] = bcnt_acc(p[q].y & v.y, s[x]);
+                s[x] = bcnt_acc(p[q].z & v.z, s[x]); s[x] = bcnt_acc(p[q].w & v.w, s[x]);
+              }
+            }
+          }
+#pragma unroll
+          for (int x = 0; x < UE; ++x)
+            if (k + x < n_ext && s[x]) acc_add(e0 + k + x, s[x]);
+        }
+      }
+      ra = na; rb = nb; rc = nc;
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < C; i += blockDim.x) {
+    const uint32_t v = kAcc16 ? (acc[i >> 1] >> ((i & 1) << 4)) & 0xFFFFu : acc[i];
+    if (v) atomicAdd(&out[i], v);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k >= 3, trie-shared slab counting (the default level kernel).
 //
 // Same slab-stationary structure as k_count_slab (one LDS slab of the used
@@ -1405,11 +1654,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_trie(
     const int64_t w0 = sb * SW;
     __syncthreads();
     if (kBuild == kBuildBM) {
-      for (int i = threadIdx.x; i < n_used * SW; i += blockDim.x) {
-        const int u = i / SW, q = i - u * SW;
-        const int64_t br = bm_rows ? bm_rows[u] : u;
-        slab[(size_t)u * SW + (q ^ ((u << 2) & SWZ))] = (w0 + q < W) ? bm[(size_t)br * Wp + w0 + q] : 0ull;
-      }
+      slab_copy_bm<SW, SW, true>(lds4, n_used, bm, Wp, bm_rows, w0, W);
     } else {
       {
         const uint4 z = make_uint4(0, 0, 0, 0);
@@ -1700,6 +1945,46 @@ FA_API int fa_hip_count_slab(const int64_t* roff, const int32_t* ranks, const in
   const int dbg = getenv("FA_SLAB_DEBUG") ? atoi(getenv("FA_SLAB_DEBUG")) : 0;
   hipLaunchKernelGGL(kern, g, b, lds, st, roff, ranks, src, ncols, item_map, n_used, gpre, m, gext_off, gext, G, C,
                      wword, out, bm, Wp, dbg, gpm, bm_rows, acc16, (const int32_t*)nullptr);
+  FA_LAUNCH_RET();
+}
+
+// Slab counting from piece records (k_count_slab_rec; records: plan.cpp, 3 x int4
+// per piece).  LDS: slab + accumulator (16-B aligned) + u16 map when F1 <= 8192
+// and the slab is built from contiguous rows.  Returns 3 when that exceeds the LDS.
+FA_API int fa_hip_count_slab_rec(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
+                                 const int32_t* item_map, int F1, int n_used, const int32_t* gpre, const void* rec,
+                                 int G, int C, const int32_t* wword, uint32_t* out, int sw, int n_wg,
+                                 const uint64_t* bm, int64_t Wp, hipStream_t st, const int32_t* bm_rows, int acc16) {
+  if (G <= 0 || C <= 0 || ncols <= 0) return 0;
+  const int64_t n_acc = acc16 ? (C + 1) / 2 : C;
+  const bool contig = !bm && !src;
+  const size_t map_b = (contig && F1 <= kMapLdsMax) ? (size_t)(((int64_t)F1 * 2 + 15) & ~(int64_t)15) : 0;
+  const size_t lds = (size_t)n_used * (sw + 2) * 8 + (size_t)((n_acc + 3) & ~(int64_t)3) * 4 + map_b;
+  if (lds > 160 * 1024 - 256) return 3;             // static build_words scratch
+  using KernT = void (*)(const int64_t*, const int32_t*, const int32_t*, int64_t, const int32_t*, int, int,
+                         const int32_t*, const int4*, int, int, const int32_t*, uint32_t*, const uint64_t*, int64_t,
+                         const int32_t*, int);
+  KernT kern = nullptr;
+#define FA_REC_MODE(S, B)                                                                       \
+  kern = wword ? (KernT)k_count_slab_rec<S, true, B, false>                                     \
+               : (acc16 ? (KernT)k_count_slab_rec<S, false, B, true> : (KernT)k_count_slab_rec<S, false, B, false>);
+#define FA_REC_CASE(S)                                    \
+  if (sw == S) {                                          \
+    if (bm) { FA_REC_MODE(S, kBuildBM) }                  \
+    else if (src) { FA_REC_MODE(S, kBuildCols) }          \
+    else { FA_REC_MODE(S, kBuildContig) }                 \
+  }
+  FA_REC_CASE(4)
+  FA_REC_CASE(8)
+  FA_REC_CASE(16)
+  FA_REC_CASE(32)
+#undef FA_REC_CASE
+#undef FA_REC_MODE
+  if (!kern) return 1;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const int dbg = getenv("FA_SLAB_DEBUG") ? atoi(getenv("FA_SLAB_DEBUG")) : 0;
+  hipLaunchKernelGGL(kern, dim3((unsigned)n_wg), dim3(kSlabThreads), lds, st, roff, ranks, src, ncols, item_map, F1,
+                     n_used, gpre, (const int4*)rec, G, C, wword, out, bm, Wp, bm_rows, dbg);
   FA_LAUNCH_RET();
 }
 

@@ -165,18 +165,24 @@ FA_API int fa_plan_trie(const int32_t* P, int64_t G, int m, const int64_t* ext_o
 //     0 kernel (0 slab, 1 trie)  1 sw  2 cap  3 n_used  4 n_pieces  5 n_witems
 //     6 n_passes  7 d1  8 d2  9 trie reads  10 slab reads  11 emax
 //     12 off item_map  13 off used  14 off gext  15 off gpre  16 off pieces/loc_off
-//     17 off witems  18 total int32 written
+//     17 off witems  18 total int32 written  19 off gpm (slab)  20 off piece records (slab)
 //   passes (int64[3 * maxpass]): slab: (piece begin, piece end, ext base);
 //                                trie: (witem begin, witem end, ext base)
 // Returns 0, 3 (buffer too small), 4 (no slab width fits: use the bitmap kernel).
 // ---------------------------------------------------------------------------
-static int slab_width(int64_t n_used, int64_t C, double lds, int64_t* cap_out, double accb = 4) {
+static int slab_width(int64_t n_used, int64_t C, double lds, int64_t* cap_out, double accb = 4,
+                      double map_lds = 0) {
   for (int sw : {32, 16, 8, 4}) {
-    const int64_t cap = (int64_t)((lds - (double)n_used * (sw + 2) * 8) / accb);
+    // + the LDS copy of the rank -> slab-row map (u16 per frequent item, k_count_slab_rec)
+    const int64_t cap = (int64_t)((lds - (double)n_used * (sw + 2) * 8 - map_lds) / accb);
     if (cap >= std::min<int64_t>(C, 8192) || (sw == 4 && cap >= 1024)) { *cap_out = cap; return sw; }
   }
   return 0;
 }
+
+// LDS bytes of k_count_slab_rec's copy of the rank -> slab-row map (u16 per
+// frequent item; 0 = the map stays in global memory).  count.hip mirrors this.
+static inline int64_t fa_slab_map_lds(int64_t F1) { return F1 <= 8192 ? ((F1 * 2 + 15) & ~(int64_t)15) : 0; }
 
 FA_API int fa_level_plan(const int32_t* Pf, const int64_t* poff, int64_t G, const int64_t* ext_off,
                          const int32_t* ext, int32_t F1, const double* params, int32_t* buf, int64_t buf_cap,
@@ -274,7 +280,7 @@ FA_API int fa_level_plan(const int32_t* Pf, const int64_t* poff, int64_t G, cons
 
   // ---- slab kernel: pieces of <= 8 extensions, passes of <= cap, size-sorted per pass
   int64_t cap = 0;
-  const int sw = slab_width(n_used, C, lds, &cap, accb);
+  const int sw = slab_width(n_used, C, lds, &cap, accb, (double)fa_slab_map_lds(F1));
   if (sw == 0) return 4;
   struct Piece { int64_t g, lo, hi; };
   std::vector<Piece> pcs;
@@ -322,6 +328,39 @@ FA_API int fa_level_plan(const int32_t* Pf, const int64_t* poff, int64_t G, cons
   }
   info[0] = 0; info[1] = sw; info[2] = cap; info[4] = NP; info[6] = npass;
   info[18] = pos + pre_total + 4 * NP;
+  // piece records for k_count_slab_rec: 48 B per piece (16-B aligned), so a piece's
+  // whole description is three 16-B loads with no dependent index chain:
+  //   a = {ext begin (pass-local), n_ext | m << 8 | (m > 12) << 16, prefix ids 0-3 (u16)}
+  //   b = extension ids 0-7 (u16),  c = prefix ids 4-11 (u16), or c.x = gpre offset when m > 12
+  {
+    const int64_t rpos = (info[18] + 3) & ~(int64_t)3;
+    if (rpos + 12 * NP > buf_cap) return 3;
+    int32_t* rec = buf + rpos;
+    const int32_t* gext_all = buf + info[14];
+    auto pk = [](int32_t x, int32_t y) { return (uint32_t)(x & 0xFFFF) | ((uint32_t)(y & 0xFFFF) << 16); };
+    for (int64_t q = 0; q < npass; ++q) {
+      const int64_t base = passes[3 * q + 2];
+      for (int64_t p = passes[3 * q]; p < passes[3 * q + 1]; ++p) {
+        const int32_t lo = loc[2 * p], hi = loc[2 * p + 1];
+        const int32_t mg = gpm[2 * p + 1];
+        const int32_t* pre = gpre + gpm[2 * p];
+        uint32_t* r = reinterpret_cast<uint32_t*>(rec + 12 * p);
+        int32_t ids[12] = {0};
+        for (int t = 0; t < std::min(mg, 12); ++t) ids[t] = pre[t];
+        r[0] = (uint32_t)lo;
+        r[1] = (uint32_t)(hi - lo) | ((uint32_t)mg << 8) | (mg > 12 ? 1u << 16 : 0u);
+        r[2] = pk(ids[0], ids[1]);
+        r[3] = pk(ids[2], ids[3]);
+        int32_t ex8[8] = {0};
+        for (int32_t e = lo; e < hi; ++e) ex8[e - lo] = gext_all[base + e];
+        for (int k = 0; k < 4; ++k) r[4 + k] = pk(ex8[2 * k], ex8[2 * k + 1]);
+        for (int k = 0; k < 4; ++k) r[8 + k] = pk(ids[4 + 2 * k], ids[5 + 2 * k]);
+        if (mg > 12) r[8] = (uint32_t)gpm[2 * p];
+      }
+    }
+    info[20] = rpos;
+    info[18] = rpos + 12 * NP;
+  }
   return 0;
 }
 

@@ -82,6 +82,8 @@ _HIP_SIGS = {
                                    C.c_int, C.c_int, vp]),
     "fa_hip_count_slab": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, vp,
                                     C.c_int, C.c_int, vp, i64, vp, vp, vp, C.c_int]),
+    "fa_hip_count_slab_rec": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, C.c_int, vp, vp, C.c_int, C.c_int, vp, vp,
+                                        C.c_int, C.c_int, vp, i64, vp, vp, C.c_int]),
     "fa_hip_trim_scan_count": (C.c_int, [vp, vp, i64, vp, C.c_int, C.c_int, vp, vp, vp, vp, vp]),
     "fa_hip_trim_emit": (C.c_int, [vp, vp, vp, C.c_int, i64, vp, vp, vp, vp, vp, vp, vp, vp]),
     "fa_hip_compress_wave": (C.c_int, [vp, vp, vp, vp, i64, vp, vp, vp, C.c_int, vp]),

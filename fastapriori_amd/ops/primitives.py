@@ -786,7 +786,7 @@ def level_plan_host(prefix: np.ndarray, ext_off: np.ndarray, ext: np.ndarray, F1
     min_saving = {"auto": _TRIE_MIN_SAVING, "trie": 0.0, "slab": 2.0}[kernel]
     params = np.array([lds_bytes or _LDS_BYTES, min_saving, _TRIE_CONFLICT[16], _TRIE_CONFLICT[8],
                        TRIE_PASS_WEIGHT, TRIE_ROUNDS, TRIE_EMAX, W, 4.0], dtype=np.float64)
-    bound = 2 * F1 + C + G * m + 6 * (G + C // 2 + 2) + (m + 4) * (G + C // 8 + 1) + 16
+    bound = 2 * F1 + C + G * m + 6 * (G + C // 2 + 2) + (m + 16) * (G + C // 8 + 1) + 20
     buf = np.zeros(bound, np.int32)
     passes = np.zeros((G + C + 2, 3), np.int64)
     info = np.zeros(24, np.int64)
@@ -828,7 +828,37 @@ def emulate_level_plan(bits_by_rank: np.ndarray, info, passes, buf, m: int, C: i
     return out
 
 
+def emulate_slab_records(bits_by_rank: np.ndarray, info, passes, buf, C: int) -> np.ndarray:
+    """CPU model of k_count_slab_rec over the 48-B piece records of a slab plan
+    (fa_level_plan info[20]); must equal emulate_level_plan."""
+    used = buf[info[13]:info[13] + int(info[3])]
+    bits = bits_by_rank[used]
+    gpre = buf[info[15]:info[16]]
+    rec = buf[info[20]:info[20] + 12 * int(info[4])].view(np.uint32).reshape(-1, 12)
+    u16 = np.stack([rec & 0xFFFF, rec >> 16], axis=-1).reshape(-1, 24)   # 24 u16 per record
+    out = np.zeros(C, np.int64)
+    for a, b, e0 in passes.tolist():
+        for pi in range(a, b):
+            r = rec[pi]
+            n_ext, m, long_pre = int(r[1] & 0xFF), int((r[1] >> 8) & 0xFF), bool((r[1] >> 16) & 1)
+            if long_pre:
+                ids = gpre[int(r[8]):int(r[8]) + m]
+            else:
+                ids = np.concatenate([u16[pi, 4:8], u16[pi, 16:24]])[:m]
+            p = np.logical_and.reduce(bits[ids])
+            for k in range(n_ext):
+                out[e0 + int(r[0]) + k] += int((p & bits[u16[pi, 8 + k]]).sum())
+    return out
+
+
 LAST_LEVEL_PLAN: dict = {}   # shape of the last count_level call (diagnostics)
+# slab path kernel: k_count_slab_rec (piece records, map in LDS) or the index-chain k_count_slab
+SLAB_REC = os.environ.get("FA_SLAB_REC", "1") == "1"
+
+
+def _slab_map_lds(F1: int) -> int:
+    """LDS bytes of k_count_slab_rec's u16 rank -> slab-row map (plan.cpp fa_slab_map_lds)."""
+    return ((F1 * 2 + 15) & ~15) if F1 <= 8192 else 0
 
 
 def _flat_prefix(prefix: np.ndarray, poff: np.ndarray | None):
@@ -870,7 +900,7 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
     acc16 = False
     params = np.array([_LDS_BYTES, min_saving, _TRIE_CONFLICT[16], _TRIE_CONFLICT[8], TRIE_PASS_WEIGHT,
                        TRIE_ROUNDS, TRIE_EMAX, W, 4.0], dtype=np.float64)
-    bound = 2 * F1 + C + G * m + 6 * (G + C // 2 + 2) + (m + 4) * (G + C // 8 + 1) + 16
+    bound = 2 * F1 + C + G * m + 6 * (G + C // 2 + 2) + (m + 16) * (G + C // 8 + 1) + 20
     on_gpu = dev.type == "cuda"
     stage = pinned_stage("level_plan") if on_gpu else None
     buf = stage.get(4 * bound).view(dtype=_I32) if on_gpu else torch.empty(bound, dtype=_I32)
@@ -899,7 +929,7 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
         stage.event.record()
     base = dbuf.data_ptr()
     passes = passes[:npass]
-    o_im, o_used, o_gext, o_gpre, o_pc, o_wi, o_gpm = (int(info[i]) for i in (12, 13, 14, 15, 16, 17, 19))
+    o_im, o_used, o_gext, o_gpre, o_pc, o_wi, o_gpm, o_rec = (int(info[i]) for i in (12, 13, 14, 15, 16, 17, 19, 20))
     out = torch.zeros(C, dtype=_I32, device=dev)
     bm, bm_rows = None, None
     if npass > 1:
@@ -923,6 +953,14 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
                       base + 4 * o_gpre, m, int(info[7]), int(info[8]), base + 4 * o_pc, base + 4 * (o_wi + 2 * a),
                       b - a, base + 4 * (o_gext + e0), Cq, _p(wword), out.data_ptr() + 4 * e0, sw, n_wg, _p(bm),
                       bm.stride(0) if bm is not None else 0, st, bm_rows, int(acc16))
+        elif SLAB_REC:
+            # piece records (k_count_slab_rec): 48 B per piece, loaded one piece ahead
+            lds = n_used * (sw + 2) * 8 + Cq * accb + _slab_map_lds(F1)
+            n_wg = int(max(wg_floor, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2))))
+            _hip_call("fa_hip_count_slab_rec", _p(roff), _p(ranks), _p(src), ncols, base + 4 * o_im, F1, n_used,
+                      base + 4 * o_gpre, base + 4 * (o_rec + 12 * a), b - a, Cq, _p(wword),
+                      out.data_ptr() + 4 * e0, sw, n_wg, _p(bm), bm.stride(0) if bm is not None else 0, st,
+                      bm_rows, int(acc16))
         else:
             lds = n_used * (sw + 2) * 8 + Cq * accb
             n_wg = int(max(wg_floor, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2))))

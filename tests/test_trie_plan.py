@@ -88,7 +88,7 @@ def test_sharing_reduces_reads_on_deep_levels():
 def test_level_plan_counts(kernel, lds_kb, k):
     # fa_level_plan (one-call planner feeding the GPU level kernels) for both kernels,
     # single- and multi-pass, must reproduce brute-force supports
-    from fastapriori_amd.ops.primitives import emulate_level_plan, level_plan_host
+    from fastapriori_amd.ops.primitives import emulate_level_plan, emulate_slab_records, level_plan_host
     rng = np.random.default_rng(k)
     bits, prev = _level(rng, n_items=16, k=k)
     pidx, eoff, ext = apriori_gen(prev)
@@ -108,11 +108,31 @@ def test_level_plan_counts(kernel, lds_kb, k):
     want = np.array([np.logical_and.reduce(bits[list(P[g]) + [e]]).sum() for g, e in zip(g_of_e, ext)])
     got = emulate_level_plan(bits, info, passes, buf, P.shape[1], ext.size)
     assert np.array_equal(got, want)
+    if info[0] == 0:                 # slab plan: the 48-B piece records of k_count_slab_rec agree
+        assert np.array_equal(emulate_slab_records(bits, info, passes, buf, ext.size), want)
+
+
+@pytest.mark.parametrize("k", [7, 11, 15])
+def test_slab_records_long_prefixes(k):
+    # k_count_slab_rec records hold prefixes of <= 12 ids inline (ids 4-11 in the
+    # third int4) and point into gpre beyond that
+    from fastapriori_amd.ops.primitives import emulate_slab_records, level_plan_host
+    rng = np.random.default_rng(k)
+    bits, prev = _level(rng, n_items=16, n_rows=300, k=k, dens=0.88)
+    pidx, eoff, ext = apriori_gen(prev)
+    if ext.size == 0:
+        pytest.skip("no candidates")
+    P = prev[pidx]
+    rc, info, passes, buf = level_plan_host(P, eoff, ext, bits.shape[0], 5, "slab")
+    assert rc == 0 and info[0] == 0
+    g_of_e = np.repeat(np.arange(pidx.size), np.diff(eoff))
+    want = np.array([np.logical_and.reduce(bits[list(P[g]) + [e]]).sum() for g, e in zip(g_of_e, ext)])
+    assert np.array_equal(emulate_slab_records(bits, info, passes, buf, ext.size), want)
 
 
 def test_level_plan_mixed_prefix_lengths():
     # groups of several levels (different k) in one slab launch: flat prefixes + poff
-    from fastapriori_amd.ops.primitives import emulate_level_plan, level_plan_host
+    from fastapriori_amd.ops.primitives import emulate_level_plan, emulate_slab_records, level_plan_host
     rng = np.random.default_rng(11)
     bits, prev3 = _level(rng, n_items=16, k=4)
     _, prev2 = _level(rng, n_items=16, k=3)
@@ -132,6 +152,7 @@ def test_level_plan_mixed_prefix_lengths():
         want += [np.logical_and.reduce(bits[list(P[g]) + [e]]).sum() for g, e in zip(g_of_e, ex)]
     got = emulate_level_plan(bits, info, passes, buf, 0, ext.size)
     assert np.array_equal(got, np.array(want))
+    assert np.array_equal(emulate_slab_records(bits, info, passes, buf, ext.size), np.array(want))
 
 
 def test_bundled_levels_match_unbundled(monkeypatch):
