@@ -147,7 +147,8 @@ template <int N>
 __global__ __launch_bounds__(256) void k_compress_regs(
     const int64_t* __restrict__ off, const int32_t* __restrict__ items, const int32_t* __restrict__ lut,
     const int32_t* __restrict__ rows, int64_t nrows, const int32_t* __restrict__ kept,
-    const int64_t* __restrict__ roff, int32_t* __restrict__ ranks, int8_t* __restrict__ over_flag) {
+    const int64_t* __restrict__ roff, int32_t* __restrict__ ranks, int8_t* __restrict__ over_flag,
+    uint8_t* __restrict__ bcnt = nullptr, int64_t bld = 0, int nb = 0) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = i < nrows;
   int64_t s = 0, L = 0, x = 0;
@@ -181,6 +182,14 @@ __global__ __launch_bounds__(256) void k_compress_regs(
 #pragma unroll
   for (int j = 0; j < N; ++j)
     if (j < c) ranks[o + j] = (int32_t)a[j];
+  if (bcnt) {
+    // 256-rank block counts of the row (see k_cmp_emit); <= 64 items: no byte carries
+    unsigned long long pc = 0;
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+      if (j < c) pc += 1ull << ((a[j] >> 8) << 3);
+    for (int b = 0; b < nb; ++b) bcnt[(int64_t)b * bld + x] = (uint8_t)(pc >> (8 * b));
+  }
 }
 
 // Tier 1 with LDS staging: a workgroup's 256 kept rows usually come from one
@@ -703,7 +712,8 @@ __global__ __launch_bounds__(256) void k_cmp_emit(const int64_t* __restrict__ of
                                                   const int64_t* __restrict__ pre_items,
                                                   const int64_t* __restrict__ pre_over,
                                                   int32_t* __restrict__ kept_out, int64_t* __restrict__ roff,
-                                                  int32_t* __restrict__ ranks, int32_t* __restrict__ over) {
+                                                  int32_t* __restrict__ ranks, int32_t* __restrict__ over,
+                                                  uint8_t* __restrict__ bcnt, int nb) {
   constexpr int N = kCmpN;
   __shared__ uint32_t buf[kCmpSpan];
   __shared__ int sh[8];
@@ -755,6 +765,17 @@ __global__ __launch_bounds__(256) void k_cmp_emit(const int64_t* __restrict__ of
   }
   const bool mine = kept && L <= N;
   if (mine) bitonic_regs<N>(a);
+  if (bcnt && mine) {
+    // per-row item counts of the pair kernel's 256-rank blocks, bcnt[b * T + row]
+    // (the layout of k_block_counts_w; T = kept rows, the scan total), byte-packed:
+    // a row of <= 16 items never carries into the next block's byte
+    const int64_t bld = pre_rows[gridDim.x];
+    unsigned long long pc = 0;
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+      if (j < c) pc += 1ull << ((a[j] >> 8) << 3);
+    for (int b = 0; b < nb; ++b) bcnt[(int64_t)b * bld + xk] = (uint8_t)(pc >> (8 * b));
+  }
   __syncthreads();   // everyone is done reading the input span
   if (staged && tb <= kCmpSpan) {
     if (mine) {
@@ -770,9 +791,81 @@ __global__ __launch_bounds__(256) void k_cmp_emit(const int64_t* __restrict__ of
       if (j < c) ranks[obase + eb + j] = (int32_t)a[j];
   }
 }
+// Block counts of the rows the emit pass left to later tiers (rows[i] = row id):
+// thread per row over its final ranks (counts need no order).
+__global__ __launch_bounds__(256) void k_block_counts_rows(const int64_t* __restrict__ roff,
+                                                           const int32_t* __restrict__ ranks,
+                                                           const int32_t* __restrict__ rows, int64_t nrows,
+                                                           uint8_t* __restrict__ bcnt, int64_t bld, int nb) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nrows) return;
+  const int64_t x = rows[i];
+  int c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t k = roff[x], e = roff[x + 1]; k < e; ++k) {
+    const int b = ranks[k] >> 8;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) c[q] += b == q;
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    if (q < nb) bcnt[(int64_t)q * bld + x] = (uint8_t)min(c[q], 255);
+}
+
+// bsum[b * nbatch + q] = items of 64-row batch q in block b (rows >= T count 0).
+// A wave takes 16 batches of one block: lane l sums the 16 count bytes of rows
+// 64q + 16(l % 4) .. +16 of batch q = q0 + l / 4 (four dword loads; a block's bytes
+// start at b * bld, so they may be unaligned), then a quad DPP sum per batch.
+__global__ __launch_bounds__(256) void k_block_bsum(const uint8_t* __restrict__ bcnt, int64_t bld, int64_t T,
+                                                    int nb, int64_t nbatch, int64_t* __restrict__ bsum) {
+  const int64_t ng = (nbatch + 15) / 16;
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= nb * ng) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t b = t / ng, q = (t - b * ng) * 16 + (lane >> 2);
+  const int64_t x0 = q * 64 + 16 * (lane & 3);
+  const uint8_t* src = bcnt + b * bld + x0;
+  uint32_t s = 0;
+  if (q < nbatch) {
+    if (x0 + 16 <= T) {
+      uint32_t acc = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint32_t d;
+        __builtin_memcpy(&d, src + 4 * k, 4);
+        acc += (d & 0x00FF00FFu) + ((d >> 8) & 0x00FF00FFu);
+      }
+      s = (acc & 0xFFFFu) + (acc >> 16);
+    } else {
+      for (int k = 0; k < 16; ++k)
+        if (x0 + k < T) s += src[k];
+    }
+  }
+  s += (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+  s += (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+  if ((lane & 3) == 0 && q < nbatch) bsum[b * nbatch + q] = s;
+}
+
 }  // namespace fa
 
 using namespace fa;
+
+FA_API int fa_hip_block_counts_rows(const int64_t* roff, const int32_t* ranks, const int32_t* rows, int64_t nrows,
+                                    uint8_t* bcnt, int64_t bld, int nb, hipStream_t st) {
+  if (nrows <= 0) return 0;
+  if (nb > 8) return 1;
+  hipLaunchKernelGGL(k_block_counts_rows, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, st, roff, ranks, rows,
+                     nrows, bcnt, bld, nb);
+  FA_LAUNCH_RET();
+}
+
+FA_API int fa_hip_block_bsum(const uint8_t* bcnt, int64_t bld, int64_t T, int nb, int64_t* bsum, hipStream_t st) {
+  if (T <= 0) return 0;
+  const int64_t nbatch = (T + 63) / 64;
+  const int64_t ng = (nbatch + 15) / 16;
+  hipLaunchKernelGGL(k_block_bsum, dim3((unsigned)((nb * ng + 3) / 4)), dim3(256), 0, st, bcnt, bld, T, nb,
+                     nbatch, bsum);
+  FA_LAUNCH_RET();
+}
 
 FA_API int fa_hip_histogram(const int32_t* items, int64_t nnz, int32_t V, uint32_t* counts,
                             hipStream_t st) {
@@ -868,6 +961,17 @@ FA_API int fa_hip_compress_regs(int tier, const int64_t* off, const int32_t* ite
   FA_LAUNCH_RET();
 }
 
+// The 64-token tier that also writes the rows' 256-rank block counts (bcnt[b * bld + row]).
+FA_API int fa_hip_compress_regs_bc(const int64_t* off, const int32_t* items, const int32_t* lut, const int32_t* rows,
+                                   int64_t nrows, const int32_t* kept, const int64_t* roff, int32_t* ranks,
+                                   int8_t* over_flag, uint8_t* bcnt, int64_t bld, int nb, hipStream_t st) {
+  if (nrows <= 0) return 0;
+  if (nb < 1 || nb > 8) return 1;
+  hipLaunchKernelGGL(k_compress_regs<64>, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, st, off, items, lut,
+                     rows, nrows, kept, roff, ranks, over_flag, bcnt, bld, nb);
+  FA_LAUNCH_RET();
+}
+
 FA_API int fa_hip_compress_staged(const int64_t* off, const int32_t* items, const int32_t* lut, int64_t T,
                                   const int32_t* kept, const int64_t* roff, int32_t* ranks, int8_t* over_flag,
                                   hipStream_t st) {
@@ -956,9 +1060,10 @@ FA_API int fa_hip_cmp_agg(const int64_t* off, const int32_t* items, const int32_
 
 FA_API int fa_hip_cmp_emit(const int64_t* off, const int32_t* items, const int32_t* lut, int64_t n,
                            const int64_t* pre_rows, const int64_t* pre_items, const int64_t* pre_over, int32_t* kept,
-                           int64_t* roff, int32_t* ranks, int32_t* over, hipStream_t st) {
+                           int64_t* roff, int32_t* ranks, int32_t* over, uint8_t* bcnt, int nb, hipStream_t st) {
   if (n <= 0) return 0;
+  if (bcnt && (nb < 1 || nb > 8)) return 1;
   hipLaunchKernelGGL(k_cmp_emit, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, off, items, lut, n, pre_rows,
-                     pre_items, pre_over, kept, roff, ranks, over);
+                     pre_items, pre_over, kept, roff, ranks, over, bcnt, nb);
   FA_LAUNCH_RET();
 }

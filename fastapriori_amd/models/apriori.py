@@ -448,7 +448,7 @@ class FastApriori:
         if (dev.type == "cuda" and n_rows > 0 and FUSED_COMPRESS
                 and shard.items.numel() <= FUSED_COMPRESS_MEAN_LEN * n_rows):
             # fused two-pass path: kept rows, offsets, sorted ranks and the length histogram
-            kept, roff, ranks, hist_t = ops.compress_rows(shard.offsets, shard.items, lut, F1)
+            kept, roff, ranks, hist_t, bcnt = ops.compress_rows(shard.offsets, shard.items, lut, F1)
             T = kept.numel()
             hist = hist_t.cpu().numpy()
         else:
@@ -460,8 +460,10 @@ class FastApriori:
                 torch.cumsum(cnt[kept.to(torch.int64)].to(torch.int64), 0, out=roff[1:])
             ranks = ops.compress(shard.offsets, shard.items, lut, kept, roff, F1)
             hist = ops.histogram(torch.clamp(cnt, max=255), 256).cpu().numpy() if cnt.numel() else np.zeros(256, np.int64)
+            bcnt = None
         db = {"roff": roff, "ranks": ranks, "T": T, "src": None, "ncols": T, "wword": None, "wrow": None,
-              "bm": None, "W": 0, "F1": F1, "alive": np.ones(F1, dtype=bool), "c1": self._counts1}
+              "bm": None, "W": 0, "F1": F1, "alive": np.ones(F1, dtype=bool), "c1": self._counts1,
+              "bcnt": bcnt}      # 256-item block counts of these rows (pair layout); dropped on re-layout
         # row-length histogram (lengths >= 255 share the last bin): drives the pair
         # cost model, the trimming model and the u8 per-block count guard
         hist[:2] = 0                         # rows with < 2 frequent items are not kept
@@ -475,6 +477,7 @@ class FastApriori:
         db["long_rows"] = bool(g[:, 0].max())
         db["pair_pick"] = None
         if g[:, 1].max():
+            db["bcnt"] = None
             self._dedup(db)
             db.pop("len_hist", None)
         else:
@@ -608,7 +611,7 @@ class FastApriori:
         K = kept.numel()
         if K > 0.9 * db["T"] and nranks.numel() > 0.9 * db["ranks"].numel():
             return   # not worth re-laying out
-        db.update(roff=nroff, ranks=nranks, T=K, bm=None, W=0)
+        db.update(roff=nroff, ranks=nranks, T=K, bm=None, W=0, bcnt=None)
         db["alive"] = np.zeros_like(db["alive"])
         db["alive"][used] = True
         db["len_hist"] = hist.cpu().numpy()
@@ -666,7 +669,8 @@ class FastApriori:
                 ra, rb = int(roff[a].item()), int(roff[b].item())
                 roff, ranks = roff[a:b + 1] - ra, ranks[ra:rb]
                 wrow = wrow[a:b] if wrow is not None else None
-            pc = ops.pair_counts_horizontal(roff, ranks, wrow, F1, db.get("long_rows", True))
+            pc = ops.pair_counts_horizontal(roff, ranks, wrow, F1, db.get("long_rows", True),
+                                            bcnt=db.get("bcnt") if nr == 1 and wrow is None else None)
         self._run_deferred()      # host-only work while the pair kernel runs
         key = (F1, pc.device)
         if key not in _TRIU_CACHE:

@@ -218,11 +218,19 @@ def compress(offsets, items, lut, kept, roff, F1: int | None = None) -> torch.Te
     return ranks[:nnz]
 
 
-def compress_rows(offsets, items, lut, F1: int):
+PAIR_PAD_BATCHES = 3 * 16 + 2   # the pair kernel's pipeline reads up to this many batches past a chunk
+
+
+def compress_rows(offsets, items, lut, F1: int, block_counts: bool = True):
     """Fused two-pass compression (device, short rows; csrc/hip/prep.hip k_cmp_agg /
     k_cmp_emit): returns (kept int32 [T], roff int64 [T+1], ranks int32 [nnz],
-    length histogram int64 [256]) with one host synchronisation.  Rows of more
-    than 16 tokens are finished by the register / wave tiers of ``compress``."""
+    length histogram int64 [256], bcnt) with one host synchronisation.  Rows of
+    more than 16 tokens are finished by the register / wave tiers of ``compress``.
+
+    bcnt (block_counts and F1 <= 2048, else None): uint8 [nb * T + pad], the
+    per-row item counts of 256-rank blocks that the pair kernel's blocked layout
+    needs (pair_counts_horizontal), written by the emit pass while the sorted row
+    is in registers instead of by a separate pass over the ranks."""
     dev = items.device
     n = offsets.numel() - 1
     nwg = (n + 255) // 256
@@ -239,16 +247,27 @@ def compress_rows(offsets, items, lut, F1: int):
     roff[0] = 0
     ranks = torch.empty(max(items.numel(), 1), dtype=_I32, device=dev)
     over = torch.empty(max(n, 1), dtype=_I32, device=dev)
+    nb = (F1 + 255) // 256
+    bcnt = None
+    if block_counts and 1 <= nb <= 8:
+        bcnt = torch.empty(nb * max(n, 1) + PAIR_PAD_BATCHES * 64 + 64, dtype=torch.uint8, device=dev)
     _hip_call("fa_hip_cmp_emit", _p(offsets), _p(items), _p(lut), n, _p(pre[0]), _p(pre[1]), _p(pre[2]), _p(kept),
-              _p(roff), _p(ranks), _p(over), st)
+              _p(roff), _p(ranks), _p(over), _p(bcnt), nb, st)
     sizes = pre[:, -1].cpu().tolist()
     T, nnz, no = int(sizes[0]), int(sizes[1]), int(sizes[2])
     kept, roff, ranks = kept[:T], roff[:T + 1], ranks[:nnz]
+    if bcnt is not None:
+        bcnt = bcnt[:nb * T + PAIR_PAD_BATCHES * 64 + 64]
+        bcnt[nb * T:].zero_()
     if no:
         over = over[:no]
         flag2 = torch.empty(no, dtype=torch.int8, device=dev)
-        _hip_call("fa_hip_compress_regs", 64, _p(offsets), _p(items), _p(lut), _p(over), no, _p(kept), _p(roff),
-                  _p(ranks), _p(flag2), st)
+        if bcnt is not None:
+            _hip_call("fa_hip_compress_regs_bc", _p(offsets), _p(items), _p(lut), _p(over), no, _p(kept), _p(roff),
+                      _p(ranks), _p(flag2), _p(bcnt), T, nb, st)
+        else:
+            _hip_call("fa_hip_compress_regs", 64, _p(offsets), _p(items), _p(lut), _p(over), no, _p(kept), _p(roff),
+                      _p(ranks), _p(flag2), st)
         over2 = over[torch.nonzero(flag2).flatten()].contiguous()
         n2 = over2.numel()
         if n2 and F1 <= COMPRESS_WAVE_MAX_F1:
@@ -262,7 +281,9 @@ def compress_rows(offsets, items, lut, F1: int):
             n3 = int(n_over3.item())
             if n3:
                 _compress_torch(offsets, items, lut, kept, roff, ranks, over3[:n3])
-    return kept, roff, ranks, hist.sum(0, dtype=_I64)
+        if bcnt is not None and n2:       # rows of > 64 tokens, finished by the later tiers
+            _hip_call("fa_hip_block_counts_rows", _p(roff), _p(ranks), _p(over2), n2, _p(bcnt), T, nb, st)
+    return kept, roff, ranks, hist.sum(0, dtype=_I64), bcnt
 
 
 def _compress_torch(offsets, items, lut, kept, roff, ranks, rows):
@@ -334,13 +355,15 @@ def build_bitmaps(roff, ranks, src, ncols: int, F1: int, item_map=None, used=Non
     return bm[:F1], W
 
 
-def pair_counts_horizontal(roff, ranks, wrow, F1: int, long_rows: bool = True) -> torch.Tensor:
+def pair_counts_horizontal(roff, ranks, wrow, F1: int, long_rows: bool = True, bcnt=None) -> torch.Tensor:
     """Pair supports from the compressed rows -> int64 [F1, F1] (upper triangle).
 
     Device path: per-row block counts + local-rank bytes (blocked layout), then
     the 256 x 256 packed-u16 tile kernel for unit-weight rows, or 128 x 128 u32
     tiles with row weights.  long_rows: some row may hold >= 256 items, which
-    would overflow a u8 count of a 256-item block -> 128-item blocks.
+    would overflow a u8 count of a 256-item block -> 128-item blocks.  bcnt: the
+    256-item block counts of these rows from compression (compress_rows), which
+    replace the counting pass.
     """
     T = roff.numel() - 1
     dev = ranks.device
@@ -354,15 +377,20 @@ def pair_counts_horizontal(roff, ranks, wrow, F1: int, long_rows: bool = True) -
             # cnt / base are padded past their ends: the pair kernel's software
             # pipeline loads up to 3 x 16 batches past a chunk unconditionally (those
             # values are never processed; padded bases must be valid lr offsets)
-            pad_b = 3 * 16 + 2
-            cnt = torch.empty(nb * T + pad_b * 64, dtype=torch.uint8, device=dev)
-            cnt[nb * T:].zero_()
+            pad_b = PAIR_PAD_BATCHES
             bsum = torch.empty(nb * nbatch, dtype=_I64, device=dev)
-            _hip_call("fa_hip_block_counts", _p(roff), _p(ranks), T, F1, _p(cnt), _p(bsum), pb, st)
+            if bcnt is not None and pb == 256 and bcnt.numel() >= nb * T + pad_b * 64:
+                cnt = bcnt
+                _hip_call("fa_hip_block_bsum", _p(cnt), T, T, nb, _p(bsum), st)
+            else:
+                cnt = torch.empty(nb * T + pad_b * 64, dtype=torch.uint8, device=dev)
+                cnt[nb * T:].zero_()
+                _hip_call("fa_hip_block_counts", _p(roff), _p(ranks), T, F1, _p(cnt), _p(bsum), pb, st)
             base = torch.zeros(nb * nbatch + pad_b, dtype=_I64, device=dev)
             torch.cumsum(bsum, 0, out=base[:nb * nbatch])
-            total = int(base[nb * nbatch - 1].item())
             base[:nb * nbatch] -= bsum
+            # every rank lands in exactly one block: the layout holds all of them (no readback)
+            total = int(ranks.numel())
             lr = torch.empty(total + 1024, dtype=torch.uint8, device=dev)   # pad: aligned dword staging reads
             _hip_call("fa_hip_block_scatter", _p(roff), _p(ranks), T, F1, _p(cnt), _p(base), _p(lr), pb, st)
             if pb == 256:

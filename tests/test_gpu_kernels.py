@@ -461,10 +461,29 @@ def test_compress_rows_fused(n, max_len, long_rows):
     off, items, lut, F1 = _prep(n=n, V=700, max_len=max_len, seed=n, long_rows=long_rows)
     cnt, kept, roff = _compress_inputs(off, items, lut)
     ref = ops.compress(off, items, lut, kept, roff)
-    gk, groff, granks, ghist = ops.compress_rows(off.to(DEV), items.to(DEV), lut.to(DEV), F1)
+    gk, groff, granks, ghist, bcnt = ops.compress_rows(off.to(DEV), items.to(DEV), lut.to(DEV), F1)
     assert torch.equal(kept, gk.cpu()) and torch.equal(roff, groff.cpu()) and torch.equal(ref, granks.cpu())
     h = torch.bincount(torch.clamp(cnt[cnt >= 2], max=255).long(), minlength=256)
     assert torch.equal(h, ghist.cpu())
+    # 256-rank block counts written by the emit pass (+ the overflow-row fixup) vs the ranks
+    T, nb = gk.numel(), (F1 + 255) // 256
+    r = ref.long()
+    row = torch.repeat_interleave(torch.arange(T), (roff[1:] - roff[:-1]).long())
+    want = torch.zeros(nb, T, dtype=torch.long)
+    want.index_put_((r >> 8, row), torch.ones_like(r), accumulate=True)
+    got = bcnt.cpu()[:nb * T].view(nb, T).long()
+    assert torch.equal(got, want.clamp(max=255))
+
+
+@pytest.mark.parametrize("long_rows", [0, 12])
+def test_pair_counts_with_compress_block_counts(long_rows):
+    # the pair layout built from the emit pass's block counts == the counting pass
+    off, items, lut, F1 = _prep(n=90000, V=900, max_len=22, seed=5, long_rows=long_rows)
+    kept, roff, ranks, _, bcnt = ops.compress_rows(off.to(DEV), items.to(DEV), lut.to(DEV), F1)
+    assert bcnt is not None
+    a = ops.pair_counts_horizontal(roff, ranks, None, F1, long_rows=False, bcnt=bcnt)
+    b = ops.pair_counts_horizontal(roff, ranks, None, F1, long_rows=False)
+    assert torch.equal(a.cpu(), b.cpu()) and int(a.sum()) > 0
 
 
 @pytest.mark.parametrize("k", [3, 4, 6])
