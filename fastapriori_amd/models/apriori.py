@@ -72,7 +72,12 @@ class _Deferred:
         if not self.done:
             self.value, self.done = self.fn(), True
         return self.value
-BUNDLE_DFS = os.environ.get("FA_BUNDLE_DFS", "1") == "1"
+
+
+# depth-2 prefix reuse for bundles (k_count_slab<kDfs>): off by default since the
+# record-driven slab kernel (k_count_slab_rec) counts the T10I4D100M bundle 5-12
+# faster (A/B on MI355X: 48.1-48.9 vs 49.5 ms per run)
+BUNDLE_DFS = os.environ.get("FA_BUNDLE_DFS", "0") == "1"
 # k = 2 across ranks: triangles of at least this many pairs are reduce-scattered and
 # thresholded per slice (Comm.reduce_scatter_select) instead of all-reduced
 PAIR_RS_MIN = int(os.environ.get("FA_PAIR_RS_MIN", str(1 << 15)))

@@ -302,6 +302,7 @@ def test_bundle_dfs_matches_slab_and_cpu(monkeypatch, n, ms):
     monkeypatch.setattr(ops.primitives, "count_bundle_dfs",
                         lambda *a, **k: seen.append(1) or real(*a, **k))
     monkeypatch.setattr(ap, "BUNDLE_DFS_MIN_M", 2)        # every bundle
+    monkeypatch.setattr(ap, "BUNDLE_DFS", True)           # (opt-in: FA_BUNDLE_DFS=1)
     a = FastApriori(ms, config=MinerConfig(min_support=ms, dedup="off")).run(shg).as_dict()
     assert seen, "no bundle took the DFS kernel"
     monkeypatch.setattr(ap, "BUNDLE_DFS", False)
