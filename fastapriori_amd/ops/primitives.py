@@ -82,7 +82,12 @@ def pinned_stage(key: str) -> _PinnedStage:
 
 
 def _hip_call(name: str, *args) -> None:
-    rc = getattr(_native.hip(), name)(*args)
+    fn = getattr(_native.hip(), name)
+    # ctypes passes surplus arguments as C varargs: a binding that lags its C signature
+    # would silently truncate pointers, so the count must match
+    if fn.argtypes is not None and len(args) != len(fn.argtypes):
+        raise TypeError(f"{name}: {len(args)} arguments for a {len(fn.argtypes)}-argument binding")
+    rc = fn(*args)
     _native.check(rc, name)
 
 
