@@ -670,6 +670,48 @@ __device__ __forceinline__ bool cmp_stage(uint32_t* buf, const int32_t* __restri
 
 constexpr int kCmpN = 16;          // rows of <= kCmpN tokens are sorted by k_cmp_emit
 constexpr int kCmpStripes = 64;    // histogram copies
+// Rows of kCmpN < L <= kCmpMid tokens in a staged span are sorted by k_cmp_emit too,
+// with wave-wide bitonic networks on the span already in LDS (rows of <= 32 tokens
+// two per network, one per 32-lane half) -- at most kCmpMidPerWave per wave, the
+// rest go to the overflow tiers.  (The thread-per-row 64-token tier,
+// k_compress_regs<64>, gathers every such row again from HBM: 1.6-1.7 ms per
+// T10I4D100M run.)
+constexpr int kCmpMid = 64;
+constexpr int kCmpMidPerWave = 8;
+
+// the same rows in k_cmp_agg and k_cmp_emit (their overflow counts must agree)
+__device__ __forceinline__ bool cmp_mid(bool kept, int64_t L, bool staged) {
+  const bool cand = kept && staged && L > kCmpN && L <= kCmpMid;
+  const unsigned long long m = __ballot(cand);
+  return cand && __popcll(m & (lanes_le_mask() >> 1)) < kCmpMidPerWave;
+}
+
+// Two ascending bitonic sorts at once (independent exchange chains interleave):
+// one value per lane of a and of b; KMAX = 64 sorts each across the wave, 32 sorts
+// each 32-lane half on its own (the last merge stage ascends in both halves).
+// (DPP / ds_swizzle exchanges instead of ds_bpermute measured no faster: 3.9 vs 3.8 ms)
+template <int KMAX>
+__device__ __forceinline__ void wave_sort2(uint32_t& a, uint32_t& b) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 2; k <= KMAX; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const uint32_t oa = (uint32_t)__shfl_xor((int)a, j, 64);
+      const uint32_t ob = (uint32_t)__shfl_xor((int)b, j, 64);
+      const bool up = k == KMAX || (lane & k) == 0;
+      const bool keep_min = up == ((lane & j) == 0);
+      a = keep_min ? min(a, oa) : max(a, oa);
+      b = keep_min ? min(b, ob) : max(b, ob);
+    }
+  }
+}
+
+// the i-th set bit of a wave-uniform mask (i < popcount)
+__device__ __forceinline__ int nth_bit(unsigned long long m, int i) {
+  for (; i > 0; --i) m &= m - 1;
+  return __builtin_ctzll(m);
+}
 
 __global__ __launch_bounds__(256) void k_cmp_agg(const int64_t* __restrict__ off, const int32_t* __restrict__ items,
                                                  const int32_t* __restrict__ lut, int64_t n,
@@ -693,7 +735,8 @@ __global__ __launch_bounds__(256) void k_cmp_agg(const int64_t* __restrict__ off
   int ea, eb, ta, tb;
   cmp_block_scan2(kept, kept ? c : 0, ea, eb, ta, tb, sh);
   if (kept) atomicAdd(&lh[min(c, 255)], 1u);
-  const unsigned long long ob = __ballot(kept && e - s > kCmpN);
+  const bool mid = cmp_mid(kept, e - s, staged);
+  const unsigned long long ob = __ballot(kept && e - s > kCmpN && !mid);
   __shared__ int ov_w[4];
   if ((threadIdx.x & 63) == 0) ov_w[threadIdx.x >> 6] = __popcll(ob);
   __syncthreads();
@@ -742,7 +785,8 @@ __global__ __launch_bounds__(256) void k_cmp_emit(const int64_t* __restrict__ of
     }
   }
   const int kept = c >= 2;
-  const int ov = kept && L > N;
+  const bool mid = cmp_mid(kept, L, staged);
+  const int ov = kept && L > N && !mid;
   int ea, eb, ta, tb;
   cmp_block_scan2(kept, kept ? c : 0, ea, eb, ta, tb, sh);
   // overflow rows go to their slot of the scanned per-workgroup counts (no atomics:
@@ -776,12 +820,78 @@ __global__ __launch_bounds__(256) void k_cmp_emit(const int64_t* __restrict__ of
       if (j < c) pc += 1ull << ((a[j] >> 8) << 3);
     for (int b = 0; b < nb; ++b) bcnt[(int64_t)b * bld + xk] = (uint8_t)(pc >> (8 * b));
   }
+  // mid rows (staged, kCmpN < L <= 64): wave-wide bitonic sorts on the input span
+  // while it is still in LDS.  Slots: rows of <= 32 tokens two per slot (one per
+  // 32-lane half), then longer rows one per slot; slots are sorted two at a time.
+  // Lane l of a slot holds element l (l & 31 in halves) of its row.
+  const int lane = threadIdx.x & 63;
+  const unsigned long long m32 = __ballot(mid && L <= 32), m64 = __ballot(mid && L > 32);
+  const int n32 = __popcll(m32), s32 = (n32 + 1) >> 1, nslot = s32 + __popcll(m64);
+  // the row (lane id in the wave) this lane holds in slot t, -1: none
+  auto slot_row = [&](int t) -> int {
+    if (t < s32) {
+      const int i = 2 * t + (lane >> 5);
+      return i < n32 ? nth_bit(m32, i) : -1;
+    }
+    return t < nslot ? nth_bit(m64, t - s32) : -1;
+  };
+  uint32_t midv[kCmpMidPerWave];
+#pragma unroll
+  for (int t = 0; t < kCmpMidPerWave; ++t) {
+    midv[t] = 0xFFFFFFFFu;
+    if (t < nslot) {                             // wave-uniform: every lane takes part in the shuffles
+      const int rw = slot_row(t);
+      const int src = rw < 0 ? 0 : rw;
+      const int idx = t < s32 ? (lane & 31) : lane;
+      const int rs = __shfl((int)(s - base), src, 64);
+      const int rl = __shfl((int)L, src, 64);
+      if (rw >= 0 && idx < rl) midv[t] = buf[rs + idx];
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < kCmpMidPerWave; t += 2) {
+    if (t < nslot) {
+      if (t + 1 < s32) {
+        wave_sort2<32>(midv[t], midv[t + 1]);
+      } else if (t >= s32) {
+        wave_sort2<64>(midv[t], midv[t + 1]);
+      } else {                                   // slot t: halves; slot t + 1 (if any): a long row
+        uint32_t none = 0xFFFFFFFFu;
+        wave_sort2<32>(midv[t], none);
+        if (t + 1 < nslot) wave_sort2<64>(midv[t + 1], none);
+      }
+    }
+  }
   __syncthreads();   // everyone is done reading the input span
   if (staged && tb <= kCmpSpan) {
     if (mine) {
 #pragma unroll
       for (int j = 0; j < N; ++j)
         if (j < c) buf[eb + j] = a[j];
+    }
+    {
+      // mid rows into the staged output (their rows are always staged), and their block counts
+      const int64_t bld = bcnt ? pre_rows[gridDim.x] : 0;
+#pragma unroll
+      for (int t = 0; t < kCmpMidPerWave; ++t) {
+        if (t < nslot) {                         // wave-uniform
+          const int rw = slot_row(t);
+          const int src = rw < 0 ? 0 : rw;
+          const int idx = t < s32 ? (lane & 31) : lane;
+          const int rc = __shfl(c, src, 64), reb = __shfl(eb, src, 64);
+          const int rxk = __shfl((int)xk, src, 64);
+          const bool in = rw >= 0 && idx < rc;
+          if (in) buf[reb + idx] = midv[t];
+          if (bcnt) {
+            const unsigned long long half =
+                t < s32 ? ((lane >> 5) ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull) : ~0ull;
+            for (int b = 0; b < nb; ++b) {
+              const int cb = __popcll(__ballot(in && (int)(midv[t] >> 8) == b) & half);
+              if (rw >= 0 && idx == 0) bcnt[(int64_t)b * bld + rxk] = (uint8_t)cb;
+            }
+          }
+        }
+      }
     }
     __syncthreads();
     for (int i = threadIdx.x; i < tb; i += blockDim.x) ranks[obase + i] = (int32_t)buf[i];
