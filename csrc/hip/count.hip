@@ -1610,12 +1610,15 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
 // Work item w = pieces [witems[w].x, witems[w].y); piece = (gpre offset of its
 // prefix row, ext begin, ext end, flags): bit 1 = recompute P2 from P1, bit 0 =
 // recompute p from P2.  The first piece of a work item recomputes everything.
+// Pieces arrive as 32-B records (plan.cpp fa_trie_records: flags, ext range,
+// the first four extension ids and the prefix ids past D1, all inline), and the
+// next piece's record is loaded while the current one is counted.
 // ---------------------------------------------------------------------------
 template <int SW, bool kWeighted, int kBuild, bool kAcc16 = false>
 __global__ __launch_bounds__(kSlabThreads) void k_count_trie(
     const int64_t* __restrict__ roff, const int32_t* __restrict__ ranks, const int32_t* __restrict__ src,
     int64_t ncols, const int32_t* __restrict__ item_map, int n_used, const int32_t* __restrict__ gpre, int m,
-    int D1, int D2, const int4* __restrict__ pieces, const int2* __restrict__ witems, int NW,
+    int D1, int D2, const int4* __restrict__ rec, const int2* __restrict__ witems, int NW,
     const int32_t* __restrict__ gext, int C, const int32_t* __restrict__ wword, uint32_t* __restrict__ out,
     const uint64_t* __restrict__ bm, int64_t Wp, const int32_t* __restrict__ bm_rows, int acc16) {
   constexpr int NQ = (SW / 2) / 2 < FA_TRIE_NQ ? (SW / 2) / 2 : FA_TRIE_NQ;   // uint4 per lane (NQ = 2: ~90 VGPRs)
@@ -1728,8 +1731,8 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_trie(
           s += (uint32_t)(__popc(p[q].x & v[q].x) + __popc(p[q].y & v[q].y)) * wt[2 * q] +
                (uint32_t)(__popc(p[q].z & v[q].z) + __popc(p[q].w & v[q].w)) * wt[2 * q + 1];
         } else {
-          s += __popc(p[q].x & v[q].x) + __popc(p[q].y & v[q].y) + __popc(p[q].z & v[q].z) +
-               __popc(p[q].w & v[q].w);
+          s = bcnt_acc(p[q].x & v[q].x, s); s = bcnt_acc(p[q].y & v[q].y, s);
+          s = bcnt_acc(p[q].z & v[q].z, s); s = bcnt_acc(p[q].w & v[q].w, s);
         }
       }
       return s;
@@ -1741,46 +1744,103 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_trie(
       if (LPP >= 8) s += (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0x141, 0xf, 0xf, false);    // half mirror
       return s;
     };
+    // AND of the slab rows whose ids are u16 slots [j0, j1) of r (record ids; j0, j1
+    // are uniform, so the guards are scalar branches)
+    auto and_ids = [&](uint4 (&a)[NQ], const int4& r, int j0, int j1) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (j >= j0 && j < j1) {
+          const int u = u16_at(r, j), x = (u << 1) & (RS - 1);
+          const uint4* ru = lds4 + (size_t)u * RS;
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) {
+            const uint4 v = ru[off[q] ^ x];
+            a[q].x &= v.x; a[q].y &= v.y; a[q].z &= v.z; a[q].w &= v.w;
+          }
+        }
+      }
+    };
+    // UE extension rows per step (UE * NQ independent slab reads in flight per lane;
+    // UE = 4 at NQ = 2, 2 at NQ = 4 -- the same registers)
+    constexpr int UE = 2;
+    constexpr int R = NQ >= 4 ? 2 : 4;   // extensions taken from the record
     for (int w = grp; w < NW; w += NGRP) {
       const int2 wi = witems[w];
+      // piece records (fa_trie_records): this piece's, and the next one's in flight
+      int4 ra = rec[2 * wi.x], rb = rec[2 * wi.x + 1];
       uint4 P1[NQ], P2[NQ], p[NQ];
 #pragma unroll
       for (int q = 0; q < NQ; ++q) P1[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
-      and_rows(P1, gpre + pieces[wi.x].x, 0, D1);
+      and_rows(P1, gpre + ra.y, 0, D1);
 #pragma unroll
       for (int q = 0; q < NQ; ++q) { P2[q] = P1[q]; p[q] = P1[q]; }
       for (int pi = wi.x; pi < wi.y; ++pi) {
-        const int4 d = pieces[pi];
-        const int32_t* it = gpre + d.x;
-        if (d.w & 2) {
-#pragma unroll
-          for (int q = 0; q < NQ; ++q) P2[q] = P1[q];
-          and_rows(P2, it, D1, D2);
-        }
-        if (d.w & 1) {
-#pragma unroll
-          for (int q = 0; q < NQ; ++q) p[q] = P2[q];
-          and_rows(p, it, D2, m);
-        }
-        int e = d.y;
-        // UE extension rows per step (UE * NQ independent slab reads in flight per lane;
-        // UE = 4 at NQ = 2, 2 at NQ = 4 -- the same registers).  The next step's ids are
-        // loaded one step ahead (an unconditional load at a clamped index), so the
-        // global latency is not exposed at every step.
-        constexpr int UE = NQ >= 4 ? 2 : 4;
+        const int pn = pi + 1 < wi.y ? pi + 1 : pi;
+        const int4 na = rec[2 * pn], nb = rec[2 * pn + 1];
+        const int flg = (ra.x >> 23) & 3;
+        const int e0 = ra.x & 0x1FFFF, n_ext = (ra.x >> 17) & 63;
+        const int ez = e0 + n_ext;
+        // ids past the record's first UE: requested now, used after the prefix ANDs
         int nx[UE];
+        {
+          const int eb = min(e0 + R, max(ez - 1, e0));
 #pragma unroll
-        for (int k = 0; k < UE; ++k) nx[k] = 0;
-        if (e + UE <= d.z) {
-#pragma unroll
-          for (int k = 0; k < UE; ++k) nx[k] = gext[e + k];
+          for (int k = 0; k < UE; ++k) nx[k] = gext[min(eb + k, max(ez - 1, e0))];
         }
-        for (; e + UE <= d.z; e += UE) {
+        if (!((ra.x >> 25) & 1)) {
+          if (flg & 2) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) P2[q] = P1[q];
+            and_ids(P2, rb, 0, D2 - D1);
+          }
+          if (flg & 1) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) p[q] = P2[q];
+            and_ids(p, rb, D2 - D1, m - D1);
+          }
+        } else {
+          const int32_t* it = gpre + ra.y;
+          if (flg & 2) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) P2[q] = P1[q];
+            and_rows(P2, it, D1, D2);
+          }
+          if (flg & 1) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) p[q] = P2[q];
+            and_rows(p, it, D2, m);
+          }
+        }
+        // extensions 0..R-1 from the record, two rows per step (an odd count reads
+        // one padding row: id 0, never accumulated)
+#pragma unroll
+        for (int k0 = 0; k0 < R; k0 += 2) {
+          if (k0 < n_ext) {
+            uint4 v[2][NQ];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+              const int u = k0 + k < 2 ? ((k0 + k) ? (int)((uint32_t)ra.z >> 16) : (ra.z & 0xFFFF))
+                                        : ((k0 + k) == 3 ? (int)((uint32_t)ra.w >> 16) : (ra.w & 0xFFFF));
+              const int xk = (u << 1) & (RS - 1);
+              const uint4* rk = lds4 + (size_t)u * RS;
+#pragma unroll
+              for (int q = 0; q < NQ; ++q) v[k][q] = rk[off[q] ^ xk];
+            }
+            const uint32_t s0 = lanes_sum(dot(p, v[0]));
+            const uint32_t s1 = lanes_sum(dot(p, v[1]));
+            if (t == 0) {
+              acc_add(e0 + k0, s0);
+              if (k0 + 1 < n_ext) acc_add(e0 + k0 + 1, s1);
+            }
+          }
+        }
+        int e = e0 + R;
+        for (; e + UE <= ez; e += UE) {
           int u[UE];
 #pragma unroll
           for (int k = 0; k < UE; ++k) u[k] = nx[k];
           {
-            const int ep = min(e + UE, d.z - UE);
+            const int ep = min(e + UE, ez - UE);
 #pragma unroll
             for (int k = 0; k < UE; ++k) nx[k] = gext[ep + k];
           }
@@ -1800,7 +1860,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_trie(
             for (int k = 0; k < UE; ++k) acc_add(e + k, sk[k]);
           }
         }
-        for (; e < d.z; ++e) {
+        for (; e < ez; ++e) {
           const int u0 = gext[e], x0 = (u0 << 1) & (RS - 1);
           const uint4* r0 = lds4 + (size_t)u0 * RS;
           uint4 v0[NQ];
@@ -1809,6 +1869,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_trie(
           const uint32_t s0 = lanes_sum(dot(p, v0));
           if (t == 0) acc_add(e, s0);
         }
+        ra = na; rb = nb;
       }
     }
   }

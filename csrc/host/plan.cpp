@@ -153,6 +153,46 @@ FA_API int fa_plan_trie(const int32_t* P, int64_t G, int m, const int64_t* ext_o
   return 0;
 }
 
+// Piece records for k_count_trie: 32 B per piece (8 int32), so a piece is two
+// 16-B loads with no dependent index chain and the kernel loads the next piece's
+// record while it counts the current one.  (A piece used to cost three
+// serialised global latencies: its descriptor, then its prefix ids, then its
+// first extension ids.)
+//   a.x = ext begin (pass-local, bits 0-16) | n_ext << 17 (6 bits) | flags << 23
+//         (2 bits) | long << 25 (prefix ids not inline: read gpre)
+//   a.y = gpre offset of the piece's prefix row
+//   a.z, a.w = extension ids 0-3 (u16 slab rows)
+//   b   = prefix ids D1 .. m-1 (u16 slab rows, <= 8 of them; else long)
+// rec must hold 8 * n_pieces int32 and be 16-B aligned.  Returns 0, or 2 when a
+// field does not fit its bits.
+FA_API int fa_trie_records(const int32_t* pieces, const int32_t* witems, const int64_t* passes, int64_t npass,
+                           const int32_t* gpre, const int32_t* gext, int m, int d1, int32_t* rec) {
+  auto pk = [](int32_t x, int32_t y) { return (uint32_t)(x & 0xFFFF) | ((uint32_t)(y & 0xFFFF) << 16); };
+  const bool inl = m - d1 <= 8;
+  for (int64_t q = 0; q < npass; ++q) {
+    const int64_t base = passes[3 * q + 2];
+    for (int64_t w = passes[3 * q]; w < passes[3 * q + 1]; ++w) {
+      for (int64_t p = witems[2 * w]; p < witems[2 * w + 1]; ++p) {
+        const int32_t* pc = pieces + 4 * p;
+        const int32_t lo = pc[1], n = pc[2] - pc[1];
+        if (lo < 0 || lo >= (1 << 17) || n < 0 || n >= 64) return 2;
+        uint32_t* r = reinterpret_cast<uint32_t*>(rec + 8 * p);
+        int32_t ex4[4] = {0, 0, 0, 0};
+        for (int32_t k = 0; k < std::min<int32_t>(n, 4); ++k) ex4[k] = gext[base + lo + k];
+        r[0] = (uint32_t)lo | ((uint32_t)n << 17) | ((uint32_t)(pc[3] & 3) << 23) | (inl ? 0u : 1u << 25);
+        r[1] = (uint32_t)pc[0];
+        r[2] = pk(ex4[0], ex4[1]);
+        r[3] = pk(ex4[2], ex4[3]);
+        int32_t ids[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (inl)
+          for (int t = d1; t < m; ++t) ids[t - d1] = gpre[pc[0] + t];
+        for (int k = 0; k < 4; ++k) r[4 + k] = pk(ids[2 * k], ids[2 * k + 1]);
+      }
+    }
+  }
+  return 0;
+}
+
 // ---------------------------------------------------------------------------
 // One-call level planner: everything the level kernels need, computed in C++
 // and written into one (pinned) int32 buffer so the driver issues a single
@@ -271,8 +311,15 @@ FA_API int fa_level_plan(const int32_t* Pf, const int64_t* poff, int64_t G, cons
         info[7] = tinfo[3]; info[8] = tinfo[4]; info[11] = emax;
         info[15] = o_gpre; info[16] = o_gpre + G * m; info[17] = o_gpre + G * m + 4 * np;
         pos = o_gpre + G * m + 4 * np + 2 * nw;
-        info[18] = pos;
         for (int64_t q = 0; q < 3 * tinfo[2]; ++q) passes[q] = pas[q];
+        // 32-B piece records (fa_trie_records), 16-B aligned
+        pos = (pos + 3) & ~(int64_t)3;
+        if (!need(8 * np)) return 3;
+        if (fa_trie_records(pieces, pieces + 4 * np, passes, tinfo[2], gpre, gext, m, (int)tinfo[3], buf + pos))
+          return 5;
+        info[20] = pos;
+        pos += 8 * np;
+        info[18] = pos;
         return 0;
       }
     }

@@ -43,6 +43,7 @@ _HOST_SIGS = {
     "fa_level_plan": (C.c_int, [vp, vp, i64, vp, vp, i32, vp, vp, i64, vp, i64, vp]),
     "fa_plan_dfs": (C.c_int, [C.c_int, vp, vp, vp, vp, vp, vp, vp, i32, C.c_int, vp, i64, vp]),
     "fa_plan_trie": (C.c_int, [vp, i64, C.c_int, vp, i64, i64, C.c_int, C.c_int, vp, vp, vp, i64, vp]),
+    "fa_trie_records": (C.c_int, [vp, vp, vp, i64, vp, vp, C.c_int, C.c_int, vp]),
     "fa_rules_build": (vp, [vp, vp, vp, C.c_int, vp, C.c_int, vp]),
     "fa_rules_nante": (i64, [vp]),
     "fa_rules_nstats": (i64, [vp]),

@@ -107,3 +107,20 @@ def plan_trie(prefix: np.ndarray, ext_off: np.ndarray, emax: int, cap: int, d1: 
     npc, nw, npass = int(info[0]), int(info[1]), int(info[2])
     return TriePlan(pieces[:npc], witems[:nw], passes[:npass], int(info[3]), int(info[4]), int(info[5]),
                     int(info[6]))
+
+
+def trie_records(plan: TriePlan, gpre: np.ndarray, gext: np.ndarray, m: int) -> np.ndarray:
+    """32-B piece records of k_count_trie (plan.cpp fa_trie_records): int32 [n_pieces, 8].
+    gpre: int32 [G, m] slab-row ids of the prefixes; gext: int32 [C] of the extensions."""
+    pieces = np.ascontiguousarray(plan.pieces, dtype=np.int32)
+    witems = np.ascontiguousarray(plan.witems, dtype=np.int32)
+    passes = np.ascontiguousarray(plan.passes, dtype=np.int64)
+    gp = np.ascontiguousarray(gpre, dtype=np.int32)
+    ge = np.ascontiguousarray(gext, dtype=np.int32)
+    rec = np.zeros((max(pieces.shape[0], 1), 8), dtype=np.int32)
+    rc = _native.host().fa_trie_records(pieces.ctypes.data, witems.ctypes.data, passes.ctypes.data,
+                                        passes.shape[0], gp.ctypes.data, ge.ctypes.data, m, plan.d1,
+                                        rec.ctypes.data)
+    if rc != 0:
+        raise RuntimeError(f"fa_trie_records failed ({rc})")
+    return rec[:pieces.shape[0]]

@@ -748,7 +748,7 @@ def count_level_trie(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, 
     any LDS slab, or (min_saving > 0) when the plan's slab-row reads exceed
     min_saving x those of the thread-per-group slab kernel (pieces of <= 8).
     """
-    from .host import plan_trie
+    from .host import plan_trie, trie_records
     dev = ranks.device
     C = int(ext.size)
     if C == 0:
@@ -773,13 +773,15 @@ def count_level_trie(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, 
     gpre = np.ascontiguousarray(item_map[prefix], dtype=np.int32)
     gext = np.ascontiguousarray(item_map[ext], dtype=np.int32)
     # one host->device copy of all int32 tables
-    nP, nW = plan.pieces.size, plan.witems.size
-    host = np.concatenate([gpre.ravel(), gext, plan.pieces.ravel(), plan.witems.ravel(), item_map])
+    rec = trie_records(plan, gpre, gext, m).ravel()
+    nP, nW = rec.size, plan.witems.size
+    # records first: the kernel reads them as int4 (16-B aligned)
+    host = np.concatenate([rec, gpre.ravel(), gext, plan.witems.ravel(), item_map])
     buf = torch.from_numpy(host).pin_memory().to(dev, non_blocking=True) if dev.type == "cuda" else \
         torch.from_numpy(host)
-    o_gext = gpre.size
-    o_pc = o_gext + gext.size
-    o_wi = o_pc + nP
+    o_gpre = nP
+    o_gext = o_gpre + gpre.size
+    o_wi = o_gext + gext.size
     o_im = o_wi + nW
     base_ptr = buf.data_ptr()
     out = torch.zeros(C, dtype=_I32, device=dev)
@@ -796,7 +798,7 @@ def count_level_trie(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, 
         per_cu = max(1, _LDS_BYTES // max(lds, 1))
         n_wg = int(max(1, min(nslabs, 256 * min(per_cu, 2))))
         _hip_call("fa_hip_count_trie", _p(roff), _p(ranks), _p(src), ncols, base_ptr + 4 * o_im, int(used.size),
-                  base_ptr, m, plan.d1, plan.d2, base_ptr + 4 * o_pc, base_ptr + 4 * (o_wi + 2 * w0),
+                  base_ptr + 4 * o_gpre, m, plan.d1, plan.d2, base_ptr, base_ptr + 4 * (o_wi + 2 * w0),
                   w1 - w0, base_ptr + 4 * (o_gext + e0), Cq, _p(wword), out.data_ptr() + 4 * e0, sw, n_wg,
                   _p(bm), bm.stride(0) if bm is not None else 0, st, None, 0)
     res = out.to(_I64)
@@ -809,6 +811,13 @@ def count_level_trie(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, 
     return res
 
 
+def _level_plan_bound(F1: int, C: int, G: int, m: int) -> int:
+    """int32 entries fa_level_plan may write: maps, gext, gpre, trie pieces + work items
+    (6 per piece, <= G + C/2 + 2 pieces) and their 32-B records (8 per piece), or the
+    slab kernel's piece tables and 48-B records."""
+    return 2 * F1 + C + G * m + 14 * (G + C // 2 + 2) + (m + 16) * (G + C // 8 + 1) + 24
+
+
 def level_plan_host(prefix: np.ndarray, ext_off: np.ndarray, ext: np.ndarray, F1: int, W: int,
                     kernel: str = "auto", lds_bytes: int | None = None, poff: np.ndarray | None = None):
     """fa_level_plan on host arrays (tests / diagnostics): (rc, info, passes, buf)."""
@@ -819,7 +828,7 @@ def level_plan_host(prefix: np.ndarray, ext_off: np.ndarray, ext: np.ndarray, F1
     min_saving = {"auto": _TRIE_MIN_SAVING, "trie": 0.0, "slab": 2.0}[kernel]
     params = np.array([lds_bytes or _LDS_BYTES, min_saving, _TRIE_CONFLICT[16], _TRIE_CONFLICT[8],
                        TRIE_PASS_WEIGHT, TRIE_ROUNDS, TRIE_EMAX, W, 4.0], dtype=np.float64)
-    bound = 2 * F1 + C + G * m + 6 * (G + C // 2 + 2) + (m + 16) * (G + C // 8 + 1) + 20
+    bound = _level_plan_bound(F1, C, G, m)
     buf = np.zeros(bound, np.int32)
     passes = np.zeros((G + C + 2, 3), np.int64)
     info = np.zeros(24, np.int64)
@@ -884,6 +893,47 @@ def emulate_slab_records(bits_by_rank: np.ndarray, info, passes, buf, C: int) ->
     return out
 
 
+def emulate_trie_records(bits_by_rank: np.ndarray, info, passes, buf, m: int, C: int) -> np.ndarray:
+    """CPU model of k_count_trie over the 32-B piece records of a trie plan
+    (fa_level_plan info[20], plan.cpp fa_trie_records); must equal emulate_level_plan."""
+    used = buf[info[13]:info[13] + int(info[3])]
+    bits = bits_by_rank[used]
+    gext = buf[info[14]:info[14] + C]
+    gpre = buf[info[15]:info[16]]
+    npc, nw = int(info[4]), int(info[5])
+    rec = buf[info[20]:info[20] + 8 * npc].view(np.uint32).reshape(-1, 8)
+    witems = buf[info[17]:info[17] + 2 * nw].reshape(-1, 2)
+    d1, d2 = int(info[7]), int(info[8])
+    out = np.zeros(C, np.int64)
+    ones = np.ones(bits.shape[1], bool)
+    for w0, w1, base in passes.tolist():
+        for wi in range(w0, w1):
+            pa, pb = witems[wi]
+            P1 = ones.copy()
+            for j in range(d1):
+                P1 &= bits[gpre[int(rec[pa, 1]) + j]]
+            P2, p = P1.copy(), P1.copy()
+            for pi in range(pa, pb):
+                r = rec[pi]
+                e0, n, flg, long_ = int(r[0] & 0x1FFFF), int((r[0] >> 17) & 63), int((r[0] >> 23) & 3), \
+                    bool((r[0] >> 25) & 1)
+                ids = gpre[int(r[1]) + d1:int(r[1]) + m] if long_ else \
+                    np.stack([r[4:8] & 0xFFFF, r[4:8] >> 16], axis=-1).reshape(-1)[:m - d1]
+                if flg & 2:
+                    P2 = P1.copy()
+                    for u in ids[:d2 - d1]:
+                        P2 &= bits[u]
+                if flg & 1:
+                    p = P2.copy()
+                    for u in ids[d2 - d1:]:
+                        p &= bits[u]
+                first = [int(r[2] & 0xFFFF), int(r[2] >> 16), int(r[3] & 0xFFFF), int(r[3] >> 16)]
+                for k in range(n):
+                    u = first[k] if k < 4 else int(gext[base + e0 + k])
+                    out[base + e0 + k] += int((p & bits[u]).sum())
+    return out
+
+
 LAST_LEVEL_PLAN: dict = {}   # shape of the last count_level call (diagnostics)
 # slab path kernel: k_count_slab_rec (piece records, map in LDS) or the index-chain k_count_slab
 SLAB_REC = os.environ.get("FA_SLAB_REC", "1") == "1"
@@ -933,7 +983,7 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
     acc16 = False
     params = np.array([_LDS_BYTES, min_saving, _TRIE_CONFLICT[16], _TRIE_CONFLICT[8], TRIE_PASS_WEIGHT,
                        TRIE_ROUNDS, TRIE_EMAX, W, 4.0], dtype=np.float64)
-    bound = 2 * F1 + C + G * m + 6 * (G + C // 2 + 2) + (m + 16) * (G + C // 8 + 1) + 20
+    bound = _level_plan_bound(F1, C, G, m)
     on_gpu = dev.type == "cuda"
     stage = pinned_stage("level_plan") if on_gpu else None
     buf = stage.get(4 * bound).view(dtype=_I32) if on_gpu else torch.empty(bound, dtype=_I32)
@@ -983,7 +1033,7 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
             lds = n_used * sw * 8 + Cq * accb
             n_wg = int(max(wg_floor, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2))))
             _hip_call("fa_hip_count_trie", _p(roff), _p(ranks), _p(src), ncols, base + 4 * o_im, n_used,
-                      base + 4 * o_gpre, m, int(info[7]), int(info[8]), base + 4 * o_pc, base + 4 * (o_wi + 2 * a),
+                      base + 4 * o_gpre, m, int(info[7]), int(info[8]), base + 4 * o_rec, base + 4 * (o_wi + 2 * a),
                       b - a, base + 4 * (o_gext + e0), Cq, _p(wword), out.data_ptr() + 4 * e0, sw, n_wg, _p(bm),
                       bm.stride(0) if bm is not None else 0, st, bm_rows, int(acc16))
         elif SLAB_REC:

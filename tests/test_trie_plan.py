@@ -110,6 +110,9 @@ def test_level_plan_counts(kernel, lds_kb, k):
     assert np.array_equal(got, want)
     if info[0] == 0:                 # slab plan: the 48-B piece records of k_count_slab_rec agree
         assert np.array_equal(emulate_slab_records(bits, info, passes, buf, ext.size), want)
+    else:                            # trie plan: the 32-B piece records of k_count_trie agree
+        from fastapriori_amd.ops.primitives import emulate_trie_records
+        assert np.array_equal(emulate_trie_records(bits, info, passes, buf, P.shape[1], ext.size), want)
 
 
 @pytest.mark.parametrize("k", [7, 11, 15])
@@ -128,6 +131,28 @@ def test_slab_records_long_prefixes(k):
     g_of_e = np.repeat(np.arange(pidx.size), np.diff(eoff))
     want = np.array([np.logical_and.reduce(bits[list(P[g]) + [e]]).sum() for g, e in zip(g_of_e, ext)])
     assert np.array_equal(emulate_slab_records(bits, info, passes, buf, ext.size), want)
+
+
+@pytest.mark.parametrize("k", [6, 10, 14])
+def test_trie_records_long_prefixes(k):
+    # k_count_trie records hold the prefix ids past D1 inline when there are <= 8 of
+    # them, and point into gpre beyond that; extensions past the first four come
+    # from gext
+    from fastapriori_amd.ops.primitives import emulate_trie_records, level_plan_host
+    rng = np.random.default_rng(k)
+    bits, prev = _level(rng, n_items=16, n_rows=300, k=k, dens=0.88)
+    pidx, eoff, ext = apriori_gen(prev)
+    if ext.size == 0:
+        pytest.skip("no candidates")
+    P = prev[pidx]
+    for lds_kb in (160, 6):
+        rc, info, passes, buf = level_plan_host(P, eoff, ext, bits.shape[0], 5, "trie", lds_bytes=lds_kb * 1024)
+        if rc == 4:                  # no slab width fits the small budget
+            continue
+        assert rc == 0 and info[0] == 1
+        g_of_e = np.repeat(np.arange(pidx.size), np.diff(eoff))
+        want = np.array([np.logical_and.reduce(bits[list(P[g]) + [e]]).sum() for g, e in zip(g_of_e, ext)])
+        assert np.array_equal(emulate_trie_records(bits, info, passes, buf, P.shape[1], ext.size), want)
 
 
 def test_level_plan_mixed_prefix_lengths():
