@@ -210,9 +210,13 @@ FA_API int fa_trie_records(const int32_t* pieces, const int32_t* witems, const i
 //                                trie: (witem begin, witem end, ext base)
 // Returns 0, 3 (buffer too small), 4 (no slab width fits: use the bitmap kernel).
 // ---------------------------------------------------------------------------
+// Width order 16, 32, 8, 4: measured per slab column on MI355X (T40I10D100M levels
+// 7-10, k_count_slab_rec), 64-B rows read ~0.43x and 256-B rows ~0.55x as many
+// columns per second as 128-B rows (the 256-B form holds 16 uint4 of prefix AND
+// per thread: fewer waves, longer row scans per LDS bank).
 static int slab_width(int64_t n_used, int64_t C, double lds, int64_t* cap_out, double accb = 4,
                       double map_lds = 0) {
-  for (int sw : {32, 16, 8, 4}) {
+  for (int sw : {16, 32, 8, 4}) {
     // + the LDS copy of the rank -> slab-row map (u16 per frequent item, k_count_slab_rec)
     const int64_t cap = (int64_t)((lds - (double)n_used * (sw + 2) * 8 - map_lds) / accb);
     if (cap >= std::min<int64_t>(C, 8192) || (sw == 4 && cap >= 1024)) { *cap_out = cap; return sw; }

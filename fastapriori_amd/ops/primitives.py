@@ -585,7 +585,7 @@ def slab_plan(n_used: int, C: int):
     force = int(os.environ.get("FA_SLAB_SW", "0"))
     if force:
         return force, int((_LDS_BYTES - n_used * (force + 2) * 8) // 4)
-    for sw in (32, 16, 8, 4):
+    for sw in (16, 32, 8, 4):     # plan.cpp slab_width order
         slab = n_used * (sw + 2) * 8
         cap = (_LDS_BYTES - slab) // 4
         if cap >= min(C, 8192) or (sw == 4 and cap >= 1024):
@@ -596,7 +596,7 @@ def slab_plan(n_used: int, C: int):
 def slab_capacity(n_used: int, C: int) -> int:
     """Accumulator capacity (candidates per pass) of the slab kernel for n_used items
     (csrc/host/plan.cpp slab_width); 0 when no width fits."""
-    for sw in (32, 16, 8, 4):
+    for sw in (16, 32, 8, 4):     # plan.cpp slab_width order
         cap = int((_LDS_BYTES - n_used * (sw + 2) * 8) // 4)
         if cap >= min(C, 8192) or (sw == 4 and cap >= 1024):
             return cap
@@ -683,7 +683,7 @@ TRIE_PASS_WEIGHT = float(os.environ.get("FA_TRIE_PASS_WEIGHT", "4"))
 ACC16 = os.environ.get("FA_ACC16", "0") == "1"   # measured: halving passes did not pay on T40I10 (more flushes, worse widths)
 # auto level kernel: trie-shared counting when its slab-row reads are below this
 # fraction of the slab kernel's (measured break-even on T10I4 / T40I10, MI355X)
-_TRIE_MIN_SAVING = float(os.environ.get("FA_TRIE_MIN_SAVING", "0.53"))
+_TRIE_MIN_SAVING = float(os.environ.get("FA_TRIE_MIN_SAVING", "0.3"))
 
 
 def trie_slab_plan(n_used: int, C: int, W: int, reads_est: float) -> tuple[int, int]:
