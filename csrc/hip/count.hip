@@ -1029,6 +1029,103 @@ __global__ __launch_bounds__(256) void k_pair_gram_mfma(const uint64_t* __restri
       }
 }
 
+// Same Gram with a 128 x 128 register tile per wave (4 x 4 MFMA tiles, 256
+// accumulator registers, one wave per SIMD) and a 256 x 256 workgroup tile.  The
+// 2 x 2-tile form above spends more VALU on unpacking bits to int8 than the MFMA
+// pipe needs (~14 VALU per 32x32x32 MFMA, i.e. longer than the MFMA's 32 cycles);
+// with 4 x 4 tiles every unpacked fragment feeds four MFMAs instead of two.  The
+// next stage's words are loaded into registers while the current one is counted.
+// On diagonal tiles the wave below the diagonal has no (row < col) entry and skips
+// its MFMAs.
+constexpr int kM4 = 4;                 // 32 x 32 MFMA tiles per wave side
+constexpr int kMT4 = 64 * kM4;         // items per workgroup tile side (2 x 2 waves)
+constexpr int kM4Ld = kMT4 * kMW / 256;   // staged words per thread and operand
+
+__global__ __launch_bounds__(256) void k_pair_gram_mfma4(const uint64_t* __restrict__ bm, int32_t F1, int64_t Wp,
+                                                         int64_t W, int nt, int ntp, int64_t kchunk,
+                                                         uint32_t* __restrict__ out) {
+  __shared__ uint64_t As[kMT4 * kMS];
+  __shared__ uint64_t Bs[kMT4 * kMS];
+  const uint32_t logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int tp = (int)(logical % (uint32_t)ntp);
+  const int64_t kc = logical / (uint32_t)ntp;
+  int ti, tj;
+  tri_index(tp, nt, ti, tj);
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int wr = (wv >> 1) * 32 * kM4, wc = (wv & 1) * 32 * kM4;   // the wave's 128 x 128 sub-tile
+  const bool live = !(ti == tj && wr > wc);
+  fa_v16i acc[kM4][kM4];
+#pragma unroll
+  for (int i = 0; i < kM4; ++i)
+#pragma unroll
+    for (int j = 0; j < kM4; ++j) acc[i][j] = fa_v16i{0};
+  const int64_t k_begin = kc * kchunk, k_end = min(W, k_begin + kchunk);
+  uint64_t pa[kM4Ld], pb[kM4Ld];
+  auto fetch = [&](int64_t k0) {
+#pragma unroll
+    for (int it = 0; it < kM4Ld; ++it) {
+      const int idx = threadIdx.x + it * 256;
+      const int row = idx >> 3, w = idx & 7;
+      const int ra = ti * kMT4 + row, rb = tj * kMT4 + row;
+      const int64_t kk = k0 + w;
+      pa[it] = (ra < F1 && kk < k_end) ? bm[(int64_t)ra * Wp + kk] : 0ull;
+      pb[it] = (rb < F1 && kk < k_end) ? bm[(int64_t)rb * Wp + kk] : 0ull;
+    }
+  };
+  if (k_begin < k_end) fetch(k_begin);
+  for (int64_t k0 = k_begin; k0 < k_end; k0 += kMW) {
+#pragma unroll
+    for (int it = 0; it < kM4Ld; ++it) {
+      const int idx = threadIdx.x + it * 256;
+      const int row = idx >> 3, w = idx & 7;
+      As[row * kMS + w] = pa[it];
+      Bs[row * kMS + w] = pb[it];
+    }
+    __syncthreads();
+    if (k0 + kMW < k_end) fetch(k0 + kMW);
+    if (live) {
+#pragma unroll 1
+      for (int w = 0; w < kMW; ++w) {
+        uint64_t a[kM4], b[kM4];
+#pragma unroll
+        for (int i = 0; i < kM4; ++i) {
+          a[i] = As[(wr + 32 * i + r) * kMS + w];
+          b[i] = Bs[(wc + 32 * i + r) * kMS + w];
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {                  // two 32-transaction k-steps per word
+          const int sh = 32 * s2 + 16 * h;
+          fa_v4i fb[kM4];
+#pragma unroll
+          for (int j = 0; j < kM4; ++j) fb[j] = unpack16_i8((uint32_t)(b[j] >> sh) & 0xFFFFu);
+#pragma unroll
+          for (int i = 0; i < kM4; ++i) {
+            const fa_v4i fa = unpack16_i8((uint32_t)(a[i] >> sh) & 0xFFFFu);
+#pragma unroll
+            for (int j = 0; j < kM4; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa, fb[j], acc[i][j], 0, 0, 0);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (!live) return;
+  // C/D layout (gfx950, 32x32): col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
+#pragma unroll
+  for (int i = 0; i < kM4; ++i)
+#pragma unroll
+    for (int j = 0; j < kM4; ++j)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int row = ti * kMT4 + wr + 32 * i + (g & 3) + 8 * (g >> 2) + 4 * h;
+        const int col = tj * kMT4 + wc + 32 * j + r;
+        const int v = acc[i][j][g];
+        if (row < col && col < F1 && v) atomicAdd(&out[(int64_t)row * F1 + col], (uint32_t)v);
+      }
+}
+
 // ---------------------------------------------------------------------------
 // k >= 3: prefix-shared candidate counting.
 // Workgroup = (super-chunk sc of 256*kWPT words) x (group block gb).  Each thread
@@ -1928,14 +2025,21 @@ FA_API int fa_hip_pair_horizontal(const int64_t* roff, const int32_t* ranks, int
 FA_API int fa_hip_pair_gram_mfma(const uint64_t* bm, int32_t F1, int64_t Wp, int64_t W, uint32_t* out,
                                  int target_wgs, hipStream_t st) {
   if (W <= 0 || F1 < 2) return 0;
-  const int nt = (F1 + kMT - 1) / kMT;
+  // 256 x 256 workgroup tiles (k_pair_gram_mfma4) unless FA_GRAM_TILE=128
+  static const bool t128 = [] { const char* e = getenv("FA_GRAM_TILE"); return e && atoi(e) == 128; }();
+  const int tile = t128 ? kMT : kMT4;
+  const int nt = (F1 + tile - 1) / tile;
   const int ntp = nt * (nt + 1) / 2;
   int64_t nk = std::max<int64_t>(1, (target_wgs + ntp - 1) / ntp);
   int64_t kchunk = (W + nk - 1) / nk;
   kchunk = std::max<int64_t>(kMW, (kchunk + kMW - 1) / kMW * kMW);
   nk = (W + kchunk - 1) / kchunk;
-  hipLaunchKernelGGL(k_pair_gram_mfma, dim3((unsigned)(nk * ntp)), dim3(256), 0, st, bm, F1, Wp, W, nt, ntp, kchunk,
-                     out);
+  if (t128)
+    hipLaunchKernelGGL(k_pair_gram_mfma, dim3((unsigned)(nk * ntp)), dim3(256), 0, st, bm, F1, Wp, W, nt, ntp, kchunk,
+                       out);
+  else
+    hipLaunchKernelGGL(k_pair_gram_mfma4, dim3((unsigned)(nk * ntp)), dim3(256), 0, st, bm, F1, Wp, W, nt, ntp,
+                       kchunk, out);
   FA_LAUNCH_RET();
 }
 
