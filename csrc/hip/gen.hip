@@ -227,7 +227,7 @@ FA_API int fa_hip_ag_gen(const int32_t* P, int64_t n, int m, int F1, void* ws, i
 // slab capacity for n_used items and C candidates, and the largest total t with
 // t <= capacity(t).
 static int64_t ag_slab_cap(int64_t n_used, int64_t C, double lds) {
-  for (int sw : {32, 16, 8, 4}) {
+  for (int sw : {16, 32, 8, 4}) {      // plan.cpp slab_width order
     const int64_t cap = (int64_t)((lds - (double)n_used * (sw + 2) * 8) / 4);
     if (cap >= std::min<int64_t>(C, 8192) || (sw == 4 && cap >= 1024)) return cap;
   }
@@ -265,6 +265,10 @@ __global__ __launch_bounds__(256) void k_ag_mark(const int32_t* __restrict__ row
   __syncthreads();
   if (threadIdx.x < 128 && lb[threadIdx.x]) atomicOr(&bits[threadIdx.x], lb[threadIdx.x]);
 }
+
+static int ag_chain_dev(const int32_t* P1, int64_t n1, int m1, int nw, char* w0, char* w, int64_t ws_bytes,
+                        int32_t* host, int64_t hoff, int64_t host_cap, int max_levels, double growth, int64_t total,
+                        int64_t last, const uint32_t* mark, double lds, int64_t* sizes, hipStream_t st);
 
 // first_free = 1 (lds > 0): P0 is F_{k-1} itself; level 0 (= level k's candidates)
 // is always emitted, its used items (a device bitset, read back with level 1's
@@ -351,6 +355,11 @@ FA_API int fa_hip_ag_chain(const int32_t* P0, int64_t n0, int m0, int F1, void* 
     P = rows_out;
     n = C;
     ++m;
+    // levels 1.. without a host round trip per level (FA_GEN_DEVCHAIN=0: the loop below)
+    static const bool devchain = [] { const char* e = getenv("FA_GEN_DEVCHAIN"); return !e || atoi(e) != 0; }();
+    if (first_free && l == 0 && devchain)
+      return ag_chain_dev(P, n, m, nw, w0, w, ws_bytes, host, hoff, host_cap, max_levels, growth, total, last, mark,
+                          lds, sizes, st);
   }
   (void)hipStreamSynchronize(st);
   sizes[0] = L;
@@ -387,7 +396,7 @@ struct ChainArgs {
 };
 
 __device__ int64_t d_slab_cap(int64_t n_used, int64_t C, double lds) {
-  const int sws[4] = {32, 16, 8, 4};
+  const int sws[4] = {16, 32, 8, 4};   // plan.cpp slab_width order
   for (int q = 0; q < 4; ++q) {
     const int sw = sws[q];
     const int64_t cap = (int64_t)((lds - (double)n_used * (sw + 2) * 8) / 4);
@@ -610,4 +619,240 @@ FA_API int fa_hip_ag_chain_coop(const int32_t* P0, int64_t n0, int m0, int F1, v
   void* args[] = {&A};
   return (int)hipLaunchCooperativeKernel((const void*)k_ag_chain_coop, dim3((unsigned)n_wg), dim3(kChainThreads),
                                          args, 0, st);
+}
+
+// ---------------------------------------------------------------------------
+// Device-sized speculative levels (first_free chains, after level 0).
+//
+// fa_hip_ag_chain used to read every speculative level's candidate count back
+// before it could size and launch the next level: one host round trip per level
+// (~0.1 ms of GPU idle each; 7 of them for the T10I4 bundle 5-12).  Here every
+// kernel of level l reads its row count from a device control block and exits
+// once the chain has stopped, the acceptance rule (C > 0, C <= growth * C_prev,
+// bundle total <= tmax) runs at the end of the one-workgroup scan kernel, and
+// tmax itself comes from level 0's used-item bitset on the device.  Buffers are
+// sized by bounds (C_l <= min(growth * n_l, accumulator limit)); levels are
+// enqueued in batches of kAgdBatch with one control-block readback per batch,
+// then the accepted levels are copied out.  (A single cooperative kernel was
+// measured slower: its grid barriers cost more than these kernel boundaries.)
+//   ctl (device int64): 0 stop, 1 accepted levels (incl. level 0), 2 total,
+//   3 last C, 4 tmax, 8 + l: n_l (input rows of level l), 40 + l: C_l.
+// ---------------------------------------------------------------------------
+namespace fa {
+
+constexpr int kAgdMaxLevels = 30;
+constexpr int kAgdBatch = 4;
+
+__global__ void k_agd_setup(long long* __restrict__ c, int64_t n1, int64_t total, int64_t last,
+                            const uint32_t* __restrict__ mark, double lds) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  int64_t n_used = 0;
+  for (int q = 0; q < 128; ++q) n_used += __popc(mark[q]);
+  c[0] = total > d_slab_cap(n_used, total, lds) ? 1 : 0;   // level k alone needs several passes
+  c[1] = 1;
+  c[2] = total;
+  c[3] = last;
+  c[4] = d_total_limit(n_used, lds);
+  c[9] = n1;
+}
+
+// clear the hash tables (-1) and Ext bitsets (0) of a batch of levels: region q is
+// [p[q], p[q] + len[q]) words of 32 bits, value val[q]
+struct AgdClear {
+  uint32_t* p[2 * kAgdBatch];
+  int64_t len[2 * kAgdBatch];
+  uint32_t val[2 * kAgdBatch];
+  int nreg;
+};
+
+__global__ __launch_bounds__(256) void k_agd_clear(AgdClear A, const long long* __restrict__ c) {
+  if (c[0]) return;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int q = 0; q < A.nreg; ++q)
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < A.len[q]; i += stride) A.p[q][i] = A.val[q];
+}
+
+__global__ __launch_bounds__(256) void k_agd_insert(const int32_t* __restrict__ P, int m, int32_t* __restrict__ table,
+                                                    uint32_t mask, const long long* __restrict__ c, int l) {
+  if (c[0]) return;
+  const int64_t n = c[8 + l];
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t* r = P + i * m;
+  if (i > 0) {
+    const int32_t* pr = P + (i - 1) * m;
+    bool same = true;
+    for (int q = 0; q < m - 1; ++q) same = same && r[q] == pr[q];
+    if (same) return;
+  }
+  uint32_t at = (uint32_t)ag_hash_drop(r, m, m - 1) & mask;
+  while (atomicCAS(&table[at], -1, (int32_t)i) != -1) at = (at + 1) & mask;
+}
+
+__global__ __launch_bounds__(256) void k_agd_ext(const int32_t* __restrict__ P, int m,
+                                                 const int32_t* __restrict__ table, uint32_t mask, int nw,
+                                                 unsigned long long* __restrict__ ext, const long long* __restrict__ c,
+                                                 int l) {
+  if (c[0]) return;
+  const int64_t n = c[8 + l];
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t* r = P + i * m;
+  const int32_t s = ag_find(P, m, table, mask, r, m - 1);
+  const int32_t y = r[m - 1];
+  atomicOr(&ext[(int64_t)s * nw + (y >> 6)], 1ull << (y & 63));
+}
+
+// kEmit = false: cnt[i] = extensions of row i;  true (accepted levels only): ext ids at
+// cnt + n + off[i] (the host layout cnt | ext) and the candidate rows at rows + off[i] * (m + 1)
+template <bool kEmit>
+__global__ __launch_bounds__(256) void k_agd_rows(const int32_t* __restrict__ P, int m,
+                                                  const int32_t* __restrict__ table, uint32_t mask, int nw,
+                                                  const unsigned long long* __restrict__ ext, int32_t* __restrict__ cnt,
+                                                  const int64_t* __restrict__ off, int32_t* __restrict__ rows,
+                                                  const long long* __restrict__ c, int l) {
+  if (c[0]) return;
+  const int64_t n = c[8 + l];
+  const int lane = threadIdx.x & 63;
+  const int64_t nwave = (int64_t)gridDim.x * (blockDim.x / 64);
+  for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); i < n; i += nwave) {
+    const unsigned long long a = chain_row_bits(P, i, m, table, mask, nw, ext, lane);
+    const int cc = __popcll(a);
+    const int incl = wave_scan_incl_dpp(cc);
+    if (!kEmit) {
+      if (lane == 63) cnt[i] = incl;
+    } else {
+      int64_t o = off[i] + (incl - cc);
+      const int32_t* x = P + i * m;
+      for (unsigned long long v = a; v; v &= v - 1) {
+        const int32_t y = lane * 64 + __builtin_ctzll(v);
+        cnt[n + o] = y;
+        int32_t* r = rows + o * (m + 1);
+        for (int q = 0; q < m; ++q) r[q] = x[q];
+        r[m] = y;
+        ++o;
+      }
+    }
+  }
+}
+
+// off[0 .. n] = exclusive offsets of cnt[0 .. n) (one workgroup), then the acceptance of
+// level l by thread 0: C_l = off[n_l]
+__global__ __launch_bounds__(1024) void k_agd_scan_decide(const int32_t* __restrict__ cnt, int64_t* __restrict__ off,
+                                                          long long* __restrict__ c, int l, double growth,
+                                                          int64_t c_bound) {
+  __shared__ int64_t part[16];
+  __shared__ int64_t carry;
+  if (c[0]) return;
+  const int64_t n = c[8 + l];
+  if (threadIdx.x == 0) { carry = 0; off[0] = 0; }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int64_t b = 0; b < n; b += 1024) {
+    const int64_t i = b + threadIdx.x;
+    const int v = i < n ? cnt[i] : 0;
+    const int incl = wave_scan_incl_dpp(v);
+    if (lane == 63) part[wv] = incl;
+    __syncthreads();
+    int64_t before = carry;
+    for (int q = 0; q < wv; ++q) before += part[q];
+    if (i < n) off[i + 1] = before + incl;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = before + incl;
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  const int64_t C = carry;
+  const int64_t total = c[2], last = c[3], tmax = c[4];
+  if (C == 0 || (double)C > growth * (double)last || total + C > tmax || C > c_bound) { c[0] = 1; return; }
+  c[40 + l] = C;
+  c[1] = l + 1;
+  c[2] = total + C;
+  c[3] = C;
+  c[8 + l + 1] = C;
+}
+
+}  // namespace fa
+
+// Levels 1 .. of a first_free chain (see above).  P1 = level 0's candidate rows
+// (device, [n1][m1]), mark = level 0's used-item bitset (device, 128 words).  The
+// host layout continues at host[hoff].  On return (rc 0) sizes[0] = accepted
+// levels including level 0 and sizes[2 + l] = C_l for l >= 1.
+static int ag_chain_dev(const int32_t* P1, int64_t n1, int m1, int nw, char* w0, char* w, int64_t ws_bytes,
+                        int32_t* host, int64_t hoff, int64_t host_cap, int max_levels, double growth, int64_t total,
+                        int64_t last, const uint32_t* mark, double lds, int64_t* sizes, hipStream_t st) {
+  using namespace fa;
+  auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
+  const int LM = std::min(max_levels - 1, kAgdMaxLevels - 2);
+  long long* c = reinterpret_cast<long long*>(w); w += al(8 * 72);
+  const int64_t acc_max = (int64_t)(lds / 4);         // no bundle total passes the accumulator capacity
+  struct Lv { int32_t* cnt; int32_t* rows; int m; };
+  Lv lv[kAgdMaxLevels];
+  int64_t nb = n1;
+  int m = m1;
+  const int32_t* P = P1;
+  long long ch[72];
+  ch[0] = LM <= 0;
+  ch[1] = 1;
+  hipLaunchKernelGGL(k_agd_setup, dim3(1), dim3(64), 0, st, c, n1, total, last, mark, lds);
+  for (int l0 = 1; l0 <= LM && !ch[0]; l0 += kAgdBatch) {
+    const int l1 = std::min(LM, l0 + kAgdBatch - 1);
+    struct Bufs { int32_t* table; uint32_t cap; unsigned long long* ext; int64_t* off; int64_t nb, cb; };
+    Bufs bf[kAgdBatch];
+    AgdClear clr{};
+    int64_t clr_max = 0;
+    for (int l = l0; l <= l1; ++l) {
+      const int64_t cb = std::min<int64_t>(acc_max, (int64_t)(growth * (double)nb) + 1);
+      uint32_t cap = 16;
+      while (cap < 2 * (uint64_t)nb) cap <<= 1;
+      const int64_t need = al(4 * (int64_t)cap) + al(8 * nb * nw) + al(8 * (nb + 1)) + al(4 * (nb + cb)) +
+                           al(4 * cb * (m + 1));
+      if ((w - w0) + need > ws_bytes) { (void)hipStreamSynchronize(st); sizes[1] = 2 * ((w - w0) + need); return 5; }
+      Bufs& b = bf[l - l0];
+      b.table = reinterpret_cast<int32_t*>(w); w += al(4 * (int64_t)cap);
+      b.ext = reinterpret_cast<unsigned long long*>(w); w += al(8 * nb * nw);
+      b.off = reinterpret_cast<int64_t*>(w); w += al(8 * (nb + 1));
+      b.cap = cap; b.nb = nb; b.cb = cb;
+      lv[l].cnt = reinterpret_cast<int32_t*>(w); w += al(4 * (nb + cb));
+      lv[l].rows = reinterpret_cast<int32_t*>(w); w += al(4 * cb * (m + 1));
+      lv[l].m = m;
+      clr.p[clr.nreg] = reinterpret_cast<uint32_t*>(b.table); clr.len[clr.nreg] = cap; clr.val[clr.nreg++] = ~0u;
+      clr.p[clr.nreg] = reinterpret_cast<uint32_t*>(b.ext); clr.len[clr.nreg] = 2 * nb * nw; clr.val[clr.nreg++] = 0u;
+      clr_max = std::max<int64_t>(clr_max, std::max<int64_t>(cap, 2 * nb * nw));
+      nb = cb;
+      ++m;
+    }
+    hipLaunchKernelGGL(k_agd_clear, dim3((unsigned)std::min<int64_t>((clr_max + 255) / 256, 2048)), dim3(256), 0, st,
+                       clr, c);
+    for (int l = l0; l <= l1; ++l) {
+      const Bufs& b = bf[l - l0];
+      const int ml = lv[l].m;
+      const dim3 g((unsigned)((b.nb + 255) / 256));
+      hipLaunchKernelGGL(k_agd_insert, g, dim3(256), 0, st, P, ml, b.table, b.cap - 1, c, l);
+      hipLaunchKernelGGL(k_agd_ext, g, dim3(256), 0, st, P, ml, b.table, b.cap - 1, nw, b.ext, c, l);
+      const unsigned nwg = (unsigned)std::min<int64_t>((b.nb + 3) / 4, 65536);
+      hipLaunchKernelGGL(k_agd_rows<false>, dim3(nwg), dim3(256), 0, st, P, ml, b.table, b.cap - 1, nw, b.ext,
+                         lv[l].cnt, b.off, lv[l].rows, c, l);
+      hipLaunchKernelGGL(k_agd_scan_decide, dim3(1), dim3(1024), 0, st, lv[l].cnt, b.off, c, l, growth, b.cb);
+      hipLaunchKernelGGL(k_agd_rows<true>, dim3(nwg), dim3(256), 0, st, P, ml, b.table, b.cap - 1, nw, b.ext,
+                         lv[l].cnt, b.off, lv[l].rows, c, l);
+      P = lv[l].rows;
+    }
+    (void)hipMemcpyAsync(ch, c, sizeof(ch), hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) return 7;
+  }
+  const int L = (int)ch[1];
+  for (int l = 1; l < L; ++l) {
+    const int64_t n = ch[8 + l], C = ch[40 + l];
+    const int ml = lv[l].m;
+    const int64_t need_host = hoff + n + C + C * (ml + 1);
+    if (need_host > host_cap) { (void)hipStreamSynchronize(st); sizes[1] = 2 * need_host; return 6; }
+    (void)hipMemcpyAsync(host + hoff, lv[l].cnt, 4 * (size_t)(n + C), hipMemcpyDeviceToHost, st);
+    (void)hipMemcpyAsync(host + hoff + n + C, lv[l].rows, 4 * (size_t)(C * (ml + 1)), hipMemcpyDeviceToHost, st);
+    hoff = need_host;
+    sizes[2 + l] = C;
+  }
+  (void)hipStreamSynchronize(st);
+  sizes[0] = L;
+  FA_LAUNCH_RET();
 }
