@@ -52,7 +52,7 @@ BUNDLE_LEVELS = os.environ.get("FA_BUNDLE", "1") == "1"
 FUSED_COMPRESS = os.environ.get("FA_FUSED_COMPRESS", "1") == "1"
 # short rows only: 256-row spans must fit the 4096-token LDS stage and most rows the
 # 16-token register sort (T40I10's 40-token rows are faster on the tiered path)
-FUSED_COMPRESS_MEAN_LEN = 12
+FUSED_COMPRESS_MEAN_LEN = float(os.environ.get("FA_FUSED_COMPRESS_MEAN_LEN", "12"))
 GEN_DEVICE = os.environ.get("FA_GEN_DEVICE", "1") == "1"
 GEN_CHAIN = os.environ.get("FA_GEN_CHAIN", "1") == "1"
 GEN_DEVICE_MIN_ROWS = int(os.environ.get("FA_GEN_DEVICE_MIN_ROWS", "512"))
@@ -616,7 +616,7 @@ class FastApriori:
         K = kept.numel()
         if K > 0.9 * db["T"] and nranks.numel() > 0.9 * db["ranks"].numel():
             return   # not worth re-laying out
-        db.update(roff=nroff, ranks=nranks, T=K, bm=None, W=0, bcnt=None)
+        db.update(roff=nroff, ranks=nranks, T=K, bm=None, W=0, bcnt=None, bm_items=None, bm_map=None)
         db["alive"] = np.zeros_like(db["alive"])
         db["alive"][used] = True
         db["len_hist"] = hist.cpu().numpy()
@@ -627,14 +627,34 @@ class FastApriori:
             db.update(src=None, ncols=K)
         self.log.metric(phase="trim", k=k, rows=K, nnz=int(nranks.numel()))
 
-    def _bitmaps(self, db):
-        """Item-major bitmaps of every item for the current row layout (built once,
-        reused by the Gram pair kernel and every multi-pass level until a trim)."""
-        if db["bm"] is None:
-            with roctx_range("bitmaps"):
+    def _bitmaps(self, db, used: np.ndarray | None = None):
+        """Item-major bitmaps for the current row layout (built once, reused by the Gram
+        pair kernel and every multi-pass level until a trim).
+
+        used=None: every item's row, rank-indexed.  used (sorted ranks): only those rows
+        -- a multi-pass level's items, which contain every later level's items (level
+        k+1's candidates are built from F_k, whose items are level-k candidate items),
+        so the rows of the next levels are a subset until the layout changes.  Returns
+        (bm, bm_map): bm_map is the device rank -> bitmap row map, or None when the
+        bitmap is rank-indexed."""
+        have = db.get("bm_items")
+        if db["bm"] is not None and (have is None or (used is not None and have[used].all())):
+            return db["bm"], db.get("bm_map")
+        with roctx_range("bitmaps"):
+            if used is None:
                 bm, W = ops.build_bitmaps(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"])
-            db["bm"], db["W"] = bm, W
-        return db["bm"]
+                db.update(bm=bm, W=W, bm_items=None, bm_map=None)
+            else:
+                dev = db["ranks"].device
+                imap = np.full(max(db["F1"], 1), -1, dtype=np.int32)
+                imap[used] = np.arange(used.size, dtype=np.int32)
+                items = np.zeros(max(db["F1"], 1), dtype=bool)
+                items[used] = True
+                imap_t = torch.from_numpy(imap).to(dev)
+                bm, W = ops.build_bitmaps(db["roff"], db["ranks"], db["src"], db["ncols"], int(used.size), imap_t,
+                                          torch.from_numpy(np.ascontiguousarray(used, dtype=np.int32)).to(dev))
+                db.update(bm=bm, W=W, bm_items=items, bm_map=imap_t)
+        return db["bm"], db.get("bm_map")
 
     # ------------------------------------------------------------------
     # k = 2 (FastApriori.scala:212-241)
@@ -825,7 +845,7 @@ class FastApriori:
             return self._cand_view
         r, nr = self.comm.rank, self.comm.world_size
         v = dict(db)
-        v.update(bm=None, W=0)
+        v.update(bm=None, W=0, bm_items=None, bm_map=None)
         if db["src"] is None:
             T = db["T"]
             a, b = T * r // nr, T * (r + 1) // nr
@@ -863,7 +883,7 @@ class FastApriori:
         eoff = np.concatenate([[0], np.cumsum(np.concatenate([np.diff(eo) for _, _, _, eo, _ in bundle]))])
         ext = np.concatenate([ex for *_, ex in bundle]).astype(np.int32)
         cnt = ops.count_level(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"], flat, eoff, ext,
-                              db["wword"], kernel="slab", poff=poff, full_bm=lambda: self._bitmaps(db))
+                              db["wword"], kernel="slab", poff=poff, full_bm=lambda u: self._bitmaps(db, u))
         if cnt is None:
             return [self._count_level(full_db, pv, pi, eo, ex) for _, pv, pi, eo, ex in bundle]
         self.comm.all_reduce_(cnt, bound=self.stats["n_lines"])
@@ -897,7 +917,7 @@ class FastApriori:
         lk = self.cfg.level_kernel
         if dev.type == "cuda" and lk in ("auto", "trie", "slab"):
             cnt = ops.count_level(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"], prev[prefix_idx],
-                                  ext_off, ext, db["wword"], kernel=lk, full_bm=lambda: self._bitmaps(db))
+                                  ext_off, ext, db["wword"], kernel=lk, full_bm=lambda u: self._bitmaps(db, u))
             if cnt is not None:
                 self.dcomm.all_reduce_(cnt, bound=self.stats["n_lines"])
                 return cnt.cpu().numpy()

@@ -964,8 +964,9 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
     kernel: auto (trie where it saves enough slab-row reads) | trie | slab.
     prefix: int32 [G, m], or (poff given) a flat int32 array with group g's
     prefix at poff[g]:poff[g+1] — groups of several levels (k) in one launch.
-    full_bm: optional callable returning the bitmap of every item [F1, Wp] of the
-    current row layout (built once, shared by all multi-pass levels until the rows
+    full_bm: optional callable(used ranks) returning (bitmap, rank -> bitmap row map
+    or None for a rank-indexed bitmap) of the current row layout, holding at least
+    the used items' rows (built once, shared by the multi-pass levels until the rows
     change); without it a used-item bitmap is built for each multi-pass level.
     Returns int64 counts [C] (ext order), or None when no LDS slab fits (the
     caller then uses the bitmap kernel)."""
@@ -1017,8 +1018,12 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
     bm, bm_rows = None, None
     if npass > 1:
         if full_bm is not None:
-            bm = full_bm()
-            bm_rows = base + 4 * o_used             # slab row u -> bitmap row used[u]
+            bm, bmap = full_bm(buf[o_used:o_used + n_used].numpy().copy())
+            if bmap is None:
+                bm_rows = base + 4 * o_used         # slab row u -> bitmap row used[u]
+            else:
+                rows_t = bmap[dbuf[o_used:o_used + n_used].to(_I64)]   # slab row u -> bitmap row of used[u]
+                bm_rows = rows_t.data_ptr()
         else:
             bm, _ = build_bitmaps(roff, ranks, src, ncols, n_used, dbuf[o_im:o_im + F1],
                                   dbuf[o_used:o_used + n_used])

@@ -39,6 +39,23 @@ def _load_checkpoint(ckpt: Checkpointer, comm, require_complete: bool = False):
     return res
 
 
+def _load_saved(cfg: JobConfig, comm):
+    """Rank 0 rebuilds the mined result from the saved ``freqItems`` / ``ItemsToRank``
+    files (io.load_saved_results, the reference's Utils.getAll) and sends it to every
+    rank; None when the files are missing."""
+    freq, rank = cfg.output + "freqItems", cfg.output + "ItemsToRank"
+    res, err = None, None
+    if comm.is_root and os.path.exists(rank) and os.path.exists(freq):
+        try:
+            res = io.load_saved_results(freq, rank)
+        except (OSError, ValueError, KeyError) as e:
+            err = f"{type(e).__name__}: {e}"
+    res, err = comm.broadcast_object((res, err))
+    if err:
+        raise ValueError(f"loading {freq} failed on rank 0: {err}")
+    return res
+
+
 def run_job(cfg: JobConfig, comm=None) -> dict:
     own_comm = comm is None
     if comm is None:
@@ -63,11 +80,15 @@ def run_job(cfg: JobConfig, comm=None) -> dict:
         t1 = time.time()
         result = None
         if cfg.rules_only:
-            if ckpt is None:
-                raise ValueError("--rules-only needs the temp path of a previous run")
-            result = _load_checkpoint(ckpt, comm, require_complete=True)
+            # the complete checkpoint under temp, else the saved result files of a
+            # --with-counts run (freqItems + ItemsToRank: Utils.getAll, Utils.scala:65-81)
+            result = _load_checkpoint(ckpt, comm, require_complete=True) if ckpt is not None else None
             if result is None:
-                raise FileNotFoundError(f"no complete checkpoint under {ckpt.dir}")
+                result = _load_saved(cfg, comm)
+            if result is None:
+                where = f"under {ckpt.dir} " if ckpt is not None else ""
+                raise FileNotFoundError(f"--rules-only: no complete checkpoint {where}and no "
+                                        f"{cfg.output}freqItems + {cfg.output}ItemsToRank (written by --with-counts)")
         else:
             resume = _load_checkpoint(ckpt, comm) if (ckpt is not None and cfg.resume) else None
             # candidate distribution: every rank holds the whole DB

@@ -69,3 +69,18 @@ def test_getall_format_roundtrip(tmp_path):
     assert back.as_dict() == res.as_dict()
     for a, b in zip(back.levels, res.levels):
         assert np.array_equal(a, b)
+
+
+def test_rules_only_from_saved_results(tmp_path):
+    # no checkpoint: --rules-only rebuilds the result from a --with-counts run's
+    # freqItems + ItemsToRank (Utils.getAll, Utils.scala:65-81)
+    _inputs(tmp_path)
+    cfg = JobConfig(input=f"{tmp_path}/", output=f"{tmp_path}/a_", min_support=0.02, device="cpu", with_counts=True)
+    run_job(cfg, Comm())
+    rec = _read(tmp_path / "a_recommends/part-00000")
+    os.remove(tmp_path / "D.dat")
+    os.rename(tmp_path / "a_recommends", tmp_path / "a_recommends.first")
+    cfg2 = JobConfig(input=f"{tmp_path}/", output=f"{tmp_path}/a_", min_support=0.02, device="cpu", rules_only=True)
+    s = run_job(cfg2, Comm())
+    assert "miner" not in s
+    assert _read(tmp_path / "a_recommends/part-00000") == rec
