@@ -118,6 +118,48 @@ __global__ __launch_bounds__(256) void k_txn_freq_count(const int64_t* __restric
   cnt[t] = c;
 }
 
+// The same with the workgroup's 256-row input span loaded coalesced and mapped
+// through the LUT into LDS as one flag byte per token; each thread then sums its
+// row's flags from LDS.  (Thread-per-row loads touch one cache line per lane and
+// load: 15.6 ms for T40I10D100M's 4 G tokens.)  Spans past SPAN bytes read their
+// rows directly.
+template <int SPAN>
+__global__ __launch_bounds__(256) void k_txn_freq_count_span(const int64_t* __restrict__ off,
+                                                             const int32_t* __restrict__ items, int64_t n,
+                                                             const int32_t* __restrict__ lut,
+                                                             int32_t* __restrict__ cnt) {
+  constexpr int PER = SPAN / 256;
+  __shared__ uint8_t fl[SPAN];
+  const int64_t x0 = (int64_t)blockIdx.x * 256;
+  const int64_t x1 = min(n, x0 + 256);
+  const int64_t x = x0 + threadIdx.x;
+  const int64_t base = off[x0], n_in = off[x1] - base;
+  const int64_t s = x < x1 ? off[x] : 0, e = x < x1 ? off[x + 1] : 0;
+  if (n_in <= SPAN) {
+    int32_t v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int64_t i = threadIdx.x + k * 256;
+      v[k] = i < n_in ? items[base + i] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int64_t i = threadIdx.x + k * 256;
+      if (i < n_in) fl[i] = lut[v[k]] >= 0 ? 1 : 0;
+    }
+    __syncthreads();
+    if (x < x1) {
+      int32_t c = 0;
+      for (int64_t j = s - base; j < e - base; ++j) c += fl[j];
+      cnt[x] = c;
+    }
+  } else if (x < x1) {
+    int32_t c = 0;
+    for (int64_t i = s; i < e; ++i) c += lut[items[i]] >= 0;
+    cnt[x] = c;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Compression: kept transaction x -> its frequent ranks, sorted ascending, at
 // ranks[roff[x] .. roff[x+1]).  Short rows are sorted in registers with an
@@ -199,13 +241,17 @@ __global__ __launch_bounds__(256) void k_compress_regs(
 // overflow list; their (garbage) slots in the output span are rewritten by the
 // next tier, which runs later on the same stream.
 constexpr int kCSpan = 8192;
-constexpr int kCPer = kCSpan / 256;   // span elements per thread, loaded with full ILP
 
-template <int N>
+// SPAN = staged input tokens per workgroup (32 KB at N = 16; 64 KB for the
+// 64-token tier of long-ish rows, e.g. T40I10's 40-token transactions, whose
+// 256-row spans do not fit 8192 and would otherwise be gathered row by row)
+template <int N, int SPAN = kCSpan>
 __global__ __launch_bounds__(256) void k_compress_staged(
     const int64_t* __restrict__ off, const int32_t* __restrict__ items, const int32_t* __restrict__ lut,
     int64_t T, const int32_t* __restrict__ kept, const int64_t* __restrict__ roff,
     int32_t* __restrict__ ranks, int8_t* __restrict__ over_flag) {
+  constexpr int kCSpan = SPAN;
+  constexpr int kCPer = kCSpan / 256;   // span elements per thread, loaded with full ILP
   __shared__ uint32_t buf[kCSpan];
   const int64_t x0 = (int64_t)blockIdx.x * blockDim.x;
   const int64_t x1 = min(T, x0 + (int64_t)blockDim.x);
@@ -1049,6 +1095,9 @@ FA_API int fa_hip_txn_freq_count(const int64_t* off, const int32_t* items, int64
   if (nnz > 48 * n)
     hipLaunchKernelGGL(k_txn_freq_count_wave, dim3((unsigned)std::min<int64_t>((n + 3) / 4, 8192)), dim3(256), 0, st,
                        off, items, n, lut, cnt);
+  else if (nnz > 8 * n)
+    hipLaunchKernelGGL(k_txn_freq_count_span<16384>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, off, items,
+                       n, lut, cnt);
   else
     hipLaunchKernelGGL(k_txn_freq_count, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, off, items, n, lut, cnt);
   FA_LAUNCH_RET();
@@ -1088,6 +1137,17 @@ FA_API int fa_hip_compress_staged(const int64_t* off, const int32_t* items, cons
   if (T <= 0) return 0;
   hipLaunchKernelGGL(k_compress_staged<16>, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, st, off, items, lut,
                      T, kept, roff, ranks, over_flag);
+  FA_LAUNCH_RET();
+}
+
+// 64-token staged tier for long-ish rows (64 KB input span per workgroup); rows
+// longer than 64 tokens are flagged for the wave / LDS tiers
+FA_API int fa_hip_compress_staged64(const int64_t* off, const int32_t* items, const int32_t* lut, int64_t T,
+                                    const int32_t* kept, const int64_t* roff, int32_t* ranks, int8_t* over_flag,
+                                    hipStream_t st) {
+  if (T <= 0) return 0;
+  hipLaunchKernelGGL((k_compress_staged<64, 16384>), dim3((unsigned)((T + 255) / 256)), dim3(256), 0, st, off, items,
+                     lut, T, kept, roff, ranks, over_flag);
   FA_LAUNCH_RET();
 }
 

@@ -80,6 +80,7 @@ _HIP_SIGS = {
     "fa_hip_block_counts_rows": (C.c_int, [vp, vp, vp, i64, vp, i64, C.c_int, vp]),
     "fa_hip_block_bsum": (C.c_int, [vp, i64, i64, C.c_int, vp, vp]),
     "fa_hip_compress_staged": (C.c_int, [vp, vp, vp, i64, vp, vp, vp, vp, vp]),
+    "fa_hip_compress_staged64": (C.c_int, [vp, vp, vp, i64, vp, vp, vp, vp, vp]),
     "fa_hip_count_trie": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, vp, C.c_int, C.c_int, C.c_int, vp, vp,
                                     C.c_int, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, i64, vp, vp, C.c_int]),
     "fa_hip_count_dfs": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, vp, vp, vp, vp, vp, C.c_int, C.c_int, vp,

@@ -174,7 +174,9 @@ def txn_freq_count(offsets: torch.Tensor, items: torch.Tensor, lut: torch.Tensor
 
 
 COMPRESS_WAVE_MAX_F1 = 65536
-COMPRESS_WAVE_MEAN_LEN = float(os.environ.get("FA_COMPRESS_WAVE_MEAN_LEN", "48"))   # mean row length above which every row goes to the wave kernel
+COMPRESS_WAVE_MEAN_LEN = float(os.environ.get("FA_COMPRESS_WAVE_MEAN_LEN", "48"))
+# mean row length above which the 64-token staged tier (64 KB input span per workgroup) runs first
+COMPRESS_STAGED64_MEAN_LEN = float(os.environ.get("FA_COMPRESS_STAGED64_MEAN_LEN", "16"))   # mean row length above which every row goes to the wave kernel
 
 
 def compress(offsets, items, lut, kept, roff, F1: int | None = None) -> torch.Tensor:
@@ -199,20 +201,24 @@ def compress(offsets, items, lut, kept, roff, F1: int | None = None) -> torch.Te
                   _p(ranks), F1, st)
         return ranks[:nnz]
     flag = torch.empty(T, dtype=torch.int8, device=items.device)
-    _hip_call("fa_hip_compress_staged", _p(offsets), _p(items), _p(lut), T, _p(kept), _p(roff), _p(ranks),
-              _p(flag), st)
+    # long-ish rows (mean > COMPRESS_STAGED64_MEAN_LEN tokens): the 64-token staged tier first
+    staged64 = items.numel() > COMPRESS_STAGED64_MEAN_LEN * max(offsets.numel() - 1, 1)
+    _hip_call("fa_hip_compress_staged64" if staged64 else "fa_hip_compress_staged", _p(offsets), _p(items), _p(lut),
+              T, _p(kept), _p(roff), _p(ranks), _p(flag), st)
     over = torch.nonzero(flag).flatten().to(_I32)
     n1 = over.numel()
-    if n1:
+    over2, n2 = over, n1                 # after the 64-token staged tier: rows of > 64 tokens
+    if n1 and not staged64:
         flag2 = torch.empty(n1, dtype=torch.int8, device=items.device)
         _hip_call("fa_hip_compress_regs", 64, _p(offsets), _p(items), _p(lut), _p(over), n1, _p(kept),
                   _p(roff), _p(ranks), _p(flag2), st)
         over2 = over[torch.nonzero(flag2).flatten()].contiguous()
         n2 = over2.numel()
-        if n2 and wave_ok:
+    if n2:
+        if wave_ok:
             _hip_call("fa_hip_compress_wave", _p(offsets), _p(items), _p(lut), _p(over2), n2, _p(kept), _p(roff),
                       _p(ranks), F1, st)
-        elif n2:
+        else:
             over3 = torch.empty(n2, dtype=_I32, device=items.device)
             n_over3 = torch.zeros(1, dtype=_I32, device=items.device)
             _hip_call("fa_hip_compress_lds", _p(offsets), _p(items), _p(lut), _p(over2), n2, _p(kept),

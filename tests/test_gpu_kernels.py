@@ -93,6 +93,19 @@ def test_compress_long_documents(V, frac):
     assert torch.equal(ref, got)
 
 
+@pytest.mark.parametrize("max_len, long_rows, n", [(80, 0, 4000), (70, 40, 3000), (90, 0, 600)])
+def test_compress_staged64(max_len, long_rows, n):
+    # mean row length > 16: span-staged counts and the 64-token staged tier (64 KB input span per
+    # workgroup; rows of > 64 tokens to the wave tier; wide spans through the unstaged path)
+    off, items, lut, F1 = _prep(n=n, V=900, max_len=max_len, seed=max_len + n, long_rows=long_rows)
+    assert items.numel() > 16 * n
+    cnt, kept, roff = _compress_inputs(off, items, lut)
+    assert torch.equal(cnt, ops.txn_freq_count(off.to(DEV), items.to(DEV), lut.to(DEV)).cpu())
+    ref = ops.compress(off, items, lut, kept, roff)
+    got = ops.compress(off.to(DEV), items.to(DEV), lut.to(DEV), kept.to(DEV), roff.to(DEV), F1).cpu()
+    assert torch.equal(ref, got)
+
+
 def test_row_hash_matches_host():
     off, items, lut, F1 = _prep(seed=3)
     _, kept, roff = _compress_inputs(off, items, lut)
