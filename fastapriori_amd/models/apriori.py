@@ -711,7 +711,8 @@ class FastApriori:
         else:
             nb = (F1 + 255) // 256
             self.stats["pair_hbm_bytes_est"] = int(2 * (4 * nnz + 8 * T) + nnz * (nb + 1) + T * nb * (nb + 1))
-        if self.comm.distributed and flat.numel() >= PAIR_RS_MIN:
+        # read at call time: spawned test ranks set FA_PAIR_RS_MIN after importing this module
+        if self.comm.distributed and flat.numel() >= int(os.environ.get("FA_PAIR_RS_MIN", PAIR_RS_MIN)):
             # X12 as reduce-scatter + local threshold + all-gather of the survivors
             # (F_2 << C_2): each rank thresholds its 1/world slice of the summed triangle
             keep, vals = self.comm.reduce_scatter_select(flat, mc, bound=self.stats["n_lines"])

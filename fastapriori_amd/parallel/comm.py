@@ -102,8 +102,10 @@ class Comm:
         mx = int(sizes.max())
         buf = torch.zeros((2, max(mx, 1)), dtype=torch.int64, device=dev)
         buf[:, :mine.shape[1]] = mine
-        out = torch.empty((W, 2, max(mx, 1)), dtype=torch.int64, device=dev)
-        dist.all_gather_into_tensor(out, buf)
+        # flat buffers: gloo's all_gather_into_tensor takes only the concatenated form
+        out = torch.empty(W * buf.numel(), dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(out, buf.view(-1))
+        out = out.view(W, 2, max(mx, 1))
         self.bytes_reduced += int(sizes.sum()) * 16
         got = torch.cat([out[r, :, :int(sizes[r])] for r in range(W)], dim=1)
         return got[0], got[1]
