@@ -219,7 +219,7 @@ class FastApriori:
                 mark[self._bundle_rows[0].ravel()] = True
                 used = np.flatnonzero(mark)
                 with tm.phase(f"trim{k}"), roctx_range("trim"):
-                    self._trim(db, used, k)
+                    self._trim(db, used, k, sum(int(b[4].size) for b in bundle))
                 with tm.phase("count"), roctx_range("count"):
                     cnts = self._count_bundle(db, bundle)
                 if tm.sync:
@@ -569,13 +569,16 @@ class FastApriori:
         wword = torch.repeat_interleave(cls_w.to(torch.int32), padded // 64)
         db.update(src=src, ncols=ncols, wword=wword)
 
-    def _trim_worth_it(self, db, used: np.ndarray, k: int) -> bool:
+    def _trim_worth_it(self, db, used: np.ndarray, k: int, C: int = 0) -> bool:
         """Binomial estimate of the rows that would survive trimming.
 
         Item occurrences survive with probability p = (occurrences of the level's
         candidate items) / (occurrences of the items still in the rows); a row of
         length L keeps >= k of them with probability P[Binom(L, p) >= k].  Trimming
-        costs two passes over the rows, so it runs only when it removes a lot.
+        costs two passes over the rows (and a rebuild of the bitmaps), so it runs
+        only when it removes a lot.  A level of C candidates that needs several
+        accumulator passes streams its slabs from the used items' bitmap, whose size
+        depends on the rows only: then dropped items do not count.
         """
         if db["T"] < self.cfg.trim_min_rows:   # a trim's fixed cost (2 launches + a host sync) dominates
             return False
@@ -595,19 +598,22 @@ class FastApriori:
             sf[ok] = betainc(k, L[ok] - k + 1, min(p, 1.0))
         est_rows = float((hist * sf).sum())
         est_nnz = float((hist * L * p).sum())
-        return est_rows < 0.75 * max(db["T"], 1) or est_nnz < 0.6 * max(int(db["ranks"].numel()), 1)
+        rows_ok = est_rows < 0.75 * max(db["T"], 1)
+        if C and db["ranks"].is_cuda and C > ops.primitives.slab_capacity(int(used.size), C):
+            return rows_ok
+        return rows_ok or est_nnz < 0.6 * max(int(db["ranks"].numel()), 1)
 
     def _len_hist(self, db) -> np.ndarray:
         lens = db["roff"][1:] - db["roff"][:-1]
         return torch.bincount(lens).cpu().numpy() if lens.numel() else np.zeros(1, np.int64)
 
-    def _trim(self, db, used: np.ndarray, k: int) -> None:
+    def _trim(self, db, used: np.ndarray, k: int, C: int = 0) -> None:
         """Transaction trimming before level k (items outside C_k, rows with < k of them)."""
         if not self.cfg.trim or db["T"] == 0:
             return
         if "len_hist" not in db:
             db["len_hist"] = self._len_hist(db)
-        if not self._trim_worth_it(db, used, k):
+        if not self._trim_worth_it(db, used, k, C):
             return
         dev = db["ranks"].device
         alive = torch.zeros(db["F1"], dtype=torch.int8)
