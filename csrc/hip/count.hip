@@ -631,9 +631,66 @@ __device__ __forceinline__ void pair_rows16_chunk_t(PairRowsLds& L, const uint8_
       sa[wv][lane + 64 * k] = X.da[k];
       if (!diag) sb[wv][lane + 64 * k] = X.db[k];
     }
-    const unsigned long long M = __ballot(ci > 0);
-    if (ci > 0) rowtab[wv][__popcll(M & lt)] = (uint8_t)lane;
+    // flattened pairs (staged batches): one lane per (row, pair) instead of per
+    // (row, position) -- see the flat branch below; rowtab then lists the rows with pairs
+    const bool flat = stA && stB && !(dbg & (8 | 16));
+    const int npr = diag ? ci * (ci - 1) / 2 : ci * cj;
+    const bool own = flat ? npr > 0 : ci > 0;
+    const unsigned long long M = __ballot(own);
+    if (own) rowtab[wv][__popcll(M & lt)] = (uint8_t)lane;
     wave_lds_sync();
+    if (flat) {
+      // Pair t of row r (t < npr) is enumerated with the row's item in block bi
+      // varying fastest, so consecutive lanes hit different tile rows (bank
+      // swizzle of pair_tile16_word):
+      //   off-diagonal: t = j * ci + i (i < ci, j < cj);  diagonal: t = j (j - 1) / 2 + i
+      //   (i < j < ci), decoded with a float square root and a +-1 fix-up.
+      // The owner row of flat index f comes from the row-start masks of its 64-wide
+      // window, as the positions do in run_windows.
+      const int incp = wave_scan_incl_dpp(npr);
+      const int NP = wave_last(incp);
+      const int pst = incp - npr;
+      const int a0 = inci - ci, b0 = diag ? a0 : incj - cj;
+      const int packed = a0 | (b0 << 10) | (ci << 20);
+      const uint8_t* As = reinterpret_cast<const uint8_t*>(sa[wv]) + sha;
+      const uint8_t* Bs = diag ? As : reinterpret_cast<const uint8_t*>(sb[wv]) + shb;
+      const int srel = npr > 0 ? pst : -(1 << 30);
+      int cs = 0;
+      for (int f0 = 0; f0 < NP; f0 += 256) {
+        unsigned long long S[4];
+        window_starts<4>(swd[wv], srel, f0, S);
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const int fb = f0 + 64 * w;
+          if (fb >= NP) break;
+          const int kk = cs + __popcll(S[w] & le) - 1;
+          cs += __popcll(S[w]);
+          const int row = rowtab[wv][kk & 63];
+          const int p_st = __shfl(pst, row, 64);
+          const int px = __shfl(packed, row, 64);
+          const int f = fb + lane;
+          const int t = f - p_st;
+          const int c = (px >> 20) & 0xFF;
+          int i, j;
+          if (diag) {
+            j = (int)((1.0f + __builtin_sqrtf(8.0f * (float)t + 1.0f)) * 0.5f);
+            if (j * (j - 1) / 2 > t) --j;
+            else if (j * (j + 1) / 2 <= t) ++j;
+            i = t - j * (j - 1) / 2;
+          } else {
+            j = (int)(((float)t + 0.5f) * __builtin_amdgcn_rcpf((float)c));
+            i = t - j * c;
+          }
+          if (f < NP && !(dbg & 1)) {
+            const int a = (int)As[(px & 0x3FF) + i];
+            const int b = (int)Bs[((px >> 10) & 0x3FF) + j];
+            atomicAdd(&tile[a * (kPB16 / 2) + ((b >> 1) ^ (a & 31))], (b & 1) ? 0x10000u : 1u);
+          }
+        }
+      }
+      wave_lds_sync();
+      return;
+    }
     const int jbeg = diag ? 0 : incj - cj;          // row owner view: my row's block-bj span
     const int jend = diag ? inci : incj;
     const int srow = ci > 0 ? inci - ci : -(1 << 30);
@@ -2296,7 +2353,9 @@ FA_API int fa_hip_pair_queue16(const uint8_t* cnt, const int64_t* base, const ui
   }
   n_wg = (int)std::min<int64_t>(n_wg, (int64_t)nsub * nbp);
   hipLaunchKernelGGL(k_pair_queue16, dim3((unsigned)n_wg), dim3(64 * kPW), 0, st, cnt, base, lr, T, nbatch, F1, ld,
-                     nb, nbp, qctr, nsub, out, getenv("FA_PAIR_DEBUG") ? atoi(getenv("FA_PAIR_DEBUG")) : 0);
+                     nb, nbp, qctr, nsub, out,
+                     (getenv("FA_PAIR_DEBUG") ? atoi(getenv("FA_PAIR_DEBUG")) : 0) |
+                         (getenv("FA_PAIR_FLAT") && atoi(getenv("FA_PAIR_FLAT")) == 0 ? 16 : 0));
   FA_LAUNCH_RET();
 }
 
