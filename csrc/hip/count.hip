@@ -633,7 +633,7 @@ __device__ __forceinline__ void pair_rows16_chunk_t(PairRowsLds& L, const uint8_
     }
     // flattened pairs (staged batches): one lane per (row, pair) instead of per
     // (row, position) -- see the flat branch below; rowtab then lists the rows with pairs
-    const bool flat = stA && stB && !(dbg & (8 | 16));
+    const bool flat = stA && stB && !(dbg & (8 | 16)) && !(dbg & (diag ? 32 : 64));
     const int npr = diag ? ci * (ci - 1) / 2 : ci * cj;
     const bool own = flat ? npr > 0 : ci > 0;
     const unsigned long long M = __ballot(own);
@@ -2079,6 +2079,12 @@ FA_API int fa_hip_pair_horizontal(const int64_t* roff, const int32_t* ranks, int
 }
 
 // Unit-weight Gram on the matrix cores (k_pair_gram_mfma); out: u32 [F1][F1] (upper triangle).
+// FA_PAIR_FLAT: 2 (default) flattened pairs in the off-diagonal tiles only, 1 in every
+// tile, 0 none, 3 diagonal tiles only -> k_pair_queue16 dbg bits 16 / 32 / 64.
+// Measured (T10I4D100M pair call): 2 13.7, 1 13.9, 0 14.5, 3 14.8 ms -- in diagonal
+// tiles the per-position loops (trip counts L-1-i) beat the square-root decode.
+static int pair_flat_bits(int v) { return v == 0 ? 16 : v == 2 ? 32 : v == 3 ? 64 : 0; }
+
 FA_API int fa_hip_pair_gram_mfma(const uint64_t* bm, int32_t F1, int64_t Wp, int64_t W, uint32_t* out,
                                  int target_wgs, hipStream_t st) {
   if (W <= 0 || F1 < 2) return 0;
@@ -2355,7 +2361,7 @@ FA_API int fa_hip_pair_queue16(const uint8_t* cnt, const int64_t* base, const ui
   hipLaunchKernelGGL(k_pair_queue16, dim3((unsigned)n_wg), dim3(64 * kPW), 0, st, cnt, base, lr, T, nbatch, F1, ld,
                      nb, nbp, qctr, nsub, out,
                      (getenv("FA_PAIR_DEBUG") ? atoi(getenv("FA_PAIR_DEBUG")) : 0) |
-                         (getenv("FA_PAIR_FLAT") && atoi(getenv("FA_PAIR_FLAT")) == 0 ? 16 : 0));
+                         pair_flat_bits(getenv("FA_PAIR_FLAT") ? atoi(getenv("FA_PAIR_FLAT")) : 2));
   FA_LAUNCH_RET();
 }
 
