@@ -544,9 +544,9 @@ __global__ __launch_bounds__(1024) void k_pair_blocked16(
 // compaction table of the non-empty rows, so the dependency chain per pair is
 // one LDS byte read and one LDS atomic.
 // ---------------------------------------------------------------------------
-constexpr int kRowsDw = 3;                  // staged dwords per lane and block
-constexpr int kRowsStage = 64 * kRowsDw * 4; // 768 staged local-rank bytes per wave and block
-constexpr int kRowsWin = kRowsStage / 64;    // 12 windows
+constexpr int kRowsDw = 2;                  // staged dwords per lane and block
+constexpr int kRowsStage = 64 * kRowsDw * 4; // 512 staged local-rank bytes per wave and block
+constexpr int kRowsWin = kRowsStage / 64;    // 8 windows
 
 // Batches [q0, q1) of tile (bi, bj) into the packed-u16 LDS tile (no barriers).
 struct PairRowsLds {
@@ -555,6 +555,7 @@ struct PairRowsLds {
   uint32_t sb[kPW][kRowsStage / 4];
   uint8_t rowtab[kPW][64];
   unsigned long long swd[kPW][kRowsWin];
+  int2 rowinfo[kPW][64];   // flattened pairs: (pair start, A start | B start << 10 | ci << 20) per row with pairs
 };
 
 // kDiag (bi == bj) is a template parameter: a runtime select between the two
@@ -637,7 +638,15 @@ __device__ __forceinline__ void pair_rows16_chunk_t(PairRowsLds& L, const uint8_
     const int npr = diag ? ci * (ci - 1) / 2 : ci * cj;
     const bool own = flat ? npr > 0 : ci > 0;
     const unsigned long long M = __ballot(own);
-    if (own) rowtab[wv][__popcll(M & lt)] = (uint8_t)lane;
+    const int incp = flat ? wave_scan_incl_dpp(npr) : 0;
+    if (own) {
+      if (flat) {
+        const int a0 = inci - ci, b0 = diag ? a0 : incj - cj;
+        L.rowinfo[wv][__popcll(M & lt)] = make_int2(incp - npr, a0 | (b0 << 10) | (ci << 20));
+      } else {
+        rowtab[wv][__popcll(M & lt)] = (uint8_t)lane;
+      }
+    }
     wave_lds_sync();
     if (flat) {
       // Pair t of row r (t < npr) is enumerated with the row's item in block bi
@@ -647,11 +656,8 @@ __device__ __forceinline__ void pair_rows16_chunk_t(PairRowsLds& L, const uint8_
       //   (i < j < ci), decoded with a float square root and a +-1 fix-up.
       // The owner row of flat index f comes from the row-start masks of its 64-wide
       // window, as the positions do in run_windows.
-      const int incp = wave_scan_incl_dpp(npr);
       const int NP = wave_last(incp);
       const int pst = incp - npr;
-      const int a0 = inci - ci, b0 = diag ? a0 : incj - cj;
-      const int packed = a0 | (b0 << 10) | (ci << 20);
       const uint8_t* As = reinterpret_cast<const uint8_t*>(sa[wv]) + sha;
       const uint8_t* Bs = diag ? As : reinterpret_cast<const uint8_t*>(sb[wv]) + shb;
       const int srel = npr > 0 ? pst : -(1 << 30);
@@ -665,9 +671,8 @@ __device__ __forceinline__ void pair_rows16_chunk_t(PairRowsLds& L, const uint8_
           if (fb >= NP) break;
           const int kk = cs + __popcll(S[w] & le) - 1;
           cs += __popcll(S[w]);
-          const int row = rowtab[wv][kk & 63];
-          const int p_st = __shfl(pst, row, 64);
-          const int px = __shfl(packed, row, 64);
+          const int2 ri = L.rowinfo[wv][kk & 63];
+          const int p_st = ri.x, px = ri.y;
           const int f = fb + lane;
           const int t = f - p_st;
           const int c = (px >> 20) & 0xFF;
