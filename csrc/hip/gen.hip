@@ -676,17 +676,19 @@ __global__ __launch_bounds__(256) void k_agd_insert(const int32_t* __restrict__ 
                                                     uint32_t mask, const long long* __restrict__ c, int l) {
   if (c[0]) return;
   const int64_t n = c[8 + l];
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int32_t* r = P + i * m;
-  if (i > 0) {
-    const int32_t* pr = P + (i - 1) * m;
-    bool same = true;
-    for (int q = 0; q < m - 1; ++q) same = same && r[q] == pr[q];
-    if (same) return;
+  // grid-stride (the grid is sized for the level's bound, capped: a stopped chain's
+  // launches then cost a few workgroups each)
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t* r = P + i * m;
+    if (i > 0) {
+      const int32_t* pr = P + (i - 1) * m;
+      bool same = true;
+      for (int q = 0; q < m - 1; ++q) same = same && r[q] == pr[q];
+      if (same) continue;
+    }
+    uint32_t at = (uint32_t)ag_hash_drop(r, m, m - 1) & mask;
+    while (atomicCAS(&table[at], -1, (int32_t)i) != -1) at = (at + 1) & mask;
   }
-  uint32_t at = (uint32_t)ag_hash_drop(r, m, m - 1) & mask;
-  while (atomicCAS(&table[at], -1, (int32_t)i) != -1) at = (at + 1) & mask;
 }
 
 __global__ __launch_bounds__(256) void k_agd_ext(const int32_t* __restrict__ P, int m,
@@ -695,12 +697,12 @@ __global__ __launch_bounds__(256) void k_agd_ext(const int32_t* __restrict__ P, 
                                                  int l) {
   if (c[0]) return;
   const int64_t n = c[8 + l];
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int32_t* r = P + i * m;
-  const int32_t s = ag_find(P, m, table, mask, r, m - 1);
-  const int32_t y = r[m - 1];
-  atomicOr(&ext[(int64_t)s * nw + (y >> 6)], 1ull << (y & 63));
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t* r = P + i * m;
+    const int32_t s = ag_find(P, m, table, mask, r, m - 1);
+    const int32_t y = r[m - 1];
+    atomicOr(&ext[(int64_t)s * nw + (y >> 6)], 1ull << (y & 63));
+  }
 }
 
 // kEmit = false: cnt[i] = extensions of row i;  true (accepted levels only): ext ids at
@@ -822,15 +824,15 @@ static int ag_chain_dev(const int32_t* P1, int64_t n1, int m1, int nw, char* w0,
       nb = cb;
       ++m;
     }
-    hipLaunchKernelGGL(k_agd_clear, dim3((unsigned)std::min<int64_t>((clr_max + 255) / 256, 2048)), dim3(256), 0, st,
+    hipLaunchKernelGGL(k_agd_clear, dim3((unsigned)std::min<int64_t>((clr_max + 255) / 256, 1024)), dim3(256), 0, st,
                        clr, c);
     for (int l = l0; l <= l1; ++l) {
       const Bufs& b = bf[l - l0];
       const int ml = lv[l].m;
-      const dim3 g((unsigned)((b.nb + 255) / 256));
+      const dim3 g((unsigned)std::min<int64_t>((b.nb + 255) / 256, 512));
       hipLaunchKernelGGL(k_agd_insert, g, dim3(256), 0, st, P, ml, b.table, b.cap - 1, c, l);
       hipLaunchKernelGGL(k_agd_ext, g, dim3(256), 0, st, P, ml, b.table, b.cap - 1, nw, b.ext, c, l);
-      const unsigned nwg = (unsigned)std::min<int64_t>((b.nb + 3) / 4, 65536);
+      const unsigned nwg = (unsigned)std::min<int64_t>((b.nb + 3) / 4, 2048);
       hipLaunchKernelGGL(k_agd_rows<false>, dim3(nwg), dim3(256), 0, st, P, ml, b.table, b.cap - 1, nw, b.ext,
                          lv[l].cnt, b.off, lv[l].rows, c, l);
       hipLaunchKernelGGL(k_agd_scan_decide, dim3(1), dim3(1024), 0, st, lv[l].cnt, b.off, c, l, growth, b.cb);

@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256) void k_txn_freq_count_span(const int64_t* __re
                                                              const int32_t* __restrict__ lut,
                                                              int32_t* __restrict__ cnt) {
   constexpr int PER = SPAN / 256;
-  __shared__ uint8_t fl[SPAN];
+  __shared__ __attribute__((aligned(16))) uint8_t fl[SPAN];
   const int64_t x0 = (int64_t)blockIdx.x * 256;
   const int64_t x1 = min(n, x0 + 256);
   const int64_t x = x0 + threadIdx.x;
@@ -149,8 +149,19 @@ __global__ __launch_bounds__(256) void k_txn_freq_count_span(const int64_t* __re
     }
     __syncthreads();
     if (x < x1) {
+      // the row's flag bytes [s, e) read a dword at a time (flags are 0 / 1 bytes:
+      // popcount of the masked dword = number of frequent tokens in it)
       int32_t c = 0;
-      for (int64_t j = s - base; j < e - base; ++j) c += fl[j];
+      const int sr = (int)(s - base), er = (int)(e - base);
+      if (er > sr) {
+        const uint32_t* fw = reinterpret_cast<const uint32_t*>(fl);
+        const int w0 = sr >> 2, w1 = (er - 1) >> 2;
+        for (int w = w0; w <= w1; ++w) {
+          const int lo = w == w0 ? (sr & 3) : 0, hi = w == w1 ? ((er - 1) & 3) + 1 : 4;
+          const uint32_t m = (hi == 4 ? 0xFFFFFFFFu : ((1u << (8 * hi)) - 1u)) & ~((1u << (8 * lo)) - 1u);
+          c += __popc(fw[w] & m);
+        }
+      }
       cnt[x] = c;
     }
   } else if (x < x1) {
