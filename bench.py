@@ -27,6 +27,7 @@ world size must equal N or the run fails.
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import shutil
@@ -228,6 +229,10 @@ def main() -> int:
     res = None
     for _ in range(args.warmup):
         res = miner.run(shard)
+    # long-lived objects (the shard, the miner, torch/numpy state) out of the cyclic GC's
+    # scans: collections between the timed runs then stay cheap
+    gc.collect()
+    gc.freeze()
     sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):

@@ -24,6 +24,7 @@ are replicated, so the only traffic is one count vector per level.
 """
 from __future__ import annotations
 
+import gc
 import math
 import os
 import time
@@ -124,6 +125,18 @@ class FastApriori:
 
     # ------------------------------------------------------------------
     def run(self, shard: TransactionShard, resume: MiningResult | None = None) -> MiningResult:
+        # no cyclic-GC passes inside a run: a generation-2 collection over the torch /
+        # numpy heap costs milliseconds of host time between kernels (the run's own
+        # temporaries are freed by reference counting)
+        gc_on = gc.isenabled()
+        gc.disable()
+        try:
+            return self._run(shard, resume)
+        finally:
+            if gc_on:
+                gc.enable()
+
+    def _run(self, shard: TransactionShard, resume: MiningResult | None = None) -> MiningResult:
         t_start = time.perf_counter()
         dev = shard.items.device
         # candidate parallelism: the data is replicated, so data-side collectives
