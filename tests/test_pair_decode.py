@@ -1,8 +1,8 @@
 """Index decode of the flattened pair enumeration in k_pair_queue16 (csrc/hip/count.hip),
 checked exhaustively in float32 for every row length the u8 block counts allow (<= 255):
 
-* off-diagonal tiles: pair t = j * ci + i  ->  j = int((t + 0.5) * rcp(ci)), i = t - j * ci
-  (also with the reciprocal one ulp off: v_rcp_f32 is not correctly rounded);
+* off-diagonal tiles: pair t = j * ci + i  ->  j = mulhi(t << 8, ceil(2^24 / ci)), i = t - j * ci
+  (and the earlier float form j = int((t + 0.5) * rcp(ci)), also with the reciprocal one ulp off);
 * diagonal tiles: t = j (j - 1) / 2 + i, i < j  ->  j = int((1 + sqrt(8 t + 1)) / 2) with a +-1
   fix-up (also with the square root one ulp off).
 """
@@ -27,3 +27,12 @@ def test_diag_decode_exhaustive():
         j = np.where(j * (j - 1) // 2 > t, j - 1, np.where(j * (j + 1) // 2 <= t, j + 1, j))
         i = t - j * (j - 1) // 2
         assert ((i >= 0) & (i < j) & (j * (j - 1) // 2 + i == t)).all()
+
+
+def test_offdiag_magic_decode_exhaustive():
+    for c in range(2, 256):
+        m = (0x1000000 + c - 1) // c
+        assert m < (1 << 24)
+        t = np.arange(c * 255, dtype=np.uint64)
+        j = ((t << np.uint64(8)) * np.uint64(m)) >> np.uint64(32)
+        assert np.array_equal(j, t // np.uint64(c)), c
