@@ -1591,8 +1591,11 @@ template <int SW, bool kWeighted, int kBuild, bool kAcc16>
 __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
     const int64_t* __restrict__ roff, const int32_t* __restrict__ ranks, const int32_t* __restrict__ src,
     int64_t ncols, const int32_t* __restrict__ item_map, int F1, int n_used, const int32_t* __restrict__ gpre,
-    const int4* __restrict__ rec, int G, int C, const int32_t* __restrict__ wword, uint32_t* __restrict__ out,
-    const uint64_t* __restrict__ bm, int64_t Wp, const int32_t* __restrict__ bm_rows, int dbg) {
+    const int4* __restrict__ rec, int G_arg, int C, const int32_t* __restrict__ wword, uint32_t* __restrict__ out,
+    const uint64_t* __restrict__ bm, int64_t Wp, const int32_t* __restrict__ bm_rows, int dbg,
+    const int32_t* __restrict__ g_dev) {
+  // g_dev: the piece count from device memory (device-planned bundles, levels.hip)
+  const int G = g_dev ? *g_dev : G_arg;
   extern __shared__ uint4 lds4[];
   __shared__ unsigned long long build_words[kSlabThreads / 64 * 2];
   constexpr int SWP = SW + 2;                       // row stride: odd number of 16-B slots
@@ -2184,11 +2187,14 @@ FA_API int fa_hip_count_slab(const int64_t* roff, const int32_t* ranks, const in
 // Slab counting from piece records (k_count_slab_rec; records: plan.cpp, 3 x int4
 // per piece).  LDS: slab + accumulator (16-B aligned) + u16 map when F1 <= 8192
 // and the slab is built from contiguous rows.  Returns 3 when that exceeds the LDS.
+// g_dev (optional): the piece count read by the kernel from device memory (G is then
+// ignored; device-planned bundles, levels.hip fa_hip_dl_plan).
 FA_API int fa_hip_count_slab_rec(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
                                  const int32_t* item_map, int F1, int n_used, const int32_t* gpre, const void* rec,
                                  int G, int C, const int32_t* wword, uint32_t* out, int sw, int n_wg,
-                                 const uint64_t* bm, int64_t Wp, hipStream_t st, const int32_t* bm_rows, int acc16) {
-  if (G <= 0 || C <= 0 || ncols <= 0) return 0;
+                                 const uint64_t* bm, int64_t Wp, hipStream_t st, const int32_t* bm_rows, int acc16,
+                                 const int32_t* g_dev) {
+  if ((G <= 0 && !g_dev) || C <= 0 || ncols <= 0) return 0;
   const int64_t n_acc = acc16 ? (C + 1) / 2 : C;
   const bool contig = !bm && !src;
   const size_t map_b = (contig && F1 <= kMapLdsMax) ? (size_t)(((int64_t)F1 * 2 + 15) & ~(int64_t)15) : 0;
@@ -2196,7 +2202,7 @@ FA_API int fa_hip_count_slab_rec(const int64_t* roff, const int32_t* ranks, cons
   if (lds > 160 * 1024 - 256) return 3;             // static build_words scratch
   using KernT = void (*)(const int64_t*, const int32_t*, const int32_t*, int64_t, const int32_t*, int, int,
                          const int32_t*, const int4*, int, int, const int32_t*, uint32_t*, const uint64_t*, int64_t,
-                         const int32_t*, int);
+                         const int32_t*, int, const int32_t*);
   KernT kern = nullptr;
 #define FA_REC_MODE(S, B)                                                                       \
   kern = wword ? (KernT)k_count_slab_rec<S, true, B, false>                                     \
@@ -2217,7 +2223,7 @@ FA_API int fa_hip_count_slab_rec(const int64_t* roff, const int32_t* ranks, cons
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const int dbg = getenv("FA_SLAB_DEBUG") ? atoi(getenv("FA_SLAB_DEBUG")) : 0;
   hipLaunchKernelGGL(kern, dim3((unsigned)n_wg), dim3(kSlabThreads), lds, st, roff, ranks, src, ncols, item_map, F1,
-                     n_used, gpre, (const int4*)rec, G, C, wword, out, bm, Wp, bm_rows, dbg);
+                     n_used, gpre, (const int4*)rec, G, C, wword, out, bm, Wp, bm_rows, dbg, g_dev);
   FA_LAUNCH_RET();
 }
 

@@ -858,3 +858,267 @@ static int ag_chain_dev(const int32_t* P1, int64_t n1, int m1, int nw, char* w0,
   sizes[0] = L;
   FA_LAUNCH_RET();
 }
+
+// ---------------------------------------------------------------------------
+// Device-resident level bundles (fastapriori_amd FastApriori._mine_device).
+//
+// The host loop above reads every bundle's candidate rows back, plans the count
+// in C++ and thresholds on the host: ~2 ms of GPU idle per run, most of the
+// 12.5M-row shard's host gap.  Here the candidates never leave the GPU: level 0
+// of a bundle is generated from F_{k-1} rows that are themselves on the device
+// (the previous bundle's thresholded output, or F_2), its row count comes from
+// a device word, and the host learns only what it must decide on: C_0, the
+// used-item bitset (trimming, slab width) and whether level k alone fits one
+// accumulator pass.  The speculative levels 1.. follow with the batched device
+// acceptance of ag_chain_dev, without copying any level out.  Planning
+// (levels.hip fa_hip_dl_plan), counting and thresholding (fa_hip_dl_threshold)
+// then run on the same stream.
+//   ctl (device int64 [kDlCtl]): 0 stop  1 accepted levels  2 total  3 last C
+//     5 multi (level 0 needs several accumulator passes: host path)  6 n_used
+//     7 end (|F_{k-1}| < k or C_0 = 0: mining is over)  8 + l: n_l  40 + l: C_l
+//     128 .. 191: used-item bitset of level 0 (4096 bits)
+// ---------------------------------------------------------------------------
+namespace fa {
+
+constexpr int kDlCtl = 256;
+
+__device__ int64_t agd_block_scan(const int32_t* __restrict__ cnt, int64_t* __restrict__ off, int64_t n) {
+  // exclusive offsets off[0 .. n] of cnt[0 .. n) by one 1024-thread workgroup; returns off[n]
+  __shared__ int64_t part[16];
+  __shared__ int64_t carry;
+  if (threadIdx.x == 0) { carry = 0; off[0] = 0; }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int64_t b = 0; b < n; b += 1024) {
+    const int64_t i = b + threadIdx.x;
+    const int v = i < n ? cnt[i] : 0;
+    const int incl = wave_scan_incl_dpp(v);
+    if (lane == 63) part[wv] = incl;
+    __syncthreads();
+    int64_t before = carry;
+    for (int q = 0; q < wv; ++q) before += part[q];
+    if (i < n) off[i + 1] = before + incl;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = before + incl;
+    __syncthreads();
+  }
+  return carry;
+}
+
+__global__ __launch_bounds__(kDlCtl) void k_dl_setup0(long long* __restrict__ c, const long long* __restrict__ n_src,
+                                                      int64_t n_const, int kmin) {
+  c[threadIdx.x] = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int64_t n = n_src ? (int64_t)n_src[0] : n_const;
+    c[8] = n;
+    c[7] = n < kmin ? 1 : 0;       // the reference's loop test |F_{k-1}| >= k (FastApriori.scala:111)
+    c[0] = c[7];
+  }
+}
+
+// level 0: the exclusive scan, then C_0 > c_bound (the level's output buffer, sized for
+// one accumulator pass) marks it "multi" (host path); C_0 = 0 ends the mining
+__global__ __launch_bounds__(1024) void k_dl_decide0(const int32_t* __restrict__ cnt, int64_t* __restrict__ off,
+                                                      long long* __restrict__ c, int64_t c_bound) {
+  if (c[0]) return;
+  const int64_t C = agd_block_scan(cnt, off, c[8]);
+  if (threadIdx.x != 0) return;
+  c[40] = C;
+  if (C == 0) { c[7] = 1; c[0] = 1; return; }
+  if (C > c_bound) { c[5] = 1; c[0] = 1; return; }
+  c[1] = 1; c[2] = C; c[3] = C; c[9] = C;
+}
+
+// used items of level 0's candidate rows (LDS-privatised, one global atomicOr per word)
+__global__ __launch_bounds__(256) void k_dl_mark(const int32_t* __restrict__ rows, int m1,
+                                                 long long* __restrict__ c) {
+  __shared__ uint32_t lb[128];
+  if (c[0] && !c[5]) return;         // (a multi level still reports its used items)
+  if (threadIdx.x < 128) lb[threadIdx.x] = 0u;
+  __syncthreads();
+  const int64_t n = c[5] ? 0 : c[40] * (int64_t)m1;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    atomicOr(&lb[rows[i] >> 5], 1u << (rows[i] & 31));
+  __syncthreads();
+  uint32_t* mk = reinterpret_cast<uint32_t*>(c + 128);
+  if (threadIdx.x < 128 && lb[threadIdx.x]) atomicOr(&mk[threadIdx.x], lb[threadIdx.x]);
+}
+
+// n_used, and whether level 0 alone exceeds one accumulator pass
+__global__ void k_dl_post0(long long* __restrict__ c, double lds) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const uint32_t* mk = reinterpret_cast<const uint32_t*>(c + 128);
+  int64_t n_used = 0;
+  for (int q = 0; q < 128; ++q) n_used += __popc(mk[q]);
+  c[6] = n_used;
+  if (c[1] == 1 && c[40] > d_slab_cap(n_used, c[40], lds)) { c[5] = 1; c[0] = 1; }
+}
+
+// acceptance of speculative level l >= 1 (same rule as k_agd_scan_decide, with the
+// exact one-pass test total + C <= slab capacity(n_used, total + C))
+__global__ __launch_bounds__(1024) void k_dl_decide(const int32_t* __restrict__ cnt, int64_t* __restrict__ off,
+                                                     long long* __restrict__ c, int l, double growth, int64_t c_bound,
+                                                     double lds) {
+  if (c[0]) return;
+  const int64_t C = agd_block_scan(cnt, off, c[8 + l]);
+  if (threadIdx.x != 0) return;
+  const int64_t total = c[2], last = c[3];
+  if (C == 0 || (double)C > growth * (double)last || C > c_bound || total + C > d_slab_cap(c[6], total + C, lds)) {
+    c[0] = 1;
+    return;
+  }
+  c[40 + l] = C;
+  c[1] = l + 1;
+  c[2] = total + C;
+  c[3] = C;
+  c[8 + l + 1] = C;
+}
+
+}  // namespace fa
+
+// Level 0 of a device bundle: candidates of F_{k-1} = P0 [n][m0] (device; n from
+// n_src[0] when given, else n_const; n_bound >= n sizes the buffers), generated
+// into the front of ws, then ONE synchronisation: ctl is copied to ctl_host.
+// c_bound: the largest C_0 the level may have (one accumulator pass); a larger
+// level is reported as multi (ctl[5]) without its rows.  lds: LDS bytes the slab
+// kernel has for slab + accumulators.  info (int64 out): 0 ws bytes used,
+// 1 cnt (ext ids at cnt + n), 2 off, 3 candidate rows [C_0][m0 + 1].
+// Returns 0, 1 (bad arguments) or 5 (ws too small: info[0] = bytes needed).
+FA_API int fa_hip_dl_level0(const int32_t* P0, const long long* n_src, int64_t n_const, int64_t n_bound, int m0,
+                            int F1, void* ws, int64_t ws_bytes, long long* ctl, long long* ctl_host,
+                            int64_t c_bound, double lds, int64_t* info, hipStream_t st) {
+  if (m0 < 2 || F1 > 4096 || F1 < 1 || n_bound < 0 || c_bound < 1) return 1;
+  auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
+  const int nw = (F1 + 63) / 64;
+  const int64_t nb = std::max<int64_t>(n_bound, 1);
+  uint32_t cap = 16;
+  while (cap < 2 * (uint64_t)nb) cap <<= 1;
+  const int64_t need = al(4 * (int64_t)cap) + al(8 * nb * nw) + al(8 * (nb + 1)) + al(4 * (nb + c_bound)) +
+                       al(4 * c_bound * (m0 + 1));
+  info[0] = need;
+  if (need > ws_bytes) return 5;
+  char* w = static_cast<char*>(ws);
+  int32_t* table = reinterpret_cast<int32_t*>(w); w += al(4 * (int64_t)cap);
+  unsigned long long* ext = reinterpret_cast<unsigned long long*>(w); w += al(8 * nb * nw);
+  int64_t* off = reinterpret_cast<int64_t*>(w); w += al(8 * (nb + 1));
+  int32_t* cnt = reinterpret_cast<int32_t*>(w); w += al(4 * (nb + c_bound));
+  int32_t* rows = reinterpret_cast<int32_t*>(w);
+  info[1] = (int64_t)(intptr_t)cnt; info[2] = (int64_t)(intptr_t)off; info[3] = (int64_t)(intptr_t)rows;
+  hipLaunchKernelGGL(k_dl_setup0, dim3(1), dim3(kDlCtl), 0, st, ctl, n_src, n_const, m0 + 1);
+  AgdClear clr{};
+  clr.p[0] = reinterpret_cast<uint32_t*>(table); clr.len[0] = cap; clr.val[0] = ~0u;
+  clr.p[1] = reinterpret_cast<uint32_t*>(ext); clr.len[1] = 2 * nb * nw; clr.val[1] = 0u;
+  clr.nreg = 2;
+  const int64_t clr_max = std::max<int64_t>(cap, 2 * nb * nw);
+  hipLaunchKernelGGL(k_agd_clear, dim3((unsigned)std::min<int64_t>((clr_max + 255) / 256, 1024)), dim3(256), 0, st,
+                     clr, ctl);
+  const dim3 g((unsigned)std::min<int64_t>((nb + 255) / 256, 512));
+  hipLaunchKernelGGL(k_agd_insert, g, dim3(256), 0, st, P0, m0, table, cap - 1, ctl, 0);
+  hipLaunchKernelGGL(k_agd_ext, g, dim3(256), 0, st, P0, m0, table, cap - 1, nw, ext, ctl, 0);
+  const unsigned nwg = (unsigned)std::min<int64_t>((nb + 3) / 4, 2048);
+  hipLaunchKernelGGL(k_agd_rows<false>, dim3(nwg), dim3(256), 0, st, P0, m0, table, cap - 1, nw, ext, cnt, off, rows,
+                     ctl, 0);
+  hipLaunchKernelGGL(k_dl_decide0, dim3(1), dim3(1024), 0, st, cnt, off, ctl, c_bound);
+  hipLaunchKernelGGL(k_agd_rows<true>, dim3(nwg), dim3(256), 0, st, P0, m0, table, cap - 1, nw, ext, cnt, off, rows,
+                     ctl, 0);
+  hipLaunchKernelGGL(k_dl_mark, dim3((unsigned)std::min<int64_t>((c_bound * (m0 + 1) + 255) / 256, 1024)), dim3(256),
+                     0, st, rows, m0 + 1, ctl);
+  hipLaunchKernelGGL(k_dl_post0, dim3(1), dim3(64), 0, st, ctl, lds);
+  (void)hipMemcpyAsync(ctl_host, ctl, sizeof(long long) * kDlCtl, hipMemcpyDeviceToHost, st);
+  if (hipStreamSynchronize(st) != hipSuccess) return 7;
+  FA_LAUNCH_RET();
+}
+
+// Speculative levels 1 .. max_levels-1 of a device bundle after fa_hip_dl_level0
+// accepted level 0: batches of kAgdBatch levels sized by bounds, one ctl readback
+// per batch.  ws + ws_used is free; desc (int64 [kDlCtl / 8][8], host) holds level
+// 0 on entry and receives every accepted level l:
+//   0 parent rows P_l  1 cnt (ext ids at cnt + n_l)  2 off  3 candidate rows
+//   4 m_l (parent row length)  5 n_l  6 C_l  7 base (candidates of levels < l)
+// Returns 0 (ctl_host[1] = accepted levels incl. level 0), 5 (ws too small:
+// info[0] = bytes needed) or 7.
+FA_API int fa_hip_dl_more(int F1, void* ws, int64_t ws_bytes, int64_t ws_used, long long* ctl, long long* ctl_host,
+                          double growth, int max_levels, double lds, int64_t* desc, int64_t* info, hipStream_t st) {
+  using namespace fa;
+  auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
+  const int nw = (F1 + 63) / 64;
+  char* const w0 = static_cast<char*>(ws);
+  char* w = w0 + ws_used;
+  const int LM = std::min(max_levels, 31);
+  const int64_t acc_max = (int64_t)(lds / 4);
+  int64_t nb = desc[6];                                  // n_1 = C_0 (exact)
+  int m = (int)desc[4] + 1;
+  const int32_t* P = reinterpret_cast<const int32_t*>((intptr_t)desc[3]);
+  struct Lv { int32_t* cnt; int64_t* off; int32_t* rows; int m; };
+  Lv lv[32];
+  int done = 1;                                          // levels whose acceptance is known
+  for (int l0 = 1; l0 < LM && ctl_host[0] == 0; l0 += kAgdBatch) {
+    const int l1 = std::min(LM - 1, l0 + kAgdBatch - 1);
+    struct Bufs { int32_t* table; uint32_t cap; unsigned long long* ext; int64_t nb, cb; };
+    Bufs bf[kAgdBatch];
+    AgdClear clr{};
+    int64_t clr_max = 0;
+    for (int l = l0; l <= l1; ++l) {
+      const int64_t cb = std::min<int64_t>(acc_max, (int64_t)(growth * (double)nb) + 1);
+      uint32_t cap = 16;
+      while (cap < 2 * (uint64_t)nb) cap <<= 1;
+      const int64_t need = al(4 * (int64_t)cap) + al(8 * nb * nw) + al(8 * (nb + 1)) + al(4 * (nb + cb)) +
+                           al(4 * cb * (m + 1));
+      if ((w - w0) + need > ws_bytes) {
+        (void)hipStreamSynchronize(st);
+        info[0] = 2 * ((w - w0) + need);
+        return 5;
+      }
+      Bufs& b = bf[l - l0];
+      b.table = reinterpret_cast<int32_t*>(w); w += al(4 * (int64_t)cap);
+      b.ext = reinterpret_cast<unsigned long long*>(w); w += al(8 * nb * nw);
+      lv[l].off = reinterpret_cast<int64_t*>(w); w += al(8 * (nb + 1));
+      b.cap = cap; b.nb = nb; b.cb = cb;
+      lv[l].cnt = reinterpret_cast<int32_t*>(w); w += al(4 * (nb + cb));
+      lv[l].rows = reinterpret_cast<int32_t*>(w); w += al(4 * cb * (m + 1));
+      lv[l].m = m;
+      clr.p[clr.nreg] = reinterpret_cast<uint32_t*>(b.table); clr.len[clr.nreg] = cap; clr.val[clr.nreg++] = ~0u;
+      clr.p[clr.nreg] = reinterpret_cast<uint32_t*>(b.ext); clr.len[clr.nreg] = 2 * nb * nw; clr.val[clr.nreg++] = 0u;
+      clr_max = std::max<int64_t>(clr_max, std::max<int64_t>(cap, 2 * nb * nw));
+      nb = cb;
+      ++m;
+    }
+    hipLaunchKernelGGL(k_agd_clear, dim3((unsigned)std::min<int64_t>((clr_max + 255) / 256, 1024)), dim3(256), 0, st,
+                       clr, ctl);
+    for (int l = l0; l <= l1; ++l) {
+      const Bufs& b = bf[l - l0];
+      const int ml = lv[l].m;
+      const dim3 g((unsigned)std::min<int64_t>((b.nb + 255) / 256, 512));
+      hipLaunchKernelGGL(k_agd_insert, g, dim3(256), 0, st, P, ml, b.table, b.cap - 1, ctl, l);
+      hipLaunchKernelGGL(k_agd_ext, g, dim3(256), 0, st, P, ml, b.table, b.cap - 1, nw, b.ext, ctl, l);
+      const unsigned nwg = (unsigned)std::min<int64_t>((b.nb + 3) / 4, 2048);
+      hipLaunchKernelGGL(k_agd_rows<false>, dim3(nwg), dim3(256), 0, st, P, ml, b.table, b.cap - 1, nw, b.ext,
+                         lv[l].cnt, lv[l].off, lv[l].rows, ctl, l);
+      hipLaunchKernelGGL(k_dl_decide, dim3(1), dim3(1024), 0, st, lv[l].cnt, lv[l].off, ctl, l, growth, b.cb, lds);
+      hipLaunchKernelGGL(k_agd_rows<true>, dim3(nwg), dim3(256), 0, st, P, ml, b.table, b.cap - 1, nw, b.ext,
+                         lv[l].cnt, lv[l].off, lv[l].rows, ctl, l);
+      P = lv[l].rows;
+    }
+    (void)hipMemcpyAsync(ctl_host, ctl, sizeof(long long) * kDlCtl, hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) return 7;
+    done = l1 + 1;
+  }
+  (void)done;
+  const int L = (int)ctl_host[1];
+  int64_t base = desc[6];
+  for (int l = 1; l < L; ++l) {
+    int64_t* d = desc + 8 * l;
+    d[0] = desc[8 * (l - 1) + 3];
+    d[1] = (int64_t)(intptr_t)lv[l].cnt;
+    d[2] = (int64_t)(intptr_t)lv[l].off;
+    d[3] = (int64_t)(intptr_t)lv[l].rows;
+    d[4] = lv[l].m;
+    d[5] = ctl_host[8 + l];
+    d[6] = ctl_host[40 + l];
+    d[7] = base;
+    base += d[6];
+  }
+  info[0] = w - w0;
+  FA_LAUNCH_RET();
+}

@@ -1,0 +1,264 @@
+// Device-resident level bundles: planning and thresholding on the GPU
+// (fastapriori_amd FastApriori._mine_device; generation: gen.hip fa_hip_dl_level0 /
+// fa_hip_dl_more).
+//
+// Reference behaviour: FastApriori.scala:110-121 (the level loop), :143-154 (a
+// group (x, ys) ANDs its prefix x once and counts every extension y) and
+// :152-154 (keep support >= minCount).  The host version of this step
+// (csrc/host/plan.cpp fa_level_plan + a count readback + a host threshold) costs
+// ~1 ms of GPU idle per bundle; here the same single-pass slab plan is built by
+// three small kernels from the generator's per-row extension lists, counted by
+// k_count_slab_rec with the piece count read from device memory, and the counts
+// are thresholded into F_k rows that feed the next bundle without a host round
+// trip.
+//
+// Piece records (48 B, the k_count_slab_rec format of plan.cpp):
+//   a = {candidate index, n_ext | m << 8, prefix slab rows 0-3 (u16)}
+//   b = {extension slab rows 0-7 (u16)},  c = {prefix slab rows 4-11 (u16)}
+// A parent row with c extensions gives c / 8 pieces of 8 and one of c % 8;
+// pieces are bucketed by n_ext, 8 first (the lanes of a wave then loop equally
+// long, as plan.cpp's counting sort).  Prefixes are at most 12 items (the chain
+// stops bundles before that).
+#include "fa_hip.h"
+
+namespace fa {
+
+constexpr int kDlMaxL = 32;
+constexpr int kDlCtlN = 256;   // gen.hip kDlCtl
+// ctl words used here: 128 .. 191 used-item bitset (gen.hip), 200 + b piece count of
+// bucket b (1..8), 210 + b bucket cursor, 220 pieces, 221 pieces as int32 (the count
+// kernel's G)
+
+struct DlLevels {
+  const int32_t* P[kDlMaxL];      // parent rows [n_l][m_l]
+  const int32_t* cnt[kDlMaxL];    // extensions per parent row; their ids at cnt + n_l
+  const int64_t* off[kDlMaxL];    // exclusive offsets of cnt [n_l + 1]
+  const int32_t* rows[kDlMaxL];   // candidate rows [C_l][m_l + 1]
+  int64_t n[kDlMaxL];             // parent rows
+  int64_t C[kDlMaxL];             // candidates
+  int64_t base[kDlMaxL];          // candidate index of the level's first candidate
+  int64_t rbase[kDlMaxL + 1];     // flattened parent-row index of the level's first row
+  int m[kDlMaxL];                 // parent row length (prefix length)
+  int L;
+};
+
+__device__ __forceinline__ int dl_level_of(const DlLevels& D, int64_t t) {
+  int l = 0;
+  while (l + 1 < D.L && t >= D.rbase[l + 1]) ++l;
+  return l;
+}
+
+// rank -> slab row from the used-item bitset (one wave)
+__global__ __launch_bounds__(64) void k_dl_map(const long long* __restrict__ c, int F1, int32_t* __restrict__ item_map) {
+  __shared__ int pre[64];
+  const uint64_t* mk = reinterpret_cast<const uint64_t*>(c + 128);
+  const int lane = threadIdx.x;
+  const uint64_t w = mk[lane];
+  const int pc = __popcll(w);
+  pre[lane] = wave_scan_incl_dpp(pc) - pc;
+  __syncthreads();
+  for (int r = lane; r < F1; r += 64) {
+    const uint64_t ww = mk[r >> 6];
+    const int b = r & 63;
+    item_map[r] = ((ww >> b) & 1ull) ? pre[r >> 6] + __popcll(ww & ((1ull << b) - 1ull)) : -1;
+  }
+}
+
+// pieces per n_ext bucket (wave-aggregated, one global atomic per wave and bucket)
+__global__ __launch_bounds__(256) void k_dl_pieces_count(const DlLevels D, long long* __restrict__ c) {
+  const int64_t R = D.rbase[D.L];
+  const int lane = threadIdx.x & 63;
+  for (int64_t t0 = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63); t0 < R; t0 += (int64_t)gridDim.x * 256) {
+    const int64_t t = t0 + lane;
+    int cc = 0;
+    if (t < R) {
+      const int l = dl_level_of(D, t);
+      cc = D.cnt[l][t - D.rbase[l]];
+    }
+#pragma unroll
+    for (int b = 1; b <= 8; ++b) {
+      const int v = b == 8 ? (cc >> 3) : ((cc & 7) == b ? 1 : 0);
+      const int tot = wave_last(wave_scan_incl_dpp(v));
+      if (lane == 0 && tot) atomicAdd(reinterpret_cast<unsigned long long*>(c + 200 + b), (unsigned long long)tot);
+    }
+  }
+}
+
+__global__ void k_dl_pieces_scan(long long* __restrict__ c) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  long long cur = 0;
+  for (int b = 8; b >= 1; --b) { c[210 + b] = cur; cur += c[200 + b]; }
+  c[220] = cur;
+  reinterpret_cast<int32_t*>(c + 221)[0] = (int32_t)cur;
+}
+
+__device__ __forceinline__ uint32_t dl_pk(int x, int y) { return (uint32_t)(x & 0xFFFF) | ((uint32_t)(y & 0xFFFF) << 16); }
+
+__device__ __forceinline__ void dl_write_rec(int4* __restrict__ rec, int64_t p, int64_t cand, int n_ext, int m,
+                                             const int (&ids)[12], const int32_t* __restrict__ ex,
+                                             const int32_t* __restrict__ item_map) {
+  int e8[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) e8[k] = k < n_ext ? item_map[ex[k]] : 0;
+  int4 a, b, cc;
+  a.x = (int)cand;
+  a.y = n_ext | (m << 8);
+  a.z = (int)dl_pk(ids[0], ids[1]);
+  a.w = (int)dl_pk(ids[2], ids[3]);
+  b.x = (int)dl_pk(e8[0], e8[1]); b.y = (int)dl_pk(e8[2], e8[3]);
+  b.z = (int)dl_pk(e8[4], e8[5]); b.w = (int)dl_pk(e8[6], e8[7]);
+  cc.x = (int)dl_pk(ids[4], ids[5]); cc.y = (int)dl_pk(ids[6], ids[7]);
+  cc.z = (int)dl_pk(ids[8], ids[9]); cc.w = (int)dl_pk(ids[10], ids[11]);
+  rec[3 * p] = a; rec[3 * p + 1] = b; rec[3 * p + 2] = cc;
+}
+
+__global__ __launch_bounds__(256) void k_dl_pieces_emit(const DlLevels D, long long* __restrict__ c,
+                                                        const int32_t* __restrict__ item_map, int4* __restrict__ rec) {
+  const int64_t R = D.rbase[D.L];
+  const int lane = threadIdx.x & 63;
+  for (int64_t t0 = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63); t0 < R; t0 += (int64_t)gridDim.x * 256) {
+    const int64_t t = t0 + lane;
+    int cc = 0, l = 0;
+    int64_t i = 0;
+    if (t < R) {
+      l = dl_level_of(D, t);
+      i = t - D.rbase[l];
+      cc = D.cnt[l][i];
+    }
+    // slots: wave-aggregated cursors per bucket
+    int64_t slot[9];
+#pragma unroll
+    for (int b = 1; b <= 8; ++b) {
+      const int v = b == 8 ? (cc >> 3) : ((cc & 7) == b ? 1 : 0);
+      const int incl = wave_scan_incl_dpp(v);
+      const int tot = wave_last(incl);
+      unsigned long long basev = 0;
+      if (lane == 63 && tot)
+        basev = atomicAdd(reinterpret_cast<unsigned long long*>(c + 210 + b), (unsigned long long)tot);
+      const long long bw = (long long)__builtin_amdgcn_readlane((int)(basev & 0xFFFFFFFFull), 63) |
+                           ((long long)__builtin_amdgcn_readlane((int)(basev >> 32), 63) << 32);
+      slot[b] = bw + (incl - v);
+    }
+    if (cc == 0) continue;
+    const int m = D.m[l];
+    const int32_t* x = D.P[l] + i * m;
+    int ids[12];
+#pragma unroll
+    for (int q = 0; q < 12; ++q) ids[q] = q < m ? item_map[x[q]] : 0;
+    const int64_t o = D.off[l][i];
+    const int32_t* ex = D.cnt[l] + D.n[l] + o;
+    const int64_t cand = D.base[l] + o;
+    const int full = cc >> 3;
+    for (int j = 0; j < full; ++j) dl_write_rec(rec, slot[8] + j, cand + 8 * j, 8, m, ids, ex + 8 * j, item_map);
+    const int rem = cc & 7;
+    if (rem) dl_write_rec(rec, slot[rem], cand + 8 * full, rem, m, ids, ex + 8 * full, item_map);
+  }
+}
+
+// keep support >= mc (FastApriori.scala:152-154): per level, the kept candidate rows
+// and counts in candidate order (lexicographic, as the rows were generated), their
+// number into fsz[l].  One workgroup; a bundle holds at most one accumulator pass
+// (~40K candidates).
+struct DlOut {
+  int64_t rows_off[kDlMaxL];      // int32 offset of level l's kept rows in rows_out
+  int64_t cnt_off[kDlMaxL];       // int32 offset of level l's kept counts in cnt_out
+};
+
+__global__ __launch_bounds__(1024) void k_dl_threshold(const DlLevels D, const DlOut O,
+                                                       const uint32_t* __restrict__ counts, int64_t mc,
+                                                       int32_t* __restrict__ rows_out, int32_t* __restrict__ cnt_out,
+                                                       long long* __restrict__ fsz) {
+  __shared__ int part[16];
+  __shared__ int64_t carry;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int l = 0; l < D.L; ++l) {
+    const int64_t C = D.C[l];
+    const int w = D.m[l] + 1;
+    const uint32_t* cl = counts + D.base[l];
+    const int32_t* src = D.rows[l];
+    int32_t* ro = rows_out + O.rows_off[l];
+    int32_t* co = cnt_out + O.cnt_off[l];
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int64_t b0 = 0; b0 < C; b0 += 1024) {
+      const int64_t e = b0 + threadIdx.x;
+      const uint32_t v = e < C ? cl[e] : 0u;
+      const int keep = (e < C && (int64_t)v >= mc) ? 1 : 0;
+      const int incl = wave_scan_incl_dpp(keep);
+      if (lane == 63) part[wv] = incl;
+      __syncthreads();
+      int64_t at = carry;
+      for (int q = 0; q < wv; ++q) at += part[q];
+      at += incl - keep;
+      if (keep) {
+        co[at] = (int32_t)v;
+        for (int q = 0; q < w; ++q) ro[at * w + q] = src[e * w + q];
+      }
+      __syncthreads();
+      if (threadIdx.x == 1023) carry = at + keep;
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) fsz[l] = carry;
+    __syncthreads();
+  }
+}
+
+static int dl_levels(const int64_t* desc, int L, DlLevels* D) {
+  if (L < 1 || L > kDlMaxL) return 1;
+  *D = DlLevels{};
+  D->L = L;
+  D->rbase[0] = 0;
+  for (int l = 0; l < L; ++l) {
+    const int64_t* d = desc + 8 * l;
+    D->P[l] = reinterpret_cast<const int32_t*>((intptr_t)d[0]);
+    D->cnt[l] = reinterpret_cast<const int32_t*>((intptr_t)d[1]);
+    D->off[l] = reinterpret_cast<const int64_t*>((intptr_t)d[2]);
+    D->rows[l] = reinterpret_cast<const int32_t*>((intptr_t)d[3]);
+    D->m[l] = (int)d[4];
+    D->n[l] = d[5];
+    D->C[l] = d[6];
+    D->base[l] = d[7];
+    D->rbase[l + 1] = D->rbase[l] + d[5];
+    if (D->m[l] < 1 || D->m[l] > 12) return 1;
+  }
+  return 0;
+}
+
+}  // namespace fa
+
+using namespace fa;
+
+// Single-pass slab plan of a device bundle (desc: gen.hip fa_hip_dl_more's level
+// table, L levels).  item_map: int32 [F1] out (rank -> slab row, -1 unused);
+// rec: int4 [3 * max_pieces] out, max_pieces >= total candidates.  The piece count
+// lands in ctl[220] (int32 copy at ctl + 221, the count kernel's G).
+FA_API int fa_hip_dl_plan(const int64_t* desc, int L, long long* ctl, int F1, int32_t* item_map, void* rec,
+                          int64_t max_pieces, hipStream_t st) {
+  DlLevels D;
+  if (dl_levels(desc, L, &D)) return 1;
+  if (F1 < 1 || F1 > 4096) return 1;
+  int64_t C = 0;
+  for (int l = 0; l < L; ++l) C += D.C[l];
+  if (max_pieces < C) return 1;
+  const int64_t R = D.rbase[L];
+  hipLaunchKernelGGL(k_dl_map, dim3(1), dim3(64), 0, st, ctl, F1, item_map);
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((R + 255) / 256, 1024));
+  hipLaunchKernelGGL(k_dl_pieces_count, dim3(g), dim3(256), 0, st, D, ctl);
+  hipLaunchKernelGGL(k_dl_pieces_scan, dim3(1), dim3(64), 0, st, ctl);
+  hipLaunchKernelGGL(k_dl_pieces_emit, dim3(g), dim3(256), 0, st, D, ctl, item_map, static_cast<int4*>(rec));
+  FA_LAUNCH_RET();
+}
+
+// Threshold of a device bundle's counts (bundle candidate order) into per-level
+// outputs: rows_out + rows_off[l] (int32 [F][m_l + 1]), cnt_out + cnt_off[l]
+// (int32 [F]); F of level l into fsz[l] (device).  rows_off / cnt_off: host int64 [L].
+FA_API int fa_hip_dl_threshold(const int64_t* desc, int L, const uint32_t* counts, int64_t mc, int32_t* rows_out,
+                               const int64_t* rows_off, int32_t* cnt_out, const int64_t* cnt_off, long long* fsz,
+                               hipStream_t st) {
+  DlLevels D;
+  if (dl_levels(desc, L, &D)) return 1;
+  DlOut O{};
+  for (int l = 0; l < L; ++l) { O.rows_off[l] = rows_off[l]; O.cnt_off[l] = cnt_off[l]; }
+  hipLaunchKernelGGL(k_dl_threshold, dim3(1), dim3(1024), 0, st, D, O, counts, mc, rows_out, cnt_out, fsz);
+  FA_LAUNCH_RET();
+}

@@ -189,8 +189,9 @@ __global__ __launch_bounds__(256) void k_compact_lines(
 // turns occupied slots into dense ids (slot order, i.e. hash order) afterwards.
 // The slot's (byte offset, length) of one occurrence lets the host decode the
 // strings it needs (frequent items) without a dictionary of every token.
-// flags[0] |= 2 when a probe sequence exceeds kMaxProbe (table too full: the
-// caller falls back to the host parser).
+// flags[0] |= 2 when a probe sequence exceeds kMaxProbe (table too full), |= 4 when
+// k_dict_verify finds two distinct tokens sharing a hash: the caller then falls
+// back to the host parser.
 // ---------------------------------------------------------------------------
 constexpr int kMaxProbe = 256;
 
@@ -274,6 +275,64 @@ __global__ __launch_bounds__(kPT) void k_parse_lines_dict(
   if (__ballot(full) != 0ull && lane_id() == 0) atomicOr(&flags[0], 2);
 }
 
+// Identity check of the table: a slot is keyed by the 64-bit hash alone, so two
+// distinct tokens with one hash would share an id.  After k_parse_lines_dict every
+// slot's representative (tpos, tlen) is written; this pass re-tokenises every line
+// and compares each token's bytes with its slot's representative.  flags[0] |= 4 on
+// any difference (the caller then parses the shard on the host, which reports the
+// collision as an error, csrc/host/parse.cpp).
+__device__ __forceinline__ bool dict_same(const uint8_t* __restrict__ buf, const unsigned long long* __restrict__ keys,
+                                          const int64_t* __restrict__ tpos, const int32_t* __restrict__ tlen,
+                                          uint32_t mask, uint64_t h, int64_t pos, int32_t len) {
+  if (h == 0) h = 1;
+  uint32_t at = (uint32_t)(h >> 20) & mask;
+  for (int p = 0; p < kMaxProbe; ++p) {
+    const unsigned long long k = keys[at];
+    if (k == h) {
+      if (tlen[at] != len) return false;
+      const int64_t q = tpos[at];
+      for (int32_t i = 0; i < len; ++i)
+        if (buf[q + i] != buf[pos + i]) return false;
+      return true;
+    }
+    if (k == 0) return false;
+    at = (at + 1) & mask;
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(kPT) void k_dict_verify(const uint8_t* __restrict__ buf, const int64_t* __restrict__ ends,
+                                                     int64_t nl, int32_t* __restrict__ flags,
+                                                     const unsigned long long* __restrict__ keys,
+                                                     const int64_t* __restrict__ tpos, const int32_t* __restrict__ tlen,
+                                                     uint32_t mask) {
+  const int64_t j = (int64_t)blockIdx.x * kPT + threadIdx.x;
+  bool bad = false;
+  if (j < nl) {
+    int64_t s = j ? ends[j - 1] + 1 : 0;
+    int64_t e = ends[j];
+    while (s < e && buf[s] <= 0x20) ++s;
+    while (e > s && buf[e - 1] <= 0x20) --e;
+    if (s < e) {        // (a blank line's token "" has length 0: nothing to compare)
+      int64_t ts = -1;
+      uint64_t h = 0;
+      for (int64_t i = s; i <= e && !bad; ++i) {
+        const uint32_t c = i < e ? buf[i] : (uint32_t)' ';
+        if (c == ' ' || c == '\t' || c == 0x0B || c == '\f') {
+          if (ts >= 0) {
+            bad = !dict_same(buf, keys, tpos, tlen, mask, dmix64(h ^ (uint64_t)(i - ts)), ts, (int32_t)(i - ts));
+            ts = -1;
+          }
+          continue;
+        }
+        if (ts < 0) { ts = i; h = 0xCBF29CE484222325ull; }
+        h = (h ^ c) * 0x100000001B3ull;
+      }
+    }
+  }
+  if (__ballot(bad) != 0ull && lane_id() == 0) atomicOr(&flags[0], 4);
+}
+
 // dense id of every occupied slot (exclusive scan of occupancy done by the caller)
 __global__ __launch_bounds__(256) void k_slot_remap(int32_t* __restrict__ ids, int64_t n,
                                                     const int32_t* __restrict__ slot_id) {
@@ -294,6 +353,15 @@ FA_API int fa_hip_parse_lines_dict(const uint8_t* buf, const int64_t* ends, int6
   hipLaunchKernelGGL(k_parse_lines_dict, dim3((unsigned)((nl + kPT - 1) / kPT)), dim3(kPT), 0, st, buf, ends, nl,
                      bound_off, scratch, xscratch, dcnt, xcnt, flags, (unsigned long long*)keys, tpos, tlen,
                      (uint32_t)(cap - 1));
+  FA_LAUNCH_RET();
+}
+
+FA_API int fa_hip_dict_verify(const uint8_t* buf, const int64_t* ends, int64_t nl, int32_t* flags, const void* keys,
+                              const int64_t* tpos, const int32_t* tlen, int64_t cap, hipStream_t st) {
+  if (nl <= 0) return 0;
+  if (cap <= 0 || (cap & (cap - 1)) || cap > ((int64_t)1 << 31)) return 1;
+  hipLaunchKernelGGL(k_dict_verify, dim3((unsigned)((nl + kPT - 1) / kPT)), dim3(kPT), 0, st, buf, ends, nl, flags,
+                     (const unsigned long long*)keys, tpos, tlen, (uint32_t)(cap - 1));
   FA_LAUNCH_RET();
 }
 

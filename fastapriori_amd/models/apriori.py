@@ -87,6 +87,9 @@ PAIR_RS_MIN = int(os.environ.get("FA_PAIR_RS_MIN", str(1 << 15)))
 # 17.7 -> 21.0 ms with it, bundle 5-12 16.2 -> 14.6 ms)
 BUNDLE_DFS_MIN_M = int(os.environ.get("FA_BUNDLE_DFS_MIN_M", "4"))
 BUNDLE_GROWTH = float(os.environ.get("FA_BUNDLE_GROWTH", "1.5"))
+# level bundles generated, planned, counted and thresholded on the GPU with no host
+# round trip per bundle beyond the generator's acceptance readbacks (_mine_device)
+DEVICE_LEVELS = os.environ.get("FA_DEVICE_LEVELS", "1") == "1"
 BUNDLE_MAX_PREFIX = int(os.environ.get("FA_BUNDLE_MAX_PREFIX", "9"))
 
 
@@ -138,6 +141,8 @@ class FastApriori:
 
     def _run(self, shard: TransactionShard, resume: MiningResult | None = None) -> MiningResult:
         t_start = time.perf_counter()
+        ops.primitives.reset_fallbacks()     # this run reports its own fallbacks only
+        self._f2_dev = None                  # F_2 rows on the device (the first device bundle's input)
         dev = shard.items.device
         # candidate parallelism: the data is replicated, so data-side collectives
         # (line count, F1, layout decisions) are local; only count vectors move
@@ -164,7 +169,8 @@ class FastApriori:
         self.log.line(f"1 freq items {F1}")
         levels = [np.arange(F1, dtype=np.int32).reshape(-1, 1)]
         counts = [counts1]
-        result = MiningResult(items, levels, counts, mc, n_global, self.stats)
+        result = MiningResult(items, levels, counts, mc, n_global, self.stats,
+                              item_hashes=None if shard.vocab.numeric else self._item_hashes)
         self._result_items(result, wait=resume is not None or self.ckpt is not None)
         if resume is not None:
             self._check_resume(resume, result)
@@ -199,7 +205,11 @@ class FastApriori:
 
         # ---- k >= 3 ----------------------------------------------------
         k = 3
-        while len(levels[-1]) >= k and (self.cfg.max_level == 0 or k <= self.cfg.max_level):
+        if self._device_levels_ok(resume):
+            # device bundles while every bundle fits one accumulator pass; None when
+            # mining is complete, else the level the host loop continues from
+            k = self._mine_device(db, levels, counts, mc, result)
+        while k is not None and len(levels[-1]) >= k and (self.cfg.max_level == 0 or k <= self.cfg.max_level):
             t0 = time.perf_counter()
             b0 = self._bytes_moved()
             if resume is not None and len(resume.levels) >= k:
@@ -266,6 +276,126 @@ class FastApriori:
         while len(levels) > 1 and len(levels[-1]) == 0:
             levels.pop(); counts.pop()
         return self._finish(result, t_start)
+
+    # ------------------------------------------------------------------
+    # k >= 3 on the device (FastApriori.scala:110-121, :132-160)
+    # ------------------------------------------------------------------
+    def _device_levels_ok(self, resume) -> bool:
+        return (DEVICE_LEVELS and self._dev.type == "cuda" and self._f2_dev is not None and resume is None
+                and self.ckpt is None and not self.cand_par and 2 <= self._F1 <= ops.primitives.AG_DEVICE_MAX_F1
+                and self.cfg.level_kernel in ("auto", "slab") and self.stats["n_lines"] < (1 << 31))
+
+    def _mine_device(self, db, levels: list, counts: list, mc: int, result: MiningResult):
+        """Level bundles with no host round trip beyond the generator's (csrc/hip/gen.hip
+        fa_hip_dl_level0 / fa_hip_dl_more, csrc/hip/levels.hip).
+
+        Per bundle: level k's candidates from F_{k-1} rows already on the GPU (F_2, or
+        the previous bundle's thresholded rows, their number read by the kernels from
+        device memory), one readback of C_k and the used items (trimming, slab width,
+        whether level k fits one accumulator pass), the speculative levels k+1..
+        accepted on the device (one readback per batch of four), then the piece plan,
+        the slab count, the count all-reduce and the threshold into F rows, all queued
+        on the stream.  The results reach the host once, after the last bundle.
+        Returns None when mining is complete, or the level from which the host loop
+        continues (a level that needs several accumulator passes, or prefixes too long
+        for inline piece records): levels/counts then hold F_1 .. F_{k-1}."""
+        Pm = ops.primitives
+        S = Pm.device_level_state(self._dev)
+        F1 = self._F1
+        lds = Pm.dl_lds_budget(F1)
+        c_bound = int(lds // 4)
+        st = torch.cuda.current_stream(self._dev).cuda_stream
+        f2 = self._f2_dev
+        P0, n_src, n_const, n_bound = f2.data_ptr(), None, int(f2.shape[0]), int(f2.shape[0])
+        m0, k = 2, 3
+        pend = []
+        tm = self._timer
+        nxt = None
+        while True:
+            if self.cfg.max_level and k > self.cfg.max_level:
+                break
+            if m0 > Pm.DL_MAX_M:
+                nxt = k
+                break
+            t0 = time.perf_counter()
+            b0 = self._bytes_moved()
+            with roctx_range(f"dlevel{k}"), tm.phase(f"level{k}"):
+                L = -1
+                while L < 0:
+                    with roctx_range("gen0"):
+                        c = Pm.dl_level0(S, P0, n_src, n_const, n_bound, m0, F1, c_bound, lds, st)
+                    if c[7] or c[5]:
+                        break
+                    C0, n_used, n0 = int(c[40]), int(c[6]), int(c[8])
+                    S.desc[:] = 0
+                    S.desc[0] = [P0, S.info[1], S.info[2], S.info[3], m0, n0, C0, 0]
+                    max_lv = min(Pm.DL_MAX_M - m0 + 1, Pm.DL_MAX_LEVELS)
+                    if self.cfg.max_level:
+                        max_lv = min(max_lv, self.cfg.max_level - k + 1)
+                    if not BUNDLE_LEVELS or k - 1 > BUNDLE_MAX_PREFIX:
+                        max_lv = 1
+                    L = 1
+                    if max_lv > 1:
+                        with roctx_range("gen_more"):
+                            L = Pm.dl_more(S, F1, BUNDLE_GROWTH, max_lv, lds, st)
+                if c[7]:
+                    break                               # |F_{k-1}| < k or no candidates: done
+                if c[5]:
+                    nxt = k                             # several accumulator passes: host path
+                    break
+                bits = np.unpackbits(c[128:192].view(np.uint8), bitorder="little")[:F1]
+                used = np.flatnonzero(bits)
+                Cs = S.desc[:L, 6].copy()
+                C = int(Cs.sum())
+                with tm.phase(f"trim{k}"), roctx_range("trim"):
+                    self._trim(db, used, k, C)
+                with tm.phase("count"), roctx_range("count"):
+                    cnt = Pm.dl_count(S, L, db["roff"], db["ranks"], db["src"], db["ncols"], F1, db["wword"],
+                                      n_used, C, lds)
+                    self.comm.all_reduce_(cnt)
+                    rows_a, cnt_a, ro, co = Pm.dl_threshold(S, L, cnt, mc, k)
+            pend.append(dict(k=k, L=L, m0=m0, C=Cs, rows=rows_a, cnt=cnt_a, ro=ro, co=co,
+                             ms=(time.perf_counter() - t0) * 1e3, bytes=self._bytes_moved() - b0,
+                             groups=int((S.desc[:L, 5]).sum())))
+            P0 = rows_a.data_ptr() + 4 * int(ro[L - 1])
+            n_src, n_const, n_bound = S.fsz.data_ptr() + 8 * (k + L - 1), 0, int(Cs[-1])
+            m0 += L
+            k += L
+        self._dl_flush(S, pend, levels, counts, result)
+        self.stats["device_bundles"] = len(pend)
+        return nxt
+
+    def _dl_flush(self, S, pend: list, levels: list, counts: list, result: MiningResult) -> None:
+        """Every device level to the host (the run's one results readback)."""
+        if not pend:
+            return
+        fsz = S.fsz.cpu().numpy()
+        rows_h = torch.cat([p["rows"] for p in pend]).cpu().numpy()
+        cnt_h = torch.cat([p["cnt"] for p in pend]).cpu().numpy()
+        ro_base = co_base = 0
+        for p in pend:
+            for l in range(p["L"]):
+                kk, w = p["k"] + l, p["m0"] + l + 1
+                F = int(fsz[kk])
+                a = ro_base + int(p["ro"][l])
+                b = co_base + int(p["co"][l])
+                levels.append(rows_h[a:a + F * w].reshape(F, w).copy())
+                counts.append(cnt_h[b:b + F].astype(np.int64))
+                if kk > p["k"] and self.log.enabled:
+                    # the reference logs the candidates generated from F_{k-1}; a bundled
+                    # level counted a superset generated from C_{k-1}
+                    self.log.line(f"{kk} candidate items {int(apriori_gen(levels[kk - 2])[2].size)}")
+                elif self.log.enabled:
+                    self.log.line(f"{kk} candidate items {int(p['C'][l])}")
+                self.log.line(f"{kk} freq items {F}")
+                self.log.line(f"Use Time {kk} items {int(p['ms']) if l == 0 else 0}")
+                self._level_recs.append((dict(phase="level", k=kk, candidates=int(p["C"][l]), frequent=F,
+                                              ms=p["ms"] if l == 0 else 0.0, groups=p["groups"] if l == 0 else 0,
+                                              bundled_with=p["k"], bytes_reduced=p["bytes"] if l == 0 else 0,
+                                              kernel="slab_dev", hbm_bytes_est=0),
+                                         f"level{p['k']}" if l == 0 else None))
+            ro_base += int(p["rows"].numel())
+            co_base += int(p["cnt"].numel())
 
     def _run_deferred(self) -> None:
         for d in self._deferred:
@@ -422,6 +552,8 @@ class FastApriori:
             fstr = vocab.decode(sel_np)
         order = sorted(range(len(fstr)), key=lambda e: (-int(fc[e]), java_string_key(fstr[e])))
         items = [fstr[e] for e in order]
+        self._item_hashes = np.asarray(fh, dtype=np.int64)[order].view(np.uint64) if order else \
+            np.zeros(0, np.uint64)
         counts1 = np.asarray(fc, dtype=np.int64)[order] if order else np.zeros(0, np.int64)
         lut = torch.full((max(Vl, 1),), -1, dtype=torch.int32, device=dev)
         if order and Vl:
@@ -741,6 +873,9 @@ class FastApriori:
             vals = flat[keep]
         # one readback: rows (a, b) and counts
         keep = keep.to(iu.device)
+        if iu.is_cuda and DEVICE_LEVELS:
+            # F_2 rows stay on the device as the first device bundle's input
+            self._f2_dev = torch.stack([iu[0][keep], iu[1][keep]], 1).to(torch.int32).contiguous()
         h = torch.stack([iu[0][keep], iu[1][keep], vals.to(device=iu.device, dtype=torch.int64)]).cpu().numpy()
         return np.ascontiguousarray(h[:2].T, dtype=np.int32), h[2].astype(np.int64)
 

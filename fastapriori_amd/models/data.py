@@ -124,6 +124,10 @@ class MiningResult:
     min_count: int
     n_lines: int
     stats: dict = field(default_factory=dict)
+    # dictionary mode: the parser's 64-bit hash of every frequent item (rank order), so
+    # U.dat tokens are matched on the raw bytes' identity, not on re-encoded strings
+    # (a token with invalid UTF-8 decodes with U+FFFD and would hash differently)
+    item_hashes: np.ndarray | None = None
 
     @property
     def n_itemsets(self) -> int:

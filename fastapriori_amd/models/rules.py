@@ -84,7 +84,10 @@ class AssociationRules:
                     lut[i] = r
         elif vocab.size and self.result.items:
             # through the parser's 64-bit token hashes: no loop over the users' vocabulary
-            rh = hash_tokens(self.result.items)
+            rh = self.result.item_hashes
+            if rh is None or len(rh) != len(self.result.items):
+                rh = hash_tokens(self.result.items)     # e.g. results reloaded from files
+            rh = np.asarray(rh, dtype=np.uint64)
             ro = np.argsort(rh)
             vh = vocab.hashes.astype(np.uint64)
             pos = np.minimum(np.searchsorted(rh[ro], vh), rh.size - 1)
@@ -178,7 +181,12 @@ class AssociationRules:
 
     def run(self, users: TransactionShard) -> list[str] | None:
         """Recommendations for every U.dat line, in file order, on rank 0 (None elsewhere)."""
+        ops.primitives.reset_fallbacks()     # the rules phase reports its own fallbacks
         rec = self.recommend_shard(users)
+        if ops.primitives.FALLBACKS:
+            self.stats["fallbacks"] = list(ops.primitives.FALLBACKS)
+            for f in ops.primitives.FALLBACKS:
+                self.log.metric(phase="fallback", what=f, stage="rules")
         parts = self.comm.gather_varlen(rec)
         if parts is None:
             return None

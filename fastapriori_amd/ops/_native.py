@@ -88,7 +88,12 @@ _HIP_SIGS = {
     "fa_hip_count_slab": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, vp,
                                     C.c_int, C.c_int, vp, i64, vp, vp, vp, C.c_int]),
     "fa_hip_count_slab_rec": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, C.c_int, vp, vp, C.c_int, C.c_int, vp, vp,
-                                        C.c_int, C.c_int, vp, i64, vp, vp, C.c_int]),
+                                        C.c_int, C.c_int, vp, i64, vp, vp, C.c_int, vp]),
+    # device-resident level bundles (gen.hip fa_hip_dl_*, levels.hip)
+    "fa_hip_dl_level0": (C.c_int, [vp, vp, i64, i64, C.c_int, C.c_int, vp, i64, vp, vp, i64, dbl, vp, vp]),
+    "fa_hip_dl_more": (C.c_int, [C.c_int, vp, i64, i64, vp, vp, dbl, C.c_int, dbl, vp, vp, vp]),
+    "fa_hip_dl_plan": (C.c_int, [vp, C.c_int, vp, C.c_int, vp, vp, i64, vp]),
+    "fa_hip_dl_threshold": (C.c_int, [vp, C.c_int, vp, i64, vp, vp, vp, vp, vp, vp]),
     "fa_hip_trim_scan_count": (C.c_int, [vp, vp, i64, vp, C.c_int, C.c_int, vp, vp, vp, vp, vp]),
     "fa_hip_trim_emit": (C.c_int, [vp, vp, vp, C.c_int, i64, vp, vp, vp, vp, vp, vp, vp, vp]),
     "fa_hip_compress_wave": (C.c_int, [vp, vp, vp, vp, i64, vp, vp, vp, C.c_int, vp]),
@@ -114,6 +119,7 @@ _HIP_SIGS = {
     "fa_hip_parse_lines": (C.c_int, [vp, vp, i64, vp, vp, vp, vp, vp, vp, vp]),
     "fa_hip_parse_lines_dict": (C.c_int, [vp, vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, vp]),
     "fa_hip_slot_remap": (C.c_int, [vp, i64, vp, vp]),
+    "fa_hip_dict_verify": (C.c_int, [vp, vp, i64, vp, vp, vp, vp, i64, vp]),
     "fa_hip_compact_lines": (C.c_int, [vp, vp, vp, vp, vp, vp, vp, i64, vp, vp, vp]),
     "fa_hip_rule_gen": (C.c_int, [vp, i64, C.c_int, vp, i64, vp, vp, vp, vp, vp]),
     "fa_hip_rule_cut": (C.c_int, [vp, vp, i64, C.c_int, vp, vp, vp, vp]),

@@ -1054,7 +1054,7 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
             _hip_call("fa_hip_count_slab_rec", _p(roff), _p(ranks), _p(src), ncols, base + 4 * o_im, F1, n_used,
                       base + 4 * o_gpre, base + 4 * (o_rec + 12 * a), b - a, Cq, _p(wword),
                       out.data_ptr() + 4 * e0, sw, n_wg, _p(bm), bm.stride(0) if bm is not None else 0, st,
-                      bm_rows, int(acc16))
+                      bm_rows, int(acc16), None)
         else:
             lds = n_used * (sw + 2) * 8 + Cq * accb
             n_wg = int(max(wg_floor, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2))))
@@ -1071,14 +1071,23 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
 
 AG_DEVICE_MAX_F1 = 4096   # bitset words per lane-wave: 64 x 64 bits
 
-# Device -> host fallbacks taken in this process (each reported once on stderr and
-# recorded here; the miner copies new ones into its metrics stream).
+# Device -> host fallbacks taken by the current phase (a mining run or a rules
+# phase clears the list when it starts, reset_fallbacks(), and reports what it
+# holds when it ends, so a run never re-reports an earlier run's fallbacks).
+# Each distinct message is printed on stderr once per process.
 FALLBACKS: list = []
+_PRINTED: set = set()
+
+
+def reset_fallbacks() -> None:
+    FALLBACKS.clear()
 
 
 def note_fallback(what: str) -> None:
     if what not in FALLBACKS:
         FALLBACKS.append(what)
+    if what not in _PRINTED:
+        _PRINTED.add(what)
         import sys
         print(f"fastapriori_amd: {what}", file=sys.stderr, flush=True)
 
@@ -1440,7 +1449,7 @@ def parse_dict_device(buf: torch.Tensor, n: int, last_is_term: bool):
     from a device hash table keyed by the parser's 64-bit token hash, then dense ids
     in hash order.  Returns (offsets, items, extras, hashes uint64 np [V], first-
     occurrence byte offsets int64 np [V], lengths int32 np [V]) or None when the
-    table overflows (-> host parser)."""
+    table overflows or two distinct tokens share a hash (k_dict_verify; -> host parser)."""
     dev = buf.device
     st = _stream(buf)
     lib = _native.hip()
@@ -1463,7 +1472,10 @@ def parse_dict_device(buf: torch.Tensor, n: int, last_is_term: bool):
     _native.check(lib.fa_hip_parse_lines_dict(_p(buf), _p(ends), nl, _p(bound_off), _p(scratch), _p(xscratch),
                                               _p(dcnt), _p(xcnt), _p(flags), _p(keys), _p(tpos), _p(tlen), cap, st),
                   "fa_hip_parse_lines_dict")
-    if int(flags[0].item()) & 2:
+    # identity check: tokens sharing a 64-bit hash would share an id (flags |= 4)
+    _native.check(lib.fa_hip_dict_verify(_p(buf), _p(ends), nl, _p(flags), _p(keys), _p(tpos), _p(tlen), cap, st),
+                  "fa_hip_dict_verify")
+    if int(flags[0].item()) & 6:
         return None
     off, items, extras = _compact_lines(scratch, xscratch, bound_off, dcnt, xcnt, nl, st)
     occ = keys != 0
@@ -1607,3 +1619,135 @@ def count_bundle_dfs(roff, ranks, src, ncols: int, F1: int, levels: list) -> tor
         (_LDS_BYTES - n_used * (sw + 2) * 8) // 4), passes=1, pieces=NP, witems=0, d1=0, d2=0, trie_reads=0,
         slab_reads=0, m=-1, C=C)
     return out.to(_I64)
+
+
+# ---------------------------------------------------------------------------
+# Device-resident level bundles (csrc/hip/gen.hip fa_hip_dl_level0 / fa_hip_dl_more,
+# csrc/hip/levels.hip fa_hip_dl_plan / fa_hip_dl_threshold; driven by
+# models.apriori.FastApriori._mine_device)
+# ---------------------------------------------------------------------------
+DL_CTL = 256            # gen.hip kDlCtl
+DL_MAX_M = 12           # prefix ids inline in the 48-B piece records
+DL_MAX_LEVELS = 31
+
+
+class DeviceLevelState:
+    """Per-device buffers of the device bundle loop, reused across mining runs:
+    the generator workspace, the control block (+ its pinned host mirror) and the
+    per-level F sizes (fsz[k] = |F_k| on the device)."""
+
+    def __init__(self, dev):
+        self.dev = dev
+        self.ws = torch.empty(64 << 20, dtype=torch.uint8, device=dev)
+        self.ctl = torch.zeros(DL_CTL, dtype=_I64, device=dev)
+        self.ctl_h = torch.zeros(DL_CTL, dtype=_I64, pin_memory=True)
+        self.fsz = torch.zeros(128, dtype=_I64, device=dev)
+        self.desc = np.zeros((32, 8), dtype=np.int64)
+        self.info = np.zeros(4, dtype=np.int64)
+
+    def grow(self, nbytes: int) -> None:
+        self.ws = torch.empty(int(nbytes * 1.25) + (1 << 20), dtype=torch.uint8, device=self.dev)
+
+
+_DL_STATE: dict = {}
+
+
+def device_level_state(dev) -> DeviceLevelState:
+    st = _DL_STATE.get(dev)
+    if st is None:
+        st = _DL_STATE[dev] = DeviceLevelState(dev)
+    return st
+
+
+def dl_lds_budget(F1: int) -> int:
+    """LDS bytes left to slab + accumulators in k_count_slab_rec (the rank map's copy
+    subtracted, as plan.cpp slab_width does)."""
+    return _LDS_BYTES - _slab_map_lds(F1)
+
+
+def dl_slab_width(n_used: int, C: int, lds: int) -> tuple[int, int]:
+    """plan.cpp slab_width: (SW, accumulator capacity) for n_used items and C candidates."""
+    for sw in (16, 32, 8, 4):
+        cap = int((lds - n_used * (sw + 2) * 8) // 4)
+        if cap >= min(C, 8192) or (sw == 4 and cap >= 1024):
+            return sw, cap
+    return 0, 0
+
+
+def dl_level0(S: DeviceLevelState, P0: int, n_src: int | None, n_const: int, n_bound: int, m0: int, F1: int,
+              c_bound: int, lds: int, stream: int) -> np.ndarray:
+    """Level 0 of a device bundle (one synchronisation).  Returns the control block
+    (host int64 [DL_CTL]); S.info holds (ws used, cnt, off, rows) pointers."""
+    lib = _native.hip()
+    for _ in range(4):
+        rc = lib.fa_hip_dl_level0(P0, n_src, n_const, n_bound, m0, F1, _p(S.ws), S.ws.numel(), _p(S.ctl),
+                                  _p(S.ctl_h), c_bound, float(lds), S.info.ctypes.data, stream)
+        if rc == 5:
+            S.grow(int(S.info[0]))
+            continue
+        _native.check(rc, "fa_hip_dl_level0")
+        return S.ctl_h.numpy().copy()
+    raise RuntimeError("fa_hip_dl_level0: workspace sizing did not converge")
+
+
+def dl_more(S: DeviceLevelState, F1: int, growth: float, max_levels: int, lds: int, stream: int) -> int:
+    """Speculative levels 1.. of a device bundle (S.desc[0] = level 0); returns the
+    accepted levels L (S.desc[:L] filled) or -1 when the workspace must grow (the
+    caller then restarts the bundle from level 0: the buffers moved)."""
+    info = np.zeros(2, dtype=np.int64)
+    rc = _native.hip().fa_hip_dl_more(F1, _p(S.ws), S.ws.numel(), int(S.info[0]), _p(S.ctl), _p(S.ctl_h),
+                                      float(growth), int(max_levels), float(lds), S.desc.ctypes.data,
+                                      info.ctypes.data, stream)
+    if rc == 5:
+        S.grow(int(info[0]))
+        return -1
+    _native.check(rc, "fa_hip_dl_more")
+    return int(S.ctl_h[1])
+
+
+def dl_count(S: DeviceLevelState, L: int, roff, ranks, src, ncols: int, F1: int, wword, n_used: int, C: int,
+             lds: int) -> torch.Tensor:
+    """Device plan + slab count of a bundle's C candidates (bundle order) -> int32 [C]
+    on the device (not yet reduced across ranks)."""
+    dev = ranks.device
+    st = _stream(ranks)
+    sw, cap = dl_slab_width(n_used, C, lds)
+    if sw == 0 or C > cap:
+        raise RuntimeError(f"device bundle of {C} candidates over {n_used} items does not fit one pass")
+    item_map = torch.empty(max(F1, 1), dtype=_I32, device=dev)
+    rec = torch.empty(12 * C + 12, dtype=_I32, device=dev)
+    _native.check(_native.hip().fa_hip_dl_plan(S.desc.ctypes.data, L, _p(S.ctl), F1, _p(item_map), _p(rec), C, st),
+                  "fa_hip_dl_plan")
+    out = torch.zeros(C, dtype=_I32, device=dev)
+    W = (ncols + 63) // 64
+    nslabs = (W + sw - 1) // sw
+    lds_k = n_used * (sw + 2) * 8 + ((C + 3) & ~3) * 4 + _slab_map_lds(F1)
+    n_wg = int(max(1, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds_k), 2))))
+    _hip_call("fa_hip_count_slab_rec", _p(roff), _p(ranks), _p(src), ncols, _p(item_map), F1, n_used, None, _p(rec),
+              0, C, _p(wword), _p(out), sw, n_wg, None, 0, st, None, 0, _p(S.ctl) + 8 * 221)
+    LAST_LEVEL_PLAN.clear()
+    LAST_LEVEL_PLAN.update(kernel="slab_dev", rows=int(roff.numel() - 1), used=n_used, sw=sw, cap=cap, passes=1,
+                           pieces=-1, witems=0, d1=0, d2=0, trie_reads=0, slab_reads=0, m=-1, C=C)
+    # (item_map and rec may be freed now: the caching allocator hands their blocks only
+    # to work queued later on this stream)
+    return out
+
+
+def dl_threshold(S: DeviceLevelState, L: int, counts: torch.Tensor, mc: int, k0: int):
+    """Keep counts >= mc per level of a device bundle.  Returns (rows int32 arena,
+    cnt int32 arena, rows_off int64 [L], cnt_off int64 [L]); |F_{k0+l}| lands in
+    S.fsz[k0 + l] on the device."""
+    dev = counts.device
+    C = S.desc[:L, 6]
+    w = S.desc[:L, 4] + 1
+    rows_off = np.zeros(L, dtype=np.int64)
+    cnt_off = np.zeros(L, dtype=np.int64)
+    if L > 1:
+        rows_off[1:] = np.cumsum(C * w)[:-1]
+        cnt_off[1:] = np.cumsum(C)[:-1]
+    rows = torch.empty(max(int((C * w).sum()), 1), dtype=_I32, device=dev)
+    cnt = torch.empty(max(int(C.sum()), 1), dtype=_I32, device=dev)
+    _native.check(_native.hip().fa_hip_dl_threshold(S.desc.ctypes.data, L, _p(counts), int(mc), _p(rows),
+                                                    rows_off.ctypes.data, _p(cnt), cnt_off.ctypes.data,
+                                                    _p(S.fsz) + 8 * k0, _stream(counts)), "fa_hip_dl_threshold")
+    return rows, cnt, rows_off, cnt_off

@@ -96,6 +96,8 @@ class Comm:
         dist.reduce_scatter_tensor(part, x)
         self.bytes_reduced += chunk * (W - 1) * x.element_size()
         loc = torch.nonzero(part >= thr).flatten()
+        # the zero padding past n is never an entry (min_support 0 would select it)
+        loc = loc[loc + self.rank * chunk < n]
         mine = torch.stack([loc + self.rank * chunk, part[loc].to(torch.int64)]) if loc.numel() else \
             torch.zeros((2, 0), dtype=torch.int64, device=dev)
         sizes = self.all_gather_ints([int(mine.shape[1])])[:, 0]
@@ -259,9 +261,11 @@ def init_comm(device: str | None = None, backend: str | None = None, timeout_s: 
     be = backend or os.environ.get("FA_DIST_BACKEND") or ("nccl" if dev.type == "cuda" else "gloo")
     if be == "nccl":
         # one process per GPU: RCCL cannot run two ranks of one communicator on one device
+        # (a launcher that gives every rank exactly one visible GPU through
+        # HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES shows device_count() == 1: no check)
         n_local = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
         n_dev = torch.cuda.device_count()
-        if n_local > n_dev:
+        if n_dev > 1 and n_local > n_dev:
             raise RuntimeError(f"{n_local} local ranks but {n_dev} visible GPUs: RCCL needs one GPU per rank "
                                "(FA_DIST_BACKEND=gloo lets ranks share a GPU for tests)")
     if not dist.is_initialized():

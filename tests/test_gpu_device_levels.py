@@ -1,0 +1,87 @@
+"""Device-resident level bundles (FastApriori._mine_device; csrc/hip/gen.hip
+fa_hip_dl_*, csrc/hip/levels.hip) against the host-driven level loop and the C++
+CPU miner: identical itemsets, counts and level order (rows lexicographic).
+
+Covers unit and weighted (dedup) layouts, transaction trimming inside a device
+bundle, max_level, the hand-off to the host loop when level k needs several
+accumulator passes (T40I10 shape), and an empty F_2.
+Reference semantics: FastApriori.scala:110-160.
+"""
+import numpy as np
+import pytest
+import torch
+
+import fastapriori_amd.models.apriori as ap
+from fastapriori_amd.models.apriori import FastApriori, MinerConfig
+from fastapriori_amd.parallel.comm import Comm
+from fastapriori_amd.utils.io import generate_shard
+from fastapriori_amd.utils.metrics import Logger
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _mine(shard, ms, **kw):
+    cfg = MinerConfig(min_support=ms, **kw)
+    m = FastApriori(ms, config=cfg, logger=Logger(0, enabled=False))
+    return m.run(shard), m.stats
+
+
+def _same(a, b):
+    assert [len(x) for x in a.levels] == [len(x) for x in b.levels]
+    for x, y in zip(a.levels, b.levels):
+        assert np.array_equal(x, y)
+    for x, y in zip(a.counts, b.counts):
+        assert np.array_equal(x, y)
+    assert a.items == b.items
+
+
+@pytest.mark.parametrize("n,ms,kw", [
+    (300_000, 0.002, {}),
+    (300_000, 0.002, {"dedup": "on"}),
+    (1_200_000, 0.002, {"trim_min_rows": 0}),
+    (200_000, 0.003, {"max_level": 5}),
+    (50_000, 0.01, {"pair_strategy": "gram"}),
+])
+def test_device_levels_match_host_loop(monkeypatch, n, ms, kw):
+    cpu = generate_shard(n, Comm(), "cpu", 10.0, 4.0, 2000, 1000, 5)
+    g = cpu.to(DEV)
+    got, st = _mine(g, ms, **kw)
+    assert st.get("device_bundles", 0) >= 1
+    monkeypatch.setattr(ap, "DEVICE_LEVELS", False)
+    ref, st2 = _mine(g, ms, **kw)
+    assert "device_bundles" not in st2
+    _same(got, ref)
+    if n <= 300_000:
+        cref, _ = _mine(cpu, ms, **kw)
+        assert got.as_dict() == cref.as_dict()
+
+
+def test_device_levels_hand_off_multipass_level():
+    # T40I10: level 4's candidates need several accumulator passes -> host loop from there
+    cpu = generate_shard(150_000, Comm(), "cpu", 40.0, 10.0, 2000, 1000, 3)
+    got, st = _mine(cpu.to(DEV), 0.01)
+    ref, _ = _mine(cpu, 0.01)
+    assert len(ref.levels) >= 6
+    assert got.as_dict() == ref.as_dict()
+    assert [len(x) for x in got.levels] == [len(x) for x in ref.levels]
+
+
+def test_device_levels_no_frequent_pairs():
+    cpu = generate_shard(20_000, Comm(), "cpu", 10.0, 4.0, 2000, 1000, 2)
+    got, _ = _mine(cpu.to(DEV), 0.2)
+    ref, _ = _mine(cpu, 0.2)
+    assert got.as_dict() == ref.as_dict()
+
+
+def test_device_levels_repeat_runs_identical():
+    # buffers (workspace, control block, F sizes) are reused across runs
+    cpu = generate_shard(100_000, Comm(), "cpu", 10.0, 4.0, 2000, 1000, 7)
+    g = cpu.to(DEV)
+    m = FastApriori(0.003, config=MinerConfig(min_support=0.003), logger=Logger(0, enabled=False))
+    a = m.run(g)
+    b = m.run(g)
+    c = FastApriori(0.002, config=MinerConfig(min_support=0.002), logger=Logger(0, enabled=False)).run(g)
+    _same(a, b)
+    cref, _ = _mine(cpu, 0.002)
+    assert c.as_dict() == cref.as_dict()
