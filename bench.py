@@ -174,6 +174,38 @@ def _e2e_window(args, comm, n_txn, min_sup, cfgv, miner_cfg, sync):
     }, path
 
 
+def _per_rank(args, comm, miner, shard, own_ms, comm_ms, comm_calls, sync) -> list | None:
+    """Per-rank diagnostics of the timed steps, gathered to rank 0: the rank's own
+    ms per step, host ms held inside collectives (Comm._timed) and collectives per
+    step; then ONE extra, untimed run with hipEvent phase timers (FA_GPU_TIMING):
+    device time of the top-level phases (F1, compression, pairs, each level or
+    bundle; gaps inside a phase count as busy) and the rest of that run's wall time
+    as host-bound time.  A bad scaling curve then shows which rank and which part
+    (kernels, collectives, host steps) is slow."""
+    import re
+    if args.steps <= 0:
+        return None
+    rec = {"rank": comm.rank, "ms_per_step": round(own_ms, 3), "comm_ms_per_step": round(comm_ms, 3),
+           "collectives_per_step": round(comm_calls, 1)}
+    if comm.device.type == "cuda":
+        os.environ["FA_GPU_TIMING"] = "1"
+        try:
+            sync()
+            t0 = time.perf_counter()
+            miner.run(shard)
+            sync()
+            run_ms = (time.perf_counter() - t0) * 1e3
+        finally:
+            os.environ.pop("FA_GPU_TIMING", None)
+        ph = miner.stats.get("gpu_phase_ms", {})
+        top = {k: v for k, v in ph.items() if re.fullmatch(r"f1|compress|pairs|level\d+", k)}
+        gpu = sum(top.values())
+        rec.update(diag_run_ms=round(run_ms, 3), gpu_phase_ms=round(gpu, 3),
+                   host_bound_ms=round(max(run_ms - gpu, 0.0), 3),
+                   phases={k: round(v, 3) for k, v in top.items()})
+    return comm.all_gather_object(rec)
+
+
 def main() -> int:
     args = parse_args()
     in_torchrun = "WORLD_SIZE" in os.environ and "RANK" in os.environ
@@ -234,15 +266,20 @@ def main() -> int:
     gc.collect()
     gc.freeze()
     sync()
+    c_ms0, c_n0 = comm.comm_ms, comm.comm_calls
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res = miner.run(shard)
     sync()
     elapsed = time.perf_counter() - t0
-    ms_step = comm.allreduce_float_max(elapsed * 1e3 / max(args.steps, 1))
+    own_ms = elapsed * 1e3 / max(args.steps, 1)
+    comm_ms = (comm.comm_ms - c_ms0) / max(args.steps, 1)
+    comm_calls = (comm.comm_calls - c_n0) / max(args.steps, 1)
+    ms_step = comm.allreduce_float_max(own_ms)
     n_sets = res.n_itemsets
     value = n_sets / (ms_step / 1e3)
     stats = dict(miner.stats)
+    per_rank = _per_rank(args, comm, miner, shard, own_ms, comm_ms, comm_calls, sync)
 
     e2e = None
     want_e2e = args.e2e == "on" or (args.e2e == "auto" and not webdocs and args.strategy == "count")
@@ -285,6 +322,9 @@ def main() -> int:
                        **({"phase_ms": stats["phase_ms"]} if "phase_ms" in stats else {}),
                        **({"level_info": stats["level_info"]} if "level_info" in stats else {})},
             "e2e": e2e,
+            "per_rank": per_rank,
+            "rank_spread_ms": (round(max(r["ms_per_step"] for r in per_rank) - min(r["ms_per_step"] for r in per_rank),
+                                     3) if per_rank else None),
         }
         print(json.dumps(line), flush=True)
     shutdown_comm(comm)

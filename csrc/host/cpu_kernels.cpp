@@ -8,6 +8,8 @@
 //   wword    optional int32 per word: weight of every column in that word
 //            (columns are grouped by dedup weight class, padded to 64);
 //   counts   int64.
+#include <atomic>
+
 #include "fa_common.h"
 
 using namespace fa;
@@ -35,6 +37,27 @@ FA_API void fa_cpu_txn_freq_count(const int64_t* off, const int32_t* items, int6
       int32_t c = 0;
       for (int64_t i = off[t]; i < off[t + 1]; ++i) c += lut[items[i]] >= 0;
       out[t] = c;
+    }
+  });
+}
+
+// Compressed rows (FastApriori.scala:66-70): kept transaction x -> the ranks
+// lut[id] >= 0 of its ids, ascending, at ranks[roff[x] ..].  Rows are short
+// (insertion sort); rows are independent, so threads take row ranges.
+FA_API void fa_cpu_compress(const int64_t* off, const int32_t* items, const int32_t* lut, const int32_t* kept,
+                            int64_t T, const int64_t* roff, int32_t* ranks, int nthreads) {
+  parallel_for(T, nthreads, 1 << 14, [&](int64_t b, int64_t e, int) {
+    for (int64_t x = b; x < e; ++x) {
+      const int64_t t = kept[x];
+      int32_t* out = ranks + roff[x];
+      int64_t n = 0;
+      for (int64_t i = off[t]; i < off[t + 1]; ++i) {
+        const int32_t r = lut[items[i]];
+        if (r < 0) continue;
+        int64_t j = n++;
+        while (j > 0 && out[j - 1] > r) { out[j] = out[j - 1]; --j; }
+        out[j] = r;
+      }
     }
   });
 }
@@ -118,32 +141,66 @@ FA_API void fa_cpu_pair_horizontal(const int64_t* roff, const int32_t* ranks, in
 
 // Prefix-shared candidate support (FastApriori.scala:132-160 semantics):
 // group g = prefix ranks prefix[g][0..m) + extensions ext[ext_off[g]..ext_off[g+1]).
+//
+// Tiled like the GPU slab kernel: the columns are cut into tiles of kTileWords
+// words (2 KB of every item row), a thread takes a tile and runs EVERY group over
+// it -- the prefix AND once per group (the reference's commonArray), then each
+// extension's AND + popcount -- so a level streams each used item row from DRAM
+// once per tile instead of once per group, and the group loop reads L1/L2-resident
+// tiles.  A group whose prefix AND is empty on a tile skips its extensions there.
+// Each thread accumulates into its own count vector; the vectors are summed last.
 FA_API void fa_cpu_count_candidates(const uint64_t* bm, int64_t Wp, int64_t W,
                                     const int32_t* prefix, int32_t m, const int64_t* ext_off,
                                     const int32_t* ext, int64_t G, const int32_t* wword,
                                     int64_t* out, int nthreads) {
-  parallel_for(G, nthreads, 4, [&](int64_t g0, int64_t g1, int) {
-    std::vector<uint64_t> common((size_t)std::max<int64_t>(1, W));
-    for (int64_t g = g0; g < g1; ++g) {
-      const int32_t* p = prefix + g * m;
-      const uint64_t* r0 = bm + (int64_t)p[0] * Wp;
-      for (int64_t w = 0; w < W; ++w) common[w] = r0[w];
-      for (int q = 1; q < m; ++q) {
-        const uint64_t* rq = bm + (int64_t)p[q] * Wp;
-        for (int64_t w = 0; w < W; ++w) common[w] &= rq[w];
-      }
-      for (int64_t e = ext_off[g]; e < ext_off[g + 1]; ++e) {
-        const uint64_t* re = bm + (int64_t)ext[e] * Wp;
-        int64_t s = 0;
-        if (wword) {
-          for (int64_t w = 0; w < W; ++w) s += (int64_t)__builtin_popcountll(common[w] & re[w]) * wword[w];
-        } else {
-          for (int64_t w = 0; w < W; ++w) s += __builtin_popcountll(common[w] & re[w]);
+  constexpr int64_t kTileWords = 256;
+  const int64_t e_base = ext_off[0];
+  const int64_t C = ext_off[G] - e_base;
+  if (C <= 0 || W <= 0) {
+    for (int64_t e = 0; e < C; ++e) out[e] = 0;
+    return;
+  }
+  const int64_t ntile = (W + kTileWords - 1) / kTileWords;
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(nthreads, ntile));
+  std::vector<std::vector<int64_t>> loc((size_t)nt);
+  std::atomic<int64_t> next{0};
+  parallel_for_threads(nt, [&](int tid) {
+    auto& acc = loc[(size_t)tid];
+    acc.assign((size_t)C, 0);
+    uint64_t common[kTileWords];
+    for (;;) {
+      const int64_t t = next.fetch_add(1);
+      if (t >= ntile) break;
+      const int64_t w0 = t * kTileWords, nw = std::min(kTileWords, W - w0);
+      for (int64_t g = 0; g < G; ++g) {
+        const int32_t* p = prefix + g * m;
+        const uint64_t* r0 = bm + (int64_t)p[0] * Wp + w0;
+        for (int64_t w = 0; w < nw; ++w) common[w] = r0[w];
+        for (int q = 1; q < m; ++q) {
+          const uint64_t* rq = bm + (int64_t)p[q] * Wp + w0;
+          for (int64_t w = 0; w < nw; ++w) common[w] &= rq[w];
         }
-        out[e] = s;
+        uint64_t any = 0;
+        for (int64_t w = 0; w < nw; ++w) any |= common[w];
+        if (!any) continue;
+        for (int64_t e = ext_off[g]; e < ext_off[g + 1]; ++e) {
+          const uint64_t* re = bm + (int64_t)ext[e] * Wp + w0;
+          int64_t s = 0;
+          if (wword) {
+            for (int64_t w = 0; w < nw; ++w) s += (int64_t)__builtin_popcountll(common[w] & re[w]) * wword[w0 + w];
+          } else {
+            for (int64_t w = 0; w < nw; ++w) s += __builtin_popcountll(common[w] & re[w]);
+          }
+          acc[(size_t)(e - e_base)] += s;
+        }
       }
     }
   });
+  for (int64_t e = 0; e < C; ++e) {
+    int64_t s = 0;
+    for (int t = 0; t < nt; ++t) s += loc[(size_t)t][(size_t)e];
+    out[e] = s;
+  }
 }
 
 // Open-addressing probe table for the heavy-hitter F1 exact pass

@@ -54,6 +54,7 @@ _HOST_SIGS = {
     "fa_cpu_histogram": (None, [vp, i64, i64, vp, C.c_int]),
     "fa_build_probe_table": (None, [vp, i64, C.c_int, C.c_uint32, vp, vp]),
     "fa_cpu_txn_freq_count": (None, [vp, vp, i64, vp, vp, C.c_int]),
+    "fa_cpu_compress": (None, [vp, vp, vp, vp, i64, vp, vp, C.c_int]),
     "fa_cpu_build_bitmaps": (None, [vp, vp, vp, i64, i64, vp, C.c_int]),
     "fa_cpu_row_hash": (None, [vp, vp, i64, vp, vp, C.c_int]),
     "fa_cpu_pair_gram": (None, [vp, i32, i64, i64, vp, vp, C.c_int]),

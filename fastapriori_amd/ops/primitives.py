@@ -193,7 +193,9 @@ def compress(offsets, items, lut, kept, roff, F1: int | None = None) -> torch.Te
     if T == 0:
         return ranks[:0]
     if not items.is_cuda:
-        return _compress_torch(offsets, items, lut, kept, roff, ranks, None)[:nnz]
+        _native.host().fa_cpu_compress(_p(offsets), _p(items), _p(lut), _p(kept), T, _p(roff), _p(ranks),
+                                       num_threads())
+        return ranks[:nnz]
     st = _stream(items)
     wave_ok = F1 is not None and F1 <= COMPRESS_WAVE_MAX_F1
     if wave_ok and items.numel() > COMPRESS_WAVE_MEAN_LEN * max(offsets.numel() - 1, 1):

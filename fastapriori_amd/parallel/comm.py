@@ -19,13 +19,34 @@ can pipeline them (``FA_BUCKET_MB``, default 64 MiB).
 """
 from __future__ import annotations
 
+import functools
 import os
 import pickle
+import time
 from dataclasses import dataclass
 
 import numpy as np
 import torch
 import torch.distributed as dist
+
+
+def _timed(fn):
+    """Host wall time spent inside the collectives (comm_ms; nested calls count once).
+    RCCL collectives are asynchronous: this is the time the host is held, including
+    the readbacks the small decision collectives need (bench.py per-rank record)."""
+    @functools.wraps(fn)
+    def wrap(self, *a, **kw):
+        if self._depth:
+            return fn(self, *a, **kw)
+        self._depth += 1
+        t0 = time.perf_counter()
+        try:
+            return fn(self, *a, **kw)
+        finally:
+            self._depth -= 1
+            self.comm_ms += (time.perf_counter() - t0) * 1e3
+            self.comm_calls += 1
+    return wrap
 
 
 @dataclass
@@ -36,6 +57,9 @@ class Comm:
     backend: str = "none"
     bytes_reduced: int = 0
     force: bool = False     # run the collective code paths even at world size 1 (FA_FORCE_PG)
+    comm_ms: float = 0.0    # host time inside collectives (see _timed)
+    comm_calls: int = 0
+    _depth: int = 0
 
     @property
     def distributed(self) -> bool:
@@ -49,6 +73,7 @@ class Comm:
     def _comm_device(self) -> torch.device:
         return self.device if self.backend == "nccl" else torch.device("cpu")
 
+    @_timed
     def all_reduce_(self, t: torch.Tensor, op=None, bound: int | None = None) -> torch.Tensor:
         """In-place sum (or ``op``) across ranks; returns the tensor on its own device.
 
@@ -76,6 +101,7 @@ class Comm:
             t.copy_(x)
         return t
 
+    @_timed
     def reduce_scatter_select(self, t: torch.Tensor, thr: int, bound: int | None = None):
         """Entries of the cross-rank sum of ``t`` that are >= ``thr``: (indices, values),
         identical on every rank and in index order.
@@ -118,6 +144,7 @@ class Comm:
         q = max(1, self.world_size * 7 * 64)
         return max(q, n // q * q)
 
+    @_timed
     def allreduce_int(self, v: int, op: str = "sum") -> int:
         if not self.distributed:
             return int(v)
@@ -125,6 +152,7 @@ class Comm:
         dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
         return int(t.item())
 
+    @_timed
     def allreduce_float_max(self, v: float) -> float:
         if not self.distributed:
             return float(v)
@@ -132,6 +160,7 @@ class Comm:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    @_timed
     def all_gather_int(self, v: int) -> list[int]:
         if not self.distributed:
             return [int(v)]
@@ -140,6 +169,7 @@ class Comm:
         dist.all_gather(out, t)
         return [int(x.item()) for x in out]
 
+    @_timed
     def all_gather_ints(self, values) -> np.ndarray:
         """One collective for several small integers: int64 [world, len(values)]."""
         v = np.asarray(values, dtype=np.int64).reshape(1, -1)
@@ -150,6 +180,7 @@ class Comm:
         dist.all_gather_into_tensor(out, t)
         return out.cpu().numpy().reshape(self.world_size, -1)
 
+    @_timed
     def all_gather_varlen_np(self, a: np.ndarray) -> list[np.ndarray]:
         """All-gather 1-D int64 arrays of different lengths (sizes, then one padded
         all_gather_into_tensor): rank order, on every rank."""
@@ -167,6 +198,7 @@ class Comm:
         o = out.cpu().numpy().reshape(self.world_size, mx)
         return [o[r, :int(sizes[r])] for r in range(self.world_size)]
 
+    @_timed
     def all_gather_object(self, obj) -> list:
         if not self.distributed:
             return [obj]
@@ -174,6 +206,7 @@ class Comm:
         dist.all_gather_object(out, obj)
         return out
 
+    @_timed
     def broadcast_object(self, obj, src: int = 0):
         if not self.distributed:
             return obj
@@ -181,6 +214,7 @@ class Comm:
         dist.broadcast_object_list(box, src=src)
         return box[0]
 
+    @_timed
     def gather_varlen(self, t: torch.Tensor) -> list[torch.Tensor] | None:
         """Gather 1-D tensors of different lengths to rank 0 (None elsewhere)."""
         if not self.distributed:
@@ -196,6 +230,7 @@ class Comm:
             return None
         return [o[:s].cpu() for o, s in zip(outs, sizes)]
 
+    @_timed
     def all_to_all_varlen(self, parts: list[np.ndarray], dtype=np.int64) -> list[np.ndarray]:
         """Exchange variable-length int arrays: parts[r] goes to rank r."""
         if not self.distributed:
@@ -217,6 +252,7 @@ class Comm:
             o += s
         return res
 
+    @_timed
     def barrier(self) -> None:
         if self.distributed:
             if self.backend == "nccl":

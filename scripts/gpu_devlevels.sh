@@ -18,3 +18,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --marker-trace --output-format csv -d
   python3 "$R/bench.py" --n-txn 12500000 --steps 2 --warmup 1 --e2e off > "$R/gpurun_out/dlmk12.log" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --marker-trace --output-format csv -d "$R/gpurun_out/dlmkh" -o run -- \
   python3 "$R/bench.py" --steps 2 --warmup 1 --e2e off > "$R/gpurun_out/dlmkh.log" 2>&1
+cd "$R"
+timeout -k 10 900 python benchmarks/run_bench.py --mode cpu --device cpu --config T10I4D100M --steps 1 --warmup 0 > gpurun_out/cpu_T10I4D100M.json 2> gpurun_out/cpu_T10I4D100M.err

@@ -165,3 +165,26 @@ def test_forced_process_group_at_world_one(numeric_db):
     ref = spawn_local(_mine_file, 1, numeric_db, 0.02, "auto", "auto")[0]
     got = spawn_local(_mine_file, 1, numeric_db, 0.02, "auto", "auto", env={"FA_FORCE_PG": "1"})[0]
     assert got == ref
+
+
+def _rs_select(n: int, thr: int):
+    import torch
+    from fastapriori_amd.parallel.comm import init_comm, shutdown_comm
+    comm = init_comm("cpu")
+    try:
+        g = torch.Generator().manual_seed(11 + comm.rank)
+        t = torch.randint(0, 3, (n,), generator=g, dtype=torch.int64)
+        idx, val = comm.reduce_scatter_select(t.clone(), thr, bound=1 << 20)
+        full = comm.all_reduce_(t.clone())
+        return idx.tolist(), val.tolist(), full.tolist()
+    finally:
+        shutdown_comm(comm)
+
+
+@pytest.mark.parametrize("thr", [0, 3])
+def test_reduce_scatter_select_ignores_padding(thr):
+    # 10 entries over 3 ranks: chunks of 4, two zero-padding slots that a threshold of 0
+    # (min_support 0) must not select (parallel/comm.py reduce_scatter_select)
+    for idx, val, full in spawn_local(_rs_select, 3, 10, thr):
+        want = [i for i, v in enumerate(full) if v >= thr]
+        assert idx == want and val == [full[i] for i in want]

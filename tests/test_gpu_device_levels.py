@@ -41,16 +41,17 @@ def _same(a, b):
     (300_000, 0.002, {"dedup": "on"}),
     (1_200_000, 0.002, {"trim_min_rows": 0}),
     (200_000, 0.003, {"max_level": 5}),
-    (50_000, 0.01, {"pair_strategy": "gram"}),
+    (50_000, 0.004, {"pair_strategy": "gram"}),
 ])
 def test_device_levels_match_host_loop(monkeypatch, n, ms, kw):
     cpu = generate_shard(n, Comm(), "cpu", 10.0, 4.0, 2000, 1000, 5)
     g = cpu.to(DEV)
     got, st = _mine(g, ms, **kw)
-    assert st.get("device_bundles", 0) >= 1
     monkeypatch.setattr(ap, "DEVICE_LEVELS", False)
     ref, st2 = _mine(g, ms, **kw)
     assert "device_bundles" not in st2
+    if len(ref.levels) >= 3:
+        assert st.get("device_bundles", 0) >= 1
     _same(got, ref)
     if n <= 300_000:
         cref, _ = _mine(cpu, ms, **kw)

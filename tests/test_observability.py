@@ -62,3 +62,21 @@ def test_world_size_launches_ranks(tmp_path):
     assert r1.returncode == 0 and r2.returncode == 0, r2.stderr[-3000:]
     for part in ("freqItemset/part-00000", "recommends/part-00000"):
         assert open(d + "o1/" + part).read() == open(d + "o2/" + part).read()
+
+
+def test_fallbacks_are_reported_by_the_run_that_took_them(tmp_path):
+    # a fallback noted by an earlier phase is not re-reported by a later mining run,
+    # and the rules phase reports its own (ops.primitives.reset_fallbacks)
+    from fastapriori_amd import ops
+    from fastapriori_amd.models.apriori import FastApriori, MinerConfig
+    from fastapriori_amd.models.rules import AssociationRules
+    from fastapriori_amd.utils.io import parse_bytes
+    from fastapriori_amd.utils.metrics import Logger
+    ops.primitives.note_fallback("test: an earlier phase took a host fallback")
+    shard = parse_bytes(b"1 2 3\n1 2 4\n2 3 4\n1 2 4\n2 4\n4 5\n1 2\n")
+    m = FastApriori(0.25, config=MinerConfig(min_support=0.25), logger=Logger(0, enabled=False))
+    res = m.run(shard)
+    assert "fallbacks" not in m.stats and ops.primitives.FALLBACKS == []
+    ar = AssociationRules(res, logger=Logger(0, enabled=False))
+    ar.run(parse_bytes(b"1\n2\n"))
+    assert "fallbacks" not in ar.stats

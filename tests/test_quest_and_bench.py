@@ -57,3 +57,22 @@ def test_bench_json_contract():
     assert d["steps"] == 2 and d["warmup"] == 1 and d["higher_is_better"] is True
     assert d["value"] > 0 and d["config"]["n_itemsets"] > 0
     assert abs(d["value"] - d["config"]["n_itemsets"] / (d["ms_per_step"] / 1e3)) / d["value"] < 0.01
+
+
+def test_bench_per_rank_record_world8():
+    # bench.py --gpus 8 relaunches itself under torch.distributed.run (gloo on the CPU here):
+    # the JSON line carries one diagnostic record per rank plus the spread
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--device", "cpu",
+                        "--config", "T10I4D1K", "--steps", "2", "--warmup", "1", "--e2e", "off"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["world_size"] == 8 and d["config"]["parallelism"] == "dp8"
+    pr = d["per_rank"]
+    assert [p["rank"] for p in pr] == list(range(8))
+    for p in pr:
+        assert p["ms_per_step"] > 0 and p["comm_ms_per_step"] >= 0 and p["collectives_per_step"] > 0
+    assert d["ms_per_step"] == max(p["ms_per_step"] for p in pr)
+    assert d["rank_spread_ms"] == round(max(p["ms_per_step"] for p in pr) - min(p["ms_per_step"] for p in pr), 3)
