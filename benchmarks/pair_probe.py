@@ -2,11 +2,11 @@
 
 Mines a config once, recording the arguments of the ops.pair_counts_horizontal
 call, then replays it under FA_PAIR_DEBUG = 0 (full), 1 (no scatter), 2 (no
-flush), 3 (neither) and each FA_PAIR_KERNEL variant given, and prints the
-times (CUDA events, median of --reps) plus a check that every full variant
-returns identical counts.
+flush), 3 (neither), 4 (layout kernels only) and each FA_PAIR_FLAT setting given,
+and prints the times (CUDA events, median of --reps) plus a check that every full
+variant returns identical counts.
 
-    python benchmarks/pair_probe.py --config T10I4D100M --kernels rows16,queue16
+    python benchmarks/pair_probe.py --config T10I4D100M --flat 2,1
 """
 import argparse
 import json
@@ -31,7 +31,7 @@ def main():
     ap.add_argument("--n-txn", type=int, default=0)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--modes", default="0,1,2,3,4")
-    ap.add_argument("--kernels", default="", help="comma list of FA_PAIR_ROWS_KERNEL values")
+    ap.add_argument("--flat", default="", help="comma list of FA_PAIR_FLAT values")
     a = ap.parse_args()
     n, L, I, P, N, ms = bench.CONFIGS[a.config]
     n = a.n_txn or n
@@ -51,9 +51,9 @@ def main():
     print(json.dumps({"rows": int(lens.numel()), "nnz": int(lens.sum()),
                       "pair_increments": int((lens * (lens - 1) // 2).sum())}), flush=True)
     ref = None
-    for kern in (a.kernels.split(",") if a.kernels else [""]):
+    for kern in (a.flat.split(",") if a.flat else [""]):
         if kern:
-            os.environ["FA_PAIR_ROWS_KERNEL"] = kern
+            os.environ["FA_PAIR_FLAT"] = kern
         row = {"kernel": kern or "default"}
         for mode in a.modes.split(","):
             os.environ["FA_PAIR_DEBUG"] = mode

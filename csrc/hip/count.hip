@@ -4,11 +4,12 @@
 // pairs, AND of two byte-per-transaction arrays + weighted sum) and
 // :132-160 (genNextFreqItemsets: prefix AND once per group, then AND + sum per
 // extension).  Here:
-//   * k_pair_horizontal  : sparse data — every transaction's sorted rank list
-//     scatters its pairs into an LDS-resident 128x128 count tile (ds_add_u32),
-//     one global atomic per non-zero tile entry per workgroup.
-//   * k_pair_gram_popc   : dense data — bit-matrix Gram B^T diag(w) B over the
-//     vertical bitmaps, 64x64 item tiles staged through LDS, v_bcnt popcounts.
+//   * k_pair_queue16 / k_pair_blocked : sparse data — rows re-laid out per rank
+//     block; every tile of the pair matrix is counted in LDS (packed u16 / u32)
+//     from its two blocks' segments, one global atomic per non-zero entry.
+//   * k_pair_gram_mfma4  : dense data — bit-matrix Gram B^T B on the int8 matrix
+//     cores (per weight class with a scale); k_pair_gram_popc the v_bcnt form
+//     for short weight classes.
 //   * k_count_candidates : k >= 3 — prefix-shared AND + popcount per group of
 //     candidates over a super-chunk of bitmap words; wave reductions into an
 //     LDS accumulator, one coalesced global atomic per candidate per chunk.
@@ -54,133 +55,6 @@ constexpr int kWSpan = 1024;           // ranks staged per wave batch
 constexpr int kWPer = kWSpan / 64;     // per lane
 
 __device__ __forceinline__ void wave_lds_fence() { wave_lds_sync(); }
-
-// Per-row block table: bt[x*(nb+1) + b] = offset (within row x) of its first
-// rank >= b*kPB; bt[x*(nb+1) + nb] = row length.  Built once per mining run so
-// tile visits find their segments with two byte loads instead of a scan.
-template <typename BT>
-__global__ __launch_bounds__(256) void k_block_table(const int64_t* __restrict__ roff,
-                                                     const int32_t* __restrict__ ranks, int64_t T, int nb,
-                                                     BT* __restrict__ bt) {
-  const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (x >= T) return;
-  const int64_t s = roff[x], e = roff[x + 1];
-  BT* out = bt + x * (nb + 1);
-  int64_t i = s;
-  for (int b = 0; b < nb; ++b) {
-    const int edge = b * kPB;
-    while (i < e && ranks[i] < edge) ++i;
-    out[b] = (BT)(i - s);
-  }
-  out[nb] = (BT)(e - s);
-}
-
-template <typename BT>
-__global__ __launch_bounds__(1024) void k_pair_horizontal(
-    const int64_t* __restrict__ roff, const int32_t* __restrict__ ranks, int64_t T,
-    const int32_t* __restrict__ wrow, const BT* __restrict__ bt, int32_t F1, int nb, int nbp, int64_t chunk,
-    uint32_t* __restrict__ out) {
-  __shared__ uint32_t tile[kPB * kPB];
-  __shared__ uint16_t wspan[kPW][kWSpan];
-  __shared__ int32_t wmeta[kPW][4][64];           // per lane: pair prefix, i-start, weight, (j0-i0)|nj<<24
-  const uint32_t logical = xcd_remap(blockIdx.x, gridDim.x);
-  const int pid = logical % nbp;
-  const int64_t ch = logical / nbp;
-  int bi, bj;
-  tri_index(pid, nb, bi, bj);
-  const int rb0 = bi * kPB, cb0 = bj * kPB;
-  const bool diag = bi == bj;
-  for (int i = threadIdx.x; i < kPB * kPB; i += blockDim.x) tile[i] = 0;
-  __syncthreads();
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  int32_t* mpre = wmeta[wv][0];
-  int32_t* mist = wmeta[wv][1];
-  int32_t* mwt = wmeta[wv][2];
-  int32_t* mjn = wmeta[wv][3];
-  const int64_t x0 = ch * chunk, x1 = min(T, x0 + chunk);
-  const int64_t nbatch = x1 > x0 ? (x1 - x0 + 63) / 64 : 0;
-  const int nbp1 = nb + 1;
-  struct Ro { int64_t ro, end; uint32_t w; int si0, si1, sj0, sj1; };
-  Ro A{}, B{};
-  auto load_ro = [&](int64_t q, Ro& r) {
-    const int64_t xb = x0 + q * 64, xe = min(x1, xb + 64), x = xb + lane;
-    const bool valid = x < xe;
-    r.ro = roff[valid ? x : xe];
-    r.end = roff[xe];
-    r.w = valid ? (wrow ? (uint32_t)wrow[x] : 1u) : 0u;
-    const BT* row = bt + (valid ? x : 0) * nbp1;
-    r.si0 = row[bi]; r.si1 = row[bi + 1];
-    if (diag) { r.sj0 = r.si0; r.sj1 = r.si1; }
-    else { r.sj0 = row[bj]; r.sj1 = row[bj + 1]; }
-  };
-  int64_t q = wv;
-  if (q < nbatch) load_ro(q, A);
-  for (; q < nbatch; q += kPW) {
-    if (q + kPW < nbatch) load_ro(q + kPW, B);     // prefetch: lands while this batch scatters
-    const int ni = A.w ? A.si1 - A.si0 : 0;
-    const int nj = A.w ? A.sj1 - A.sj0 : 0;
-    const int P = (ni > 0 && nj > 0) ? ni * nj : 0;
-    int incl = P;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int t = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += t;
-    }
-    const int total = __shfl(incl, 63, 64);
-    if (total > 0) {
-      // row-local pair rectangle, addressed relative to this batch's first row
-      const int64_t base = __shfl(A.ro, 0, 64);
-      // lazily stage this batch's ranks (coalesced) — only batches with pairs in the tile
-      const int64_t n = A.end - base;
-      const bool staged = n <= kWSpan;
-      uint16_t* sp = wspan[wv];
-      if (staged) {
-        int32_t v[kWPer];
-#pragma unroll
-        for (int k = 0; k < kWPer; ++k) {
-          const int64_t i = lane + 64 * k;
-          v[k] = i < n ? ranks[base + i] : 0;
-        }
-#pragma unroll
-        for (int k = 0; k < kWPer; ++k) {
-          const int64_t i = lane + 64 * k;
-          if (i < n) sp[i] = (uint16_t)v[k];
-        }
-      }
-      mpre[lane] = incl - P;
-      mist[lane] = (int)(A.ro - base + A.si0);                  // i-segment start within the batch
-      mwt[lane] = (int)A.w;
-      mjn[lane] = (A.sj0 - A.si0) | (nj << 24);                 // j-segment offset | nj (<= 128)
-      wave_lds_fence();
-      for (int f = lane; f < total; f += 64) {
-        int owner = 0;
-#pragma unroll
-        for (int step = 32; step > 0; step >>= 1)
-          if (mpre[owner + step] <= f) owner += step;
-        const int loc = f - mpre[owner];
-        const int packed = mjn[owner];
-        const int cols = (int)((uint32_t)packed >> 24);
-        const int ii = (int)(((float)loc + 0.5f) * __builtin_amdgcn_rcpf((float)cols));
-        const int jj = loc - ii * cols;
-        if (diag && jj <= ii) continue;
-        const int64_t ia = mist[owner] + ii;
-        const int64_t jb = ia - ii + (packed & 0xFFFFFF) + jj;
-        const int ra = staged ? (int)sp[ia] : ranks[base + ia];
-        const int rb = staged ? (int)sp[jb] : ranks[base + jb];
-        atomicAdd(&tile[(ra - rb0) * kPB + (rb - cb0)], (uint32_t)mwt[owner]);
-      }
-      wave_lds_fence();
-    }
-    A = B;
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < kPB * kPB; i += blockDim.x) {
-    const uint32_t v = tile[i];
-    if (!v) continue;
-    const int r = rb0 + i / kPB, c = cb0 + i % kPB;
-    if (r < F1 && c < F1) atomicAdd(&out[(int64_t)r * F1 + c], v);
-  }
-}
 
 // ---------------------------------------------------------------------------
 // k = 2, blocked layout.  Rows are re-laid out per 128-rank block:
@@ -458,85 +332,11 @@ __global__ __launch_bounds__(1024) void k_pair_blocked(
 // can carry into its neighbour before the flush.
 constexpr int kPB16 = 256;
 
-__global__ __launch_bounds__(1024) void k_pair_blocked16(
-    const uint8_t* __restrict__ cnt, const int64_t* __restrict__ base, const uint8_t* __restrict__ lr,
-    int64_t T, int64_t nbatch, int32_t F1, int nb, int nbp, int64_t chunk_b, uint32_t* __restrict__ out) {
-  __shared__ uint32_t tile[kPB16 * kPB16 / 2];
-  __shared__ int32_t wmeta[kPW][4][64];
-  const uint32_t logical = xcd_remap(blockIdx.x, gridDim.x);
-  const int pid = logical % nbp;
-  const int64_t ch = logical / nbp;
-  int bi, bj;
-  tri_index(pid, nb, bi, bj);
-  const int rb0 = bi * kPB16, cb0 = bj * kPB16;
-  const bool diag = bi == bj;
-  for (int i = threadIdx.x; i < kPB16 * kPB16 / 2; i += blockDim.x) tile[i] = 0;
-  __syncthreads();
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  int32_t* mpre = wmeta[wv][0];
-  int32_t* mist = wmeta[wv][1];
-  int32_t* mjst = wmeta[wv][2];
-  int32_t* mnj = wmeta[wv][3];
-  const int64_t q0 = ch * chunk_b, q1 = min(nbatch, q0 + chunk_b);
-  const uint8_t* ci_row = cnt + (int64_t)bi * T;
-  const uint8_t* cj_row = cnt + (int64_t)bj * T;
-  int ci = 0, cj = 0, ci_n = 0, cj_n = 0;
-  auto load = [&](int64_t q, int& a, int& b) {
-    const int64_t x = q * 64 + lane;
-    a = x < T ? ci_row[x] : 0;
-    b = diag ? a : (x < T ? cj_row[x] : 0);
-  };
-  int64_t q = q0 + wv;
-  if (q < q1) load(q, ci, cj);
-  for (; q < q1; q += kPW) {
-    if (q + kPW < q1) load(q + kPW, ci_n, cj_n);
-    const int P = (ci > 0 && cj > 0) ? ci * cj : 0;
-    const int incl = wave_scan_incl_dpp(P);
-    const int total = wave_last(incl);
-    if (total > 0) {
-      const int inci = wave_scan_incl_dpp(ci);
-      const int incj = diag ? inci : wave_scan_incl_dpp(cj);
-      const uint8_t* A = lr + base[(int64_t)bi * nbatch + q];
-      const uint8_t* B = lr + base[(int64_t)bj * nbatch + q];
-      mpre[lane] = incl - P;
-      mist[lane] = inci - ci;
-      mjst[lane] = incj - cj;
-      mnj[lane] = cj;
-      wave_lds_fence();
-      for (int f = lane; f < total; f += 64) {
-        int owner = 0;
-#pragma unroll
-        for (int step = 32; step > 0; step >>= 1)
-          if (mpre[owner + step] <= f) owner += step;
-        const int loc = f - mpre[owner];
-        const int cols = mnj[owner];
-        const int ii = (int)(((float)loc + 0.5f) * __builtin_amdgcn_rcpf((float)cols));
-        const int jj = loc - ii * cols;
-        if (diag && jj <= ii) continue;
-        const int idx = (int)A[mist[owner] + ii] * kPB16 + (int)B[mjst[owner] + jj];
-        atomicAdd(&tile[idx >> 1], (idx & 1) ? 0x10000u : 1u);
-      }
-      wave_lds_fence();
-    }
-    ci = ci_n; cj = cj_n;
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < kPB16 * kPB16 / 2; i += blockDim.x) {
-    const uint32_t v = tile[i];
-    if (!v) continue;
-    const int idx = 2 * i;
-    const int r = rb0 + idx / kPB16, c = cb0 + idx % kPB16;
-    if (r >= F1) continue;
-    if ((v & 0xFFFF) && c < F1) atomicAdd(&out[(int64_t)r * F1 + c], v & 0xFFFF);
-    if ((v >> 16) && c + 1 < F1) atomicAdd(&out[(int64_t)r * F1 + c + 1], v >> 16);
-  }
-}
-
 // ---------------------------------------------------------------------------
 // k = 2, unit-weight rows: one lane per (row, item-in-block-bi) position.
 //
-// Same blocked layout and 256x256 packed-u16 LDS tile as k_pair_blocked16, but
-// instead of flattening pairs (a 6-step dependent LDS binary search per pair),
+// Blocked layout with 256-rank blocks and a 256x256 packed-u16 LDS tile.  Instead
+// of flattening pairs by a dependent LDS binary search per pair,
 // a lane takes one position p of the batch's block-bi local ranks and loops
 // over its row's block-bj ranks.  The batch's local-rank bytes are staged in
 // per-wave LDS (coalesced loads); the row of position p comes from the
@@ -818,34 +618,14 @@ __device__ __forceinline__ void pair_tile16_flush(const uint32_t* tile, int bi, 
   }
 }
 
-__global__ __launch_bounds__(1024) void k_pair_rows16(
-    const uint8_t* __restrict__ cnt, const int64_t* __restrict__ base, const uint8_t* __restrict__ lr,
-    int64_t T, int64_t nbatch, int32_t F1, int nb, int nbp, int64_t chunk_b, uint32_t* __restrict__ out, int dbg) {
-  __shared__ PairRowsLds L;
-  const uint32_t logical = xcd_remap(blockIdx.x, gridDim.x);
-  const int pid = logical % nbp;
-  // one chunk of <= 65472 rows per workgroup keeps the 16-bit counters exact.
-  // (Folding many chunks into u32 register accumulators instead, to cut the
-  // flush atomics, measured slower: 64 more VGPRs spill at 16 waves/CU.)
-  const int64_t ch = logical / nbp;
-  int bi, bj;
-  tri_index(pid, nb, bi, bj);
-  for (int i = threadIdx.x; i < kPB16 * kPB16 / 2; i += blockDim.x) L.tile[i] = 0;
-  __syncthreads();
-  const int64_t q0 = ch * chunk_b, q1 = min(nbatch, q0 + chunk_b);
-  pair_rows16_chunk(L, cnt, base, lr, T, nbatch, bi, bj, q0, q1, dbg);
-  __syncthreads();
-  if (!(dbg & 2)) pair_tile16_flush(L.tile, bi, bj, F1, F1, out);
-}
-
 // Work-queue schedule of the same tiles: one persistent workgroup per CU, a
 // queue of sub-chunks (<= 32767 rows) per tile.  A workgroup starts on its home
 // tile (blockIdx % nbp) and keeps its LDS tile across sub-chunks: after each
 // one, counters with bit 15 set give 32768 to the global count ("drain"), so
 // every counter stays < 32768 + 32767 and a tile is flushed only when the
 // workgroup moves to another tile (then: the tile with the most sub-chunks
-// left) or ends.  The one-chunk-per-workgroup schedule (k_pair_rows16) flushes
-// a full 64K-counter tile per 65K rows: ~1e9 global atomics on T10I4D100M.
+// left) or ends.  (A one-chunk-per-workgroup schedule flushed a full 64K-counter
+// tile per 65K rows: ~1e9 global atomics on T10I4D100M.)
 // Every workgroup exits once all queues are exhausted (each grab increments a
 // queue counter, which never decreases).
 constexpr int64_t kQSubB = 511;   // batches per sub-chunk: 32704 rows
@@ -993,14 +773,14 @@ __global__ __launch_bounds__(256) void k_pair_gram_popc(
 }
 
 // ---------------------------------------------------------------------------
-// k = 2, dense bit-matrix Gram on the matrix cores (unit weights).
+// k = 2, dense bit-matrix Gram on the matrix cores (one weight class per launch).
 //
 // count[a][b] = sum_t bit_a(t) bit_b(t) = (B^T B)[a][b] with B the T x F1 0/1
 // matrix: a GEMM with K = transactions.  Bits are unpacked to int8 in registers
 // (a nibble n -> 4 bytes by (n * 0x204081) & 0x01010101, no carries) and fed
-// to v_mfma_i32_32x32x32_i8 with exact int32 accumulation.  A workgroup owns a
-// 128 x 128 item tile (4 waves x 64 x 64 = 2 x 2 MFMA tiles each) and a chunk
-// of bitmap words, staged through LDS 8 words (512 transactions) at a time
+// to v_mfma_i32_32x32x32_i8 with exact int32 accumulation.  A workgroup owns an
+// item tile (4 waves, each a square of 32 x 32 MFMA tiles) and a chunk of bitmap
+// words, staged through LDS 8 words (512 transactions) at a time
 // with coalesced 64-byte row reads; partial tiles are added with one atomic
 // per element.  Lane (r, h) supplies A[r][16h + j] and B[16h + j][c] from the
 // same 16 transactions, so the K pairing is exact whatever the hardware's
@@ -1008,7 +788,6 @@ __global__ __launch_bounds__(256) void k_pair_gram_popc(
 // ---------------------------------------------------------------------------
 typedef int fa_v4i __attribute__((ext_vector_type(4)));
 typedef int fa_v16i __attribute__((ext_vector_type(16)));
-constexpr int kMT = 128;     // items per tile side
 constexpr int kMW = 8;       // words staged per step
 constexpr int kMS = kMW + 1; // LDS row stride (words): 72 B rows -> conflict-free ds_read_b64
 
@@ -1021,79 +800,9 @@ __device__ __forceinline__ fa_v4i unpack16_i8(uint32_t b) {
   return r;
 }
 
-__global__ __launch_bounds__(256) void k_pair_gram_mfma(const uint64_t* __restrict__ bm, int32_t F1, int64_t Wp,
-                                                        int64_t W, int nt, int ntp, int64_t kchunk,
-                                                        uint32_t* __restrict__ out) {
-  __shared__ uint64_t As[kMT * kMS];
-  __shared__ uint64_t Bs[kMT * kMS];
-  const int tp = blockIdx.x % ntp;
-  const int64_t kc = blockIdx.x / ntp;
-  int ti, tj;
-  tri_index(tp, nt, ti, tj);
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int r = lane & 31, h = lane >> 5;
-  const int wr = (wv >> 1) * 64, wc = (wv & 1) * 64;     // the wave's 64 x 64 sub-tile
-  fa_v16i acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = fa_v16i{0};
-  const int64_t k_begin = kc * kchunk, k_end = min(W, k_begin + kchunk);
-  for (int64_t k0 = k_begin; k0 < k_end; k0 += kMW) {
-    // stage 128 rows x 8 words of each operand: thread = (row, word), 4 per thread
-#pragma unroll
-    for (int it = 0; it < (kMT * kMW) / 256; ++it) {
-      const int idx = threadIdx.x + it * 256;
-      const int row = idx >> 3, w = idx & 7;
-      const int ra = ti * kMT + row, rb = tj * kMT + row;
-      const int64_t kk = k0 + w;
-      As[row * kMS + w] = (ra < F1 && kk < k_end) ? bm[(int64_t)ra * Wp + kk] : 0ull;
-      Bs[row * kMS + w] = (rb < F1 && kk < k_end) ? bm[(int64_t)rb * Wp + kk] : 0ull;
-    }
-    __syncthreads();
-#pragma unroll 2
-    for (int w = 0; w < kMW; ++w) {
-      uint64_t a[2], b[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        a[i] = As[(wr + 32 * i + r) * kMS + w];
-        b[i] = Bs[(wc + 32 * i + r) * kMS + w];
-      }
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2) {                  // two 32-transaction k-steps per word
-        const int sh = 32 * s2 + 16 * h;
-        fa_v4i fa[2], fb[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          fa[i] = unpack16_i8((uint32_t)(a[i] >> sh) & 0xFFFFu);
-          fb[i] = unpack16_i8((uint32_t)(b[i] >> sh) & 0xFFFFu);
-        }
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[i], fb[j], acc[i][j], 0, 0, 0);
-      }
-    }
-    __syncthreads();
-  }
-  // C/D layout (gfx950, 32x32): col = lane & 31, row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5)
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        const int row = ti * kMT + wr + 32 * i + (g & 3) + 8 * (g >> 2) + 4 * h;
-        const int col = tj * kMT + wc + 32 * j + r;
-        const int v = acc[i][j][g];
-        if (row < col && col < F1 && v) atomicAdd(&out[(int64_t)row * F1 + col], (uint32_t)v);
-      }
-}
-
-// Same Gram with a 128 x 128 register tile per wave (4 x 4 MFMA tiles, 256
-// accumulator registers, one wave per SIMD) and a 256 x 256 workgroup tile.  The
-// 2 x 2-tile form above spends more VALU on unpacking bits to int8 than the MFMA
+// Bit-matrix Gram on the matrix cores with a 128 x 128 register tile per wave (4 x 4
+// MFMA tiles, 256 accumulator registers, one wave per SIMD) and a 256 x 256 workgroup
+// tile.  A 2 x 2-tile form (removed) spent more VALU on unpacking bits to int8 than the MFMA
 // pipe needs (~14 VALU per 32x32x32 MFMA, i.e. longer than the MFMA's 32 cycles);
 // with 4 x 4 tiles every unpacked fragment feeds four MFMAs instead of two.  The
 // next stage's words are loaded into registers while the current one is counted.
@@ -1105,7 +814,7 @@ constexpr int kM4Ld = kMT4 * kMW / 256;   // staged words per thread and operand
 
 __global__ __launch_bounds__(256) void k_pair_gram_mfma4(const uint64_t* __restrict__ bm, int32_t F1, int64_t Wp,
                                                          int64_t W, int nt, int ntp, int64_t kchunk,
-                                                         uint32_t* __restrict__ out) {
+                                                         uint32_t* __restrict__ out, uint32_t scale) {
   __shared__ uint64_t As[kMT4 * kMS];
   __shared__ uint64_t Bs[kMT4 * kMS];
   const uint32_t logical = xcd_remap(blockIdx.x, gridDim.x);
@@ -1184,7 +893,7 @@ __global__ __launch_bounds__(256) void k_pair_gram_mfma4(const uint64_t* __restr
         const int row = ti * kMT4 + wr + 32 * i + (g & 3) + 8 * (g >> 2) + 4 * h;
         const int col = tj * kMT4 + wc + 32 * j + r;
         const int v = acc[i][j][g];
-        if (row < col && col < F1 && v) atomicAdd(&out[(int64_t)row * F1 + col], (uint32_t)v);
+        if (row < col && col < F1 && v) atomicAdd(&out[(int64_t)row * F1 + col], (uint32_t)v * scale);
       }
 }
 
@@ -1392,7 +1101,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
     int64_t ncols, const int32_t* __restrict__ item_map, int n_used, const int32_t* __restrict__ gpre, int m,
     const int32_t* __restrict__ gext_off, const int32_t* __restrict__ gext, int G, int C,
     const int32_t* __restrict__ wword, uint32_t* __restrict__ out, const uint64_t* __restrict__ bm,
-    int64_t Wp, int dbg, const int32_t* __restrict__ gpm, const int32_t* __restrict__ bm_rows, int acc16,
+    int64_t Wp, int dbg, const int32_t* __restrict__ gpm, const int32_t* __restrict__ bm_rows,
     const int32_t* __restrict__ dfs2 = nullptr) {
   extern __shared__ uint4 lds4[];                  // 16-B aligned base
   __shared__ unsigned long long build_words[kSlabThreads / 64 * 2];   // window_starts scratch
@@ -1401,10 +1110,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
   constexpr int RPC = 32 / CPT;                     // ranks per column prefetched in registers
   uint64_t* slab = reinterpret_cast<uint64_t*>(lds4);
   uint32_t* acc = reinterpret_cast<uint32_t*>(slab + (size_t)n_used * SWP);
-  // acc16: two 16-bit counters per word (unit weights, <= 65535 columns per
-  // workgroup, guaranteed by the launcher's grid): twice the candidates per pass
-  const int n_acc = acc16 ? (C + 1) >> 1 : C;
-  for (int i = threadIdx.x; i < n_acc; i += blockDim.x) acc[i] = 0;
+  for (int i = threadIdx.x; i < C; i += blockDim.x) acc[i] = 0;
   const int64_t W = (ncols + 63) >> 6;
   const int64_t nslabs = (W + SW - 1) / SW;
 
@@ -1512,8 +1218,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
             v1[q].x = p[q].x & v.x; v1[q].y = p[q].y & v.y; v1[q].z = p[q].z & v.z; v1[q].w = p[q].w & v.w;
             s += __popc(v1[q].x) + __popc(v1[q].y) + __popc(v1[q].z) + __popc(v1[q].w);
           }
-          if (acc16) atomicAdd(&acc[nd.y >> 1], s << ((nd.y & 1) << 4));
-          else acc[nd.y] += s;
+          acc[nd.y] += s;
           if (!s) continue;                          // no column holds the node: children are 0
           for (int j = nd.z; j < nd.w; ++j) {
             const int2 c2 = n2[j];
@@ -1524,8 +1229,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
               const uint4 v = r2[q];
               s2 += __popc(v1[q].x & v.x) + __popc(v1[q].y & v.y) + __popc(v1[q].z & v.z) + __popc(v1[q].w & v.w);
             }
-            if (acc16) atomicAdd(&acc[c2.y >> 1], s2 << ((c2.y & 1) << 4));
-            else acc[c2.y] += s2;
+            acc[c2.y] += s2;
           }
         }
         continue;
@@ -1543,14 +1247,13 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
             s += __popc(p[q].x & v.x) + __popc(p[q].y & v.y) + __popc(p[q].z & v.z) + __popc(p[q].w & v.w);
           }
         }
-        if (acc16) atomicAdd(&acc[e >> 1], s << ((e & 1) << 4));
-        else acc[e] += s;
+        acc[e] += s;
       }
     }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < C; i += blockDim.x) {
-    const uint32_t v = acc16 ? (acc[i >> 1] >> ((i & 1) << 4)) & 0xFFFFu : acc[i];
+    const uint32_t v = acc[i];
     if (v) atomicAdd(&out[i], v);
   }
 }
@@ -1587,7 +1290,7 @@ __device__ __forceinline__ int u16_at(const int4& v, int k) {
   return (k & 1) ? (int)((uint32_t)w >> 16) : (w & 0xFFFF);
 }
 
-template <int SW, bool kWeighted, int kBuild, bool kAcc16>
+template <int SW, bool kWeighted, int kBuild>
 __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
     const int64_t* __restrict__ roff, const int32_t* __restrict__ ranks, const int32_t* __restrict__ src,
     int64_t ncols, const int32_t* __restrict__ item_map, int F1, int n_used, const int32_t* __restrict__ gpre,
@@ -1602,10 +1305,9 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
   constexpr int RS = SWP / 2;
   uint64_t* slab = reinterpret_cast<uint64_t*>(lds4);
   uint32_t* acc = reinterpret_cast<uint32_t*>(slab + (size_t)n_used * SWP);
-  const int n_acc = kAcc16 ? (C + 1) >> 1 : C;
-  uint16_t* smap = reinterpret_cast<uint16_t*>(acc + ((n_acc + 3) & ~3));
+  uint16_t* smap = reinterpret_cast<uint16_t*>(acc + ((C + 3) & ~3));
   const bool map_lds = kBuild == kBuildContig && F1 <= kMapLdsMax;
-  for (int i = threadIdx.x; i < n_acc; i += blockDim.x) acc[i] = 0;
+  for (int i = threadIdx.x; i < C; i += blockDim.x) acc[i] = 0;
   if (map_lds) {
     for (int i = threadIdx.x; i < F1; i += blockDim.x) {
       const int v = item_map[i];
@@ -1627,10 +1329,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
       p[q].x &= v.x; p[q].y &= v.y; p[q].z &= v.z; p[q].w &= v.w;
     }
   };
-  auto acc_add = [&](int e, uint32_t v) {
-    if constexpr (kAcc16) atomicAdd(&acc[e >> 1], v << ((e & 1) << 4));
-    else atomicAdd(&acc[e], v);
-  };
+  auto acc_add = [&](int e, uint32_t v) { atomicAdd(&acc[e], v); };
 
   for (int64_t sb = blockIdx.x; sb < nslabs; sb += gridDim.x) {
     const int64_t w0 = sb * SW;
@@ -1743,7 +1442,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
   }
   __syncthreads();
   for (int i = threadIdx.x; i < C; i += blockDim.x) {
-    const uint32_t v = kAcc16 ? (acc[i >> 1] >> ((i & 1) << 4)) & 0xFFFFu : acc[i];
+    const uint32_t v = acc[i];
     if (v) atomicAdd(&out[i], v);
   }
 }
@@ -1776,13 +1475,13 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
 // the first four extension ids and the prefix ids past D1, all inline), and the
 // next piece's record is loaded while the current one is counted.
 // ---------------------------------------------------------------------------
-template <int SW, bool kWeighted, int kBuild, bool kAcc16 = false>
+template <int SW, bool kWeighted, int kBuild>
 __global__ __launch_bounds__(kSlabThreads) void k_count_trie(
     const int64_t* __restrict__ roff, const int32_t* __restrict__ ranks, const int32_t* __restrict__ src,
     int64_t ncols, const int32_t* __restrict__ item_map, int n_used, const int32_t* __restrict__ gpre, int m,
     int D1, int D2, const int4* __restrict__ rec, const int2* __restrict__ witems, int NW,
     const int32_t* __restrict__ gext, int C, const int32_t* __restrict__ wword, uint32_t* __restrict__ out,
-    const uint64_t* __restrict__ bm, int64_t Wp, const int32_t* __restrict__ bm_rows, int acc16) {
+    const uint64_t* __restrict__ bm, int64_t Wp, const int32_t* __restrict__ bm_rows) {
   constexpr int NQ = (SW / 2) / 2 < FA_TRIE_NQ ? (SW / 2) / 2 : FA_TRIE_NQ;   // uint4 per lane (NQ = 2: ~90 VGPRs)
   constexpr int RS = SW / 2;                   // uint4 slots per slab row
   constexpr int LPP = RS / NQ;                 // lanes per work item: 2 / 4 / 8 for SW = 8 / 16 / 32
@@ -1796,13 +1495,8 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_trie(
   __shared__ unsigned long long build_words[kSlabThreads / 64 * 2];
   uint64_t* slab = reinterpret_cast<uint64_t*>(lds4);
   uint32_t* acc = reinterpret_cast<uint32_t*>(slab + (size_t)n_used * SW);
-  (void)acc16;                                  // kAcc16: the launcher's choice as a template flag
-  const int n_acc = kAcc16 ? (C + 1) >> 1 : C;  // packed 16-bit counters (see k_count_slab)
-  for (int i = threadIdx.x; i < n_acc; i += blockDim.x) acc[i] = 0;
-  auto acc_add = [&](int e, uint32_t v) {
-    if constexpr (kAcc16) atomicAdd(&acc[e >> 1], v << ((e & 1) << 4));
-    else atomicAdd(&acc[e], v);
-  };
+  for (int i = threadIdx.x; i < C; i += blockDim.x) acc[i] = 0;
+  auto acc_add = [&](int e, uint32_t v) { atomicAdd(&acc[e], v); };
   const int64_t W = (ncols + 63) >> 6;
   const int64_t nslabs = (W + SW - 1) / SW;
 
@@ -2037,7 +1731,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_trie(
   }
   __syncthreads();
   for (int i = threadIdx.x; i < C; i += blockDim.x) {
-    const uint32_t v = kAcc16 ? (acc[i >> 1] >> ((i & 1) << 4)) & 0xFFFFu : acc[i];
+    const uint32_t v = acc[i];
     if (v) atomicAdd(&out[i], v);
   }
 }
@@ -2046,71 +1740,26 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_trie(
 
 using namespace fa;
 
-// bt: per-row block table built by fa_hip_block_table (u8 when every row has
-// <= 255 frequent items, else u16 — bt_bytes says which).
-FA_API int fa_hip_block_table(const int64_t* roff, const int32_t* ranks, int64_t T, int32_t F1, void* bt,
-                              int bt_bytes, hipStream_t st) {
-  if (T <= 0) return 0;
-  const int nb = (F1 + kPB - 1) / kPB;
-  dim3 g((unsigned)((T + 255) / 256));
-  if (bt_bytes == 1) hipLaunchKernelGGL(k_block_table<uint8_t>, g, dim3(256), 0, st, roff, ranks, T, nb, (uint8_t*)bt);
-  else hipLaunchKernelGGL(k_block_table<uint16_t>, g, dim3(256), 0, st, roff, ranks, T, nb, (uint16_t*)bt);
-  FA_LAUNCH_RET();
-}
-
-FA_API int fa_hip_pair_horizontal(const int64_t* roff, const int32_t* ranks, int64_t T,
-                                  const int32_t* wrow, const void* bt, int bt_bytes, int32_t F1, uint32_t* out,
-                                  int target_wgs, hipStream_t st) {
-  if (T <= 0 || F1 < 2) return 0;
-  if (F1 > 65535) return 4;   // u16 staging
-  const int nb = (F1 + kPB - 1) / kPB;
-  const int nbp = nb * (nb + 1) / 2;
-  // target_wgs <= 0: |target_wgs| rows per chunk (locality mode: the nbp tiles of a
-  // chunk run together and share it through L2 / Infinity Cache)
-  int64_t nch;
-  if (target_wgs > 0) {
-    nch = std::max<int64_t>(1, (target_wgs + nbp - 1) / nbp);
-    nch = std::min<int64_t>(nch, std::max<int64_t>(1, T / 512));
-  } else {
-    nch = std::max<int64_t>(1, (T + (-target_wgs) - 1) / (-target_wgs));
-  }
-  const int64_t chunk = (T + nch - 1) / nch;
-  nch = (T + chunk - 1) / chunk;
-  dim3 g((unsigned)(nch * nbp)), b(64 * kPW);
-  if (bt_bytes == 1)
-    hipLaunchKernelGGL(k_pair_horizontal<uint8_t>, g, b, 0, st, roff, ranks, T, wrow, (const uint8_t*)bt, F1, nb,
-                       nbp, chunk, out);
-  else
-    hipLaunchKernelGGL(k_pair_horizontal<uint16_t>, g, b, 0, st, roff, ranks, T, wrow, (const uint16_t*)bt, F1, nb,
-                       nbp, chunk, out);
-  FA_LAUNCH_RET();
-}
-
-// Unit-weight Gram on the matrix cores (k_pair_gram_mfma); out: u32 [F1][F1] (upper triangle).
 // FA_PAIR_FLAT: 2 (default) flattened pairs in the off-diagonal tiles only, 1 in every
 // tile, 0 none, 3 diagonal tiles only -> k_pair_queue16 dbg bits 16 / 32 / 64.
 // Measured (T10I4D100M pair call): 2 13.7, 1 13.9, 0 14.5, 3 14.8 ms -- in diagonal
 // tiles the per-position loops (trip counts L-1-i) beat the square-root decode.
 static int pair_flat_bits(int v) { return v == 0 ? 16 : v == 2 ? 32 : v == 3 ? 64 : 0; }
 
+// Gram of words [0, W) of bm's rows on the matrix cores, every count multiplied by
+// scale before it is added to out (a weight class of a deduplicated layout: its
+// columns all carry the same weight, FastApriori.scala:233-235).
 FA_API int fa_hip_pair_gram_mfma(const uint64_t* bm, int32_t F1, int64_t Wp, int64_t W, uint32_t* out,
-                                 int target_wgs, hipStream_t st) {
+                                 int target_wgs, uint32_t scale, hipStream_t st) {
   if (W <= 0 || F1 < 2) return 0;
-  // 256 x 256 workgroup tiles (k_pair_gram_mfma4) unless FA_GRAM_TILE=128
-  static const bool t128 = [] { const char* e = getenv("FA_GRAM_TILE"); return e && atoi(e) == 128; }();
-  const int tile = t128 ? kMT : kMT4;
-  const int nt = (F1 + tile - 1) / tile;
+  const int nt = (F1 + kMT4 - 1) / kMT4;
   const int ntp = nt * (nt + 1) / 2;
   int64_t nk = std::max<int64_t>(1, (target_wgs + ntp - 1) / ntp);
   int64_t kchunk = (W + nk - 1) / nk;
   kchunk = std::max<int64_t>(kMW, (kchunk + kMW - 1) / kMW * kMW);
   nk = (W + kchunk - 1) / kchunk;
-  if (t128)
-    hipLaunchKernelGGL(k_pair_gram_mfma, dim3((unsigned)(nk * ntp)), dim3(256), 0, st, bm, F1, Wp, W, nt, ntp, kchunk,
-                       out);
-  else
-    hipLaunchKernelGGL(k_pair_gram_mfma4, dim3((unsigned)(nk * ntp)), dim3(256), 0, st, bm, F1, Wp, W, nt, ntp,
-                       kchunk, out);
+  hipLaunchKernelGGL(k_pair_gram_mfma4, dim3((unsigned)(nk * ntp)), dim3(256), 0, st, bm, F1, Wp, W, nt, ntp,
+                     kchunk, out, scale);
   FA_LAUNCH_RET();
 }
 
@@ -2146,44 +1795,6 @@ FA_API int fa_hip_count_candidates(const uint64_t* bm, int64_t Wp, int64_t W, co
   FA_LAUNCH_RET();
 }
 
-// Slab-stationary level counting.  gpre/gext hold slab-row ids (item_map
-// applied); C <= cap of the LDS accumulator.  Returns 3 when the LDS budget
-// cannot hold the slab + accumulator (the caller splits the candidates).
-FA_API int fa_hip_count_slab(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
-                             const int32_t* item_map, int n_used, const int32_t* gpre, int m,
-                             const int32_t* gext_off, const int32_t* gext, int G, int C, const int32_t* wword,
-                             uint32_t* out, int sw, int n_wg, const uint64_t* bm, int64_t Wp, hipStream_t st,
-                             const int32_t* gpm, const int32_t* bm_rows, int acc16) {
-  if (G <= 0 || C <= 0 || ncols <= 0) return 0;
-  const size_t lds = (size_t)n_used * (sw + 2) * 8 + (acc16 ? (size_t)((C + 1) / 2) * 4 : (size_t)C * 4);
-  if (lds > 160 * 1024 - 512) return 3;   // static build_words scratch
-  dim3 g((unsigned)n_wg), b(kSlabThreads);
-  using KernT = void (*)(const int64_t*, const int32_t*, const int32_t*, int64_t, const int32_t*, int,
-                         const int32_t*, int, const int32_t*, const int32_t*, int, int, const int32_t*,
-                         uint32_t*, const uint64_t*, int64_t, int, const int32_t*, const int32_t*, int,
-                         const int32_t*);
-  KernT kern = nullptr;
-#define FA_SLAB_MODE(S, B) kern = wword ? (KernT)k_count_slab<S, true, B> : (KernT)k_count_slab<S, false, B>;
-#define FA_SLAB_CASE(S)                                   \
-  if (sw == S) {                                          \
-    if (bm) { FA_SLAB_MODE(S, kBuildBM) }                 \
-    else if (src) { FA_SLAB_MODE(S, kBuildCols) }         \
-    else { FA_SLAB_MODE(S, kBuildContig) }                \
-  }
-  FA_SLAB_CASE(4)
-  FA_SLAB_CASE(8)
-  FA_SLAB_CASE(16)
-  FA_SLAB_CASE(32)
-#undef FA_SLAB_CASE
-#undef FA_SLAB_MODE
-  if (!kern) return 1;
-  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  const int dbg = getenv("FA_SLAB_DEBUG") ? atoi(getenv("FA_SLAB_DEBUG")) : 0;
-  hipLaunchKernelGGL(kern, g, b, lds, st, roff, ranks, src, ncols, item_map, n_used, gpre, m, gext_off, gext, G, C,
-                     wword, out, bm, Wp, dbg, gpm, bm_rows, acc16, (const int32_t*)nullptr);
-  FA_LAUNCH_RET();
-}
-
 // Slab counting from piece records (k_count_slab_rec; records: plan.cpp, 3 x int4
 // per piece).  LDS: slab + accumulator (16-B aligned) + u16 map when F1 <= 8192
 // and the slab is built from contiguous rows.  Returns 3 when that exceeds the LDS.
@@ -2192,10 +1803,10 @@ FA_API int fa_hip_count_slab(const int64_t* roff, const int32_t* ranks, const in
 FA_API int fa_hip_count_slab_rec(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
                                  const int32_t* item_map, int F1, int n_used, const int32_t* gpre, const void* rec,
                                  int G, int C, const int32_t* wword, uint32_t* out, int sw, int n_wg,
-                                 const uint64_t* bm, int64_t Wp, hipStream_t st, const int32_t* bm_rows, int acc16,
+                                 const uint64_t* bm, int64_t Wp, hipStream_t st, const int32_t* bm_rows,
                                  const int32_t* g_dev) {
   if ((G <= 0 && !g_dev) || C <= 0 || ncols <= 0) return 0;
-  const int64_t n_acc = acc16 ? (C + 1) / 2 : C;
+  const int64_t n_acc = C;
   const bool contig = !bm && !src;
   const size_t map_b = (contig && F1 <= kMapLdsMax) ? (size_t)(((int64_t)F1 * 2 + 15) & ~(int64_t)15) : 0;
   const size_t lds = (size_t)n_used * (sw + 2) * 8 + (size_t)((n_acc + 3) & ~(int64_t)3) * 4 + map_b;
@@ -2204,9 +1815,7 @@ FA_API int fa_hip_count_slab_rec(const int64_t* roff, const int32_t* ranks, cons
                          const int32_t*, const int4*, int, int, const int32_t*, uint32_t*, const uint64_t*, int64_t,
                          const int32_t*, int, const int32_t*);
   KernT kern = nullptr;
-#define FA_REC_MODE(S, B)                                                                       \
-  kern = wword ? (KernT)k_count_slab_rec<S, true, B, false>                                     \
-               : (acc16 ? (KernT)k_count_slab_rec<S, false, B, true> : (KernT)k_count_slab_rec<S, false, B, false>);
+#define FA_REC_MODE(S, B) kern = wword ? (KernT)k_count_slab_rec<S, true, B> : (KernT)k_count_slab_rec<S, false, B>;
 #define FA_REC_CASE(S)                                    \
   if (sw == S) {                                          \
     if (bm) { FA_REC_MODE(S, kBuildBM) }                  \
@@ -2240,7 +1849,7 @@ FA_API int fa_hip_count_dfs(const int64_t* roff, const int32_t* ranks, const int
   if (lds > 160 * 1024 - 512) return 3;
   using KernT = void (*)(const int64_t*, const int32_t*, const int32_t*, int64_t, const int32_t*, int,
                          const int32_t*, int, const int32_t*, const int32_t*, int, int, const int32_t*,
-                         uint32_t*, const uint64_t*, int64_t, int, const int32_t*, const int32_t*, int,
+                         uint32_t*, const uint64_t*, int64_t, int, const int32_t*, const int32_t*,
                          const int32_t*);
   KernT kern = nullptr;
 #define FA_DFS_CASE(S)                                                              \
@@ -2256,7 +1865,7 @@ FA_API int fa_hip_count_dfs(const int64_t* roff, const int32_t* ranks, const int
   const int dbg = getenv("FA_SLAB_DEBUG") ? atoi(getenv("FA_SLAB_DEBUG")) : 0;
   hipLaunchKernelGGL(kern, dim3((unsigned)n_wg), dim3(kSlabThreads), lds, st, roff, ranks, src, ncols, item_map,
                      n_used, gpre, 0, prng, node1, NP, C, (const int32_t*)nullptr, out, (const uint64_t*)nullptr,
-                     (int64_t)0, dbg, gpm, (const int32_t*)nullptr, 0, node2);
+                     (int64_t)0, dbg, gpm, (const int32_t*)nullptr, node2);
   FA_LAUNCH_RET();
 }
 
@@ -2267,18 +1876,16 @@ FA_API int fa_hip_count_trie(const int64_t* roff, const int32_t* ranks, const in
                              const int32_t* item_map, int n_used, const int32_t* gpre, int m, int D1, int D2,
                              const void* pieces, const void* witems, int NW, const int32_t* gext, int C,
                              const int32_t* wword, uint32_t* out, int sw, int n_wg, const uint64_t* bm, int64_t Wp,
-                             hipStream_t st, const int32_t* bm_rows, int acc16) {
+                             hipStream_t st, const int32_t* bm_rows) {
   if (NW <= 0 || C <= 0 || ncols <= 0) return 0;
   if (!(0 <= D1 && D1 <= D2 && D2 <= m)) return 2;
-  const size_t lds = (size_t)n_used * sw * 8 + (acc16 ? (size_t)((C + 1) / 2) * 4 : (size_t)C * 4);
+  const size_t lds = (size_t)n_used * sw * 8 + (size_t)C * 4;
   if (lds > 160 * 1024 - 512) return 3;
   using KernT = void (*)(const int64_t*, const int32_t*, const int32_t*, int64_t, const int32_t*, int,
                          const int32_t*, int, int, int, const int4*, const int2*, int, const int32_t*, int,
-                         const int32_t*, uint32_t*, const uint64_t*, int64_t, const int32_t*, int);
+                         const int32_t*, uint32_t*, const uint64_t*, int64_t, const int32_t*);
   KernT kern = nullptr;
-#define FA_TRIE_MODE(S, B)                                                                        \
-  kern = wword ? (KernT)k_count_trie<S, true, B>                                                  \
-               : (acc16 ? (KernT)k_count_trie<S, false, B, true> : (KernT)k_count_trie<S, false, B>);
+#define FA_TRIE_MODE(S, B) kern = wword ? (KernT)k_count_trie<S, true, B> : (KernT)k_count_trie<S, false, B>;
 #define FA_TRIE_CASE(S)                                   \
   if (sw == S) {                                          \
     if (bm) { FA_TRIE_MODE(S, kBuildBM) }                 \
@@ -2294,7 +1901,7 @@ FA_API int fa_hip_count_trie(const int64_t* roff, const int32_t* ranks, const in
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, dim3((unsigned)n_wg), dim3(kSlabThreads), lds, st, roff, ranks, src, ncols, item_map,
                      n_used, gpre, m, D1, D2, (const int4*)pieces, (const int2*)witems, NW, gext, C, wword, out, bm,
-                     Wp, bm_rows, acc16);
+                     Wp, bm_rows);
   FA_LAUNCH_RET();
 }
 
@@ -2341,20 +1948,6 @@ FA_API int fa_hip_pair_blocked(const uint8_t* cnt, const int64_t* base, const ui
   FA_LAUNCH_RET();
 }
 
-// unit-weight rows only (chunks of <= 65535 rows keep the 16-bit counters exact)
-FA_API int fa_hip_pair_blocked16(const uint8_t* cnt, const int64_t* base, const uint8_t* lr, int64_t T, int32_t F1,
-                                 uint32_t* out, hipStream_t st) {
-  if (T <= 0 || F1 < 2) return 0;
-  const int nb = (F1 + kPB16 - 1) / kPB16;
-  const int nbp = nb * (nb + 1) / 2;
-  const int64_t nbatch = (T + 63) / 64;
-  const int64_t chunk_b = 65535 / 64;   // 1023 batches = 65472 rows
-  const int64_t nch = (nbatch + chunk_b - 1) / chunk_b;
-  hipLaunchKernelGGL(k_pair_blocked16, dim3((unsigned)(nch * nbp)), dim3(64 * kPW), 0, st, cnt, base, lr, T, nbatch,
-                     F1, nb, nbp, chunk_b, out);
-  FA_LAUNCH_RET();
-}
-
 // Work-queue schedule (k_pair_queue16): qctr = nbp zeroed ints, out has row stride ld.
 FA_API int fa_hip_pair_queue16(const uint8_t* cnt, const int64_t* base, const uint8_t* lr, int64_t T, int32_t F1,
                                int64_t ld, int* qctr, uint32_t* out, int n_wg, hipStream_t st) {
@@ -2373,18 +1966,5 @@ FA_API int fa_hip_pair_queue16(const uint8_t* cnt, const int64_t* base, const ui
                      nb, nbp, qctr, nsub, out,
                      (getenv("FA_PAIR_DEBUG") ? atoi(getenv("FA_PAIR_DEBUG")) : 0) |
                          pair_flat_bits(getenv("FA_PAIR_FLAT") ? atoi(getenv("FA_PAIR_FLAT")) : 2));
-  FA_LAUNCH_RET();
-}
-
-FA_API int fa_hip_pair_rows16(const uint8_t* cnt, const int64_t* base, const uint8_t* lr, int64_t T, int32_t F1,
-                              uint32_t* out, hipStream_t st) {
-  if (T <= 0 || F1 < 2) return 0;
-  const int nb = (F1 + kPB16 - 1) / kPB16;
-  const int nbp = nb * (nb + 1) / 2;
-  const int64_t nbatch = (T + 63) / 64;
-  const int64_t chunk_b = 65535 / 64;   // 1023 batches = 65472 rows: 16-bit counters stay exact
-  const int64_t nch = (nbatch + chunk_b - 1) / chunk_b;
-  hipLaunchKernelGGL(k_pair_rows16, dim3((unsigned)(nch * nbp)), dim3(64 * kPW), 0, st, cnt, base, lr, T, nbatch,
-                     F1, nb, nbp, chunk_b, out, getenv("FA_PAIR_DEBUG") ? atoi(getenv("FA_PAIR_DEBUG")) : 0);
   FA_LAUNCH_RET();
 }

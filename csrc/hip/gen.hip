@@ -10,7 +10,6 @@
 // One wave per row, lane w owning bitset word w (ranks < 64 * 64 = 4096), so a
 // row's m-1 subset lookups are wave-uniform hash probes and its extensions come
 // out ascending from a popcount + DPP prefix scan over the lanes.
-#include <hip/hip_cooperative_groups.h>
 #include <hipcub/hipcub.hpp>
 
 #include "fa_hip.h"
@@ -367,33 +366,12 @@ FA_API int fa_hip_ag_chain(const int32_t* P0, int64_t n0, int m0, int F1, void* 
 }
 
 // ---------------------------------------------------------------------------
-// The speculative level chain as ONE cooperative kernel (no host round trip per
-// level).  Same levels, same acceptance rule and the same host layout as
-// fa_hip_ag_chain; every step of a level is a grid-stride phase separated by grid
-// barriers (cooperative_groups::this_grid().sync(); the launch guarantees that
-// all workgroups are resident), and the acceptance decision is taken on the
-// device by one thread between two barriers, so every thread sees the same
-// control word and takes the same number of barriers.
-//   out (device int32): [128 mark words if first_free] then per accepted level
-//       cnt [n_l] | ext [C_l] | rows [C_l][m_l + 1]   (the host layout)
-//   work (device): hash table | Ext bitsets | exclusive offsets | chunk sums
-//   dctl (device, int64 [72]): [0] L  [1] rc (0 ok, 5 work area, 6 out area)
-//       [2] int32 words of out used  [3] stop  [4 + l] C_l  [64..] running totals
+// Device helpers of the speculative chains below: the slab accumulator limit
+// (ops.primitives.slab_capacity) and one row's pruned extension bits.
+// (A single cooperative kernel for the whole chain, every level's phases split by
+// grid barriers, measured slower than the kernel boundaries: removed.)
 // ---------------------------------------------------------------------------
 namespace fa {
-
-struct ChainArgs {
-  const int32_t* P0;
-  int64_t n0;
-  int m0, nw, max_levels, first_free;
-  double growth, lds;
-  int64_t total0, tmax;
-  int32_t* out;
-  int64_t out_cap;           // int32 words
-  char* work;
-  int64_t work_cap;          // bytes
-  long long* dctl;           // control words (device)
-};
 
 __device__ int64_t d_slab_cap(int64_t n_used, int64_t C, double lds) {
   const int sws[4] = {16, 32, 8, 4};   // plan.cpp slab_width order
@@ -413,8 +391,6 @@ __device__ int64_t d_total_limit(int64_t n_used, double lds) {
   }
   return lo;
 }
-
-__device__ __forceinline__ int64_t al256(int64_t b) { return (b + 255) & ~(int64_t)255; }
 
 // Ext bits of row x (own class restricted to y > last, pruned by every (m-1)-subset)
 __device__ __forceinline__ unsigned long long chain_row_bits(const int32_t* __restrict__ P, int64_t i, int m,
@@ -439,187 +415,7 @@ __device__ __forceinline__ unsigned long long chain_row_bits(const int32_t* __re
   return a;
 }
 
-constexpr int kChainThreads = 256;
-
-__global__ __launch_bounds__(kChainThreads) void k_ag_chain_coop(ChainArgs A) {
-  namespace cg = cooperative_groups;
-  cg::grid_group grid = cg::this_grid();
-  __shared__ long long sh_scan[kChainThreads / 64 + 1];
-  const int64_t tid = (int64_t)blockIdx.x * kChainThreads + threadIdx.x;
-  const int64_t nthr = (int64_t)gridDim.x * kChainThreads;
-  const int lane = threadIdx.x & 63;
-  const int64_t wid = tid >> 6, nwav = nthr >> 6;
-  const int nw = A.nw;
-  long long* ctl = A.dctl;
-  // ctl words (device): 0 L, 1 rc, 2 out words, 3 stop, 4.. C_l, 64 total, 65 last, 66 tmax,
-  // 67 next-level table cap, 68 out offset of this level
-  uint32_t* mark = reinterpret_cast<uint32_t*>(A.out);
-  if (tid == 0) {
-    ctl[0] = 0; ctl[1] = 0; ctl[2] = A.first_free ? 128 : 0; ctl[3] = 0;
-    ctl[64] = A.total0; ctl[65] = A.n0; ctl[66] = A.tmax;
-  }
-  if (A.first_free)
-    for (int64_t i = tid; i < 128; i += nthr) A.out[i] = 0;
-  grid.sync();
-  const int32_t* P = A.P0;
-  int64_t n = A.n0;
-  int m = A.m0;
-  for (int l = 0; l < A.max_levels; ++l) {
-    uint32_t cap = 16;
-    while (cap < 2 * (uint64_t)n) cap <<= 1;
-    const uint32_t mask = cap - 1;
-    // work area: table | ext bits | off (int64 [n + 1]) | chunk sums (int64 [grid + 1])
-    char* w = A.work;
-    int32_t* table = reinterpret_cast<int32_t*>(w); w += al256(4 * (int64_t)cap);
-    unsigned long long* ext = reinterpret_cast<unsigned long long*>(w); w += al256(8 * n * nw);
-    int64_t* off = reinterpret_cast<int64_t*>(w); w += al256(8 * (n + 1));
-    int64_t* sums = reinterpret_cast<int64_t*>(w); w += al256(8 * ((int64_t)gridDim.x + 1));
-    const int64_t hoff = ctl[2];
-    int32_t* cnt = A.out + hoff;
-    const bool fits = (w - A.work) <= A.work_cap && hoff + n <= A.out_cap;
-    if (!fits) {                       // uniform: every thread computes the same sizes
-      if (tid == 0) { ctl[1] = (w - A.work) > A.work_cap ? 5 : 6; ctl[3] = 1; }
-      break;
-    }
-    // phase 0: clear the table and the Ext bitsets
-    for (int64_t i = tid; i < cap; i += nthr) table[i] = -1;
-    for (int64_t i = tid; i < n * nw; i += nthr) ext[i] = 0ull;
-    grid.sync();
-    // phase 1: class starts into the table
-    for (int64_t i = tid; i < n; i += nthr) {
-      const int32_t* r = P + i * m;
-      bool start = true;
-      if (i > 0) {
-        const int32_t* pr = P + (i - 1) * m;
-        bool same = true;
-        for (int q = 0; q < m - 1; ++q) same = same && r[q] == pr[q];
-        start = !same;
-      }
-      if (start) {
-        uint32_t at = (uint32_t)ag_hash_drop(r, m, m - 1) & mask;
-        while (atomicCAS(&table[at], -1, (int32_t)i) != -1) at = (at + 1) & mask;
-      }
-    }
-    grid.sync();
-    // phase 2: Ext bitsets of the classes
-    for (int64_t i = tid; i < n; i += nthr) {
-      const int32_t* r = P + i * m;
-      const int32_t sc = ag_find(P, m, table, mask, r, m - 1);
-      const int32_t y = r[m - 1];
-      atomicOr(&ext[(int64_t)sc * nw + (y >> 6)], 1ull << (y & 63));
-    }
-    grid.sync();
-    // phase 3: extensions per row (one wave per row)
-    for (int64_t i = wid; i < n; i += nwav) {
-      const unsigned long long a = chain_row_bits(P, i, m, table, mask, nw, ext, lane);
-      const int tot = wave_last(wave_scan_incl_dpp(__popcll(a)));
-      if (lane == 0) cnt[i] = tot;
-    }
-    grid.sync();
-    // phase 4: exclusive scan of cnt, chunk per workgroup
-    {
-      const int64_t c0 = n * blockIdx.x / gridDim.x, c1 = n * (blockIdx.x + 1) / gridDim.x;
-      long long run = 0;
-      for (int64_t b = c0; b < c1; b += kChainThreads) {
-        const int64_t i = b + threadIdx.x;
-        const int v = i < c1 ? cnt[i] : 0;
-        const int incl = wave_scan_incl_dpp(v);
-        if (lane == 63) sh_scan[threadIdx.x >> 6] = incl;
-        __syncthreads();
-        long long before = run;
-        for (int q = 0; q < (int)(threadIdx.x >> 6); ++q) before += sh_scan[q];
-        if (i < c1) off[i] = before + incl - v;
-        long long blk = 0;
-        for (int q = 0; q < kChainThreads / 64; ++q) blk += sh_scan[q];
-        __syncthreads();
-        run += blk;
-      }
-      if (threadIdx.x == 0) sums[blockIdx.x] = run;
-    }
-    grid.sync();
-    // phase 5: chunk offsets and the acceptance decision (one thread)
-    if (tid == 0) {
-      long long acc = 0;
-      for (unsigned g = 0; g < gridDim.x; ++g) { const long long t = sums[g]; sums[g] = acc; acc += t; }
-      sums[gridDim.x] = acc;
-      const int64_t C = acc;
-      long long total = ctl[64], last = ctl[65], tmax = ctl[66];
-      bool stop = false;
-      if (A.first_free && l == 1) {
-        int64_t n_used = 0;
-        for (int q = 0; q < 128; ++q) n_used += __popc(mark[q]);
-        tmax = d_total_limit(n_used, A.lds);
-        ctl[66] = tmax;
-        if (total > d_slab_cap(n_used, total, A.lds)) stop = true;   // level k alone: several passes
-      }
-      if (C == 0) stop = true;
-      if (!stop && !(A.first_free && l == 0) && ((double)C > A.growth * (double)last || total + C > tmax))
-        stop = true;
-      if (!stop && hoff + n + C + C * (m + 1) > A.out_cap) { ctl[1] = 6; stop = true; }
-      if (!stop) {
-        ctl[4 + l] = C;
-        ctl[0] = l + 1;
-        ctl[64] = total + C;
-        ctl[65] = C;
-        ctl[68] = hoff;
-        ctl[2] = hoff + n + C + C * (m + 1);
-      }
-      ctl[3] = stop ? 1 : 0;
-    }
-    grid.sync();
-    if (ctl[3]) break;
-    // phase 6: emit extensions and the candidate rows (one wave per row)
-    const int64_t C = ctl[4 + l];
-    int32_t* ext_out = cnt + n;
-    int32_t* rows_out = ext_out + C;
-    for (int64_t i = wid; i < n; i += nwav) {
-      const unsigned long long a = chain_row_bits(P, i, m, table, mask, nw, ext, lane);
-      const int c = __popcll(a);
-      const int incl = wave_scan_incl_dpp(c);
-      const int64_t g = (i * (int64_t)gridDim.x) / n;          // the chunk that scanned row i
-      int64_t gg = g;
-      while (gg + 1 < (int64_t)gridDim.x && n * (gg + 1) / gridDim.x <= i) ++gg;
-      while (gg > 0 && n * gg / gridDim.x > i) --gg;
-      int64_t o = sums[gg] + off[i] + (incl - c);
-      const int32_t* x = P + i * m;
-      for (unsigned long long v = a; v; v &= v - 1) {
-        const int32_t y = lane * 64 + __builtin_ctzll(v);
-        ext_out[o] = y;
-        int32_t* r = rows_out + o * (m + 1);
-        for (int q = 0; q < m; ++q) r[q] = x[q];
-        r[m] = y;
-        if (A.first_free && l == 0) {
-          for (int q = 0; q < m; ++q) atomicOr(&mark[x[q] >> 5], 1u << (x[q] & 31));
-          atomicOr(&mark[y >> 5], 1u << (y & 31));
-        }
-        ++o;
-      }
-    }
-    grid.sync();
-    P = rows_out;
-    n = C;
-    ++m;
-  }
-}
-
 }  // namespace fa
-
-// One cooperative launch for the whole speculative chain (see k_ag_chain_coop).
-// dctl: device int64 [72].  Returns the launch error (the caller then uses
-// fa_hip_ag_chain).  Once the stream has run it: dctl[1] == 0 -> dctl[0] levels,
-// C_l = dctl[4 + l], and the first dctl[2] int32 of out hold the host layout.
-FA_API int fa_hip_ag_chain_coop(const int32_t* P0, int64_t n0, int m0, int F1, void* work, int64_t work_bytes,
-                                int32_t* out, int64_t out_cap, int max_levels, double growth, int64_t total0,
-                                int64_t tmax, long long* dctl, int first_free, double lds, int n_wg,
-                                hipStream_t st) {
-  if (n0 <= 0 || max_levels <= 0) return 0;
-  if (m0 < 2 || F1 > 4096 || max_levels > 60) return 1;
-  ChainArgs A{P0, n0, m0, (F1 + 63) / 64, max_levels, first_free, growth, lds, total0, tmax, out, out_cap,
-              static_cast<char*>(work), work_bytes, dctl};
-  void* args[] = {&A};
-  return (int)hipLaunchCooperativeKernel((const void*)k_ag_chain_coop, dim3((unsigned)n_wg), dim3(kChainThreads),
-                                         args, 0, st);
-}
 
 // ---------------------------------------------------------------------------
 // Device-sized speculative levels (first_free chains, after level 0).

@@ -25,9 +25,8 @@ namespace fa {
 
 constexpr int kDlMaxL = 32;
 constexpr int kDlCtlN = 256;   // gen.hip kDlCtl
-// ctl words used here: 128 .. 191 used-item bitset (gen.hip), 200 + b piece count of
-// bucket b (1..8), 210 + b bucket cursor, 220 pieces, 221 pieces as int32 (the count
-// kernel's G)
+// ctl words used here: 128 .. 191 used-item bitset (gen.hip), 220 pieces, 221 pieces
+// as int32 (the count kernel's G)
 
 struct DlLevels {
   const int32_t* P[kDlMaxL];      // parent rows [n_l][m_l]
@@ -64,32 +63,69 @@ __global__ __launch_bounds__(64) void k_dl_map(const long long* __restrict__ c, 
   }
 }
 
-// pieces per n_ext bucket (wave-aggregated, one global atomic per wave and bucket)
-__global__ __launch_bounds__(256) void k_dl_pieces_count(const DlLevels D, long long* __restrict__ c) {
+// Piece slots are assigned by a stable counting sort over the flattened parent rows
+// (level order, then row order = lexicographic): the same order as plan.cpp's
+// per-pass counting sort, so neighbouring threads of the count kernel take pieces
+// with shared prefix items (LDS broadcasts) and one prefix length.  Three kernels:
+// per-block bucket counts, one scan over (bucket, block), per-block emit.
+constexpr int kDlPB = 256;        // parent rows per planner block
+
+__device__ __forceinline__ int dl_bucket_count(int cc, int b) { return b == 8 ? (cc >> 3) : ((cc & 7) == b ? 1 : 0); }
+
+__device__ __forceinline__ int dl_row_count(const DlLevels& D, int64_t t, int64_t R) {
+  if (t >= R) return 0;
+  const int l = dl_level_of(D, t);
+  return D.cnt[l][t - D.rbase[l]];
+}
+
+// part[blk * 8 + (b - 1)]: pieces of bucket b in block blk
+__global__ __launch_bounds__(kDlPB) void k_dl_pieces_count(const DlLevels D, int32_t* __restrict__ part) {
+  __shared__ int sh[kDlPB / 64][8];
   const int64_t R = D.rbase[D.L];
-  const int lane = threadIdx.x & 63;
-  for (int64_t t0 = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63); t0 < R; t0 += (int64_t)gridDim.x * 256) {
-    const int64_t t = t0 + lane;
-    int cc = 0;
-    if (t < R) {
-      const int l = dl_level_of(D, t);
-      cc = D.cnt[l][t - D.rbase[l]];
-    }
+  const int64_t t = (int64_t)blockIdx.x * kDlPB + threadIdx.x;
+  const int cc = dl_row_count(D, t, R);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
-    for (int b = 1; b <= 8; ++b) {
-      const int v = b == 8 ? (cc >> 3) : ((cc & 7) == b ? 1 : 0);
-      const int tot = wave_last(wave_scan_incl_dpp(v));
-      if (lane == 0 && tot) atomicAdd(reinterpret_cast<unsigned long long*>(c + 200 + b), (unsigned long long)tot);
-    }
+  for (int b = 1; b <= 8; ++b) {
+    const int tot = wave_last(wave_scan_incl_dpp(dl_bucket_count(cc, b)));
+    if (lane == 0) sh[wv][b - 1] = tot;
+  }
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    int s = 0;
+    for (int w = 0; w < kDlPB / 64; ++w) s += sh[w][threadIdx.x];
+    part[(int64_t)blockIdx.x * 8 + threadIdx.x] = s;
   }
 }
 
-__global__ void k_dl_pieces_scan(long long* __restrict__ c) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  long long cur = 0;
-  for (int b = 8; b >= 1; --b) { c[210 + b] = cur; cur += c[200 + b]; }
-  c[220] = cur;
-  reinterpret_cast<int32_t*>(c + 221)[0] = (int32_t)cur;
+// part -> exclusive slot base per (block, bucket), buckets 8, 7, .., 1 in that order;
+// the piece count into ctl[220] (int32 copy at ctl + 221, the count kernel's G)
+__global__ __launch_bounds__(1024) void k_dl_pieces_scan(int32_t* __restrict__ part, int64_t nblk,
+                                                         long long* __restrict__ c) {
+  __shared__ int wsum[16];
+  __shared__ int64_t carry;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int b = 8; b >= 1; --b) {
+    for (int64_t b0 = 0; b0 < nblk; b0 += 1024) {
+      const int64_t k = b0 + threadIdx.x;
+      const int v = k < nblk ? part[k * 8 + (b - 1)] : 0;
+      const int incl = wave_scan_incl_dpp(v);
+      if (lane == 63) wsum[wv] = incl;
+      __syncthreads();
+      int64_t before = carry;
+      for (int q = 0; q < wv; ++q) before += wsum[q];
+      if (k < nblk) part[k * 8 + (b - 1)] = (int32_t)(before + incl - v);
+      __syncthreads();
+      if (threadIdx.x == 1023) carry = before + incl;
+      __syncthreads();
+    }
+  }
+  if (threadIdx.x == 0) {
+    c[220] = carry;
+    reinterpret_cast<int32_t*>(c + 221)[0] = (int32_t)carry;
+  }
 }
 
 __device__ __forceinline__ uint32_t dl_pk(int x, int y) { return (uint32_t)(x & 0xFFFF) | ((uint32_t)(y & 0xFFFF) << 16); }
@@ -112,47 +148,45 @@ __device__ __forceinline__ void dl_write_rec(int4* __restrict__ rec, int64_t p, 
   rec[3 * p] = a; rec[3 * p + 1] = b; rec[3 * p + 2] = cc;
 }
 
-__global__ __launch_bounds__(256) void k_dl_pieces_emit(const DlLevels D, long long* __restrict__ c,
-                                                        const int32_t* __restrict__ item_map, int4* __restrict__ rec) {
+__global__ __launch_bounds__(kDlPB) void k_dl_pieces_emit(const DlLevels D, const int32_t* __restrict__ part,
+                                                          const int32_t* __restrict__ item_map,
+                                                          int4* __restrict__ rec) {
+  __shared__ int sh[kDlPB / 64][8];
   const int64_t R = D.rbase[D.L];
-  const int lane = threadIdx.x & 63;
-  for (int64_t t0 = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63); t0 < R; t0 += (int64_t)gridDim.x * 256) {
-    const int64_t t = t0 + lane;
-    int cc = 0, l = 0;
-    int64_t i = 0;
-    if (t < R) {
-      l = dl_level_of(D, t);
-      i = t - D.rbase[l];
-      cc = D.cnt[l][i];
-    }
-    // slots: wave-aggregated cursors per bucket
-    int64_t slot[9];
+  const int64_t t = (int64_t)blockIdx.x * kDlPB + threadIdx.x;
+  const int cc = dl_row_count(D, t, R);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int excl[9];
 #pragma unroll
-    for (int b = 1; b <= 8; ++b) {
-      const int v = b == 8 ? (cc >> 3) : ((cc & 7) == b ? 1 : 0);
-      const int incl = wave_scan_incl_dpp(v);
-      const int tot = wave_last(incl);
-      unsigned long long basev = 0;
-      if (lane == 63 && tot)
-        basev = atomicAdd(reinterpret_cast<unsigned long long*>(c + 210 + b), (unsigned long long)tot);
-      const long long bw = (long long)__builtin_amdgcn_readlane((int)(basev & 0xFFFFFFFFull), 63) |
-                           ((long long)__builtin_amdgcn_readlane((int)(basev >> 32), 63) << 32);
-      slot[b] = bw + (incl - v);
-    }
-    if (cc == 0) continue;
-    const int m = D.m[l];
-    const int32_t* x = D.P[l] + i * m;
-    int ids[12];
-#pragma unroll
-    for (int q = 0; q < 12; ++q) ids[q] = q < m ? item_map[x[q]] : 0;
-    const int64_t o = D.off[l][i];
-    const int32_t* ex = D.cnt[l] + D.n[l] + o;
-    const int64_t cand = D.base[l] + o;
-    const int full = cc >> 3;
-    for (int j = 0; j < full; ++j) dl_write_rec(rec, slot[8] + j, cand + 8 * j, 8, m, ids, ex + 8 * j, item_map);
-    const int rem = cc & 7;
-    if (rem) dl_write_rec(rec, slot[rem], cand + 8 * full, rem, m, ids, ex + 8 * full, item_map);
+  for (int b = 1; b <= 8; ++b) {
+    const int v = dl_bucket_count(cc, b);
+    const int incl = wave_scan_incl_dpp(v);
+    excl[b] = incl - v;
+    if (lane == 63) sh[wv][b - 1] = incl;
   }
+  __syncthreads();
+  if (cc == 0) return;
+  int64_t slot[9];
+#pragma unroll
+  for (int b = 1; b <= 8; ++b) {
+    int before = 0;
+    for (int q = 0; q < wv; ++q) before += sh[q][b - 1];
+    slot[b] = (int64_t)part[(int64_t)blockIdx.x * 8 + (b - 1)] + before + excl[b];
+  }
+  const int l = dl_level_of(D, t);
+  const int64_t i = t - D.rbase[l];
+  const int m = D.m[l];
+  const int32_t* x = D.P[l] + i * m;
+  int ids[12];
+#pragma unroll
+  for (int q = 0; q < 12; ++q) ids[q] = q < m ? item_map[x[q]] : 0;
+  const int64_t o = D.off[l][i];
+  const int32_t* ex = D.cnt[l] + D.n[l] + o;
+  const int64_t cand = D.base[l] + o;
+  const int full = cc >> 3;
+  for (int j = 0; j < full; ++j) dl_write_rec(rec, slot[8] + j, cand + 8 * j, 8, m, ids, ex + 8 * j, item_map);
+  const int rem = cc & 7;
+  if (rem) dl_write_rec(rec, slot[rem], cand + 8 * full, rem, m, ids, ex + 8 * full, item_map);
 }
 
 // keep support >= mc (FastApriori.scala:152-154): per level, the kept candidate rows
@@ -230,10 +264,11 @@ using namespace fa;
 
 // Single-pass slab plan of a device bundle (desc: gen.hip fa_hip_dl_more's level
 // table, L levels).  item_map: int32 [F1] out (rank -> slab row, -1 unused);
-// rec: int4 [3 * max_pieces] out, max_pieces >= total candidates.  The piece count
+// rec: int4 [3 * max_pieces] out, max_pieces >= total candidates; part: int32
+// scratch of 8 per 256 parent rows (part_cap).  The piece count
 // lands in ctl[220] (int32 copy at ctl + 221, the count kernel's G).
 FA_API int fa_hip_dl_plan(const int64_t* desc, int L, long long* ctl, int F1, int32_t* item_map, void* rec,
-                          int64_t max_pieces, hipStream_t st) {
+                          int64_t max_pieces, int32_t* part, int64_t part_cap, hipStream_t st) {
   DlLevels D;
   if (dl_levels(desc, L, &D)) return 1;
   if (F1 < 1 || F1 > 4096) return 1;
@@ -241,11 +276,13 @@ FA_API int fa_hip_dl_plan(const int64_t* desc, int L, long long* ctl, int F1, in
   for (int l = 0; l < L; ++l) C += D.C[l];
   if (max_pieces < C) return 1;
   const int64_t R = D.rbase[L];
+  const int64_t nblk = std::max<int64_t>(1, (R + kDlPB - 1) / kDlPB);
+  if (part_cap < 8 * nblk) return 1;
   hipLaunchKernelGGL(k_dl_map, dim3(1), dim3(64), 0, st, ctl, F1, item_map);
-  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((R + 255) / 256, 1024));
-  hipLaunchKernelGGL(k_dl_pieces_count, dim3(g), dim3(256), 0, st, D, ctl);
-  hipLaunchKernelGGL(k_dl_pieces_scan, dim3(1), dim3(64), 0, st, ctl);
-  hipLaunchKernelGGL(k_dl_pieces_emit, dim3(g), dim3(256), 0, st, D, ctl, item_map, static_cast<int4*>(rec));
+  hipLaunchKernelGGL(k_dl_pieces_count, dim3((unsigned)nblk), dim3(kDlPB), 0, st, D, part);
+  hipLaunchKernelGGL(k_dl_pieces_scan, dim3(1), dim3(1024), 0, st, part, nblk, ctl);
+  hipLaunchKernelGGL(k_dl_pieces_emit, dim3((unsigned)nblk), dim3(kDlPB), 0, st, D, part, item_map,
+                     static_cast<int4*>(rec));
   FA_LAUNCH_RET();
 }
 

@@ -698,7 +698,8 @@ class FastApriori:
         nd = rep.numel()
         if nd == 0:
             db.update(src=torch.full((64,), -1, dtype=torch.int32, device=dev), ncols=64,
-                      wword=torch.ones(1, dtype=torch.int32, device=dev))
+                      wword=torch.ones(1, dtype=torch.int32, device=dev),
+                      wcls=(np.ones(1, np.int64), np.ones(1, np.int64)))
             return
         wo = torch.argsort(weight, stable=True)
         w_sorted, rep_sorted = weight[wo], rep[wo]
@@ -708,11 +709,14 @@ class FastApriori:
         cls_first = torch.cumsum(cls_n, 0) - cls_n
         cls_of = torch.repeat_interleave(torch.arange(cls_n.numel(), device=dev), cls_n)
         col = cls_col0[cls_of] + (torch.arange(nd, device=dev) - cls_first[cls_of])
-        ncols = int(padded.sum().item())
+        # the weight classes on the host (one readback): (weight, words) per class, the
+        # matrix-core Gram's launch list (ops.primitives.gram_segments)
+        wcls = torch.stack([cls_w.to(torch.int64), padded // 64]).cpu().numpy()
+        ncols = int(wcls[1].sum()) * 64
         src = torch.full((ncols,), -1, dtype=torch.int32, device=dev)
         src[col] = rep_sorted.to(torch.int32)
         wword = torch.repeat_interleave(cls_w.to(torch.int32), padded // 64)
-        db.update(src=src, ncols=ncols, wword=wword)
+        db.update(src=src, ncols=ncols, wword=wword, wcls=(wcls[0], wcls[1]))
 
     def _trim_worth_it(self, db, used: np.ndarray, k: int, C: int = 0) -> bool:
         """Binomial estimate of the rows that would survive trimming.
@@ -826,6 +830,17 @@ class FastApriori:
         t_g = (F1 * (F1 - 1) / 2) * W / GRAM_WORDPAIRS_PER_S
         return t_g < t_h
 
+    @staticmethod
+    def _slice_classes(wcls, w0: int, w1: int):
+        """Weight classes (weights, words) restricted to the word range [w0, w1)."""
+        if wcls is None:
+            return None
+        end = np.cumsum(wcls[1])
+        beg = end - wcls[1]
+        nw = np.clip(np.minimum(end, w1) - np.maximum(beg, w0), 0, None)
+        keep = nw > 0
+        return wcls[0][keep], nw[keep]
+
     def _pairs(self, db, F1: int, mc: int):
         strat = self._pick_pair_strategy(db, F1)
         self.stats["pair_strategy"] = strat
@@ -836,7 +851,8 @@ class FastApriori:
             W = db["W"]
             w0, w1 = (W * r // nr) // 32 * 32, (W if r == nr - 1 else (W * (r + 1) // nr) // 32 * 32)
             wword = db["wword"][w0:w1] if db["wword"] is not None else None
-            pc = ops.pair_counts_gram(db["bm"][:, w0:], max(w1 - w0, 0), wword)
+            pc = ops.pair_counts_gram(db["bm"][:, w0:], max(w1 - w0, 0), wword,
+                                      self._slice_classes(db.get("wcls"), w0, w1))
         else:
             roff, ranks, wrow = db["roff"], db["ranks"], db["wrow"]
             if nr > 1:   # candidate parallelism: each rank takes a slice of the rows

@@ -71,8 +71,6 @@ _HIP_SIGS = {
     "fa_hip_ag_gen": (C.c_int, [vp, i64, C.c_int, C.c_int, vp, i64, vp, i64, vp, vp]),
     "fa_hip_ag_chain": (C.c_int, [vp, i64, C.c_int, C.c_int, vp, i64, vp, i64, C.c_int, dbl, i64, i64, vp, vp,
                                   C.c_int, dbl]),
-    "fa_hip_ag_chain_coop": (C.c_int, [vp, i64, C.c_int, C.c_int, vp, i64, vp, i64, C.c_int, dbl, i64, i64, vp,
-                                       C.c_int, dbl, C.c_int, vp]),
     "fa_hip_ag_build": (C.c_int, [vp, i64, C.c_int, vp, C.c_uint32, C.c_int, vp, vp]),
     "fa_hip_ag_rows": (C.c_int, [vp, i64, C.c_int, vp, C.c_uint32, C.c_int, vp, vp, vp, vp, C.c_int, vp]),
     "fa_hip_cmp_agg": (C.c_int, [vp, vp, vp, i64, vp, vp, vp]),
@@ -83,17 +81,15 @@ _HIP_SIGS = {
     "fa_hip_compress_staged": (C.c_int, [vp, vp, vp, i64, vp, vp, vp, vp, vp]),
     "fa_hip_compress_staged64": (C.c_int, [vp, vp, vp, i64, vp, vp, vp, vp, vp]),
     "fa_hip_count_trie": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, vp, C.c_int, C.c_int, C.c_int, vp, vp,
-                                    C.c_int, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, i64, vp, vp, C.c_int]),
+                                    C.c_int, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, i64, vp, vp]),
     "fa_hip_count_dfs": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, vp, vp, vp, vp, vp, C.c_int, C.c_int, vp,
                                    C.c_int, C.c_int, vp]),
-    "fa_hip_count_slab": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, vp,
-                                    C.c_int, C.c_int, vp, i64, vp, vp, vp, C.c_int]),
     "fa_hip_count_slab_rec": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, C.c_int, vp, vp, C.c_int, C.c_int, vp, vp,
-                                        C.c_int, C.c_int, vp, i64, vp, vp, C.c_int, vp]),
+                                        C.c_int, C.c_int, vp, i64, vp, vp, vp]),
     # device-resident level bundles (gen.hip fa_hip_dl_*, levels.hip)
     "fa_hip_dl_level0": (C.c_int, [vp, vp, i64, i64, C.c_int, C.c_int, vp, i64, vp, vp, i64, dbl, vp, vp]),
     "fa_hip_dl_more": (C.c_int, [C.c_int, vp, i64, i64, vp, vp, dbl, C.c_int, dbl, vp, vp, vp]),
-    "fa_hip_dl_plan": (C.c_int, [vp, C.c_int, vp, C.c_int, vp, vp, i64, vp]),
+    "fa_hip_dl_plan": (C.c_int, [vp, C.c_int, vp, C.c_int, vp, vp, i64, vp, i64, vp]),
     "fa_hip_dl_threshold": (C.c_int, [vp, C.c_int, vp, i64, vp, vp, vp, vp, vp, vp]),
     "fa_hip_trim_scan_count": (C.c_int, [vp, vp, i64, vp, C.c_int, C.c_int, vp, vp, vp, vp, vp]),
     "fa_hip_trim_emit": (C.c_int, [vp, vp, vp, C.c_int, i64, vp, vp, vp, vp, vp, vp, vp, vp]),
@@ -101,15 +97,11 @@ _HIP_SIGS = {
     "fa_hip_compress_lds": (C.c_int, [vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp]),
     "fa_hip_row_hash": (C.c_int, [vp, vp, i64, vp, vp, vp]),
     "fa_hip_build_bitmaps": (C.c_int, [vp, vp, vp, i64, i32, i64, C.c_int, C.c_int, vp, vp, vp, vp]),
-    "fa_hip_block_table": (C.c_int, [vp, vp, i64, i32, vp, C.c_int, vp]),
-    "fa_hip_pair_horizontal": (C.c_int, [vp, vp, i64, vp, vp, C.c_int, i32, vp, C.c_int, vp]),
     "fa_hip_block_counts": (C.c_int, [vp, vp, i64, i32, vp, vp, C.c_int, vp]),
     "fa_hip_block_scatter": (C.c_int, [vp, vp, i64, i32, vp, vp, vp, C.c_int, vp]),
-    "fa_hip_pair_rows16": (C.c_int, [vp, vp, vp, i64, C.c_int, vp, vp]),
     "fa_hip_pair_queue16": (C.c_int, [vp, vp, vp, i64, C.c_int, i64, vp, vp, C.c_int, vp]),
-    "fa_hip_pair_blocked16": (C.c_int, [vp, vp, vp, i64, i32, vp, vp]),
     "fa_hip_pair_blocked": (C.c_int, [vp, vp, vp, i64, vp, i32, vp, i64, vp]),
-    "fa_hip_pair_gram_mfma": (C.c_int, [vp, i32, i64, i64, vp, C.c_int, vp]),
+    "fa_hip_pair_gram_mfma": (C.c_int, [vp, i32, i64, i64, vp, C.c_int, C.c_uint32, vp]),
     "fa_hip_pair_gram_popc": (C.c_int, [vp, i32, i64, i64, vp, vp, C.c_int, vp]),
     "fa_hip_count_candidates": (C.c_int, [vp, i64, i64, vp, C.c_int, vp, vp, vp, C.c_int, vp, vp, vp]),
     "fa_hip_recommend": (C.c_int, [vp, vp, vp, i64, i32, vp, vp, i64, vp, vp]),

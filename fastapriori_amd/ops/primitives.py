@@ -380,7 +380,7 @@ def pair_counts_horizontal(roff, ranks, wrow, F1: int, long_rows: bool = True, b
     """
     T = roff.numel() - 1
     dev = ranks.device
-    if ranks.is_cuda and os.environ.get("FA_PAIR_KERNEL", "blocked") == "blocked":
+    if ranks.is_cuda:
         out = torch.zeros((F1, F1), dtype=_I32, device=dev)
         if T > 0 and F1 >= 2:
             st = _stream(ranks)
@@ -407,10 +407,7 @@ def pair_counts_horizontal(roff, ranks, wrow, F1: int, long_rows: bool = True, b
             lr = torch.empty(total + 1024, dtype=torch.uint8, device=dev)   # pad: aligned dword staging reads
             _hip_call("fa_hip_block_scatter", _p(roff), _p(ranks), T, F1, _p(cnt), _p(base), _p(lr), pb, st)
             if pb == 256:
-                kern = os.environ.get("FA_PAIR_ROWS_KERNEL", "queue16")
-                if os.environ.get("FA_PAIR_DEBUG") == "4":
-                    pass        # profiling split (benchmarks/pair_probe.py): layout kernels only
-                elif kern == "queue16":
+                if os.environ.get("FA_PAIR_DEBUG") != "4":   # 4: layout kernels only (benchmarks/pair_probe.py)
                     # work-queue schedule: persistent workgroups keep their tile across
                     # sub-chunks; even row stride -> two counters per 64-bit flush atomic
                     ld = F1 + (F1 & 1)
@@ -420,24 +417,9 @@ def pair_counts_horizontal(roff, ranks, wrow, F1: int, long_rows: bool = True, b
                     _hip_call("fa_hip_pair_queue16", _p(cnt), _p(base), _p(lr), T, F1, ld, _p(qctr), _p(out),
                               int(os.environ.get("FA_PAIR_WG", "0")), st)
                     out = out[:, :F1]
-                else:
-                    k16 = "fa_hip_pair_blocked16" if kern == "blocked16" else "fa_hip_pair_rows16"
-                    _hip_call(k16, _p(cnt), _p(base), _p(lr), T, F1, _p(out), st)
             else:
                 _hip_call("fa_hip_pair_blocked", _p(cnt), _p(base), _p(lr), T, _p(wrow), F1, _p(out),
                           PAIR_CHUNK_ROWS, st)
-        return out.to(_I64)
-    if ranks.is_cuda:
-        out = torch.zeros((F1, F1), dtype=_I32, device=dev)
-        if T > 0 and F1 >= 2:
-            nb = (F1 + 127) // 128
-            maxlen = int((roff[1:] - roff[:-1]).max().item())
-            bt_bytes = 1 if maxlen <= 255 else 2
-            bt = torch.empty(T * (nb + 1) * bt_bytes, dtype=torch.uint8, device=dev)
-            st = _stream(ranks)
-            _hip_call("fa_hip_block_table", _p(roff), _p(ranks), T, F1, _p(bt), bt_bytes, st)
-            _hip_call("fa_hip_pair_horizontal", _p(roff), _p(ranks), T, _p(wrow), _p(bt), bt_bytes, F1, _p(out),
-                      -PAIR_CHUNK_ROWS, st)
         return out.to(_I64)
     out = torch.zeros((F1, F1), dtype=_I64)
     if T > 0 and F1 >= 2:
@@ -445,16 +427,56 @@ def pair_counts_horizontal(roff, ranks, wrow, F1: int, long_rows: bool = True, b
     return out
 
 
-def pair_counts_gram(bm: torch.Tensor, W: int, wword) -> torch.Tensor:
+# weight classes shorter than this many words go to the popcount Gram (a matrix-core
+# launch per short class would cost more than its work)
+GRAM_MFMA_MIN_CLASS_WORDS = int(os.environ.get("FA_GRAM_MFMA_MIN_WORDS", "512"))
+
+
+def gram_segments(W: int, weighted: bool, wcls=None, force_popc: bool = False) -> list[tuple[int, int, int]]:
+    """(word begin, word end, weight) launches of the Gram over words [0, W): one
+    matrix-core launch per weight class (weight = its scale; unit weights: one
+    class), and the runs of short classes merged into popcount launches (weight 0 =
+    per-word weights from wword).  wcls: (weights, words) per class in column order
+    (FastApriori._layout_weighted); a weighted layout without it takes the popcount
+    Gram throughout."""
+    if not weighted:
+        return [(0, W, 0 if force_popc else 1)]
+    if wcls is None:
+        return [(0, W, 0)]
+    segs, w0, run0 = [], 0, None
+    for wt, nw in zip(*wcls):
+        w1 = min(w0 + int(nw), W)
+        if w1 > w0:
+            if w1 - w0 >= GRAM_MFMA_MIN_CLASS_WORDS and not force_popc:
+                if run0 is not None:
+                    segs.append((run0, w0, 0))
+                    run0 = None
+                segs.append((w0, w1, int(wt)))
+            elif run0 is None:
+                run0 = w0
+        w0 = w1
+    if run0 is not None and run0 < W:
+        segs.append((run0, W, 0))
+    return segs
+
+
+def pair_counts_gram(bm: torch.Tensor, W: int, wword, wcls=None, force_popc: bool = False) -> torch.Tensor:
+    """Pair supports from the item-major bitmaps over words [0, W) -> int64 [F1, F1]
+    (upper triangle).  Device: the int8 matrix-core Gram (k_pair_gram_mfma4) per
+    weight class, scaled by the class weight (FastApriori.scala:233-235's weighted
+    sum), short classes by the popcount Gram with per-word weights."""
     F1, Wp = bm.shape[0], bm.stride(0)
     if bm.is_cuda:
         out = torch.zeros((F1, F1), dtype=_I32, device=bm.device)
         if W > 0 and F1 >= 2:
-            if wword is None and os.environ.get("FA_GRAM_KERNEL", "mfma") == "mfma":
-                # unit weights: int8 GEMM on the matrix cores (weights > 1 need the popcount form)
-                _hip_call("fa_hip_pair_gram_mfma", _p(bm), F1, Wp, W, _p(out), 4096, _stream(bm))
-            else:
-                _hip_call("fa_hip_pair_gram_popc", _p(bm), F1, Wp, W, _p(wword), _p(out), 4096, _stream(bm))
+            st = _stream(bm)
+            segs = gram_segments(W, wword is not None, wcls, force_popc)
+            for a, b, wt in segs:
+                if wt > 0:
+                    _hip_call("fa_hip_pair_gram_mfma", bm.data_ptr() + 8 * a, F1, Wp, b - a, _p(out), 4096, wt, st)
+                else:
+                    _hip_call("fa_hip_pair_gram_popc", bm.data_ptr() + 8 * a, F1, Wp, b - a,
+                              wword.data_ptr() + 4 * a if wword is not None else None, _p(out), 4096, st)
         return out.to(_I64)
     out = torch.zeros((F1, F1), dtype=_I64)
     if W > 0 and F1 >= 2:
@@ -588,19 +610,6 @@ def trim_rows(roff, ranks, alive: torch.Tensor, min_len: int, wrow=None):
 _LDS_BYTES = 160 * 1024 - 512   # minus the slab kernel's static scratch (build_words)
 
 
-def slab_plan(n_used: int, C: int):
-    """Pick the slab width SW (words) and the accumulator capacity for k_count_slab."""
-    force = int(os.environ.get("FA_SLAB_SW", "0"))
-    if force:
-        return force, int((_LDS_BYTES - n_used * (force + 2) * 8) // 4)
-    for sw in (16, 32, 8, 4):     # plan.cpp slab_width order
-        slab = n_used * (sw + 2) * 8
-        cap = (_LDS_BYTES - slab) // 4
-        if cap >= min(C, 8192) or (sw == 4 and cap >= 1024):
-            return sw, int(cap)
-    return 0, 0
-
-
 def slab_capacity(n_used: int, C: int) -> int:
     """Accumulator capacity (candidates per pass) of the slab kernel for n_used items
     (csrc/host/plan.cpp slab_width); 0 when no width fits."""
@@ -609,74 +618,6 @@ def slab_capacity(n_used: int, C: int) -> int:
         if cap >= min(C, 8192) or (sw == 4 and cap >= 1024):
             return cap
     return 0
-
-
-LAST_SLAB_PLAN: dict = {}   # shape of the last count_level_slab call (diagnostics)
-
-
-def count_level_slab(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_off: np.ndarray,
-                     ext: np.ndarray, wword) -> torch.Tensor | None:
-    """Slab-stationary support counting for one level (device only).
-
-    prefix: int32 [G, m] rank ids; ext_off int64 [G+1]; ext int32 [C].
-    Returns int64 counts [C], or None when the items do not fit the LDS slab
-    (the caller then uses the bitmap kernel).
-    """
-    dev = ranks.device
-    C = int(ext.size)
-    if C == 0:
-        return torch.zeros(0, dtype=_I64, device=dev)
-    used = np.unique(np.concatenate([prefix.ravel(), ext]))
-    sw, cap = slab_plan(used.size, C)
-    if sw == 0:
-        return None
-    item_map = np.full(max(F1, 1), -1, dtype=np.int32)
-    item_map[used] = np.arange(used.size, dtype=np.int32)
-    gpre = item_map[prefix]
-    gext = item_map[ext]
-    # split groups into passes of <= cap extensions (big groups into pieces)
-    # pieces of <= 8 extensions per prefix keep the lanes of a wave balanced
-    gidx8, off8, _ = _split_groups(ext_off, 8, max_block_ext=8)
-    gidx, new_off, starts = _split_groups(off8, cap, max_block_ext=cap)
-    gpre = np.ascontiguousarray(gpre[gidx8[gidx]], dtype=np.int32)
-    # within each pass, order pieces by extension count (desc): neighbouring lanes then
-    # loop equally long.  Pieces are (start, end) ranges, so reordering them is free.
-    piece_lo, piece_hi = new_off[:-1].copy(), new_off[1:].copy()
-    m = gpre.shape[1]
-    out = torch.zeros(C, dtype=_I32, device=dev)
-    imap_t = torch.from_numpy(item_map).to(dev)
-    gext_t = torch.from_numpy(np.ascontiguousarray(gext, dtype=np.int32)).to(dev)
-    W = (ncols + 63) // 64
-    nslabs = (W + sw - 1) // sw
-    st = _stream(ranks)
-    keep = []
-    bm = None
-    if starts.size - 1 > 1:
-        # several accumulator passes: build the used-item bitmap once, stream tiles from it
-        bm, _ = build_bitmaps(roff, ranks, src, ncols, int(used.size), imap_t,
-                              torch.from_numpy(used.astype(np.int32)).to(dev))
-    for pi in range(starts.size - 1):
-        g0, g1 = int(starts[pi]), int(starts[pi + 1])
-        e0, e1 = int(new_off[g0]), int(new_off[g1])
-        sz = piece_hi[g0:g1] - piece_lo[g0:g1]
-        order = np.argsort(-sz, kind="stable")
-        lo = (piece_lo[g0:g1][order] - e0).astype(np.int32)
-        hi = (piece_hi[g0:g1][order] - e0).astype(np.int32)
-        loc_off = torch.from_numpy(np.stack([lo, hi], 1).reshape(-1)).to(dev)   # (begin, end) pairs
-        pre_t = torch.from_numpy(np.ascontiguousarray(gpre[g0:g1][order])).to(dev)
-        keep += [loc_off, pre_t]
-        lds = used.size * (sw + 2) * 8 + (e1 - e0) * 4
-        per_cu = max(1, _LDS_BYTES // max(lds, 1))
-        n_wg = int(max(1, min(nslabs, 256 * min(per_cu, 2))))
-        _hip_call("fa_hip_count_slab", _p(roff), _p(ranks), _p(src), ncols, _p(imap_t), int(used.size), _p(pre_t),
-                  m, _p(loc_off), gext_t.data_ptr() + 4 * e0, g1 - g0, e1 - e0, _p(wword),
-                  out.data_ptr() + 4 * e0, sw, n_wg, _p(bm), bm.stride(0) if bm is not None else 0, st, None, None, 0)
-    res = out.to(_I64)
-    del keep
-    LAST_SLAB_PLAN.clear()
-    LAST_SLAB_PLAN.update(rows=int(roff.numel() - 1), ncols=int(ncols), used=int(used.size), sw=sw, cap=cap,
-                          passes=int(starts.size - 1), pieces=int(gpre.shape[0]), m=m, C=C)
-    return res
 
 
 # ---------------------------------------------------------------------------
@@ -688,7 +629,6 @@ _TRIE_CONFLICT = {32: 1.0, 16: 1.6, 8: 2.2}
 TRIE_EMAX = int(os.environ.get("FA_TRIE_EMAX", "24"))     # max extensions per work item
 TRIE_ROUNDS = int(os.environ.get("FA_TRIE_ROUNDS", "4"))   # work items per lane group and pass (target)
 TRIE_PASS_WEIGHT = float(os.environ.get("FA_TRIE_PASS_WEIGHT", "4"))
-ACC16 = os.environ.get("FA_ACC16", "0") == "1"   # measured: halving passes did not pay on T40I10 (more flushes, worse widths)
 # auto level kernel: trie-shared counting when its slab-row reads are below this
 # fraction of the slab kernel's (measured break-even on T10I4 / T40I10, MI355X)
 _TRIE_MIN_SAVING = float(os.environ.get("FA_TRIE_MIN_SAVING", "0.3"))
@@ -808,7 +748,7 @@ def count_level_trie(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, 
         _hip_call("fa_hip_count_trie", _p(roff), _p(ranks), _p(src), ncols, base_ptr + 4 * o_im, int(used.size),
                   base_ptr + 4 * o_gpre, m, plan.d1, plan.d2, base_ptr, base_ptr + 4 * (o_wi + 2 * w0),
                   w1 - w0, base_ptr + 4 * (o_gext + e0), Cq, _p(wword), out.data_ptr() + 4 * e0, sw, n_wg,
-                  _p(bm), bm.stride(0) if bm is not None else 0, st, None, 0)
+                  _p(bm), bm.stride(0) if bm is not None else 0, st, None)
     res = out.to(_I64)
     LAST_TRIE_PLAN.clear()
     LAST_TRIE_PLAN.update(rows=int(roff.numel() - 1), used=int(used.size), sw=sw, cap=cap,
@@ -943,8 +883,6 @@ def emulate_trie_records(bits_by_rank: np.ndarray, info, passes, buf, m: int, C:
 
 
 LAST_LEVEL_PLAN: dict = {}   # shape of the last count_level call (diagnostics)
-# slab path kernel: k_count_slab_rec (piece records, map in LDS) or the index-chain k_count_slab
-SLAB_REC = os.environ.get("FA_SLAB_REC", "1") == "1"
 
 
 def _slab_map_lds(F1: int) -> int:
@@ -987,9 +925,6 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
     ex = np.ascontiguousarray(ext, dtype=np.int32)
     W = (ncols + 63) // 64
     min_saving = {"auto": _TRIE_MIN_SAVING, "trie": 0.0, "slab": 2.0}[kernel]
-    # packed 16-bit LDS counters for unit weights: twice the candidates per pass; the
-    # grid then keeps every workgroup at <= 65535 columns (see the n_wg floor below)
-    acc16 = False
     params = np.array([_LDS_BYTES, min_saving, _TRIE_CONFLICT[16], _TRIE_CONFLICT[8], TRIE_PASS_WEIGHT,
                        TRIE_ROUNDS, TRIE_EMAX, W, 4.0], dtype=np.float64)
     bound = _level_plan_bound(F1, C, G, m)
@@ -1002,13 +937,6 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
     rc = _native.host().fa_level_plan(P.ctypes.data, po.ctypes.data, G, eo.ctypes.data, ex.ctypes.data, F1,
                                       params.ctypes.data, buf.data_ptr(), bound, passes.ctypes.data, max_pass,
                                       info.ctypes.data)
-    if rc in (0, 4) and (rc == 4 or info[6] > 1) and wword is None and ACC16:
-        # several accumulator passes (or none fits): replan with packed 16-bit counters
-        params[8] = 2.0
-        rc = _native.host().fa_level_plan(P.ctypes.data, po.ctypes.data, G, eo.ctypes.data, ex.ctypes.data, F1,
-                                          params.ctypes.data, buf.data_ptr(), bound, passes.ctypes.data, max_pass,
-                                          info.ctypes.data)
-        acc16 = rc == 0
     if rc == 4:
         return None
     if rc != 0:
@@ -1038,32 +966,23 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
     st = _stream(ranks)
     bounds = passes[:, 2].tolist() + [C]
     nslabs = (W + sw - 1) // sw
-    wg_floor = -(-nslabs // max(1, 65535 // (64 * sw))) if acc16 else 1
-    accb = 2 if acc16 else 4
     for q, (a, b, e0) in enumerate(passes.tolist()):
         Cq = bounds[q + 1] - e0
         if kern == 1:
-            lds = n_used * sw * 8 + Cq * accb
-            n_wg = int(max(wg_floor, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2))))
+            lds = n_used * sw * 8 + Cq * 4
+            n_wg = int(max(1, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2))))
             _hip_call("fa_hip_count_trie", _p(roff), _p(ranks), _p(src), ncols, base + 4 * o_im, n_used,
                       base + 4 * o_gpre, m, int(info[7]), int(info[8]), base + 4 * o_rec, base + 4 * (o_wi + 2 * a),
                       b - a, base + 4 * (o_gext + e0), Cq, _p(wword), out.data_ptr() + 4 * e0, sw, n_wg, _p(bm),
-                      bm.stride(0) if bm is not None else 0, st, bm_rows, int(acc16))
-        elif SLAB_REC:
+                      bm.stride(0) if bm is not None else 0, st, bm_rows)
+        else:
             # piece records (k_count_slab_rec): 48 B per piece, loaded one piece ahead
-            lds = n_used * (sw + 2) * 8 + Cq * accb + _slab_map_lds(F1)
-            n_wg = int(max(wg_floor, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2))))
+            lds = n_used * (sw + 2) * 8 + Cq * 4 + _slab_map_lds(F1)
+            n_wg = int(max(1, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2))))
             _hip_call("fa_hip_count_slab_rec", _p(roff), _p(ranks), _p(src), ncols, base + 4 * o_im, F1, n_used,
                       base + 4 * o_gpre, base + 4 * (o_rec + 12 * a), b - a, Cq, _p(wword),
                       out.data_ptr() + 4 * e0, sw, n_wg, _p(bm), bm.stride(0) if bm is not None else 0, st,
-                      bm_rows, int(acc16), None)
-        else:
-            lds = n_used * (sw + 2) * 8 + Cq * accb
-            n_wg = int(max(wg_floor, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2))))
-            _hip_call("fa_hip_count_slab", _p(roff), _p(ranks), _p(src), ncols, base + 4 * o_im, n_used,
-                      base + 4 * o_gpre, m, base + 4 * (o_pc + 2 * a), base + 4 * (o_gext + e0), b - a, Cq,
-                      _p(wword), out.data_ptr() + 4 * e0, sw, n_wg, _p(bm), bm.stride(0) if bm is not None else 0,
-                      st, base + 4 * (o_gpm + 2 * a), bm_rows, int(acc16))
+                      bm_rows, None)
     LAST_LEVEL_PLAN.clear()
     LAST_LEVEL_PLAN.update(kernel="trie" if kern == 1 else "slab", rows=int(roff.numel() - 1), used=n_used, sw=sw,
                            cap=cap, passes=npass, pieces=int(info[4]), witems=int(info[5]), d1=int(info[7]),
@@ -1153,12 +1072,7 @@ def apriori_gen_chain(rows: np.ndarray, F1: int, dev, max_levels: int, growth: f
     sizes = np.zeros(2 + max_levels, dtype=np.int64)
     host_stage = pinned_stage("gen_out")
     need_host = 1 << 20
-    # (a chain capped at 60 levels only ends a bundle early: the miner goes on from there)
-    got = _ag_chain_coop(P, n, m, F1, dev, min(max_levels, 60), growth, total0, tmax, first_free, sizes) \
-        if GEN_COOP else None
-    if got is not None:
-        h = got
-    for _ in range(0 if got is not None else 32):
+    for _ in range(32):
         ws = _GEN_WS.get(dev)
         if ws is None or ws.numel() < (64 << 20):
             ws = _GEN_WS[dev] = torch.empty(64 << 20, dtype=torch.uint8, device=dev)
@@ -1175,10 +1089,8 @@ def apriori_gen_chain(rows: np.ndarray, F1: int, dev, max_levels: int, growth: f
         _native.check(rc, "fa_hip_ag_chain")
         break
     else:
-        if got is None:
-            raise RuntimeError("fa_hip_ag_chain: buffer sizing did not converge")
-    if got is None:
-        h = host.numpy()
+        raise RuntimeError("fa_hip_ag_chain: buffer sizing did not converge")
+    h = host.numpy()
     out, o = [], (128 if first_free else 0)
     for lv in range(int(sizes[0])):
         C = int(sizes[2 + lv])
@@ -1192,53 +1104,6 @@ def apriori_gen_chain(rows: np.ndarray, F1: int, dev, max_levels: int, growth: f
         o += n + C + C * (m + 1)
         n, m = C, m + 1
     return out
-
-
-# Off by default: measured slower on MI355X (T10I4D100M 53.3 -> 56.8 ms, 12.5M-row shard
-# 9.9 -> 12.3 ms).  Eight grid barriers per level over 256 workgroups on 8 XCDs cost
-# more than the per-level host round trip they replace.
-GEN_COOP = os.environ.get("FA_GEN_COOP", "0") == "1"
-_COOP: dict = {}
-
-
-def _ag_chain_coop(P, n: int, m: int, F1: int, dev, max_levels: int, growth: float, total0: int, tmax: int,
-                   first_free: bool, sizes: np.ndarray):
-    """The chain as one cooperative kernel (k_ag_chain_coop): one launch, then two
-    small readbacks (control words, then the used part of the output area).  Returns
-    the host int32 array in fa_hip_ag_chain's layout and fills sizes, or None (launch
-    refused or an area too small: the caller runs the per-level chain)."""
-    st = _stream(P)
-    bufs = _COOP.get(dev)
-    if bufs is None:
-        props = torch.cuda.get_device_properties(dev)
-        bufs = _COOP[dev] = dict(work=torch.empty(64 << 20, dtype=torch.uint8, device=dev),
-                                 out=torch.empty(16 << 20, dtype=_I32, device=dev),
-                                 dctl=torch.zeros(72, dtype=_I64, device=dev),
-                                 ctl=torch.zeros(72, dtype=_I64, pin_memory=True),
-                                 n_wg=int(props.multi_processor_count))
-    rc = _native.hip().fa_hip_ag_chain_coop(_p(P), n, m, F1, _p(bufs["work"]), bufs["work"].numel(),
-                                            _p(bufs["out"]), bufs["out"].numel(), max_levels, growth, total0, tmax,
-                                            _p(bufs["dctl"]), int(first_free), float(_LDS_BYTES), bufs["n_wg"], st)
-    if rc != 0:
-        note_fallback(f"cooperative apriori-gen chain not launched (hip error {rc}): per-level chain")
-        return None
-    ctl = bufs["ctl"]
-    ctl.copy_(bufs["dctl"], non_blocking=True)
-    torch.cuda.current_stream(dev).synchronize()
-    c = ctl.numpy()
-    if os.environ.get("FA_DEBUG_COOP"):
-        import sys
-        print(f"ag_chain_coop: n={n} m={m} ctl={c[:8].tolist()} C={c[4:4 + int(c[0])].tolist()}", file=sys.stderr)
-    if int(c[1]) != 0:
-        return None
-    used = int(c[2])
-    host = pinned_stage("gen_out").get(4 * max(used, 1)).view(dtype=_I32)[:max(used, 1)]
-    if used:
-        host[:used].copy_(bufs["out"][:used], non_blocking=True)
-        torch.cuda.current_stream(dev).synchronize()
-    sizes[0] = int(c[0])
-    sizes[2:2 + int(c[0])] = c[4:4 + int(c[0])]
-    return host.numpy()
 
 
 def slab_total_limit(n_used: int) -> int:
@@ -1718,15 +1583,17 @@ def dl_count(S: DeviceLevelState, L: int, roff, ranks, src, ncols: int, F1: int,
         raise RuntimeError(f"device bundle of {C} candidates over {n_used} items does not fit one pass")
     item_map = torch.empty(max(F1, 1), dtype=_I32, device=dev)
     rec = torch.empty(12 * C + 12, dtype=_I32, device=dev)
-    _native.check(_native.hip().fa_hip_dl_plan(S.desc.ctypes.data, L, _p(S.ctl), F1, _p(item_map), _p(rec), C, st),
-                  "fa_hip_dl_plan")
+    R = int(S.desc[:L, 5].sum())                     # parent rows of the bundle
+    part = torch.empty(8 * max(1, (R + 255) // 256), dtype=_I32, device=dev)
+    _native.check(_native.hip().fa_hip_dl_plan(S.desc.ctypes.data, L, _p(S.ctl), F1, _p(item_map), _p(rec), C,
+                                               _p(part), part.numel(), st), "fa_hip_dl_plan")
     out = torch.zeros(C, dtype=_I32, device=dev)
     W = (ncols + 63) // 64
     nslabs = (W + sw - 1) // sw
     lds_k = n_used * (sw + 2) * 8 + ((C + 3) & ~3) * 4 + _slab_map_lds(F1)
     n_wg = int(max(1, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds_k), 2))))
     _hip_call("fa_hip_count_slab_rec", _p(roff), _p(ranks), _p(src), ncols, _p(item_map), F1, n_used, None, _p(rec),
-              0, C, _p(wword), _p(out), sw, n_wg, None, 0, st, None, 0, _p(S.ctl) + 8 * 221)
+              0, C, _p(wword), _p(out), sw, n_wg, None, 0, st, None, _p(S.ctl) + 8 * 221)
     LAST_LEVEL_PLAN.clear()
     LAST_LEVEL_PLAN.update(kernel="slab_dev", rows=int(roff.numel() - 1), used=n_used, sw=sw, cap=cap, passes=1,
                            pieces=-1, witems=0, d1=0, d2=0, trie_reads=0, slab_reads=0, m=-1, C=C)

@@ -146,7 +146,7 @@ def test_bitmaps_pairs_candidates(F1_frac):
     ref = ops.count_candidates(bm, W, prefix, eoff, ext_t, None)
     got = ops.count_candidates(gbm, gW, prefix.to(DEV), eoff, ext_t.to(DEV), None).cpu()
     assert torch.equal(ref, got)
-    slab = ops.count_level_slab(roff.to(DEV), ranks.to(DEV), None, T, F1, prev[pidx], eoff, ext, None)
+    slab = ops.count_level(roff.to(DEV), ranks.to(DEV), None, T, F1, prev[pidx], eoff, ext, None, kernel="slab")
     assert slab is not None and torch.equal(ref, slab.cpu())
     trie = ops.count_level_trie(roff.to(DEV), ranks.to(DEV), None, T, F1, prev[pidx], eoff, ext, None)
     assert trie is not None and torch.equal(ref, trie.cpu())
@@ -259,40 +259,6 @@ def test_gen_chain_matches_iterated_gen():
     assert len(ops.primitives.apriori_gen_chain(cand, F1, DEV, 4, (c0 - 0.5) / cand.shape[0], 0, 1 << 40)) == 0
 
 
-@pytest.mark.parametrize("first_free", [True, False])
-def test_coop_chain_matches_per_level_chain(monkeypatch, first_free):
-    # k_ag_chain_coop (one cooperative launch, decisions on the device) == fa_hip_ag_chain
-    sh = generate_shard(200000, Comm(), "cpu", 10.0, 4.0, 60, 80, seed=8)
-    res = FastApriori(0.003, config=MinerConfig(min_support=0.003)).run(sh)
-    F1 = len(res.items)
-    n_levels = 0
-    for k in (2, 3, 4):
-        prev = res.levels[k - 1]
-        if first_free:
-            args = (prev, F1, DEV, 64, 1.5, 0, 0, True)
-        else:
-            pi, eo, ex = apriori_gen(prev)
-            g = np.repeat(np.arange(pi.size), np.diff(eo))
-            cand = np.ascontiguousarray(np.concatenate([prev[pi[g]], ex[:, None]], axis=1), dtype=np.int32)
-            args = (cand, F1, DEV, 64, 1.5, 0, 1 << 40, False)
-        monkeypatch.setattr(ops.primitives, "GEN_COOP", True)      # opt-in path (FA_GEN_COOP=1)
-        calls = []
-        real = ops.primitives._ag_chain_coop
-        monkeypatch.setattr(ops.primitives, "_ag_chain_coop", lambda *a, **k: calls.append(1) or real(*a, **k))
-        a = ops.primitives.apriori_gen_chain(*args)
-        monkeypatch.setattr(ops.primitives, "_ag_chain_coop", real)
-        assert calls
-        monkeypatch.setattr(ops.primitives, "GEN_COOP", False)
-        b = ops.primitives.apriori_gen_chain(*args)
-        assert len(a) == len(b)
-        n_levels += len(a)
-        for x, y in zip(a, b):
-            for u, v in zip(x, y):
-                assert np.array_equal(u, v)
-    assert n_levels >= 2
-    assert not any("cooperative" in f for f in ops.primitives.FALLBACKS)
-
-
 def test_bundling_chain_matches_python_loop(monkeypatch):
     import fastapriori_amd.models.apriori as ap
     sh = generate_shard(200000, Comm(), "cpu", 10.0, 4.0, 60, 80, seed=8).to(DEV)
@@ -341,12 +307,10 @@ def test_slab_multipass_from_bitmap(monkeypatch):
     assert ref.as_dict() == got_w.as_dict()
 
 
-@pytest.mark.parametrize("kernel,rows16", [("blocked", "rows16"), ("blocked", "blocked16"), ("blocked", "queue16"),
-                                           ("tile", "queue16")])
 @pytest.mark.parametrize("long_rows", [False, True])
-def test_pair_kernels_agree(monkeypatch, kernel, rows16, long_rows):
-    monkeypatch.setenv("FA_PAIR_KERNEL", kernel)
-    monkeypatch.setenv("FA_PAIR_ROWS_KERNEL", rows16)
+def test_pair_kernels_agree(long_rows):
+    # unit weights: 256-rank blocks + k_pair_queue16 (long_rows: 128-rank blocks +
+    # k_pair_blocked); row weights: k_pair_blocked
     off, items, lut, F1 = _prep(n=20000, V=900, seed=21, long_rows=30, F1_frac=0.9)
     _, kept, roff = _compress_inputs(off, items, lut)
     ranks = ops.compress(off, items, lut, kept, roff)
@@ -364,7 +328,6 @@ def test_pair_queue_drain_and_stealing(monkeypatch, F1, n_wg):
     """k_pair_queue16 over many sub-chunks: pair counts far above 2^16 (the u16 LDS
     counters drain bit 15 into the global count), odd F1 (u32 flush path), and few
     workgroups for many tiles (tile switches and stealing)."""
-    monkeypatch.setenv("FA_PAIR_ROWS_KERNEL", "queue16")
     monkeypatch.setenv("FA_PAIR_WG", str(n_wg))
     rng = np.random.default_rng(F1)
     n = 150_000
@@ -538,23 +501,36 @@ def test_pair_gram_mfma_matches_popcount(monkeypatch, F1, T):
     words[:, :W] = pad.view(np.uint64)
     bm = torch.from_numpy(words.view(np.int64)).to(DEV)
     got = ops.pair_counts_gram(bm, W, None).cpu()
-    monkeypatch.setenv("FA_GRAM_KERNEL", "popc")
-    ref = ops.pair_counts_gram(bm, W, None).cpu()
+    ref = ops.pair_counts_gram(bm, W, None, force_popc=True).cpu()
     want = torch.from_numpy(bits.astype(np.int64) @ bits.astype(np.int64).T)
     iu = torch.triu_indices(F1, F1, 1)
     assert torch.equal(got[iu[0], iu[1]], want[iu[0], iu[1]])
     assert torch.equal(ref[iu[0], iu[1]], want[iu[0], iu[1]])
 
 
-@pytest.mark.parametrize("kernel", ["slab", "trie"])
-def test_acc16_multipass_matches(monkeypatch, kernel):
-    # packed 16-bit LDS counters: forced multi-pass levels (small LDS budget) replan with
-    # 2-byte accumulators and a grid floor of <= 65535 columns per workgroup
-    import fastapriori_amd.ops.primitives as prim
-    sh = generate_shard(150000, Comm(), "cpu", 12.0, 5.0, 200, 100, seed=31)
-    ref = FastApriori(0.004, config=MinerConfig(min_support=0.004, trim_min_rows=0, level_kernel="bitmap")).run(sh)
-    monkeypatch.setattr(prim, "_LDS_BYTES", 40 * 1024)
-    monkeypatch.setattr(prim, "ACC16", True)
-    got = FastApriori(0.004, config=MinerConfig(min_support=0.004, trim_min_rows=0, level_kernel=kernel)).run(
-        sh.to(DEV))
-    assert ref.as_dict() == got.as_dict()
+@pytest.mark.parametrize("F1,classes", [(300, [(1, 700), (2, 40), (3, 600), (7, 3), (9, 520)]),
+                                        (37, [(1, 9), (4, 530)])])
+def test_weighted_gram_mfma_matches_popcount(monkeypatch, F1, classes):
+    # deduplicated layouts: one scaled matrix-core launch per weight class of >= 512
+    # words, the short classes by the popcount Gram -- exact against the weighted
+    # popcount Gram and a numpy reference (FastApriori.scala:233-235)
+    rng = np.random.default_rng(F1 + len(classes))
+    W = sum(n for _, n in classes)
+    Wp = (W + 63) // 64 * 64
+    words = rng.integers(0, 1 << 63, size=(F1, Wp), dtype=np.int64) & rng.integers(0, 1 << 63, size=(F1, Wp),
+                                                                                     dtype=np.int64)
+    words[:, W:] = 0
+    wword = np.concatenate([np.full(n, wt, np.int32) for wt, n in classes])
+    wcls = (np.array([wt for wt, _ in classes], np.int64), np.array([n for _, n in classes], np.int64))
+    segs = ops.primitives.gram_segments(W, True, wcls)
+    assert any(w > 1 for _, _, w in segs) and any(w == 0 for _, _, w in segs)
+    bm = torch.from_numpy(words).to(DEV)
+    ww = torch.from_numpy(wword).to(DEV)
+    got = ops.pair_counts_gram(bm, W, ww, wcls).cpu()
+    ref = ops.pair_counts_gram(bm, W, ww, wcls, force_popc=True).cpu()
+    bits = np.unpackbits(words[:, :W].view(np.uint8), axis=1, bitorder="little").astype(np.int64)
+    wcol = np.repeat(wword.astype(np.int64), 64)
+    want = torch.from_numpy((bits * wcol) @ bits.T)
+    iu = torch.triu_indices(F1, F1, 1)
+    assert torch.equal(got[iu[0], iu[1]], want[iu[0], iu[1]])
+    assert torch.equal(ref[iu[0], iu[1]], want[iu[0], iu[1]])
