@@ -78,8 +78,69 @@ __global__ __launch_bounds__(256) void k_ag_ext(const int32_t* __restrict__ P, i
   atomicOr(&ext[(int64_t)s * nw + (y >> 6)], 1ull << (y & 63));
 }
 
+// Extension bits of row i: its own class's Ext restricted to y > last, pruned by
+// Ext of every other (m-1)-subset.  Lane `lane` owns bitset words [lane * NWL,
+// lane * NWL + NWL), so one wave covers F1 <= 4096 * NWL ranks and the extensions
+// come out ascending in lane order.  Returns the lane's extension count.
+template <int NWL>
+__device__ __forceinline__ int ag_row_bits(const int32_t* __restrict__ P, int64_t i, int m,
+                                           const int32_t* __restrict__ table, uint32_t mask, int nw,
+                                           const unsigned long long* __restrict__ ext, int lane,
+                                           unsigned long long (&a)[NWL]) {
+  const int32_t* x = P + i * m;
+  const int32_t last = x[m - 1];
+  const int32_t s0 = ag_find(P, m, table, mask, x, m - 1);
+  const int lw = last >> 6;
+  unsigned long long any = 0;
+#pragma unroll
+  for (int j = 0; j < NWL; ++j) {
+    const int w = lane * NWL + j;
+    unsigned long long v = 0;
+    if (w < nw && w >= lw) {
+      v = ext[(int64_t)s0 * nw + w];
+      if (w == lw) v &= (last & 63) == 63 ? 0ull : (~0ull << ((last & 63) + 1));
+    }
+    a[j] = v;
+    any |= v;
+  }
+  for (int p = 0; p < m - 1 && __ballot(any != 0) != 0ull; ++p) {
+    const int32_t sp = ag_find(P, m, table, mask, x, p);
+    any = 0;
+#pragma unroll
+    for (int j = 0; j < NWL; ++j) {
+      const int w = lane * NWL + j;
+      if (sp < 0) a[j] = 0;
+      else if (w < nw) a[j] &= ext[(int64_t)sp * nw + w];
+      any |= a[j];
+    }
+    if (sp < 0) break;
+  }
+  int c = 0;
+#pragma unroll
+  for (int j = 0; j < NWL; ++j) c += __popcll(a[j]);
+  return c;
+}
+
+// the extension ids of a row at out[o ..] (and, with rows, the candidate rows (x, y))
+template <int NWL>
+__device__ __forceinline__ void ag_emit(const unsigned long long (&a)[NWL], int lane, const int32_t* __restrict__ x,
+                                        int m, int64_t o, int32_t* __restrict__ out, int32_t* __restrict__ rows) {
+#pragma unroll
+  for (int j = 0; j < NWL; ++j)
+    for (unsigned long long v = a[j]; v; v &= v - 1) {
+      const int32_t y = (lane * NWL + j) * 64 + __builtin_ctzll(v);
+      out[o] = y;
+      if (rows) {   // the full candidate row (x, y): the next speculative level's input
+        int32_t* r = rows + o * (m + 1);
+        for (int q = 0; q < m; ++q) r[q] = x[q];
+        r[m] = y;
+      }
+      ++o;
+    }
+}
+
 // pass 0: cnt[i] = number of extensions of row i;  pass 1: write them at off[i].
-template <bool kEmit>
+template <bool kEmit, int NWL = 1>
 __global__ __launch_bounds__(256) void k_ag_rows(const int32_t* __restrict__ P, int64_t n, int m,
                                                  const int32_t* __restrict__ table, uint32_t mask, int nw,
                                                  const unsigned long long* __restrict__ ext,
@@ -88,42 +149,30 @@ __global__ __launch_bounds__(256) void k_ag_rows(const int32_t* __restrict__ P, 
   const int lane = threadIdx.x & 63;
   const int64_t nwave = (int64_t)gridDim.x * (blockDim.x / 64);
   for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); i < n; i += nwave) {
-    const int32_t* x = P + i * m;
-    const int32_t last = x[m - 1];
-    // own class: Ext(x[0..m-2]) restricted to y > last
-    const int32_t s0 = ag_find(P, m, table, mask, x, m - 1);
-    unsigned long long a = 0;
-    if (lane < nw) {
-      a = ext[(int64_t)s0 * nw + lane];
-      const int lw = last >> 6;
-      if (lane < lw) a = 0;
-      else if (lane == lw) a &= (last & 63) == 63 ? 0ull : (~0ull << ((last & 63) + 1));
-    }
-    for (int p = 0; p < m - 1 && __ballot(a != 0) != 0ull; ++p) {
-      const int32_t sp = ag_find(P, m, table, mask, x, p);
-      if (sp < 0) { a = 0; break; }
-      if (lane < nw) a &= ext[(int64_t)sp * nw + lane];
-    }
-    const int c = __popcll(a);
+    unsigned long long a[NWL];
+    const int c = ag_row_bits<NWL>(P, i, m, table, mask, nw, ext, lane, a);
+    const int incl = wave_scan_incl_dpp(c);
     if (!kEmit) {
-      const int tot = wave_last(wave_scan_incl_dpp(c));
-      if (lane == 0) cnt[i] = tot;
+      if (lane == 63) cnt[i] = incl;
     } else {
-      const int incl = wave_scan_incl_dpp(c);
-      int64_t o = off[i] + (incl - c);
-      for (unsigned long long v = a; v; v &= v - 1) {
-        const int32_t y = lane * 64 + __builtin_ctzll(v);
-        out[o] = y;
-        if (rows) {   // the full candidate row (x, y): the next speculative level's input
-          int32_t* r = rows + o * (m + 1);
-          for (int q = 0; q < m; ++q) r[q] = x[q];
-          r[m] = y;
-        }
-        ++o;
-      }
+      ag_emit<NWL>(a, lane, P + i * m, m, off[i] + (incl - c), out, rows);
     }
   }
 }
+
+// bitset words per lane for nw words: 1, 2, 4 or 8 (F1 <= 32768)
+static inline int ag_nwl(int nw) { return nw <= 64 ? 1 : nw <= 128 ? 2 : nw <= 256 ? 4 : 8; }
+constexpr int kAgMaxF1 = 64 * 64 * 8;
+// u32 words of a chain's used-item bitset (ops.primitives.ag_mark_words mirrors this)
+static inline int ag_mark_words(int F1) { return std::max(128, (F1 + 31) / 32); }
+// LAUNCH(N) for the lane width N of nw bitset words
+#define FA_AG_NWL_SWITCH(nw, LAUNCH) \
+  switch (ag_nwl(nw)) {              \
+    case 1: LAUNCH(1) break;         \
+    case 2: LAUNCH(2) break;         \
+    case 4: LAUNCH(4) break;         \
+    default: LAUNCH(8) break;        \
+  }
 
 }  // namespace fa
 
@@ -133,7 +182,7 @@ using namespace fa;
 FA_API int fa_hip_ag_build(const int32_t* P, int64_t n, int m, int32_t* table, uint32_t mask, int nw, void* ext,
                            hipStream_t st) {
   if (n <= 0) return 0;
-  if (m < 2 || nw > 64) return 1;
+  if (m < 2 || nw > kAgMaxF1 / 64) return 1;
   dim3 g((unsigned)((n + 255) / 256));
   hipLaunchKernelGGL(k_ag_insert, g, dim3(256), 0, st, P, n, m, table, mask);
   hipLaunchKernelGGL(k_ag_ext, g, dim3(256), 0, st, P, n, m, table, mask, nw, (unsigned long long*)ext);
@@ -144,14 +193,17 @@ FA_API int fa_hip_ag_build(const int32_t* P, int64_t n, int m, int32_t* table, u
 FA_API int fa_hip_ag_rows(const int32_t* P, int64_t n, int m, const int32_t* table, uint32_t mask, int nw,
                           const void* ext, int32_t* cnt, const int64_t* off, int32_t* out, int emit, hipStream_t st) {
   if (n <= 0) return 0;
-  if (m < 2 || nw > 64) return 1;
+  if (m < 2 || nw > kAgMaxF1 / 64) return 1;
   const unsigned nwg = (unsigned)std::min<int64_t>((n + 3) / 4, 65536);
-  if (emit)
-    hipLaunchKernelGGL(k_ag_rows<true>, dim3(nwg), dim3(256), 0, st, P, n, m, table, mask, nw,
-                       (const unsigned long long*)ext, cnt, off, out);
-  else
-    hipLaunchKernelGGL(k_ag_rows<false>, dim3(nwg), dim3(256), 0, st, P, n, m, table, mask, nw,
-                       (const unsigned long long*)ext, cnt, off, out);
+#define FA_AG_ROWS(N)                                                                                      \
+  if (emit)                                                                                                \
+    hipLaunchKernelGGL((k_ag_rows<true, N>), dim3(nwg), dim3(256), 0, st, P, n, m, table, mask, nw,       \
+                       (const unsigned long long*)ext, cnt, off, out, nullptr);                            \
+  else                                                                                                     \
+    hipLaunchKernelGGL((k_ag_rows<false, N>), dim3(nwg), dim3(256), 0, st, P, n, m, table, mask, nw,      \
+                       (const unsigned long long*)ext, cnt, off, out, nullptr);
+  FA_AG_NWL_SWITCH(nw, FA_AG_ROWS)
+#undef FA_AG_ROWS
   FA_LAUNCH_RET();
 }
 
@@ -164,7 +216,7 @@ FA_API int fa_hip_ag_gen(const int32_t* P, int64_t n, int m, int F1, void* ws, i
                          int64_t host_cap, int64_t* sizes, hipStream_t st) {
   sizes[0] = 0;
   if (n <= 0) return 0;
-  if (m < 2 || F1 > 4096) return 1;
+  if (m < 2 || F1 > kAgMaxF1) return 1;
   const int nw = (F1 + 63) / 64;
   uint32_t cap = 16;
   while (cap < 2 * (uint64_t)n) cap <<= 1;
@@ -186,8 +238,10 @@ FA_API int fa_hip_ag_gen(const int32_t* P, int64_t n, int m, int F1, void* ws, i
   hipLaunchKernelGGL(k_ag_insert, g, dim3(256), 0, st, P, n, m, table, cap - 1);
   hipLaunchKernelGGL(k_ag_ext, g, dim3(256), 0, st, P, n, m, table, cap - 1, nw, ext);
   const unsigned nwg = (unsigned)std::min<int64_t>((n + 3) / 4, 65536);
-  hipLaunchKernelGGL(k_ag_rows<false>, dim3(nwg), dim3(256), 0, st, P, n, m, table, cap - 1, nw, ext, cnt, nullptr,
-                     nullptr, nullptr);
+#define FA_AG_CNT(N)                                                                                        \
+  hipLaunchKernelGGL((k_ag_rows<false, N>), dim3(nwg), dim3(256), 0, st, P, n, m, table, cap - 1, nw, ext, cnt, \
+                     nullptr, nullptr, nullptr);
+  FA_AG_NWL_SWITCH(nw, FA_AG_CNT)
   (void)hipcub::DeviceScan::InclusiveSum(cub_tmp, cub_bytes, cnt, off + 1, (int)n, st);
   int64_t C = 0;
   (void)hipMemcpyAsync(&C, off + n, 8, hipMemcpyDeviceToHost, st);
@@ -198,9 +252,10 @@ FA_API int fa_hip_ag_gen(const int32_t* P, int64_t n, int m, int F1, void* ws, i
   if (need_host > host_cap) { sizes[1] = need_host; return 6; }
   int32_t* ext_out = reinterpret_cast<int32_t*>(w); w += al(4 * C);
   int32_t* rows_out = reinterpret_cast<int32_t*>(w);
-  if (C)
-    hipLaunchKernelGGL(k_ag_rows<true>, dim3(nwg), dim3(256), 0, st, P, n, m, table, cap - 1, nw, ext, nullptr, off,
-                       ext_out, rows_out);
+#define FA_AG_EMIT(N)                                                                                        \
+  hipLaunchKernelGGL((k_ag_rows<true, N>), dim3(nwg), dim3(256), 0, st, P, n, m, table, cap - 1, nw, ext, nullptr, \
+                     off, ext_out, rows_out);
+  if (C) { FA_AG_NWL_SWITCH(nw, FA_AG_EMIT) }
   (void)hipMemcpyAsync(host, cnt, 4 * (size_t)n, hipMemcpyDeviceToHost, st);
   if (C) {
     (void)hipMemcpyAsync(host + n, ext_out, 4 * (size_t)C, hipMemcpyDeviceToHost, st);
@@ -251,23 +306,24 @@ __global__ __launch_bounds__(256) void k_ag_init(int32_t* __restrict__ table, in
   if (blockIdx.x == 0 && threadIdx.x == 0) off[0] = 0;
 }
 
-// Bitset of the items in rows (4096 bits): privatised in LDS per workgroup, then one
-// global atomicOr per non-zero word (every thread OR-ing into the same 128 global
+// Bitset of the items in rows (MW u32 words): privatised in LDS per workgroup, then
+// one global atomicOr per non-zero word (every thread OR-ing into the same global
 // words serialised: 2.6 ms per call on T40I10's 150K-candidate levels).
 __global__ __launch_bounds__(256) void k_ag_mark(const int32_t* __restrict__ rows, int64_t n,
-                                                 uint32_t* __restrict__ bits) {
-  __shared__ uint32_t lb[128];
-  if (threadIdx.x < 128) lb[threadIdx.x] = 0u;
+                                                 uint32_t* __restrict__ bits, int MW) {
+  __shared__ uint32_t lb[kAgMaxF1 / 32];
+  for (int q = threadIdx.x; q < MW; q += 256) lb[q] = 0u;
   __syncthreads();
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
     atomicOr(&lb[rows[i] >> 5], 1u << (rows[i] & 31));
   __syncthreads();
-  if (threadIdx.x < 128 && lb[threadIdx.x]) atomicOr(&bits[threadIdx.x], lb[threadIdx.x]);
+  for (int q = threadIdx.x; q < MW; q += 256)
+    if (lb[q]) atomicOr(&bits[q], lb[q]);
 }
 
 static int ag_chain_dev(const int32_t* P1, int64_t n1, int m1, int nw, char* w0, char* w, int64_t ws_bytes,
                         int32_t* host, int64_t hoff, int64_t host_cap, int max_levels, double growth, int64_t total,
-                        int64_t last, const uint32_t* mark, double lds, int64_t* sizes, hipStream_t st);
+                        int64_t last, const uint32_t* mark, int MW, double lds, int64_t* sizes, hipStream_t st);
 
 // first_free = 1 (lds > 0): P0 is F_{k-1} itself; level 0 (= level k's candidates)
 // is always emitted, its used items (a device bitset, read back with level 1's
@@ -279,19 +335,20 @@ FA_API int fa_hip_ag_chain(const int32_t* P0, int64_t n0, int m0, int F1, void* 
                            int64_t* sizes, hipStream_t st, int first_free, double lds) {
   sizes[0] = 0;
   if (n0 <= 0 || max_levels <= 0) return 0;
-  if (m0 < 2 || F1 > 4096) return 1;
+  if (m0 < 2 || F1 > kAgMaxF1) return 1;
   const int nw = (F1 + 63) / 64;
+  const int MW = ag_mark_words(F1);
   auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
   char* const w0 = static_cast<char*>(ws);
   char* w = w0;
   const int32_t* P = P0;
-  int64_t n = n0, last = n0, total = total0, hoff = first_free ? 128 : 0;
+  int64_t n = n0, last = n0, total = total0, hoff = first_free ? MW : 0;
   int m = m0, L = 0;
   uint32_t* mark = nullptr;
   if (first_free) {
-    if (host_cap < 128) { sizes[1] = 1 << 20; return 6; }
-    mark = reinterpret_cast<uint32_t*>(w); w += al(512);
-    (void)hipMemsetAsync(mark, 0, 512, st);
+    if (host_cap < MW) { sizes[1] = 1 << 20; return 6; }
+    mark = reinterpret_cast<uint32_t*>(w); w += al(4 * MW);
+    (void)hipMemsetAsync(mark, 0, 4 * MW, st);
   }
   int64_t* Cdev = nullptr;
   int64_t Ch = 0;
@@ -315,8 +372,7 @@ FA_API int fa_hip_ag_chain(const int32_t* P0, int64_t n0, int m0, int F1, void* 
     hipLaunchKernelGGL(k_ag_insert, g, dim3(256), 0, st, P, n, m, table, cap - 1);
     hipLaunchKernelGGL(k_ag_ext, g, dim3(256), 0, st, P, n, m, table, cap - 1, nw, ext);
     const unsigned nwg = (unsigned)std::min<int64_t>((n + 3) / 4, 65536);
-    hipLaunchKernelGGL(k_ag_rows<false>, dim3(nwg), dim3(256), 0, st, P, n, m, table, cap - 1, nw, ext, cnt,
-                       nullptr, nullptr, nullptr);
+    FA_AG_NWL_SWITCH(nw, FA_AG_CNT)
     (void)hipcub::DeviceScan::InclusiveSum(cub_tmp, cub_bytes, cnt, off + 1, (int)n, st);
     Cdev = off + n;
     (void)hipMemcpyAsync(&Ch, Cdev, 8, hipMemcpyDeviceToHost, st);
@@ -325,7 +381,7 @@ FA_API int fa_hip_ag_chain(const int32_t* P0, int64_t n0, int m0, int F1, void* 
     if (first_free && l == 1) {
       // level k's used items arrived with this sync: the bundle limit
       int64_t n_used = 0;
-      for (int q = 0; q < 128; ++q) n_used += __builtin_popcount((uint32_t)host[q]);
+      for (int q = 0; q < MW; ++q) n_used += __builtin_popcount((uint32_t)host[q]);
       tmax = ag_total_limit(n_used, lds);
       if (total > ag_slab_cap(n_used, total, lds)) break;   // level k alone needs several passes
     }
@@ -338,13 +394,12 @@ FA_API int fa_hip_ag_chain(const int32_t* P0, int64_t n0, int m0, int F1, void* 
     int32_t* ext_out = cnt + n;
     int32_t* rows_out = ext_out + C;
     w += al(4 * (n + C + C * (m + 1)));
-    hipLaunchKernelGGL(k_ag_rows<true>, dim3(nwg), dim3(256), 0, st, P, n, m, table, cap - 1, nw, ext, nullptr, off,
-                       ext_out, rows_out);
+    FA_AG_NWL_SWITCH(nw, FA_AG_EMIT)
     (void)hipMemcpyAsync(host + hoff, cnt, 4 * (size_t)(n + C + C * (m + 1)), hipMemcpyDeviceToHost, st);
     if (first_free && l == 0) {
       hipLaunchKernelGGL(k_ag_mark, dim3((unsigned)std::min<int64_t>((C * (m + 1) + 255) / 256, 1024)), dim3(256), 0,
-                         st, rows_out, C * (m + 1), mark);
-      (void)hipMemcpyAsync(host, mark, 512, hipMemcpyDeviceToHost, st);
+                         st, rows_out, C * (m + 1), mark, MW);
+      (void)hipMemcpyAsync(host, mark, 4 * MW, hipMemcpyDeviceToHost, st);
     }
     hoff = need_host;
     sizes[2 + l] = C;
@@ -358,7 +413,7 @@ FA_API int fa_hip_ag_chain(const int32_t* P0, int64_t n0, int m0, int F1, void* 
     static const bool devchain = [] { const char* e = getenv("FA_GEN_DEVCHAIN"); return !e || atoi(e) != 0; }();
     if (first_free && l == 0 && devchain)
       return ag_chain_dev(P, n, m, nw, w0, w, ws_bytes, host, hoff, host_cap, max_levels, growth, total, last, mark,
-                          lds, sizes, st);
+                          MW, lds, sizes, st);
   }
   (void)hipStreamSynchronize(st);
   sizes[0] = L;
@@ -392,29 +447,6 @@ __device__ int64_t d_total_limit(int64_t n_used, double lds) {
   return lo;
 }
 
-// Ext bits of row x (own class restricted to y > last, pruned by every (m-1)-subset)
-__device__ __forceinline__ unsigned long long chain_row_bits(const int32_t* __restrict__ P, int64_t i, int m,
-                                                            const int32_t* __restrict__ table, uint32_t mask,
-                                                            int nw, const unsigned long long* __restrict__ ext,
-                                                            int lane) {
-  const int32_t* x = P + i * m;
-  const int32_t last = x[m - 1];
-  const int32_t s0 = ag_find(P, m, table, mask, x, m - 1);
-  unsigned long long a = 0;
-  if (lane < nw) {
-    a = ext[(int64_t)s0 * nw + lane];
-    const int lw = last >> 6;
-    if (lane < lw) a = 0;
-    else if (lane == lw) a &= (last & 63) == 63 ? 0ull : (~0ull << ((last & 63) + 1));
-  }
-  for (int p = 0; p < m - 1 && __ballot(a != 0) != 0ull; ++p) {
-    const int32_t sp = ag_find(P, m, table, mask, x, p);
-    if (sp < 0) { a = 0; break; }
-    if (lane < nw) a &= ext[(int64_t)sp * nw + lane];
-  }
-  return a;
-}
-
 }  // namespace fa
 
 // ---------------------------------------------------------------------------
@@ -440,10 +472,10 @@ constexpr int kAgdMaxLevels = 30;
 constexpr int kAgdBatch = 4;
 
 __global__ void k_agd_setup(long long* __restrict__ c, int64_t n1, int64_t total, int64_t last,
-                            const uint32_t* __restrict__ mark, double lds) {
+                            const uint32_t* __restrict__ mark, int MW, double lds) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   int64_t n_used = 0;
-  for (int q = 0; q < 128; ++q) n_used += __popc(mark[q]);
+  for (int q = 0; q < MW; ++q) n_used += __popc(mark[q]);
   c[0] = total > d_slab_cap(n_used, total, lds) ? 1 : 0;   // level k alone needs several passes
   c[1] = 1;
   c[2] = total;
@@ -503,7 +535,7 @@ __global__ __launch_bounds__(256) void k_agd_ext(const int32_t* __restrict__ P, 
 
 // kEmit = false: cnt[i] = extensions of row i;  true (accepted levels only): ext ids at
 // cnt + n + off[i] (the host layout cnt | ext) and the candidate rows at rows + off[i] * (m + 1)
-template <bool kEmit>
+template <bool kEmit, int NWL = 1>
 __global__ __launch_bounds__(256) void k_agd_rows(const int32_t* __restrict__ P, int m,
                                                   const int32_t* __restrict__ table, uint32_t mask, int nw,
                                                   const unsigned long long* __restrict__ ext, int32_t* __restrict__ cnt,
@@ -514,22 +546,13 @@ __global__ __launch_bounds__(256) void k_agd_rows(const int32_t* __restrict__ P,
   const int lane = threadIdx.x & 63;
   const int64_t nwave = (int64_t)gridDim.x * (blockDim.x / 64);
   for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); i < n; i += nwave) {
-    const unsigned long long a = chain_row_bits(P, i, m, table, mask, nw, ext, lane);
-    const int cc = __popcll(a);
+    unsigned long long a[NWL];
+    const int cc = ag_row_bits<NWL>(P, i, m, table, mask, nw, ext, lane, a);
     const int incl = wave_scan_incl_dpp(cc);
     if (!kEmit) {
       if (lane == 63) cnt[i] = incl;
     } else {
-      int64_t o = off[i] + (incl - cc);
-      const int32_t* x = P + i * m;
-      for (unsigned long long v = a; v; v &= v - 1) {
-        const int32_t y = lane * 64 + __builtin_ctzll(v);
-        cnt[n + o] = y;
-        int32_t* r = rows + o * (m + 1);
-        for (int q = 0; q < m; ++q) r[q] = x[q];
-        r[m] = y;
-        ++o;
-      }
+      ag_emit<NWL>(a, lane, P + i * m, m, off[i] + (incl - cc), cnt + n, rows);
     }
   }
 }
@@ -578,7 +601,7 @@ __global__ __launch_bounds__(1024) void k_agd_scan_decide(const int32_t* __restr
 // levels including level 0 and sizes[2 + l] = C_l for l >= 1.
 static int ag_chain_dev(const int32_t* P1, int64_t n1, int m1, int nw, char* w0, char* w, int64_t ws_bytes,
                         int32_t* host, int64_t hoff, int64_t host_cap, int max_levels, double growth, int64_t total,
-                        int64_t last, const uint32_t* mark, double lds, int64_t* sizes, hipStream_t st) {
+                        int64_t last, const uint32_t* mark, int MW, double lds, int64_t* sizes, hipStream_t st) {
   using namespace fa;
   auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
   const int LM = std::min(max_levels - 1, kAgdMaxLevels - 2);
@@ -592,7 +615,7 @@ static int ag_chain_dev(const int32_t* P1, int64_t n1, int m1, int nw, char* w0,
   long long ch[72];
   ch[0] = LM <= 0;
   ch[1] = 1;
-  hipLaunchKernelGGL(k_agd_setup, dim3(1), dim3(64), 0, st, c, n1, total, last, mark, lds);
+  hipLaunchKernelGGL(k_agd_setup, dim3(1), dim3(64), 0, st, c, n1, total, last, mark, MW, lds);
   for (int l0 = 1; l0 <= LM && !ch[0]; l0 += kAgdBatch) {
     const int l1 = std::min(LM, l0 + kAgdBatch - 1);
     struct Bufs { int32_t* table; uint32_t cap; unsigned long long* ext; int64_t* off; int64_t nb, cb; };
@@ -629,11 +652,17 @@ static int ag_chain_dev(const int32_t* P1, int64_t n1, int m1, int nw, char* w0,
       hipLaunchKernelGGL(k_agd_insert, g, dim3(256), 0, st, P, ml, b.table, b.cap - 1, c, l);
       hipLaunchKernelGGL(k_agd_ext, g, dim3(256), 0, st, P, ml, b.table, b.cap - 1, nw, b.ext, c, l);
       const unsigned nwg = (unsigned)std::min<int64_t>((b.nb + 3) / 4, 2048);
-      hipLaunchKernelGGL(k_agd_rows<false>, dim3(nwg), dim3(256), 0, st, P, ml, b.table, b.cap - 1, nw, b.ext,
-                         lv[l].cnt, b.off, lv[l].rows, c, l);
+#define FA_AGD_ROWS(E, N)                                                                                   \
+  hipLaunchKernelGGL((k_agd_rows<E, N>), dim3(nwg), dim3(256), 0, st, P, ml, b.table, b.cap - 1, nw, b.ext,   \
+                     lv[l].cnt, b.off, lv[l].rows, c, l);
+#define FA_AGD_CNT(N) FA_AGD_ROWS(false, N)
+#define FA_AGD_EMIT(N) FA_AGD_ROWS(true, N)
+      FA_AG_NWL_SWITCH(nw, FA_AGD_CNT)
       hipLaunchKernelGGL(k_agd_scan_decide, dim3(1), dim3(1024), 0, st, lv[l].cnt, b.off, c, l, growth, b.cb);
-      hipLaunchKernelGGL(k_agd_rows<true>, dim3(nwg), dim3(256), 0, st, P, ml, b.table, b.cap - 1, nw, b.ext,
-                         lv[l].cnt, b.off, lv[l].rows, c, l);
+      FA_AG_NWL_SWITCH(nw, FA_AGD_EMIT)
+#undef FA_AGD_EMIT
+#undef FA_AGD_CNT
+#undef FA_AGD_ROWS
       P = lv[l].rows;
     }
     (void)hipMemcpyAsync(ch, c, sizeof(ch), hipMemcpyDeviceToHost, st);
@@ -775,7 +804,8 @@ __global__ __launch_bounds__(1024) void k_dl_decide(const int32_t* __restrict__ 
 
 // Level 0 of a device bundle: candidates of F_{k-1} = P0 [n][m0] (device; n from
 // n_src[0] when given, else n_const; n_bound >= n sizes the buffers), generated
-// into the front of ws, then ONE synchronisation: ctl is copied to ctl_host.
+// into the front of ws; with sync, ONE synchronisation copies ctl to ctl_host
+// (without it the caller queues fa_hip_dl_more and reads everything once).
 // c_bound: the largest C_0 the level may have (one accumulator pass); a larger
 // level is reported as multi (ctl[5]) without its rows.  lds: LDS bytes the slab
 // kernel has for slab + accumulators.  info (int64 out): 0 ws bytes used,
@@ -783,7 +813,7 @@ __global__ __launch_bounds__(1024) void k_dl_decide(const int32_t* __restrict__ 
 // Returns 0, 1 (bad arguments) or 5 (ws too small: info[0] = bytes needed).
 FA_API int fa_hip_dl_level0(const int32_t* P0, const long long* n_src, int64_t n_const, int64_t n_bound, int m0,
                             int F1, void* ws, int64_t ws_bytes, long long* ctl, long long* ctl_host,
-                            int64_t c_bound, double lds, int64_t* info, hipStream_t st) {
+                            int64_t c_bound, double lds, int64_t* info, int sync, hipStream_t st) {
   if (m0 < 2 || F1 > 4096 || F1 < 1 || n_bound < 0 || c_bound < 1) return 1;
   auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
   const int nw = (F1 + 63) / 64;
@@ -821,21 +851,29 @@ FA_API int fa_hip_dl_level0(const int32_t* P0, const long long* n_src, int64_t n
   hipLaunchKernelGGL(k_dl_mark, dim3((unsigned)std::min<int64_t>((c_bound * (m0 + 1) + 255) / 256, 1024)), dim3(256),
                      0, st, rows, m0 + 1, ctl);
   hipLaunchKernelGGL(k_dl_post0, dim3(1), dim3(64), 0, st, ctl, lds);
-  (void)hipMemcpyAsync(ctl_host, ctl, sizeof(long long) * kDlCtl, hipMemcpyDeviceToHost, st);
-  if (hipStreamSynchronize(st) != hipSuccess) return 7;
+  if (sync) {
+    (void)hipMemcpyAsync(ctl_host, ctl, sizeof(long long) * kDlCtl, hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) return 7;
+  }
   FA_LAUNCH_RET();
 }
 
-// Speculative levels 1 .. max_levels-1 of a device bundle after fa_hip_dl_level0
-// accepted level 0: batches of kAgdBatch levels sized by bounds, one ctl readback
-// per batch.  ws + ws_used is free; desc (int64 [kDlCtl / 8][8], host) holds level
-// 0 on entry and receives every accepted level l:
+// Speculative levels 1 .. max_levels-1 of a device bundle, queued right after
+// fa_hip_dl_level0 (with or without its synchronisation): batches of kAgdBatch
+// levels sized by bounds (n_1 <= n1_bound), each followed by an asynchronous copy of
+// the control block into one of two pinned mirrors.  The next batch is queued
+// before the host waits on the previous one, so the GPU does not idle while the
+// host reads a batch's acceptance; levels of a stopped chain exit at once.  One
+// final synchronisation copies ctl to ctl_host.  ws + ws_used is free; desc (int64
+// [32][8], host) holds level 0's pointers and m on entry (rows 0..3 and 4) and
+// receives every accepted level l:
 //   0 parent rows P_l  1 cnt (ext ids at cnt + n_l)  2 off  3 candidate rows
 //   4 m_l (parent row length)  5 n_l  6 C_l  7 base (candidates of levels < l)
 // Returns 0 (ctl_host[1] = accepted levels incl. level 0), 5 (ws too small:
 // info[0] = bytes needed) or 7.
 FA_API int fa_hip_dl_more(int F1, void* ws, int64_t ws_bytes, int64_t ws_used, long long* ctl, long long* ctl_host,
-                          double growth, int max_levels, double lds, int64_t* desc, int64_t* info, hipStream_t st) {
+                          double growth, int max_levels, double lds, int64_t n1_bound, int64_t* desc, int64_t* info,
+                          hipStream_t st) {
   using namespace fa;
   auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
   const int nw = (F1 + 63) / 64;
@@ -843,13 +881,20 @@ FA_API int fa_hip_dl_more(int F1, void* ws, int64_t ws_bytes, int64_t ws_used, l
   char* w = w0 + ws_used;
   const int LM = std::min(max_levels, 31);
   const int64_t acc_max = (int64_t)(lds / 4);
-  int64_t nb = desc[6];                                  // n_1 = C_0 (exact)
+  int64_t nb = n1_bound;
   int m = (int)desc[4] + 1;
   const int32_t* P = reinterpret_cast<const int32_t*>((intptr_t)desc[3]);
   struct Lv { int32_t* cnt; int64_t* off; int32_t* rows; int m; };
   Lv lv[32];
-  int done = 1;                                          // levels whose acceptance is known
-  for (int l0 = 1; l0 < LM && ctl_host[0] == 0; l0 += kAgdBatch) {
+  // two pinned mirrors of the control block and their events (allocated once)
+  static long long* mirror = nullptr;
+  static hipEvent_t ev[2];
+  if (!mirror) {
+    if (hipHostMalloc(reinterpret_cast<void**>(&mirror), 2 * sizeof(long long) * kDlCtl) != hipSuccess) return 7;
+    for (int k = 0; k < 2; ++k) (void)hipEventCreateWithFlags(&ev[k], hipEventDisableTiming);
+  }
+  int nbatch = 0;
+  auto enqueue = [&](int l0) -> int {
     const int l1 = std::min(LM - 1, l0 + kAgdBatch - 1);
     struct Bufs { int32_t* table; uint32_t cap; unsigned long long* ext; int64_t nb, cb; };
     Bufs bf[kAgdBatch];
@@ -862,7 +907,6 @@ FA_API int fa_hip_dl_more(int F1, void* ws, int64_t ws_bytes, int64_t ws_used, l
       const int64_t need = al(4 * (int64_t)cap) + al(8 * nb * nw) + al(8 * (nb + 1)) + al(4 * (nb + cb)) +
                            al(4 * cb * (m + 1));
       if ((w - w0) + need > ws_bytes) {
-        (void)hipStreamSynchronize(st);
         info[0] = 2 * ((w - w0) + need);
         return 5;
       }
@@ -896,11 +940,26 @@ FA_API int fa_hip_dl_more(int F1, void* ws, int64_t ws_bytes, int64_t ws_used, l
                          lv[l].cnt, lv[l].off, lv[l].rows, ctl, l);
       P = lv[l].rows;
     }
-    (void)hipMemcpyAsync(ctl_host, ctl, sizeof(long long) * kDlCtl, hipMemcpyDeviceToHost, st);
-    if (hipStreamSynchronize(st) != hipSuccess) return 7;
-    done = l1 + 1;
+    long long* hb = mirror + (nbatch & 1) * kDlCtl;
+    (void)hipMemcpyAsync(hb, ctl, sizeof(long long) * kDlCtl, hipMemcpyDeviceToHost, st);
+    (void)hipEventRecord(ev[nbatch & 1], st);
+    ++nbatch;
+    return 0;
+  };
+  int next = 1;                 // first level of the next batch to queue
+  int rc = 0;
+  for (int q = 0; q < 2 && next < LM && rc == 0; ++q, next += kAgdBatch) rc = enqueue(next);
+  for (int waited = 0; rc == 0 && waited < nbatch; ++waited) {
+    if (hipEventSynchronize(ev[waited & 1]) != hipSuccess) return 7;
+    if (mirror[(waited & 1) * kDlCtl]) break;                     // the chain stopped
+    if (next < LM) { rc = enqueue(next); next += kAgdBatch; }     // keep one batch ahead
   }
-  (void)done;
+  (void)hipMemcpyAsync(ctl_host, ctl, sizeof(long long) * kDlCtl, hipMemcpyDeviceToHost, st);
+  if (hipStreamSynchronize(st) != hipSuccess) return 7;
+  if (rc) return rc;
+  desc[5] = ctl_host[8];
+  desc[6] = ctl_host[40];
+  desc[7] = 0;
   const int L = (int)ctl_host[1];
   int64_t base = desc[6];
   for (int l = 1; l < L; ++l) {

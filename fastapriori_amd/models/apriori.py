@@ -47,6 +47,8 @@ HORIZONTAL_PAIRS_PER_S = 2.0e11
 GRAM_WORDPAIRS_PER_S = 1.2e13
 # numeric vocabularies at least this wide count F1 with the sketch + exact pass
 F1_SKETCH_MIN_VOCAB = 1 << 20
+# numeric vocabularies up to this wide read the whole F1 histogram back at once
+F1_HIST_READBACK = 1 << 16
 F1_MAX_CANDIDATES = ops.primitives.F1_MAX_CANDIDATES
 # level bundling (FastApriori._plan_bundle)
 BUNDLE_LEVELS = os.environ.get("FA_BUNDLE", "1") == "1"
@@ -282,7 +284,7 @@ class FastApriori:
     # ------------------------------------------------------------------
     def _device_levels_ok(self, resume) -> bool:
         return (DEVICE_LEVELS and self._dev.type == "cuda" and self._f2_dev is not None and resume is None
-                and self.ckpt is None and not self.cand_par and 2 <= self._F1 <= ops.primitives.AG_DEVICE_MAX_F1
+                and self.ckpt is None and not self.cand_par and 2 <= self._F1 <= ops.primitives.DL_MAX_F1
                 and self.cfg.level_kernel in ("auto", "slab") and self.stats["n_lines"] < (1 << 31))
 
     def _mine_device(self, db, levels: list, counts: list, mc: int, result: MiningResult):
@@ -291,11 +293,12 @@ class FastApriori:
 
         Per bundle: level k's candidates from F_{k-1} rows already on the GPU (F_2, or
         the previous bundle's thresholded rows, their number read by the kernels from
-        device memory), one readback of C_k and the used items (trimming, slab width,
-        whether level k fits one accumulator pass), the speculative levels k+1..
-        accepted on the device (one readback per batch of four), then the piece plan,
-        the slab count, the count all-reduce and the threshold into F rows, all queued
-        on the stream.  The results reach the host once, after the last bundle.
+        device memory) and the speculative levels k+1.. accepted on the device, all
+        queued before ONE synchronisation that returns C_k.., the used items
+        (trimming, slab width) and whether level k fits one accumulator pass; then the
+        piece plan, the slab count, the count all-reduce and the threshold into F
+        rows, queued on the stream.  The results reach the host once, after the last
+        bundle.
         Returns None when mining is complete, or the level from which the host loop
         continues (a level that needs several accumulator passes, or prefixes too long
         for inline piece records): levels/counts then hold F_1 .. F_{k-1}."""
@@ -320,29 +323,20 @@ class FastApriori:
             t0 = time.perf_counter()
             b0 = self._bytes_moved()
             with roctx_range(f"dlevel{k}"), tm.phase(f"level{k}"):
-                L = -1
-                while L < 0:
-                    with roctx_range("gen0"):
-                        c = Pm.dl_level0(S, P0, n_src, n_const, n_bound, m0, F1, c_bound, lds, st)
-                    if c[7] or c[5]:
-                        break
-                    C0, n_used, n0 = int(c[40]), int(c[6]), int(c[8])
-                    S.desc[:] = 0
-                    S.desc[0] = [P0, S.info[1], S.info[2], S.info[3], m0, n0, C0, 0]
-                    max_lv = min(Pm.DL_MAX_M - m0 + 1, Pm.DL_MAX_LEVELS)
-                    if self.cfg.max_level:
-                        max_lv = min(max_lv, self.cfg.max_level - k + 1)
-                    if not BUNDLE_LEVELS or k - 1 > BUNDLE_MAX_PREFIX:
-                        max_lv = 1
-                    L = 1
-                    if max_lv > 1:
-                        with roctx_range("gen_more"):
-                            L = Pm.dl_more(S, F1, BUNDLE_GROWTH, max_lv, lds, st)
+                max_lv = min(Pm.DL_MAX_M - m0 + 1, Pm.DL_MAX_LEVELS)
+                if self.cfg.max_level:
+                    max_lv = min(max_lv, self.cfg.max_level - k + 1)
+                if not BUNDLE_LEVELS or k - 1 > BUNDLE_MAX_PREFIX:
+                    max_lv = 1
+                with roctx_range("gen"):
+                    c = Pm.dl_bundle_gen(S, P0, n_src, n_const, n_bound, m0, F1, c_bound, lds, BUNDLE_GROWTH, max_lv,
+                                         st)
                 if c[7]:
                     break                               # |F_{k-1}| < k or no candidates: done
                 if c[5]:
                     nxt = k                             # several accumulator passes: host path
                     break
+                L, n_used = int(c[1]), int(c[6])
                 bits = np.unpackbits(c[128:192].view(np.uint8), bitorder="little")[:F1]
                 used = np.flatnonzero(bits)
                 Cs = S.desc[:L, 6].copy()
@@ -482,9 +476,15 @@ class FastApriori:
                 if shard.extras.size:
                     hist += torch.bincount(torch.from_numpy(shard.extras.astype(np.int64)), minlength=V).to(dev)
                 comm.all_reduce_(hist)
-                fid = torch.nonzero(hist >= thr).flatten()
-                h = torch.stack([fid, hist[fid].to(torch.int64)]).cpu().numpy()     # one readback
-                got = h[0], h[1]
+                if V <= F1_HIST_READBACK:
+                    # narrow vocabulary: the whole histogram in one readback (no nonzero sync)
+                    hh = hist.cpu().numpy()
+                    fid = np.flatnonzero(hh >= thr)
+                    got = fid, hh[fid]
+                else:
+                    fid = torch.nonzero(hist >= thr).flatten()
+                    h = torch.stack([fid, hist[fid].to(torch.int64)]).cpu().numpy()     # one readback
+                    got = h[0], h[1]
             fid, fcnt = got
             # numeric tokens are ASCII decimal strings, and Java String order of decimals
             # is the order of (digits left-aligned to 10 places, then length): ties of
@@ -499,6 +499,11 @@ class FastApriori:
             items = _Deferred(lambda: ["" if i == 0 else str(i - 1) for i in ids.tolist()])
             self._deferred.append(items)
             counts1 = np.asarray(fcnt)[order].astype(np.int64)
+            if V <= F1_HIST_READBACK and dev.type == "cuda":
+                # the id -> rank LUT built on the host, one asynchronous copy
+                lut_h = np.full(max(V, 1), -1, dtype=np.int32)
+                lut_h[ids] = np.arange(len(order), dtype=np.int32)
+                return items, counts1, ops.primitives.pinned_stage("f1_lut").h2d(lut_h, dev)
             lut = torch.full((max(V, 1),), -1, dtype=torch.int32, device=dev)
             if len(order):
                 lut[torch.from_numpy(fid[order].astype(np.int64)).to(dev)] = torch.arange(

@@ -990,7 +990,12 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
     return out.to(_I64)
 
 
-AG_DEVICE_MAX_F1 = 4096   # bitset words per lane-wave: 64 x 64 bits
+AG_DEVICE_MAX_F1 = 32768  # device apriori-gen: up to 8 bitset words per lane of a 64-lane wave (gen.hip)
+
+
+def ag_mark_words(F1: int) -> int:
+    """u32 words of the chain's used-item bitset (gen.hip ag_mark_words)."""
+    return max(128, (F1 + 31) // 32)
 
 # Device -> host fallbacks taken by the current phase (a mining run or a rules
 # phase clears the list when it starts, reset_fallbacks(), and reports what it
@@ -1091,7 +1096,7 @@ def apriori_gen_chain(rows: np.ndarray, F1: int, dev, max_levels: int, growth: f
     else:
         raise RuntimeError("fa_hip_ag_chain: buffer sizing did not converge")
     h = host.numpy()
-    out, o = [], (128 if first_free else 0)
+    out, o = [], (ag_mark_words(F1) if first_free else 0)
     for lv in range(int(sizes[0])):
         C = int(sizes[2 + lv])
         cnt_h = h[o:o + n]
@@ -1494,6 +1499,7 @@ def count_bundle_dfs(roff, ranks, src, ncols: int, F1: int, levels: list) -> tor
 # models.apriori.FastApriori._mine_device)
 # ---------------------------------------------------------------------------
 DL_CTL = 256            # gen.hip kDlCtl
+DL_MAX_F1 = 4096        # the control block's used-item bitset (ctl[128:192])
 DL_MAX_M = 12           # prefix ids inline in the 48-B piece records
 DL_MAX_LEVELS = 31
 
@@ -1541,35 +1547,36 @@ def dl_slab_width(n_used: int, C: int, lds: int) -> tuple[int, int]:
     return 0, 0
 
 
-def dl_level0(S: DeviceLevelState, P0: int, n_src: int | None, n_const: int, n_bound: int, m0: int, F1: int,
-              c_bound: int, lds: int, stream: int) -> np.ndarray:
-    """Level 0 of a device bundle (one synchronisation).  Returns the control block
-    (host int64 [DL_CTL]); S.info holds (ws used, cnt, off, rows) pointers."""
+def dl_bundle_gen(S: DeviceLevelState, P0: int, n_src: int | None, n_const: int, n_bound: int, m0: int, F1: int,
+                  c_bound: int, lds: int, growth: float, max_levels: int, stream: int) -> np.ndarray:
+    """Candidates of a device bundle: level 0 from F_{k-1} rows P0 and the speculative
+    levels 1 .. max_levels-1 (accepted on the device), all queued before ONE
+    synchronisation.  Returns the control block (host int64 [DL_CTL]); S.desc[:L]
+    describes the accepted levels (L = ctl[1])."""
     lib = _native.hip()
-    for _ in range(4):
+    info = np.zeros(2, dtype=np.int64)
+    for _ in range(6):
+        S.desc[:] = 0
         rc = lib.fa_hip_dl_level0(P0, n_src, n_const, n_bound, m0, F1, _p(S.ws), S.ws.numel(), _p(S.ctl),
-                                  _p(S.ctl_h), c_bound, float(lds), S.info.ctypes.data, stream)
+                                  _p(S.ctl_h), c_bound, float(lds), S.info.ctypes.data, int(max_levels <= 1), stream)
         if rc == 5:
             S.grow(int(S.info[0]))
             continue
         _native.check(rc, "fa_hip_dl_level0")
+        S.desc[0, :5] = [P0, S.info[1], S.info[2], S.info[3], m0]
+        if max_levels <= 1:
+            c = S.ctl_h.numpy()
+            S.desc[0, 5:8] = [c[8], c[40], 0]
+            return c.copy()
+        rc = lib.fa_hip_dl_more(F1, _p(S.ws), S.ws.numel(), int(S.info[0]), _p(S.ctl), _p(S.ctl_h), float(growth),
+                                int(max_levels), float(lds), int(c_bound), S.desc.ctypes.data, info.ctypes.data,
+                                stream)
+        if rc == 5:
+            S.grow(int(info[0]))
+            continue
+        _native.check(rc, "fa_hip_dl_more")
         return S.ctl_h.numpy().copy()
-    raise RuntimeError("fa_hip_dl_level0: workspace sizing did not converge")
-
-
-def dl_more(S: DeviceLevelState, F1: int, growth: float, max_levels: int, lds: int, stream: int) -> int:
-    """Speculative levels 1.. of a device bundle (S.desc[0] = level 0); returns the
-    accepted levels L (S.desc[:L] filled) or -1 when the workspace must grow (the
-    caller then restarts the bundle from level 0: the buffers moved)."""
-    info = np.zeros(2, dtype=np.int64)
-    rc = _native.hip().fa_hip_dl_more(F1, _p(S.ws), S.ws.numel(), int(S.info[0]), _p(S.ctl), _p(S.ctl_h),
-                                      float(growth), int(max_levels), float(lds), S.desc.ctypes.data,
-                                      info.ctypes.data, stream)
-    if rc == 5:
-        S.grow(int(info[0]))
-        return -1
-    _native.check(rc, "fa_hip_dl_more")
-    return int(S.ctl_h[1])
+    raise RuntimeError("device bundle generation: workspace sizing did not converge")
 
 
 def dl_count(S: DeviceLevelState, L: int, roff, ranks, src, ncols: int, F1: int, wword, n_used: int, C: int,

@@ -86,3 +86,20 @@ def test_device_levels_repeat_runs_identical():
     _same(a, b)
     cref, _ = _mine(cpu, 0.002)
     assert c.as_dict() == cref.as_dict()
+
+
+def test_wide_f1_generates_on_device_without_fallbacks(monkeypatch):
+    # F1 = 6319 > 4096: the generator's lanes hold two bitset words each
+    # (gen.hip ag_row_bits<2>); no level may fall back to the host generator
+    from fastapriori_amd import ops
+    cpu = generate_shard(300_000, Comm(), "cpu", 10.0, 4.0, 6000, 12000, 3)
+    calls = []
+    real = ops.primitives.apriori_gen_chain
+    monkeypatch.setattr(ops.primitives, "apriori_gen_chain", lambda *a, **k: calls.append(a[1]) or real(*a, **k))
+    got, st = _mine(cpu.to(DEV), 0.0004)
+    ref, _ = _mine(cpu, 0.0004)
+    assert len(got.items) > 4096 and len(ref.levels) >= 8
+    assert calls and all(f1 == len(got.items) for f1 in calls)
+    assert "fallbacks" not in st
+    assert got.as_dict() == ref.as_dict()
+    _same(got, ref)
