@@ -1102,7 +1102,8 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
     const int32_t* __restrict__ gext_off, const int32_t* __restrict__ gext, int G, int C,
     const int32_t* __restrict__ wword, uint32_t* __restrict__ out, const uint64_t* __restrict__ bm,
     int64_t Wp, int dbg, const int32_t* __restrict__ gpm, const int32_t* __restrict__ bm_rows,
-    const int32_t* __restrict__ dfs2 = nullptr) {
+    const int32_t* __restrict__ dfs2 = nullptr, int nA = 0, uint32_t* __restrict__ outB = nullptr) {
+  // nA / outB (multi-pass DFS): accumulators [0, nA) go to out, [nA, C) to outB
   extern __shared__ uint4 lds4[];                  // 16-B aligned base
   __shared__ unsigned long long build_words[kSlabThreads / 64 * 2];   // window_starts scratch
   constexpr int SWP = SW + 2;                       // row stride: 16-B aligned, odd number of 16-B slots
@@ -1254,7 +1255,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab(
   __syncthreads();
   for (int i = threadIdx.x; i < C; i += blockDim.x) {
     const uint32_t v = acc[i];
-    if (v) atomicAdd(&out[i], v);
+    if (v) atomicAdd(outB && i >= nA ? &outB[i - nA] : &out[i], v);
   }
 }
 
@@ -1836,25 +1837,29 @@ FA_API int fa_hip_count_slab_rec(const int64_t* roff, const int32_t* ranks, cons
   FA_LAUNCH_RET();
 }
 
-// Bundle counting with depth-2 prefix reuse (k_count_slab<.., kDfs = true>):
-// unit weights, one accumulator pass (C <= LDS capacity).  gpre/gpm: prefix slab
-// rows and per-piece (offset, length); prng: per-piece node-1 range; node1: int4,
-// node2: int2 (see the kernel).  Returns 3 when slab + accumulator exceed the LDS.
+// Bundle counting with depth-2 prefix reuse (k_count_slab<.., kDfs = true>), unit
+// weights, one accumulator pass of C counters: gpre/gpm: prefix slab rows and
+// per-piece (offset, length); prng: per-piece node-1 range; node1: int4, node2: int2
+// (see the kernel).  Multi-pass levels (plan.cpp fa_plan_dfs passes) copy the slab
+// from the used-item bitmap bm (bm_rows: slab row -> bitmap row) and flush counters
+// [0, nA) to out, [nA, C) to outB.  Returns 3 when slab + accumulator exceed the LDS.
 FA_API int fa_hip_count_dfs(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
                             const int32_t* item_map, int n_used, const int32_t* gpre, const int32_t* gpm,
                             const int32_t* prng, const int32_t* node1, const int32_t* node2, int NP, int C,
-                            uint32_t* out, int sw, int n_wg, hipStream_t st) {
+                            uint32_t* out, int sw, int n_wg, const uint64_t* bm, int64_t Wp, const int32_t* bm_rows,
+                            int nA, uint32_t* outB, hipStream_t st) {
   if (NP <= 0 || C <= 0 || ncols <= 0) return 0;
   const size_t lds = (size_t)n_used * (sw + 2) * 8 + (size_t)C * 4;
   if (lds > 160 * 1024 - 512) return 3;
   using KernT = void (*)(const int64_t*, const int32_t*, const int32_t*, int64_t, const int32_t*, int,
                          const int32_t*, int, const int32_t*, const int32_t*, int, int, const int32_t*,
                          uint32_t*, const uint64_t*, int64_t, int, const int32_t*, const int32_t*,
-                         const int32_t*);
+                         const int32_t*, int, uint32_t*);
   KernT kern = nullptr;
-#define FA_DFS_CASE(S)                                                              \
-  if (sw == S) kern = src ? (KernT)k_count_slab<S, false, kBuildCols, true>          \
-                          : (KernT)k_count_slab<S, false, kBuildContig, true>;
+#define FA_DFS_CASE(S)                                                                      \
+  if (sw == S) kern = bm ? (KernT)k_count_slab<S, false, kBuildBM, true>                     \
+                         : src ? (KernT)k_count_slab<S, false, kBuildCols, true>             \
+                               : (KernT)k_count_slab<S, false, kBuildContig, true>;
   FA_DFS_CASE(4)
   FA_DFS_CASE(8)
   FA_DFS_CASE(16)
@@ -1864,8 +1869,8 @@ FA_API int fa_hip_count_dfs(const int64_t* roff, const int32_t* ranks, const int
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const int dbg = getenv("FA_SLAB_DEBUG") ? atoi(getenv("FA_SLAB_DEBUG")) : 0;
   hipLaunchKernelGGL(kern, dim3((unsigned)n_wg), dim3(kSlabThreads), lds, st, roff, ranks, src, ncols, item_map,
-                     n_used, gpre, 0, prng, node1, NP, C, (const int32_t*)nullptr, out, (const uint64_t*)nullptr,
-                     (int64_t)0, dbg, gpm, (const int32_t*)nullptr, node2);
+                     n_used, gpre, 0, prng, node1, NP, C, (const int32_t*)nullptr, out, bm, Wp, dbg, gpm, bm_rows,
+                     node2, nA, outB);
   FA_LAUNCH_RET();
 }
 

@@ -424,12 +424,14 @@ FA_API int fa_level_plan(const int32_t* Pf, const int64_t* poff, int64_t G, cons
 // pi[j+1][g'].  Even levels are roots; the odd level after each is read as
 // depth-2 nodes.  buf (int32) receives, at the offsets written to info:
 //   item_map [F1] | used [n_used] | gpre | gpm [NP][2] | prng [NP][2] | node1 [N1][4] | node2 [N2][2]
-// info: 0 n_used 1 NP 2 N1 3 N2 4 C 5..11 offsets of the seven arrays 12 total.
-// Returns 0, or 3 when buf is too small.
+// info: 0 n_used 1 NP 2 N1 3 N2 4 C 5..11 offsets of the seven arrays 12 total
+// 13 accumulator passes (rows of passes, see below; one pass unless cap > 0 and L = 2).
+// Returns 0, or 3 when buf or passes is too small.
 // ---------------------------------------------------------------------------
 FA_API int fa_plan_dfs(int L, const int32_t* const* pv, const int32_t* m, const int32_t* const* pi,
                        const int64_t* const* eo, const int32_t* const* ex, const int64_t* G, const int64_t* Cn,
-                       int32_t F1, int piece_nodes, int32_t* buf, int64_t buf_cap, int64_t* info) {
+                       int32_t F1, int piece_nodes, int32_t* buf, int64_t buf_cap, int64_t* info, int64_t cap,
+                       int64_t* passes, int64_t max_pass) {
   for (int i = 0; i < 16; ++i) info[i] = 0;
   if (L <= 0) return 0;
   std::vector<int64_t> off(L + 1, 0);
@@ -507,13 +509,51 @@ FA_API int fa_plan_dfs(int L, const int32_t* const* pv, const int32_t* m, const 
     n1 += Cn[j];
     if (j + 1 < L) n2 += Cn[j + 1];
   }
-  // cost-sorted pieces (the lanes of a wave then run loops of similar length)
-  std::stable_sort(pcs.begin(), pcs.end(), [](const Piece& x, const Piece& y) { return x.cost > y.cost; });
+  // accumulator passes (two levels, cap > 0): consecutive pieces while their level-k
+  // nodes plus those nodes' children fit the LDS accumulator.  The nodes of a pass
+  // are one contiguous candidate range [A0, A1) and their children one contiguous
+  // range [B0, B1) (children follow their parents' order), so the pass counts into
+  // acc[0, A1 - A0) and acc[A1 - A0, ..) and the launcher flushes the two ranges to
+  // out[A0 ..] and out[C_k + B0 ..].  Output indices in node1 / node2 become
+  // pass-local.  Each pass row: (piece begin, piece end, A0, nA, C_k + B0).
+  int64_t npass = 0;
+  const int64_t NPc = (int64_t)pcs.size();
+  if (cap > 0 && L == 2) {
+    std::vector<int64_t> chst((size_t)Cn[0] + 1, 0);      // children before node c
+    for (int64_t c = 0; c < Cn[0]; ++c) chst[c + 1] = chst[c] + (node1[4 * c + 3] - node1[4 * c + 2]);
+    int64_t p0 = 0;
+    while (p0 < NPc) {
+      const int64_t a0 = pcs[p0].b;
+      int64_t p1 = p0;
+      while (p1 < NPc) {
+        const int64_t a1 = pcs[p1].e;
+        if (p1 > p0 && (a1 - a0) + (chst[a1] - chst[a0]) > cap) break;
+        ++p1;
+      }
+      if (npass >= max_pass) return 3;
+      const int64_t a1 = pcs[p1 - 1].e, na = a1 - a0, b0 = chst[a0];
+      for (int64_t c = a0; c < a1; ++c) node1[4 * c + 1] = (int32_t)(c - a0);
+      for (int64_t j = chst[a0]; j < chst[a1]; ++j) node2[2 * j + 1] = (int32_t)(na + j - b0);
+      int64_t* ps = passes + 5 * npass;
+      ps[0] = p0; ps[1] = p1; ps[2] = a0; ps[3] = na; ps[4] = off[1] + b0;
+      ++npass;
+      p0 = p1;
+    }
+  } else {
+    if (max_pass < 1) return 3;
+    passes[0] = 0; passes[1] = NPc; passes[2] = 0; passes[3] = off[L]; passes[4] = off[L];
+    npass = 1;
+  }
+  // cost-sorted pieces within each pass (the lanes of a wave then run loops of similar length)
+  for (int64_t q = 0; q < npass; ++q)
+    std::stable_sort(pcs.begin() + passes[5 * q], pcs.begin() + passes[5 * q + 1],
+                     [](const Piece& x, const Piece& y) { return x.cost > y.cost; });
   for (size_t i = 0; i < pcs.size(); ++i) {
     gpm[2 * i] = pcs[i].po; gpm[2 * i + 1] = pcs[i].pl;
     prng[2 * i] = pcs[i].b; prng[2 * i + 1] = pcs[i].e;
   }
   info[0] = n_used; info[1] = (int64_t)pcs.size(); info[2] = N1; info[3] = N2; info[4] = off[L];
   info[12] = pos;
+  info[13] = npass;
   return 0;
 }

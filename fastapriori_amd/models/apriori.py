@@ -89,6 +89,10 @@ PAIR_RS_MIN = int(os.environ.get("FA_PAIR_RS_MIN", str(1 << 15)))
 # 17.7 -> 21.0 ms with it, bundle 5-12 16.2 -> 14.6 ms)
 BUNDLE_DFS_MIN_M = int(os.environ.get("FA_BUNDLE_DFS_MIN_M", "4"))
 BUNDLE_GROWTH = float(os.environ.get("FA_BUNDLE_GROWTH", "1.5"))
+# deep levels that need several accumulator passes are counted together with the next
+# level depth-first (_pair_multipass_level) from this prefix length on
+DFS_PAIR = os.environ.get("FA_DFS_PAIR", "1") == "1"
+DFS_PAIR_MIN_M = int(os.environ.get("FA_DFS_PAIR_MIN_M", "4"))
 # level bundles generated, planned, counted and thresholded on the GPU with no host
 # round trip per bundle beyond the generator's acceptance readbacks (_mine_device)
 DEVICE_LEVELS = os.environ.get("FA_DEVICE_LEVELS", "1") == "1"
@@ -239,6 +243,10 @@ class FastApriori:
                 else:
                     with tm.phase("apriori_gen"), roctx_range("bundle"):
                         bundle = self._plan_bundle(db, k, levels[-1], prefix_idx, ext_off, ext, cand_rows)
+                self._dfs_pair = False
+                if len(bundle) == 1:
+                    with tm.phase("apriori_gen"), roctx_range("dfs_pair"):
+                        self._pair_multipass_level(db, k, bundle)
                 # later bundled levels only use items of level k's candidates
                 mark = np.zeros(max(db["F1"], 1), dtype=bool)
                 mark[self._bundle_rows[0].ravel()] = True
@@ -1007,6 +1015,33 @@ class FastApriori:
             cand = nxt
         return bundle
 
+    def _pair_multipass_level(self, db, k: int, bundle: list) -> None:
+        """Cross-level prefix reuse for deep levels (FastApriori.scala:143-145 ANDs a
+        prefix once per group; here a level-k candidate's AND is reused by its own
+        extensions): a level k whose candidates need several accumulator passes is
+        counted together with level k+1 generated from its candidates (a superset of
+        apriori-gen(F_k) with exact counts, as for bundles), depth-first per slab tile
+        (k_count_slab<kDfs>): a level-(k+1) candidate then costs one slab-row read
+        instead of its k prefix rows.  Taken when the prefix is long (the saved reads
+        grow with k), the speculative level grows by at most BUNDLE_GROWTH and the
+        layout has unit weights."""
+        if not (DFS_PAIR and self._dev.type == "cuda" and db["wword"] is None and k - 1 >= DFS_PAIR_MIN_M
+                and self._F1 <= ops.primitives.AG_DEVICE_MAX_F1
+                and (self.cfg.max_level == 0 or k + 1 <= self.cfg.max_level)):
+            return
+        cand = self._bundle_rows[0]
+        C = int(cand.shape[0])
+        used = np.unique(cand)
+        if C == 0 or C <= ops.primitives.slab_capacity(int(used.size), C):
+            return                                   # one pass: the plain slab kernel is faster
+        nxt = ops.primitives.apriori_gen_chain(cand, self._F1, self._dev, 1, BUNDLE_GROWTH, 0, 1 << 40)
+        if not nxt:
+            return
+        pi, eo, ex, rows = nxt[0]
+        bundle.append((k + 1, cand, pi, eo, ex))
+        self._bundle_rows.append(np.ascontiguousarray(rows, np.int32))
+        self._dfs_pair = True
+
     def _cand_rows_view(self, db) -> dict:
         """Candidate mode: this rank's 1/W slice of the replicated rows.
 
@@ -1044,11 +1079,14 @@ class FastApriori:
         if self.cand_par:
             db = self._cand_rows_view(db)
         sizes = [int(ex.size) for *_, ex in bundle]
-        if BUNDLE_DFS and db["wword"] is None and bundle[0][1].shape[1] >= BUNDLE_DFS_MIN_M:
+        if db["wword"] is None and (getattr(self, "_dfs_pair", False) or (
+                BUNDLE_DFS and bundle[0][1].shape[1] >= BUNDLE_DFS_MIN_M)):
             # depth-2 prefix reuse: level k+1 candidates read one slab row under their
-            # parent level-k candidate's AND (k_count_slab<kDfs>)
+            # parent level-k candidate's AND (k_count_slab<kDfs>); a multi-pass level
+            # paired with its children streams the slabs from the used items' bitmap
             cnt = ops.primitives.count_bundle_dfs(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"],
-                                                  [(pv, pi, eo, ex) for _, pv, pi, eo, ex in bundle])
+                                                  [(pv, pi, eo, ex) for _, pv, pi, eo, ex in bundle],
+                                                  full_bm=lambda u: self._bitmaps(db, u), multi=self._dfs_pair)
             if cnt is not None:
                 self.comm.all_reduce_(cnt, bound=self.stats["n_lines"])
                 return np.split(cnt.cpu().numpy(), np.cumsum(sizes)[:-1])

@@ -1425,11 +1425,13 @@ def plan_bundle_dfs(levels: list, F1: int):
                 node1=node1, node2=node2, C=int(off[-1]))
 
 
-def plan_bundle_dfs_native(levels: list, F1: int, out: torch.Tensor | None = None):
+def plan_bundle_dfs_native(levels: list, F1: int, out: torch.Tensor | None = None, cap: int = 0):
     """plan_bundle_dfs in C++ (csrc/host/plan.cpp fa_plan_dfs), written into one int32
-    buffer (``out``, e.g. pinned, grown as needed).  Returns (buf, info) with info =
-    (n_used, NP, N1, N2, C, offsets of item_map, used, gpre, gpm, prng, node1, node2,
-    total)."""
+    buffer (``out``, e.g. pinned, grown as needed).  Returns (buf, info, passes) with
+    info = (n_used, NP, N1, N2, C, offsets of item_map, used, gpre, gpm, prng, node1,
+    node2, total, n_passes) and passes int64 [n_passes, 5] = (piece begin, piece end,
+    A0, nA, B0): cap > 0 with two levels splits the pieces into accumulator passes of
+    <= cap counters (node outputs then pass-local; see fa_plan_dfs)."""
     L = len(levels)
     pv = [np.ascontiguousarray(lv[0], dtype=np.int32) for lv in levels]
     pi = [np.ascontiguousarray(lv[1], dtype=np.int32) for lv in levels]
@@ -1444,31 +1446,51 @@ def plan_bundle_dfs_native(levels: list, F1: int, out: torch.Tensor | None = Non
     need = int(2 * F1 + (G * m)[::2].sum() + 4 * NP + 4 * Cn[::2].sum() + 2 * max(int(Cn[1::2].sum()), 1) + 64 + 8)
     buf = out if out is not None and out.numel() >= need else torch.empty(need, dtype=_I32)
     info = np.zeros(16, dtype=np.int64)
+    passes = np.zeros((NP + 1, 5), dtype=np.int64)
     rc = _native.host().fa_plan_dfs(L, C.cast(arr(pv), C.c_void_p), m.ctypes.data, C.cast(arr(pi), C.c_void_p),
                                     C.cast(arr(eo), C.c_void_p), C.cast(arr(ex), C.c_void_p), G.ctypes.data,
                                     Cn.ctypes.data, F1, DFS_PIECE_NODES, buf.data_ptr(), buf.numel(),
-                                    info.ctypes.data)
+                                    info.ctypes.data, int(cap), passes.ctypes.data, passes.shape[0])
     if rc != 0:
         raise RuntimeError(f"fa_plan_dfs failed ({rc})")
-    return buf, info
+    return buf, info, passes[:int(info[13])]
 
 
-def count_bundle_dfs(roff, ranks, src, ncols: int, F1: int, levels: list) -> torch.Tensor | None:
+def dfs_width(n_used: int, C: int) -> tuple[int, int]:
+    """Slab width and accumulator capacity of the DFS kernel (no rank map in LDS)."""
+    for s in (16, 32, 8, 4):
+        cap = (_LDS_BYTES - n_used * (s + 2) * 8) // 4
+        if cap >= min(C, 8192) or (s == 4 and cap >= 1024):
+            return s, int(cap)
+    return 0, 0
+
+
+def count_bundle_dfs(roff, ranks, src, ncols: int, F1: int, levels: list, full_bm=None,
+                     multi: bool = False) -> torch.Tensor | None:
     """Counts of every level of a bundle (concatenated, level order) with depth-2
-    prefix reuse; None when the bundle does not fit one LDS accumulator pass."""
+    prefix reuse (k_count_slab<kDfs>): a level-(k+1) candidate costs one slab-row
+    read under its parent level-k candidate's AND.  One accumulator pass, or (multi,
+    two levels) several passes streaming the slab tiles from the used items' bitmap
+    (full_bm(used) -> (bitmap, rank -> row map or None), as count_level).  None when
+    the bundle does not fit (then the caller counts level by level)."""
     dev = ranks.device
     stage = pinned_stage("level_plan")
     est = 2 * F1 + 8 * sum(int(lv[3].size) + int(lv[1].size) * (lv[0].shape[1] + 2) for lv in levels) + 1024
-    buf, info = plan_bundle_dfs_native(levels, F1, stage.get(4 * est).view(dtype=_I32))
-    n_used, NP, C = int(info[0]), int(info[1]), int(info[4])
-    sw = 0
-    for s in (32, 16, 8, 4):
-        cap = (_LDS_BYTES - n_used * (s + 2) * 8) // 4
-        if cap >= min(C, 8192) or (s == 4 and cap >= 1024):
-            sw = s
-            break
-    if sw == 0 or C > (_LDS_BYTES - n_used * (sw + 2) * 8) // 4:
+    # the used items first (they fix the slab width and so the capacity), then the plan
+    used_mask = np.zeros(max(F1, 1), dtype=bool)
+    used_mask[levels[0][0][levels[0][1]].ravel()] = True
+    used_mask[levels[0][3]] = True
+    n_used = int(used_mask.sum())
+    C_all = sum(int(lv[3].size) for lv in levels)
+    sw, cap = dfs_width(n_used, C_all)
+    if sw == 0:
         return None
+    npass_needed = C_all > cap
+    if npass_needed and not (multi and len(levels) == 2 and full_bm is not None):
+        return None
+    buf, info, passes = plan_bundle_dfs_native(levels, F1, stage.get(4 * est).view(dtype=_I32),
+                                               cap if npass_needed else 0)
+    NP, C = int(info[1]), int(info[4])
     total = int(info[12])
     dbuf = buf[:total].to(dev, non_blocking=True)
     if buf.is_pinned():
@@ -1479,17 +1501,35 @@ def count_bundle_dfs(roff, ranks, src, ncols: int, F1: int, levels: list) -> tor
     out = torch.zeros(C, dtype=_I32, device=dev)
     W = (ncols + 63) // 64
     nslabs = (W + sw - 1) // sw
-    lds = n_used * (sw + 2) * 8 + C * 4
-    n_wg = int(min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2)))
-    rc = _native.hip().fa_hip_count_dfs(_p(roff), _p(ranks), _p(src), ncols, ptr[0], n_used, ptr[2], ptr[3], ptr[4],
-                                        ptr[5], ptr[6], NP, C, out.data_ptr(), sw, n_wg, _stream(ranks))
-    if rc == 3:
-        return None
-    _native.check(rc, "fa_hip_count_dfs")
+    st = _stream(ranks)
+    bm, bm_rows, Wp = None, None, 0
+    if len(passes) > 1:
+        used = np.flatnonzero(used_mask).astype(np.int32)
+        bm, bmap = full_bm(used)
+        Wp = bm.stride(0)
+        if bmap is None:
+            bm_rows = ptr[1]                            # slab row u -> bitmap row used[u] (rank-indexed bitmap)
+        else:
+            rows_t = bmap[dbuf[int(info[6]):int(info[6]) + n_used].to(_I64)]
+            bm_rows = rows_t.data_ptr()
+    P = passes.tolist()
+    for q, (p0, p1, a0, na, b0) in enumerate(P):
+        if len(P) == 1:
+            Cq, nA, outB = C, C, None
+        else:       # this pass's nodes, then their children (up to the next pass's first child)
+            Cq = na + (P[q + 1][4] if q + 1 < len(P) else C) - b0
+            nA, outB = na, out.data_ptr() + 4 * b0
+        lds = n_used * (sw + 2) * 8 + Cq * 4
+        n_wg = int(min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2)))
+        rc = _native.hip().fa_hip_count_dfs(_p(roff), _p(ranks), _p(src), ncols, ptr[0], n_used, ptr[2],
+                                            ptr[3] + 8 * p0, ptr[4] + 8 * p0, ptr[5], ptr[6], p1 - p0, Cq,
+                                            out.data_ptr() + 4 * a0, sw, n_wg, _p(bm), Wp, bm_rows, nA, outB, st)
+        if rc == 3:
+            return None
+        _native.check(rc, "fa_hip_count_dfs")
     LAST_LEVEL_PLAN.clear()
-    LAST_LEVEL_PLAN.update(kernel="dfs", rows=int(roff.numel() - 1), used=n_used, sw=sw, cap=int(
-        (_LDS_BYTES - n_used * (sw + 2) * 8) // 4), passes=1, pieces=NP, witems=0, d1=0, d2=0, trie_reads=0,
-        slab_reads=0, m=-1, C=C)
+    LAST_LEVEL_PLAN.update(kernel="dfs", rows=int(roff.numel() - 1), used=n_used, sw=sw, cap=cap,
+                           passes=len(passes), pieces=NP, witems=0, d1=0, d2=0, trie_reads=0, slab_reads=0, m=-1, C=C)
     return out.to(_I64)
 
 
