@@ -450,6 +450,46 @@ __global__ __launch_bounds__(256) void k_row_hash(const int64_t* __restrict__ ro
   h2[x] = (int64_t)(b >> 1);
 }
 
+// Dedup probe (models.apriori FastApriori._want_dedup): the row hash h1 of the
+// first min(T, n_max) compressed rows marks a bit of a 2^22-bit occupancy bitmap;
+// the marked bits estimate the distinct rows by linear counting.  T is read from
+// device memory (the compression scan's total), so the probe is queued behind the
+// emit pass and its result travels with the compression sizes in one readback.
+constexpr int kProbeBits = 1 << 22;
+
+// Only rows of <= kCmpProbeLen items are hashed (the emit pass has written them; longer
+// rows are finished by later tiers); hashed counts them.
+constexpr int kCmpProbeLen = 16;
+
+__global__ __launch_bounds__(256) void k_dedup_probe(const int64_t* __restrict__ roff,
+                                                     const int32_t* __restrict__ ranks,
+                                                     const int64_t* __restrict__ T_dev, int64_t n_max,
+                                                     uint32_t* __restrict__ occ,
+                                                     unsigned long long* __restrict__ hashed) {
+  const int64_t n = min(T_dev[0], n_max);
+  uint32_t mine = 0;
+  for (int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x; x < n; x += (int64_t)gridDim.x * 256) {
+    const int64_t s = roff[x], e = roff[x + 1];
+    if (e - s > kCmpProbeLen) continue;
+    uint64_t a = 0x243F6A8885A308D3ull;
+    for (int64_t i = s; i < e; ++i) a = dmix64(a ^ (uint64_t)(uint32_t)ranks[i]);
+    a = dmix64(a ^ (uint64_t)(e - s));
+    const uint32_t slot = (uint32_t)((a >> 1) & (kProbeBits - 1));      // = (h1 of k_row_hash) mod 2^22
+    atomicOr(&occ[slot >> 5], 1u << (slot & 31));
+    ++mine;
+  }
+  mine = wave_sum_u32(mine);
+  if ((threadIdx.x & 63) == 0 && mine) atomicAdd(hashed, (unsigned long long)mine);
+}
+
+__global__ __launch_bounds__(256) void k_popcount_sum(const uint32_t* __restrict__ w, int64_t n,
+                                                      unsigned long long* __restrict__ out) {
+  uint32_t c = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) c += __popc(w[i]);
+  c = wave_sum_u32(c);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, (unsigned long long)c);
+}
+
 // ---------------------------------------------------------------------------
 // Vertical bitmap build from the compressed rows.  Workgroup (wx, ry) owns the
 // WT-word column block wx and the rank slice [ry*R, ry*R+R): it ORs bits into an
@@ -1188,6 +1228,16 @@ FA_API int fa_hip_row_hash(const int64_t* roff, const int32_t* ranks, int64_t T,
                            int64_t* h2, hipStream_t st) {
   if (T <= 0) return 0;
   hipLaunchKernelGGL(k_row_hash, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, st, roff, ranks, T, h1, h2);
+  FA_LAUNCH_RET();
+}
+
+// occ: 2^17 zeroed u32 words; tail: two zeroed int64 (marked slots, hashed rows)
+FA_API int fa_hip_dedup_probe(const int64_t* roff, const int32_t* ranks, const int64_t* T_dev, int64_t n_max,
+                              uint32_t* occ, unsigned long long* tail, hipStream_t st) {
+  if (n_max <= 0) return 0;
+  hipLaunchKernelGGL(k_dedup_probe, dim3((unsigned)std::min<int64_t>((n_max + 255) / 256, 4096)), dim3(256), 0, st,
+                     roff, ranks, T_dev, n_max, occ, tail + 1);
+  hipLaunchKernelGGL(k_popcount_sum, dim3(128), dim3(256), 0, st, occ, (int64_t)(kProbeBits / 32), tail);
   FA_LAUNCH_RET();
 }
 

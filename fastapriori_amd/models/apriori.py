@@ -371,9 +371,14 @@ class FastApriori:
         """Every device level to the host (the run's one results readback)."""
         if not pend:
             return
-        fsz = S.fsz.cpu().numpy()
-        rows_h = torch.cat([p["rows"] for p in pend]).cpu().numpy()
-        cnt_h = torch.cat([p["cnt"] for p in pend]).cpu().numpy()
+        # one readback: F sizes (int64 as int32 pairs), every bundle's rows, then counts
+        nrow = sum(int(p["rows"].numel()) for p in pend)
+        blob = torch.cat([S.fsz.view(torch.int32)] + [p["rows"] for p in pend] + [p["cnt"] for p in pend])
+        blob = blob.cpu().numpy()
+        nf = S.fsz.numel() * 2
+        fsz = blob[:nf].view(np.int64)
+        rows_h = blob[nf:nf + nrow]
+        cnt_h = blob[nf + nrow:]
         ro_base = co_base = 0
         for p in pend:
             for l in range(p["L"]):
@@ -611,10 +616,14 @@ class FastApriori:
         if (dev.type == "cuda" and n_rows > 0 and FUSED_COMPRESS
                 and shard.items.numel() <= FUSED_COMPRESS_MEAN_LEN * n_rows):
             # fused two-pass path: kept rows, offsets, sorted ranks and the length histogram
-            kept, roff, ranks, hist_t, bcnt = ops.compress_rows(shard.offsets, shard.items, lut, F1)
+            # the dedup estimate's probe rides along with the compression sizes (one readback)
+            self._dedup_probe = {} if self.cfg.dedup == "auto" else None
+            kept, roff, ranks, hist_t, bcnt = ops.compress_rows(shard.offsets, shard.items, lut, F1,
+                                                                probe=self._dedup_probe)
             T = kept.numel()
             hist = hist_t.cpu().numpy()
         else:
+            self._dedup_probe = None
             cnt = ops.txn_freq_count(shard.offsets, shard.items, lut)
             kept = torch.nonzero(cnt >= 2).flatten().to(torch.int32)
             T = kept.numel()
@@ -657,15 +666,19 @@ class FastApriori:
         elif mode == "on":
             decision = True
         else:
-            # estimate the distinct fraction on a prefix sample of the rows
-            n = min(db["T"], 1 << 20)
-            h1, _ = ops.row_hash(db["roff"][: n + 1], db["ranks"])
-            # distinct fraction by linear counting (occupied slots of a 4M-slot bitmap of
-            # the row hashes: one scatter + one sum, instead of sorting the sample)
+            # estimate the distinct fraction on a prefix sample of the rows: linear
+            # counting (occupied slots of a 4M-slot bitmap of the row hashes: one
+            # scatter + one sum, instead of sorting the sample)
             m = 1 << 22
-            occ = torch.zeros(m, dtype=torch.uint8, device=h1.device)
-            occ[h1 & (m - 1)] = 1
-            filled = int(occ.sum().item())
+            probe = getattr(self, "_dedup_probe", None)
+            if probe and probe.get("n"):
+                n, filled = probe["n"], probe["filled"]      # computed with the compression (device)
+            else:
+                n = min(db["T"], ops.primitives.DEDUP_PROBE_ROWS)
+                h1, _ = ops.row_hash(db["roff"][: n + 1], db["ranks"])
+                occ = torch.zeros(m, dtype=torch.uint8, device=h1.device)
+                occ[h1 & (m - 1)] = 1
+                filled = int(occ.sum().item())
             est = -m * math.log(max(1.0 - filled / m, 1.0 / m))
             frac = est / max(n, 1)
             decision = frac < self.cfg.dedup_threshold

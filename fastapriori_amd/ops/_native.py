@@ -95,6 +95,7 @@ _HIP_SIGS = {
     "fa_hip_trim_emit": (C.c_int, [vp, vp, vp, C.c_int, i64, vp, vp, vp, vp, vp, vp, vp, vp]),
     "fa_hip_compress_wave": (C.c_int, [vp, vp, vp, vp, i64, vp, vp, vp, C.c_int, vp]),
     "fa_hip_compress_lds": (C.c_int, [vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp]),
+    "fa_hip_dedup_probe": (C.c_int, [vp, vp, vp, i64, vp, vp, vp]),
     "fa_hip_row_hash": (C.c_int, [vp, vp, i64, vp, vp, vp]),
     "fa_hip_build_bitmaps": (C.c_int, [vp, vp, vp, i64, i32, i64, C.c_int, C.c_int, vp, vp, vp, vp]),
     "fa_hip_block_counts": (C.c_int, [vp, vp, i64, i32, vp, vp, C.c_int, vp]),

@@ -234,7 +234,10 @@ def compress(offsets, items, lut, kept, roff, F1: int | None = None) -> torch.Te
 PAIR_PAD_BATCHES = 3 * 16 + 2   # the pair kernel's pipeline reads up to this many batches past a chunk
 
 
-def compress_rows(offsets, items, lut, F1: int, block_counts: bool = True):
+DEDUP_PROBE_ROWS = 1 << 20     # rows hashed by the dedup estimate (FastApriori._want_dedup)
+
+
+def compress_rows(offsets, items, lut, F1: int, block_counts: bool = True, probe: dict | None = None):
     """Fused two-pass compression (device, short rows; csrc/hip/prep.hip k_cmp_agg /
     k_cmp_emit): returns (kept int32 [T], roff int64 [T+1], ranks int32 [nnz],
     length histogram int64 [256], bcnt) with one host synchronisation.  Rows of
@@ -243,7 +246,11 @@ def compress_rows(offsets, items, lut, F1: int, block_counts: bool = True):
     bcnt (block_counts and F1 <= 2048, else None): uint8 [nb * T + pad], the
     per-row item counts of 256-rank blocks that the pair kernel's blocked layout
     needs (pair_counts_horizontal), written by the emit pass while the sorted row
-    is in registers instead of by a separate pass over the ranks."""
+    is in registers instead of by a separate pass over the ranks.
+
+    probe (a dict): also run the dedup probe (prep.hip k_dedup_probe) over the first
+    min(T, DEDUP_PROBE_ROWS) rows, read back with the sizes: probe["n"] rows hashed,
+    probe["filled"] occupied slots of its 2^22-slot bitmap."""
     dev = items.device
     n = offsets.numel() - 1
     nwg = (n + 255) // 256
@@ -266,7 +273,17 @@ def compress_rows(offsets, items, lut, F1: int, block_counts: bool = True):
         bcnt = torch.empty(nb * max(n, 1) + PAIR_PAD_BATCHES * 64 + 64, dtype=torch.uint8, device=dev)
     _hip_call("fa_hip_cmp_emit", _p(offsets), _p(items), _p(lut), n, _p(pre[0]), _p(pre[1]), _p(pre[2]), _p(kept),
               _p(roff), _p(ranks), _p(over), _p(bcnt), nb, st)
-    sizes = pre[:, -1].cpu().tolist()
+    if probe is not None:
+        # the kernel reads T = pre[0, -1] on the device and hashes the rows the emit
+        # pass has finished (<= 16 items; the later tiers write the longer ones)
+        occ = torch.zeros(1 << 17, dtype=_I32, device=dev)
+        tail = torch.zeros(2, dtype=_I64, device=dev)
+        _hip_call("fa_hip_dedup_probe", _p(roff), _p(ranks), pre[0].data_ptr() + 8 * (pre.shape[1] - 1),
+                  DEDUP_PROBE_ROWS, _p(occ), _p(tail), st)
+        sizes = torch.cat([pre[:, -1], tail]).cpu().tolist()
+        probe["filled"], probe["n"] = int(sizes[3]), int(sizes[4])
+    else:
+        sizes = pre[:, -1].cpu().tolist()
     T, nnz, no = int(sizes[0]), int(sizes[1]), int(sizes[2])
     kept, roff, ranks = kept[:T], roff[:T + 1], ranks[:nnz]
     if bcnt is not None:
