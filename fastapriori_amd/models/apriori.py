@@ -89,9 +89,13 @@ PAIR_RS_MIN = int(os.environ.get("FA_PAIR_RS_MIN", str(1 << 15)))
 # 17.7 -> 21.0 ms with it, bundle 5-12 16.2 -> 14.6 ms)
 BUNDLE_DFS_MIN_M = int(os.environ.get("FA_BUNDLE_DFS_MIN_M", "4"))
 BUNDLE_GROWTH = float(os.environ.get("FA_BUNDLE_GROWTH", "1.5"))
-# deep levels that need several accumulator passes are counted together with the next
-# level depth-first (_pair_multipass_level) from this prefix length on
-DFS_PAIR = os.environ.get("FA_DFS_PAIR", "1") == "1"
+# deep levels that need several accumulator passes, counted together with the next level
+# depth-first (_pair_multipass_level) from this prefix length on.  Opt-in: measured slower
+# on T40I10D100M (716 -> 836 ms per run): the depth-2 kernel still walks index chains
+# (piece -> prefix ids -> rows, node -> children) that the record-driven slab kernel
+# removed, and its lanes' child loops are uneven; it halves the slab-row reads of the
+# paired levels, so a record-driven depth-2 kernel is the route to take it further
+DFS_PAIR = os.environ.get("FA_DFS_PAIR", "0") == "1"
 DFS_PAIR_MIN_M = int(os.environ.get("FA_DFS_PAIR_MIN_M", "4"))
 # level bundles generated, planned, counted and thresholded on the GPU with no host
 # round trip per bundle beyond the generator's acceptance readbacks (_mine_device)

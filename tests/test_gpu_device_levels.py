@@ -113,6 +113,7 @@ def test_multipass_level_paired_depth_first(monkeypatch):
     ref, _ = _mine(cpu, 0.004, trim_min_rows=0)
     monkeypatch.setattr(prim, "_LDS_BYTES", 24 * 1024)
     monkeypatch.setattr(ap, "DFS_PAIR_MIN_M", 2)
+    monkeypatch.setattr(ap, "DFS_PAIR", True)            # opt-in (FA_DFS_PAIR=1)
     seen = []
     real = prim.count_bundle_dfs
 
