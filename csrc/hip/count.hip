@@ -349,6 +349,8 @@ constexpr int kRowsStage = 64 * kRowsDw * 4; // 512 staged local-rank bytes per 
 constexpr int kRowsWin = kRowsStage / 64;    // 8 windows
 
 // Batches [q0, q1) of tile (bi, bj) into the packed-u16 LDS tile (no barriers).
+constexpr int kTriTab = 64 * 63 / 2;
+
 struct PairRowsLds {
   uint32_t tile[kPB16 * kPB16 / 2];
   uint32_t sa[kPW][kRowsStage / 4];
@@ -356,6 +358,7 @@ struct PairRowsLds {
   uint8_t rowtab[kPW][64];
   unsigned long long swd[kPW][kRowsWin];
   int2 rowinfo[kPW][64];   // flattened pairs: (pair start, A start | B start << 10 | ci << 20) per row with pairs
+  uint16_t tri[kTriTab];   // diagonal flat decode: t = j (j - 1) / 2 + i -> i | j << 8 (rows of <= 64 items)
 };
 
 // kDiag (bi == bj) is a template parameter: a runtime select between the two
@@ -478,10 +481,18 @@ __device__ __forceinline__ void pair_rows16_chunk_t(PairRowsLds& L, const uint8_
           const int c = (px >> 20) & 0xFF;
           int i, j;
           if (diag) {
-            j = (int)((1.0f + __builtin_sqrtf(8.0f * (float)t + 1.0f)) * 0.5f);
-            if (j * (j - 1) / 2 > t) --j;
-            else if (j * (j + 1) / 2 <= t) ++j;
-            i = t - j * (j - 1) / 2;
+            // the triangular index does not depend on the row: a table (rows of <= 64
+            // items) instead of a quarter-rate square root and its fix-ups
+            if (c <= 64) {
+              const int e = L.tri[t < kTriTab ? t : 0];
+              i = e & 0xFF;
+              j = e >> 8;
+            } else {
+              j = (int)((1.0f + __builtin_sqrtf(8.0f * (float)t + 1.0f)) * 0.5f);
+              if (j * (j - 1) / 2 > t) --j;
+              else if (j * (j + 1) / 2 <= t) ++j;
+              i = t - j * (j - 1) / 2;
+            }
           } else {
             j = (int)(((float)t + 0.5f) * __builtin_amdgcn_rcpf((float)c));
             i = t - j * c;
@@ -636,6 +647,11 @@ __global__ __launch_bounds__(1024) void k_pair_queue16(
     uint32_t* __restrict__ out, int dbg) {
   __shared__ PairRowsLds L;
   __shared__ int s_take[2];
+  for (int t = threadIdx.x; t < kTriTab; t += blockDim.x) {
+    int j = 1;
+    while ((j + 1) * j / 2 <= t) ++j;            // t in [j (j - 1) / 2, j (j + 1) / 2)
+    L.tri[t] = (uint16_t)((t - j * (j - 1) / 2) | (j << 8));
+  }                                             // (ordered before use by the first tile's barriers)
   int cur = -1;                                 // tile held in LDS
   int t = (int)(blockIdx.x % (unsigned)nbp);    // tile to take work from
   for (;;) {
@@ -1741,10 +1757,11 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_trie(
 
 using namespace fa;
 
-// FA_PAIR_FLAT: 2 (default) flattened pairs in the off-diagonal tiles only, 1 in every
-// tile, 0 none, 3 diagonal tiles only -> k_pair_queue16 dbg bits 16 / 32 / 64.
-// Measured (T10I4D100M pair call): 2 13.7, 1 13.9, 0 14.5, 3 14.8 ms -- in diagonal
-// tiles the per-position loops (trip counts L-1-i) beat the square-root decode.
+// FA_PAIR_FLAT: 1 (default) flattened pairs in every tile, 2 in the off-diagonal tiles
+// only, 0 none, 3 diagonal tiles only -> k_pair_queue16 dbg bits 16 / 32 / 64.
+// Measured (T10I4D100M pair call) with the square-root decode of the diagonal tiles:
+// 2 13.7, 1 13.9, 0 14.5, 3 14.8 ms (the per-position loops won); with the triangular
+// decode table (PairRowsLds::tri) 1 beats 2 (headline A/B 45.5-46.3 vs 47.1-47.3 ms).
 static int pair_flat_bits(int v) { return v == 0 ? 16 : v == 2 ? 32 : v == 3 ? 64 : 0; }
 
 // Gram of words [0, W) of bm's rows on the matrix cores, every count multiplied by
@@ -1970,6 +1987,6 @@ FA_API int fa_hip_pair_queue16(const uint8_t* cnt, const int64_t* base, const ui
   hipLaunchKernelGGL(k_pair_queue16, dim3((unsigned)n_wg), dim3(64 * kPW), 0, st, cnt, base, lr, T, nbatch, F1, ld,
                      nb, nbp, qctr, nsub, out,
                      (getenv("FA_PAIR_DEBUG") ? atoi(getenv("FA_PAIR_DEBUG")) : 0) |
-                         pair_flat_bits(getenv("FA_PAIR_FLAT") ? atoi(getenv("FA_PAIR_FLAT")) : 2));
+                         pair_flat_bits(getenv("FA_PAIR_FLAT") ? atoi(getenv("FA_PAIR_FLAT")) : 1));
   FA_LAUNCH_RET();
 }

@@ -148,7 +148,8 @@ def hip():
         with _lock:
             if _hip is None:
                 import torch  # noqa: F401  (load torch's HIP runtime first; see module doc)
-                path = _build.HIP_LIB
+                # FA_HIP_LIB: another build of the same sources' ABI (A/B runs of kernel variants)
+                path = os.environ.get("FA_HIP_LIB") or _build.HIP_LIB
                 if not os.path.exists(path):
                     raise RuntimeError(
                         f"{path} is missing: build it with `python -m fastapriori_amd.ops.build` "
