@@ -1465,201 +1465,6 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
 }
 
 // ---------------------------------------------------------------------------
-// k >= 3, slab counting by lane pairs over unpadded 256-B rows: bank-conflict-free
-// LDS reads (FastApriori.scala:143-154: AND a group's prefix once, popcount each
-// extension against it).
-//
-// k_count_slab_rec gives every thread a piece and reads whole rows at an odd
-// 16-B-slot stride: the 16 lanes of a ds_read_b128 group read random rows, so
-// their slots collide (PMC on T10I4D100M: 42-52 % of the LDS-active cycles were
-// bank conflicts).  Here the two lanes of a pair (2j, 2j+1) share a piece and each
-// takes one 128-B half of the 256-B row (SW = 32 words, 2048 columns per slab).
-// Every pair of a 16-lane group has its own key r = (lane >> 1) & 7 (the four
-// ds_read_b128 groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, ... each hold eight
-// pairs with eight distinct r), and lane (h, r) reads slot 8h + (q ^ r) of the row
-// at step q: the 16 lanes cover the 16 slots of the 256-B bank row whatever rows
-// they read.  A lane reads every row in the same permuted order, so its prefix AND
-// p[q] and extension slot q line up without register indexing; the cost is one
-// v_xor (address ^ 16q) per 16-B read.  The pair's two popcounts are summed with one DPP
-// quad_perm (the pair's lanes have identical control flow: same piece), and lane 0
-// of the pair adds the count into the LDS accumulator.
-// Row stride 256 B means the slab build's ds_or_b64 of one word over random items
-// hits one bank (kBuildContig); the bitmap copy of multi-pass levels (kBuildBM)
-// writes whole rows and stays conflict-free.
-// ---------------------------------------------------------------------------
-constexpr int kPlSW = 32;                  // words per slab row (2048 columns)
-constexpr int kPlRS = kPlSW / 2;           // uint4 per row (256 B, unpadded)
-
-__device__ __forceinline__ uint32_t pair_partner(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-}
-
-template <bool kWeighted, int kBuild>
-__global__ __launch_bounds__(kSlabThreads) void k_count_slab_pl(
-    const int64_t* __restrict__ roff, const int32_t* __restrict__ ranks, const int32_t* __restrict__ src,
-    int64_t ncols, const int32_t* __restrict__ item_map, int F1, int n_used, const int32_t* __restrict__ gpre,
-    const int4* __restrict__ rec, int G_arg, int C, const int32_t* __restrict__ wword, uint32_t* __restrict__ out,
-    const uint64_t* __restrict__ bm, int64_t Wp, const int32_t* __restrict__ bm_rows, int dbg,
-    const int32_t* __restrict__ g_dev) {
-  const int G = g_dev ? *g_dev : G_arg;
-  extern __shared__ uint4 lds4[];
-  __shared__ unsigned long long build_words[kSlabThreads / 64 * 2];
-  __shared__ uint32_t wl[kWeighted ? kPlSW : 1];
-  uint64_t* slab = reinterpret_cast<uint64_t*>(lds4);
-  uint32_t* acc = reinterpret_cast<uint32_t*>(lds4 + (size_t)n_used * kPlRS);
-  uint16_t* smap = reinterpret_cast<uint16_t*>(acc + ((C + 3) & ~3));
-  const bool map_lds = kBuild == kBuildContig && F1 <= kMapLdsMax;
-  for (int i = threadIdx.x; i < C; i += blockDim.x) acc[i] = 0;
-  if (map_lds) {
-    for (int i = threadIdx.x; i < F1; i += blockDim.x) {
-      const int v = item_map[i];
-      smap[i] = v < 0 ? (uint16_t)0xFFFF : (uint16_t)v;
-    }
-  }
-  const int64_t W = (ncols + 63) >> 6;
-  const int64_t nslabs = (W + kPlSW - 1) / kPlSW;
-  constexpr int NPAIR = kSlabThreads / 2;
-  const int lane = (int)(threadIdx.x & 63);
-  const int h = lane & 1;
-  const int rot = (lane >> 1) & 7;
-  const int g0 = (int)(threadIdx.x >> 1);
-  // a row's lane base: row * 256 + this lane's half and key; step q reads base ^ 16q
-  const uint32_t hr = (uint32_t)(128 * h + 16 * rot);
-  const char* ldsb = reinterpret_cast<const char*>(lds4);
-  auto rd = [&](uint32_t rowb, int q) -> uint4 {
-    return *reinterpret_cast<const uint4*>(ldsb + (rowb ^ (uint32_t)(16 * q)));
-  };
-  auto and_row = [&](uint4 (&p)[8], int u) {
-    const uint32_t rowb = ((uint32_t)u << 8) | hr;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const uint4 v = rd(rowb, q);
-      p[q].x &= v.x; p[q].y &= v.y; p[q].z &= v.z; p[q].w &= v.w;
-    }
-  };
-  const int4 z4 = make_int4(0, 0, 0, 0);
-  int4 ra = z4, rb = z4, rc = z4;
-  if (g0 < G) { ra = rec[3 * g0]; rb = rec[3 * g0 + 1]; rc = rec[3 * g0 + 2]; }
-
-  for (int64_t sb = blockIdx.x; sb < nslabs; sb += gridDim.x) {
-    const int64_t w0 = sb * kPlSW;
-    __syncthreads();
-    if (dbg & 1) {
-      // profiling split (FA_SLAB_DEBUG=1): no slab build
-    } else if (kBuild == kBuildBM) {
-      slab_copy_bm<kPlSW, kPlSW, false>(lds4, n_used, bm, Wp, bm_rows, w0, W);
-    } else {
-      {
-        const uint4 z = make_uint4(0, 0, 0, 0);
-        for (int i = threadIdx.x; i < n_used * kPlRS; i += blockDim.x) lds4[i] = z;
-      }
-      __syncthreads();
-      if (kBuild == kBuildContig) {
-        constexpr int NW = kSlabThreads / 64;         // 16 waves, 32 words: no word sharing
-        const int wv = threadIdx.x >> 6;
-        for (int q = wv; q < kPlSW; q += NW) {
-          if ((w0 + q) * 64 >= ncols) continue;
-          if (map_lds)
-            slab_build_word_m(slab, kPlSW, q, (w0 + q) * 64, ncols, roff, ranks, MapLds{smap}, 0, 1,
-                              build_words + wv * 2);
-          else
-            slab_build_word_m(slab, kPlSW, q, (w0 + q) * 64, ncols, roff, ranks, MapGlobal{item_map}, 0, 1,
-                              build_words + wv * 2);
-        }
-      } else {
-        for (int j = threadIdx.x; j < kPlSW * 64; j += blockDim.x) {
-          const int64_t col = w0 * 64 + j;
-          if (col >= ncols) break;
-          const int64_t row = src ? (int64_t)src[col] : col;
-          if (row < 0) continue;
-          const unsigned long long bit = 1ull << (j & 63);
-          uint64_t* base = slab + (j >> 6);
-          for (int64_t r = roff[row], r1 = roff[row + 1]; r < r1; ++r) {
-            const int uu = item_map[ranks[r]];
-            if (uu >= 0) atomicOr((unsigned long long*)(base + (size_t)uu * kPlSW), bit);
-          }
-        }
-      }
-    }
-    __syncthreads();
-    // dedup layouts: word weights of this slab in LDS (wl); a slab of one weight (the
-    // common case: weight classes are contiguous word ranges) counts unweighted and
-    // scales each count by wuni, other slabs read the word weights in the loop
-    uint32_t wuni = 1;
-    if (kWeighted) {
-      if (threadIdx.x < 32) wl[threadIdx.x] = (w0 + threadIdx.x < W) ? (uint32_t)wword[w0 + threadIdx.x] : 0u;
-      __syncthreads();
-      wuni = wl[0];
-#pragma unroll 4
-      for (int q = 1; q < kPlSW; ++q) wuni = wl[q] == wuni ? wuni : 0u;
-    }
-    for (int g = g0; g < ((dbg & 2) ? 0 : G); g += NPAIR) {
-      // this pair's next piece (after its last one: its first, for the next slab)
-      const int gn = g + NPAIR < G ? g + NPAIR : g0;
-      const int4 na = rec[3 * gn], nb = rec[3 * gn + 1], nc = rec[3 * gn + 2];
-      const int n_ext = ra.y & 0xFF, m = (ra.y >> 8) & 0xFF;
-      uint4 p[8];
-      {
-        const uint32_t rowb = ((uint32_t)(ra.z & 0xFFFF) << 8) | hr;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) p[q] = rd(rowb, q);
-      }
-      if (!((ra.y >> 16) & 1)) {
-#pragma unroll
-        for (int j = 1; j < 4; ++j)
-          if (j < m) and_row(p, u16_at(ra, 4 + j));
-        if (m > 4) {
-#pragma unroll
-          for (int j = 4; j < 12; ++j)
-            if (j < m) and_row(p, u16_at(rc, j - 4));
-        }
-      } else {
-        const int32_t* pr = gpre + rc.x;              // long prefixes (m > 12): ids from the plan's gpre
-        for (int j = 1; j < m; ++j) and_row(p, pr[j]);
-      }
-      uint32_t any = 0;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) any |= p[q].x | p[q].y | p[q].z | p[q].w;
-      any |= pair_partner(any);
-      if (any) {
-        const int e0 = ra.x;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          if (k >= n_ext) break;
-          const uint32_t rowb = ((uint32_t)u16_at(rb, k) << 8) | hr;
-          uint32_t s = 0;
-          if (kWeighted && wuni == 0) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-              const uint4 v = rd(rowb, q);
-              const int sq = 8 * h + (q ^ rot);
-              s += (uint32_t)(__popc(p[q].x & v.x) + __popc(p[q].y & v.y)) * wl[2 * sq] +
-                   (uint32_t)(__popc(p[q].z & v.z) + __popc(p[q].w & v.w)) * wl[2 * sq + 1];
-            }
-          } else {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-              const uint4 v = rd(rowb, q);
-              s = bcnt_acc(p[q].x & v.x, s); s = bcnt_acc(p[q].y & v.y, s);
-              s = bcnt_acc(p[q].z & v.z, s); s = bcnt_acc(p[q].w & v.w, s);
-            }
-            if (kWeighted) s *= wuni;
-          }
-          s += pair_partner(s);
-          if (h == 0 && s) atomicAdd(&acc[e0 + k], s);
-        }
-      }
-      ra = na; rb = nb; rc = nc;
-    }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < C; i += blockDim.x) {
-    const uint32_t v = acc[i];
-    if (v) atomicAdd(&out[i], v);
-  }
-}
-
-// ---------------------------------------------------------------------------
 // k >= 3, trie-shared slab counting (the default level kernel).
 //
 // Same slab-stationary structure as k_count_slab (one LDS slab of the used
@@ -2042,37 +1847,6 @@ FA_API int fa_hip_count_slab_rec(const int64_t* roff, const int32_t* ranks, cons
 #undef FA_REC_CASE
 #undef FA_REC_MODE
   if (!kern) return 1;
-  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  const int dbg = getenv("FA_SLAB_DEBUG") ? atoi(getenv("FA_SLAB_DEBUG")) : 0;
-  hipLaunchKernelGGL(kern, dim3((unsigned)n_wg), dim3(kSlabThreads), lds, st, roff, ranks, src, ncols, item_map, F1,
-                     n_used, gpre, (const int4*)rec, G, C, wword, out, bm, Wp, bm_rows, dbg, g_dev);
-  FA_LAUNCH_RET();
-}
-
-// Lane-pair slab counting over unpadded 256-B rows (k_count_slab_pl): the same
-// piece records and arguments as fa_hip_count_slab_rec, sw must be 32.  LDS:
-// n_used * 256 B of slab + accumulators + the u16 map.  Returns 3 when that
-// exceeds the LDS, 1 for another sw.
-FA_API int fa_hip_count_slab_pl(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
-                                const int32_t* item_map, int F1, int n_used, const int32_t* gpre, const void* rec,
-                                int G, int C, const int32_t* wword, uint32_t* out, int sw, int n_wg,
-                                const uint64_t* bm, int64_t Wp, hipStream_t st, const int32_t* bm_rows,
-                                const int32_t* g_dev) {
-  if ((G <= 0 && !g_dev) || C <= 0 || ncols <= 0) return 0;
-  if (sw != kPlSW) return 1;
-  const bool contig = !bm && !src;
-  const size_t map_b = (contig && F1 <= kMapLdsMax) ? (size_t)(((int64_t)F1 * 2 + 15) & ~(int64_t)15) : 0;
-  const size_t lds = (size_t)n_used * kPlSW * 8 + (size_t)((C + 3) & ~3) * 4 + map_b;
-  if (lds > 160 * 1024 - 384) return 3;             // static build_words + word weights
-  using KernT = void (*)(const int64_t*, const int32_t*, const int32_t*, int64_t, const int32_t*, int, int,
-                         const int32_t*, const int4*, int, int, const int32_t*, uint32_t*, const uint64_t*, int64_t,
-                         const int32_t*, int, const int32_t*);
-  KernT kern;
-#define FA_PL_MODE(B) kern = wword ? (KernT)k_count_slab_pl<true, B> : (KernT)k_count_slab_pl<false, B>;
-  if (bm) { FA_PL_MODE(kBuildBM) }
-  else if (src) { FA_PL_MODE(kBuildCols) }
-  else { FA_PL_MODE(kBuildContig) }
-#undef FA_PL_MODE
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const int dbg = getenv("FA_SLAB_DEBUG") ? atoi(getenv("FA_SLAB_DEBUG")) : 0;
   hipLaunchKernelGGL(kern, dim3((unsigned)n_wg), dim3(kSlabThreads), lds, st, roff, ranks, src, ncols, item_map, F1,

@@ -198,7 +198,7 @@ FA_API int fa_trie_records(const int32_t* pieces, const int32_t* witems, const i
 // and written into one (pinned) int32 buffer so the driver issues a single
 // host->device copy per level.
 //
-//   params (double[10]): lds_bytes, min_saving (0 = always trie, >1 = never),
+//   params (double[9]): lds_bytes, min_saving (0 = always trie, >1 = never),
 //                       conflict16, conflict8, pass_weight, rounds, emax_max, W,
 //                       LDS bytes per accumulator (4, or 2 for packed 16-bit counters)
 //   info (int64[24]) out:
@@ -206,8 +206,6 @@ FA_API int fa_trie_records(const int32_t* pieces, const int32_t* witems, const i
 //     6 n_passes  7 d1  8 d2  9 trie reads  10 slab reads  11 emax
 //     12 off item_map  13 off used  14 off gext  15 off gpre  16 off pieces/loc_off
 //     17 off witems  18 total int32 written  19 off gpm (slab)  20 off piece records (slab)
-//     21 lane-pair slab kernel (k_count_slab_pl, 256-B rows)
-//   params[9]: lane-pair kernel min accumulator capacity (0 = off)
 //   passes (int64[3 * maxpass]): slab: (piece begin, piece end, ext base);
 //                                trie: (witem begin, witem end, ext base)
 // Returns 0, 3 (buffer too small), 4 (no slab width fits: use the bitmap kernel).
@@ -216,17 +214,8 @@ FA_API int fa_trie_records(const int32_t* pieces, const int32_t* witems, const i
 // 7-10, k_count_slab_rec), 64-B rows read ~0.43x and 256-B rows ~0.55x as many
 // columns per second as 128-B rows (the 256-B form holds 16 uint4 of prefix AND
 // per thread: fewer waves, longer row scans per LDS bank).
-//
-// pl_min_cap > 0: the lane-pair kernel (k_count_slab_pl: unpadded 256-B rows, SW = 32,
-// conflict-free LDS reads) comes first when its accumulator holds at least
-// min(C, pl_min_cap) candidates; *pl_out is then 1.
 static int slab_width(int64_t n_used, int64_t C, double lds, int64_t* cap_out, double accb = 4,
-                      double map_lds = 0, int64_t pl_min_cap = 0, int* pl_out = nullptr) {
-  if (pl_out) *pl_out = 0;
-  if (pl_min_cap > 0 && pl_out) {
-    const int64_t cap = (int64_t)((lds - (double)n_used * 32 * 8 - map_lds) / accb);
-    if (cap >= std::min<int64_t>(C, pl_min_cap) && cap >= 1024) { *cap_out = cap; *pl_out = 1; return 32; }
-  }
+                      double map_lds = 0) {
   for (int sw : {16, 32, 8, 4}) {
     // + the LDS copy of the rank -> slab-row map (u16 per frequent item, k_count_slab_rec)
     const int64_t cap = (int64_t)((lds - (double)n_used * (sw + 2) * 8 - map_lds) / accb);
@@ -247,7 +236,6 @@ FA_API int fa_level_plan(const int32_t* Pf, const int64_t* poff, int64_t G, cons
   const int64_t emax_max = (int64_t)params[6];
   const double W = params[7];
   const double accb = params[8] > 0 ? params[8] : 4;   // LDS bytes per accumulator (2: packed 16-bit)
-  const int64_t pl_min_cap = (int64_t)params[9];
   const int64_t C = ext_off[G] - ext_off[0];
   for (int i = 0; i < 24; ++i) info[i] = 0;
   if (G <= 0 || C <= 0) return 1;
@@ -343,10 +331,8 @@ FA_API int fa_level_plan(const int32_t* Pf, const int64_t* poff, int64_t G, cons
 
   // ---- slab kernel: pieces of <= 8 extensions, passes of <= cap, size-sorted per pass
   int64_t cap = 0;
-  int pl = 0;
-  const int sw = slab_width(n_used, C, lds, &cap, accb, (double)fa_slab_map_lds(F1), pl_min_cap, &pl);
+  const int sw = slab_width(n_used, C, lds, &cap, accb, (double)fa_slab_map_lds(F1));
   if (sw == 0) return 4;
-  info[21] = pl;
   struct Piece { int64_t g, lo, hi; };
   std::vector<Piece> pcs;
   pcs.reserve((size_t)pieces8);

@@ -625,10 +625,6 @@ def trim_rows(roff, ranks, alive: torch.Tensor, min_len: int, wrow=None):
 
 
 _LDS_BYTES = 160 * 1024 - 512   # minus the slab kernel's static scratch (build_words)
-# Lane-pair slab kernel (count.hip k_count_slab_pl: unpadded 256-B rows read without
-# bank conflicts): taken whenever its accumulator holds min(C, SLAB_PL_MIN_CAP)
-# candidates (0 = never; plan.cpp slab_width, dl_slab_width).
-SLAB_PL_MIN_CAP = int(os.environ.get("FA_SLAB_PL_MIN_CAP", "8192"))
 
 
 def slab_capacity(n_used: int, C: int) -> int:
@@ -796,7 +792,7 @@ def level_plan_host(prefix: np.ndarray, ext_off: np.ndarray, ext: np.ndarray, F1
     ex = np.ascontiguousarray(ext, dtype=np.int32)
     min_saving = {"auto": _TRIE_MIN_SAVING, "trie": 0.0, "slab": 2.0}[kernel]
     params = np.array([lds_bytes or _LDS_BYTES, min_saving, _TRIE_CONFLICT[16], _TRIE_CONFLICT[8],
-                       TRIE_PASS_WEIGHT, TRIE_ROUNDS, TRIE_EMAX, W, 4.0, SLAB_PL_MIN_CAP], dtype=np.float64)
+                       TRIE_PASS_WEIGHT, TRIE_ROUNDS, TRIE_EMAX, W, 4.0], dtype=np.float64)
     bound = _level_plan_bound(F1, C, G, m)
     buf = np.zeros(bound, np.int32)
     passes = np.zeros((G + C + 2, 3), np.int64)
@@ -947,7 +943,7 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
     W = (ncols + 63) // 64
     min_saving = {"auto": _TRIE_MIN_SAVING, "trie": 0.0, "slab": 2.0}[kernel]
     params = np.array([_LDS_BYTES, min_saving, _TRIE_CONFLICT[16], _TRIE_CONFLICT[8], TRIE_PASS_WEIGHT,
-                       TRIE_ROUNDS, TRIE_EMAX, W, 4.0, SLAB_PL_MIN_CAP], dtype=np.float64)
+                       TRIE_ROUNDS, TRIE_EMAX, W, 4.0], dtype=np.float64)
     bound = _level_plan_bound(F1, C, G, m)
     on_gpu = dev.type == "cuda"
     stage = pinned_stage("level_plan") if on_gpu else None
@@ -963,7 +959,6 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
     if rc != 0:
         raise RuntimeError(f"fa_level_plan failed ({rc})")
     kern, sw, cap, n_used, npass = int(info[0]), int(info[1]), int(info[2]), int(info[3]), int(info[6])
-    pl = kern == 0 and int(info[21]) == 1
     total = int(info[18])
     dbuf = buf[:total].to(dev, non_blocking=True)
     if on_gpu:
@@ -998,17 +993,15 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
                       b - a, base + 4 * (o_gext + e0), Cq, _p(wword), out.data_ptr() + 4 * e0, sw, n_wg, _p(bm),
                       bm.stride(0) if bm is not None else 0, st, bm_rows)
         else:
-            # piece records (k_count_slab_rec / _pl): 48 B per piece, loaded one piece ahead
-            lds = n_used * (sw if pl else sw + 2) * 8 + Cq * 4 + _slab_map_lds(F1)
+            # piece records (k_count_slab_rec): 48 B per piece, loaded one piece ahead
+            lds = n_used * (sw + 2) * 8 + Cq * 4 + _slab_map_lds(F1)
             n_wg = int(max(1, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2))))
-            _hip_call("fa_hip_count_slab_pl" if pl else "fa_hip_count_slab_rec", _p(roff), _p(ranks), _p(src),
-                      ncols, base + 4 * o_im, F1, n_used,
+            _hip_call("fa_hip_count_slab_rec", _p(roff), _p(ranks), _p(src), ncols, base + 4 * o_im, F1, n_used,
                       base + 4 * o_gpre, base + 4 * (o_rec + 12 * a), b - a, Cq, _p(wword),
                       out.data_ptr() + 4 * e0, sw, n_wg, _p(bm), bm.stride(0) if bm is not None else 0, st,
                       bm_rows, None)
     LAST_LEVEL_PLAN.clear()
-    LAST_LEVEL_PLAN.update(kernel="trie" if kern == 1 else "slab_pl" if pl else "slab", rows=int(roff.numel() - 1),
-                           used=n_used, sw=sw,
+    LAST_LEVEL_PLAN.update(kernel="trie" if kern == 1 else "slab", rows=int(roff.numel() - 1), used=n_used, sw=sw,
                            cap=cap, passes=npass, pieces=int(info[4]), witems=int(info[5]), d1=int(info[7]),
                            d2=int(info[8]), trie_reads=int(info[9]), slab_reads=int(info[10]), m=m, C=C)
     return out.to(_I64)
@@ -1602,22 +1595,13 @@ def dl_lds_budget(F1: int) -> int:
     return _LDS_BYTES - _slab_map_lds(F1)
 
 
-def dl_slab_width(n_used: int, C: int, lds: int) -> tuple[int, int, bool]:
-    """plan.cpp slab_width: (SW, accumulator capacity, lane-pair kernel) for n_used
-    items and C candidates."""
-    if SLAB_PL_MIN_CAP > 0:
-        cap = int((lds - n_used * 32 * 8) // 4)
-        if cap >= min(C, SLAB_PL_MIN_CAP) and cap >= 1024:
-            return 32, cap, True
-    return _dl_padded_width(n_used, C, lds)
-
-
-def _dl_padded_width(n_used: int, C: int, lds: int) -> tuple[int, int, bool]:
+def dl_slab_width(n_used: int, C: int, lds: int) -> tuple[int, int]:
+    """plan.cpp slab_width: (SW, accumulator capacity) for n_used items and C candidates."""
     for sw in (16, 32, 8, 4):
         cap = int((lds - n_used * (sw + 2) * 8) // 4)
         if cap >= min(C, 8192) or (sw == 4 and cap >= 1024):
-            return sw, cap, False
-    return 0, 0, False
+            return sw, cap
+    return 0, 0
 
 
 def dl_bundle_gen(S: DeviceLevelState, P0: int, n_src: int | None, n_const: int, n_bound: int, m0: int, F1: int,
@@ -1658,9 +1642,7 @@ def dl_count(S: DeviceLevelState, L: int, roff, ranks, src, ncols: int, F1: int,
     on the device (not yet reduced across ranks)."""
     dev = ranks.device
     st = _stream(ranks)
-    sw, cap, pl = dl_slab_width(n_used, C, lds)
-    if pl and C > cap:          # one pass is required here: the padded kernel's capacity may hold C
-        sw, cap, pl = _dl_padded_width(n_used, C, lds)
+    sw, cap = dl_slab_width(n_used, C, lds)
     if sw == 0 or C > cap:
         raise RuntimeError(f"device bundle of {C} candidates over {n_used} items does not fit one pass")
     item_map = torch.empty(max(F1, 1), dtype=_I32, device=dev)
@@ -1672,14 +1654,12 @@ def dl_count(S: DeviceLevelState, L: int, roff, ranks, src, ncols: int, F1: int,
     out = torch.zeros(C, dtype=_I32, device=dev)
     W = (ncols + 63) // 64
     nslabs = (W + sw - 1) // sw
-    lds_k = n_used * (sw if pl else sw + 2) * 8 + ((C + 3) & ~3) * 4 + _slab_map_lds(F1)
+    lds_k = n_used * (sw + 2) * 8 + ((C + 3) & ~3) * 4 + _slab_map_lds(F1)
     n_wg = int(max(1, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds_k), 2))))
-    _hip_call("fa_hip_count_slab_pl" if pl else "fa_hip_count_slab_rec", _p(roff), _p(ranks), _p(src), ncols,
-              _p(item_map), F1, n_used, None, _p(rec), 0, C, _p(wword), _p(out), sw, n_wg, None, 0, st, None,
-              _p(S.ctl) + 8 * 221)
+    _hip_call("fa_hip_count_slab_rec", _p(roff), _p(ranks), _p(src), ncols, _p(item_map), F1, n_used, None, _p(rec),
+              0, C, _p(wword), _p(out), sw, n_wg, None, 0, st, None, _p(S.ctl) + 8 * 221)
     LAST_LEVEL_PLAN.clear()
-    LAST_LEVEL_PLAN.update(kernel="slab_dev_pl" if pl else "slab_dev", rows=int(roff.numel() - 1), used=n_used,
-                           sw=sw, cap=cap, passes=1,
+    LAST_LEVEL_PLAN.update(kernel="slab_dev", rows=int(roff.numel() - 1), used=n_used, sw=sw, cap=cap, passes=1,
                            pieces=-1, witems=0, d1=0, d2=0, trie_reads=0, slab_reads=0, m=-1, C=C)
     # (item_map and rec may be freed now: the caching allocator hands their blocks only
     # to work queued later on this stream)
