@@ -730,12 +730,15 @@ __device__ int64_t agd_block_scan(const int32_t* __restrict__ cnt, int64_t* __re
   return carry;
 }
 
+// ctl[4] = 1: the device row count n_src[0] exceeds n_bound (the buffers' size):
+// nothing runs and the host raises
 __global__ __launch_bounds__(kDlCtl) void k_dl_setup0(long long* __restrict__ c, const long long* __restrict__ n_src,
-                                                      int64_t n_const, int kmin) {
+                                                      int64_t n_const, int kmin, int64_t n_bound) {
   c[threadIdx.x] = 0;
   __syncthreads();
   if (threadIdx.x == 0) {
     const int64_t n = n_src ? (int64_t)n_src[0] : n_const;
+    if (n > n_bound) { c[4] = 1; c[0] = 1; return; }
     c[8] = n;
     c[7] = n < kmin ? 1 : 0;       // the reference's loop test |F_{k-1}| >= k (FastApriori.scala:111)
     c[0] = c[7];
@@ -800,6 +803,55 @@ __global__ __launch_bounds__(1024) void k_dl_decide(const int32_t* __restrict__ 
   c[8 + l + 1] = C;
 }
 
+// Speculative level l >= 2 of a device bundle with the next level's structures fused
+// in.  Level l+1's parent rows are level l's candidates (x, y): the candidates of one
+// parent row x are contiguous and form exactly one class of level l+1 (its first m
+// items are x), starting at off[i].  So the class's Ext bitset is the parent's own
+// extension bits a[] and its hash-table entry is hash(x) -> off[i]: the emit pass of
+// level l writes both (no insert / ext kernels, no Ext clear: only class starts are
+// ever looked up), and the count pass clears level l+1's hash table (ntab, ncap
+// entries) while it runs.  kEmit = false: cnt[i] = extensions of row i (+ the clear);
+// true: ext ids at cnt + n + off[i], candidate rows at rows + off[i] * (m + 1), and
+// level l+1's Ext / table (next_ext, ntab; nullptr when no level follows).
+template <bool kEmit>
+__global__ __launch_bounds__(256) void k_dl_rows(const int32_t* __restrict__ P, int m,
+                                                 const int32_t* __restrict__ table, uint32_t mask, int nw,
+                                                 const unsigned long long* __restrict__ ext, int32_t* __restrict__ cnt,
+                                                 const int64_t* __restrict__ off, int32_t* __restrict__ rows,
+                                                 const long long* __restrict__ c, int l, int32_t* __restrict__ ntab,
+                                                 uint32_t ncap, unsigned long long* __restrict__ next_ext) {
+  if (c[0]) return;
+  const int64_t n = c[8 + l];
+  if (!kEmit && ntab) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < (int64_t)ncap; q += stride) ntab[q] = -1;
+  }
+  const int lane = threadIdx.x & 63;
+  const int64_t nwave = (int64_t)gridDim.x * (blockDim.x / 64);
+  for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); i < n; i += nwave) {
+    unsigned long long a[1];
+    const int cc = ag_row_bits<1>(P, i, m, table, mask, nw, ext, lane, a);
+    const int incl = wave_scan_incl_dpp(cc);
+    if (!kEmit) {
+      if (lane == 63) cnt[i] = incl;
+      continue;
+    }
+    const int64_t o = off[i];
+    ag_emit<1>(a, lane, P + i * m, m, o + (incl - cc), cnt + n, rows);
+    if (next_ext && wave_last(incl) > 0) {
+      if (lane < nw) next_ext[o * nw + lane] = a[0];
+      if (lane == 0) {
+        // = ag_hash_drop(candidate row (x, y), m + 1, m): x's items, seed m
+        const int32_t* x = P + i * m;
+        uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)m;
+        for (int q = 0; q < m; ++q) h = ag_mix(h ^ (uint32_t)x[q]);
+        uint32_t at = (uint32_t)h & (ncap - 1);
+        while (atomicCAS(&ntab[at], -1, (int32_t)o) != -1) at = (at + 1) & (ncap - 1);
+      }
+    }
+  }
+}
+
 }  // namespace fa
 
 // Level 0 of a device bundle: candidates of F_{k-1} = P0 [n][m0] (device; n from
@@ -831,7 +883,7 @@ FA_API int fa_hip_dl_level0(const int32_t* P0, const long long* n_src, int64_t n
   int32_t* cnt = reinterpret_cast<int32_t*>(w); w += al(4 * (nb + c_bound));
   int32_t* rows = reinterpret_cast<int32_t*>(w);
   info[1] = (int64_t)(intptr_t)cnt; info[2] = (int64_t)(intptr_t)off; info[3] = (int64_t)(intptr_t)rows;
-  hipLaunchKernelGGL(k_dl_setup0, dim3(1), dim3(kDlCtl), 0, st, ctl, n_src, n_const, m0 + 1);
+  hipLaunchKernelGGL(k_dl_setup0, dim3(1), dim3(kDlCtl), 0, st, ctl, n_src, n_const, m0 + 1, nb);
   AgdClear clr{};
   clr.p[0] = reinterpret_cast<uint32_t*>(table); clr.len[0] = cap; clr.val[0] = ~0u;
   clr.p[1] = reinterpret_cast<uint32_t*>(ext); clr.len[1] = 2 * nb * nw; clr.val[1] = 0u;
@@ -894,51 +946,60 @@ FA_API int fa_hip_dl_more(int F1, void* ws, int64_t ws_bytes, int64_t ws_used, l
     for (int k = 0; k < 2; ++k) (void)hipEventCreateWithFlags(&ev[k], hipEventDisableTiming);
   }
   int nbatch = 0;
+  // level l's hash table and Ext bitsets; for l >= 2 allocated while enqueuing level
+  // l - 1, whose emit pass fills them (k_dl_rows)
+  struct Tab { int32_t* table = nullptr; uint32_t cap = 0; unsigned long long* ext = nullptr; };
+  Tab cur;
+  auto tab_alloc = [&](int64_t rows, Tab& t) -> bool {
+    uint32_t cap = 16;
+    while (cap < 2 * (uint64_t)rows) cap <<= 1;
+    const int64_t need = al(4 * (int64_t)cap) + al(8 * rows * nw);
+    if ((w - w0) + need > ws_bytes) { info[0] = 2 * ((w - w0) + need); return false; }
+    t.table = reinterpret_cast<int32_t*>(w); w += al(4 * (int64_t)cap);
+    t.ext = reinterpret_cast<unsigned long long*>(w); w += al(8 * rows * nw);
+    t.cap = cap;
+    return true;
+  };
   auto enqueue = [&](int l0) -> int {
     const int l1 = std::min(LM - 1, l0 + kAgdBatch - 1);
-    struct Bufs { int32_t* table; uint32_t cap; unsigned long long* ext; int64_t nb, cb; };
-    Bufs bf[kAgdBatch];
-    AgdClear clr{};
-    int64_t clr_max = 0;
     for (int l = l0; l <= l1; ++l) {
       const int64_t cb = std::min<int64_t>(acc_max, (int64_t)(growth * (double)nb) + 1);
-      uint32_t cap = 16;
-      while (cap < 2 * (uint64_t)nb) cap <<= 1;
-      const int64_t need = al(4 * (int64_t)cap) + al(8 * nb * nw) + al(8 * (nb + 1)) + al(4 * (nb + cb)) +
-                           al(4 * cb * (m + 1));
+      if (l == 1) {
+        // level 1's parents are level 0's candidates, emitted by fa_hip_dl_level0: its
+        // table and Ext are built here (clear, insert, ext)
+        if (!tab_alloc(nb, cur)) return 5;
+        AgdClear clr{};
+        clr.p[0] = reinterpret_cast<uint32_t*>(cur.table); clr.len[0] = cur.cap; clr.val[0] = ~0u;
+        clr.p[1] = reinterpret_cast<uint32_t*>(cur.ext); clr.len[1] = 2 * nb * nw; clr.val[1] = 0u;
+        clr.nreg = 2;
+        const int64_t clr_max = std::max<int64_t>(cur.cap, 2 * nb * nw);
+        hipLaunchKernelGGL(k_agd_clear, dim3((unsigned)std::min<int64_t>((clr_max + 255) / 256, 1024)), dim3(256), 0,
+                           st, clr, ctl);
+        const dim3 g((unsigned)std::min<int64_t>((nb + 255) / 256, 512));
+        hipLaunchKernelGGL(k_agd_insert, g, dim3(256), 0, st, P, m, cur.table, cur.cap - 1, ctl, l);
+        hipLaunchKernelGGL(k_agd_ext, g, dim3(256), 0, st, P, m, cur.table, cur.cap - 1, nw, cur.ext, ctl, l);
+      }
+      const int64_t need = al(8 * (nb + 1)) + al(4 * (nb + cb)) + al(4 * cb * (m + 1));
       if ((w - w0) + need > ws_bytes) {
         info[0] = 2 * ((w - w0) + need);
         return 5;
       }
-      Bufs& b = bf[l - l0];
-      b.table = reinterpret_cast<int32_t*>(w); w += al(4 * (int64_t)cap);
-      b.ext = reinterpret_cast<unsigned long long*>(w); w += al(8 * nb * nw);
       lv[l].off = reinterpret_cast<int64_t*>(w); w += al(8 * (nb + 1));
-      b.cap = cap; b.nb = nb; b.cb = cb;
       lv[l].cnt = reinterpret_cast<int32_t*>(w); w += al(4 * (nb + cb));
       lv[l].rows = reinterpret_cast<int32_t*>(w); w += al(4 * cb * (m + 1));
       lv[l].m = m;
-      clr.p[clr.nreg] = reinterpret_cast<uint32_t*>(b.table); clr.len[clr.nreg] = cap; clr.val[clr.nreg++] = ~0u;
-      clr.p[clr.nreg] = reinterpret_cast<uint32_t*>(b.ext); clr.len[clr.nreg] = 2 * nb * nw; clr.val[clr.nreg++] = 0u;
-      clr_max = std::max<int64_t>(clr_max, std::max<int64_t>(cap, 2 * nb * nw));
+      Tab nxt;
+      if (l + 1 < LM && !tab_alloc(cb, nxt)) return 5;
+      const unsigned nwg = (unsigned)std::min<int64_t>((nb + 3) / 4, 2048);
+      hipLaunchKernelGGL(k_dl_rows<false>, dim3(nwg), dim3(256), 0, st, P, m, cur.table, cur.cap - 1, nw, cur.ext,
+                         lv[l].cnt, lv[l].off, lv[l].rows, ctl, l, nxt.table, nxt.cap, nxt.ext);
+      hipLaunchKernelGGL(k_dl_decide, dim3(1), dim3(1024), 0, st, lv[l].cnt, lv[l].off, ctl, l, growth, cb, lds);
+      hipLaunchKernelGGL(k_dl_rows<true>, dim3(nwg), dim3(256), 0, st, P, m, cur.table, cur.cap - 1, nw, cur.ext,
+                         lv[l].cnt, lv[l].off, lv[l].rows, ctl, l, nxt.table, nxt.cap, nxt.ext);
+      P = lv[l].rows;
+      cur = nxt;
       nb = cb;
       ++m;
-    }
-    hipLaunchKernelGGL(k_agd_clear, dim3((unsigned)std::min<int64_t>((clr_max + 255) / 256, 1024)), dim3(256), 0, st,
-                       clr, ctl);
-    for (int l = l0; l <= l1; ++l) {
-      const Bufs& b = bf[l - l0];
-      const int ml = lv[l].m;
-      const dim3 g((unsigned)std::min<int64_t>((b.nb + 255) / 256, 512));
-      hipLaunchKernelGGL(k_agd_insert, g, dim3(256), 0, st, P, ml, b.table, b.cap - 1, ctl, l);
-      hipLaunchKernelGGL(k_agd_ext, g, dim3(256), 0, st, P, ml, b.table, b.cap - 1, nw, b.ext, ctl, l);
-      const unsigned nwg = (unsigned)std::min<int64_t>((b.nb + 3) / 4, 2048);
-      hipLaunchKernelGGL(k_agd_rows<false>, dim3(nwg), dim3(256), 0, st, P, ml, b.table, b.cap - 1, nw, b.ext,
-                         lv[l].cnt, lv[l].off, lv[l].rows, ctl, l);
-      hipLaunchKernelGGL(k_dl_decide, dim3(1), dim3(1024), 0, st, lv[l].cnt, lv[l].off, ctl, l, growth, b.cb, lds);
-      hipLaunchKernelGGL(k_agd_rows<true>, dim3(nwg), dim3(256), 0, st, P, ml, b.table, b.cap - 1, nw, b.ext,
-                         lv[l].cnt, lv[l].off, lv[l].rows, ctl, l);
-      P = lv[l].rows;
     }
     long long* hb = mirror + (nbatch & 1) * kDlCtl;
     (void)hipMemcpyAsync(hb, ctl, sizeof(long long) * kDlCtl, hipMemcpyDeviceToHost, st);

@@ -153,6 +153,7 @@ class FastApriori:
         t_start = time.perf_counter()
         ops.primitives.reset_fallbacks()     # this run reports its own fallbacks only
         self._f2_dev = None                  # F_2 rows on the device (the first device bundle's input)
+        self._f2_n_dev = None                # |F_2| on the device (F_2 not read back yet: _dl_flush)
         dev = shard.items.device
         # candidate parallelism: the data is replicated, so data-side collectives
         # (line count, F1, layout decisions) are local; only count vectors move
@@ -196,6 +197,9 @@ class FastApriori:
         # ---- k = 2 -----------------------------------------------------
         t0 = time.perf_counter()
         b0 = self._bytes_moved()
+        # F_2 may stay on the device (no readback between the pair kernel and the first
+        # device bundle): its host copy then arrives with the run's one results readback
+        self._f2_defer = self._device_levels_planned(resume)
         if resume is not None and len(resume.levels) >= 2:
             levels.append(resume.levels[1]); counts.append(resume.counts[1])
         else:
@@ -205,13 +209,9 @@ class FastApriori:
             if self.ckpt is not None:
                 self.ckpt.save_level(result, 2)
         self.log.line(f"2 candidates items {F1 * (F1 - 1) // 2}")
-        self.log.line(f"2 freq items {len(levels[1])}")
-        self.log.line(f"Use Time 2 items {int((time.perf_counter() - t0) * 1000)}")
-        self._level_recs.append((dict(phase="level", k=2, candidates=F1 * (F1 - 1) // 2, frequent=len(levels[1]),
-                                      ms=(time.perf_counter() - t0) * 1e3, strategy=self.stats.get("pair_strategy"),
-                                      bytes_reduced=self._bytes_moved() - b0,
-                                      hbm_bytes_est=self.stats.get("pair_hbm_bytes_est", 0)),
-                                 "pairs"))
+        self._level2_ms, self._level2_bytes = (time.perf_counter() - t0) * 1e3, self._bytes_moved() - b0
+        if levels[1] is not None:
+            self._log_level2(len(levels[1]))
 
         # ---- k >= 3 ----------------------------------------------------
         k = 3
@@ -291,13 +291,27 @@ class FastApriori:
             levels.pop(); counts.pop()
         return self._finish(result, t_start)
 
+    def _log_level2(self, n2: int) -> None:
+        F1 = self._F1
+        self.log.line(f"2 freq items {n2}")
+        self.log.line(f"Use Time 2 items {int(self._level2_ms)}")
+        self._level_recs.append((dict(phase="level", k=2, candidates=F1 * (F1 - 1) // 2, frequent=n2,
+                                      ms=self._level2_ms, strategy=self.stats.get("pair_strategy"),
+                                      bytes_reduced=self._level2_bytes,
+                                      hbm_bytes_est=self.stats.get("pair_hbm_bytes_est", 0)),
+                                 "pairs"))
+
     # ------------------------------------------------------------------
     # k >= 3 on the device (FastApriori.scala:110-121, :132-160)
     # ------------------------------------------------------------------
-    def _device_levels_ok(self, resume) -> bool:
-        return (DEVICE_LEVELS and self._dev.type == "cuda" and self._f2_dev is not None and resume is None
+    def _device_levels_planned(self, resume) -> bool:
+        return (DEVICE_LEVELS and self._dev.type == "cuda" and resume is None
                 and self.ckpt is None and not self.cand_par and 2 <= self._F1 <= ops.primitives.DL_MAX_F1
-                and self.cfg.level_kernel in ("auto", "slab") and self.stats["n_lines"] < (1 << 31))
+                and self.cfg.level_kernel in ("auto", "slab") and self.stats["n_lines"] < (1 << 31)
+                and (self.cfg.max_level == 0 or self.cfg.max_level >= 3))
+
+    def _device_levels_ok(self, resume) -> bool:
+        return self._device_levels_planned(resume) and self._f2_dev is not None
 
     def _mine_device(self, db, levels: list, counts: list, mc: int, result: MiningResult):
         """Level bundles with no host round trip beyond the generator's (csrc/hip/gen.hip
@@ -321,7 +335,10 @@ class FastApriori:
         c_bound = int(lds // 4)
         st = torch.cuda.current_stream(self._dev).cuda_stream
         f2 = self._f2_dev
-        P0, n_src, n_const, n_bound = f2.data_ptr(), None, int(f2.shape[0]), int(f2.shape[0])
+        if self._f2_n_dev is not None:      # |F_2| only on the device; n_bound sizes the buffers
+            P0, n_src, n_const, n_bound = f2.data_ptr(), self._f2_n_dev.data_ptr(), 0, self._f2_bound
+        else:
+            P0, n_src, n_const, n_bound = f2.data_ptr(), None, int(f2.shape[0]), int(f2.shape[0])
         m0, k = 2, 3
         pend = []
         tm = self._timer
@@ -343,6 +360,8 @@ class FastApriori:
                 with roctx_range("gen"):
                     c = Pm.dl_bundle_gen(S, P0, n_src, n_const, n_bound, m0, F1, c_bound, lds, BUNDLE_GROWTH, max_lv,
                                          st)
+                if c[4]:
+                    raise RuntimeError(f"device bundle at level {k}: |F_{k - 1}| exceeds its bound {n_bound}")
                 if c[7]:
                     break                               # |F_{k-1}| < k or no candidates: done
                 if c[5]:
@@ -353,11 +372,12 @@ class FastApriori:
                 used = np.flatnonzero(bits)
                 Cs = S.desc[:L, 6].copy()
                 C = int(Cs.sum())
+                with roctx_range("plan"):
+                    plan = Pm.dl_plan(S, L, F1, n_used, C, lds, self._dev)
                 with tm.phase(f"trim{k}"), roctx_range("trim"):
                     self._trim(db, used, k, C)
                 with tm.phase("count"), roctx_range("count"):
-                    cnt = Pm.dl_count(S, L, db["roff"], db["ranks"], db["src"], db["ncols"], F1, db["wword"],
-                                      n_used, C, lds)
+                    cnt = Pm.dl_count(S, plan, db["roff"], db["ranks"], db["src"], db["ncols"], F1, db["wword"])
                     self.comm.all_reduce_(cnt)
                     rows_a, cnt_a, ro, co = Pm.dl_threshold(S, L, cnt, mc, k)
             pend.append(dict(k=k, L=L, m0=m0, C=Cs, rows=rows_a, cnt=cnt_a, ro=ro, co=co,
@@ -372,13 +392,28 @@ class FastApriori:
         return nxt
 
     def _dl_flush(self, S, pend: list, levels: list, counts: list, result: MiningResult) -> None:
-        """Every device level to the host (the run's one results readback)."""
-        if not pend:
+        """Every device level to the host (the run's one results readback); F_2 too when
+        it stayed on the device (_pairs with _f2_defer)."""
+        f2 = []
+        if self._f2_n_dev is not None:
+            nb = self._f2_bound
+            f2 = [self._f2_n_dev.view(torch.int32), self._f2_dev[:nb].reshape(-1), self._f2_cnt_dev[:nb]]
+        if not pend and not f2:
             return
         # one readback: F sizes (int64 as int32 pairs), every bundle's rows, then counts
         nrow = sum(int(p["rows"].numel()) for p in pend)
-        blob = torch.cat([S.fsz.view(torch.int32)] + [p["rows"] for p in pend] + [p["cnt"] for p in pend])
+        blob = torch.cat(f2 + [S.fsz.view(torch.int32)] + [p["rows"] for p in pend] + [p["cnt"] for p in pend])
         blob = blob.cpu().numpy()
+        if f2:
+            nb = self._f2_bound
+            n2 = int(blob[:2].view(np.int64)[0])
+            levels[1] = np.ascontiguousarray(blob[2:2 + 2 * n2].reshape(n2, 2))
+            counts[1] = blob[2 + 2 * nb:2 + 2 * nb + n2].astype(np.int64)
+            self._log_level2(n2)
+            blob = blob[2 + 3 * nb:]
+            self._f2_n_dev = None
+        if not pend:
+            return
         nf = S.fsz.numel() * 2
         fsz = blob[:nf].view(np.int64)
         rows_h = blob[nf:nf + nrow]
@@ -649,8 +684,9 @@ class FastApriori:
         # every rank must take the same layout decisions: long rows, dedup and (when the
         # layout stays undeduplicated) the pair strategy, agreed in one collective
         g = self.dcomm.all_gather_ints([int(hist[255] > 0), int(self._want_dedup(db)),
-                                        int(self._pick_gram_local(db, F1))])
+                                        int(self._pick_gram_local(db, F1)), db["pair_work"]])
         db["long_rows"] = bool(g[:, 0].max())
+        db["pair_work_all"] = int(g[:, 3].sum())      # pair increments of every rank (bounds |F_2|)
         db["pair_pick"] = None
         if g[:, 1].max():
             db["bcnt"] = None
@@ -909,7 +945,10 @@ class FastApriori:
             nb = (F1 + 255) // 256
             self.stats["pair_hbm_bytes_est"] = int(2 * (4 * nnz + 8 * T) + nnz * (nb + 1) + T * nb * (nb + 1))
         # read at call time: spawned test ranks set FA_PAIR_RS_MIN after importing this module
-        if self.comm.distributed and flat.numel() >= int(os.environ.get("FA_PAIR_RS_MIN", PAIR_RS_MIN)):
+        rs = self.comm.distributed and flat.numel() >= int(os.environ.get("FA_PAIR_RS_MIN", PAIR_RS_MIN))
+        if self._f2_defer and not rs and iu.is_cuda:
+            return self._pairs_on_device(flat, iu, mc, db)
+        if rs:
             # X12 as reduce-scatter + local threshold + all-gather of the survivors
             # (F_2 << C_2): each rank thresholds its 1/world slice of the summed triangle
             keep, vals = self.comm.reduce_scatter_select(flat, mc, bound=self.stats["n_lines"])
@@ -924,6 +963,31 @@ class FastApriori:
             self._f2_dev = torch.stack([iu[0][keep], iu[1][keep]], 1).to(torch.int32).contiguous()
         h = torch.stack([iu[0][keep], iu[1][keep], vals.to(device=iu.device, dtype=torch.int64)]).cpu().numpy()
         return np.ascontiguousarray(h[:2].T, dtype=np.int32), h[2].astype(np.int64)
+
+    def _pairs_on_device(self, flat: torch.Tensor, iu, mc: int, db):
+        """F_2 = pairs with count >= mc (FastApriori.scala:236-238), compacted on the
+        device in pair order with no host synchronisation: a scan of the keep mask
+        gives every kept pair its row; the rest write to a dump row.  |F_2| stays on
+        the device (the first device bundle reads it); the host copy of F_2 arrives
+        with _dl_flush.  The readback bound: every frequent pair has count >= mc and
+        the counts sum to the pair increments, so |F_2| <= pair increments / mc."""
+        self.comm.all_reduce_(flat, bound=self.stats["n_lines"])
+        C2 = flat.numel()
+        keep = flat >= mc
+        pos = torch.cumsum(keep, 0, dtype=torch.int64)
+        dst = torch.where(keep, pos - 1, C2)
+        pairs = _TRIU_CACHE.get(("i32", self._F1, flat.device))
+        if pairs is None:
+            pairs = _TRIU_CACHE[("i32", self._F1, flat.device)] = torch.stack([iu[0], iu[1]], 1).to(torch.int32)
+        rows = torch.empty((C2 + 1, 2), dtype=torch.int32, device=flat.device)
+        rows.index_copy_(0, dst, pairs)
+        cnt = torch.empty(C2 + 1, dtype=torch.int32, device=flat.device)
+        cnt.index_copy_(0, dst, flat.to(torch.int32))
+        pw = db.get("pair_work_all")      # exact only without rows of >= 255 items (histogram's last bin)
+        exact = pw is not None and not db.get("long_rows", True) and not self.cand_par
+        bound = min(C2, int(pw) // mc + 1) if exact and mc > 0 else C2
+        self._f2_dev, self._f2_cnt_dev, self._f2_n_dev, self._f2_bound = rows, cnt, pos[-1:], max(int(bound), 1)
+        return None, None
 
     # ------------------------------------------------------------------
     # k >= 3 (FastApriori.scala:132-160)

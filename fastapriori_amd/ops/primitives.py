@@ -234,7 +234,10 @@ def compress(offsets, items, lut, kept, roff, F1: int | None = None) -> torch.Te
 PAIR_PAD_BATCHES = 3 * 16 + 2   # the pair kernel's pipeline reads up to this many batches past a chunk
 
 
-DEDUP_PROBE_ROWS = 1 << 20     # rows hashed by the dedup estimate (FastApriori._want_dedup)
+# rows hashed by the dedup estimate (FastApriori._want_dedup): linear counting of 2^18
+# row hashes in 2^22 slots estimates the distinct fraction to ~0.03 % (one standard
+# error); the probe is a fixed cost per rank (1M rows: 0.22 ms)
+DEDUP_PROBE_ROWS = 1 << 18
 
 
 def compress_rows(offsets, items, lut, F1: int, block_counts: bool = True, probe: dict | None = None):
@@ -1636,12 +1639,12 @@ def dl_bundle_gen(S: DeviceLevelState, P0: int, n_src: int | None, n_const: int,
     raise RuntimeError("device bundle generation: workspace sizing did not converge")
 
 
-def dl_count(S: DeviceLevelState, L: int, roff, ranks, src, ncols: int, F1: int, wword, n_used: int, C: int,
-             lds: int) -> torch.Tensor:
-    """Device plan + slab count of a bundle's C candidates (bundle order) -> int32 [C]
-    on the device (not yet reduced across ranks)."""
-    dev = ranks.device
-    st = _stream(ranks)
+def dl_plan(S: DeviceLevelState, L: int, F1: int, n_used: int, C: int, lds: int, dev) -> dict:
+    """Device piece plan of a bundle's C candidates (levels.hip fa_hip_dl_plan), queued
+    on the stream right after the generator's synchronisation: it depends on the
+    candidates only, not on the row layout, so the host's trimming decision runs
+    while it executes.  Returns the plan for dl_count."""
+    st = torch.cuda.current_stream(dev).cuda_stream
     sw, cap = dl_slab_width(n_used, C, lds)
     if sw == 0 or C > cap:
         raise RuntimeError(f"device bundle of {C} candidates over {n_used} items does not fit one pass")
@@ -1652,6 +1655,15 @@ def dl_count(S: DeviceLevelState, L: int, roff, ranks, src, ncols: int, F1: int,
     _native.check(_native.hip().fa_hip_dl_plan(S.desc.ctypes.data, L, _p(S.ctl), F1, _p(item_map), _p(rec), C,
                                                _p(part), part.numel(), st), "fa_hip_dl_plan")
     out = torch.zeros(C, dtype=_I32, device=dev)
+    return dict(sw=sw, cap=cap, item_map=item_map, rec=rec, out=out, n_used=n_used, C=C)
+
+
+def dl_count(S: DeviceLevelState, plan: dict, roff, ranks, src, ncols: int, F1: int, wword) -> torch.Tensor:
+    """Slab count of a planned bundle (dl_plan) over the current rows -> int32 [C] on
+    the device, bundle order (not yet reduced across ranks)."""
+    st = _stream(ranks)
+    sw, cap, n_used, C = plan["sw"], plan["cap"], plan["n_used"], plan["C"]
+    item_map, rec, out = plan["item_map"], plan["rec"], plan["out"]
     W = (ncols + 63) // 64
     nslabs = (W + sw - 1) // sw
     lds_k = n_used * (sw + 2) * 8 + ((C + 3) & ~3) * 4 + _slab_map_lds(F1)

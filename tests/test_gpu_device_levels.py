@@ -127,3 +127,30 @@ def test_multipass_level_paired_depth_first(monkeypatch):
     assert len(ref.levels) >= 5
     assert got.as_dict() == ref.as_dict()
     _same(got, ref)
+
+
+def test_f2_stays_on_device_until_the_flush(monkeypatch):
+    # F_2 compacted on the device (no readback between the pair kernel and the first
+    # bundle): same itemsets, and the reference's log lines in level order
+    import io
+    cpu = generate_shard(200_000, Comm(), "cpu", 10.0, 4.0, 2000, 1000, 9)
+    g = cpu.to(DEV)
+    logs = {}
+    for dl in (True, False):
+        monkeypatch.setattr(ap, "DEVICE_LEVELS", dl)
+        buf = io.StringIO()
+        lg = Logger(0, enabled=True)
+        lg.stream = buf
+        m = FastApriori(0.002, config=MinerConfig(min_support=0.002), logger=lg)
+        res = m.run(g)
+        if dl:
+            assert m._f2_defer and m.stats.get("device_bundles", 0) >= 1
+            got = res
+        else:
+            ref = res
+        logs[dl] = [l.split(" items")[0] for l in buf.getvalue().splitlines() if "items" in l and "Use Time" not in l]
+    _same(got, ref)
+    assert got.as_dict() == _mine(cpu, 0.002)[0].as_dict()
+    # "k candidate items" / "k freq items" lines in the same order (counts may differ only for
+    # bundled candidate supersets, which both loops log the same way)
+    assert logs[True] == logs[False]
