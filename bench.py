@@ -15,8 +15,11 @@ written to a D.dat file: once with the file's pages dropped from the page cache
 JSON line's "e2e" record (``--e2e off`` skips them).
 
 ``vs_baseline`` = this run's itemsets/s over the multi-threaded C++ CPU path of
-the same miner on the same config (BASELINE.md:27; benchmarks/cpu_baselines.json,
-measured by benchmarks/run_bench.py --mode cpu).
+the same miner on the same config (BASELINE.md:27: the reference publishes no
+numbers; benchmarks/cpu_baselines.json, measured on the GPU box's 16 host threads
+by scripts/gpu_cpu_baselines.sh).  That CPU path compresses rows, counts pairs per
+row and counts every level with a column-tiled prefix-shared AND+popcount (its
+"what" field is copied into the JSON line).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config T10I4D100M]
 
@@ -306,7 +309,7 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": round(value / base["itemsets_per_s"], 2) if base else None,
-            "baseline": ({"what": "C++ CPU path of the same miner, same config (BASELINE.md:27)",
+            "baseline": ({"what": base.get("what", "C++ CPU path of the same miner, same config (BASELINE.md:27)"),
                           "itemsets_per_s": base["itemsets_per_s"], "ms": base["ms"],
                           "threads": base.get("threads"), "source": "benchmarks/cpu_baselines.json"}
                          if base else None),
