@@ -810,37 +810,9 @@ __device__ __forceinline__ int nth_bit(unsigned long long m, int i) {
   return __builtin_ctzll(m);
 }
 
-// Pair layout written by the compression (FastApriori._pairs' blocked layout,
-// count.hip k_block_scatter_w semantics): lr holds, block by block (256 ranks), the
-// low bytes of every kept row's ranks of that block, rows in order.  A row's block-b
-// items start at  sum_{b' < b} |block b'| + sum_{kept rows before it} (block-b items).
-// k_cmp_agg writes each workgroup's block-b item count to blk[b * nwg + w]; one
-// exclusive scan of that block-major array gives lrpre[b * nwg + w], the start of
-// workgroup w's block-b items, and the emit pass adds the row prefix inside the
-// workgroup.  Per-row block counts are packed as 16-bit fields (blocks 2q, 2q + 1 in
-// word q): a workgroup of more than 65535 staged tokens could carry, so such a
-// workgroup flags the layout as unusable (lrflag) and the separate scatter pass runs.
-constexpr int kLrMaxWgTokens = 65535;
-
-__device__ __forceinline__ void lr_count(uint32_t v, uint32_t (&cb)[4]) {
-  if (v == 0xFFFFFFFFu) return;
-  const uint32_t b = v >> 8, inc = 1u << ((b & 1u) << 4);
-  cb[0] += (b >> 1) == 0 ? inc : 0u;
-  cb[1] += (b >> 1) == 1 ? inc : 0u;
-  cb[2] += (b >> 1) == 2 ? inc : 0u;
-  cb[3] += (b >> 1) == 3 ? inc : 0u;
-}
-
-__device__ __forceinline__ uint32_t lr_field(const uint32_t (&cb)[4], int b) {
-  const int q = b >> 1;
-  const uint32_t w = q == 0 ? cb[0] : q == 1 ? cb[1] : q == 2 ? cb[2] : cb[3];
-  return (w >> ((b & 1) << 4)) & 0xFFFFu;
-}
-
 __global__ __launch_bounds__(256) void k_cmp_agg(const int64_t* __restrict__ off, const int32_t* __restrict__ items,
                                                  const int32_t* __restrict__ lut, int64_t n,
-                                                 int32_t* __restrict__ agg, uint32_t* __restrict__ hist,
-                                                 int32_t* __restrict__ blk, int nb) {
+                                                 int32_t* __restrict__ agg, uint32_t* __restrict__ hist) {
   __shared__ uint32_t buf[kCmpSpan];
   __shared__ uint32_t lh[256];
   __shared__ int sh[8];
@@ -852,31 +824,13 @@ __global__ __launch_bounds__(256) void k_cmp_agg(const int64_t* __restrict__ off
   const bool staged = cmp_stage(buf, items, lut, base, n_in);
   __syncthreads();
   int c = 0;
-  uint32_t cb[4] = {0u, 0u, 0u, 0u};
   for (int64_t i = s; i < e; ++i) {
     const uint32_t v = staged ? buf[i - base] : (uint32_t)lut[items[i]];
     c += v != 0xFFFFFFFFu;
-    if (blk) lr_count(v, cb);
   }
   const int kept = c >= 2;
   int ea, eb, ta, tb;
   cmp_block_scan2(kept, kept ? c : 0, ea, eb, ta, tb, sh);
-  if (blk) {
-    // the workgroup's block-b item counts of its kept rows (blocks 2q, 2q + 1 packed)
-    __shared__ uint32_t bsh[4][4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t t = (uint32_t)wave_last(wave_scan_incl_dpp(kept ? (int)cb[q] : 0));
-      if ((threadIdx.x & 63) == 0) bsh[threadIdx.x >> 6][q] = t;
-    }
-    __syncthreads();
-    if (threadIdx.x < nb) {
-      const int b = threadIdx.x, q = b >> 1;
-      uint32_t t = 0;
-      for (int w = 0; w < 4; ++w) t += (bsh[w][q] >> ((b & 1) << 4)) & 0xFFFFu;
-      blk[(int64_t)b * gridDim.x + blockIdx.x] = (int32_t)t;
-    }
-  }
   if (kept) atomicAdd(&lh[min(c, 255)], 1u);
   const bool mid = cmp_mid(kept, e - s, staged);
   const unsigned long long ob = __ballot(kept && e - s > kCmpN && !mid);
@@ -892,20 +846,17 @@ __global__ __launch_bounds__(256) void k_cmp_agg(const int64_t* __restrict__ off
   if (lh[threadIdx.x]) atomicAdd(&hist[(blockIdx.x & (kCmpStripes - 1)) * 256 + threadIdx.x], lh[threadIdx.x]);
 }
 
-__global__ __launch_bounds__(256, 8) void k_cmp_emit(const int64_t* __restrict__ off, const int32_t* __restrict__ items,
+__global__ __launch_bounds__(256) void k_cmp_emit(const int64_t* __restrict__ off, const int32_t* __restrict__ items,
                                                   const int32_t* __restrict__ lut, int64_t n,
                                                   const int64_t* __restrict__ pre_rows,
                                                   const int64_t* __restrict__ pre_items,
                                                   const int64_t* __restrict__ pre_over,
                                                   int32_t* __restrict__ kept_out, int64_t* __restrict__ roff,
                                                   int32_t* __restrict__ ranks, int32_t* __restrict__ over,
-                                                  uint8_t* __restrict__ bcnt, int nb,
-                                                  const int64_t* __restrict__ lrpre, uint8_t* __restrict__ lr,
-                                                  int32_t* __restrict__ lrflag) {
+                                                  uint8_t* __restrict__ bcnt, int nb) {
   constexpr int N = kCmpN;
   __shared__ uint32_t buf[kCmpSpan];
   __shared__ int sh[8];
-  __shared__ int64_t wlr[8];                 // this workgroup's block-b start in lr
   const int64_t r0 = (int64_t)blockIdx.x * 256, r1 = min(n, r0 + 256);
   const int64_t r = r0 + threadIdx.x;
   const int64_t base = off[r0], n_in = off[r1] - base;
@@ -916,10 +867,6 @@ __global__ __launch_bounds__(256, 8) void k_cmp_emit(const int64_t* __restrict__
   const int64_t L = e - s;
   uint32_t a[N];
   int c = 0;
-  // lr: the pair layout is written here (lr != nullptr and the workgroup's counts fit 16 bits)
-  const bool do_lr = lr && n_in <= kLrMaxWgTokens;
-  if (lr && !do_lr && threadIdx.x == 0) atomicOr(lrflag, 1);
-  uint32_t cb[4] = {0u, 0u, 0u, 0u};
   if (L <= N) {
 #pragma unroll
     for (int j = 0; j < N; ++j) {
@@ -927,13 +874,11 @@ __global__ __launch_bounds__(256, 8) void k_cmp_emit(const int64_t* __restrict__
       if (j < L) v = staged ? buf[s - base + j] : (uint32_t)lut[items[s + j]];
       a[j] = v;
       c += v != 0xFFFFFFFFu;
-      if (do_lr) lr_count(v, cb);
     }
   } else {
     for (int64_t i = s; i < e; ++i) {
       const uint32_t v = staged ? buf[i - base] : (uint32_t)lut[items[i]];
       c += v != 0xFFFFFFFFu;
-      if (do_lr) lr_count(v, cb);
     }
   }
   const int kept = c >= 2;
@@ -961,40 +906,6 @@ __global__ __launch_bounds__(256, 8) void k_cmp_emit(const int64_t* __restrict__
   }
   const bool mine = kept && L <= N;
   if (mine) bitonic_regs<N>(a);
-  // lr: the row's block-b items go to wlr[b] + (block-b items of the workgroup's
-  // earlier kept rows) + their index inside the block (rows are sorted)
-  uint32_t rp[4] = {0u, 0u, 0u, 0u};
-  __shared__ int lbo[9];                     // block b's bytes at [lbo[b], lbo[b + 1]) of the LDS stage
-  if (do_lr) {
-    if (!kept) { cb[0] = cb[1] = cb[2] = cb[3] = 0u; }
-    int e0, e1, t0, t1;
-    cmp_block_scan2((int)cb[0], (int)cb[1], e0, e1, t0, t1, sh);
-    __syncthreads();
-    int e2, e3, t2, t3;
-    cmp_block_scan2((int)cb[2], (int)cb[3], e2, e3, t2, t3, sh);
-    rp[0] = (uint32_t)e0; rp[1] = (uint32_t)e1; rp[2] = (uint32_t)e2; rp[3] = (uint32_t)e3;
-    if (threadIdx.x < nb) wlr[threadIdx.x] = lrpre[(int64_t)threadIdx.x * gridDim.x + blockIdx.x];
-    if (threadIdx.x == 0) {
-      const uint32_t tp[4] = {(uint32_t)t0, (uint32_t)t1, (uint32_t)t2, (uint32_t)t3};
-      int o = 0;
-      for (int b = 0; b < 8; ++b) { lbo[b] = o; o += b < nb ? (int)lr_field(tp, b) : 0; }
-      lbo[8] = o;
-    }
-    __syncthreads();
-  }
-  // a sorted row's bytes: block-b item k at base(b) + lr_field(rp, b) + k
-  auto lr_row = [&](uint8_t* dst, bool global) {
-    int prevb = -1, k = 0;
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-      if (j < c) {
-        const int b = (int)(a[j] >> 8);
-        k = b == prevb ? k + 1 : 0;
-        prevb = b;
-        dst[(global ? wlr[b] : (int64_t)lbo[b]) + lr_field(rp, b) + k] = (uint8_t)(a[j] & 0xFFu);
-      }
-    }
-  };
   if (bcnt && mine) {
     // per-row item counts of the pair kernel's 256-rank blocks, bcnt[b * T + row]
     // (the layout of k_block_counts_w; T = kept rows, the scan total), byte-packed:
@@ -1081,73 +992,12 @@ __global__ __launch_bounds__(256, 8) void k_cmp_emit(const int64_t* __restrict__
     }
     __syncthreads();
     for (int i = threadIdx.x; i < tb; i += blockDim.x) ranks[obase + i] = (int32_t)buf[i];
-    if (do_lr) {
-      // the workgroup's lr bytes staged in LDS (the ranks' stage is free now), then each
-      // block's contiguous range written coalesced; bytes of overflow rows stay
-      // unwritten here (fa_hip_lr_rows writes them once their ranks are final)
-      __syncthreads();
-      uint8_t* lb = reinterpret_cast<uint8_t*>(buf);
-      if (mine) lr_row(lb, false);
-#pragma unroll
-      for (int t = 0; t < kCmpMidPerWave; ++t) {
-        if (t < nslot) {                         // wave-uniform
-          const int rw = slot_row(t);
-          const int src = rw < 0 ? 0 : rw;
-          const int idx = t < s32 ? (lane & 31) : lane;
-          const int rc = __shfl(c, src, 64);
-          const bool in = rw >= 0 && idx < rc;
-          const unsigned long long half =
-              t < s32 ? ((lane >> 5) ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull) : ~0ull;
-          const int mb = (int)(midv[t] >> 8);
-          const unsigned long long lt = lane == 0 ? 0ull : ((1ull << lane) - 1ull);
-          uint32_t orp[4];                       // the slot row's block prefix (its owner lane's)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) orp[q] = (uint32_t)__shfl((int)rp[q], src, 64);
-          for (int b = 0; b < nb; ++b) {
-            const unsigned long long bm = __ballot(in && mb == b) & half;
-            if (in && mb == b) lb[lbo[b] + lr_field(orp, b) + __popcll(bm & lt)] = (uint8_t)(midv[t] & 0xFFu);
-          }
-        }
-      }
-      __syncthreads();
-      for (int b = 0; b < nb; ++b) {
-        const int n_b = lbo[b + 1] - lbo[b];
-        for (int i = threadIdx.x; i < n_b; i += blockDim.x) lr[wlr[b] + i] = lb[lbo[b] + i];
-      }
-    }
   } else if (mine) {
 #pragma unroll
     for (int j = 0; j < N; ++j)
       if (j < c) ranks[obase + eb + j] = (int32_t)a[j];
-    if (do_lr) lr_row(lr, true);
   }
 }
-// lr bytes of the rows the emit pass left to later tiers (rows[i] = kept row id),
-// from their final sorted ranks: the row's block-b items start at base[b * nbatch +
-// q] (its 64-row batch q) plus the block-b counts of the batch's rows before it.
-__global__ __launch_bounds__(256) void k_lr_rows(const int64_t* __restrict__ roff, const int32_t* __restrict__ ranks,
-                                                 const int32_t* __restrict__ rows, int64_t nrows,
-                                                 const uint8_t* __restrict__ bcnt, int64_t bld,
-                                                 const int64_t* __restrict__ base, int64_t nbatch,
-                                                 uint8_t* __restrict__ lr) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nrows) return;
-  const int64_t x = rows[i], q = x >> 6;
-  int prevb = -1;
-  int64_t pos = 0;
-  for (int64_t k = roff[x], e = roff[x + 1]; k < e; ++k) {
-    const int v = ranks[k], b = v >> 8;
-    if (b != prevb) {
-      pos = base[(int64_t)b * nbatch + q];
-      for (int64_t t = q << 6; t < x; ++t) pos += bcnt[(int64_t)b * bld + t];
-    } else {
-      ++pos;
-    }
-    prevb = b;
-    lr[pos] = (uint8_t)(v & 0xFF);
-  }
-}
-
 // Block counts of the rows the emit pass left to later tiers (rows[i] = row id):
 // thread per row over its final ranks (counts need no order).
 __global__ __launch_bounds__(256) void k_block_counts_rows(const int64_t* __restrict__ roff,
@@ -1432,39 +1282,19 @@ FA_API int fa_hip_trim_emit(const int64_t* roff, const int32_t* ranks, const int
 }
 
 // Two-pass fused compression: agg int32 [3 * nwg], hist u32 [64 * 256] striped copies (zeroed by the caller).
-// blk (optional, with 1 <= nb <= 8): int32 [nb * nWG] block-b item counts per workgroup
 FA_API int fa_hip_cmp_agg(const int64_t* off, const int32_t* items, const int32_t* lut, int64_t n, int32_t* agg,
-                          uint32_t* hist, int32_t* blk, int nb, hipStream_t st) {
+                          uint32_t* hist, hipStream_t st) {
   if (n <= 0) return 0;
-  if (blk && (nb < 1 || nb > 8)) return 1;
-  hipLaunchKernelGGL(k_cmp_agg, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, off, items, lut, n, agg, hist,
-                     blk, nb);
+  hipLaunchKernelGGL(k_cmp_agg, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, off, items, lut, n, agg, hist);
   FA_LAUNCH_RET();
 }
 
-// lr (optional, with bcnt): the pair layout (see kLrMaxWgTokens) of the rows this
-// pass sorts; lrpre: exclusive scan of k_cmp_agg's blk; lrflag: int32, set to 1 when
-// some workgroup could not write its rows (the caller then scatters all of them).
-// The overflow rows' bytes come from fa_hip_lr_rows once their ranks are final.
 FA_API int fa_hip_cmp_emit(const int64_t* off, const int32_t* items, const int32_t* lut, int64_t n,
                            const int64_t* pre_rows, const int64_t* pre_items, const int64_t* pre_over, int32_t* kept,
-                           int64_t* roff, int32_t* ranks, int32_t* over, uint8_t* bcnt, int nb, const int64_t* lrpre,
-                           uint8_t* lr, int32_t* lrflag, hipStream_t st) {
+                           int64_t* roff, int32_t* ranks, int32_t* over, uint8_t* bcnt, int nb, hipStream_t st) {
   if (n <= 0) return 0;
   if (bcnt && (nb < 1 || nb > 8)) return 1;
-  if (lr && (!bcnt || !lrpre || !lrflag)) return 1;
   hipLaunchKernelGGL(k_cmp_emit, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, off, items, lut, n, pre_rows,
-                     pre_items, pre_over, kept, roff, ranks, over, bcnt, nb, lrpre, lr, lrflag);
-  FA_LAUNCH_RET();
-}
-
-// rows: kept row ids whose lr bytes the emit pass left out; bcnt: [nb][bld] block
-// counts; base: the pair layout's (block, 64-row batch) starts (count.hip k_block_scatter_w)
-FA_API int fa_hip_lr_rows(const int64_t* roff, const int32_t* ranks, const int32_t* rows, int64_t nrows,
-                          const uint8_t* bcnt, int64_t bld, const int64_t* base, int64_t nbatch, uint8_t* lr,
-                          hipStream_t st) {
-  if (nrows <= 0) return 0;
-  hipLaunchKernelGGL(k_lr_rows, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, st, roff, ranks, rows, nrows,
-                     bcnt, bld, base, nbatch, lr);
+                     pre_items, pre_over, kept, roff, ranks, over, bcnt, nb);
   FA_LAUNCH_RET();
 }

@@ -100,9 +100,6 @@ DFS_PAIR_MIN_M = int(os.environ.get("FA_DFS_PAIR_MIN_M", "4"))
 # level bundles generated, planned, counted and thresholded on the GPU with no host
 # round trip per bundle beyond the generator's acceptance readbacks (_mine_device)
 DEVICE_LEVELS = os.environ.get("FA_DEVICE_LEVELS", "1") == "1"
-# the pair kernel's local-rank bytes written by the compression's emit pass instead of
-# a separate scatter pass over the ranks (prep.hip kLrMaxWgTokens)
-PAIR_LR_FROM_COMPRESS = os.environ.get("FA_PAIR_LR", "1") == "1"
 BUNDLE_MAX_PREFIX = int(os.environ.get("FA_BUNDLE_MAX_PREFIX", "9"))
 
 
@@ -660,9 +657,8 @@ class FastApriori:
             # fused two-pass path: kept rows, offsets, sorted ranks and the length histogram
             # the dedup estimate's probe rides along with the compression sizes (one readback)
             self._dedup_probe = {} if self.cfg.dedup == "auto" else None
-            pair_lr = {} if PAIR_LR_FROM_COMPRESS else None
             kept, roff, ranks, hist_t, bcnt = ops.compress_rows(shard.offsets, shard.items, lut, F1,
-                                                                probe=self._dedup_probe, layout=pair_lr)
+                                                                probe=self._dedup_probe)
             T = kept.numel()
             hist = hist_t.cpu().numpy()
         else:
@@ -675,11 +671,10 @@ class FastApriori:
                 torch.cumsum(cnt[kept.to(torch.int64)].to(torch.int64), 0, out=roff[1:])
             ranks = ops.compress(shard.offsets, shard.items, lut, kept, roff, F1)
             hist = ops.histogram(torch.clamp(cnt, max=255), 256).cpu().numpy() if cnt.numel() else np.zeros(256, np.int64)
-            bcnt = pair_lr = None
+            bcnt = None
         db = {"roff": roff, "ranks": ranks, "T": T, "src": None, "ncols": T, "wword": None, "wrow": None,
               "bm": None, "W": 0, "F1": F1, "alive": np.ones(F1, dtype=bool), "c1": self._counts1,
-              "bcnt": bcnt,      # 256-item block counts of these rows (pair layout); dropped on re-layout
-              "pair_lr": pair_lr}   # the pair layout's local-rank bytes (compress_rows layout=)
+              "bcnt": bcnt}      # 256-item block counts of these rows (pair layout); dropped on re-layout
         # row-length histogram (lengths >= 255 share the last bin): drives the pair
         # cost model, the trimming model and the u8 per-block count guard
         hist[:2] = 0                         # rows with < 2 frequent items are not kept
@@ -694,7 +689,7 @@ class FastApriori:
         db["pair_work_all"] = int(g[:, 3].sum())      # pair increments of every rank (bounds |F_2|)
         db["pair_pick"] = None
         if g[:, 1].max():
-            db["bcnt"] = db["pair_lr"] = None
+            db["bcnt"] = None
             self._dedup(db)
             db.pop("len_hist", None)
         else:
@@ -842,7 +837,7 @@ class FastApriori:
         K = kept.numel()
         if K > 0.9 * db["T"] and nranks.numel() > 0.9 * db["ranks"].numel():
             return   # not worth re-laying out
-        db.update(roff=nroff, ranks=nranks, T=K, bm=None, W=0, bcnt=None, pair_lr=None, bm_items=None, bm_map=None)
+        db.update(roff=nroff, ranks=nranks, T=K, bm=None, W=0, bcnt=None, bm_items=None, bm_map=None)
         db["alive"] = np.zeros_like(db["alive"])
         db["alive"][used] = True
         db["len_hist"] = hist.cpu().numpy()
@@ -933,8 +928,7 @@ class FastApriori:
                 roff, ranks = roff[a:b + 1] - ra, ranks[ra:rb]
                 wrow = wrow[a:b] if wrow is not None else None
             pc = ops.pair_counts_horizontal(roff, ranks, wrow, F1, db.get("long_rows", True),
-                                            bcnt=db.get("bcnt") if nr == 1 and wrow is None else None,
-                                            layout=db.get("pair_lr") if nr == 1 and wrow is None else None)
+                                            bcnt=db.get("bcnt") if nr == 1 and wrow is None else None)
         self._run_deferred()      # host-only work while the pair kernel runs
         key = (F1, pc.device)
         if key not in _TRIU_CACHE:

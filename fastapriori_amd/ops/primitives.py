@@ -240,8 +240,7 @@ PAIR_PAD_BATCHES = 3 * 16 + 2   # the pair kernel's pipeline reads up to this ma
 DEDUP_PROBE_ROWS = 1 << 18
 
 
-def compress_rows(offsets, items, lut, F1: int, block_counts: bool = True, probe: dict | None = None,
-                  layout: dict | None = None):
+def compress_rows(offsets, items, lut, F1: int, block_counts: bool = True, probe: dict | None = None):
     """Fused two-pass compression (device, short rows; csrc/hip/prep.hip k_cmp_agg /
     k_cmp_emit): returns (kept int32 [T], roff int64 [T+1], ranks int32 [nnz],
     length histogram int64 [256], bcnt) with one host synchronisation.  Rows of
@@ -254,23 +253,14 @@ def compress_rows(offsets, items, lut, F1: int, block_counts: bool = True, probe
 
     probe (a dict): also run the dedup probe (prep.hip k_dedup_probe) over the first
     min(T, DEDUP_PROBE_ROWS) rows, read back with the sizes: probe["n"] rows hashed,
-    probe["filled"] occupied slots of its 2^22-slot bitmap.
-
-    layout (a dict, with bcnt): the pair kernel's local-rank bytes are written by the
-    emit pass too (prep.hip kLrMaxWgTokens; replaces count.hip k_block_scatter_w):
-    layout["lr"] (uint8, or None when some workgroup could not write them) and
-    layout["lr_rows"] (the overflow rows, finished by pair_counts_horizontal)."""
+    probe["filled"] occupied slots of its 2^22-slot bitmap."""
     dev = items.device
     n = offsets.numel() - 1
     nwg = (n + 255) // 256
     st = _stream(items)
     agg = torch.empty(3 * max(nwg, 1), dtype=_I32, device=dev)
     hist = torch.zeros(64, 256, dtype=_I32, device=dev)
-    nb = (F1 + 255) // 256
-    want_bc = block_counts and 1 <= nb <= 8
-    want_lr = want_bc and layout is not None
-    blk = torch.empty(nb * max(nwg, 1), dtype=_I32, device=dev) if want_lr else None
-    _hip_call("fa_hip_cmp_agg", _p(offsets), _p(items), _p(lut), n, _p(agg), _p(hist), _p(blk), nb, st)
+    _hip_call("fa_hip_cmp_agg", _p(offsets), _p(items), _p(lut), n, _p(agg), _p(hist), st)
     pre = torch.zeros(3, nwg + 1, dtype=_I64, device=dev)
     a3 = agg.view(-1, 3).t().to(_I64).contiguous()
     for q in range(3):   # 1-D scans (the batched innermost-dim scan is ~20x slower here)
@@ -280,17 +270,12 @@ def compress_rows(offsets, items, lut, F1: int, block_counts: bool = True, probe
     roff[0] = 0
     ranks = torch.empty(max(items.numel(), 1), dtype=_I32, device=dev)
     over = torch.empty(max(n, 1), dtype=_I32, device=dev)
-    bcnt = lr = lrpre = None
-    flag = torch.zeros(1, dtype=_I64, device=dev)
-    if want_bc:
+    nb = (F1 + 255) // 256
+    bcnt = None
+    if block_counts and 1 <= nb <= 8:
         bcnt = torch.empty(nb * max(n, 1) + PAIR_PAD_BATCHES * 64 + 64, dtype=torch.uint8, device=dev)
-    if want_lr:
-        # block-major exclusive scan: workgroup w's block-b items start at lrpre[b * nwg + w]
-        lrpre = torch.zeros(nb * max(nwg, 1) + 1, dtype=_I64, device=dev)
-        torch.cumsum(blk, 0, out=lrpre[1:])
-        lr = torch.empty(max(items.numel(), 1) + 1024, dtype=torch.uint8, device=dev)   # nnz bound + staging pad
     _hip_call("fa_hip_cmp_emit", _p(offsets), _p(items), _p(lut), n, _p(pre[0]), _p(pre[1]), _p(pre[2]), _p(kept),
-              _p(roff), _p(ranks), _p(over), _p(bcnt), nb, _p(lrpre), _p(lr), _p(flag), st)
+              _p(roff), _p(ranks), _p(over), _p(bcnt), nb, st)
     if probe is not None:
         # the kernel reads T = pre[0, -1] on the device and hashes the rows the emit
         # pass has finished (<= 16 items; the later tiers write the longer ones)
@@ -298,18 +283,15 @@ def compress_rows(offsets, items, lut, F1: int, block_counts: bool = True, probe
         tail = torch.zeros(2, dtype=_I64, device=dev)
         _hip_call("fa_hip_dedup_probe", _p(roff), _p(ranks), pre[0].data_ptr() + 8 * (pre.shape[1] - 1),
                   DEDUP_PROBE_ROWS, _p(occ), _p(tail), st)
-        sizes = torch.cat([pre[:, -1], flag, tail]).cpu().tolist()
-        probe["filled"], probe["n"] = int(sizes[4]), int(sizes[5])
+        sizes = torch.cat([pre[:, -1], tail]).cpu().tolist()
+        probe["filled"], probe["n"] = int(sizes[3]), int(sizes[4])
     else:
-        sizes = torch.cat([pre[:, -1], flag]).cpu().tolist()
+        sizes = pre[:, -1].cpu().tolist()
     T, nnz, no = int(sizes[0]), int(sizes[1]), int(sizes[2])
     kept, roff, ranks = kept[:T], roff[:T + 1], ranks[:nnz]
     if bcnt is not None:
         bcnt = bcnt[:nb * T + PAIR_PAD_BATCHES * 64 + 64]
         bcnt[nb * T:].zero_()
-    if layout is not None:
-        layout["lr"] = lr if (lr is not None and not int(sizes[3])) else None
-        layout["lr_rows"] = over[:no]
     if no:
         over = over[:no]
         flag2 = torch.empty(no, dtype=torch.int8, device=dev)
@@ -406,8 +388,7 @@ def build_bitmaps(roff, ranks, src, ncols: int, F1: int, item_map=None, used=Non
     return bm[:F1], W
 
 
-def pair_counts_horizontal(roff, ranks, wrow, F1: int, long_rows: bool = True, bcnt=None,
-                           layout: dict | None = None) -> torch.Tensor:
+def pair_counts_horizontal(roff, ranks, wrow, F1: int, long_rows: bool = True, bcnt=None) -> torch.Tensor:
     """Pair supports from the compressed rows -> int64 [F1, F1] (upper triangle).
 
     Device path: per-row block counts + local-rank bytes (blocked layout), then
@@ -415,8 +396,7 @@ def pair_counts_horizontal(roff, ranks, wrow, F1: int, long_rows: bool = True, b
     tiles with row weights.  long_rows: some row may hold >= 256 items, which
     would overflow a u8 count of a 256-item block -> 128-item blocks.  bcnt: the
     256-item block counts of these rows from compression (compress_rows), which
-    replace the counting pass; layout: compress_rows' local-rank bytes of these rows
-    (with bcnt), which replace the scatter pass.
+    replace the counting pass.
     """
     T = roff.numel() - 1
     dev = ranks.device
@@ -432,12 +412,9 @@ def pair_counts_horizontal(roff, ranks, wrow, F1: int, long_rows: bool = True, b
             # values are never processed; padded bases must be valid lr offsets)
             pad_b = PAIR_PAD_BATCHES
             bsum = torch.empty(nb * nbatch, dtype=_I64, device=dev)
-            pre_lr = None
             if bcnt is not None and pb == 256 and bcnt.numel() >= nb * T + pad_b * 64:
                 cnt = bcnt
                 _hip_call("fa_hip_block_bsum", _p(cnt), T, T, nb, _p(bsum), st)
-                if layout is not None and layout.get("lr") is not None and layout["lr"].numel() >= ranks.numel() + 1024:
-                    pre_lr = layout
             else:
                 cnt = torch.empty(nb * T + pad_b * 64, dtype=torch.uint8, device=dev)
                 cnt[nb * T:].zero_()
@@ -446,16 +423,9 @@ def pair_counts_horizontal(roff, ranks, wrow, F1: int, long_rows: bool = True, b
             torch.cumsum(bsum, 0, out=base[:nb * nbatch])
             base[:nb * nbatch] -= bsum
             # every rank lands in exactly one block: the layout holds all of them (no readback)
-            if pre_lr is not None:
-                # written by the compression's emit pass; its overflow rows from their final ranks
-                lr = pre_lr["lr"]
-                rows = pre_lr["lr_rows"]
-                _hip_call("fa_hip_lr_rows", _p(roff), _p(ranks), _p(rows), rows.numel(), _p(cnt), T, _p(base),
-                          nbatch, _p(lr), st)
-            else:
-                total = int(ranks.numel())
-                lr = torch.empty(total + 1024, dtype=torch.uint8, device=dev)   # pad: aligned dword staging reads
-                _hip_call("fa_hip_block_scatter", _p(roff), _p(ranks), T, F1, _p(cnt), _p(base), _p(lr), pb, st)
+            total = int(ranks.numel())
+            lr = torch.empty(total + 1024, dtype=torch.uint8, device=dev)   # pad: aligned dword staging reads
+            _hip_call("fa_hip_block_scatter", _p(roff), _p(ranks), T, F1, _p(cnt), _p(base), _p(lr), pb, st)
             if pb == 256:
                 if os.environ.get("FA_PAIR_DEBUG") != "4":   # 4: layout kernels only (benchmarks/pair_probe.py)
                     # work-queue schedule: persistent workgroups keep their tile across

@@ -463,37 +463,6 @@ def test_pair_counts_with_compress_block_counts(long_rows):
     assert torch.equal(a.cpu(), b.cpu()) and int(a.sum()) > 0
 
 
-@pytest.mark.parametrize("n,V,max_len,long_rows,frac", [(90000, 900, 22, 0, 0.6), (70001, 1900, 40, 30, 0.9),
-                                                          (40000, 300, 70, 0, 1.0), (5000, 700, 12, 0, 0.3)])
-def test_pair_layout_written_by_compression(n, V, max_len, long_rows, frac):
-    # the local-rank bytes written by the emit pass (register rows, wave-sorted mid rows) and
-    # by fa_hip_lr_rows (overflow rows) == the scatter pass's layout, byte for byte
-    from fastapriori_amd.ops import primitives as P
-    off, items, lut, F1 = _prep(n=n, V=V, max_len=max_len, seed=n + 1, long_rows=long_rows, F1_frac=frac)
-    lay = {}
-    kept, roff, ranks, hist, bcnt = ops.compress_rows(off.to(DEV), items.to(DEV), lut.to(DEV), F1, layout=lay)
-    assert bcnt is not None and lay["lr"] is not None
-    T, nb = kept.numel(), (F1 + 255) // 256
-    nbatch = (T + 63) // 64
-    st = torch.cuda.current_stream().cuda_stream
-    bsum = torch.empty(nb * nbatch, dtype=torch.int64, device=DEV)
-    P._hip_call("fa_hip_block_bsum", P._p(bcnt), T, T, nb, P._p(bsum), st)
-    base = torch.zeros(nb * nbatch + P.PAIR_PAD_BATCHES, dtype=torch.int64, device=DEV)
-    torch.cumsum(bsum, 0, out=base[:nb * nbatch])
-    base[:nb * nbatch] -= bsum
-    rows = lay["lr_rows"]
-    P._hip_call("fa_hip_lr_rows", P._p(roff), P._p(ranks), P._p(rows), rows.numel(), P._p(bcnt), T, P._p(base),
-                nbatch, P._p(lay["lr"]), st)
-    ref = torch.empty(ranks.numel() + 1024, dtype=torch.uint8, device=DEV)
-    P._hip_call("fa_hip_block_scatter", P._p(roff), P._p(ranks), T, F1, P._p(bcnt), P._p(base), P._p(ref), 256, st)
-    nnz = ranks.numel()
-    assert torch.equal(lay["lr"][:nnz].cpu(), ref[:nnz].cpu())
-    if int(hist[255]) == 0:
-        a = ops.pair_counts_horizontal(roff, ranks, None, F1, long_rows=False, bcnt=bcnt, layout=lay)
-        b = ops.pair_counts_horizontal(roff, ranks, None, F1, long_rows=False)
-        assert torch.equal(a.cpu(), b.cpu())
-
-
 @pytest.mark.parametrize("k", [3, 4, 6])
 def test_apriori_gen_device_matches_host(k):
     # GPU bitset apriori-gen == host apriori-gen on real levels (and speculative candidate levels)
