@@ -12,6 +12,9 @@
 // out ascending from a popcount + DPP prefix scan over the lanes.
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+#include <cmath>
+
 #include "fa_hip.h"
 
 namespace fa {
@@ -923,9 +926,119 @@ FA_API int fa_hip_dl_level0(const int32_t* P0, const long long* n_src, int64_t n
 //   4 m_l (parent row length)  5 n_l  6 C_l  7 base (candidates of levels < l)
 // Returns 0 (ctl_host[1] = accepted levels incl. level 0), 5 (ws too small:
 // info[0] = bytes needed) or 7.
+//
+// post (optional, host DlPost): right after the synchronisation, with no return to
+// the host interpreter in between, the bundle's device piece plan is queued
+// (levels.hip fa_hip_dl_plan), the transaction-trimming decision is taken
+// (FastApriori._trim_worth_it, the same binomial estimate), and when no trim is
+// due the slab count itself is queued (count.hip fa_hip_count_slab_rec): the GPU
+// then counts while the host does its bookkeeping.  post->done: 0 nothing queued
+// (stopped chain, multi-pass level, buffers too small), 1 planned (the caller trims,
+// then counts), 2 planned and counted into post->out.
+struct DlPost {
+  // plan buffers (grow-only, the caller's): item_map int32 [F1], rec int4 [3 * rec_cap],
+  // part int32 [part_cap], out uint32 [out_cap]
+  int32_t* item_map; void* rec; int32_t* part; uint32_t* out;
+  int64_t rec_cap, part_cap, out_cap;
+  // the count's rows and LDS budget
+  const int64_t* roff; const int32_t* ranks; const int32_t* src; const int32_t* wword;
+  int64_t ncols; double lds_kernel; double lds_budget;
+  // trimming decision (trim_ok = 0: never): c1 int64 [F1] item supports, alive uint8 [F1],
+  // len_hist int64 [256] (nullptr: decided by the caller), T rows, nnz, min rows, level k
+  const int64_t* c1; const uint8_t* alive; const int64_t* len_hist;
+  int64_t T, nnz, trim_min_rows, trim_ok, k;
+  // out
+  int64_t done, sw, cap, n_wg, C, trim;
+};
+static_assert(sizeof(DlPost) == 28 * 8, "DlPost layout (ops.primitives.DlPostC)");
+
+FA_API int fa_hip_dl_plan(const int64_t* desc, int L, long long* ctl, int F1, int32_t* item_map, void* rec,
+                          int64_t max_pieces, int32_t* part, int64_t part_cap, hipStream_t st);
+FA_API int fa_hip_count_slab_rec(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
+                                 const int32_t* item_map, int F1, int n_used, const int32_t* gpre, const void* rec,
+                                 int G, int C, const int32_t* wword, uint32_t* out, int sw, int n_wg,
+                                 const uint64_t* bm, int64_t Wp, hipStream_t st, const int32_t* bm_rows,
+                                 const int32_t* g_dev);
+
+// P[Binom(L, p) >= k] (the regularised incomplete beta of FastApriori._trim_worth_it)
+static double binom_tail(int L, double p, int k) {
+  if (L < k) return 0.0;
+  if (p <= 0.0) return k <= 0 ? 1.0 : 0.0;
+  if (p >= 1.0) return 1.0;
+  double pmf = std::pow(1.0 - p, (double)L), below = 0.0;
+  const double r = p / (1.0 - p);
+  for (int i = 0; i < k; ++i) {
+    below += pmf;
+    pmf *= (double)(L - i) / (double)(i + 1) * r;
+  }
+  return std::min(1.0, std::max(0.0, 1.0 - below));
+}
+
+static void dl_post(DlPost* P, const int64_t* desc, int L, long long* ctl, const long long* ch, int F1,
+                    hipStream_t st) {
+  P->done = 0;
+  if (ch[0] && ch[1] == 0) return;                 // nothing accepted
+  if (ch[4] || ch[5] || ch[7] || L < 1) return;    // bound error, multi-pass level, end of mining
+  int64_t C = 0, R = 0;
+  for (int l = 0; l < L; ++l) { C += desc[8 * l + 6]; R += desc[8 * l + 5]; }
+  const int64_t n_used = ch[6];
+  P->C = C;
+  if (C < 1 || C > P->rec_cap || C > P->out_cap || 8 * ((R + 255) / 256) > P->part_cap) return;
+  // slab width: plan.cpp slab_width order, one accumulator pass
+  int sw = 0;
+  int64_t cap = 0;
+  for (int w : {16, 32, 8, 4}) {
+    cap = (int64_t)((P->lds_budget - (double)n_used * (w + 2) * 8) / 4);
+    if (cap >= std::min<int64_t>(C, 8192) || (w == 4 && cap >= 1024)) { sw = w; break; }
+  }
+  if (sw == 0 || C > cap) return;
+  if (fa_hip_dl_plan(desc, L, ctl, F1, P->item_map, P->rec, C, P->part, P->part_cap, st) != 0) return;
+  (void)hipMemsetAsync(P->out, 0, 4 * (size_t)C, st);
+  P->sw = sw;
+  P->cap = cap;
+  P->done = 1;
+  // trimming before level k: the rows that keep >= k of the bundle's items
+  P->trim = 0;
+  if (!P->trim_ok || P->T <= 0) {
+    // no trimming
+  } else if (!P->len_hist || P->T < P->trim_min_rows) {
+    if (!P->len_hist && P->T >= P->trim_min_rows) return;   // the caller decides (and counts)
+  } else {
+    const uint64_t* mk = reinterpret_cast<const uint64_t*>(ch + 128);
+    double num = 0.0, den = 0.0;
+    for (int r = 0; r < F1; ++r) {
+      if (P->alive[r]) den += (double)P->c1[r];
+      if ((mk[r >> 6] >> (r & 63)) & 1ull) num += (double)P->c1[r];
+    }
+    if (den > 0.0) {
+      const double p = num / den;
+      double est_rows = 0.0, est_nnz = 0.0;
+      for (int Lr = 0; Lr < 256; ++Lr) {
+        const double h = (double)P->len_hist[Lr];
+        if (h == 0.0) continue;
+        est_rows += h * binom_tail(Lr, p, (int)P->k);
+        est_nnz += h * Lr * p;
+      }
+      const double T = (double)std::max<int64_t>(P->T, 1), nnz = (double)std::max<int64_t>(P->nnz, 1);
+      P->trim = (est_rows < 0.75 * T || est_nnz < 0.6 * nnz) ? 1 : 0;
+    }
+  }
+  if (P->trim) return;                                      // the caller trims, then counts
+  const int64_t W = (P->ncols + 63) / 64, nslabs = (W + sw - 1) / sw;
+  const int64_t map_b = F1 <= 8192 ? (((int64_t)F1 * 2 + 15) & ~(int64_t)15) : 0;
+  const int64_t lds_k = n_used * (sw + 2) * 8 + ((C + 3) & ~(int64_t)3) * 4 + map_b;
+  const int64_t per_cu = std::min<int64_t>(std::max<int64_t>(1, (int64_t)P->lds_kernel / std::max<int64_t>(lds_k, 1)), 2);
+  P->n_wg = std::max<int64_t>(1, std::min<int64_t>(nslabs, 256 * per_cu));
+  if (fa_hip_count_slab_rec(P->roff, P->ranks, P->src, P->ncols, P->item_map, F1, (int)n_used, nullptr, P->rec, 0,
+                            (int)C, P->wword, P->out, sw, (int)P->n_wg, nullptr, 0, st, nullptr,
+                            reinterpret_cast<const int32_t*>(ctl + 221)) != 0)
+    return;
+  P->done = 2;
+}
+
 FA_API int fa_hip_dl_more(int F1, void* ws, int64_t ws_bytes, int64_t ws_used, long long* ctl, long long* ctl_host,
                           double growth, int max_levels, double lds, int64_t n1_bound, int64_t* desc, int64_t* info,
-                          hipStream_t st) {
+                          hipStream_t st, void* post) {
   using namespace fa;
   auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
   const int nw = (F1 + 63) / 64;
@@ -1036,5 +1149,6 @@ FA_API int fa_hip_dl_more(int F1, void* ws, int64_t ws_bytes, int64_t ws_used, l
     base += d[6];
   }
   info[0] = w - w0;
+  if (post) dl_post(static_cast<DlPost*>(post), desc, L, ctl, ctl_host, F1, st);
   FA_LAUNCH_RET();
 }

@@ -82,8 +82,12 @@ class _Deferred:
 # faster (A/B on MI355X: 48.1-48.9 vs 49.5 ms per run)
 BUNDLE_DFS = os.environ.get("FA_BUNDLE_DFS", "0") == "1"
 # k = 2 across ranks: triangles of at least this many pairs are reduce-scattered and
-# thresholded per slice (Comm.reduce_scatter_select) instead of all-reduced
-PAIR_RS_MIN = int(os.environ.get("FA_PAIR_RS_MIN", str(1 << 15)))
+# thresholded per slice (Comm.reduce_scatter_select) instead of all-reduced.  Below it
+# the triangle is all-reduced and F_2 compacted on the device with no host round trip
+# (_pairs_on_device): for the T10I4 triangle (474K pairs, 1.9 MB) one ring all-reduce
+# over xGMI costs less than the reduce-scatter's three collectives and two host syncs.
+# 4M pairs (F1 ~ 2900, 16 MB) is where the all-reduce's 2(W-1)/W volume starts to dominate.
+PAIR_RS_MIN = int(os.environ.get("FA_PAIR_RS_MIN", str(1 << 22)))
 # depth-2 reuse pays where prefixes are long; on short prefixes (k = 3: two items) the
 # lanes' uneven child loops cost more than the saved reads (T10I4D100M: bundle 3-4
 # 17.7 -> 21.0 ms with it, bundle 5-12 16.2 -> 14.6 ms)
@@ -100,6 +104,9 @@ DFS_PAIR_MIN_M = int(os.environ.get("FA_DFS_PAIR_MIN_M", "4"))
 # level bundles generated, planned, counted and thresholded on the GPU with no host
 # round trip per bundle beyond the generator's acceptance readbacks (_mine_device)
 DEVICE_LEVELS = os.environ.get("FA_DEVICE_LEVELS", "1") == "1"
+# the bundle's plan, trimming decision and slab count queued by the generator's native
+# call right after its synchronisation (gen.hip DlPost), not after a return to Python
+DL_POST = os.environ.get("FA_DL_POST", "1") == "1"
 BUNDLE_MAX_PREFIX = int(os.environ.get("FA_BUNDLE_MAX_PREFIX", "9"))
 
 
@@ -357,9 +364,12 @@ class FastApriori:
                     max_lv = min(max_lv, self.cfg.max_level - k + 1)
                 if not BUNDLE_LEVELS or k - 1 > BUNDLE_MAX_PREFIX:
                     max_lv = 1
+                post = DL_POST and max_lv > 1
+                if post:
+                    self._dl_post_setup(S, db, k, F1, c_bound, n_bound, lds)
                 with roctx_range("gen"):
                     c = Pm.dl_bundle_gen(S, P0, n_src, n_const, n_bound, m0, F1, c_bound, lds, BUNDLE_GROWTH, max_lv,
-                                         st)
+                                         st, post=post)
                 if c[4]:
                     raise RuntimeError(f"device bundle at level {k}: |F_{k - 1}| exceeds its bound {n_bound}")
                 if c[7]:
@@ -368,16 +378,25 @@ class FastApriori:
                     nxt = k                             # several accumulator passes: host path
                     break
                 L, n_used = int(c[1]), int(c[6])
-                bits = np.unpackbits(c[128:192].view(np.uint8), bitorder="little")[:F1]
-                used = np.flatnonzero(bits)
                 Cs = S.desc[:L, 6].copy()
                 C = int(Cs.sum())
-                with roctx_range("plan"):
-                    plan = Pm.dl_plan(S, L, F1, n_used, C, lds, self._dev)
-                with tm.phase(f"trim{k}"), roctx_range("trim"):
-                    self._trim(db, used, k, C)
+                done = int(S.post.done) if post else 0
+                if done == 2:
+                    # planned and counted by fa_hip_dl_more's post step (no trim due)
+                    cnt = S.post_bufs["out"][:C]
+                else:
+                    bits = np.unpackbits(c[128:192].view(np.uint8), bitorder="little")[:F1]
+                    used = np.flatnonzero(bits)
+                    if done == 1:
+                        plan = Pm.dl_plan_from_post(S, n_used)
+                    else:
+                        with roctx_range("plan"):
+                            plan = Pm.dl_plan(S, L, F1, n_used, C, lds, self._dev)
+                    with tm.phase(f"trim{k}"), roctx_range("trim"):
+                        self._trim(db, used, k, C, decided=bool(done == 1 and S.post.trim))
+                    with tm.phase("count"), roctx_range("count"):
+                        cnt = Pm.dl_count(S, plan, db["roff"], db["ranks"], db["src"], db["ncols"], F1, db["wword"])
                 with tm.phase("count"), roctx_range("count"):
-                    cnt = Pm.dl_count(S, plan, db["roff"], db["ranks"], db["src"], db["ncols"], F1, db["wword"])
                     self.comm.all_reduce_(cnt)
                     rows_a, cnt_a, ro, co = Pm.dl_threshold(S, L, cnt, mc, k)
             pend.append(dict(k=k, L=L, m0=m0, C=Cs, rows=rows_a, cnt=cnt_a, ro=ro, co=co,
@@ -390,6 +409,29 @@ class FastApriori:
         self._dl_flush(S, pend, levels, counts, result)
         self.stats["device_bundles"] = len(pend)
         return nxt
+
+    def _dl_post_setup(self, S, db, k: int, F1: int, c_bound: int, n_bound: int, lds: int) -> None:
+        """Fill the post step of fa_hip_dl_more (ops.primitives.DlPostC): buffers, the
+        current rows and the trimming inputs of level k (FastApriori._trim_worth_it)."""
+        Pm = ops.primitives
+        b = S.post_buffers(F1, c_bound, n_bound + c_bound)
+        P = S.post
+        P.item_map, P.rec, P.part, P.out = (b["item_map"].data_ptr(), b["rec"].data_ptr(), b["part"].data_ptr(),
+                                            b["out"].data_ptr())
+        P.rec_cap, P.part_cap, P.out_cap = b["c_cap"], b["part"].numel(), b["c_cap"]
+        P.roff, P.ranks = db["roff"].data_ptr(), db["ranks"].data_ptr()
+        P.src = db["src"].data_ptr() if db["src"] is not None else None
+        P.wword = db["wword"].data_ptr() if db["wword"] is not None else None
+        P.ncols, P.lds_kernel, P.lds_budget = int(db["ncols"]), float(Pm._LDS_BYTES), float(lds)
+        c1 = np.ascontiguousarray(db["c1"], dtype=np.int64)
+        alive = np.ascontiguousarray(db["alive"], dtype=np.uint8)
+        hist = db.get("len_hist")
+        hist = np.ascontiguousarray(hist, dtype=np.int64) if hist is not None and hist.size == 256 else None
+        S.post_keep = (c1, alive, hist)                # alive while the native call reads them
+        P.c1, P.alive = c1.ctypes.data, alive.ctypes.data
+        P.len_hist = hist.ctypes.data if hist is not None else None
+        P.T, P.nnz = int(db["T"]), int(db["ranks"].numel())
+        P.trim_min_rows, P.trim_ok, P.k = int(self.cfg.trim_min_rows), int(bool(self.cfg.trim) and db["T"] > 0), k
 
     def _dl_flush(self, S, pend: list, levels: list, counts: list, result: MiningResult) -> None:
         """Every device level to the host (the run's one results readback); F_2 too when
@@ -822,13 +864,14 @@ class FastApriori:
         lens = db["roff"][1:] - db["roff"][:-1]
         return torch.bincount(lens).cpu().numpy() if lens.numel() else np.zeros(1, np.int64)
 
-    def _trim(self, db, used: np.ndarray, k: int, C: int = 0) -> None:
-        """Transaction trimming before level k (items outside C_k, rows with < k of them)."""
+    def _trim(self, db, used: np.ndarray, k: int, C: int = 0, decided: bool = False) -> None:
+        """Transaction trimming before level k (items outside C_k, rows with < k of them).
+        decided: the estimate already said yes (fa_hip_dl_more's post step)."""
         if not self.cfg.trim or db["T"] == 0:
             return
         if "len_hist" not in db:
             db["len_hist"] = self._len_hist(db)
-        if not self._trim_worth_it(db, used, k, C):
+        if not decided and not self._trim_worth_it(db, used, k, C):
             return
         dev = db["ranks"].device
         alive = torch.zeros(db["F1"], dtype=torch.int8)

@@ -88,7 +88,7 @@ _HIP_SIGS = {
                                         C.c_int, C.c_int, vp, i64, vp, vp, vp]),
     # device-resident level bundles (gen.hip fa_hip_dl_*, levels.hip)
     "fa_hip_dl_level0": (C.c_int, [vp, vp, i64, i64, C.c_int, C.c_int, vp, i64, vp, vp, i64, dbl, vp, C.c_int, vp]),
-    "fa_hip_dl_more": (C.c_int, [C.c_int, vp, i64, i64, vp, vp, dbl, C.c_int, dbl, i64, vp, vp, vp]),
+    "fa_hip_dl_more": (C.c_int, [C.c_int, vp, i64, i64, vp, vp, dbl, C.c_int, dbl, i64, vp, vp, vp, vp]),
     "fa_hip_dl_plan": (C.c_int, [vp, C.c_int, vp, C.c_int, vp, vp, i64, vp, i64, vp]),
     "fa_hip_dl_threshold": (C.c_int, [vp, C.c_int, vp, i64, vp, vp, vp, vp, vp, vp]),
     "fa_hip_trim_scan_count": (C.c_int, [vp, vp, i64, vp, C.c_int, C.c_int, vp, vp, vp, vp, vp]),

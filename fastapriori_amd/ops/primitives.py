@@ -13,6 +13,7 @@ Conventions: bitmaps are int64 tensors [F1, Wp] holding raw 64-bit words
 from __future__ import annotations
 
 import ctypes as C
+import ctypes
 import os
 
 import numpy as np
@@ -1564,10 +1565,23 @@ DL_MAX_M = 12           # prefix ids inline in the 48-B piece records
 DL_MAX_LEVELS = 31
 
 
+class DlPostC(ctypes.Structure):
+    """gen.hip DlPost: what fa_hip_dl_more queues right after its synchronisation
+    (device plan, trimming decision, slab count) without returning to Python first."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("item_map", "rec", "part", "out")] + \
+               [(n, ctypes.c_int64) for n in ("rec_cap", "part_cap", "out_cap")] + \
+               [(n, ctypes.c_void_p) for n in ("roff", "ranks", "src", "wword")] + \
+               [("ncols", ctypes.c_int64), ("lds_kernel", ctypes.c_double), ("lds_budget", ctypes.c_double)] + \
+               [(n, ctypes.c_void_p) for n in ("c1", "alive", "len_hist")] + \
+               [(n, ctypes.c_int64) for n in ("T", "nnz", "trim_min_rows", "trim_ok", "k",
+                                               "done", "sw", "cap", "n_wg", "C", "trim")]
+
+
 class DeviceLevelState:
     """Per-device buffers of the device bundle loop, reused across mining runs:
-    the generator workspace, the control block (+ its pinned host mirror) and the
-    per-level F sizes (fsz[k] = |F_k| on the device)."""
+    the generator workspace, the control block (+ its pinned host mirror), the
+    per-level F sizes (fsz[k] = |F_k| on the device) and the post-step's plan and
+    count buffers (DlPostC; sized for one accumulator pass)."""
 
     def __init__(self, dev):
         self.dev = dev
@@ -1577,9 +1591,27 @@ class DeviceLevelState:
         self.fsz = torch.zeros(128, dtype=_I64, device=dev)
         self.desc = np.zeros((32, 8), dtype=np.int64)
         self.info = np.zeros(4, dtype=np.int64)
+        self.post = DlPostC()
+        self.post_bufs = None
+        self.post_keep = ()
 
     def grow(self, nbytes: int) -> None:
         self.ws = torch.empty(int(nbytes * 1.25) + (1 << 20), dtype=torch.uint8, device=self.dev)
+
+    def post_buffers(self, F1: int, c_cap: int, rows_cap: int):
+        """Grow-only plan / count buffers of the post step: item_map [F1], piece
+        records [c_cap], planner scratch for rows_cap parent rows, counts [c_cap]."""
+        part_n = 8 * ((rows_cap + 255) // 256 + 2)
+        b = self.post_bufs
+        if b is None or b["F1"] < F1 or b["c_cap"] < c_cap or b["part"].numel() < part_n:
+            F1, c_cap = max(F1, b["F1"] if b else 0), max(c_cap, b["c_cap"] if b else 0)
+            part_n = max(part_n, b["part"].numel() if b else 0)
+            b = self.post_bufs = dict(F1=F1, c_cap=c_cap,
+                                      item_map=torch.empty(max(F1, 1), dtype=_I32, device=self.dev),
+                                      rec=torch.empty(12 * c_cap + 12, dtype=_I32, device=self.dev),
+                                      part=torch.empty(part_n, dtype=_I32, device=self.dev),
+                                      out=torch.empty(c_cap, dtype=_I32, device=self.dev))
+        return b
 
 
 _DL_STATE: dict = {}
@@ -1608,7 +1640,7 @@ def dl_slab_width(n_used: int, C: int, lds: int) -> tuple[int, int]:
 
 
 def dl_bundle_gen(S: DeviceLevelState, P0: int, n_src: int | None, n_const: int, n_bound: int, m0: int, F1: int,
-                  c_bound: int, lds: int, growth: float, max_levels: int, stream: int) -> np.ndarray:
+                  c_bound: int, lds: int, growth: float, max_levels: int, stream: int, post: bool = False) -> np.ndarray:
     """Candidates of a device bundle: level 0 from F_{k-1} rows P0 and the speculative
     levels 1 .. max_levels-1 (accepted on the device), all queued before ONE
     synchronisation.  Returns the control block (host int64 [DL_CTL]); S.desc[:L]
@@ -1628,9 +1660,10 @@ def dl_bundle_gen(S: DeviceLevelState, P0: int, n_src: int | None, n_const: int,
             c = S.ctl_h.numpy()
             S.desc[0, 5:8] = [c[8], c[40], 0]
             return c.copy()
+        S.post.done = 0
         rc = lib.fa_hip_dl_more(F1, _p(S.ws), S.ws.numel(), int(S.info[0]), _p(S.ctl), _p(S.ctl_h), float(growth),
                                 int(max_levels), float(lds), int(c_bound), S.desc.ctypes.data, info.ctypes.data,
-                                stream)
+                                stream, ctypes.addressof(S.post) if post else None)
         if rc == 5:
             S.grow(int(info[0]))
             continue
@@ -1656,6 +1689,14 @@ def dl_plan(S: DeviceLevelState, L: int, F1: int, n_used: int, C: int, lds: int,
                                                _p(part), part.numel(), st), "fa_hip_dl_plan")
     out = torch.zeros(C, dtype=_I32, device=dev)
     return dict(sw=sw, cap=cap, item_map=item_map, rec=rec, out=out, n_used=n_used, C=C)
+
+
+def dl_plan_from_post(S: DeviceLevelState, n_used: int) -> dict:
+    """The plan the post step queued (S.post.done >= 1), in dl_plan's form."""
+    P, b = S.post, S.post_bufs
+    C = int(P.C)
+    out = b["out"][:C]
+    return dict(sw=int(P.sw), cap=int(P.cap), item_map=b["item_map"], rec=b["rec"], out=out, n_used=n_used, C=C)
 
 
 def dl_count(S: DeviceLevelState, plan: dict, roff, ranks, src, ncols: int, F1: int, wword) -> torch.Tensor:
