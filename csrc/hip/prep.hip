@@ -377,7 +377,8 @@ constexpr int kCwMaxWords = 16;   // words per lane -> F1 <= 16 * 64 * 64
 __global__ __launch_bounds__(256) void k_compress_wave(
     const int64_t* __restrict__ off, const int32_t* __restrict__ items, const int32_t* __restrict__ lut,
     const int32_t* __restrict__ rows, int64_t nrows, const int32_t* __restrict__ kept,
-    const int64_t* __restrict__ roff, int32_t* __restrict__ ranks, int M) {
+    const int64_t* __restrict__ roff, int32_t* __restrict__ ranks, int M, const int8_t* __restrict__ flags) {
+  // flags (optional): only rows i with flags[i] != 0 (the rows an earlier tier left)
   __shared__ unsigned long long bm[4][kCwMaxWords * 64];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   unsigned long long* b = bm[w];
@@ -385,6 +386,7 @@ __global__ __launch_bounds__(256) void k_compress_wave(
   wave_lds_sync();
   const int64_t nw = (int64_t)gridDim.x * 4;
   for (int64_t i = (int64_t)blockIdx.x * 4 + w; i < nrows; i += nw) {
+    if (flags && !flags[i]) continue;             // wave-uniform: one row per wave
     const int32_t x = rows ? rows[i] : (int32_t)i;
     const int64_t t = kept[x];
     const int64_t s = off[t], L = off[t + 1] - s;
@@ -1003,9 +1005,10 @@ __global__ __launch_bounds__(256) void k_cmp_emit(const int64_t* __restrict__ of
 __global__ __launch_bounds__(256) void k_block_counts_rows(const int64_t* __restrict__ roff,
                                                            const int32_t* __restrict__ ranks,
                                                            const int32_t* __restrict__ rows, int64_t nrows,
-                                                           uint8_t* __restrict__ bcnt, int64_t bld, int nb) {
+                                                           uint8_t* __restrict__ bcnt, int64_t bld, int nb,
+                                                           const int8_t* __restrict__ flags) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nrows) return;
+  if (i >= nrows || (flags && !flags[i])) return;
   const int64_t x = rows[i];
   int c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int64_t k = roff[x], e = roff[x + 1]; k < e; ++k) {
@@ -1057,11 +1060,11 @@ __global__ __launch_bounds__(256) void k_block_bsum(const uint8_t* __restrict__ 
 using namespace fa;
 
 FA_API int fa_hip_block_counts_rows(const int64_t* roff, const int32_t* ranks, const int32_t* rows, int64_t nrows,
-                                    uint8_t* bcnt, int64_t bld, int nb, hipStream_t st) {
+                                    uint8_t* bcnt, int64_t bld, int nb, const int8_t* flags, hipStream_t st) {
   if (nrows <= 0) return 0;
   if (nb > 8) return 1;
   hipLaunchKernelGGL(k_block_counts_rows, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, st, roff, ranks, rows,
-                     nrows, bcnt, bld, nb);
+                     nrows, bcnt, bld, nb, flags);
   FA_LAUNCH_RET();
 }
 
@@ -1212,15 +1215,16 @@ FA_API int fa_hip_compress_lds(const int64_t* off, const int32_t* items, const i
 }
 
 // rows == nullptr: kept rows 0..nrows-1.  Requires F1 <= 65536.
+// flags (optional): int8 [nrows], only rows with a non-zero flag are compressed
 FA_API int fa_hip_compress_wave(const int64_t* off, const int32_t* items, const int32_t* lut, const int32_t* rows,
                                 int64_t nrows, const int32_t* kept, const int64_t* roff, int32_t* ranks, int F1,
-                                hipStream_t st) {
+                                const int8_t* flags, hipStream_t st) {
   if (nrows <= 0) return 0;
   const int M = (F1 + 4095) / 4096;
   if (M > kCwMaxWords) return 1;
   const int64_t g = std::min<int64_t>((nrows + 3) / 4, 8192);
   hipLaunchKernelGGL(k_compress_wave, dim3((unsigned)g), dim3(256), 0, st, off, items, lut, rows, nrows, kept, roff,
-                     ranks, std::max(M, 1));
+                     ranks, std::max(M, 1), flags);
   FA_LAUNCH_RET();
 }
 

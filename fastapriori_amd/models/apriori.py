@@ -702,7 +702,7 @@ class FastApriori:
             kept, roff, ranks, hist_t, bcnt = ops.compress_rows(shard.offsets, shard.items, lut, F1,
                                                                 probe=self._dedup_probe)
             T = kept.numel()
-            hist = hist_t.cpu().numpy()
+            hist = np.asarray(hist_t, dtype=np.int64).copy()
         else:
             self._dedup_probe = None
             cnt = ops.txn_freq_count(shard.offsets, shard.items, lut)

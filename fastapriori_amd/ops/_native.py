@@ -76,7 +76,7 @@ _HIP_SIGS = {
     "fa_hip_cmp_agg": (C.c_int, [vp, vp, vp, i64, vp, vp, vp]),
     "fa_hip_cmp_emit": (C.c_int, [vp, vp, vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, C.c_int, vp]),
     "fa_hip_compress_regs_bc": (C.c_int, [vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, i64, C.c_int, vp]),
-    "fa_hip_block_counts_rows": (C.c_int, [vp, vp, vp, i64, vp, i64, C.c_int, vp]),
+    "fa_hip_block_counts_rows": (C.c_int, [vp, vp, vp, i64, vp, i64, C.c_int, vp, vp]),
     "fa_hip_block_bsum": (C.c_int, [vp, i64, i64, C.c_int, vp, vp]),
     "fa_hip_compress_staged": (C.c_int, [vp, vp, vp, i64, vp, vp, vp, vp, vp]),
     "fa_hip_compress_staged64": (C.c_int, [vp, vp, vp, i64, vp, vp, vp, vp, vp]),
@@ -93,7 +93,7 @@ _HIP_SIGS = {
     "fa_hip_dl_threshold": (C.c_int, [vp, C.c_int, vp, i64, vp, vp, vp, vp, vp, vp]),
     "fa_hip_trim_scan_count": (C.c_int, [vp, vp, i64, vp, C.c_int, C.c_int, vp, vp, vp, vp, vp]),
     "fa_hip_trim_emit": (C.c_int, [vp, vp, vp, C.c_int, i64, vp, vp, vp, vp, vp, vp, vp, vp]),
-    "fa_hip_compress_wave": (C.c_int, [vp, vp, vp, vp, i64, vp, vp, vp, C.c_int, vp]),
+    "fa_hip_compress_wave": (C.c_int, [vp, vp, vp, vp, i64, vp, vp, vp, C.c_int, vp, vp]),
     "fa_hip_compress_lds": (C.c_int, [vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp]),
     "fa_hip_dedup_probe": (C.c_int, [vp, vp, vp, i64, vp, vp, vp]),
     "fa_hip_row_hash": (C.c_int, [vp, vp, i64, vp, vp, vp]),

@@ -201,7 +201,7 @@ def compress(offsets, items, lut, kept, roff, F1: int | None = None) -> torch.Te
     wave_ok = F1 is not None and F1 <= COMPRESS_WAVE_MAX_F1
     if wave_ok and items.numel() > COMPRESS_WAVE_MEAN_LEN * max(offsets.numel() - 1, 1):
         _hip_call("fa_hip_compress_wave", _p(offsets), _p(items), _p(lut), None, T, _p(kept), _p(roff),
-                  _p(ranks), F1, st)
+                  _p(ranks), F1, None, st)
         return ranks[:nnz]
     flag = torch.empty(T, dtype=torch.int8, device=items.device)
     # long-ish rows (mean > COMPRESS_STAGED64_MEAN_LEN tokens): the 64-token staged tier first
@@ -220,7 +220,7 @@ def compress(offsets, items, lut, kept, roff, F1: int | None = None) -> torch.Te
     if n2:
         if wave_ok:
             _hip_call("fa_hip_compress_wave", _p(offsets), _p(items), _p(lut), _p(over2), n2, _p(kept), _p(roff),
-                      _p(ranks), F1, st)
+                      _p(ranks), F1, None, st)
         else:
             over3 = torch.empty(n2, dtype=_I32, device=items.device)
             n_over3 = torch.zeros(1, dtype=_I32, device=items.device)
@@ -244,8 +244,9 @@ DEDUP_PROBE_ROWS = 1 << 18
 def compress_rows(offsets, items, lut, F1: int, block_counts: bool = True, probe: dict | None = None):
     """Fused two-pass compression (device, short rows; csrc/hip/prep.hip k_cmp_agg /
     k_cmp_emit): returns (kept int32 [T], roff int64 [T+1], ranks int32 [nnz],
-    length histogram int64 [256], bcnt) with one host synchronisation.  Rows of
-    more than 16 tokens are finished by the register / wave tiers of ``compress``.
+    length histogram (host int64 [256]), bcnt) with one host synchronisation.  Rows
+    of more than 16 tokens are finished by the register / wave tiers of ``compress``
+    (the rows the register tier leaves go to the wave tier by flag, no compaction).
 
     bcnt (block_counts and F1 <= 2048, else None): uint8 [nb * T + pad], the
     per-row item counts of 256-rank blocks that the pair kernel's blocked layout
@@ -284,11 +285,16 @@ def compress_rows(offsets, items, lut, F1: int, block_counts: bool = True, probe
         tail = torch.zeros(2, dtype=_I64, device=dev)
         _hip_call("fa_hip_dedup_probe", _p(roff), _p(ranks), pre[0].data_ptr() + 8 * (pre.shape[1] - 1),
                   DEDUP_PROBE_ROWS, _p(occ), _p(tail), st)
-        sizes = torch.cat([pre[:, -1], tail]).cpu().tolist()
-        probe["filled"], probe["n"] = int(sizes[3]), int(sizes[4])
+    # one readback: sizes, the probe's two counts, the row-length histogram
+    hs = hist.sum(0, dtype=_I64)
+    if probe is not None:
+        got = torch.cat([pre[:, -1], tail, hs]).cpu().numpy()
+        probe["filled"], probe["n"] = int(got[3]), int(got[4])
+        hist_h = got[5:]
     else:
-        sizes = pre[:, -1].cpu().tolist()
-    T, nnz, no = int(sizes[0]), int(sizes[1]), int(sizes[2])
+        got = torch.cat([pre[:, -1], hs]).cpu().numpy()
+        hist_h = got[3:]
+    T, nnz, no = int(got[0]), int(got[1]), int(got[2])
     kept, roff, ranks = kept[:T], roff[:T + 1], ranks[:nnz]
     if bcnt is not None:
         bcnt = bcnt[:nb * T + PAIR_PAD_BATCHES * 64 + 64]
@@ -302,12 +308,18 @@ def compress_rows(offsets, items, lut, F1: int, block_counts: bool = True, probe
         else:
             _hip_call("fa_hip_compress_regs", 64, _p(offsets), _p(items), _p(lut), _p(over), no, _p(kept), _p(roff),
                       _p(ranks), _p(flag2), st)
+        if F1 <= COMPRESS_WAVE_MAX_F1:
+            # rows of > 64 tokens (flag2) through the wave tier and the block counts, by
+            # flag: no compaction, no host synchronisation
+            _hip_call("fa_hip_compress_wave", _p(offsets), _p(items), _p(lut), _p(over), no, _p(kept), _p(roff),
+                      _p(ranks), F1, _p(flag2), st)
+            if bcnt is not None:
+                _hip_call("fa_hip_block_counts_rows", _p(roff), _p(ranks), _p(over), no, _p(bcnt), T, nb, _p(flag2),
+                          st)
+            return kept, roff, ranks, hist_h, bcnt
         over2 = over[torch.nonzero(flag2).flatten()].contiguous()
         n2 = over2.numel()
-        if n2 and F1 <= COMPRESS_WAVE_MAX_F1:
-            _hip_call("fa_hip_compress_wave", _p(offsets), _p(items), _p(lut), _p(over2), n2, _p(kept), _p(roff),
-                      _p(ranks), F1, st)
-        elif n2:
+        if n2:
             over3 = torch.empty(n2, dtype=_I32, device=dev)
             n_over3 = torch.zeros(1, dtype=_I32, device=dev)
             _hip_call("fa_hip_compress_lds", _p(offsets), _p(items), _p(lut), _p(over2), n2, _p(kept), _p(roff),
@@ -316,8 +328,8 @@ def compress_rows(offsets, items, lut, F1: int, block_counts: bool = True, probe
             if n3:
                 _compress_torch(offsets, items, lut, kept, roff, ranks, over3[:n3])
         if bcnt is not None and n2:       # rows of > 64 tokens, finished by the later tiers
-            _hip_call("fa_hip_block_counts_rows", _p(roff), _p(ranks), _p(over2), n2, _p(bcnt), T, nb, st)
-    return kept, roff, ranks, hist.sum(0, dtype=_I64), bcnt
+            _hip_call("fa_hip_block_counts_rows", _p(roff), _p(ranks), _p(over2), n2, _p(bcnt), T, nb, None, st)
+    return kept, roff, ranks, hist_h, bcnt
 
 
 def _compress_torch(offsets, items, lut, kept, roff, ranks, rows):
