@@ -350,6 +350,7 @@ class FastApriori:
         pend = []
         tm = self._timer
         nxt = None
+        self._dl_staged = None
         while True:
             if self.cfg.max_level and k > self.cfg.max_level:
                 break
@@ -367,12 +368,16 @@ class FastApriori:
                 post = DL_POST and max_lv > 1
                 if post:
                     self._dl_post_setup(S, db, k, F1, c_bound, n_bound, lds)
+                # the results so far, copied to the host ahead of this bundle's synchronisation:
+                # when the generator finds the mining over, _dl_flush needs no further round trip
+                staged = self._dl_stage(S, pend) if pend else None
                 with roctx_range("gen"):
                     c = Pm.dl_bundle_gen(S, P0, n_src, n_const, n_bound, m0, F1, c_bound, lds, BUNDLE_GROWTH, max_lv,
                                          st, post=post)
                 if c[4]:
                     raise RuntimeError(f"device bundle at level {k}: |F_{k - 1}| exceeds its bound {n_bound}")
                 if c[7]:
+                    self._dl_staged = staged
                     break                               # |F_{k-1}| < k or no candidates: done
                 if c[5]:
                     nxt = k                             # several accumulator passes: host path
@@ -433,19 +438,34 @@ class FastApriori:
         P.T, P.nnz = int(db["T"]), int(db["ranks"].numel())
         P.trim_min_rows, P.trim_ok, P.k = int(self.cfg.trim_min_rows), int(bool(self.cfg.trim) and db["T"] > 0), k
 
-    def _dl_flush(self, S, pend: list, levels: list, counts: list, result: MiningResult) -> None:
-        """Every device level to the host (the run's one results readback); F_2 too when
-        it stayed on the device (_pairs with _f2_defer)."""
+    def _dl_parts(self, S, pend: list) -> list:
         f2 = []
         if self._f2_n_dev is not None:
             nb = self._f2_bound
             f2 = [self._f2_n_dev.view(torch.int32), self._f2_dev[:nb].reshape(-1), self._f2_cnt_dev[:nb]]
+        return f2 + [S.fsz.view(torch.int32)] + [p["rows"] for p in pend] + [p["cnt"] for p in pend]
+
+    def _dl_stage(self, S, pend: list):
+        """Queue the D2H copy of the results so far into a pinned buffer (no wait)."""
+        blob = torch.cat(self._dl_parts(S, pend))
+        host = ops.primitives.pinned_stage("dl_results").get(4 * blob.numel()).view(torch.int32)
+        host.copy_(blob, non_blocking=True)
+        return len(pend), host
+
+    def _dl_flush(self, S, pend: list, levels: list, counts: list, result: MiningResult) -> None:
+        """Every device level to the host (the run's one results readback); F_2 too when
+        it stayed on the device (_pairs with _f2_defer).  When the last bundle's
+        synchronisation already covered a copy of all of them (_dl_stage), that copy."""
+        f2 = self._f2_n_dev is not None
         if not pend and not f2:
             return
         # one readback: F sizes (int64 as int32 pairs), every bundle's rows, then counts
         nrow = sum(int(p["rows"].numel()) for p in pend)
-        blob = torch.cat(f2 + [S.fsz.view(torch.int32)] + [p["rows"] for p in pend] + [p["cnt"] for p in pend])
-        blob = blob.cpu().numpy()
+        staged, self._dl_staged = self._dl_staged, None
+        if staged is not None and staged[0] == len(pend):
+            blob = staged[1].numpy().copy()               # complete: the generator's sync waited for it
+        else:
+            blob = torch.cat(self._dl_parts(S, pend)).cpu().numpy()
         if f2:
             nb = self._f2_bound
             n2 = int(blob[:2].view(np.int64)[0])
