@@ -120,3 +120,8 @@ def test_rccl_code_paths_match_single_process(strategy):
     got = spawn_local(_rccl_rank, 1, 60000, 0.004, strategy, env={"FA_FORCE_PG": "1", "FA_PAIR_RS_MIN": "0"})[0]
     assert got[0] == ref[0] and got[1] == ref[1] and got[2] == ref[2] and got[3] == ref[3]
     assert got[4] == 1.5 and got[5] > 0 and ref[5] == 0
+    if strategy == "count":
+        # default threshold: the triangle is all-reduced on RCCL and F_2 compacted on the device
+        # (no host round trip before the first device bundle)
+        got = spawn_local(_rccl_rank, 1, 60000, 0.004, strategy, env={"FA_FORCE_PG": "1"})[0]
+        assert got[0] == ref[0] and got[1] == ref[1] and got[2] == ref[2] and got[3] == ref[3]
