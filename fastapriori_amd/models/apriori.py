@@ -590,6 +590,24 @@ class FastApriori:
                 if shard.extras.size:
                     hist += torch.bincount(torch.from_numpy(shard.extras.astype(np.int64)), minlength=V).to(dev)
                 comm.all_reduce_(hist)
+                if V <= F1_HIST_READBACK and dev.type == "cuda":
+                    # narrow vocabulary: the whole histogram in one readback (no nonzero sync),
+                    # ranked and mapped to the LUT in one native call (csrc/host/f1.cpp)
+                    hh = np.ascontiguousarray(hist.cpu().numpy(), dtype=np.int64)
+                    Vh = max(V, 1)
+                    st = ops.primitives.pinned_stage("f1_lut")
+                    buf = st.get(4 * Vh)
+                    ids = np.empty(Vh, np.int64)
+                    cnt = np.empty(Vh, np.int64)
+                    F = int(ops._native.host().fa_f1_rank_numeric(hh.ctypes.data, V, thr, ids.ctypes.data,
+                                                                   cnt.ctypes.data, buf.data_ptr()))
+                    lut = buf.to(dev, non_blocking=True).view(torch.int32)
+                    st.event = torch.cuda.Event()
+                    st.event.record()
+                    ids = ids[:F]
+                    items = _Deferred(lambda: ["" if i == 0 else str(i - 1) for i in ids.tolist()])
+                    self._deferred.append(items)
+                    return items, cnt[:F].copy(), lut
                 if V <= F1_HIST_READBACK:
                     # narrow vocabulary: the whole histogram in one readback (no nonzero sync)
                     hh = hist.cpu().numpy()

@@ -41,6 +41,7 @@ _HOST_SIGS = {
     "fa_cands_export": (None, [vp, vp, vp, vp]),
     "fa_cands_free": (None, [vp]),
     "fa_level_plan": (C.c_int, [vp, vp, i64, vp, vp, i32, vp, vp, i64, vp, i64, vp]),
+    "fa_f1_rank_numeric": (i64, [vp, i64, i64, vp, vp, vp]),
     "fa_plan_dfs": (C.c_int, [C.c_int, vp, vp, vp, vp, vp, vp, vp, i32, C.c_int, vp, i64, vp, i64, vp, i64]),
     "fa_plan_trie": (C.c_int, [vp, i64, C.c_int, vp, i64, i64, C.c_int, C.c_int, vp, vp, vp, i64, vp]),
     "fa_trie_records": (C.c_int, [vp, vp, vp, i64, vp, vp, C.c_int, C.c_int, vp]),

@@ -1,0 +1,53 @@
+"""Native F1 ranking (csrc/host/f1.cpp fa_f1_rank_numeric) against the numpy form of
+FastApriori._frequent_items: count descending, ties in Java String order of the
+decimal token (digits left-aligned to 10 places, then length), id 0 = "" first.
+Reference semantics: FastApriori.scala:55-62."""
+import numpy as np
+import pytest
+
+from fastapriori_amd.ops import _native
+from fastapriori_amd.utils.jvm import java_string_key
+
+_POW10 = 10 ** np.arange(1, 11, dtype=np.int64)
+_POW10_PAD = 10 ** (10 - np.arange(0, 12).clip(max=10)).astype(np.int64)
+
+
+def _numpy_rank(hh, thr):
+    fid = np.flatnonzero(hh >= thr).astype(np.int64)
+    fc = hh[fid]
+    v = fid - 1
+    d = np.searchsorted(_POW10, v, side="right") + 1
+    key = v * _POW10_PAD[d]
+    key[fid == 0], d[fid == 0] = -1, 0
+    order = np.lexsort((d, key, -fc))
+    return fid[order], fc[order]
+
+
+@pytest.mark.parametrize("V,hi,thr", [(1, 3, 0), (7, 3, 1), (1001, 40, 20), (20000, 5, 3), (65536, 50, 25)])
+def test_native_rank_matches_numpy(V, hi, thr):
+    hh = np.random.default_rng(V).integers(0, hi, V).astype(np.int64)
+    ids = np.empty(V, np.int64)
+    cnt = np.empty(V, np.int64)
+    lut = np.empty(V, np.int32)
+    F = _native.host().fa_f1_rank_numeric(hh.ctypes.data, V, thr, ids.ctypes.data, cnt.ctypes.data, lut.ctypes.data)
+    ref_ids, ref_cnt = _numpy_rank(hh, thr)
+    assert F == ref_ids.size
+    assert np.array_equal(ids[:F], ref_ids) and np.array_equal(cnt[:F], ref_cnt)
+    want = np.full(V, -1, np.int32)
+    want[ref_ids] = np.arange(F, dtype=np.int32)
+    assert np.array_equal(lut, want)
+
+
+def test_ties_follow_java_string_order():
+    # equal counts: "" < "0" < "1" < "10" < "100" < "11" < "2" (Java String.compareTo)
+    toks = ["", "0", "1", "10", "100", "11", "2", "9", "99"]
+    fids = [0] + [int(t) + 1 for t in toks[1:]]
+    V = max(fids) + 1
+    hh = np.zeros(V, np.int64)
+    hh[fids] = 5
+    ids = np.empty(V, np.int64)
+    cnt = np.empty(V, np.int64)
+    lut = np.empty(V, np.int32)
+    F = _native.host().fa_f1_rank_numeric(hh.ctypes.data, V, 1, ids.ctypes.data, cnt.ctypes.data, lut.ctypes.data)
+    got = ["" if i == 0 else str(i - 1) for i in ids[:F]]
+    assert got == sorted(toks, key=java_string_key)
