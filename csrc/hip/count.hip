@@ -1032,13 +1032,23 @@ __device__ __forceinline__ void slab_build_word_m(uint64_t* __restrict__ slab, i
   const int srel = (int)(st - base);
   const int n = (int)(end - base);
   const unsigned long long le = lanes_le_mask();
-  constexpr int U = 2;                                // windows in flight per wave (4 measured slower)
-  for (int p0 = 64 * U * h; p0 < n; p0 += 64 * U * nsub) {
+  constexpr int U = 2;                                // windows per step (4 measured slower)
+  const int step = 64 * U * nsub;
+  // software pipeline: the next step's ranks are loaded before this step's window
+  // masks and LDS atomics, so the HBM latency of a step overlaps the previous one
+  int rn[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int p = 64 * U * h + 64 * u + lane;
+    rn[u] = p < n ? ranks[base + p] : -1;
+  }
+  for (int p0 = 64 * U * h; p0 < n; p0 += step) {
     int r[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int p = p0 + 64 * u + lane;
-      r[u] = p < n ? ranks[base + p] : -1;
+      r[u] = rn[u];
+      const int p = p0 + step + 64 * u + lane;
+      rn[u] = p < n ? ranks[base + p] : -1;
     }
     // starts before p0: rows with srel < p0 (ballot over the row owners)
     const int cs0 = __popcll(__ballot(srel < p0));
