@@ -1020,35 +1020,58 @@ struct MapLds {
   }
 };
 
+// The CSR span of a 64-column word: this lane's row start, the word's first and end
+// positions (loaded ahead of the build by k_count_slab_rec: one HBM round trip less
+// in every slab's build phase).
+struct WordSpan {
+  int64_t st, base, end;
+};
+__device__ __forceinline__ WordSpan word_span(const int64_t* __restrict__ roff, int64_t col0, int64_t ncols) {
+  const int lane = threadIdx.x & 63;
+  return WordSpan{roff[min(col0 + lane, ncols)], roff[col0], roff[min(col0 + 64, ncols)]};
+}
+
+template <class Map>
+__device__ __forceinline__ void slab_build_word_span(uint64_t* __restrict__ slab, int swp, int q, const WordSpan& ws,
+                                                     const int32_t* __restrict__ ranks, Map item_map, int h,
+                                                     int nsub, unsigned long long* words, int swz);
+
 template <class Map = MapGlobal>
 __device__ __forceinline__ void slab_build_word_m(uint64_t* __restrict__ slab, int swp, int q, int64_t col0,
                                                   int64_t ncols, const int64_t* __restrict__ roff,
                                                   const int32_t* __restrict__ ranks, Map item_map, int h,
                                                   int nsub, unsigned long long* words, int swz = 0) {
+  slab_build_word_span(slab, swp, q, word_span(roff, col0, ncols), ranks, item_map, h, nsub, words, swz);
+}
+
+template <class Map>
+__device__ __forceinline__ void slab_build_word_span(uint64_t* __restrict__ slab, int swp, int q, const WordSpan& ws,
+                                                     const int32_t* __restrict__ ranks, Map item_map, int h,
+                                                     int nsub, unsigned long long* words, int swz) {
   const int lane = threadIdx.x & 63;
-  const int64_t st = roff[min(col0 + lane, ncols)];
-  const int64_t base = roff[col0];
-  const int64_t end = roff[min(col0 + 64, ncols)];
+  const int64_t st = ws.st, base = ws.base, end = ws.end;
   const int srel = (int)(st - base);
   const int n = (int)(end - base);
   const unsigned long long le = lanes_le_mask();
   constexpr int U = 2;                                // windows per step (4 measured slower)
   const int step = 64 * U * nsub;
-  // software pipeline: the next step's ranks are loaded before this step's window
-  // masks and LDS atomics, so the HBM latency of a step overlaps the previous one
-  int rn[U];
+  // software pipeline: the ranks of the next two steps are loaded before this step's
+  // window masks and LDS atomics, so the HBM latency of a step overlaps the previous ones
+  int rn[U], rn2[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int p = 64 * U * h + 64 * u + lane;
     rn[u] = p < n ? ranks[base + p] : -1;
+    rn2[u] = p + step < n ? ranks[base + p + step] : -1;
   }
   for (int p0 = 64 * U * h; p0 < n; p0 += step) {
     int r[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       r[u] = rn[u];
-      const int p = p0 + step + 64 * u + lane;
-      rn[u] = p < n ? ranks[base + p] : -1;
+      rn[u] = rn2[u];
+      const int p = p0 + 2 * step + 64 * u + lane;
+      rn2[u] = p < n ? ranks[base + p] : -1;
     }
     // starts before p0: rows with srel < p0 (ballot over the row owners)
     const int cs0 = __popcll(__ballot(srel < p0));
@@ -1357,6 +1380,18 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
     }
   };
   auto acc_add = [&](int e, uint32_t v) { atomicAdd(&acc[e], v); };
+  // contiguous build with one word per wave (SW <= 8; at SW = 16 the span spills): the word's CSR span for the
+  // next slab is loaded before this slab's counting, so the build starts without
+  // waiting on the row offsets
+  constexpr int kNW = kSlabThreads / 64;
+  constexpr bool kOneWord = kBuild == kBuildContig && SW <= 8 && SW * (kNW > SW ? kNW / SW : 1) == kNW;
+  const int my_q = (int)(threadIdx.x >> 6) / (kNW > SW ? kNW / SW : 1);
+  WordSpan span{0, 0, 0};
+  auto load_span = [&](int64_t sb_) {
+    const int64_t col0 = (sb_ * SW + my_q) * 64;
+    if (kOneWord && sb_ < nslabs && col0 < ncols) span = word_span(roff, col0, ncols);
+  };
+  load_span(blockIdx.x);
 
   for (int64_t sb = blockIdx.x; sb < nslabs; sb += gridDim.x) {
     const int64_t w0 = sb * SW;
@@ -1375,14 +1410,26 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
         constexpr int NW = kSlabThreads / 64;
         constexpr int NSUB = NW > SW ? NW / SW : 1;
         const int wv = threadIdx.x >> 6;
-        for (int q = wv / NSUB; q < SW; q += NW / NSUB) {
-          if ((w0 + q) * 64 >= ncols) continue;
-          if (map_lds)
-            slab_build_word_m(slab, SWP, q, (w0 + q) * 64, ncols, roff, ranks, MapLds{smap}, wv % NSUB, NSUB,
-                              build_words + wv * 2);
-          else
-            slab_build_word_m(slab, SWP, q, (w0 + q) * 64, ncols, roff, ranks, MapGlobal{item_map}, wv % NSUB,
-                              NSUB, build_words + wv * 2);
+        if (kOneWord) {
+          // one word per wave: its span was loaded ahead (during the previous slab's count)
+          const int q = wv / NSUB;
+          if ((w0 + q) * 64 < ncols) {
+            if (map_lds)
+              slab_build_word_span(slab, SWP, q, span, ranks, MapLds{smap}, wv % NSUB, NSUB, build_words + wv * 2, 0);
+            else
+              slab_build_word_span(slab, SWP, q, span, ranks, MapGlobal{item_map}, wv % NSUB, NSUB,
+                                   build_words + wv * 2, 0);
+          }
+        } else {
+          for (int q = wv / NSUB; q < SW; q += NW / NSUB) {
+            if ((w0 + q) * 64 >= ncols) continue;
+            if (map_lds)
+              slab_build_word_m(slab, SWP, q, (w0 + q) * 64, ncols, roff, ranks, MapLds{smap}, wv % NSUB, NSUB,
+                                build_words + wv * 2);
+            else
+              slab_build_word_m(slab, SWP, q, (w0 + q) * 64, ncols, roff, ranks, MapGlobal{item_map}, wv % NSUB,
+                                NSUB, build_words + wv * 2);
+          }
         }
       } else {
         // dedup layout: column j of the tile gathers row src[col]
@@ -1401,6 +1448,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
       }
     }
     __syncthreads();
+    load_span(sb + gridDim.x);                      // in flight during the counting below
     uint32_t wt[SW];
 #pragma unroll
     for (int q = 0; q < SW; ++q) wt[q] = kWeighted ? ((w0 + q < W) ? (uint32_t)wword[w0 + q] : 0u) : 1u;
