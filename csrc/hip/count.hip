@@ -1340,7 +1340,7 @@ __device__ __forceinline__ int u16_at(const int4& v, int k) {
   return (k & 1) ? (int)((uint32_t)w >> 16) : (w & 0xFFFF);
 }
 
-template <int SW, bool kWeighted, int kBuild>
+template <int SW, bool kWeighted, int kBuild, bool kCls = false>
 __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
     const int64_t* __restrict__ roff, const int32_t* __restrict__ ranks, const int32_t* __restrict__ src,
     int64_t ncols, const int32_t* __restrict__ item_map, int F1, int n_used, const int32_t* __restrict__ gpre,
@@ -1452,12 +1452,40 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
     uint32_t wt[SW];
 #pragma unroll
     for (int q = 0; q < SW; ++q) wt[q] = kWeighted ? ((w0 + q < W) ? (uint32_t)wword[w0 + q] : 0u) : 1u;
+    // kCls (plan.cpp cls_layout): q = AND of the first m-1 prefix rows, kept while
+    // the record says the piece is a sibling of this thread's previous one (flag 1),
+    // p = q & the last prefix row, kept for the next piece of the same prefix (flag 2)
+    uint4 p[SW / 2], qv[SW / 2];
     for (int g = g0; g < ((dbg & 2) ? 0 : G); g += kSlabThreads) {
       // this thread's next piece (after its last one: its first, for the next slab)
       const int gn = g + kSlabThreads < G ? g + kSlabThreads : g0;
       const int4 na = rec[3 * gn], nb = rec[3 * gn + 1], nc = rec[3 * gn + 2];
       const int n_ext = ra.y & 0xFF, m = (ra.y >> 8) & 0xFF;
-      uint4 p[SW / 2];
+      if constexpr (kCls) {
+        const int fl = (ra.y >> 17) & 3;
+        if (!(fl & 1)) {
+          const uint4* r0 = lds4 + (size_t)(ra.z & 0xFFFF) * RS;
+#pragma unroll
+          for (int q = 0; q < SW / 2; ++q) qv[q] = r0[q];
+#pragma unroll
+          for (int j = 1; j < 4; ++j)
+            if (j < m - 1) and_row(qv, u16_at(ra, 4 + j));
+          if (m > 5) {
+#pragma unroll
+            for (int j = 4; j < 11; ++j)
+              if (j < m - 1) and_row(qv, u16_at(rc, j - 4));
+          }
+        }
+        if (!(fl & 2)) {
+          const int last = m - 1;
+          const uint4* rl = lds4 + (size_t)(last < 4 ? u16_at(ra, 4 + last) : u16_at(rc, last - 4)) * RS;
+#pragma unroll
+          for (int q = 0; q < SW / 2; ++q) {
+            const uint4 v = rl[q];
+            p[q].x = qv[q].x & v.x; p[q].y = qv[q].y & v.y; p[q].z = qv[q].z & v.z; p[q].w = qv[q].w & v.w;
+          }
+        }
+      } else {
       {
         const uint4* r0 = lds4 + (size_t)(ra.z & 0xFFFF) * RS;
 #pragma unroll
@@ -1475,6 +1503,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
       } else {
         const int32_t* pr = gpre + rc.x;            // long prefixes (m > 12): ids from the plan's gpre
         for (int j = 1; j < m; ++j) and_row(p, pr[j]);
+      }
       }
       uint32_t any = 0;
 #pragma unroll
@@ -1876,11 +1905,14 @@ FA_API int fa_hip_count_candidates(const uint64_t* bm, int64_t Wp, int64_t W, co
 // and the slab is built from contiguous rows.  Returns 3 when that exceeds the LDS.
 // g_dev (optional): the piece count read by the kernel from device memory (G is then
 // ignored; device-planned bundles, levels.hip fa_hip_dl_plan).
-FA_API int fa_hip_count_slab_rec(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
-                                 const int32_t* item_map, int F1, int n_used, const int32_t* gpre, const void* rec,
-                                 int G, int C, const int32_t* wword, uint32_t* out, int sw, int n_wg,
-                                 const uint64_t* bm, int64_t Wp, hipStream_t st, const int32_t* bm_rows,
-                                 const int32_t* g_dev) {
+// cls: the records carry class-layout flags (plan.cpp cls_layout): unit weights run
+// k_count_slab_rec<.., kCls> (the flags are hints: the plain kernel ignores them and
+// recomputes every prefix, with the same counts).
+FA_API int fa_hip_count_slab_rec_cls(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
+                                     const int32_t* item_map, int F1, int n_used, const int32_t* gpre,
+                                     const void* rec, int G, int C, const int32_t* wword, uint32_t* out, int sw,
+                                     int n_wg, const uint64_t* bm, int64_t Wp, hipStream_t st,
+                                     const int32_t* bm_rows, const int32_t* g_dev, int cls) {
   if ((G <= 0 && !g_dev) || C <= 0 || ncols <= 0) return 0;
   const int64_t n_acc = C;
   const bool contig = !bm && !src;
@@ -1891,7 +1923,9 @@ FA_API int fa_hip_count_slab_rec(const int64_t* roff, const int32_t* ranks, cons
                          const int32_t*, const int4*, int, int, const int32_t*, uint32_t*, const uint64_t*, int64_t,
                          const int32_t*, int, const int32_t*);
   KernT kern = nullptr;
-#define FA_REC_MODE(S, B) kern = wword ? (KernT)k_count_slab_rec<S, true, B> : (KernT)k_count_slab_rec<S, false, B>;
+#define FA_REC_MODE(S, B)                                                                     \
+  kern = wword ? (KernT)k_count_slab_rec<S, true, B>                                          \
+               : cls ? (KernT)k_count_slab_rec<S, false, B, true> : (KernT)k_count_slab_rec<S, false, B>;
 #define FA_REC_CASE(S)                                    \
   if (sw == S) {                                          \
     if (bm) { FA_REC_MODE(S, kBuildBM) }                  \
@@ -1910,6 +1944,15 @@ FA_API int fa_hip_count_slab_rec(const int64_t* roff, const int32_t* ranks, cons
   hipLaunchKernelGGL(kern, dim3((unsigned)n_wg), dim3(kSlabThreads), lds, st, roff, ranks, src, ncols, item_map, F1,
                      n_used, gpre, (const int4*)rec, G, C, wword, out, bm, Wp, bm_rows, dbg, g_dev);
   FA_LAUNCH_RET();
+}
+
+FA_API int fa_hip_count_slab_rec(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
+                                 const int32_t* item_map, int F1, int n_used, const int32_t* gpre, const void* rec,
+                                 int G, int C, const int32_t* wword, uint32_t* out, int sw, int n_wg,
+                                 const uint64_t* bm, int64_t Wp, hipStream_t st, const int32_t* bm_rows,
+                                 const int32_t* g_dev) {
+  return fa_hip_count_slab_rec_cls(roff, ranks, src, ncols, item_map, F1, n_used, gpre, rec, G, C, wword, out, sw,
+                                   n_wg, bm, Wp, st, bm_rows, g_dev, 0);
 }
 
 // Bundle counting with depth-2 prefix reuse (k_count_slab<.., kDfs = true>), unit

@@ -15,7 +15,9 @@
 //   passes      (consecutive work items whose extensions fit the LDS accumulator)
 // and sorts the work items of a pass by estimated cost so the lanes of a wave
 // run loops of similar length.
+#include <algorithm>
 #include <cstring>
+#include <vector>
 
 #include "fa_common.h"
 
@@ -198,14 +200,17 @@ FA_API int fa_trie_records(const int32_t* pieces, const int32_t* witems, const i
 // and written into one (pinned) int32 buffer so the driver issues a single
 // host->device copy per level.
 //
-//   params (double[9]): lds_bytes, min_saving (0 = always trie, >1 = never),
+//   params (double[10]): lds_bytes, min_saving (0 = always trie, >1 = never),
 //                       conflict16, conflict8, pass_weight, rounds, emax_max, W,
-//                       LDS bytes per accumulator (4, or 2 for packed 16-bit counters)
+//                       LDS bytes per accumulator (4, or 2 for packed 16-bit counters),
+//                       class layout of slab passes (1: where it saves reads, 2: always)
 //   info (int64[24]) out:
 //     0 kernel (0 slab, 1 trie)  1 sw  2 cap  3 n_used  4 n_pieces  5 n_witems
 //     6 n_passes  7 d1  8 d2  9 trie reads  10 slab reads  11 emax
 //     12 off item_map  13 off used  14 off gext  15 off gpre  16 off pieces/loc_off
 //     17 off witems  18 total int32 written  19 off gpm (slab)  20 off piece records (slab)
+//     21 slab wave-step reads, size-sorted  22 the same, class layout (0: not tried)
+//     23 class layout used by some pass (record flags set: k_count_slab_rec<.., kCls>)
 //   passes (int64[3 * maxpass]): slab: (piece begin, piece end, ext base);
 //                                trie: (witem begin, witem end, ext base)
 // Returns 0, 3 (buffer too small), 4 (no slab width fits: use the bitmap kernel).
@@ -227,6 +232,102 @@ static int slab_width(int64_t n_used, int64_t C, double lds, int64_t* cap_out, d
 // LDS bytes of k_count_slab_rec's copy of the rank -> slab-row map (u16 per
 // frequent item; 0 = the map stays in global memory).  count.hip mirrors this.
 static inline int64_t fa_slab_map_lds(int64_t F1) { return F1 <= 8192 ? ((F1 * 2 + 15) & ~(int64_t)15) : 0; }
+
+// ---------------------------------------------------------------------------
+// Class layout of a slab pass (k_count_slab_rec<.., kCls>).  Pieces whose prefixes
+// share their first m-1 items (siblings in the candidate trie: one equivalence
+// class of the (k-2)-prefix, FastApriori.scala:132-160 groups by the (k-1)-prefix
+// only) are counted by one thread in a row: it ANDs the m-1 shared rows once (q),
+// then per piece one row (p = q & last item) and its extensions.  On T40I10D100K
+// levels 7-11 this reads 0.63-0.67x the slab rows of the size-sorted layout.
+// A wave's 64 lanes must branch alike, so classes of equal length s (<= 8 pieces)
+// fill the lanes of one "wave row" (s steps), classes sorted by their extension
+// counts so the lanes' extension loops match, and the wave rows go to the 16 waves
+// of the workgroup longest first onto the least-loaded wave.  Slot s of a pass is
+// step s / 1024 of thread s % 1024 (count.hip kSlabThreads); idle slots keep both
+// partial ANDs and have no extensions.  Record flags: kRecKeepQ = the shared
+// m-1 rows are the previous piece's, kRecKeepP = the whole prefix is.
+// ---------------------------------------------------------------------------
+struct SlabPiece { int64_t g, lo, hi; };
+constexpr int kSlabWg = 1024;              // count.hip kSlabThreads
+constexpr int kClsMaxRun = 8;              // pieces per class run (longer classes are cut)
+constexpr double kClsMinGain = 0.9;        // class layout only when its wave-step reads are < 0.9x
+constexpr uint8_t kRecKeepQ = 1, kRecKeepP = 2;
+
+// Slab-row reads per lane summed over wave steps (the SIMT cost: a wave runs the
+// longest extension loop of its lanes, and a recompute if any lane needs one).
+static int64_t slot_cost(const std::vector<SlabPiece>& pcs, const std::vector<int64_t>& slots,
+                         const std::vector<uint8_t>& flags, int m) {
+  int64_t cost = 0;
+  const int64_t n = (int64_t)slots.size();
+  for (int64_t w0 = 0; w0 < n; w0 += 64) {
+    bool q = false, p = false;
+    int64_t e = 0;
+    for (int64_t s = w0; s < std::min(n, w0 + 64); ++s) {
+      if (slots[s] < 0) continue;
+      q = q || !(flags[s] & kRecKeepQ);
+      p = p || !(flags[s] & kRecKeepP);
+      e = std::max(e, pcs[slots[s]].hi - pcs[slots[s]].lo);
+    }
+    cost += (q ? m - 1 : 0) + (p ? 1 : 0) + e;
+  }
+  return cost;
+}
+
+static void cls_layout(const std::vector<SlabPiece>& pcs, int64_t i, int64_t j, const int32_t* Pf,
+                       const int64_t* poff, int m, std::vector<int64_t>& slots, std::vector<uint8_t>& flags) {
+  struct Run { int64_t k0; int s; };
+  std::vector<Run> runs;
+  for (int64_t k = i; k < j; ++k) {
+    bool same = k > i && runs.back().s < kClsMaxRun;
+    if (same && pcs[k].g != pcs[k - 1].g) {
+      const int32_t* a = Pf + poff[pcs[k - 1].g];
+      const int32_t* b = Pf + poff[pcs[k].g];
+      same = std::equal(a, a + m - 1, b);
+    }
+    if (same) runs.back().s += 1;
+    else runs.push_back({k, 1});
+  }
+  // runs longest first; equal lengths by extension counts (descending, lexicographic)
+  auto n_ext = [&](int64_t k) { return pcs[k].hi - pcs[k].lo; };
+  std::stable_sort(runs.begin(), runs.end(), [&](const Run& x, const Run& y) {
+    if (x.s != y.s) return x.s > y.s;
+    for (int e = 0; e < x.s; ++e)
+      if (n_ext(x.k0 + e) != n_ext(y.k0 + e)) return n_ext(x.k0 + e) > n_ext(y.k0 + e);
+    return false;
+  });
+  // wave rows of 64 runs of one length, each to the least-loaded wave
+  constexpr int NWv = kSlabWg / 64;
+  std::vector<std::vector<std::pair<int64_t, int64_t>>> rows_of(NWv);   // (first run, end run)
+  int64_t load[NWv] = {0};
+  for (int64_t r = 0; r < (int64_t)runs.size();) {
+    int64_t r1 = r + 1;
+    while (r1 < (int64_t)runs.size() && r1 - r < 64 && runs[r1].s == runs[r].s) ++r1;
+    const int w = (int)(std::min_element(load, load + NWv) - load);
+    rows_of[w].push_back({r, r1});
+    load[w] += runs[r].s;
+    r = r1;
+  }
+  const int64_t T = *std::max_element(load, load + NWv);
+  slots.assign((size_t)(T * kSlabWg), -1);
+  flags.assign((size_t)(T * kSlabWg), kRecKeepQ | kRecKeepP);
+  for (int w = 0; w < NWv; ++w) {
+    int64_t t = 0;
+    for (const auto& row : rows_of[w]) {
+      const int s = runs[row.first].s;
+      for (int64_t r = row.first; r < row.second; ++r) {
+        const int64_t lane = r - row.first;
+        for (int e = 0; e < s; ++e) {
+          const int64_t k = runs[r].k0 + e;
+          const size_t at = (size_t)((t + e) * kSlabWg + w * 64 + lane);
+          slots[at] = k;
+          flags[at] = e == 0 ? 0 : (uint8_t)(kRecKeepQ | (pcs[k].g == pcs[k - 1].g ? kRecKeepP : 0));
+        }
+      }
+      t += s;
+    }
+  }
+}
 
 FA_API int fa_level_plan(const int32_t* Pf, const int64_t* poff, int64_t G, const int64_t* ext_off,
                          const int32_t* ext, int32_t F1, const double* params, int32_t* buf, int64_t buf_cap,
@@ -333,59 +434,100 @@ FA_API int fa_level_plan(const int32_t* Pf, const int64_t* poff, int64_t G, cons
   int64_t cap = 0;
   const int sw = slab_width(n_used, C, lds, &cap, accb, (double)fa_slab_map_lds(F1));
   if (sw == 0) return 4;
-  struct Piece { int64_t g, lo, hi; };
-  std::vector<Piece> pcs;
+  std::vector<SlabPiece> pcs;
   pcs.reserve((size_t)pieces8);
-  int64_t pre_total = 0;
   for (int64_t g = 0; g < G; ++g) {
     const int64_t a = ext_off[g] - ext_off[0], b = ext_off[g + 1] - ext_off[0];
-    const int64_t mg = poff[g + 1] - poff[g];
-    if (a == b) { pcs.push_back({g, a, a}); pre_total += mg; continue; }
-    for (int64_t x = a; x < b; x += 8) { pcs.push_back({g, x, std::min(b, x + 8)}); pre_total += mg; }
+    if (a == b) { pcs.push_back({g, a, a}); continue; }
+    for (int64_t x = a; x < b; x += 8) pcs.push_back({g, x, std::min(b, x + 8)});
   }
   const int64_t NP = (int64_t)pcs.size();
-  if (!need(pre_total + 4 * NP)) return 3;
+  // passes: consecutive pieces while their extensions fit the accumulator; then the
+  // slot order of each pass (slot s = step s / 1024 of thread s % 1024): size-sorted
+  // pieces, or (class layout, see cls_layout) sibling runs with sharing flags
+  const bool cls_ok = params[9] > 0 && uniform && m0 >= 2 && m0 <= 12;
+  std::vector<int64_t> slot;        // piece index, -1 = idle slot
+  std::vector<uint8_t> sflag;       // kRecKeepQ | kRecKeepP
+  std::vector<int64_t> pass_rng;    // (piece begin, piece end, slot begin, slot end, ext base) per pass
+  int64_t cost_sorted = 0, cost_cls = 0;
+  {
+    int64_t i = 0;
+    std::vector<int64_t> ord;
+    std::vector<int64_t> cs;
+    std::vector<uint8_t> cf;
+    while (i < NP) {
+      const int64_t base = pcs[i].lo;
+      int64_t j = i;
+      while (j < NP && pcs[j].hi - base <= cap) ++j;
+      if (j == i) j = i + 1;   // a single piece always fits (<= 8 extensions)
+      // stable order by extension count (8..0, descending): counting sort
+      int64_t bucket[10] = {0};
+      for (int64_t k = i; k < j; ++k) bucket[8 - (pcs[k].hi - pcs[k].lo) + 1] += 1;
+      for (int b = 1; b < 10; ++b) bucket[b] += bucket[b - 1];
+      ord.resize((size_t)(j - i));
+      for (int64_t k = i; k < j; ++k) ord[bucket[8 - (pcs[k].hi - pcs[k].lo)]++] = k;
+      std::vector<uint8_t> of(ord.size(), 0);
+      const int64_t c_sorted = slot_cost(pcs, ord, of, m0);
+      cost_sorted += c_sorted;
+      bool use_cls = false;
+      if (cls_ok) {
+        cls_layout(pcs, i, j, Pf, poff, m0, cs, cf);
+        const int64_t c_cls = slot_cost(pcs, cs, cf, m0);
+        cost_cls += c_cls;
+        use_cls = params[9] >= 2 || (double)c_cls < kClsMinGain * (double)c_sorted;   // 2: always (tests)
+      }
+      const int64_t s0 = (int64_t)slot.size();
+      if (use_cls) {
+        slot.insert(slot.end(), cs.begin(), cs.end());
+        sflag.insert(sflag.end(), cf.begin(), cf.end());
+      } else {
+        slot.insert(slot.end(), ord.begin(), ord.end());
+        sflag.insert(sflag.end(), of.begin(), of.end());
+      }
+      pass_rng.insert(pass_rng.end(), {i, j, s0, (int64_t)slot.size(), base});
+      i = j;
+    }
+  }
+  const int64_t npass = (int64_t)pass_rng.size() / 5;
+  if (npass > max_pass) return 3;
+  const int64_t NS = (int64_t)slot.size();
+  int64_t pre_total = 0;
+  for (int64_t s = 0; s < NS; ++s)
+    if (slot[s] >= 0) pre_total += poff[pcs[slot[s]].g + 1] - poff[pcs[slot[s]].g];
+  if (!need(pre_total + 4 * NS)) return 3;
   int32_t* gpre = buf + pos;
   int32_t* loc = gpre + pre_total;
-  int32_t* gpm = loc + 2 * NP;
-  info[15] = pos; info[16] = pos + pre_total; info[19] = pos + pre_total + 2 * NP;
-  int64_t npass = 0, i = 0, wpos = 0;
-  std::vector<int64_t> ord;
-  while (i < NP) {
-    // a pass takes pieces while their extensions fit the accumulator
-    const int64_t base = pcs[i].lo;
-    int64_t j = i;
-    while (j < NP && pcs[j].hi - base <= cap) ++j;
-    if (j == i) j = i + 1;   // a single piece always fits (<= 8 extensions)
-    if (npass >= max_pass) return 3;
-    // stable order by extension count (8..0, descending): counting sort
-    int64_t bucket[10] = {0};
-    for (int64_t k = i; k < j; ++k) bucket[8 - (pcs[k].hi - pcs[k].lo) + 1] += 1;
-    for (int b = 1; b < 10; ++b) bucket[b] += bucket[b - 1];
-    ord.resize((size_t)(j - i));
-    for (int64_t k = i; k < j; ++k) ord[bucket[8 - (pcs[k].hi - pcs[k].lo)]++] = k;
-    for (int64_t k = 0; k < j - i; ++k) {
-      const Piece& pc = pcs[ord[k]];
+  int32_t* gpm = loc + 2 * NS;
+  info[15] = pos; info[16] = pos + pre_total; info[19] = pos + pre_total + 2 * NS;
+  int64_t wpos = 0;
+  for (int64_t q = 0; q < npass; ++q) {
+    const int64_t base = pass_rng[5 * q + 4];
+    for (int64_t s = pass_rng[5 * q + 2]; s < pass_rng[5 * q + 3]; ++s) {
+      if (slot[s] < 0) {   // idle slot: no prefix, no extensions
+        gpm[2 * s] = 0; gpm[2 * s + 1] = 0; loc[2 * s] = 0; loc[2 * s + 1] = 0;
+        continue;
+      }
+      const SlabPiece& pc = pcs[slot[s]];
       const int64_t mg = poff[pc.g + 1] - poff[pc.g];
-      gpm[2 * (i + k)] = (int32_t)wpos;
-      gpm[2 * (i + k) + 1] = (int32_t)mg;
+      gpm[2 * s] = (int32_t)wpos;
+      gpm[2 * s + 1] = (int32_t)mg;
       for (int64_t t = 0; t < mg; ++t) gpre[wpos++] = item_map[Pf[poff[pc.g] + t]];
-      loc[2 * (i + k)] = (int32_t)(pc.lo - base);
-      loc[2 * (i + k) + 1] = (int32_t)(pc.hi - base);
+      loc[2 * s] = (int32_t)(pc.lo - base);
+      loc[2 * s + 1] = (int32_t)(pc.hi - base);
     }
-    passes[3 * npass] = i; passes[3 * npass + 1] = j; passes[3 * npass + 2] = base;
-    ++npass;
-    i = j;
+    passes[3 * q] = pass_rng[5 * q + 2]; passes[3 * q + 1] = pass_rng[5 * q + 3]; passes[3 * q + 2] = base;
   }
-  info[0] = 0; info[1] = sw; info[2] = cap; info[4] = NP; info[6] = npass;
-  info[18] = pos + pre_total + 4 * NP;
+  info[0] = 0; info[1] = sw; info[2] = cap; info[4] = NS; info[6] = npass;
+  info[18] = pos + pre_total + 4 * NS;
+  info[21] = cost_sorted; info[22] = cost_cls;
+  info[23] = std::any_of(sflag.begin(), sflag.end(), [](uint8_t f) { return f != 0; }) ? 1 : 0;
   // piece records for k_count_slab_rec: 48 B per piece (16-B aligned), so a piece's
   // whole description is three 16-B loads with no dependent index chain:
   //   a = {ext begin (pass-local), n_ext | m << 8 | (m > 12) << 16, prefix ids 0-3 (u16)}
   //   b = extension ids 0-7 (u16),  c = prefix ids 4-11 (u16), or c.x = gpre offset when m > 12
   {
     const int64_t rpos = (info[18] + 3) & ~(int64_t)3;
-    if (rpos + 12 * NP > buf_cap) return 3;
+    if (rpos + 12 * NS > buf_cap) return 3;
     int32_t* rec = buf + rpos;
     const int32_t* gext_all = buf + info[14];
     auto pk = [](int32_t x, int32_t y) { return (uint32_t)(x & 0xFFFF) | ((uint32_t)(y & 0xFFFF) << 16); };
@@ -399,7 +541,9 @@ FA_API int fa_level_plan(const int32_t* Pf, const int64_t* poff, int64_t G, cons
         int32_t ids[12] = {0};
         for (int t = 0; t < std::min(mg, 12); ++t) ids[t] = pre[t];
         r[0] = (uint32_t)lo;
-        r[1] = (uint32_t)(hi - lo) | ((uint32_t)mg << 8) | (mg > 12 ? 1u << 16 : 0u);
+        // an idle slot keeps both partial ANDs and has no extensions: it reads nothing
+        r[1] = (uint32_t)(hi - lo) | ((uint32_t)(slot[p] < 0 ? m0 : mg) << 8) | (mg > 12 ? 1u << 16 : 0u) |
+               ((uint32_t)sflag[p] << 17);
         r[2] = pk(ids[0], ids[1]);
         r[3] = pk(ids[2], ids[3]);
         int32_t ex8[8] = {0};
@@ -410,7 +554,7 @@ FA_API int fa_level_plan(const int32_t* Pf, const int64_t* poff, int64_t G, cons
       }
     }
     info[20] = rpos;
-    info[18] = rpos + 12 * NP;
+    info[18] = rpos + 12 * NS;
   }
   return 0;
 }

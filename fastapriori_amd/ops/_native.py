@@ -87,6 +87,8 @@ _HIP_SIGS = {
                                    C.c_int, C.c_int, vp, i64, vp, C.c_int, vp, vp]),
     "fa_hip_count_slab_rec": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, C.c_int, vp, vp, C.c_int, C.c_int, vp, vp,
                                         C.c_int, C.c_int, vp, i64, vp, vp, vp]),
+    "fa_hip_count_slab_rec_cls": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, C.c_int, vp, vp, C.c_int, C.c_int, vp,
+                                            vp, C.c_int, C.c_int, vp, i64, vp, vp, vp, C.c_int]),
     # device-resident level bundles (gen.hip fa_hip_dl_*, levels.hip)
     "fa_hip_dl_level0": (C.c_int, [vp, vp, i64, i64, C.c_int, C.c_int, vp, i64, vp, vp, i64, dbl, vp, C.c_int, vp]),
     "fa_hip_dl_more": (C.c_int, [C.c_int, vp, i64, i64, vp, vp, dbl, C.c_int, dbl, i64, vp, vp, vp, vp]),

@@ -665,6 +665,9 @@ TRIE_PASS_WEIGHT = float(os.environ.get("FA_TRIE_PASS_WEIGHT", "4"))
 # auto level kernel: trie-shared counting when its slab-row reads are below this
 # fraction of the slab kernel's (measured break-even on T10I4 / T40I10, MI355X)
 _TRIE_MIN_SAVING = float(os.environ.get("FA_TRIE_MIN_SAVING", "0.3"))
+# class layout of slab passes (plan.cpp cls_layout, k_count_slab_rec<.., kCls>): sibling
+# prefixes share their first m-1 rows in registers; 0 disables it
+SLAB_CLS = int(os.environ.get("FA_SLAB_CLS", "1"))
 
 
 def trie_slab_plan(n_used: int, C: int, W: int, reads_est: float) -> tuple[int, int]:
@@ -800,7 +803,8 @@ def _level_plan_bound(F1: int, C: int, G: int, m: int) -> int:
 
 
 def level_plan_host(prefix: np.ndarray, ext_off: np.ndarray, ext: np.ndarray, F1: int, W: int,
-                    kernel: str = "auto", lds_bytes: int | None = None, poff: np.ndarray | None = None):
+                    kernel: str = "auto", lds_bytes: int | None = None, poff: np.ndarray | None = None,
+                    cls: int | None = None):
     """fa_level_plan on host arrays (tests / diagnostics): (rc, info, passes, buf)."""
     P, po, G, m = _flat_prefix(prefix, poff)
     C = int(ext.size)
@@ -808,14 +812,19 @@ def level_plan_host(prefix: np.ndarray, ext_off: np.ndarray, ext: np.ndarray, F1
     ex = np.ascontiguousarray(ext, dtype=np.int32)
     min_saving = {"auto": _TRIE_MIN_SAVING, "trie": 0.0, "slab": 2.0}[kernel]
     params = np.array([lds_bytes or _LDS_BYTES, min_saving, _TRIE_CONFLICT[16], _TRIE_CONFLICT[8],
-                       TRIE_PASS_WEIGHT, TRIE_ROUNDS, TRIE_EMAX, W, 4.0], dtype=np.float64)
+                       TRIE_PASS_WEIGHT, TRIE_ROUNDS, TRIE_EMAX, W, 4.0, SLAB_CLS if cls is None else cls],
+                      dtype=np.float64)
     bound = _level_plan_bound(F1, C, G, m)
-    buf = np.zeros(bound, np.int32)
     passes = np.zeros((G + C + 2, 3), np.int64)
     info = np.zeros(24, np.int64)
-    rc = _native.host().fa_level_plan(P.ctypes.data, po.ctypes.data, G, eo.ctypes.data, ex.ctypes.data, F1,
-                                      params.ctypes.data, buf.ctypes.data, bound, passes.ctypes.data,
-                                      passes.shape[0], info.ctypes.data)
+    while True:
+        buf = np.zeros(bound, np.int32)
+        rc = _native.host().fa_level_plan(P.ctypes.data, po.ctypes.data, G, eo.ctypes.data, ex.ctypes.data, F1,
+                                          params.ctypes.data, buf.ctypes.data, bound, passes.ctypes.data,
+                                          passes.shape[0], info.ctypes.data)
+        if rc != 3:
+            break
+        bound *= 2    # class layouts pad their passes with idle slots
     return rc, info, passes[:int(info[6])], buf[:int(info[18])]
 
 
@@ -861,16 +870,25 @@ def emulate_slab_records(bits_by_rank: np.ndarray, info, passes, buf, C: int) ->
     u16 = np.stack([rec & 0xFFFF, rec >> 16], axis=-1).reshape(-1, 24)   # 24 u16 per record
     out = np.zeros(C, np.int64)
     for a, b, e0 in passes.tolist():
-        for pi in range(a, b):
-            r = rec[pi]
-            n_ext, m, long_pre = int(r[1] & 0xFF), int((r[1] >> 8) & 0xFF), bool((r[1] >> 16) & 1)
-            if long_pre:
-                ids = gpre[int(r[8]):int(r[8]) + m]
-            else:
-                ids = np.concatenate([u16[pi, 4:8], u16[pi, 16:24]])[:m]
-            p = np.logical_and.reduce(bits[ids])
-            for k in range(n_ext):
-                out[e0 + int(r[0]) + k] += int((p & bits[u16[pi, 8 + k]]).sum())
+        # slot s = step (s - a) // 1024 of thread (s - a) % 1024; class-layout flags
+        # (bit 17: keep q = AND of the first m-1 rows, bit 18: keep p) refer to the
+        # thread's previous slot
+        for t in range(min(1024, b - a)):
+            q = p = None
+            for pi in range(a + t, b, 1024):
+                r = rec[pi]
+                n_ext, m, long_pre = int(r[1] & 0xFF), int((r[1] >> 8) & 0xFF), bool((r[1] >> 16) & 1)
+                fl = int((r[1] >> 17) & 3)
+                if long_pre:
+                    ids = gpre[int(r[8]):int(r[8]) + m]
+                else:
+                    ids = np.concatenate([u16[pi, 4:8], u16[pi, 16:24]])[:m]
+                if not fl & 1:
+                    q = np.logical_and.reduce(bits[ids[:m - 1]])
+                if not fl & 2:
+                    p = q & bits[ids[m - 1]]
+                for k in range(n_ext):
+                    out[e0 + int(r[0]) + k] += int((p & bits[u16[pi, 8 + k]]).sum())
     return out
 
 
@@ -959,17 +977,21 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
     W = (ncols + 63) // 64
     min_saving = {"auto": _TRIE_MIN_SAVING, "trie": 0.0, "slab": 2.0}[kernel]
     params = np.array([_LDS_BYTES, min_saving, _TRIE_CONFLICT[16], _TRIE_CONFLICT[8], TRIE_PASS_WEIGHT,
-                       TRIE_ROUNDS, TRIE_EMAX, W, 4.0], dtype=np.float64)
+                       TRIE_ROUNDS, TRIE_EMAX, W, 4.0, SLAB_CLS], dtype=np.float64)
     bound = _level_plan_bound(F1, C, G, m)
     on_gpu = dev.type == "cuda"
     stage = pinned_stage("level_plan") if on_gpu else None
-    buf = stage.get(4 * bound).view(dtype=_I32) if on_gpu else torch.empty(bound, dtype=_I32)
     max_pass = G + C + 2
     passes = np.zeros((max_pass, 3), dtype=np.int64)
     info = np.zeros(24, dtype=np.int64)
-    rc = _native.host().fa_level_plan(P.ctypes.data, po.ctypes.data, G, eo.ctypes.data, ex.ctypes.data, F1,
-                                      params.ctypes.data, buf.data_ptr(), bound, passes.ctypes.data, max_pass,
-                                      info.ctypes.data)
+    while True:
+        buf = stage.get(4 * bound).view(dtype=_I32) if on_gpu else torch.empty(bound, dtype=_I32)
+        rc = _native.host().fa_level_plan(P.ctypes.data, po.ctypes.data, G, eo.ctypes.data, ex.ctypes.data, F1,
+                                          params.ctypes.data, buf.data_ptr(), bound, passes.ctypes.data, max_pass,
+                                          info.ctypes.data)
+        if rc != 3:
+            break
+        bound *= 2    # class layouts pad their passes with idle slots
     if rc == 4:
         return None
     if rc != 0:
@@ -1012,14 +1034,15 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
             # piece records (k_count_slab_rec): 48 B per piece, loaded one piece ahead
             lds = n_used * (sw + 2) * 8 + Cq * 4 + _slab_map_lds(F1)
             n_wg = int(max(1, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2))))
-            _hip_call("fa_hip_count_slab_rec", _p(roff), _p(ranks), _p(src), ncols, base + 4 * o_im, F1, n_used,
-                      base + 4 * o_gpre, base + 4 * (o_rec + 12 * a), b - a, Cq, _p(wword),
+            _hip_call("fa_hip_count_slab_rec_cls", _p(roff), _p(ranks), _p(src), ncols, base + 4 * o_im, F1,
+                      n_used, base + 4 * o_gpre, base + 4 * (o_rec + 12 * a), b - a, Cq, _p(wword),
                       out.data_ptr() + 4 * e0, sw, n_wg, _p(bm), bm.stride(0) if bm is not None else 0, st,
-                      bm_rows, None)
+                      bm_rows, None, int(info[23]))
     LAST_LEVEL_PLAN.clear()
     LAST_LEVEL_PLAN.update(kernel="trie" if kern == 1 else "slab", rows=int(roff.numel() - 1), used=n_used, sw=sw,
                            cap=cap, passes=npass, pieces=int(info[4]), witems=int(info[5]), d1=int(info[7]),
-                           d2=int(info[8]), trie_reads=int(info[9]), slab_reads=int(info[10]), m=m, C=C)
+                           d2=int(info[8]), trie_reads=int(info[9]), slab_reads=int(info[10]), m=m, C=C,
+                           cls=int(info[23]), step_reads=int(info[21]), step_reads_cls=int(info[22]))
     return out.to(_I64)
 
 

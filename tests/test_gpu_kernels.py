@@ -307,6 +307,23 @@ def test_slab_multipass_from_bitmap(monkeypatch):
     assert ref.as_dict() == got_w.as_dict()
 
 
+@pytest.mark.parametrize("lds_kb", [160, 24])
+def test_slab_class_layout_on_gpu(monkeypatch, lds_kb):
+    # every slab pass in the class layout (plan.cpp cls_layout, FA_SLAB_CLS=2), so
+    # k_count_slab_rec<.., kCls> runs single-pass (contiguous build) and multi-pass
+    # (bitmap copy) levels; counts must equal the bitmap kernel's
+    import fastapriori_amd.ops.primitives as prim
+    sh = generate_shard(60000, Comm(), "cpu", 14.0, 6.0, 300, 120, seed=11)
+    cfg = dict(min_support=0.004, dedup="off")
+    ref = FastApriori(0.004, config=MinerConfig(trim_min_rows=0, level_kernel="bitmap", **cfg)).run(sh)
+    monkeypatch.setattr(prim, "SLAB_CLS", 2)
+    monkeypatch.setattr(prim, "_LDS_BYTES", lds_kb * 1024 - 512)
+    got = FastApriori(0.004, config=MinerConfig(trim_min_rows=0, level_kernel="slab", **cfg)).run(sh.to(DEV))
+    assert len(ref.levels) >= 5
+    assert prim.LAST_LEVEL_PLAN.get("cls") == 1
+    assert ref.as_dict() == got.as_dict()
+
+
 @pytest.mark.parametrize("long_rows", [False, True])
 def test_pair_kernels_agree(long_rows):
     # unit weights: 256-rank blocks + k_pair_queue16 (long_rows: 128-rank blocks +

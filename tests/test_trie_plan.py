@@ -201,3 +201,45 @@ def test_bundled_levels_match_unbundled(monkeypatch):
     monkeypatch.setattr(ap, "BUNDLE_LEVELS", False)
     off = FastApriori(0.003, config=MinerConfig(min_support=0.003)).run(sh)
     assert on.as_dict() == off.as_dict() and on.items == off.items
+
+
+@pytest.mark.parametrize("k", [3, 5, 7])
+@pytest.mark.parametrize("lds_kb", [160, 6])
+def test_slab_class_layout_counts(k, lds_kb):
+    # plan.cpp cls_layout: sibling pieces in one thread's slots with keep-q / keep-p
+    # flags, idle slots padding the wave rows; the record emulation follows the flags
+    # slot by slot (k_count_slab_rec<.., kCls>) and must reproduce brute-force supports
+    from fastapriori_amd.ops.primitives import emulate_level_plan, emulate_slab_records, level_plan_host
+    rng = np.random.default_rng(k + lds_kb)
+    bits, prev = _level(rng, n_items=16, n_rows=300, k=k, dens=0.6 if k < 7 else 0.8)
+    pidx, eoff, ext = apriori_gen(prev)
+    if ext.size == 0:
+        pytest.skip("no candidates")
+    P = prev[pidx]
+    rc, info, passes, buf = level_plan_host(P, eoff, ext, bits.shape[0], 5, "slab", lds_bytes=lds_kb * 1024, cls=2)
+    assert rc == 0 and info[0] == 0 and info[23] == 1
+    g_of_e = np.repeat(np.arange(pidx.size), np.diff(eoff))
+    want = np.array([np.logical_and.reduce(bits[list(P[g]) + [e]]).sum() for g, e in zip(g_of_e, ext)])
+    assert np.array_equal(emulate_level_plan(bits, info, passes, buf, P.shape[1], ext.size), want)
+    assert np.array_equal(emulate_slab_records(bits, info, passes, buf, ext.size), want)
+    # every pass's slots are whole steps of the 1024-thread workgroup
+    assert all((b - a) % 1024 == 0 for a, b, _ in passes.tolist())
+
+
+def test_slab_class_layout_chosen_on_deep_levels():
+    # a deep downward-closed level has long sibling runs: the class layout's wave-step
+    # reads are well below the size-sorted layout's, so the planner takes it (cls=1)
+    from itertools import combinations
+    from fastapriori_amd.ops.primitives import level_plan_host
+    rng = np.random.default_rng(2)
+    rows = set()
+    for _ in range(40):
+        big = np.sort(rng.choice(40, 11, replace=False))
+        rows.update(combinations(big.tolist(), 6))
+    prev = np.array(sorted(rows), np.int32)
+    pidx, eoff, ext = apriori_gen(prev)
+    rc, info, passes, buf = level_plan_host(prev[pidx], eoff, ext, 40, 1 << 14, "slab", cls=1)
+    assert rc == 0 and info[0] == 0
+    assert info[22] < 0.9 * info[21] and info[23] == 1
+    rc0, info0, _, _ = level_plan_host(prev[pidx], eoff, ext, 40, 1 << 14, "slab", cls=0)
+    assert rc0 == 0 and info0[23] == 0 and info0[22] == 0
