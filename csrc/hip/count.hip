@@ -1477,8 +1477,9 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
           }
         }
         if (!(fl & 2)) {
-          const int last = m - 1;
-          const uint4* rl = lds4 + (size_t)(last < 4 ? u16_at(ra, 4 + last) : u16_at(rc, last - 4)) * RS;
+          // the last prefix id rides in the record's bits 19-31 (a runtime u16_at index
+          // would put the record in scratch memory)
+          const uint4* rl = lds4 + (size_t)((uint32_t)ra.y >> 19) * RS;
 #pragma unroll
           for (int q = 0; q < SW / 2; ++q) {
             const uint4 v = rl[q];

@@ -251,7 +251,7 @@ static inline int64_t fa_slab_map_lds(int64_t F1) { return F1 <= 8192 ? ((F1 * 2
 struct SlabPiece { int64_t g, lo, hi; };
 constexpr int kSlabWg = 1024;              // count.hip kSlabThreads
 constexpr int kClsMaxRun = 8;              // pieces per class run (longer classes are cut)
-constexpr double kClsMinGain = 0.9;        // class layout only when its wave-step reads are < 0.9x
+constexpr double kClsMinGain = 0.8;        // class layout only when its wave-step reads are < 0.8x
 constexpr uint8_t kRecKeepQ = 1, kRecKeepP = 2;
 
 // Slab-row reads per lane summed over wave steps (the SIMT cost: a wave runs the
@@ -288,14 +288,10 @@ static void cls_layout(const std::vector<SlabPiece>& pcs, int64_t i, int64_t j, 
     if (same) runs.back().s += 1;
     else runs.push_back({k, 1});
   }
-  // runs longest first; equal lengths by extension counts (descending, lexicographic)
-  auto n_ext = [&](int64_t k) { return pcs[k].hi - pcs[k].lo; };
-  std::stable_sort(runs.begin(), runs.end(), [&](const Run& x, const Run& y) {
-    if (x.s != y.s) return x.s > y.s;
-    for (int e = 0; e < x.s; ++e)
-      if (n_ext(x.k0 + e) != n_ext(y.k0 + e)) return n_ext(x.k0 + e) > n_ext(y.k0 + e);
-    return false;
-  });
+  // runs longest first; equal lengths keep their lexicographic order, so the lanes of a
+  // wave read mostly the same prefix rows (LDS broadcast) -- measured better than
+  // ordering them by extension counts
+  std::stable_sort(runs.begin(), runs.end(), [&](const Run& x, const Run& y) { return x.s > y.s; });
   // wave rows of 64 runs of one length, each to the least-loaded wave
   constexpr int NWv = kSlabWg / 64;
   std::vector<std::vector<std::pair<int64_t, int64_t>>> rows_of(NWv);   // (first run, end run)
@@ -448,7 +444,9 @@ FA_API int fa_level_plan(const int32_t* Pf, const int64_t* poff, int64_t G, cons
   const bool cls_ok = params[9] > 0 && uniform && m0 >= 2 && m0 <= 12;
   std::vector<int64_t> slot;        // piece index, -1 = idle slot
   std::vector<uint8_t> sflag;       // kRecKeepQ | kRecKeepP
-  std::vector<int64_t> pass_rng;    // (piece begin, piece end, slot begin, slot end, ext base) per pass
+  std::vector<int64_t> pass_rng;    // (piece begin, piece end, slot begin, slot end, ext base, class slot end)
+  std::vector<int64_t> cslot;       // the class layout's slots and flags
+  std::vector<uint8_t> cflag;
   int64_t cost_sorted = 0, cost_cls = 0;
   {
     int64_t i = 0;
@@ -469,26 +467,30 @@ FA_API int fa_level_plan(const int32_t* Pf, const int64_t* poff, int64_t G, cons
       std::vector<uint8_t> of(ord.size(), 0);
       const int64_t c_sorted = slot_cost(pcs, ord, of, m0);
       cost_sorted += c_sorted;
-      bool use_cls = false;
+      const int64_t s0 = (int64_t)slot.size();
+      slot.insert(slot.end(), ord.begin(), ord.end());
+      sflag.insert(sflag.end(), of.begin(), of.end());
       if (cls_ok) {
         cls_layout(pcs, i, j, Pf, poff, m0, cs, cf);
-        const int64_t c_cls = slot_cost(pcs, cs, cf, m0);
-        cost_cls += c_cls;
-        use_cls = params[9] >= 2 || (double)c_cls < kClsMinGain * (double)c_sorted;   // 2: always (tests)
+        cost_cls += slot_cost(pcs, cs, cf, m0);
+        cslot.insert(cslot.end(), cs.begin(), cs.end());
+        cflag.insert(cflag.end(), cf.begin(), cf.end());
       }
-      const int64_t s0 = (int64_t)slot.size();
-      if (use_cls) {
-        slot.insert(slot.end(), cs.begin(), cs.end());
-        sflag.insert(sflag.end(), cf.begin(), cf.end());
-      } else {
-        slot.insert(slot.end(), ord.begin(), ord.end());
-        sflag.insert(sflag.end(), of.begin(), of.end());
-      }
-      pass_rng.insert(pass_rng.end(), {i, j, s0, (int64_t)slot.size(), base});
+      pass_rng.insert(pass_rng.end(), {i, j, s0, (int64_t)slot.size(), base, (int64_t)cslot.size()});
       i = j;
     }
   }
-  const int64_t npass = (int64_t)pass_rng.size() / 5;
+  // one layout for the whole level (one kernel per level): the class layout when its
+  // wave-step reads are below kClsMinGain of the size-sorted layout's (params[9] = 2: always)
+  if (cls_ok && (params[9] >= 2 || (double)cost_cls < kClsMinGain * (double)cost_sorted)) {
+    slot.swap(cslot);
+    sflag.swap(cflag);
+    for (size_t q = 0; q < pass_rng.size(); q += 6) {
+      pass_rng[q + 2] = q ? pass_rng[q - 1] : 0;
+      pass_rng[q + 3] = pass_rng[q + 5];
+    }
+  }
+  const int64_t npass = (int64_t)pass_rng.size() / 6;
   if (npass > max_pass) return 3;
   const int64_t NS = (int64_t)slot.size();
   int64_t pre_total = 0;
@@ -501,8 +503,8 @@ FA_API int fa_level_plan(const int32_t* Pf, const int64_t* poff, int64_t G, cons
   info[15] = pos; info[16] = pos + pre_total; info[19] = pos + pre_total + 2 * NS;
   int64_t wpos = 0;
   for (int64_t q = 0; q < npass; ++q) {
-    const int64_t base = pass_rng[5 * q + 4];
-    for (int64_t s = pass_rng[5 * q + 2]; s < pass_rng[5 * q + 3]; ++s) {
+    const int64_t base = pass_rng[6 * q + 4];
+    for (int64_t s = pass_rng[6 * q + 2]; s < pass_rng[6 * q + 3]; ++s) {
       if (slot[s] < 0) {   // idle slot: no prefix, no extensions
         gpm[2 * s] = 0; gpm[2 * s + 1] = 0; loc[2 * s] = 0; loc[2 * s + 1] = 0;
         continue;
@@ -515,7 +517,7 @@ FA_API int fa_level_plan(const int32_t* Pf, const int64_t* poff, int64_t G, cons
       loc[2 * s] = (int32_t)(pc.lo - base);
       loc[2 * s + 1] = (int32_t)(pc.hi - base);
     }
-    passes[3 * q] = pass_rng[5 * q + 2]; passes[3 * q + 1] = pass_rng[5 * q + 3]; passes[3 * q + 2] = base;
+    passes[3 * q] = pass_rng[6 * q + 2]; passes[3 * q + 1] = pass_rng[6 * q + 3]; passes[3 * q + 2] = base;
   }
   info[0] = 0; info[1] = sw; info[2] = cap; info[4] = NS; info[6] = npass;
   info[18] = pos + pre_total + 4 * NS;
@@ -523,7 +525,8 @@ FA_API int fa_level_plan(const int32_t* Pf, const int64_t* poff, int64_t G, cons
   info[23] = std::any_of(sflag.begin(), sflag.end(), [](uint8_t f) { return f != 0; }) ? 1 : 0;
   // piece records for k_count_slab_rec: 48 B per piece (16-B aligned), so a piece's
   // whole description is three 16-B loads with no dependent index chain:
-  //   a = {ext begin (pass-local), n_ext | m << 8 | (m > 12) << 16, prefix ids 0-3 (u16)}
+  //   a = {ext begin (pass-local), n_ext | m << 8 | (m > 12) << 16 | class flags << 17 | last prefix id << 19,
+  //        prefix ids 0-3 (u16)}
   //   b = extension ids 0-7 (u16),  c = prefix ids 4-11 (u16), or c.x = gpre offset when m > 12
   {
     const int64_t rpos = (info[18] + 3) & ~(int64_t)3;
@@ -543,7 +546,7 @@ FA_API int fa_level_plan(const int32_t* Pf, const int64_t* poff, int64_t G, cons
         r[0] = (uint32_t)lo;
         // an idle slot keeps both partial ANDs and has no extensions: it reads nothing
         r[1] = (uint32_t)(hi - lo) | ((uint32_t)(slot[p] < 0 ? m0 : mg) << 8) | (mg > 12 ? 1u << 16 : 0u) |
-               ((uint32_t)sflag[p] << 17);
+               ((uint32_t)sflag[p] << 17) | (mg >= 1 && mg <= 12 ? (uint32_t)ids[mg - 1] << 19 : 0u);
         r[2] = pk(ids[0], ids[1]);
         r[3] = pk(ids[2], ids[3]);
         int32_t ex8[8] = {0};

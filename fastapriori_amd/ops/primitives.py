@@ -934,6 +934,7 @@ def emulate_trie_records(bits_by_rank: np.ndarray, info, passes, buf, m: int, C:
 
 
 LAST_LEVEL_PLAN: dict = {}   # shape of the last count_level call (diagnostics)
+CLS_LEVELS = [0]             # count_level calls that ran the class layout (diagnostics, tests)
 
 
 def _slab_map_lds(F1: int) -> int:
@@ -1038,6 +1039,7 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
                       n_used, base + 4 * o_gpre, base + 4 * (o_rec + 12 * a), b - a, Cq, _p(wword),
                       out.data_ptr() + 4 * e0, sw, n_wg, _p(bm), bm.stride(0) if bm is not None else 0, st,
                       bm_rows, None, int(info[23]))
+    CLS_LEVELS[0] += int(info[23])
     LAST_LEVEL_PLAN.clear()
     LAST_LEVEL_PLAN.update(kernel="trie" if kern == 1 else "slab", rows=int(roff.numel() - 1), used=n_used, sw=sw,
                            cap=cap, passes=npass, pieces=int(info[4]), witems=int(info[5]), d1=int(info[7]),

@@ -318,9 +318,10 @@ def test_slab_class_layout_on_gpu(monkeypatch, lds_kb):
     ref = FastApriori(0.004, config=MinerConfig(trim_min_rows=0, level_kernel="bitmap", **cfg)).run(sh)
     monkeypatch.setattr(prim, "SLAB_CLS", 2)
     monkeypatch.setattr(prim, "_LDS_BYTES", lds_kb * 1024 - 512)
+    n0 = prim.CLS_LEVELS[0]
     got = FastApriori(0.004, config=MinerConfig(trim_min_rows=0, level_kernel="slab", **cfg)).run(sh.to(DEV))
     assert len(ref.levels) >= 5
-    assert prim.LAST_LEVEL_PLAN.get("cls") == 1
+    assert prim.CLS_LEVELS[0] > n0
     assert ref.as_dict() == got.as_dict()
 
 
