@@ -1506,9 +1506,13 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
         for (int j = 1; j < m; ++j) and_row(p, pr[j]);
       }
       }
-      uint32_t any = 0;
+      // an all-zero prefix skips its extensions; dense levels (dbg & 4: every frequent
+      // prefix expects >= 4 rows per slab) skip the test instead (32 VALU ops per piece at SW = 16)
+      uint32_t any = dbg & 4;
+      if (!any) {
 #pragma unroll
-      for (int q = 0; q < SW / 2; ++q) any |= p[q].x | p[q].y | p[q].z | p[q].w;
+        for (int q = 0; q < SW / 2; ++q) any |= p[q].x | p[q].y | p[q].z | p[q].w;
+      }
       if (any) {
         const int e0 = ra.x;
         // UE extension rows in flight per step (2 x 64 B at SW <= 8; wider rows one at a time)
@@ -1906,9 +1910,10 @@ FA_API int fa_hip_count_candidates(const uint64_t* bm, int64_t Wp, int64_t W, co
 // and the slab is built from contiguous rows.  Returns 3 when that exceeds the LDS.
 // g_dev (optional): the piece count read by the kernel from device memory (G is then
 // ignored; device-planned bundles, levels.hip fa_hip_dl_plan).
-// cls: the records carry class-layout flags (plan.cpp cls_layout): unit weights run
-// k_count_slab_rec<.., kCls> (the flags are hints: the plain kernel ignores them and
-// recomputes every prefix, with the same counts).
+// cls bit 0: the records carry class-layout flags (plan.cpp cls_layout): unit weights
+// run k_count_slab_rec<.., kCls> (the flags are hints: the plain kernel ignores them and
+// recomputes every prefix, with the same counts).  cls bit 1: dense level, no
+// all-zero-prefix test (the counts are the same either way).
 FA_API int fa_hip_count_slab_rec_cls(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
                                      const int32_t* item_map, int F1, int n_used, const int32_t* gpre,
                                      const void* rec, int G, int C, const int32_t* wword, uint32_t* out, int sw,
@@ -1926,7 +1931,7 @@ FA_API int fa_hip_count_slab_rec_cls(const int64_t* roff, const int32_t* ranks, 
   KernT kern = nullptr;
 #define FA_REC_MODE(S, B)                                                                     \
   kern = wword ? (KernT)k_count_slab_rec<S, true, B>                                          \
-               : cls ? (KernT)k_count_slab_rec<S, false, B, true> : (KernT)k_count_slab_rec<S, false, B>;
+               : (cls & 1) ? (KernT)k_count_slab_rec<S, false, B, true> : (KernT)k_count_slab_rec<S, false, B>;
 #define FA_REC_CASE(S)                                    \
   if (sw == S) {                                          \
     if (bm) { FA_REC_MODE(S, kBuildBM) }                  \
@@ -1941,7 +1946,7 @@ FA_API int fa_hip_count_slab_rec_cls(const int64_t* roff, const int32_t* ranks, 
 #undef FA_REC_MODE
   if (!kern) return 1;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  const int dbg = getenv("FA_SLAB_DEBUG") ? atoi(getenv("FA_SLAB_DEBUG")) : 0;
+  const int dbg = (getenv("FA_SLAB_DEBUG") ? atoi(getenv("FA_SLAB_DEBUG")) : 0) | ((cls & 2) ? 4 : 0);
   hipLaunchKernelGGL(kern, dim3((unsigned)n_wg), dim3(kSlabThreads), lds, st, roff, ranks, src, ncols, item_map, F1,
                      n_used, gpre, (const int4*)rec, G, C, wword, out, bm, Wp, bm_rows, dbg, g_dev);
   FA_LAUNCH_RET();

@@ -1259,7 +1259,8 @@ class FastApriori:
         eoff = np.concatenate([[0], np.cumsum(np.concatenate([np.diff(eo) for _, _, _, eo, _ in bundle]))])
         ext = np.concatenate([ex for *_, ex in bundle]).astype(np.int32)
         cnt = ops.count_level(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"], flat, eoff, ext,
-                              db["wword"], kernel="slab", poff=poff, full_bm=lambda u: self._bitmaps(db, u))
+                              db["wword"], kernel="slab", poff=poff, full_bm=lambda u: self._bitmaps(db, u),
+                              sup_frac=self.stats["min_count"] / max(1, self.stats["n_lines"]))
         if cnt is None:
             return [self._count_level(full_db, pv, pi, eo, ex) for _, pv, pi, eo, ex in bundle]
         self.comm.all_reduce_(cnt, bound=self.stats["n_lines"])
@@ -1293,7 +1294,8 @@ class FastApriori:
         lk = self.cfg.level_kernel
         if dev.type == "cuda" and lk in ("auto", "trie", "slab"):
             cnt = ops.count_level(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"], prev[prefix_idx],
-                                  ext_off, ext, db["wword"], kernel=lk, full_bm=lambda u: self._bitmaps(db, u))
+                                  ext_off, ext, db["wword"], kernel=lk, full_bm=lambda u: self._bitmaps(db, u),
+                                  sup_frac=self.stats["min_count"] / max(1, self.stats["n_lines"]))
             if cnt is not None:
                 self.dcomm.all_reduce_(cnt, bound=self.stats["n_lines"])
                 return cnt.cpu().numpy()

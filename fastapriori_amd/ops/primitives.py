@@ -668,6 +668,9 @@ _TRIE_MIN_SAVING = float(os.environ.get("FA_TRIE_MIN_SAVING", "0.3"))
 # class layout of slab passes (plan.cpp cls_layout, k_count_slab_rec<.., kCls>): sibling
 # prefixes share their first m-1 rows in registers; 0 disables it
 SLAB_CLS = int(os.environ.get("FA_SLAB_CLS", "1"))
+# count_level: expected rows per slab of the rarest frequent prefix above which the slab
+# kernel skips its all-zero-prefix test (0 disables)
+DENSE_MIN_ROWS = float(os.environ.get("FA_DENSE_MIN_ROWS", "4"))
 
 
 def trie_slab_plan(n_used: int, C: int, W: int, reads_est: float) -> tuple[int, int]:
@@ -953,7 +956,8 @@ def _flat_prefix(prefix: np.ndarray, poff: np.ndarray | None):
 
 
 def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_off: np.ndarray, ext: np.ndarray,
-                wword, kernel: str = "auto", poff: np.ndarray | None = None, full_bm=None) -> torch.Tensor | None:
+                wword, kernel: str = "auto", poff: np.ndarray | None = None, full_bm=None,
+                sup_frac: float = 0.0) -> torch.Tensor | None:
     """Support counts of one level on the device: one native planning call
     (csrc/host/plan.cpp fa_level_plan: used items, kernel choice, work items,
     accumulator passes) into one pinned buffer, one host->device copy, then the
@@ -966,6 +970,9 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
     or None for a rank-indexed bitmap) of the current row layout, holding at least
     the used items' rows (built once, shared by the multi-pass levels until the rows
     change); without it a used-item bitmap is built for each multi-pass level.
+    sup_frac: the minimum support as a fraction of the rows; when every frequent prefix
+    then expects >= 4 rows per slab (e^-4: ~2 % of a slab's prefixes empty at worst), the
+    slab kernel drops its all-zero-prefix test (DENSE_MIN_ROWS).
     Returns int64 counts [C] (ext order), or None when no LDS slab fits (the
     caller then uses the bitmap kernel)."""
     dev = ranks.device
@@ -1022,6 +1029,7 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
     st = _stream(ranks)
     bounds = passes[:, 2].tolist() + [C]
     nslabs = (W + sw - 1) // sw
+    dense = wword is None and DENSE_MIN_ROWS > 0 and sup_frac * sw * 64 >= DENSE_MIN_ROWS
     for q, (a, b, e0) in enumerate(passes.tolist()):
         Cq = bounds[q + 1] - e0
         if kern == 1:
@@ -1038,13 +1046,14 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
             _hip_call("fa_hip_count_slab_rec_cls", _p(roff), _p(ranks), _p(src), ncols, base + 4 * o_im, F1,
                       n_used, base + 4 * o_gpre, base + 4 * (o_rec + 12 * a), b - a, Cq, _p(wword),
                       out.data_ptr() + 4 * e0, sw, n_wg, _p(bm), bm.stride(0) if bm is not None else 0, st,
-                      bm_rows, None, int(info[23]))
+                      bm_rows, None, int(info[23]) | (2 if dense else 0))
     CLS_LEVELS[0] += int(info[23])
     LAST_LEVEL_PLAN.clear()
     LAST_LEVEL_PLAN.update(kernel="trie" if kern == 1 else "slab", rows=int(roff.numel() - 1), used=n_used, sw=sw,
                            cap=cap, passes=npass, pieces=int(info[4]), witems=int(info[5]), d1=int(info[7]),
                            d2=int(info[8]), trie_reads=int(info[9]), slab_reads=int(info[10]), m=m, C=C,
-                           cls=int(info[23]), step_reads=int(info[21]), step_reads_cls=int(info[22]))
+                           cls=int(info[23]), step_reads=int(info[21]), step_reads_cls=int(info[22]),
+                           dense=bool(dense))
     return out.to(_I64)
 
 

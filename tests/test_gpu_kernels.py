@@ -307,8 +307,8 @@ def test_slab_multipass_from_bitmap(monkeypatch):
     assert ref.as_dict() == got_w.as_dict()
 
 
-@pytest.mark.parametrize("lds_kb", [160, 24])
-def test_slab_class_layout_on_gpu(monkeypatch, lds_kb):
+@pytest.mark.parametrize("lds_kb,dense", [(160, 0), (24, 0), (24, 1e-9)])
+def test_slab_class_layout_on_gpu(monkeypatch, lds_kb, dense):
     # every slab pass in the class layout (plan.cpp cls_layout, FA_SLAB_CLS=2), so
     # k_count_slab_rec<.., kCls> runs single-pass (contiguous build) and multi-pass
     # (bitmap copy) levels; counts must equal the bitmap kernel's
@@ -318,6 +318,8 @@ def test_slab_class_layout_on_gpu(monkeypatch, lds_kb):
     ref = FastApriori(0.004, config=MinerConfig(trim_min_rows=0, level_kernel="bitmap", **cfg)).run(sh)
     monkeypatch.setattr(prim, "SLAB_CLS", 2)
     monkeypatch.setattr(prim, "_LDS_BYTES", lds_kb * 1024 - 512)
+    if dense:   # every level "dense": the slab kernel runs without its all-zero-prefix test
+        monkeypatch.setattr(prim, "DENSE_MIN_ROWS", dense)
     n0 = prim.CLS_LEVELS[0]
     got = FastApriori(0.004, config=MinerConfig(trim_min_rows=0, level_kernel="slab", **cfg)).run(sh.to(DEV))
     assert len(ref.levels) >= 5
