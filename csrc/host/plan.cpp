@@ -254,24 +254,27 @@ constexpr int kClsMaxRun = 8;              // pieces per class run (longer class
 constexpr double kClsMinGain = 0.8;        // class layout only when its wave-step reads are < 0.8x
 constexpr uint8_t kRecKeepQ = 1, kRecKeepP = 2;
 
-// Slab-row reads per lane summed over wave steps (the SIMT cost: a wave runs the
-// longest extension loop of its lanes, and a recompute if any lane needs one).
+// Critical path of a pass in slab-row reads per lane: the SIMT cost of a wave step (the
+// longest extension loop of its lanes, a recompute if any lane needs one, + 1 for the
+// record and loop), summed over each wave's steps; the busiest wave, since all 16 meet
+// at every slab's barrier.
 static int64_t slot_cost(const std::vector<SlabPiece>& pcs, const std::vector<int64_t>& slots,
                          const std::vector<uint8_t>& flags, int m) {
-  int64_t cost = 0;
+  int64_t wc[kSlabWg / 64] = {0};
   const int64_t n = (int64_t)slots.size();
   for (int64_t w0 = 0; w0 < n; w0 += 64) {
-    bool q = false, p = false;
+    bool q = false, p = false, any = false;
     int64_t e = 0;
     for (int64_t s = w0; s < std::min(n, w0 + 64); ++s) {
       if (slots[s] < 0) continue;
+      any = true;
       q = q || !(flags[s] & kRecKeepQ);
       p = p || !(flags[s] & kRecKeepP);
       e = std::max(e, pcs[slots[s]].hi - pcs[slots[s]].lo);
     }
-    cost += (q ? m - 1 : 0) + (p ? 1 : 0) + e;
+    if (any) wc[(w0 % kSlabWg) / 64] += (q ? m - 1 : 0) + (p ? 1 : 0) + e + 1;
   }
-  return cost;
+  return *std::max_element(wc, wc + kSlabWg / 64);
 }
 
 static void cls_layout(const std::vector<SlabPiece>& pcs, int64_t i, int64_t j, const int32_t* Pf,
@@ -292,17 +295,37 @@ static void cls_layout(const std::vector<SlabPiece>& pcs, int64_t i, int64_t j, 
   // wave read mostly the same prefix rows (LDS broadcast) -- measured better than
   // ordering them by extension counts
   std::stable_sort(runs.begin(), runs.end(), [&](const Run& x, const Run& y) { return x.s > y.s; });
-  // wave rows of 64 runs of one length, each to the least-loaded wave
+  // wave rows of <= 64 runs of one length, costliest first, each to the wave with the
+  // least estimated reads so far: the waves meet at every slab's barrier, so the
+  // critical path is the busiest wave (slot_cost)
   constexpr int NWv = kSlabWg / 64;
-  std::vector<std::vector<std::pair<int64_t, int64_t>>> rows_of(NWv);   // (first run, end run)
-  int64_t load[NWv] = {0};
+  struct Row { int64_t r0, r1, cost; };
+  std::vector<Row> rows;
   for (int64_t r = 0; r < (int64_t)runs.size();) {
     int64_t r1 = r + 1;
     while (r1 < (int64_t)runs.size() && r1 - r < 64 && runs[r1].s == runs[r].s) ++r1;
-    const int w = (int)(std::min_element(load, load + NWv) - load);
-    rows_of[w].push_back({r, r1});
-    load[w] += runs[r].s;
+    int64_t c = 0;
+    for (int e = 0; e < runs[r].s; ++e) {
+      int64_t mx = 0;
+      bool newp = e == 0;
+      for (int64_t x = r; x < r1; ++x) {
+        const int64_t k = runs[x].k0 + e;
+        mx = std::max(mx, pcs[k].hi - pcs[k].lo);
+        newp = newp || pcs[k].g != pcs[k - 1].g;
+      }
+      c += (e == 0 ? m - 1 : 0) + (newp ? 1 : 0) + mx + 1;   // + 1: per-step record and loop cost
+    }
+    rows.push_back({r, r1, c});
     r = r1;
+  }
+  std::stable_sort(rows.begin(), rows.end(), [](const Row& x, const Row& y) { return x.cost > y.cost; });
+  std::vector<std::vector<std::pair<int64_t, int64_t>>> rows_of(NWv);   // (first run, end run)
+  int64_t load[NWv] = {0}, wcost[NWv] = {0};
+  for (const Row& rw : rows) {
+    const int w = (int)(std::min_element(wcost, wcost + NWv) - wcost);
+    rows_of[w].push_back({rw.r0, rw.r1});
+    load[w] += runs[rw.r0].s;
+    wcost[w] += rw.cost;
   }
   const int64_t T = *std::max_element(load, load + NWv);
   slots.assign((size_t)(T * kSlabWg), -1);
