@@ -704,23 +704,30 @@ static int ag_chain_dev(const int32_t* P1, int64_t n1, int m1, int nw, char* w0,
 //   ctl (device int64 [kDlCtl]): 0 stop  1 accepted levels  2 total  3 last C
 //     5 multi (level 0 needs several accumulator passes: host path)  6 n_used
 //     7 end (|F_{k-1}| < k or C_0 = 0: mining is over)  8 + l: n_l  40 + l: C_l
+//     72 + l: G_l (parent rows with >= 1 candidate: the reference's group count)
 //     128 .. 191: used-item bitset of level 0 (4096 bits)
 // ---------------------------------------------------------------------------
 namespace fa {
 
 constexpr int kDlCtl = 256;
 
-__device__ int64_t agd_block_scan(const int32_t* __restrict__ cnt, int64_t* __restrict__ off, int64_t n) {
-  // exclusive offsets off[0 .. n] of cnt[0 .. n) by one 1024-thread workgroup; returns off[n]
+__device__ int64_t agd_block_scan(const int32_t* __restrict__ cnt, int64_t* __restrict__ off, int64_t n,
+                                  int64_t* groups = nullptr) {
+  // exclusive offsets off[0 .. n] of cnt[0 .. n) by one 1024-thread workgroup; returns off[n].
+  // groups (thread 0's copy): rows with cnt > 0, the reference's prefix-group count
+  // (genCandidates drops empty groups, FastApriori.scala:189-190)
   __shared__ int64_t part[16];
   __shared__ int64_t carry;
-  if (threadIdx.x == 0) { carry = 0; off[0] = 0; }
+  __shared__ unsigned int nz;
+  if (threadIdx.x == 0) { carry = 0; off[0] = 0; nz = 0u; }
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   for (int64_t b = 0; b < n; b += 1024) {
     const int64_t i = b + threadIdx.x;
     const int v = i < n ? cnt[i] : 0;
     const int incl = wave_scan_incl_dpp(v);
+    const unsigned long long had = __ballot(v > 0);
+    if (lane == 0 && had) atomicAdd(&nz, (unsigned int)__popcll(had));
     if (lane == 63) part[wv] = incl;
     __syncthreads();
     int64_t before = carry;
@@ -730,6 +737,7 @@ __device__ int64_t agd_block_scan(const int32_t* __restrict__ cnt, int64_t* __re
     if (threadIdx.x == 1023) carry = before + incl;
     __syncthreads();
   }
+  if (groups && threadIdx.x == 0) *groups = (int64_t)nz;
   return carry;
 }
 
@@ -753,9 +761,11 @@ __global__ __launch_bounds__(kDlCtl) void k_dl_setup0(long long* __restrict__ c,
 __global__ __launch_bounds__(1024) void k_dl_decide0(const int32_t* __restrict__ cnt, int64_t* __restrict__ off,
                                                       long long* __restrict__ c, int64_t c_bound) {
   if (c[0]) return;
-  const int64_t C = agd_block_scan(cnt, off, c[8]);
+  int64_t g = 0;
+  const int64_t C = agd_block_scan(cnt, off, c[8], &g);
   if (threadIdx.x != 0) return;
   c[40] = C;
+  c[72] = g;
   if (C == 0) { c[7] = 1; c[0] = 1; return; }
   if (C > c_bound) { c[5] = 1; c[0] = 1; return; }
   c[1] = 1; c[2] = C; c[3] = C; c[9] = C;
@@ -792,7 +802,8 @@ __global__ __launch_bounds__(1024) void k_dl_decide(const int32_t* __restrict__ 
                                                      long long* __restrict__ c, int l, double growth, int64_t c_bound,
                                                      double lds) {
   if (c[0]) return;
-  const int64_t C = agd_block_scan(cnt, off, c[8 + l]);
+  int64_t g = 0;
+  const int64_t C = agd_block_scan(cnt, off, c[8 + l], &g);
   if (threadIdx.x != 0) return;
   const int64_t total = c[2], last = c[3];
   if (C == 0 || (double)C > growth * (double)last || C > c_bound || total + C > d_slab_cap(c[6], total + C, lds)) {
@@ -800,6 +811,7 @@ __global__ __launch_bounds__(1024) void k_dl_decide(const int32_t* __restrict__ 
     return;
   }
   c[40 + l] = C;
+  c[72 + l] = g;
   c[1] = l + 1;
   c[2] = total + C;
   c[3] = C;

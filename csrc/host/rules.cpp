@@ -14,6 +14,7 @@
 //     fastapriori_amd/utils/jvm.py rule_tiebreak_key), then antecedent ranks.
 //   * recommend (:80-106): first rule in that order with antecedent subset of the
 //     basket and consequent not in the basket; otherwise "0".
+#include <chrono>
 #include <unordered_map>
 
 #include "fa_common.h"
@@ -25,7 +26,7 @@ struct RuleSet {
   std::vector<int32_t> ante;       // concatenated antecedent ranks (ascending)
   std::vector<int32_t> cons;
   std::vector<double> conf;
-  std::vector<int64_t> stats;      // per antecedent level: before, after (pairs)
+  std::vector<int64_t> stats;      // per antecedent level: before, after, cut microseconds
 };
 
 static inline int cmp_row(const int32_t* a, const int32_t* b, int m) {
@@ -85,8 +86,13 @@ FA_API RuleSet* fa_rules_build(const int32_t* const* rows, const int64_t* const*
   // level-wise cut
   std::vector<std::vector<char>> keep(raw.size());
   for (size_t L = 0; L < raw.size(); ++L) {
+    const auto t_cut = std::chrono::steady_clock::now();
     keep[L].assign(raw[L].size(), L == 0 ? 1 : 0);
-    if (L == 0) { rs->stats.push_back((int64_t)raw[0].size()); rs->stats.push_back((int64_t)raw[0].size()); continue; }
+    if (L == 0) {
+      rs->stats.push_back((int64_t)raw[0].size()); rs->stats.push_back((int64_t)raw[0].size());
+      rs->stats.push_back(0);
+      continue;
+    }
     // kept rules of the level below, keyed by (antecedent index, consequent)
     std::unordered_map<uint64_t, double> low;
     low.reserve(raw[L - 1].size() * 2);
@@ -120,6 +126,8 @@ FA_API RuleSet* fa_rules_build(const int32_t* const* rows, const int64_t* const*
     for (auto v : kept_t) kept += v;
     rs->stats.push_back((int64_t)raw[L].size());
     rs->stats.push_back(kept);
+    rs->stats.push_back((int64_t)std::chrono::duration_cast<std::chrono::microseconds>(
+        std::chrono::steady_clock::now() - t_cut).count());
   }
   // gather kept rules and sort
   struct Ref { int32_t level; int64_t idx; };

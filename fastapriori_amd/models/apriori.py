@@ -184,16 +184,19 @@ class FastApriori:
         F1 = len(counts1)
         self._F1, self._dev = F1, dev
         self._counts1 = counts1
-        self.log.line(f"1 freq items {F1}")
+        self.log.metric(phase="f1", frequent=F1)
         levels = [np.arange(F1, dtype=np.int32).reshape(-1, 1)]
         counts = [counts1]
         result = MiningResult(items, levels, counts, mc, n_global, self.stats,
                               item_hashes=None if shard.vocab.numeric else self._item_hashes)
-        self._result_items(result, wait=resume is not None or self.ckpt is not None)
+        # the device level loop reads its levels back once, at the end: its checkpoint
+        # levels are then written in one go (in the background: _finish), else per level
+        self._ckpt_saved = 0
+        self._ckpt_deferred = self.ckpt is not None and self._device_levels_planned(resume)
+        self._result_items(result, wait=resume is not None or (self.ckpt is not None and not self._ckpt_deferred))
         if resume is not None:
             self._check_resume(resume, result)
-        if self.ckpt is not None:
-            self.ckpt.save_level(result, 1)
+        self._ckpt_level(result, 1)
         if F1 < 2:
             return self._finish(result, t_start)
 
@@ -206,15 +209,15 @@ class FastApriori:
         b0 = self._bytes_moved()
         # F_2 may stay on the device (no readback between the pair kernel and the first
         # device bundle): its host copy then arrives with the run's one results readback
-        self._f2_defer = self._device_levels_planned(resume)
-        if resume is not None and len(resume.levels) >= 2:
+        resumed = 0 if resume is None else len(resume.levels)
+        self._f2_defer = self._device_levels_planned(resume) and resumed < 2
+        if resumed >= 2:
             levels.append(resume.levels[1]); counts.append(resume.counts[1])
         else:
             with roctx_range("pairs"), tm.phase("pairs"):
                 rows2, cnt2 = self._pairs(db, F1, mc)
             levels.append(rows2); counts.append(cnt2)
-            if self.ckpt is not None:
-                self.ckpt.save_level(result, 2)
+            self._ckpt_level(result, 2)
         self.log.line(f"2 candidates items {F1 * (F1 - 1) // 2}")
         self._level2_ms, self._level2_bytes = (time.perf_counter() - t0) * 1e3, self._bytes_moved() - b0
         if levels[1] is not None:
@@ -222,17 +225,21 @@ class FastApriori:
 
         # ---- k >= 3 ----------------------------------------------------
         k = 3
-        if self._device_levels_ok(resume):
+        while resumed >= k:                  # levels the checkpoint already holds
+            levels.append(resume.levels[k - 1]); counts.append(resume.counts[k - 1])
+            k += 1
+        if self._device_levels_ok(resume, levels):
             # device bundles while every bundle fits one accumulator pass; None when
             # mining is complete, else the level the host loop continues from
             k = self._mine_device(db, levels, counts, mc, result)
+            if k is not None and self._ckpt_deferred:
+                # the host loop checkpoints per level from here: the device levels first
+                self._ckpt_deferred = False
+                self._result_items(result)
+                self._ckpt_upto(result, len(levels), background=False)
         while k is not None and len(levels[-1]) >= k and (self.cfg.max_level == 0 or k <= self.cfg.max_level):
             t0 = time.perf_counter()
             b0 = self._bytes_moved()
-            if resume is not None and len(resume.levels) >= k:
-                levels.append(resume.levels[k - 1]); counts.append(resume.counts[k - 1])
-                k += 1
-                continue
             with roctx_range(f"level{k}"), tm.phase(f"level{k}"):
                 fused = self._gen_bundle_fused(k, levels[-1])
                 if fused is None:
@@ -242,7 +249,9 @@ class FastApriori:
                     prefix_idx, ext_off, ext, cand_rows = fused[0] if fused else (None, None, np.zeros(0, np.int32),
                                                                                   None)
                 C = int(ext.size)
-                self.log.line(f"{k} candidate items {C}")
+                # the reference logs candidates.length: its (prefix, extensions) groups
+                # (FastApriori.scala:114, :189-190)
+                self.log.line(f"{k} candidate items {0 if prefix_idx is None else int(prefix_idx.size)}")
                 if C == 0:
                     levels.append(np.zeros((0, k), np.int32)); counts.append(np.zeros(0, np.int64))
                     self.log.line(f"{k} freq items 0")
@@ -275,23 +284,25 @@ class FastApriori:
                     levels.append(np.ascontiguousarray(cand_k[keep], dtype=np.int32))
                     counts.append(cnt[keep].astype(np.int64))
             ms = (time.perf_counter() - t0) * 1e3
+            plan = ops.primitives.LAST_LEVEL_PLAN
+            hbm_b, moved = self._level_hbm_bytes(db, plan), self._bytes_moved() - b0
+            c_tot = max(sum(int(b[4].size) for b in bundle), 1)
             for j, (kk, pv, pi, eo, ex) in enumerate(bundle):
                 Fk = levels[kk - 1]
                 if kk > k and self.log.enabled:
-                    # the reference logs the candidates generated from F_{k-1}; a bundled
+                    # the reference logs the groups generated from F_{k-1}; a bundled
                     # level counted a superset generated from C_{k-1}
-                    self.log.line(f"{kk} candidate items {int(apriori_gen(levels[kk - 2])[2].size)}")
+                    self.log.line(f"{kk} candidate items {int(apriori_gen(levels[kk - 2])[0].size)}")
                 self.log.line(f"{kk} freq items {len(Fk)}")
-                self.log.line(f"Use Time {kk} items {int(ms) if j == 0 else 0}")
-                plan = ops.primitives.LAST_LEVEL_PLAN
+                # one launch counts the bundle: each level gets its candidates' share
+                share = int(ex.size) / c_tot
+                self.log.line(f"Use Time {kk} items {int(ms * share)}")
                 rec = dict(phase="level", k=kk, candidates=int(ex.size), frequent=len(Fk),
-                           ms=ms if j == 0 else 0.0, groups=int(pi.size), bundled_with=k,
-                           bytes_reduced=(self._bytes_moved() - b0) if j == 0 else 0,
-                           kernel=plan.get("kernel"),
-                           hbm_bytes_est=(self._level_hbm_bytes(db, plan) if j == 0 else 0))
-                self._level_recs.append((rec, f"level{k}" if j == 0 else None))
-                if self.ckpt is not None:
-                    self.ckpt.save_level(result, kk)
+                           ms=ms * share, groups=int(pi.size), bundled_with=k, bytes_reduced=int(moved * share),
+                           kernel=plan.get("kernel"), hbm_bytes_est=int(hbm_b * share) + 4 * int(ex.size) * (kk + 3),
+                           _share=share)
+                self._level_recs.append((rec, f"level{k}"))
+                self._ckpt_level(result, kk)
             k += len(bundle)
         # drop a trailing empty level (the reference never emits empty levels)
         while len(levels) > 1 and len(levels[-1]) == 0:
@@ -312,13 +323,29 @@ class FastApriori:
     # k >= 3 on the device (FastApriori.scala:110-121, :132-160)
     # ------------------------------------------------------------------
     def _device_levels_planned(self, resume) -> bool:
-        return (DEVICE_LEVELS and self._dev.type == "cuda" and resume is None
-                and self.ckpt is None and not self.cand_par and 2 <= self._F1 <= ops.primitives.DL_MAX_F1
+        return (DEVICE_LEVELS and self._dev.type == "cuda" and not self.cand_par
+                and 2 <= self._F1 <= ops.primitives.DL_MAX_F1
                 and self.cfg.level_kernel in ("auto", "slab") and self.stats["n_lines"] < (1 << 31)
                 and (self.cfg.max_level == 0 or self.cfg.max_level >= 3))
 
-    def _device_levels_ok(self, resume) -> bool:
-        return self._device_levels_planned(resume) and self._f2_dev is not None
+    def _device_levels_ok(self, resume, levels: list) -> bool:
+        """F_2 on the device (_pairs_on_device / _pairs), or a resumed checkpoint's last
+        level, uploaded by _mine_device as the first bundle's parent rows."""
+        if not self._device_levels_planned(resume):
+            return False
+        return self._f2_dev is not None or (resume is not None and len(levels) >= 2 and levels[-1] is not None)
+
+    def _ckpt_level(self, result: MiningResult, k: int) -> None:
+        """Checkpoint level k now (host level loop), unless the device loop's levels are
+        written together at the end (_ckpt_deferred)."""
+        if self.ckpt is not None and not self._ckpt_deferred:
+            self.ckpt.save_level(result, k)
+            self._ckpt_saved = max(self._ckpt_saved, k)
+
+    def _ckpt_upto(self, result: MiningResult, K: int, background: bool) -> None:
+        if self.ckpt is not None and K > self._ckpt_saved:
+            self.ckpt.save_levels(result, range(self._ckpt_saved + 1, K + 1), background=background)
+            self._ckpt_saved = K
 
     def _mine_device(self, db, levels: list, counts: list, mc: int, result: MiningResult):
         """Level bundles with no host round trip beyond the generator's (csrc/hip/gen.hip
@@ -342,11 +369,16 @@ class FastApriori:
         c_bound = int(lds // 4)
         st = torch.cuda.current_stream(self._dev).cuda_stream
         f2 = self._f2_dev
+        m0, k = 2, 3
+        if f2 is None:
+            # resumed from a checkpoint: its last level's rows are the first parents
+            last = np.ascontiguousarray(levels[-1], dtype=np.int32)
+            m0, k = last.shape[1], last.shape[1] + 1
+            f2 = self._resume_rows = torch.from_numpy(last.reshape(-1, m0)).to(self._dev)
         if self._f2_n_dev is not None:      # |F_2| only on the device; n_bound sizes the buffers
             P0, n_src, n_const, n_bound = f2.data_ptr(), self._f2_n_dev.data_ptr(), 0, self._f2_bound
         else:
             P0, n_src, n_const, n_bound = f2.data_ptr(), None, int(f2.shape[0]), int(f2.shape[0])
-        m0, k = 2, 3
         pend = []
         tm = self._timer
         nxt = None
@@ -404,9 +436,13 @@ class FastApriori:
                 with tm.phase("count"), roctx_range("count"):
                     self.comm.all_reduce_(cnt)
                     rows_a, cnt_a, ro, co = Pm.dl_threshold(S, L, cnt, mc, k)
-            pend.append(dict(k=k, L=L, m0=m0, C=Cs, rows=rows_a, cnt=cnt_a, ro=ro, co=co,
+            # HBM bytes the bundle's slab count streams (rows + offsets, one pass)
+            hbm_rows = (db["ranks"].numel() * db["ranks"].element_size()
+                        + db["roff"].numel() * db["roff"].element_size())
+            pend.append(dict(k=k, L=L, m0=m0, C=Cs, rows=rows_a, cnt=cnt_a, ro=ro, co=co, hbm_rows=int(hbm_rows),
+                             n_par=S.desc[:L, 5].copy(),
                              ms=(time.perf_counter() - t0) * 1e3, bytes=self._bytes_moved() - b0,
-                             groups=int((S.desc[:L, 5]).sum())))
+                             G=c[72:72 + L].copy()))
             P0 = rows_a.data_ptr() + 4 * int(ro[L - 1])
             n_src, n_const, n_bound = S.fsz.data_ptr() + 8 * (k + L - 1), 0, int(Cs[-1])
             m0 += L
@@ -490,18 +526,24 @@ class FastApriori:
                 levels.append(rows_h[a:a + F * w].reshape(F, w).copy())
                 counts.append(cnt_h[b:b + F].astype(np.int64))
                 if kk > p["k"] and self.log.enabled:
-                    # the reference logs the candidates generated from F_{k-1}; a bundled
+                    # the reference logs the groups generated from F_{k-1}; a bundled
                     # level counted a superset generated from C_{k-1}
-                    self.log.line(f"{kk} candidate items {int(apriori_gen(levels[kk - 2])[2].size)}")
+                    self.log.line(f"{kk} candidate items {int(apriori_gen(levels[kk - 2])[0].size)}")
                 elif self.log.enabled:
-                    self.log.line(f"{kk} candidate items {int(p['C'][l])}")
+                    self.log.line(f"{kk} candidate items {int(p['G'][l])}")
                 self.log.line(f"{kk} freq items {F}")
-                self.log.line(f"Use Time {kk} items {int(p['ms']) if l == 0 else 0}")
+                # one launch counts the whole bundle: a level's time, device time and
+                # streamed bytes are its candidates' share of the bundle's
+                share = float(p["C"][l]) / max(float(p["C"].sum()), 1.0)
+                self.log.line(f"Use Time {kk} items {int(p['ms'] * share)}")
+                m = p["m0"] + l              # parent row length of level kk
+                hbm = int(share * p["hbm_rows"] + 4 * int(p["n_par"][l]) * m
+                          + 4 * int(p["C"][l]) * (m + 1) + 3 * 4 * int(p["C"][l]))
                 self._level_recs.append((dict(phase="level", k=kk, candidates=int(p["C"][l]), frequent=F,
-                                              ms=p["ms"] if l == 0 else 0.0, groups=p["groups"] if l == 0 else 0,
-                                              bundled_with=p["k"], bytes_reduced=p["bytes"] if l == 0 else 0,
-                                              kernel="slab_dev", hbm_bytes_est=0),
-                                         f"level{p['k']}" if l == 0 else None))
+                                              ms=p["ms"] * share, groups=int(p["G"][l]), bundled_with=p["k"],
+                                              bytes_reduced=int(p["bytes"] * share), kernel="slab_rec_dev",
+                                              hbm_bytes_est=hbm, _share=share),
+                                         f"level{p['k']}"))
             ro_base += int(p["rows"].numel())
             co_base += int(p["cnt"].numel())
 
@@ -540,8 +582,9 @@ class FastApriori:
         if tm is not None and tm.events:
             self.stats["gpu_phase_ms"] = {k: round(v, 3) for k, v in gpu.items()}
         for rec, span in getattr(self, "_level_recs", []):
+            share = rec.pop("_share", 1.0)
             if span is not None and span in gpu:
-                rec["gpu_ms"] = round(gpu[span], 3)
+                rec["gpu_ms"] = round(gpu[span] * share, 3)
             self.log.metric(**rec)
         self._level_recs = []
         if os.environ.get("FA_TRACE") == "1" and tm is not None:
@@ -549,6 +592,10 @@ class FastApriori:
 
     def _finish(self, result: MiningResult, t_start: float) -> MiningResult:
         self._result_items(result)
+        if getattr(self, "_ckpt_deferred", False):
+            # every level in one batch, written by a background thread while the caller
+            # writes the outputs (Checkpointer.wait / mark_complete join it)
+            self._ckpt_upto(result, len(result.levels), background=True)
         db = getattr(self, "_db_local", None)
         if db is not None:
             # layout sizes for the metrics, one collective after the last level

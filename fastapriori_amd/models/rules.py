@@ -58,13 +58,19 @@ class AssociationRules:
             if self.device.type == "cuda":
                 d = ops.primitives.rules_build_device(self.result.levels, self.result.counts, tie_pos, self.device)
                 self._rules = RuleTable(d["ante_off"].cpu().numpy(), d["ante"].cpu().numpy(),
-                                        d["cons"].cpu().numpy(), d["conf"].cpu().numpy(), d["level_stats"])
+                                        d["cons"].cpu().numpy(), d["conf"].cpu().numpy(), d["level_stats"],
+                                        d["level_ms"])
                 self._rules_dev = (self.device, d["ante_off"], d["ante"], d["cons"])
             else:
                 self._rules = rules_build(self.result.levels, self.result.counts, tie_pos)
-            for size, before, after in self._rules.level_stats[1:]:
+            # the cut's log lines per antecedent size (AssociationRules.scala:155,177,181),
+            # then the rule total (:75)
+            ms = list(self._rules.level_ms) + [0.0] * len(self._rules.level_stats)
+            for (size, before, after), t in zip(self._rules.level_stats[1:], ms[1:]):
                 self.log.line(f"Before cut level {size} Nums: {before}")
                 self.log.line(f"After cut level {size} Nums: {after}")
+                self.log.line(f"Use Time cut leaves {size} Time: {int(t)}")
+                self.log.metric(phase="rule_cut", level=size, before=before, after=after, ms=round(t, 3))
             self.log.line(f"Size association rules {self._rules.n_rules}")
         return self._rules
 

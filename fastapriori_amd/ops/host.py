@@ -2,7 +2,7 @@
 from __future__ import annotations
 
 import ctypes as C
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import numpy as np
 
@@ -38,6 +38,7 @@ class RuleTable:
     cons: np.ndarray       # int32 [R]
     conf: np.ndarray       # float64 [R]
     level_stats: list      # [(antecedent size, before cut, after cut)]
+    level_ms: list = field(default_factory=list)   # [ms of each level's cut], same order
 
     @property
     def n_rules(self) -> int:
@@ -72,9 +73,10 @@ def rules_build(levels: list[np.ndarray], counts: list[np.ndarray], tie_pos: np.
     lib.fa_rules_export(h, ante_off.ctypes.data, ante.ctypes.data, cons.ctypes.data, conf.ctypes.data,
                         stats.ctypes.data)
     lib.fa_rules_free(h)
-    st = stats[:ns].reshape(-1, 2)
-    level_stats = [(i + 1, int(b), int(a)) for i, (b, a) in enumerate(st.tolist())]
-    return RuleTable(ante_off, ante[:na], cons[:R], conf[:R], level_stats)
+    st = stats[:ns].reshape(-1, 3)
+    level_stats = [(i + 1, int(b), int(a)) for i, (b, a, _) in enumerate(st.tolist())]
+    level_ms = [us / 1e3 for _, _, us in st.tolist()]
+    return RuleTable(ante_off, ante[:na], cons[:R], conf[:R], level_stats, level_ms)
 
 
 @dataclass

@@ -15,6 +15,7 @@ from __future__ import annotations
 import ctypes as C
 import ctypes
 import os
+import time
 
 import numpy as np
 import torch
@@ -1245,7 +1246,7 @@ def rules_build_device(levels: list, counts: list, tie_pos: np.ndarray, dev) -> 
     K = len(levels)
     empty = dict(ante_off=torch.zeros(1, dtype=_I64, device=dev), ante=torch.zeros(0, dtype=_I32, device=dev),
                  cons=torch.zeros(0, dtype=_I32, device=dev), conf=torch.zeros(0, dtype=torch.float64, device=dev),
-                 level_stats=[])
+                 level_stats=[], level_ms=[])
     if K < 2 or len(levels[1]) == 0:
         return empty
     lv = [np.ascontiguousarray(l, dtype=np.int32).reshape(-1) for l in levels]
@@ -1267,10 +1268,12 @@ def rules_build_device(levels: list, counts: list, tie_pos: np.ndarray, dev) -> 
     kept_prev = conf_prev = None
     parts = []          # per level: (flat rule ids kept, conf, sub)
     stats = []
+    level_ms = []       # wall ms of each level's generation + cut (the nonzero readback syncs)
     for k in range(2, K + 1):
         nS, nA = len(levels[k - 1]), len(levels[k - 2])
         if nS == 0:
             break
+        t_lv = time.perf_counter()
         sub = torch.empty(nS * k, dtype=_I32, device=dev)
         conf = torch.empty(nS * k, dtype=torch.float64, device=dev)
         _native.check(lib.fa_hip_rule_gen(rows(k), nS, k, rows(k - 1), nA, cnts(k), cnts(k - 1), _p(sub), _p(conf),
@@ -1284,11 +1287,12 @@ def rules_build_device(levels: list, counts: list, tie_pos: np.ndarray, dev) -> 
         ids = torch.nonzero(kept).flatten()
         parts.append((k, ids, conf, sub))
         stats.append((k - 1, nS * k, ids.numel()))
+        level_ms.append((time.perf_counter() - t_lv) * 1e3)
         kept_prev, conf_prev = kept, conf
     conf_r = torch.cat([c[i] for _, i, c, _ in parts])
     R = conf_r.numel()
     if R == 0:
-        return dict(empty, level_stats=stats)
+        return dict(empty, level_stats=stats, level_ms=level_ms)
     cons_r = torch.cat([rows_all[int(base[k]):int(base[k + 1])][i] for k, i, _, _ in parts])
     ante_idx = torch.cat([s[i] for _, i, _, s in parts])
     msz = torch.cat([torch.full((i.numel(),), k - 1, dtype=_I32, device=dev) for k, i, _, _ in parts])
@@ -1311,7 +1315,7 @@ def rules_build_device(levels: list, counts: list, tie_pos: np.ndarray, dev) -> 
     _native.check(lib.fa_hip_rule_emit(_p(rows_all), _p(base_t), _p(msz_s), _p(idx_s), _p(ante_off), R, _p(ante), st),
                   "fa_hip_rule_emit")
     return dict(ante_off=ante_off, ante=ante, cons=cons_r[o].contiguous(), conf=conf_r[o].contiguous(),
-                level_stats=stats)
+                level_stats=stats, level_ms=level_ms)
 
 
 def _device_lines(buf: torch.Tensor, n: int, last_is_term: bool):

@@ -100,6 +100,7 @@ def run_job(cfg: JobConfig, comm=None) -> dict:
             miner = FastApriori(cfg.min_support, comm, mcfg, log, ckpt)
             result = miner.run(shard, resume=resume)
             summary["miner"] = dict(miner.stats)
+            summary["device_bundles"] = int(miner.stats.get("device_bundles", 0))
             trace = summary["miner"].pop("trace", None)
             if cfg.profile and trace is not None and comm.is_root:
                 # Chrome trace of the mining phases (host spans + hipEvent device spans)
@@ -108,8 +109,6 @@ def run_job(cfg: JobConfig, comm=None) -> dict:
                     json.dump({"traceEvents": trace, "displayTimeUnit": "ms"}, f)
                 summary["trace_path"] = tpath
             del shard
-            if ckpt is not None:
-                ckpt.mark_complete(result)
             t_write = time.time()
             if comm.is_root:
                 io.write_freq_itemsets(result, out_freq, overwrite=cfg.overwrite)
@@ -118,6 +117,9 @@ def run_job(cfg: JobConfig, comm=None) -> dict:
                                            overwrite=cfg.overwrite)
                     io.write_items_to_rank(result, cfg.output + "ItemsToRank")
                     io.write_freq_items(result, cfg.output + "FreqItems")
+            if ckpt is not None:
+                # joins the checkpoint writer the device level loop started in the background
+                ckpt.mark_complete(result)
         comm.barrier()
         if not cfg.rules_only:
             summary["write_ms"] = round((time.time() - t_write) * 1000, 1)

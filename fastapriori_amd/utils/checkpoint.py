@@ -31,6 +31,8 @@ class Checkpointer:
         self.dir = os.path.join(temp, "fastapriori_ckpt")
         self.rank = rank
         self.fingerprint = fingerprint or {}
+        self._thread = None           # background writer of save_levels(background=True)
+        self._error = None
         if rank == 0:
             os.makedirs(self.dir, exist_ok=True)
 
@@ -39,7 +41,15 @@ class Checkpointer:
         write(tmp)
         os.replace(tmp, path)
 
-    def save_level(self, result: MiningResult, k: int) -> None:
+    @staticmethod
+    def fault_level(rank: int) -> int:
+        """FA_FAULT_AT_LEVEL for this rank (0: no injected fault)."""
+        fault = os.environ.get("FA_FAULT_AT_LEVEL")
+        if fault and rank == int(os.environ.get("FA_FAULT_RANK", "0")):
+            return int(fault)
+        return 0
+
+    def _write_level(self, result: MiningResult, k: int) -> None:
         if self.rank == 0 and k <= len(result.levels):
             def w(tmp):
                 with open(tmp, "wb") as f:
@@ -49,21 +59,65 @@ class Checkpointer:
                     "levels_done": k, "fingerprint": self.fingerprint}
             self._atomic(os.path.join(self.dir, "meta.json"),
                          lambda tmp: open(tmp, "w", encoding="utf-8").write(json.dumps(meta)))
-        fault = os.environ.get("FA_FAULT_AT_LEVEL")
-        if fault and int(fault) == k and self.rank == int(os.environ.get("FA_FAULT_RANK", "0")):
+
+    def save_level(self, result: MiningResult, k: int) -> None:
+        self.wait()
+        self._write_level(result, k)
+        if self.fault_level(self.rank) == k:
             raise InjectedFault(17)
 
+    def save_levels(self, result: MiningResult, ks, background: bool = False) -> None:
+        """Levels ks (ascending), meta.json rewritten after each, so a crash part-way
+        leaves a consistent checkpoint of the levels before it.  background: written by
+        a thread while the caller goes on (the device level loop hands its levels over
+        in one go after its single results readback); wait() joins it.  An injected
+        fault at one of the levels is taken synchronously: the levels up to it are
+        written, then the process exits as save_level's would."""
+        self.wait()
+        ks = list(ks)
+        fault = self.fault_level(self.rank)
+        if fault and fault in ks:
+            for k in ks[:ks.index(fault) + 1]:
+                self._write_level(result, k)
+            raise InjectedFault(17)
+        if self.rank != 0 or not ks:
+            return
+        if not background:
+            for k in ks:
+                self._write_level(result, k)
+            return
+        import threading
+
+        def work():
+            try:
+                for k in ks:
+                    self._write_level(result, k)
+            except BaseException as e:       # surfaced by wait()
+                self._error = e
+
+        self._thread = threading.Thread(target=work, name="fa-ckpt", daemon=True)
+        self._thread.start()
+
+    def wait(self) -> None:
+        t, self._thread = self._thread, None
+        if t is not None:
+            t.join()
+        if self._error is not None:
+            e, self._error = self._error, None
+            raise e
+
     def mark_complete(self, result: MiningResult) -> None:
+        self.wait()
         if self.rank == 0:
             path = os.path.join(self.dir, "meta.json")
             meta = json.load(open(path, encoding="utf-8")) if os.path.exists(path) else {}
             meta.update(items=result.items, min_count=result.min_count, n_lines=result.n_lines,
                         levels_done=len(result.levels), complete=True, fingerprint=self.fingerprint)
-            self._atomic(path, lambda tmp: open(tmp, "w", encoding="utf-8").write(json.dumps(meta)))
             for k in range(1, len(result.levels) + 1):
                 f = os.path.join(self.dir, f"level_{k}.npz")
                 if not os.path.exists(f):
-                    self.save_level(result, k)
+                    self._write_level(result, k)
+            self._atomic(path, lambda tmp: open(tmp, "w", encoding="utf-8").write(json.dumps(meta)))
 
     def load(self, require_complete: bool = False) -> MiningResult | None:
         path = os.path.join(self.dir, "meta.json")

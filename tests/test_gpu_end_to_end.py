@@ -15,13 +15,21 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _job_record(path):
+    import json
+    recs = [json.loads(l) for l in open(path)]
+    return [r for r in recs if r.get("phase") == "job"][-1]
+
+
 def test_cli_on_gpu_matches_oracle(tmp_path):
+    # the reference's three-argument form (input output temp: checkpointing on) mines
+    # through the device level bundles, and its checkpoint is complete and resumable
     write_quest_file(str(tmp_path / "D.dat"), 2000, 8.0, 3.0, 40, 40, seed=6)
     write_quest_file(str(tmp_path / "U.dat"), 500, 8.0, 3.0, 40, 40, seed=6, users=True)
     env = dict(os.environ, PYTHONPATH=ROOT)
     r = subprocess.run([sys.executable, "-m", "fastapriori_amd", f"{tmp_path}/", f"{tmp_path}/o_", f"{tmp_path}/t",
-                        "--min-support", "0.03", "--device", "cuda"], capture_output=True, text=True, env=env,
-                       timeout=600)
+                        "--min-support", "0.03", "--device", "cuda", "--metrics", f"{tmp_path}/m.jsonl"],
+                       capture_output=True, text=True, env=env, timeout=600)
     assert r.returncode == 0, r.stderr
     d = open(tmp_path / "D.dat").read().splitlines()
     u = open(tmp_path / "U.dat").read().splitlines()
@@ -30,6 +38,38 @@ def test_cli_on_gpu_matches_oracle(tmp_path):
     # ties in F1 counts are ordered identically (count desc, Java string asc) -> exact lines
     assert got == lines
     assert open(tmp_path / "o_recommends/part-00000").read().splitlines() == recs
+    assert _job_record(f"{tmp_path}/m.jsonl")["device_bundles"] > 0
+    from fastapriori_amd.utils.checkpoint import Checkpointer
+    ck = Checkpointer(str(tmp_path / "t")).load(require_complete=True)
+    assert ck is not None
+    got_ck = {frozenset(ck.items[r] for r in s): c for s, c in ck.as_dict().items()}
+    want = {frozenset(res.items[r] for r in s): c for s, c in res.itemsets.items()}
+    assert got_ck == want
+
+
+def test_cli_fault_then_resume_on_gpu(tmp_path):
+    # an injected crash after level 3 on the device path, then --resume: the device
+    # loop restarts from the checkpoint's last level (uploaded as the first parents)
+    write_quest_file(str(tmp_path / "D.dat"), 3000, 9.0, 4.0, 40, 40, seed=3)
+    write_quest_file(str(tmp_path / "U.dat"), 400, 9.0, 4.0, 40, 40, seed=3, users=True)
+    env = dict(os.environ, PYTHONPATH=ROOT, FA_FAULT_AT_LEVEL="3")
+    args = [sys.executable, "-m", "fastapriori_amd", f"{tmp_path}/", f"{tmp_path}/a_", f"{tmp_path}/tmp",
+            "--min-support", "0.02", "--device", "cuda", "--metrics", f"{tmp_path}/m.jsonl"]
+    r = subprocess.run(args, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 17, r.stderr[-3000:]
+    assert not os.path.exists(tmp_path / "a_freqItemset")
+    from fastapriori_amd.utils.checkpoint import Checkpointer
+    ck = Checkpointer(str(tmp_path / "tmp")).load()
+    assert ck is not None and len(ck.levels) == 3 and not ck.stats.get("complete")
+    env.pop("FA_FAULT_AT_LEVEL")
+    r = subprocess.run(args + ["--resume"], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert _job_record(f"{tmp_path}/m.jsonl")["device_bundles"] > 0
+    d = open(tmp_path / "D.dat").read().splitlines()
+    u = open(tmp_path / "U.dat").read().splitlines()
+    lines, recs, _ = run_oracle(d, u, 0.02)
+    assert open(tmp_path / "a_freqItemset/part-00000").read().splitlines() == lines
+    assert open(tmp_path / "a_recommends/part-00000").read().splitlines() == recs
 
 
 def test_cli_under_torchrun_rccl_matches_oracle(tmp_path):
