@@ -132,15 +132,37 @@ def _declare(lib, sigs):
     return lib
 
 
+BUILD_IDS: dict = {}     # loaded library -> (embedded FA_BUILD_ID, id of the sources next to it)
+
+
+def _check_id(kind: str, lib, path: str) -> None:
+    """The loaded library must have been built from the sources in this tree
+    (ops/build.py source_id): a stale or foreign build fails loudly instead of
+    running code the tree does not hold.  FA_HIP_LIB (another build for A/B runs)
+    and a tree without sources (an installed copy) are recorded, not checked."""
+    fn = lib.fa_build_id
+    fn.restype, fn.argtypes = cp, []
+    got = fn().decode("ascii", "replace")
+    have_src = bool(_build.hip_sources() if kind == "hip" else _build.host_sources())
+    want = _build.source_id(kind) if have_src else None
+    BUILD_IDS[kind] = (got, want, path)
+    override = kind == "hip" and bool(os.environ.get("FA_HIP_LIB"))
+    if want is not None and got != want and not override:
+        raise RuntimeError(f"{path} was built from other sources (build id {got}, these sources {want}): "
+                           "rebuild with `python -m fastapriori_amd.ops.build`")
+
+
 def host():
     global _host
     if _host is None:
         with _lock:
             if _host is None:
                 path = _build.HOST_LIB
-                if not os.path.exists(path):
+                if _build.embedded_id(path) != _build.source_id("host") and _build.host_sources():
                     _build.build_host()
-                _host = _declare(C.CDLL(path), _HOST_SIGS)
+                lib = C.CDLL(path)
+                _check_id("host", lib, path)
+                _host = _declare(lib, _HOST_SIGS)
     return _host
 
 
@@ -157,7 +179,9 @@ def hip():
                     raise RuntimeError(
                         f"{path} is missing: build it with `python -m fastapriori_amd.ops.build` "
                         "(the GPU path has no non-native fallback)")
-                _hip = _declare(C.CDLL(path), _HIP_SIGS)
+                lib = C.CDLL(path)
+                _check_id("hip", lib, path)
+                _hip = _declare(lib, _HIP_SIGS)
     return _hip
 
 
