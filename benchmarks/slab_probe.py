@@ -1,7 +1,7 @@
 """Time decomposition of the k >= 3 slab kernel on a real mining run.
 
 Mines a config once, recording the arguments of every ops.count_level call
-(slab or trie kernel, bundles included), then replays each call under FA_SLAB_DEBUG = 0 (full), 1 (no slab build),
+(slab kernel, bundles included), then replays each call under FA_SLAB_DEBUG = 0 (full), 1 (no slab build),
 2 (no counting), 3 (neither: launch + prefetch + final atomics) and prints the
 per-level times (CUDA events, median of --reps).
 
@@ -29,47 +29,36 @@ def main():
     ap.add_argument("--config", default="T10I4D100M")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--modes", default="0,1,2,3")
-    ap.add_argument("--sw", default="", help="comma list of FA_SLAB_SW values to replay (default: planner)")
     a = ap.parse_args()
     n, L, I, P, N, ms = bench.CONFIGS[a.config]
     shard = generate_shard(n, Comm(), "cuda", L, I, P, N, 1)
     calls = []
     real = ops.count_level
-    real_dfs = ops.primitives.count_bundle_dfs
 
     def rec(*args, **kw):
         calls.append((real, args, kw))
         return real(*args, **kw)
 
-    def rec_dfs(*args, **kw):
-        calls.append((real_dfs, args, kw))
-        return real_dfs(*args, **kw)
-
     apriori.ops.count_level = rec
-    ops.primitives.count_bundle_dfs = rec_dfs
     FastApriori(ms, config=MinerConfig(min_support=ms)).run(shard)
     apriori.ops.count_level = real
-    ops.primitives.count_bundle_dfs = real_dfs
     out = []
     for i, (fn, args, kw) in enumerate(calls):
-        for sw in (a.sw.split(",") if a.sw else [""]):
-            os.environ["FA_SLAB_SW"] = sw or "0"
-            row = {"call": i, "fn": fn.__name__, "force_sw": sw}
-            for mode in a.modes.split(","):
-                os.environ["FA_SLAB_DEBUG"] = mode
-                ts = []
-                for _ in range(a.reps):
-                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                    e0.record()
-                    fn(*args, **kw)
-                    e1.record()
-                    torch.cuda.synchronize()
-                    ts.append(e0.elapsed_time(e1))
-                row[f"mode{mode}_ms"] = round(sorted(ts)[len(ts) // 2], 3)
-            row.update(ops.primitives.LAST_LEVEL_PLAN)
-            out.append(row)
-            print(json.dumps(row), flush=True)
-        os.environ["FA_SLAB_SW"] = "0"
+        row = {"call": i, "fn": fn.__name__}
+        for mode in a.modes.split(","):
+            os.environ["FA_SLAB_DEBUG"] = mode
+            ts = []
+            for _ in range(a.reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                fn(*args, **kw)
+                e1.record()
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            row[f"mode{mode}_ms"] = round(sorted(ts)[len(ts) // 2], 3)
+        row.update(ops.primitives.LAST_LEVEL_PLAN)
+        out.append(row)
+        print(json.dumps(row), flush=True)
     os.environ["FA_SLAB_DEBUG"] = "0"
 
 

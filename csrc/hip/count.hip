@@ -990,9 +990,6 @@ __global__ __launch_bounds__(256) void k_count_candidates(
 // per workgroup at the end.
 // ---------------------------------------------------------------------------
 constexpr int kSlabThreads = 1024;
-#ifndef FA_TRIE_NQ
-#define FA_TRIE_NQ 2
-#endif
 
 // Slab build modes: per-column rank prefetch (dedup: columns gather rows through
 // src), wave-cooperative coalesced build (columns = rows, contiguous ranks), or
@@ -1101,12 +1098,12 @@ __device__ __forceinline__ void slab_build_word(uint64_t* __restrict__ slab, int
 // round trip per 16 B a thread copies (~8-10 per slab at 1024 threads);
 // here every thread issues all its loads (after one batched load of the
 // bitmap row ids) before its first LDS store.  ROWW: LDS row stride in words;
-// kSwz: the trie kernel's word XOR ((u << 2) & (SW - 4)).
+// kSwz: an XOR of the word slot by ((u << 2) & (SW - 4)) (rotated row layouts).
 template <int SW, int ROWW, bool kSwz>
 __device__ __forceinline__ void slab_copy_bm(uint4* lds4, int n_used, const uint64_t* __restrict__ bm, int64_t Wp,
                                              const int32_t* __restrict__ bm_rows, int64_t w0, int64_t W) {
   constexpr int QW = SW / 2;                 // uint4 per row
-  constexpr int KMAX = 4;                    // loads in flight per thread (more: the trie kernel spills)
+  constexpr int KMAX = 4;                    // loads in flight per thread
   const int total = n_used * QW;
   for (int base = 0; base < total; base += KMAX * kSlabThreads) {
     int32_t br[KMAX];
@@ -1137,183 +1134,12 @@ __device__ __forceinline__ void slab_copy_bm(uint4* lds4, int n_used, const uint
   }
 }
 
-// kDfs (bundles of levels, unit weights): a work piece is a prefix plus up to 8
-// depth-1 nodes (candidates of level k) and, under each, its depth-2 nodes (the
-// level k+1 candidates whose prefix is that level-k candidate).  The AND of a
-// depth-1 node is counted and kept in registers for its children, so a level
-// k+1 candidate costs one slab-row read instead of its whole k-item prefix.
-//   gext_off[2g..2g+1]: node-1 range of piece g;  gext: int4 node-1 (slab row,
-//   output index, node-2 begin, node-2 end);  dfs2: int2 node-2 (slab row, output).
-template <int SW, bool kWeighted, int kBuild, bool kDfs = false>
-__global__ __launch_bounds__(kSlabThreads) void k_count_slab(
-    const int64_t* __restrict__ roff, const int32_t* __restrict__ ranks, const int32_t* __restrict__ src,
-    int64_t ncols, const int32_t* __restrict__ item_map, int n_used, const int32_t* __restrict__ gpre, int m,
-    const int32_t* __restrict__ gext_off, const int32_t* __restrict__ gext, int G, int C,
-    const int32_t* __restrict__ wword, uint32_t* __restrict__ out, const uint64_t* __restrict__ bm,
-    int64_t Wp, int dbg, const int32_t* __restrict__ gpm, const int32_t* __restrict__ bm_rows,
-    const int32_t* __restrict__ dfs2 = nullptr, int nA = 0, uint32_t* __restrict__ outB = nullptr) {
-  // nA / outB (multi-pass DFS): accumulators [0, nA) go to out, [nA, C) to outB
-  extern __shared__ uint4 lds4[];                  // 16-B aligned base
-  __shared__ unsigned long long build_words[kSlabThreads / 64 * 2];   // window_starts scratch
-  constexpr int SWP = SW + 2;                       // row stride: 16-B aligned, odd number of 16-B slots
-  constexpr int CPT = SW * 64 / kSlabThreads > 0 ? SW * 64 / kSlabThreads : 1;   // columns per thread
-  constexpr int RPC = 32 / CPT;                     // ranks per column prefetched in registers
-  uint64_t* slab = reinterpret_cast<uint64_t*>(lds4);
-  uint32_t* acc = reinterpret_cast<uint32_t*>(slab + (size_t)n_used * SWP);
-  for (int i = threadIdx.x; i < C; i += blockDim.x) acc[i] = 0;
-  const int64_t W = (ncols + 63) >> 6;
-  const int64_t nslabs = (W + SW - 1) / SW;
-
-  // register prefetch of the next slab's columns: row start, length, first RPC ranks
-  int64_t pbeg[CPT], plen[CPT];
-  int32_t pv[CPT][RPC];
-  auto prefetch = [&](int64_t sb) {
-    if (kBuild != kBuildCols) return;
-#pragma unroll
-    for (int c = 0; c < CPT; ++c) {
-      const int j = threadIdx.x + c * kSlabThreads;
-      const int64_t col = sb * SW * 64 + j;
-      int64_t row = -1;
-      if (sb < nslabs && j < SW * 64 && col < ncols) row = src ? (int64_t)src[col] : col;
-      pbeg[c] = row >= 0 ? roff[row] : 0;
-      plen[c] = row >= 0 ? roff[row + 1] - pbeg[c] : 0;
-#pragma unroll
-      for (int r = 0; r < RPC; ++r) pv[c][r] = r < plen[c] ? ranks[pbeg[c] + r] : 0;
-    }
-  };
-  prefetch(blockIdx.x);
-  for (int64_t sb = blockIdx.x; sb < nslabs; sb += gridDim.x) {
-    const int64_t w0 = sb * SW;
-    __syncthreads();
-    if (dbg & 1) {
-      // profiling split (FA_SLAB_DEBUG=1): no slab build
-    } else if (kBuild == kBuildBM) {
-      // multi-pass level: the used-item bitmap is materialised once; copy the slab tile
-      // (bm_rows: slab row -> bitmap row when the bitmap holds every item)
-      slab_copy_bm<SW, SWP, false>(lds4, n_used, bm, Wp, bm_rows, w0, W);
-    } else {
-      {
-        uint4* s4 = lds4;
-        const uint4 z = make_uint4(0, 0, 0, 0);
-        for (int i = threadIdx.x; i < n_used * SWP / 2; i += blockDim.x) s4[i] = z;
-      }
-      __syncthreads();
-      if (kBuild == kBuildContig) {
-        constexpr int NW = kSlabThreads / 64;                 // waves
-        constexpr int NSUB = NW > SW ? NW / SW : 1;           // waves per word
-        const int wv = threadIdx.x >> 6;
-        for (int q = wv / NSUB; q < SW; q += NW / NSUB)
-          if ((w0 + q) * 64 < ncols)
-            slab_build_word(slab, SWP, q, (w0 + q) * 64, ncols, roff, ranks, item_map, wv % NSUB, NSUB,
-                            build_words + wv * 2);
-      } else {
-#pragma unroll
-      for (int c = 0; c < CPT; ++c) {
-        const int j = threadIdx.x + c * kSlabThreads;
-        const unsigned long long bit = 1ull << (j & 63);
-        uint64_t* base = slab + (j >> 6);
-        int32_t u[RPC];
-#pragma unroll
-        for (int r = 0; r < RPC; ++r) u[r] = r < plen[c] ? item_map[pv[c][r]] : -1;
-#pragma unroll
-        for (int r = 0; r < RPC; ++r)
-          if (u[r] >= 0) atomicOr((unsigned long long*)(base + (size_t)u[r] * SWP), bit);
-        for (int64_t r = RPC; r < plen[c]; ++r) {   // long rows: rest straight from global
-          const int uu = item_map[ranks[pbeg[c] + r]];
-          if (uu >= 0) atomicOr((unsigned long long*)(base + (size_t)uu * SWP), bit);
-        }
-      }
-      }
-    }
-    __syncthreads();
-    prefetch(sb + gridDim.x);                       // overlaps the counting below
-    int32_t wt[SW];
-#pragma unroll
-    for (int q = 0; q < SW; ++q) wt[q] = kWeighted ? ((w0 + q < W) ? wword[w0 + q] : 0) : 1;
-    // work pieces: a prefix with <= 8 extensions, host-sorted by size so the lanes of
-    // a wave run loops of (nearly) equal length (FA_SLAB_DEBUG=2: no counting)
-    for (int g = threadIdx.x; g < ((dbg & 2) ? 0 : G); g += blockDim.x) {
-      uint4 p[SW / 2];
-      // gpm: per-piece (prefix offset, length) when levels of different k share a launch
-      const int32_t* pr = gpm ? gpre + gpm[2 * g] : gpre + (size_t)g * m;
-      const int mg = gpm ? gpm[2 * g + 1] : m;
-      {
-        const uint4* r0 = lds4 + (size_t)pr[0] * (SWP / 2);
-#pragma unroll
-        for (int q = 0; q < SW / 2; ++q) p[q] = r0[q];
-      }
-      for (int j = 1; j < mg; ++j) {
-        const uint4* rj = lds4 + (size_t)pr[j] * (SWP / 2);
-#pragma unroll
-        for (int q = 0; q < SW / 2; ++q) {
-          const uint4 v = rj[q];
-          p[q].x &= v.x; p[q].y &= v.y; p[q].z &= v.z; p[q].w &= v.w;
-        }
-      }
-      uint32_t any = 0;
-#pragma unroll
-      for (int q = 0; q < SW / 2; ++q) any |= p[q].x | p[q].y | p[q].z | p[q].w;
-      if (!any) continue;
-      if constexpr (kDfs) {
-        const int4* n1 = reinterpret_cast<const int4*>(gext);
-        const int2* n2 = reinterpret_cast<const int2*>(dfs2);
-        for (int i = gext_off[2 * g], i1 = gext_off[2 * g + 1]; i < i1; ++i) {
-          const int4 nd = n1[i];
-          const uint4* re = lds4 + (size_t)nd.x * (SWP / 2);
-          uint4 v1[SW / 2];
-          uint32_t s = 0;
-#pragma unroll
-          for (int q = 0; q < SW / 2; ++q) {
-            const uint4 v = re[q];
-            v1[q].x = p[q].x & v.x; v1[q].y = p[q].y & v.y; v1[q].z = p[q].z & v.z; v1[q].w = p[q].w & v.w;
-            s += __popc(v1[q].x) + __popc(v1[q].y) + __popc(v1[q].z) + __popc(v1[q].w);
-          }
-          acc[nd.y] += s;
-          if (!s) continue;                          // no column holds the node: children are 0
-          for (int j = nd.z; j < nd.w; ++j) {
-            const int2 c2 = n2[j];
-            const uint4* r2 = lds4 + (size_t)c2.x * (SWP / 2);
-            uint32_t s2 = 0;
-#pragma unroll
-            for (int q = 0; q < SW / 2; ++q) {
-              const uint4 v = r2[q];
-              s2 += __popc(v1[q].x & v.x) + __popc(v1[q].y & v.y) + __popc(v1[q].z & v.z) + __popc(v1[q].w & v.w);
-            }
-            acc[c2.y] += s2;
-          }
-        }
-        continue;
-      }
-      for (int e = gext_off[2 * g], e1 = gext_off[2 * g + 1]; e < e1; ++e) {
-        const uint4* re = lds4 + (size_t)gext[e] * (SWP / 2);
-        uint32_t s = 0;
-#pragma unroll
-        for (int q = 0; q < SW / 2; ++q) {
-          const uint4 v = re[q];
-          if (kWeighted) {
-            s += (uint32_t)(__popc(p[q].x & v.x) + __popc(p[q].y & v.y)) * (uint32_t)wt[2 * q] +
-                 (uint32_t)(__popc(p[q].z & v.z) + __popc(p[q].w & v.w)) * (uint32_t)wt[2 * q + 1];
-          } else {
-            s += __popc(p[q].x & v.x) + __popc(p[q].y & v.y) + __popc(p[q].z & v.z) + __popc(p[q].w & v.w);
-          }
-        }
-        acc[e] += s;
-      }
-    }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < C; i += blockDim.x) {
-    const uint32_t v = acc[i];
-    if (v) atomicAdd(outB && i >= nA ? &outB[i - nA] : &out[i], v);
-  }
-}
-
 // ---------------------------------------------------------------------------
 // k >= 3, slab-stationary counting from piece records (the slab path of
 // fa_level_plan).
 //
-// Same slab build and thread-per-piece counting as k_count_slab, with the piece
-// metadata laid out for latency.  PMC of k_count_slab on the T10I4D100M level 3-4
+// Slab build (above) and thread-per-piece counting, with the piece metadata laid
+// out for latency.  PMC of the earlier per-group kernel on the T10I4D100M level 3-4
 // bundle: waves wait ~64 % of their cycles, only ~3 % of it on LDS -- every piece
 // walked a chain of dependent global loads (gpm -> prefix ids -> slab rows,
 // gext_off -> each extension id).  Here a piece is one 48-B record (plan.cpp):
@@ -1556,295 +1382,6 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
   }
 }
 
-// ---------------------------------------------------------------------------
-// k >= 3, trie-shared slab counting (the default level kernel).
-//
-// Same slab-stationary structure as k_count_slab (one LDS slab of the used
-// items per tile, per-candidate LDS accumulators across tiles), with two
-// changes measured to matter on MI355X:
-//
-//  * Prefix sharing along the candidate trie (FastApriori.scala:143-145 ANDs a
-//    group's prefix once; here the sharing extends across groups).  The
-//    active (k-1)-prefixes are visited in lexicographic order inside a work
-//    item; the AND of the first D1 items (P1), of the first D2 items (P2) and
-//    of the whole prefix (p) are kept in registers and recomputed only when
-//    the prefix changes at that depth (piece flags).  On T40I10 levels 8-11
-//    this reads 2.1-2.4x fewer slab rows than recomputing every prefix.
-//  * SW/4 lanes per work item (4 words each) with a per-item slot rotation:
-//    at SW = 32 the 16 lanes of every ds_read_b128 lane group
-//    ({0-3,12-15,20-27}, ...) cover 16 distinct 16-byte slots of the 256-byte
-//    rows, so slab reads are bank-conflict free (thread-per-group reads of
-//    random rows were ~3.5-way conflicted).  Partial popcounts are summed
-//    over the item's lanes with DPP (quad_perm, row_half_mirror).
-//
-// Work item w = pieces [witems[w].x, witems[w].y); piece = (gpre offset of its
-// prefix row, ext begin, ext end, flags): bit 1 = recompute P2 from P1, bit 0 =
-// recompute p from P2.  The first piece of a work item recomputes everything.
-// Pieces arrive as 32-B records (plan.cpp fa_trie_records: flags, ext range,
-// the first four extension ids and the prefix ids past D1, all inline), and the
-// next piece's record is loaded while the current one is counted.
-// ---------------------------------------------------------------------------
-template <int SW, bool kWeighted, int kBuild>
-__global__ __launch_bounds__(kSlabThreads) void k_count_trie(
-    const int64_t* __restrict__ roff, const int32_t* __restrict__ ranks, const int32_t* __restrict__ src,
-    int64_t ncols, const int32_t* __restrict__ item_map, int n_used, const int32_t* __restrict__ gpre, int m,
-    int D1, int D2, const int4* __restrict__ rec, const int2* __restrict__ witems, int NW,
-    const int32_t* __restrict__ gext, int C, const int32_t* __restrict__ wword, uint32_t* __restrict__ out,
-    const uint64_t* __restrict__ bm, int64_t Wp, const int32_t* __restrict__ bm_rows) {
-  constexpr int NQ = (SW / 2) / 2 < FA_TRIE_NQ ? (SW / 2) / 2 : FA_TRIE_NQ;   // uint4 per lane (NQ = 2: ~90 VGPRs)
-  constexpr int RS = SW / 2;                   // uint4 slots per slab row
-  constexpr int LPP = RS / NQ;                 // lanes per work item: 2 / 4 / 8 for SW = 8 / 16 / 32
-  static_assert(LPP == 2 || LPP == 4 || LPP == 8, "SW in {8, 16, 32}");
-  // Row u stores logical 16-B slot L at physical slot L ^ (2u mod RS) (word q at
-  // q ^ (4u mod SW)).  The XOR is even, so a read's slot parity is kept and the
-  // rotation below stays conflict-free, while the slab build's atomicOr of one
-  // word q over random items u spreads over 8 slots instead of one bank pair.
-  constexpr int SWZ = SW - 4;                  // word-index XOR mask applied to (u << 2)
-  extern __shared__ uint4 lds4[];
-  __shared__ unsigned long long build_words[kSlabThreads / 64 * 2];
-  uint64_t* slab = reinterpret_cast<uint64_t*>(lds4);
-  uint32_t* acc = reinterpret_cast<uint32_t*>(slab + (size_t)n_used * SW);
-  for (int i = threadIdx.x; i < C; i += blockDim.x) acc[i] = 0;
-  auto acc_add = [&](int e, uint32_t v) { atomicAdd(&acc[e], v); };
-  const int64_t W = (ncols + 63) >> 6;
-  const int64_t nslabs = (W + SW - 1) / SW;
-
-  const int lane = threadIdx.x & 63;
-  const int t = lane & (LPP - 1);
-  const int grp = threadIdx.x / LPP;           // work-item slot in the workgroup
-  constexpr int NGRP = kSlabThreads / LPP;
-  const int rot = (lane / LPP) % NQ;
-  int off[NQ];                                 // rotated slot of step q (conflict-free lane groups)
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) off[q] = t * NQ + (q + rot) % NQ;
-
-  for (int64_t sb = blockIdx.x; sb < nslabs; sb += gridDim.x) {
-    const int64_t w0 = sb * SW;
-    __syncthreads();
-    if (kBuild == kBuildBM) {
-      slab_copy_bm<SW, SW, true>(lds4, n_used, bm, Wp, bm_rows, w0, W);
-    } else {
-      {
-        const uint4 z = make_uint4(0, 0, 0, 0);
-        for (int i = threadIdx.x; i < n_used * RS; i += blockDim.x) lds4[i] = z;
-      }
-      __syncthreads();
-      if (kBuild == kBuildContig) {
-        constexpr int NWV = kSlabThreads / 64;
-        constexpr int NSUB = NWV > SW ? NWV / SW : 1;
-        const int wv = threadIdx.x >> 6;
-        for (int q = wv / NSUB; q < SW; q += NWV / NSUB)
-          if ((w0 + q) * 64 < ncols)
-            slab_build_word(slab, SW, q, (w0 + q) * 64, ncols, roff, ranks, item_map, wv % NSUB, NSUB,
-                            build_words + wv * 2, SWZ);
-      } else {
-        // dedup layout: column j of the tile gathers row src[col]
-        for (int j = threadIdx.x; j < SW * 64; j += blockDim.x) {
-          const int64_t col = w0 * 64 + j;
-          if (col >= ncols) break;
-          const int64_t row = src ? (int64_t)src[col] : col;
-          if (row < 0) continue;
-          const unsigned long long bit = 1ull << (j & 63);
-          const int qw = j >> 6;
-          for (int64_t r = roff[row], r1 = roff[row + 1]; r < r1; ++r) {
-            const int uu = item_map[ranks[r]];
-            if (uu >= 0) atomicOr((unsigned long long*)(slab + (size_t)uu * SW + (qw ^ ((uu << 2) & SWZ))), bit);
-          }
-        }
-      }
-    }
-    __syncthreads();
-    uint32_t wt[2 * NQ];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int64_t wa = w0 + 2 * off[q];
-      wt[2 * q] = kWeighted ? ((wa < W) ? (uint32_t)wword[wa] : 0u) : 1u;
-      wt[2 * q + 1] = kWeighted ? ((wa + 1 < W) ? (uint32_t)wword[wa + 1] : 0u) : 1u;
-    }
-    // AND of slab rows it[j0..j1) into a[]; two rows per step keep 2*NQ reads in flight
-    auto and_rows = [&](uint4 (&a)[NQ], const int32_t* it, int j0, int j1) {
-      int j = j0;
-      for (; j + 2 <= j1; j += 2) {
-        const int ua = it[j], ub = it[j + 1];
-        const int xa = (ua << 1) & (RS - 1), xb = (ub << 1) & (RS - 1);
-        const uint4* ra = lds4 + (size_t)ua * RS;
-        const uint4* rb = lds4 + (size_t)ub * RS;
-        uint4 va[NQ], vb[NQ];
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) { va[q] = ra[off[q] ^ xa]; vb[q] = rb[off[q] ^ xb]; }
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          a[q].x &= va[q].x & vb[q].x; a[q].y &= va[q].y & vb[q].y;
-          a[q].z &= va[q].z & vb[q].z; a[q].w &= va[q].w & vb[q].w;
-        }
-      }
-      if (j < j1) {
-        const int ua = it[j], xa = (ua << 1) & (RS - 1);
-        const uint4* ra = lds4 + (size_t)ua * RS;
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          const uint4 v = ra[off[q] ^ xa];
-          a[q].x &= v.x; a[q].y &= v.y; a[q].z &= v.z; a[q].w &= v.w;
-        }
-      }
-    };
-    auto dot = [&](const uint4 (&p)[NQ], const uint4 (&v)[NQ]) -> uint32_t {
-      uint32_t s = 0;
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        if (kWeighted) {
-          s += (uint32_t)(__popc(p[q].x & v[q].x) + __popc(p[q].y & v[q].y)) * wt[2 * q] +
-               (uint32_t)(__popc(p[q].z & v[q].z) + __popc(p[q].w & v[q].w)) * wt[2 * q + 1];
-        } else {
-          s = bcnt_acc(p[q].x & v[q].x, s); s = bcnt_acc(p[q].y & v[q].y, s);
-          s = bcnt_acc(p[q].z & v[q].z, s); s = bcnt_acc(p[q].w & v[q].w, s);
-        }
-      }
-      return s;
-    };
-    // sum over the work item's LPP consecutive lanes (DPP: quad_perm, row_half_mirror)
-    auto lanes_sum = [&](uint32_t s) -> uint32_t {
-      s += (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0xB1, 0xf, 0xf, false);                   // [1,0,3,2]
-      if (LPP >= 4) s += (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0x4E, 0xf, 0xf, false);     // [2,3,0,1]
-      if (LPP >= 8) s += (uint32_t)__builtin_amdgcn_mov_dpp((int)s, 0x141, 0xf, 0xf, false);    // half mirror
-      return s;
-    };
-    // AND of the slab rows whose ids are u16 slots [j0, j1) of r (record ids; j0, j1
-    // are uniform, so the guards are scalar branches)
-    auto and_ids = [&](uint4 (&a)[NQ], const int4& r, int j0, int j1) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (j >= j0 && j < j1) {
-          const int u = u16_at(r, j), x = (u << 1) & (RS - 1);
-          const uint4* ru = lds4 + (size_t)u * RS;
-#pragma unroll
-          for (int q = 0; q < NQ; ++q) {
-            const uint4 v = ru[off[q] ^ x];
-            a[q].x &= v.x; a[q].y &= v.y; a[q].z &= v.z; a[q].w &= v.w;
-          }
-        }
-      }
-    };
-    // UE extension rows per step (UE * NQ independent slab reads in flight per lane;
-    // UE = 4 at NQ = 2, 2 at NQ = 4 -- the same registers)
-    constexpr int UE = 2;
-    constexpr int R = NQ >= 4 ? 2 : 4;   // extensions taken from the record
-    for (int w = grp; w < NW; w += NGRP) {
-      const int2 wi = witems[w];
-      // piece records (fa_trie_records): this piece's, and the next one's in flight
-      int4 ra = rec[2 * wi.x], rb = rec[2 * wi.x + 1];
-      uint4 P1[NQ], P2[NQ], p[NQ];
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) P1[q] = make_uint4(~0u, ~0u, ~0u, ~0u);
-      and_rows(P1, gpre + ra.y, 0, D1);
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) { P2[q] = P1[q]; p[q] = P1[q]; }
-      for (int pi = wi.x; pi < wi.y; ++pi) {
-        const int pn = pi + 1 < wi.y ? pi + 1 : pi;
-        const int4 na = rec[2 * pn], nb = rec[2 * pn + 1];
-        const int flg = (ra.x >> 23) & 3;
-        const int e0 = ra.x & 0x1FFFF, n_ext = (ra.x >> 17) & 63;
-        const int ez = e0 + n_ext;
-        // ids past the record's first UE: requested now, used after the prefix ANDs
-        int nx[UE];
-        {
-          const int eb = min(e0 + R, max(ez - 1, e0));
-#pragma unroll
-          for (int k = 0; k < UE; ++k) nx[k] = gext[min(eb + k, max(ez - 1, e0))];
-        }
-        if (!((ra.x >> 25) & 1)) {
-          if (flg & 2) {
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) P2[q] = P1[q];
-            and_ids(P2, rb, 0, D2 - D1);
-          }
-          if (flg & 1) {
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) p[q] = P2[q];
-            and_ids(p, rb, D2 - D1, m - D1);
-          }
-        } else {
-          const int32_t* it = gpre + ra.y;
-          if (flg & 2) {
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) P2[q] = P1[q];
-            and_rows(P2, it, D1, D2);
-          }
-          if (flg & 1) {
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) p[q] = P2[q];
-            and_rows(p, it, D2, m);
-          }
-        }
-        // extensions 0..R-1 from the record, two rows per step (an odd count reads
-        // one padding row: id 0, never accumulated)
-#pragma unroll
-        for (int k0 = 0; k0 < R; k0 += 2) {
-          if (k0 < n_ext) {
-            uint4 v[2][NQ];
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-              const int u = k0 + k < 2 ? ((k0 + k) ? (int)((uint32_t)ra.z >> 16) : (ra.z & 0xFFFF))
-                                        : ((k0 + k) == 3 ? (int)((uint32_t)ra.w >> 16) : (ra.w & 0xFFFF));
-              const int xk = (u << 1) & (RS - 1);
-              const uint4* rk = lds4 + (size_t)u * RS;
-#pragma unroll
-              for (int q = 0; q < NQ; ++q) v[k][q] = rk[off[q] ^ xk];
-            }
-            const uint32_t s0 = lanes_sum(dot(p, v[0]));
-            const uint32_t s1 = lanes_sum(dot(p, v[1]));
-            if (t == 0) {
-              acc_add(e0 + k0, s0);
-              if (k0 + 1 < n_ext) acc_add(e0 + k0 + 1, s1);
-            }
-          }
-        }
-        int e = e0 + R;
-        for (; e + UE <= ez; e += UE) {
-          int u[UE];
-#pragma unroll
-          for (int k = 0; k < UE; ++k) u[k] = nx[k];
-          {
-            const int ep = min(e + UE, ez - UE);
-#pragma unroll
-            for (int k = 0; k < UE; ++k) nx[k] = gext[ep + k];
-          }
-          uint4 v[UE][NQ];
-#pragma unroll
-          for (int k = 0; k < UE; ++k) {
-            const int xk = (u[k] << 1) & (RS - 1);
-            const uint4* rk = lds4 + (size_t)u[k] * RS;
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) v[k][q] = rk[off[q] ^ xk];
-          }
-          uint32_t sk[UE];
-#pragma unroll
-          for (int k = 0; k < UE; ++k) sk[k] = lanes_sum(dot(p, v[k]));
-          if (t == 0) {
-#pragma unroll
-            for (int k = 0; k < UE; ++k) acc_add(e + k, sk[k]);
-          }
-        }
-        for (; e < ez; ++e) {
-          const int u0 = gext[e], x0 = (u0 << 1) & (RS - 1);
-          const uint4* r0 = lds4 + (size_t)u0 * RS;
-          uint4 v0[NQ];
-#pragma unroll
-          for (int q = 0; q < NQ; ++q) v0[q] = r0[off[q] ^ x0];
-          const uint32_t s0 = lanes_sum(dot(p, v0));
-          if (t == 0) acc_add(e, s0);
-        }
-        ra = na; rb = nb;
-      }
-    }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < C; i += blockDim.x) {
-    const uint32_t v = acc[i];
-    if (v) atomicAdd(&out[i], v);
-  }
-}
-
 }  // namespace fa
 
 using namespace fa;
@@ -1959,79 +1496,6 @@ FA_API int fa_hip_count_slab_rec(const int64_t* roff, const int32_t* ranks, cons
                                  const int32_t* g_dev) {
   return fa_hip_count_slab_rec_cls(roff, ranks, src, ncols, item_map, F1, n_used, gpre, rec, G, C, wword, out, sw,
                                    n_wg, bm, Wp, st, bm_rows, g_dev, 0);
-}
-
-// Bundle counting with depth-2 prefix reuse (k_count_slab<.., kDfs = true>), unit
-// weights, one accumulator pass of C counters: gpre/gpm: prefix slab rows and
-// per-piece (offset, length); prng: per-piece node-1 range; node1: int4, node2: int2
-// (see the kernel).  Multi-pass levels (plan.cpp fa_plan_dfs passes) copy the slab
-// from the used-item bitmap bm (bm_rows: slab row -> bitmap row) and flush counters
-// [0, nA) to out, [nA, C) to outB.  Returns 3 when slab + accumulator exceed the LDS.
-FA_API int fa_hip_count_dfs(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
-                            const int32_t* item_map, int n_used, const int32_t* gpre, const int32_t* gpm,
-                            const int32_t* prng, const int32_t* node1, const int32_t* node2, int NP, int C,
-                            uint32_t* out, int sw, int n_wg, const uint64_t* bm, int64_t Wp, const int32_t* bm_rows,
-                            int nA, uint32_t* outB, hipStream_t st) {
-  if (NP <= 0 || C <= 0 || ncols <= 0) return 0;
-  const size_t lds = (size_t)n_used * (sw + 2) * 8 + (size_t)C * 4;
-  if (lds > 160 * 1024 - 512) return 3;
-  using KernT = void (*)(const int64_t*, const int32_t*, const int32_t*, int64_t, const int32_t*, int,
-                         const int32_t*, int, const int32_t*, const int32_t*, int, int, const int32_t*,
-                         uint32_t*, const uint64_t*, int64_t, int, const int32_t*, const int32_t*,
-                         const int32_t*, int, uint32_t*);
-  KernT kern = nullptr;
-#define FA_DFS_CASE(S)                                                                      \
-  if (sw == S) kern = bm ? (KernT)k_count_slab<S, false, kBuildBM, true>                     \
-                         : src ? (KernT)k_count_slab<S, false, kBuildCols, true>             \
-                               : (KernT)k_count_slab<S, false, kBuildContig, true>;
-  FA_DFS_CASE(4)
-  FA_DFS_CASE(8)
-  FA_DFS_CASE(16)
-  FA_DFS_CASE(32)
-#undef FA_DFS_CASE
-  if (!kern) return 1;
-  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  const int dbg = getenv("FA_SLAB_DEBUG") ? atoi(getenv("FA_SLAB_DEBUG")) : 0;
-  hipLaunchKernelGGL(kern, dim3((unsigned)n_wg), dim3(kSlabThreads), lds, st, roff, ranks, src, ncols, item_map,
-                     n_used, gpre, 0, prng, node1, NP, C, (const int32_t*)nullptr, out, bm, Wp, dbg, gpm, bm_rows,
-                     node2, nA, outB);
-  FA_LAUNCH_RET();
-}
-
-// Trie-shared slab counting (k_count_trie).  pieces: int4 [NP], witems: int2 [NW]
-// (see the kernel); gext/out are pass-local (C <= LDS accumulator capacity).
-// Returns 3 when the slab + accumulator exceed the LDS budget.
-FA_API int fa_hip_count_trie(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
-                             const int32_t* item_map, int n_used, const int32_t* gpre, int m, int D1, int D2,
-                             const void* pieces, const void* witems, int NW, const int32_t* gext, int C,
-                             const int32_t* wword, uint32_t* out, int sw, int n_wg, const uint64_t* bm, int64_t Wp,
-                             hipStream_t st, const int32_t* bm_rows) {
-  if (NW <= 0 || C <= 0 || ncols <= 0) return 0;
-  if (!(0 <= D1 && D1 <= D2 && D2 <= m)) return 2;
-  const size_t lds = (size_t)n_used * sw * 8 + (size_t)C * 4;
-  if (lds > 160 * 1024 - 512) return 3;
-  using KernT = void (*)(const int64_t*, const int32_t*, const int32_t*, int64_t, const int32_t*, int,
-                         const int32_t*, int, int, int, const int4*, const int2*, int, const int32_t*, int,
-                         const int32_t*, uint32_t*, const uint64_t*, int64_t, const int32_t*);
-  KernT kern = nullptr;
-#define FA_TRIE_MODE(S, B) kern = wword ? (KernT)k_count_trie<S, true, B> : (KernT)k_count_trie<S, false, B>;
-#define FA_TRIE_CASE(S)                                   \
-  if (sw == S) {                                          \
-    if (bm) { FA_TRIE_MODE(S, kBuildBM) }                 \
-    else if (src) { FA_TRIE_MODE(S, kBuildCols) }         \
-    else { FA_TRIE_MODE(S, kBuildContig) }                \
-  }
-  FA_TRIE_CASE(8)
-  FA_TRIE_CASE(16)
-  FA_TRIE_CASE(32)
-#undef FA_TRIE_CASE
-#undef FA_TRIE_MODE
-  if (!kern) return 1;
-  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(kern, dim3((unsigned)n_wg), dim3(kSlabThreads), lds, st, roff, ranks, src, ncols, item_map,
-                     n_used, gpre, m, D1, D2, (const int4*)pieces, (const int2*)witems, NW, gext, C, wword, out, bm,
-                     Wp, bm_rows);
-  FA_LAUNCH_RET();
 }
 
 FA_API int fa_hip_block_counts(const int64_t* roff, const int32_t* ranks, int64_t T, int32_t F1, uint8_t* cnt,

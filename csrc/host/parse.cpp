@@ -453,3 +453,33 @@ FA_API int64_t fa_file_size(const char* path) {
 FA_API int64_t fa_next_line_start(const char* data, int64_t size, int64_t pos) {
   return next_line_start(data, size, pos);
 }
+
+// Line structure of one chunk of a file as it lands in a pinned buffer (the device
+// parser's streamed regions, utils/io.py): info[0] = '\n' bytes, info[1] = offset of
+// the last '\n' (-1: none), info[2] = 1 when any '\r' occurs (lone '\r' ends a line
+// too: such chunks leave the rest of the file to the whole-region path).  Eight
+// bytes per step with an exact zero-byte test, so one host thread keeps up with
+// its share of the pread ring.
+FA_API void fa_chunk_scan(const uint8_t* p, int64_t m, int64_t* info) {
+  const uint64_t lo7 = 0x7F7F7F7F7F7F7F7Full;
+  auto zeros = [lo7](uint64_t t) { return ~(((t & lo7) + lo7) | t | lo7); };   // 0x80 per zero byte
+  int64_t nl = 0;
+  uint64_t cr = 0;
+  int64_t i = 0;
+  for (; i + 8 <= m; i += 8) {
+    uint64_t x;
+    std::memcpy(&x, p + i, 8);
+    nl += __builtin_popcountll(zeros(x ^ 0x0A0A0A0A0A0A0A0Aull));
+    cr |= zeros(x ^ 0x0D0D0D0D0D0D0D0Dull);
+  }
+  for (; i < m; ++i) {
+    nl += p[i] == '\n';
+    cr |= p[i] == '\r';
+  }
+  int64_t last = -1;
+  for (int64_t j = m - 1; j >= 0; --j)
+    if (p[j] == '\n') { last = j; break; }
+  info[0] = nl;
+  info[1] = last;
+  info[2] = cr ? 1 : 0;
+}

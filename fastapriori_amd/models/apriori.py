@@ -77,10 +77,6 @@ class _Deferred:
         return self.value
 
 
-# depth-2 prefix reuse for bundles (k_count_slab<kDfs>): off by default since the
-# record-driven slab kernel (k_count_slab_rec) counts the T10I4D100M bundle 5-12
-# faster (A/B on MI355X: 48.1-48.9 vs 49.5 ms per run)
-BUNDLE_DFS = os.environ.get("FA_BUNDLE_DFS", "0") == "1"
 # k = 2 across ranks: triangles of at least this many pairs are reduce-scattered and
 # thresholded per slice (Comm.reduce_scatter_select) instead of all-reduced.  Below it
 # the triangle is all-reduced and F_2 compacted on the device with no host round trip
@@ -88,19 +84,7 @@ BUNDLE_DFS = os.environ.get("FA_BUNDLE_DFS", "0") == "1"
 # over xGMI costs less than the reduce-scatter's three collectives and two host syncs.
 # 4M pairs (F1 ~ 2900, 16 MB) is where the all-reduce's 2(W-1)/W volume starts to dominate.
 PAIR_RS_MIN = int(os.environ.get("FA_PAIR_RS_MIN", str(1 << 22)))
-# depth-2 reuse pays where prefixes are long; on short prefixes (k = 3: two items) the
-# lanes' uneven child loops cost more than the saved reads (T10I4D100M: bundle 3-4
-# 17.7 -> 21.0 ms with it, bundle 5-12 16.2 -> 14.6 ms)
-BUNDLE_DFS_MIN_M = int(os.environ.get("FA_BUNDLE_DFS_MIN_M", "4"))
 BUNDLE_GROWTH = float(os.environ.get("FA_BUNDLE_GROWTH", "1.5"))
-# deep levels that need several accumulator passes, counted together with the next level
-# depth-first (_pair_multipass_level) from this prefix length on.  Opt-in: measured slower
-# on T40I10D100M (716 -> 836 ms per run): the depth-2 kernel still walks index chains
-# (piece -> prefix ids -> rows, node -> children) that the record-driven slab kernel
-# removed, and its lanes' child loops are uneven; it halves the slab-row reads of the
-# paired levels, so a record-driven depth-2 kernel is the route to take it further
-DFS_PAIR = os.environ.get("FA_DFS_PAIR", "0") == "1"
-DFS_PAIR_MIN_M = int(os.environ.get("FA_DFS_PAIR_MIN_M", "4"))
 # level bundles generated, planned, counted and thresholded on the GPU with no host
 # round trip per bundle beyond the generator's acceptance readbacks (_mine_device)
 DEVICE_LEVELS = os.environ.get("FA_DEVICE_LEVELS", "1") == "1"
@@ -117,7 +101,7 @@ class MinerConfig:
     pair_strategy: str = "auto"     # auto | horizontal | gram
     dedup_threshold: float = 0.8    # dedup when distinct/T below this (auto)
     max_level: int = 0              # 0 = unlimited
-    level_kernel: str = os.environ.get("FA_LEVEL_KERNEL", "auto")   # auto (= trie) | trie | slab | bitmap
+    level_kernel: str = os.environ.get("FA_LEVEL_KERNEL", "auto")   # auto (= slab) | slab | bitmap
     trim: bool = True               # transaction trimming before every level k >= 3
     f1: str = "auto"                # auto | sketch | histogram  (frequent-item counting)
     trim_min_rows: int = 1 << 20    # no trimming below this many rows (fixed cost > gain)
@@ -263,10 +247,6 @@ class FastApriori:
                 else:
                     with tm.phase("apriori_gen"), roctx_range("bundle"):
                         bundle = self._plan_bundle(db, k, levels[-1], prefix_idx, ext_off, ext, cand_rows)
-                self._dfs_pair = False
-                if len(bundle) == 1:
-                    with tm.phase("apriori_gen"), roctx_range("dfs_pair"):
-                        self._pair_multipass_level(db, k, bundle)
                 # later bundled levels only use items of level k's candidates
                 mark = np.zeros(max(db["F1"], 1), dtype=bool)
                 mark[self._bundle_rows[0].ravel()] = True
@@ -633,9 +613,11 @@ class FastApriori:
                                               and V >= F1_SKETCH_MIN_VOCAB):
                 got = self._f1_heavy_hitters(shard, V, thr)
             if got is None:
-                hist = ops.histogram(shard.items, V)
-                if shard.extras.size:
-                    hist += torch.bincount(torch.from_numpy(shard.extras.astype(np.int64)), minlength=V).to(dev)
+                hist = self._parsed_hist(shard, V)
+                if hist is None:
+                    hist = ops.histogram(shard.items, V)
+                    if shard.extras.size:
+                        hist += torch.bincount(torch.from_numpy(shard.extras.astype(np.int64)), minlength=V).to(dev)
                 comm.all_reduce_(hist)
                 if V <= F1_HIST_READBACK and dev.type == "cuda":
                     # narrow vocabulary: the whole histogram in one readback (no nonzero sync),
@@ -648,6 +630,8 @@ class FastApriori:
                     cnt = np.empty(Vh, np.int64)
                     F = int(ops._native.host().fa_f1_rank_numeric(hh.ctypes.data, V, thr, ids.ctypes.data,
                                                                    cnt.ctypes.data, buf.data_ptr()))
+                    if V == 0:
+                        buf.view(torch.int32)[0] = -1      # the native call writes lut[0 .. V) only
                     lut = buf.to(dev, non_blocking=True).view(torch.int32)
                     st.event = torch.cuda.Event()
                     st.event.record()
@@ -747,6 +731,18 @@ class FastApriori:
             hit = rs[pos] == hashes_t
             lut[:Vl][hit] = ro[pos[hit]].to(torch.int32)
         return items, counts1, lut
+
+    @staticmethod
+    def _parsed_hist(shard: TransactionShard, V: int):
+        """The occurrence histogram the device parser counted while compacting the ids
+        (csrc/hip/parse.hip k_tcompact), widened to the ranks' common V; None when
+        the shard has none (then F1 reads the items)."""
+        h = shard.hist
+        if h is None or h.device != shard.items.device or h.numel() > V:
+            return None
+        out = torch.zeros(V, dtype=torch.int64, device=h.device)
+        out[:h.numel()] = h
+        return out
 
     def _f1_heavy_hitters(self, shard: TransactionShard, V: int, thr: int):
         """Numeric-mode F1 for wide vocabularies without a V-bin histogram.
@@ -1115,6 +1111,7 @@ class FastApriori:
         exact = pw is not None and not db.get("long_rows", True) and not self.cand_par
         bound = min(C2, int(pw) // mc + 1) if exact and mc > 0 else C2
         self._f2_dev, self._f2_cnt_dev, self._f2_n_dev, self._f2_bound = rows, cnt, pos[-1:], max(int(bound), 1)
+        self.stats["f2_on_device"] = True
         return None, None
 
     # ------------------------------------------------------------------
@@ -1224,39 +1221,12 @@ class FastApriori:
             cand = nxt
         return bundle
 
-    def _pair_multipass_level(self, db, k: int, bundle: list) -> None:
-        """Cross-level prefix reuse for deep levels (FastApriori.scala:143-145 ANDs a
-        prefix once per group; here a level-k candidate's AND is reused by its own
-        extensions): a level k whose candidates need several accumulator passes is
-        counted together with level k+1 generated from its candidates (a superset of
-        apriori-gen(F_k) with exact counts, as for bundles), depth-first per slab tile
-        (k_count_slab<kDfs>): a level-(k+1) candidate then costs one slab-row read
-        instead of its k prefix rows.  Taken when the prefix is long (the saved reads
-        grow with k), the speculative level grows by at most BUNDLE_GROWTH and the
-        layout has unit weights."""
-        if not (DFS_PAIR and self._dev.type == "cuda" and db["wword"] is None and k - 1 >= DFS_PAIR_MIN_M
-                and self._F1 <= ops.primitives.AG_DEVICE_MAX_F1
-                and (self.cfg.max_level == 0 or k + 1 <= self.cfg.max_level)):
-            return
-        cand = self._bundle_rows[0]
-        C = int(cand.shape[0])
-        used = np.unique(cand)
-        if C == 0 or C <= ops.primitives.slab_capacity(int(used.size), C):
-            return                                   # one pass: the plain slab kernel is faster
-        nxt = ops.primitives.apriori_gen_chain(cand, self._F1, self._dev, 1, BUNDLE_GROWTH, 0, 1 << 40)
-        if not nxt:
-            return
-        pi, eo, ex, rows = nxt[0]
-        bundle.append((k + 1, cand, pi, eo, ex))
-        self._bundle_rows.append(np.ascontiguousarray(rows, np.int32))
-        self._dfs_pair = True
-
     def _cand_rows_view(self, db) -> dict:
         """Candidate mode: this rank's 1/W slice of the replicated rows.
 
         Bundled levels (one launch over many levels' candidates) are split by rows
         like the k = 2 pairs, not by candidate groups: every rank holds the whole
-        DB, so any split is local, and the row split keeps the bundle/DFS kernels'
+        DB, so any split is local, and the row split keeps the bundle kernel's
         one-launch plans intact.  The all-reduce over the rank group sums the slices.
         Unweighted rows: a row range (absolute offsets into the shared ranks);
         weighted (dedup) layout: a range of 64-column words."""
@@ -1287,18 +1257,6 @@ class FastApriori:
         full_db = db
         if self.cand_par:
             db = self._cand_rows_view(db)
-        sizes = [int(ex.size) for *_, ex in bundle]
-        if db["wword"] is None and (getattr(self, "_dfs_pair", False) or (
-                BUNDLE_DFS and bundle[0][1].shape[1] >= BUNDLE_DFS_MIN_M)):
-            # depth-2 prefix reuse: level k+1 candidates read one slab row under their
-            # parent level-k candidate's AND (k_count_slab<kDfs>); a multi-pass level
-            # paired with its children streams the slabs from the used items' bitmap
-            cnt = ops.primitives.count_bundle_dfs(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"],
-                                                  [(pv, pi, eo, ex) for _, pv, pi, eo, ex in bundle],
-                                                  full_bm=lambda u: self._bitmaps(db, u), multi=self._dfs_pair)
-            if cnt is not None:
-                self.comm.all_reduce_(cnt, bound=self.stats["n_lines"])
-                return np.split(cnt.cpu().numpy(), np.cumsum(sizes)[:-1])
         pre = [pv[pi] for _, pv, pi, _, _ in bundle]
         poff = np.concatenate([[0], np.cumsum(np.concatenate([np.full(p.shape[0], p.shape[1]) for p in pre]))])
         flat = np.concatenate([p.ravel() for p in pre]).astype(np.int32)
@@ -1313,7 +1271,6 @@ class FastApriori:
         self.comm.all_reduce_(cnt, bound=self.stats["n_lines"])
         c = cnt.cpu().numpy()
         return np.split(c, np.cumsum(sizes)[:-1])
-
 
     def _count_level(self, db, prev: np.ndarray, prefix_idx, ext_off, ext) -> np.ndarray:
         if self.cand_par:
@@ -1339,7 +1296,7 @@ class FastApriori:
         the row shards in count parallelism (a no-op collective in candidate mode)."""
         dev = db["ranks"].device
         lk = self.cfg.level_kernel
-        if dev.type == "cuda" and lk in ("auto", "trie", "slab"):
+        if dev.type == "cuda" and lk in ("auto", "slab"):
             cnt = ops.count_level(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"], prev[prefix_idx],
                                   ext_off, ext, db["wword"], kernel=lk, full_bm=lambda u: self._bitmaps(db, u),
                                   sup_frac=self.stats["min_count"] / max(1, self.stats["n_lines"]))

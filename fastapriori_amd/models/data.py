@@ -105,6 +105,9 @@ class TransactionShard:
     extras: np.ndarray             # int32
     vocab: Vocabulary
     line_base: int = 0             # global index of this shard's first line
+    # numeric mode: occurrences per id (items + extras), int64 [vocab.size], counted by
+    # the device parser (F1 then needs no pass over the items); None: not counted
+    hist: torch.Tensor | None = None
 
     @property
     def n_lines(self) -> int:
@@ -112,7 +115,7 @@ class TransactionShard:
 
     def to(self, device) -> "TransactionShard":
         return TransactionShard(self.offsets.to(device), self.items.to(device), self.extras, self.vocab,
-                                self.line_base)
+                                self.line_base, None if self.hist is None else self.hist.to(device))
 
 
 @dataclass

@@ -27,6 +27,7 @@ _HOST_SIGS = {
     "fa_parse_buffer": (vp, [cp, i64, C.c_int, C.c_int]),
     "fa_file_size": (i64, [cp]),
     "fa_next_line_start": (i64, [cp, i64, i64]),
+    "fa_chunk_scan": (None, [vp, i64, vp]),
     "fa_txndb_info": (None, [vp, vp]),
     "fa_txndb_export": (None, [vp, vp, vp, vp, C.c_int]),
     "fa_txndb_export_dict": (None, [vp, vp, vp, vp, C.c_int]),
@@ -42,9 +43,6 @@ _HOST_SIGS = {
     "fa_cands_free": (None, [vp]),
     "fa_level_plan": (C.c_int, [vp, vp, i64, vp, vp, i32, vp, vp, i64, vp, i64, vp]),
     "fa_f1_rank_numeric": (i64, [vp, i64, i64, vp, vp, vp]),
-    "fa_plan_dfs": (C.c_int, [C.c_int, vp, vp, vp, vp, vp, vp, vp, i32, C.c_int, vp, i64, vp, i64, vp, i64]),
-    "fa_plan_trie": (C.c_int, [vp, i64, C.c_int, vp, i64, i64, C.c_int, C.c_int, vp, vp, vp, i64, vp]),
-    "fa_trie_records": (C.c_int, [vp, vp, vp, i64, vp, vp, C.c_int, C.c_int, vp]),
     "fa_rules_build": (vp, [vp, vp, vp, C.c_int, vp, C.c_int, vp]),
     "fa_rules_nante": (i64, [vp]),
     "fa_rules_nstats": (i64, [vp]),
@@ -81,10 +79,6 @@ _HIP_SIGS = {
     "fa_hip_block_bsum": (C.c_int, [vp, i64, i64, C.c_int, vp, vp]),
     "fa_hip_compress_staged": (C.c_int, [vp, vp, vp, i64, vp, vp, vp, vp, vp]),
     "fa_hip_compress_staged64": (C.c_int, [vp, vp, vp, i64, vp, vp, vp, vp, vp]),
-    "fa_hip_count_trie": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, vp, C.c_int, C.c_int, C.c_int, vp, vp,
-                                    C.c_int, vp, C.c_int, vp, vp, C.c_int, C.c_int, vp, i64, vp, vp]),
-    "fa_hip_count_dfs": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, vp, vp, vp, vp, vp, C.c_int, C.c_int, vp,
-                                   C.c_int, C.c_int, vp, i64, vp, C.c_int, vp, vp]),
     "fa_hip_count_slab_rec": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, C.c_int, vp, vp, C.c_int, C.c_int, vp, vp,
                                         C.c_int, C.c_int, vp, i64, vp, vp, vp]),
     "fa_hip_count_slab_rec_cls": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, C.c_int, vp, vp, C.c_int, C.c_int, vp,
@@ -111,9 +105,15 @@ _HIP_SIGS = {
     "fa_hip_recommend": (C.c_int, [vp, vp, vp, i64, i32, vp, vp, i64, vp, vp]),
     "fa_hip_recommend_indexed": (C.c_int, [vp, vp, vp, vp, vp, i64, i32, vp, vp, i64, vp, vp]),
     "fa_hip_parse_tiles": (i64, [i64]),
+    "fa_hip_tparse_tiles": (i64, [i64, i64]),
+    "fa_hip_tparse_hist_cap": (C.c_int, []),
+    "fa_hip_tline_count": (C.c_int, [vp, i64, i64, vp, vp]),
+    "fa_hip_tparse": (C.c_int, [vp, i64, i64, i64, C.c_int, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "fa_hip_scan_small": (C.c_int, [C.c_int, vp, i64, vp, vp, vp]),
+    "fa_hip_tcompact": (C.c_int, [vp, vp, i64, vp, vp, vp, vp, vp, vp, vp, i64, vp, C.c_int, vp, vp, vp]),
+    "fa_hip_hist_reduce": (C.c_int, [vp, C.c_int, vp, vp]),
     "fa_hip_line_count": (C.c_int, [vp, i64, vp, vp]),
     "fa_hip_line_ends": (C.c_int, [vp, i64, vp, vp, vp]),
-    "fa_hip_parse_lines": (C.c_int, [vp, vp, i64, vp, vp, vp, vp, vp, vp, vp]),
     "fa_hip_parse_lines_dict": (C.c_int, [vp, vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, vp]),
     "fa_hip_slot_remap": (C.c_int, [vp, i64, vp, vp]),
     "fa_hip_dict_verify": (C.c_int, [vp, vp, i64, vp, vp, vp, vp, i64, vp]),

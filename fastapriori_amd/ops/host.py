@@ -77,52 +77,3 @@ def rules_build(levels: list[np.ndarray], counts: list[np.ndarray], tie_pos: np.
     level_stats = [(i + 1, int(b), int(a)) for i, (b, a, _) in enumerate(st.tolist())]
     level_ms = [us / 1e3 for _, _, us in st.tolist()]
     return RuleTable(ante_off, ante[:na], cons[:R], conf[:R], level_stats, level_ms)
-
-
-@dataclass
-class TriePlan:
-    """Work items of the trie-shared level kernel (csrc/host/plan.cpp)."""
-    pieces: np.ndarray     # int32 [NP, 4]: (gpre offset, ext begin, ext end, flags), ext pass-local
-    witems: np.ndarray     # int32 [NW, 2]: piece ranges, cost-sorted within each pass
-    passes: np.ndarray     # int64 [npass, 3]: (work-item begin, end, ext base)
-    d1: int
-    d2: int
-    reads: int             # estimated slab-row reads (per tile)
-    reads_unshared: int    # the same without prefix sharing
-
-
-def plan_trie(prefix: np.ndarray, ext_off: np.ndarray, emax: int, cap: int, d1: int = -1, d2: int = -1) -> TriePlan:
-    """prefix: int32 [G, m] prefix rows in lexicographic order; ext_off: int64 [G+1]."""
-    P = np.ascontiguousarray(prefix, dtype=np.int32)
-    G, m = P.shape
-    eo = np.ascontiguousarray(ext_off, dtype=np.int64)
-    C = int(eo[-1] - eo[0])
-    maxp = G + C // max(emax, 1) + 2
-    pieces = np.zeros((maxp, 4), dtype=np.int32)
-    witems = np.zeros((maxp, 2), dtype=np.int32)
-    passes = np.zeros((maxp, 3), dtype=np.int64)
-    info = np.zeros(8, dtype=np.int64)
-    rc = _native.host().fa_plan_trie(P.ctypes.data, G, m, eo.ctypes.data, emax, cap, d1, d2, pieces.ctypes.data,
-                                     witems.ctypes.data, passes.ctypes.data, maxp, info.ctypes.data)
-    if rc != 0:
-        raise RuntimeError(f"fa_plan_trie failed ({rc})")
-    npc, nw, npass = int(info[0]), int(info[1]), int(info[2])
-    return TriePlan(pieces[:npc], witems[:nw], passes[:npass], int(info[3]), int(info[4]), int(info[5]),
-                    int(info[6]))
-
-
-def trie_records(plan: TriePlan, gpre: np.ndarray, gext: np.ndarray, m: int) -> np.ndarray:
-    """32-B piece records of k_count_trie (plan.cpp fa_trie_records): int32 [n_pieces, 8].
-    gpre: int32 [G, m] slab-row ids of the prefixes; gext: int32 [C] of the extensions."""
-    pieces = np.ascontiguousarray(plan.pieces, dtype=np.int32)
-    witems = np.ascontiguousarray(plan.witems, dtype=np.int32)
-    passes = np.ascontiguousarray(plan.passes, dtype=np.int64)
-    gp = np.ascontiguousarray(gpre, dtype=np.int32)
-    ge = np.ascontiguousarray(gext, dtype=np.int32)
-    rec = np.zeros((max(pieces.shape[0], 1), 8), dtype=np.int32)
-    rc = _native.host().fa_trie_records(pieces.ctypes.data, witems.ctypes.data, passes.ctypes.data,
-                                        passes.shape[0], gp.ctypes.data, ge.ctypes.data, m, plan.d1,
-                                        rec.ctypes.data)
-    if rc != 0:
-        raise RuntimeError(f"fa_trie_records failed ({rc})")
-    return rec[:pieces.shape[0]]

@@ -654,18 +654,6 @@ def slab_capacity(n_used: int, C: int) -> int:
     return 0
 
 
-# ---------------------------------------------------------------------------
-# k >= 3, trie-shared slab counting (k_count_trie + csrc/host/plan.cpp)
-# ---------------------------------------------------------------------------
-# relative cost of one slab-row read at slab width SW (16-B slot conflicts of the
-# rotated 4-word lane layout: none at 256-B rows, ~1.6x at 128 B, ~2.2x at 64 B)
-_TRIE_CONFLICT = {32: 1.0, 16: 1.6, 8: 2.2}
-TRIE_EMAX = int(os.environ.get("FA_TRIE_EMAX", "24"))     # max extensions per work item
-TRIE_ROUNDS = int(os.environ.get("FA_TRIE_ROUNDS", "4"))   # work items per lane group and pass (target)
-TRIE_PASS_WEIGHT = float(os.environ.get("FA_TRIE_PASS_WEIGHT", "4"))
-# auto level kernel: trie-shared counting when its slab-row reads are below this
-# fraction of the slab kernel's (measured break-even on T10I4 / T40I10, MI355X)
-_TRIE_MIN_SAVING = float(os.environ.get("FA_TRIE_MIN_SAVING", "0.3"))
 # class layout of slab passes (plan.cpp cls_layout, k_count_slab_rec<.., kCls>): sibling
 # prefixes share their first m-1 rows in registers; 0 disables it
 SLAB_CLS = int(os.environ.get("FA_SLAB_CLS", "1"))
@@ -674,150 +662,20 @@ SLAB_CLS = int(os.environ.get("FA_SLAB_CLS", "1"))
 DENSE_MIN_ROWS = float(os.environ.get("FA_DENSE_MIN_ROWS", "4"))
 
 
-def trie_slab_plan(n_used: int, C: int, W: int, reads_est: float) -> tuple[int, int]:
-    """Slab width SW and accumulator capacity for k_count_trie, by a time model:
-    slab-row reads x words x conflict factor, plus one used-item bitmap stream per
-    extra accumulator pass.  (0, 0) when no width fits the LDS."""
-    force = int(os.environ.get("FA_SLAB_SW", "0"))
-    best = None
-    for sw in ((force,) if force else (32, 16, 8)):
-        cap = (_LDS_BYTES - n_used * sw * 8) // 4
-        if cap < min(C, 1024):
-            continue
-        passes = -(-C // cap)
-        t = reads_est * W * 8 * _TRIE_CONFLICT.get(sw, 2.0) / 60e12
-        if passes > 1:   # a pass re-streams the used-item bitmap and re-runs every tile's skeleton
-            t += TRIE_PASS_WEIGHT * passes * n_used * W * 8 / 5e12
-        if best is None or t < best[0]:
-            best = (t, sw, int(cap))
-    return (best[1], best[2]) if best else (0, 0)
-
-
-def emulate_trie(bits: np.ndarray, gpre: np.ndarray, gext: np.ndarray, plan, weights=None) -> np.ndarray:
-    """CPU model of k_count_trie's plan semantics over a bool matrix bits [n_used, ncols]
-    (tests: any piece-flag or pass-offset error shows up as a wrong count)."""
-    m = gpre.shape[1]
-    flat = gpre.reshape(-1)
-    w = np.ones(bits.shape[1], np.int64) if weights is None else weights
-    out = np.zeros(gext.size, np.int64)
-    ones = np.ones(bits.shape[1], bool)
-    for w0, w1, base in plan.passes.tolist():
-        for wi in range(w0, w1):
-            pa, pb = plan.witems[wi]
-            g0 = plan.pieces[pa, 0]
-            P1 = ones.copy()
-            for j in range(plan.d1):
-                P1 &= bits[flat[g0 + j]]
-            P2 = P1.copy(); p = P1.copy()
-            for pi in range(pa, pb):
-                off, e0, e1, f = plan.pieces[pi]
-                if f & 2:
-                    P2 = P1.copy()
-                    for j in range(plan.d1, plan.d2):
-                        P2 &= bits[flat[off + j]]
-                if f & 1:
-                    p = P2.copy()
-                    for j in range(plan.d2, m):
-                        p &= bits[flat[off + j]]
-                for e in range(e0, e1):
-                    out[base + e] += int(((p & bits[gext[base + e]]) * w).sum())
-    return out
-
-
-LAST_TRIE_PLAN: dict = {}
-
-
-def count_level_trie(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_off: np.ndarray,
-                     ext: np.ndarray, wword, min_saving: float = 0.0) -> torch.Tensor | None:
-    """Trie-shared slab counting for one level (device only).
-
-    prefix: int32 [G, m] prefix rows (lexicographic); ext_off int64 [G+1]; ext int32 [C].
-    Returns int64 counts [C] in ext order, or None when the used items do not fit
-    any LDS slab, or (min_saving > 0) when the plan's slab-row reads exceed
-    min_saving x those of the thread-per-group slab kernel (pieces of <= 8).
-    """
-    from .host import plan_trie, trie_records
-    dev = ranks.device
-    C = int(ext.size)
-    if C == 0:
-        return torch.zeros(0, dtype=_I64, device=dev)
-    G, m = prefix.shape
-    used = np.unique(np.concatenate([prefix.ravel(), ext]))
-    W = (ncols + 63) // 64
-    sw, cap = trie_slab_plan(int(used.size), C, W, C + 0.5 * G * m)
-    if sw == 0:
-        return None
-    # enough work items per pass for every lane group of the workgroup to have several
-    # (latency hiding): NGRP = 1024 threads / (SW/4 lanes per item)
-    ngrp = 4096 // sw
-    emax = int(max(2, min(TRIE_EMAX, min(C, cap) // (TRIE_ROUNDS * ngrp))))
-    plan = plan_trie(prefix, ext_off, emax, cap)
-    if min_saving > 0:
-        slab_reads = int(np.ceil(np.diff(ext_off) / 8).sum()) * m + C
-        if plan.reads > min_saving * slab_reads:
-            return None
-    item_map = np.full(max(F1, 1), -1, dtype=np.int32)
-    item_map[used] = np.arange(used.size, dtype=np.int32)
-    gpre = np.ascontiguousarray(item_map[prefix], dtype=np.int32)
-    gext = np.ascontiguousarray(item_map[ext], dtype=np.int32)
-    # one host->device copy of all int32 tables
-    rec = trie_records(plan, gpre, gext, m).ravel()
-    nP, nW = rec.size, plan.witems.size
-    # records first: the kernel reads them as int4 (16-B aligned)
-    host = np.concatenate([rec, gpre.ravel(), gext, plan.witems.ravel(), item_map])
-    buf = torch.from_numpy(host).pin_memory().to(dev, non_blocking=True) if dev.type == "cuda" else \
-        torch.from_numpy(host)
-    o_gpre = nP
-    o_gext = o_gpre + gpre.size
-    o_wi = o_gext + gext.size
-    o_im = o_wi + nW
-    base_ptr = buf.data_ptr()
-    out = torch.zeros(C, dtype=_I32, device=dev)
-    bm = None
-    if plan.passes.shape[0] > 1:
-        bm, _ = build_bitmaps(roff, ranks, src, ncols, int(used.size), buf[o_im:o_im + item_map.size],
-                              torch.from_numpy(used.astype(np.int32)).to(dev))
-    st = _stream(ranks)
-    bounds = list(plan.passes[:, 2].tolist()) + [int(ext_off[-1] - ext_off[0])]
-    nslabs = (W + sw - 1) // sw
-    for q, (w0, w1, e0) in enumerate(plan.passes.tolist()):
-        Cq = bounds[q + 1] - e0
-        lds = used.size * sw * 8 + Cq * 4
-        per_cu = max(1, _LDS_BYTES // max(lds, 1))
-        n_wg = int(max(1, min(nslabs, 256 * min(per_cu, 2))))
-        _hip_call("fa_hip_count_trie", _p(roff), _p(ranks), _p(src), ncols, base_ptr + 4 * o_im, int(used.size),
-                  base_ptr + 4 * o_gpre, m, plan.d1, plan.d2, base_ptr, base_ptr + 4 * (o_wi + 2 * w0),
-                  w1 - w0, base_ptr + 4 * (o_gext + e0), Cq, _p(wword), out.data_ptr() + 4 * e0, sw, n_wg,
-                  _p(bm), bm.stride(0) if bm is not None else 0, st, None)
-    res = out.to(_I64)
-    LAST_TRIE_PLAN.clear()
-    LAST_TRIE_PLAN.update(rows=int(roff.numel() - 1), used=int(used.size), sw=sw, cap=cap,
-                          passes=int(plan.passes.shape[0]), pieces=int(plan.pieces.shape[0]),
-                          witems=int(plan.witems.shape[0]), emax=emax, m=m, C=C, d1=plan.d1, d2=plan.d2,
-                          reads=plan.reads, reads_unshared=plan.reads_unshared)
-    del buf
-    return res
-
-
 def _level_plan_bound(F1: int, C: int, G: int, m: int) -> int:
-    """int32 entries fa_level_plan may write: maps, gext, gpre, trie pieces + work items
-    (6 per piece, <= G + C/2 + 2 pieces) and their 32-B records (8 per piece), or the
-    slab kernel's piece tables and 48-B records."""
+    """int32 entries fa_level_plan may write: maps, gext, gpre, the slab kernel's piece
+    tables and 48-B records."""
     return 2 * F1 + C + G * m + 14 * (G + C // 2 + 2) + (m + 16) * (G + C // 8 + 1) + 24
 
 
 def level_plan_host(prefix: np.ndarray, ext_off: np.ndarray, ext: np.ndarray, F1: int, W: int,
-                    kernel: str = "auto", lds_bytes: int | None = None, poff: np.ndarray | None = None,
-                    cls: int | None = None):
+                    lds_bytes: int | None = None, poff: np.ndarray | None = None, cls: int | None = None):
     """fa_level_plan on host arrays (tests / diagnostics): (rc, info, passes, buf)."""
     P, po, G, m = _flat_prefix(prefix, poff)
     C = int(ext.size)
     eo = np.ascontiguousarray(ext_off, dtype=np.int64)
     ex = np.ascontiguousarray(ext, dtype=np.int32)
-    min_saving = {"auto": _TRIE_MIN_SAVING, "trie": 0.0, "slab": 2.0}[kernel]
-    params = np.array([lds_bytes or _LDS_BYTES, min_saving, _TRIE_CONFLICT[16], _TRIE_CONFLICT[8],
-                       TRIE_PASS_WEIGHT, TRIE_ROUNDS, TRIE_EMAX, W, 4.0, SLAB_CLS if cls is None else cls],
-                      dtype=np.float64)
+    params = _plan_params(lds_bytes or _LDS_BYTES, W, SLAB_CLS if cls is None else cls)
     bound = _level_plan_bound(F1, C, G, m)
     passes = np.zeros((G + C + 2, 3), np.int64)
     info = np.zeros(24, np.int64)
@@ -832,26 +690,20 @@ def level_plan_host(prefix: np.ndarray, ext_off: np.ndarray, ext: np.ndarray, F1
     return rc, info, passes[:int(info[6])], buf[:int(info[18])]
 
 
+def _plan_params(lds_bytes: int, W: int, cls: int) -> np.ndarray:
+    """fa_level_plan's params (plan.cpp): LDS bytes, bitmap words, accumulator bytes,
+    class layout (0: off, 1: by the wave-step read model, 2: always)."""
+    return np.array([lds_bytes, W, 4.0, cls], dtype=np.float64)
+
+
 def emulate_level_plan(bits_by_rank: np.ndarray, info, passes, buf, m: int, C: int) -> np.ndarray:
-    """CPU model of both level kernels over the plan written by fa_level_plan;
+    """CPU model of the slab kernel over the plan written by fa_level_plan;
     bits_by_rank: bool [F1, ncols]."""
     n_used = int(info[3])
     used = buf[info[13]:info[13] + n_used]
     bits = bits_by_rank[used]
     gext = buf[info[14]:info[14] + C]
     out = np.zeros(C, np.int64)
-    if info[0] == 1:
-        class _Plan:
-            pass
-        pl = _Plan()
-        npc, nw = int(info[4]), int(info[5])
-        pl.pieces = buf[info[16]:info[16] + 4 * npc].reshape(-1, 4)
-        pl.witems = buf[info[17]:info[17] + 2 * nw].reshape(-1, 2)
-        pl.passes = passes
-        pl.d1, pl.d2 = int(info[7]), int(info[8])
-        G = (int(info[16]) - int(info[15])) // m
-        gpre = buf[info[15]:info[15] + G * m].reshape(-1, m)
-        return emulate_trie(bits, gpre, gext, pl)
     npc = int(info[4])
     gpre = buf[info[15]:info[16]]
     loc = buf[info[16]:info[16] + 2 * npc].reshape(-1, 2)
@@ -896,47 +748,6 @@ def emulate_slab_records(bits_by_rank: np.ndarray, info, passes, buf, C: int) ->
     return out
 
 
-def emulate_trie_records(bits_by_rank: np.ndarray, info, passes, buf, m: int, C: int) -> np.ndarray:
-    """CPU model of k_count_trie over the 32-B piece records of a trie plan
-    (fa_level_plan info[20], plan.cpp fa_trie_records); must equal emulate_level_plan."""
-    used = buf[info[13]:info[13] + int(info[3])]
-    bits = bits_by_rank[used]
-    gext = buf[info[14]:info[14] + C]
-    gpre = buf[info[15]:info[16]]
-    npc, nw = int(info[4]), int(info[5])
-    rec = buf[info[20]:info[20] + 8 * npc].view(np.uint32).reshape(-1, 8)
-    witems = buf[info[17]:info[17] + 2 * nw].reshape(-1, 2)
-    d1, d2 = int(info[7]), int(info[8])
-    out = np.zeros(C, np.int64)
-    ones = np.ones(bits.shape[1], bool)
-    for w0, w1, base in passes.tolist():
-        for wi in range(w0, w1):
-            pa, pb = witems[wi]
-            P1 = ones.copy()
-            for j in range(d1):
-                P1 &= bits[gpre[int(rec[pa, 1]) + j]]
-            P2, p = P1.copy(), P1.copy()
-            for pi in range(pa, pb):
-                r = rec[pi]
-                e0, n, flg, long_ = int(r[0] & 0x1FFFF), int((r[0] >> 17) & 63), int((r[0] >> 23) & 3), \
-                    bool((r[0] >> 25) & 1)
-                ids = gpre[int(r[1]) + d1:int(r[1]) + m] if long_ else \
-                    np.stack([r[4:8] & 0xFFFF, r[4:8] >> 16], axis=-1).reshape(-1)[:m - d1]
-                if flg & 2:
-                    P2 = P1.copy()
-                    for u in ids[:d2 - d1]:
-                        P2 &= bits[u]
-                if flg & 1:
-                    p = P2.copy()
-                    for u in ids[d2 - d1:]:
-                        p &= bits[u]
-                first = [int(r[2] & 0xFFFF), int(r[2] >> 16), int(r[3] & 0xFFFF), int(r[3] >> 16)]
-                for k in range(n):
-                    u = first[k] if k < 4 else int(gext[base + e0 + k])
-                    out[base + e0 + k] += int((p & bits[u]).sum())
-    return out
-
-
 LAST_LEVEL_PLAN: dict = {}   # shape of the last count_level call (diagnostics)
 CLS_LEVELS = [0]             # count_level calls that ran the class layout (diagnostics, tests)
 
@@ -960,11 +771,11 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
                 wword, kernel: str = "auto", poff: np.ndarray | None = None, full_bm=None,
                 sup_frac: float = 0.0) -> torch.Tensor | None:
     """Support counts of one level on the device: one native planning call
-    (csrc/host/plan.cpp fa_level_plan: used items, kernel choice, work items,
-    accumulator passes) into one pinned buffer, one host->device copy, then the
-    trie-shared (k_count_trie) or slab (k_count_slab) kernel per pass.
+    (csrc/host/plan.cpp fa_level_plan: used items, slab width, pieces, accumulator
+    passes, class layout) into one pinned buffer, one host->device copy, then the
+    slab kernel (k_count_slab_rec) per pass.
 
-    kernel: auto (trie where it saves enough slab-row reads) | trie | slab.
+    kernel: accepted for compatibility ("auto" | "slab": both the slab kernel).
     prefix: int32 [G, m], or (poff given) a flat int32 array with group g's
     prefix at poff[g]:poff[g+1] — groups of several levels (k) in one launch.
     full_bm: optional callable(used ranks) returning (bitmap, rank -> bitmap row map
@@ -984,9 +795,8 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
     eo = np.ascontiguousarray(ext_off, dtype=np.int64)
     ex = np.ascontiguousarray(ext, dtype=np.int32)
     W = (ncols + 63) // 64
-    min_saving = {"auto": _TRIE_MIN_SAVING, "trie": 0.0, "slab": 2.0}[kernel]
-    params = np.array([_LDS_BYTES, min_saving, _TRIE_CONFLICT[16], _TRIE_CONFLICT[8], TRIE_PASS_WEIGHT,
-                       TRIE_ROUNDS, TRIE_EMAX, W, 4.0, SLAB_CLS], dtype=np.float64)
+    # the class layout has no weighted (dedup) kernel: unit weights only
+    params = _plan_params(_LDS_BYTES, W, SLAB_CLS if wword is None else 0)
     bound = _level_plan_bound(F1, C, G, m)
     on_gpu = dev.type == "cuda"
     stage = pinned_stage("level_plan") if on_gpu else None
@@ -1005,7 +815,7 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
         return None
     if rc != 0:
         raise RuntimeError(f"fa_level_plan failed ({rc})")
-    kern, sw, cap, n_used, npass = int(info[0]), int(info[1]), int(info[2]), int(info[3]), int(info[6])
+    sw, cap, n_used, npass = int(info[1]), int(info[2]), int(info[3]), int(info[6])
     total = int(info[18])
     dbuf = buf[:total].to(dev, non_blocking=True)
     if on_gpu:
@@ -1013,7 +823,7 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
         stage.event.record()
     base = dbuf.data_ptr()
     passes = passes[:npass]
-    o_im, o_used, o_gext, o_gpre, o_pc, o_wi, o_gpm, o_rec = (int(info[i]) for i in (12, 13, 14, 15, 16, 17, 19, 20))
+    o_im, o_used, o_gpre, o_rec = (int(info[i]) for i in (12, 13, 15, 20))
     out = torch.zeros(C, dtype=_I32, device=dev)
     bm, bm_rows = None, None
     if npass > 1:
@@ -1033,26 +843,17 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
     dense = wword is None and DENSE_MIN_ROWS > 0 and sup_frac * sw * 64 >= DENSE_MIN_ROWS
     for q, (a, b, e0) in enumerate(passes.tolist()):
         Cq = bounds[q + 1] - e0
-        if kern == 1:
-            lds = n_used * sw * 8 + Cq * 4
-            n_wg = int(max(1, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2))))
-            _hip_call("fa_hip_count_trie", _p(roff), _p(ranks), _p(src), ncols, base + 4 * o_im, n_used,
-                      base + 4 * o_gpre, m, int(info[7]), int(info[8]), base + 4 * o_rec, base + 4 * (o_wi + 2 * a),
-                      b - a, base + 4 * (o_gext + e0), Cq, _p(wword), out.data_ptr() + 4 * e0, sw, n_wg, _p(bm),
-                      bm.stride(0) if bm is not None else 0, st, bm_rows)
-        else:
-            # piece records (k_count_slab_rec): 48 B per piece, loaded one piece ahead
-            lds = n_used * (sw + 2) * 8 + Cq * 4 + _slab_map_lds(F1)
-            n_wg = int(max(1, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2))))
-            _hip_call("fa_hip_count_slab_rec_cls", _p(roff), _p(ranks), _p(src), ncols, base + 4 * o_im, F1,
-                      n_used, base + 4 * o_gpre, base + 4 * (o_rec + 12 * a), b - a, Cq, _p(wword),
-                      out.data_ptr() + 4 * e0, sw, n_wg, _p(bm), bm.stride(0) if bm is not None else 0, st,
-                      bm_rows, None, int(info[23]) | (2 if dense else 0))
+        # piece records (k_count_slab_rec): 48 B per piece, loaded one piece ahead
+        lds = n_used * (sw + 2) * 8 + Cq * 4 + _slab_map_lds(F1)
+        n_wg = int(max(1, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2))))
+        _hip_call("fa_hip_count_slab_rec_cls", _p(roff), _p(ranks), _p(src), ncols, base + 4 * o_im, F1,
+                  n_used, base + 4 * o_gpre, base + 4 * (o_rec + 12 * a), b - a, Cq, _p(wword),
+                  out.data_ptr() + 4 * e0, sw, n_wg, _p(bm), bm.stride(0) if bm is not None else 0, st,
+                  bm_rows, None, int(info[23]) | (2 if dense else 0))
     CLS_LEVELS[0] += int(info[23])
     LAST_LEVEL_PLAN.clear()
-    LAST_LEVEL_PLAN.update(kernel="trie" if kern == 1 else "slab", rows=int(roff.numel() - 1), used=n_used, sw=sw,
-                           cap=cap, passes=npass, pieces=int(info[4]), witems=int(info[5]), d1=int(info[7]),
-                           d2=int(info[8]), trie_reads=int(info[9]), slab_reads=int(info[10]), m=m, C=C,
+    LAST_LEVEL_PLAN.update(kernel="slab", rows=int(roff.numel() - 1), used=n_used, sw=sw,
+                           cap=cap, passes=npass, pieces=int(info[4]), slab_reads=int(info[10]), m=m, C=C,
                            cls=int(info[23]), step_reads=int(info[21]), step_reads_cls=int(info[22]),
                            dense=bool(dense))
     return out.to(_I64)
@@ -1360,31 +1161,134 @@ def _compact_lines(scratch, xscratch, bound_off, dcnt, xcnt, nl, st):
     return off, items, extras
 
 
+PARSE_HIST_CAP = None       # kHistCap of the tile parser's fused F1 histogram (parse.hip)
+
+
+def parse_hist_cap() -> int:
+    global PARSE_HIST_CAP
+    if PARSE_HIST_CAP is None:
+        PARSE_HIST_CAP = int(_native.hip().fa_hip_tparse_hist_cap())
+    return PARSE_HIST_CAP
+
+
+class TileParse:
+    """The tile parser's per-region steps (csrc/hip/parse.hip k_tline_count,
+    k_tparse, k_tcompact), all queued on one stream.  Line counts come either
+    from a device scan with one readback (whole shard) or from the host's count
+    of the region's '\n' bytes (streamed regions: no readback at all).  Items of
+    every region are written at a device-side running offset into one buffer
+    sized by the upper bound (bytes + 1) / 2; the F1 histogram (items and repeats,
+    ids < parse_hist_cap()) accumulates per compaction block."""
+
+    GRID = 1024       # compaction workgroups (rows of the histogram partials): 4 per CU
+
+    def __init__(self, buf: torch.Tensor, n: int, dev, scratch_bytes: int, xcap: int | None = None):
+        self.buf, self.n, self.dev = buf, n, dev
+        self.st = _stream(buf)
+        self.lib = _native.hip()
+        cap = parse_hist_cap()
+        tok_cap = (n + 1) // 2 + 1           # tokens are separated: at most (bytes + 1) / 2
+        self.items = torch.empty(tok_cap, dtype=_I32, device=dev)
+        # repeated ids are rare: a small buffer, and a second parse in the rare file that overflows it
+        self.xcap = max(int(xcap if xcap is not None else n // 64 + 4096), 1)
+        self.extras = torch.empty(self.xcap, dtype=_I32, device=dev)
+        self.hpart = torch.zeros(self.GRID * cap, dtype=_I64, device=dev)
+        self.flags = torch.zeros(4, dtype=_I32, device=dev)
+        self.cursor = torch.zeros(2, dtype=_I64, device=dev)     # items, repeats written so far
+        self.offs = []                                           # per region: int64 line offsets
+        self.scratch_ids = scratch_bytes // 2 + 2
+        self.scratch = torch.empty(self.scratch_ids, dtype=_I32, device=dev)
+        self.xscratch = torch.empty(self.scratch_ids, dtype=_I32, device=dev)
+        self.n_lines = 0
+
+    def region(self, lo: int, hi: int, n_lines: int | None, tail: bool) -> None:
+        """Lines of bytes [lo, hi): lo is a line start, hi follows a terminator (or
+        is the shard end; tail: its last byte is no terminator, so one more line
+        ends at hi).  n_lines: the region's lines when the host knows them (else one
+        readback of the device count).  Five launches, no host synchronisation:
+        line ends per tile, their scan, the parse, the scan of the tiles' id totals
+        (from the running cursor) and the compaction."""
+        lib, st, dev = self.lib, self.st, self.dev
+        if hi <= lo:
+            return
+        if (hi - lo) // 2 + 1 > self.scratch_ids:
+            # a region past the planned size (long lines carried over, or the final region
+            # after a '\r'): larger slots; the old ones are freed in stream order
+            self.scratch_ids = (hi - lo) // 2 + 2
+            self.scratch = torch.empty(self.scratch_ids, dtype=_I32, device=dev)
+            self.xscratch = torch.empty(self.scratch_ids, dtype=_I32, device=dev)
+        tiles = int(lib.fa_hip_tparse_tiles(lo, hi))
+        tile_cnt = torch.empty(tiles, dtype=_I32, device=dev)
+        _native.check(lib.fa_hip_tline_count(_p(self.buf), lo, hi, _p(tile_cnt), st), "fa_hip_tline_count")
+        tile_base = torch.empty(tiles + 1, dtype=_I64, device=dev)
+        _native.check(lib.fa_hip_scan_small(1, _p(tile_cnt), tiles, _p(tile_base), None, st), "fa_hip_scan_small")
+        if n_lines is None:
+            n_lines = int(tile_base[-1].item()) + (1 if tail else 0)
+        nl = n_lines
+        if nl == 0:
+            return
+        dcnt = torch.empty(nl, dtype=_I32, device=dev)
+        xcnt = torch.empty(nl, dtype=_I32, device=dev)
+        lbase = torch.empty(nl, dtype=_I64, device=dev)
+        tile_dx = torch.empty(2 * tiles, dtype=_I32, device=dev)
+        _native.check(lib.fa_hip_tparse(_p(self.buf), self.buf.numel(), lo, hi, int(bool(tail)), lo,
+                                        _p(tile_base), _p(dcnt), _p(xcnt), _p(lbase), _p(self.scratch),
+                                        _p(self.xscratch), _p(tile_dx), _p(self.flags), st), "fa_hip_tparse")
+        tile_xb = torch.empty(2 * (tiles + 1), dtype=_I64, device=dev)
+        _native.check(lib.fa_hip_scan_small(2, _p(tile_dx), tiles, _p(tile_xb), _p(self.cursor), st),
+                      "fa_hip_scan_small")
+        off = torch.empty(nl, dtype=_I64, device=dev)
+        grid = max(1, min(self.GRID, tiles))
+        _native.check(lib.fa_hip_tcompact(_p(tile_base), _p(tile_xb), tiles, _p(dcnt), _p(xcnt), _p(lbase),
+                                          _p(self.scratch), _p(self.xscratch), _p(self.items), _p(self.extras),
+                                          self.xcap, _p(off), grid, _p(self.hpart), _p(self.flags), st),
+                      "fa_hip_tcompact")
+        self.offs.append(off)
+        self.n_lines += nl
+
+    def finish(self):
+        """(offsets int64 [nl+1], items, extras, vocab size, hist int64 [V] or None), None
+        when a token is not canonical numeric, or the number of repeated ids when they
+        overflowed the repeat buffer (parse again with that room).  One readback."""
+        dev = self.dev
+        tail = torch.cat([self.cursor, self.flags.to(_I64)]).cpu().tolist()
+        n_items, n_extras, bad, mx, over, xover = (int(v) for v in tail)
+        if bad & 1:
+            return None
+        if xover:
+            return n_extras
+        off = torch.cat(self.offs + [self.cursor[:1]]) if self.offs else torch.zeros(1, dtype=_I64, device=dev)
+        V = mx + 1 if self.n_lines else 0       # no lines: an empty vocabulary (as the host parser)
+        hist = None
+        if not over:
+            cap = parse_hist_cap()
+            hist = torch.empty(cap, dtype=_I64, device=dev)
+            _native.check(self.lib.fa_hip_hist_reduce(_p(self.hpart), self.GRID, _p(hist), self.st),
+                          "fa_hip_hist_reduce")
+            hist = hist[:V]
+        return off, self.items[:n_items], self.extras[:n_extras], V, hist
+
+
 def parse_numeric_device(buf: torch.Tensor, n: int, last_is_term: bool):
-    """Parse n file bytes already in HBM (csrc/hip/parse.hip).  ``buf`` is uint8,
-    padded with >= 64 zero bytes past a multiple of 64.  Returns (offsets int64
-    [nl+1], items int32, extras int32, vocab size), all on the device except the
-    vocab size, or None when a token is not canonical numeric (-> dictionary mode)."""
+    """Parse n file bytes already in HBM (csrc/hip/parse.hip tile parser).  ``buf`` is
+    uint8, padded with >= 64 zero bytes past a multiple of 64.  Returns (offsets
+    int64 [nl+1], items int32, extras int32, vocab size, F1 histogram int64 [V] or
+    None), all on the device except the vocab size, or None when a token is not
+    canonical numeric (-> dictionary mode)."""
     dev = buf.device
-    st = _stream(buf)
-    lib = _native.hip()
     if n <= 0:
         return (torch.zeros(1, dtype=_I64, device=dev), torch.zeros(0, dtype=_I32, device=dev),
-                torch.zeros(0, dtype=_I32, device=dev), 0)
+                torch.zeros(0, dtype=_I32, device=dev), 0, None)
     assert buf.numel() >= (n + 63) // 64 * 64 + 64 and buf.dtype == torch.uint8
-    ends, nl, bound_off, nb = _device_lines(buf, n, last_is_term)
-    scratch = torch.empty(nb, dtype=_I32, device=dev)
-    xscratch = torch.empty(nb, dtype=_I32, device=dev)
-    dcnt = torch.empty(nl, dtype=_I32, device=dev)
-    xcnt = torch.empty(nl, dtype=_I32, device=dev)
-    flags = torch.zeros(2, dtype=_I32, device=dev)
-    _native.check(lib.fa_hip_parse_lines(_p(buf), _p(ends), nl, _p(bound_off), _p(scratch), _p(xscratch), _p(dcnt),
-                                         _p(xcnt), _p(flags), st), "fa_hip_parse_lines")
-    fl = flags.cpu().tolist()
-    if fl[0]:
-        return None
-    off, items, extras = _compact_lines(scratch, xscratch, bound_off, dcnt, xcnt, nl, st)
-    return off, items, extras, int(fl[1]) + 1
+    xcap = None
+    for _ in range(2):
+        tp = TileParse(buf, n, dev, n, xcap)
+        tp.region(0, n, None, tail=not last_is_term)
+        got = tp.finish()
+        if not isinstance(got, int):
+            return got
+        xcap = got                     # every repeated id, counted by the first pass
+    raise RuntimeError("device parser: repeat buffer overflow on the second pass")
 
 
 def parse_dict_device(buf: torch.Tensor, n: int, last_is_term: bool):
@@ -1428,180 +1332,6 @@ def parse_dict_device(buf: torch.Tensor, n: int, last_is_term: bool):
     sel = torch.nonzero(occ).flatten()
     hashes = keys[sel].cpu().numpy().view(np.uint64)
     return off, items, extras, hashes, tpos[sel].cpu().numpy(), tlen[sel].cpu().numpy()
-
-
-DFS_PIECE_NODES = 8        # depth-1 nodes per work piece (as the slab kernel's extensions per piece)
-
-
-def plan_bundle_dfs(levels: list, F1: int):
-    """Work pieces of a level bundle for k_count_slab<kDfs> (see csrc/hip/count.hip).
-
-    levels[j] = (pv, pi, eo, ex) of bundle level j: groups' prefixes are pv[pi[g]],
-    candidates eo[g]..eo[g+1] extend them by ex.  Level j+1's prefix rows pv are
-    level j's candidate rows, so level j+1 group g is the child of level-j
-    candidate pi[g].  Even levels are roots (explicit prefix, depth-1 nodes); the
-    odd level after each is read as depth-2 nodes under its parent candidate.
-    Output index of level-j candidate c: sum(C_<j) + c.
-    Returns dict(used, item_map, gpre, gpm, prng, node1, node2, C) (numpy int32)."""
-    sizes = [int(lv[3].size) for lv in levels]
-    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
-    mark = np.zeros(max(F1, 1), dtype=bool)
-    mark[levels[0][0][levels[0][1]].ravel()] = True
-    mark[levels[0][3]] = True
-    used = np.flatnonzero(mark).astype(np.int32)
-    item_map = np.full(max(F1, 1), -1, dtype=np.int32)
-    item_map[used] = np.arange(used.size, dtype=np.int32)
-    gpre_l, gpm_l, prng_l, n1_l, n2_l = [], [], [], [], []
-    gpre_n = n1_n = n2_n = 0
-    for j in range(0, len(levels), 2):
-        pv, pi, eo, ex = levels[j]
-        G, Cj = int(pi.size), int(ex.size)
-        pre = item_map[pv[pi]]                                  # [G, m]
-        m = pre.shape[1]
-        gpre_l.append(pre.ravel())
-        # depth-2 ranges: the child group of every level-j candidate (if any)
-        n2b = np.zeros(Cj, dtype=np.int64)
-        n2e = np.zeros(Cj, dtype=np.int64)
-        if j + 1 < len(levels):
-            _, pi1, eo1, ex1 = levels[j + 1]
-            n2b[pi1] = n2_n + eo1[:-1]
-            n2e[pi1] = n2_n + eo1[1:]
-            n2_l.append(np.stack([item_map[ex1], (off[j + 1] + np.arange(ex1.size)).astype(np.int32)], 1))
-            n2_n += int(ex1.size)
-        n1_l.append(np.stack([item_map[ex], (off[j] + np.arange(Cj)).astype(np.int32),
-                              n2b.astype(np.int32), n2e.astype(np.int32)], 1))
-        # pieces: each group's candidates in chunks of DFS_PIECE_NODES, sharing the group's prefix
-        cnt = np.diff(eo)
-        npc = np.maximum(1, (cnt + DFS_PIECE_NODES - 1) // DFS_PIECE_NODES)
-        gi = np.repeat(np.arange(G), npc)
-        first = np.cumsum(npc) - npc
-        k_in = np.arange(gi.size) - np.repeat(first, npc)
-        b = eo[gi] + k_in * DFS_PIECE_NODES
-        e = np.minimum(eo[gi + 1], b + DFS_PIECE_NODES)
-        gpm_l.append(np.stack([gpre_n + gi * m, np.full(gi.size, m)], 1))
-        prng_l.append(np.stack([n1_n + b, n1_n + e], 1))
-        gpre_n += G * m
-        n1_n += Cj
-    gpm = np.concatenate(gpm_l).astype(np.int32)
-    prng = np.concatenate(prng_l).astype(np.int64)
-    node1 = np.concatenate(n1_l).astype(np.int32)
-    node2 = np.concatenate(n2_l).astype(np.int32) if n2_l else np.zeros((1, 2), np.int32)
-    # cost-sorted pieces (the lanes of a wave then run loops of similar length)
-    n2cnt = (node1[:, 3] - node1[:, 2]).astype(np.int64)
-    c2 = np.concatenate([[0], np.cumsum(n2cnt)])
-    cost = (prng[:, 1] - prng[:, 0]) + (c2[prng[:, 1]] - c2[prng[:, 0]]) + gpm[:, 1]
-    order = np.argsort(-cost, kind="stable")
-    return dict(used=used, item_map=item_map, gpre=np.concatenate(gpre_l).astype(np.int32),
-                gpm=np.ascontiguousarray(gpm[order]), prng=np.ascontiguousarray(prng[order].astype(np.int32)),
-                node1=node1, node2=node2, C=int(off[-1]))
-
-
-def plan_bundle_dfs_native(levels: list, F1: int, out: torch.Tensor | None = None, cap: int = 0):
-    """plan_bundle_dfs in C++ (csrc/host/plan.cpp fa_plan_dfs), written into one int32
-    buffer (``out``, e.g. pinned, grown as needed).  Returns (buf, info, passes) with
-    info = (n_used, NP, N1, N2, C, offsets of item_map, used, gpre, gpm, prng, node1,
-    node2, total, n_passes) and passes int64 [n_passes, 5] = (piece begin, piece end,
-    A0, nA, B0): cap > 0 with two levels splits the pieces into accumulator passes of
-    <= cap counters (node outputs then pass-local; see fa_plan_dfs)."""
-    L = len(levels)
-    pv = [np.ascontiguousarray(lv[0], dtype=np.int32) for lv in levels]
-    pi = [np.ascontiguousarray(lv[1], dtype=np.int32) for lv in levels]
-    eo = [np.ascontiguousarray(lv[2], dtype=np.int64) for lv in levels]
-    ex = [np.ascontiguousarray(lv[3], dtype=np.int32) for lv in levels]
-    arr = lambda xs: (C.c_void_p * L)(*[x.ctypes.data for x in xs])   # noqa: E731
-    m = np.array([x.shape[1] for x in pv], dtype=np.int32)
-    G = np.array([x.size for x in pi], dtype=np.int64)
-    Cn = np.array([x.size for x in ex], dtype=np.int64)
-    NP = sum(int(np.maximum(1, (np.diff(eo[j]) + DFS_PIECE_NODES - 1) // DFS_PIECE_NODES).sum())
-             for j in range(0, L, 2))
-    need = int(2 * F1 + (G * m)[::2].sum() + 4 * NP + 4 * Cn[::2].sum() + 2 * max(int(Cn[1::2].sum()), 1) + 64 + 8)
-    buf = out if out is not None and out.numel() >= need else torch.empty(need, dtype=_I32)
-    info = np.zeros(16, dtype=np.int64)
-    passes = np.zeros((NP + 1, 5), dtype=np.int64)
-    rc = _native.host().fa_plan_dfs(L, C.cast(arr(pv), C.c_void_p), m.ctypes.data, C.cast(arr(pi), C.c_void_p),
-                                    C.cast(arr(eo), C.c_void_p), C.cast(arr(ex), C.c_void_p), G.ctypes.data,
-                                    Cn.ctypes.data, F1, DFS_PIECE_NODES, buf.data_ptr(), buf.numel(),
-                                    info.ctypes.data, int(cap), passes.ctypes.data, passes.shape[0])
-    if rc != 0:
-        raise RuntimeError(f"fa_plan_dfs failed ({rc})")
-    return buf, info, passes[:int(info[13])]
-
-
-def dfs_width(n_used: int, C: int) -> tuple[int, int]:
-    """Slab width and accumulator capacity of the DFS kernel (no rank map in LDS)."""
-    for s in (16, 32, 8, 4):
-        cap = (_LDS_BYTES - n_used * (s + 2) * 8) // 4
-        if cap >= min(C, 8192) or (s == 4 and cap >= 1024):
-            return s, int(cap)
-    return 0, 0
-
-
-def count_bundle_dfs(roff, ranks, src, ncols: int, F1: int, levels: list, full_bm=None,
-                     multi: bool = False) -> torch.Tensor | None:
-    """Counts of every level of a bundle (concatenated, level order) with depth-2
-    prefix reuse (k_count_slab<kDfs>): a level-(k+1) candidate costs one slab-row
-    read under its parent level-k candidate's AND.  One accumulator pass, or (multi,
-    two levels) several passes streaming the slab tiles from the used items' bitmap
-    (full_bm(used) -> (bitmap, rank -> row map or None), as count_level).  None when
-    the bundle does not fit (then the caller counts level by level)."""
-    dev = ranks.device
-    stage = pinned_stage("level_plan")
-    est = 2 * F1 + 8 * sum(int(lv[3].size) + int(lv[1].size) * (lv[0].shape[1] + 2) for lv in levels) + 1024
-    # the used items first (they fix the slab width and so the capacity), then the plan
-    used_mask = np.zeros(max(F1, 1), dtype=bool)
-    used_mask[levels[0][0][levels[0][1]].ravel()] = True
-    used_mask[levels[0][3]] = True
-    n_used = int(used_mask.sum())
-    C_all = sum(int(lv[3].size) for lv in levels)
-    sw, cap = dfs_width(n_used, C_all)
-    if sw == 0:
-        return None
-    npass_needed = C_all > cap
-    if npass_needed and not (multi and len(levels) == 2 and full_bm is not None):
-        return None
-    buf, info, passes = plan_bundle_dfs_native(levels, F1, stage.get(4 * est).view(dtype=_I32),
-                                               cap if npass_needed else 0)
-    NP, C = int(info[1]), int(info[4])
-    total = int(info[12])
-    dbuf = buf[:total].to(dev, non_blocking=True)
-    if buf.is_pinned():
-        stage.event = torch.cuda.Event()
-        stage.event.record()
-    base = dbuf.data_ptr()
-    ptr = [base + 4 * int(info[i]) for i in range(5, 12)]
-    out = torch.zeros(C, dtype=_I32, device=dev)
-    W = (ncols + 63) // 64
-    nslabs = (W + sw - 1) // sw
-    st = _stream(ranks)
-    bm, bm_rows, Wp = None, None, 0
-    if len(passes) > 1:
-        used = np.flatnonzero(used_mask).astype(np.int32)
-        bm, bmap = full_bm(used)
-        Wp = bm.stride(0)
-        if bmap is None:
-            bm_rows = ptr[1]                            # slab row u -> bitmap row used[u] (rank-indexed bitmap)
-        else:
-            rows_t = bmap[dbuf[int(info[6]):int(info[6]) + n_used].to(_I64)]
-            bm_rows = rows_t.data_ptr()
-    P = passes.tolist()
-    for q, (p0, p1, a0, na, b0) in enumerate(P):
-        if len(P) == 1:
-            Cq, nA, outB = C, C, None
-        else:       # this pass's nodes, then their children (up to the next pass's first child)
-            Cq = na + (P[q + 1][4] if q + 1 < len(P) else C) - b0
-            nA, outB = na, out.data_ptr() + 4 * b0
-        lds = n_used * (sw + 2) * 8 + Cq * 4
-        n_wg = int(min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2)))
-        rc = _native.hip().fa_hip_count_dfs(_p(roff), _p(ranks), _p(src), ncols, ptr[0], n_used, ptr[2],
-                                            ptr[3] + 8 * p0, ptr[4] + 8 * p0, ptr[5], ptr[6], p1 - p0, Cq,
-                                            out.data_ptr() + 4 * a0, sw, n_wg, _p(bm), Wp, bm_rows, nA, outB, st)
-        if rc == 3:
-            return None
-        _native.check(rc, "fa_hip_count_dfs")
-    LAST_LEVEL_PLAN.clear()
-    LAST_LEVEL_PLAN.update(kernel="dfs", rows=int(roff.numel() - 1), used=n_used, sw=sw, cap=cap,
-                           passes=len(passes), pieces=NP, witems=0, d1=0, d2=0, trie_reads=0, slab_reads=0, m=-1, C=C)
-    return out.to(_I64)
 
 
 # ---------------------------------------------------------------------------
@@ -1763,7 +1493,7 @@ def dl_count(S: DeviceLevelState, plan: dict, roff, ranks, src, ncols: int, F1: 
               0, C, _p(wword), _p(out), sw, n_wg, None, 0, st, None, _p(S.ctl) + 8 * 221)
     LAST_LEVEL_PLAN.clear()
     LAST_LEVEL_PLAN.update(kernel="slab_dev", rows=int(roff.numel() - 1), used=n_used, sw=sw, cap=cap, passes=1,
-                           pieces=-1, witems=0, d1=0, d2=0, trie_reads=0, slab_reads=0, m=-1, C=C)
+                           pieces=-1, slab_reads=0, m=-1, C=C)
     # (item_map and rec may be freed now: the caching allocator hands their blocks only
     # to work queued later on this stream)
     return out

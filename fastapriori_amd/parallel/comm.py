@@ -40,12 +40,17 @@ def _timed(fn):
             return fn(self, *a, **kw)
         self._depth += 1
         t0 = time.perf_counter()
+        b0 = self.bytes_reduced
         try:
             return fn(self, *a, **kw)
         finally:
             self._depth -= 1
-            self.comm_ms += (time.perf_counter() - t0) * 1e3
+            dt = (time.perf_counter() - t0) * 1e3
+            self.comm_ms += dt
             self.comm_calls += 1
+            if self.trace is not None:
+                # (collective, payload bytes it moved per rank, host ms)
+                self.trace.append((fn.__name__, self.bytes_reduced - b0, round(dt, 3)))
     return wrap
 
 
@@ -60,6 +65,7 @@ class Comm:
     comm_ms: float = 0.0    # host time inside collectives (see _timed)
     comm_calls: int = 0
     _depth: int = 0
+    trace: list | None = None   # set to [] to record every top-level collective (_timed)
 
     @property
     def distributed(self) -> bool:
@@ -301,7 +307,11 @@ def init_comm(device: str | None = None, backend: str | None = None, timeout_s: 
         # HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES shows device_count() == 1: no check)
         n_local = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
         n_dev = torch.cuda.device_count()
-        if n_dev > 1 and n_local > n_dev:
+        # one visible GPU is fine when the launcher narrowed each rank's view to its own
+        # GPU; without such a per-rank variable the ranks would share the device
+        narrowed = any(os.environ.get(v) for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES",
+                                                   "CUDA_VISIBLE_DEVICES"))
+        if n_local > n_dev and not (n_dev == 1 and narrowed):
             raise RuntimeError(f"{n_local} local ranks but {n_dev} visible GPUs: RCCL needs one GPU per rank "
                                "(FA_DIST_BACKEND=gloo lets ranks share a GPU for tests)")
     if not dist.is_initialized():

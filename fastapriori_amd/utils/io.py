@@ -101,47 +101,94 @@ def _next_line_start(fd: int, size: int, pos: int) -> int:
     return size
 
 
-def _file_to_device(fd: int, first: int, n: int, dev) -> torch.Tensor:
-    """Bytes [first, first + n) of the file -> uint8 device tensor padded with zeros
-    to a multiple of 64 plus 64."""
+_copy_streams: dict = {}
+STREAM_PARSE = os.environ.get("FA_STREAM_PARSE", "1") == "1"
+
+
+def _file_to_device(fd: int, first: int, n: int, dev, parse: bool = False, last_is_term: bool = True):
+    r"""Bytes [first, first + n) of the file -> uint8 device tensor padded with zeros
+    to a multiple of 64 plus 64.  Host threads pread _RING_SLOT chunks into a ring
+    of pinned slots; each lands in HBM by an asynchronous copy on a copy stream.
+
+    parse=True also parses while the bytes stream in (csrc/hip/parse.hip tile
+    parser, ops.primitives.TileParse): every chunk's reader thread counts its '\n'
+    bytes and finds the last one (fa_chunk_scan), and as soon as a chunk's copy
+    lands, the lines it completes -- from the previous region's end to just past its
+    last '\n' -- are parsed on the compute stream (it waits for that copy only)
+    while the next chunks are still being read and copied.  The partial last line
+    carries into the next region.  From the first chunk holding a '\r' on (lone
+    '\r' ends lines too), the rest is one final region parsed after the last copy.
+    Returns the buffer, and with parse=True the parser's result
+    (TileParse.finish) as a second value."""
     from concurrent.futures import ThreadPoolExecutor
 
     out = torch.empty((n + 63) // 64 * 64 + 64, dtype=torch.uint8, device=dev)
     out[n:].zero_()
+    tp = None
+    if parse:
+        from ..ops import primitives as prim
+        tp = prim.TileParse(out, n, dev, scratch_bytes=min(n, 2 * _RING_SLOT))
     if n == 0:
-        return out
+        return (out, tp.finish()) if parse else out
     if not _ring:
         _ring.extend(torch.empty(_RING_SLOT, dtype=torch.uint8, pin_memory=True) for _ in range(_RING_SLOTS))
+    cs = _copy_streams.get(dev)
+    if cs is None:
+        cs = _copy_streams[dev] = torch.cuda.Stream(dev)
+    compute = torch.cuda.current_stream(dev)
+    cs.wait_stream(compute)             # the buffer's allocation and zero fill come first
     nch = (n + _RING_SLOT - 1) // _RING_SLOT
     events: list = [None] * _RING_SLOTS
+    lib = _native.host()
 
-    def read_chunk(c: int) -> None:
+    def read_chunk(c: int):
         ev = events[c % _RING_SLOTS]
         if ev is not None:
             ev.synchronize()          # the slot's previous H2D copy has finished
         off = c * _RING_SLOT
         m = min(_RING_SLOT, n - off)
-        mv = memoryview(_ring[c % _RING_SLOTS].numpy())
+        slot = _ring[c % _RING_SLOTS]
+        mv = memoryview(slot.numpy())
         got = 0
         while got < m:
             r = os.preadv(fd, [mv[got:m]], first + off + got)
             if r <= 0:
                 raise OSError(f"short read at {first + off + got}")
             got += r
+        if not parse:
+            return None
+        info = np.zeros(3, dtype=np.int64)
+        lib.fa_chunk_scan(slot.data_ptr(), m, info.ctypes.data)
+        return info
 
+    streaming = parse and STREAM_PARSE
+    rend = 0                            # parsed up to here (a line start)
     with ThreadPoolExecutor(min(num_threads(), _RING_SLOTS)) as ex:
         fut = {c: ex.submit(read_chunk, c) for c in range(min(_RING_SLOTS, nch))}
         for c in range(nch):
-            fut.pop(c).result()
+            info = fut.pop(c).result()
             s, off = c % _RING_SLOTS, c * _RING_SLOT
             m = min(_RING_SLOT, n - off)
-            out[off:off + m].copy_(_ring[s][:m], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
+            with torch.cuda.stream(cs):
+                out[off:off + m].copy_(_ring[s][:m], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(cs)
             events[s] = ev
             if c + _RING_SLOTS < nch:
                 fut[c + _RING_SLOTS] = ex.submit(read_chunk, c + _RING_SLOTS)
-    return out
+            if streaming and c + 1 < nch:
+                if info[2]:
+                    streaming = False   # a '\r': the rest is the final region
+                elif info[1] >= 0:
+                    compute.wait_event(ev)
+                    end = off + int(info[1]) + 1
+                    tp.region(rend, end, int(info[0]), tail=False)
+                    rend = end
+    compute.wait_event(events[(nch - 1) % _RING_SLOTS])
+    if not parse:
+        return out
+    tp.region(rend, n, None, tail=not last_is_term)
+    return out, tp.finish()
 
 
 def parse_file_device(path: str, byte_begin: int, byte_end: int, device, line_base: int = 0,
@@ -165,14 +212,19 @@ def parse_file_device(path: str, byte_begin: int, byte_end: int, device, line_ba
         last = max(last, first)
         n = last - first
         last_is_term = n == 0 or os.pread(fd, 1, last - 1) in (b"\n", b"\r")
-        buf = _file_to_device(fd, first, n, device)
+        if force_dict:
+            buf, got = _file_to_device(fd, first, n, device), None
+        else:
+            buf, got = _file_to_device(fd, first, n, device, parse=True, last_is_term=last_is_term)
+            if isinstance(got, int):
+                # more repeated ids than the streamed parse's repeat buffer: again, with room
+                got = prim.parse_numeric_device(buf, n, last_is_term)
     finally:
         os.close(fd)
-    got = None if force_dict else prim.parse_numeric_device(buf, n, last_is_term)
     if got is not None:
         del buf
-        off, items, extras, vocab = got
-        return TransactionShard(off, items, extras.cpu().numpy(), Vocabulary(True, vocab), line_base)
+        off, items, extras, vocab, hist = got
+        return TransactionShard(off, items, extras.cpu().numpy(), Vocabulary(True, vocab), line_base, hist)
     got = prim.parse_dict_device(buf, n, last_is_term) if DEVICE_DICT else None
     del buf
     if got is None:

@@ -1,0 +1,19 @@
+#!/bin/bash
+# round 4 iteration pass: parser + changed-path tests, e2e breakdown, kernel stats of the
+# read path, all GPU tests, the 8-rank rehearsal, a T40 marker trace (host gaps)
+set -e -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/it
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parse.py tests/test_log_parity.py -m gpu -x -v --timeout 120 --timeout-method thread > $O/tests_parse.log 2>&1
+timeout -k 10 400 python benchmarks/e2e_probe.py --reps 3 --job > $O/probe.json 2> $O/probe.err
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt" -o run -- \
+  python3 "$R/benchmarks/e2e_probe.py" --reps 1 > "$O/kt.log" 2>&1
+cd $R
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/all_tests.log 2>&1
+timeout -k 10 600 python benchmarks/multirank_probe.py --world 8 --n-txn 4000000 > $O/multirank.json 2> $O/multirank.err
+cd /tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --marker-trace --output-format csv -d "$O/mk40" -o run -- \
+  python3 "$R/bench.py" --config T40I10D100M --steps 1 --warmup 0 --e2e off > "$O/mk40.log" 2>&1

@@ -105,30 +105,6 @@ def test_wide_f1_generates_on_device_without_fallbacks(monkeypatch):
     _same(got, ref)
 
 
-def test_multipass_level_paired_depth_first(monkeypatch):
-    # a level that needs several accumulator passes is counted with its children
-    # depth-first (FastApriori._pair_multipass_level, k_count_slab<kDfs> from the bitmap)
-    import fastapriori_amd.ops.primitives as prim
-    cpu = generate_shard(60_000, Comm(), "cpu", 14.0, 6.0, 300, 120, 11)
-    ref, _ = _mine(cpu, 0.004, trim_min_rows=0)
-    monkeypatch.setattr(prim, "_LDS_BYTES", 24 * 1024)
-    monkeypatch.setattr(ap, "DFS_PAIR_MIN_M", 2)
-    monkeypatch.setattr(ap, "DFS_PAIR", True)            # opt-in (FA_DFS_PAIR=1)
-    seen = []
-    real = prim.count_bundle_dfs
-
-    def spy(*a, **kw):
-        out = real(*a, **kw)
-        seen.append((kw.get("multi"), prim.LAST_LEVEL_PLAN.get("passes"), out is not None))
-        return out
-    monkeypatch.setattr(prim, "count_bundle_dfs", spy)
-    got, _ = _mine(cpu.to(DEV), 0.004, trim_min_rows=0)
-    assert any(m and p and p > 1 and ok for m, p, ok in seen), seen
-    assert len(ref.levels) >= 5
-    assert got.as_dict() == ref.as_dict()
-    _same(got, ref)
-
-
 def test_f2_stays_on_device_until_the_flush(monkeypatch):
     # F_2 compacted on the device (no readback between the pair kernel and the first
     # bundle): same itemsets, and the reference's log lines in level order

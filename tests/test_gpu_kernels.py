@@ -148,8 +148,6 @@ def test_bitmaps_pairs_candidates(F1_frac):
     assert torch.equal(ref, got)
     slab = ops.count_level(roff.to(DEV), ranks.to(DEV), None, T, F1, prev[pidx], eoff, ext, None, kernel="slab")
     assert slab is not None and torch.equal(ref, slab.cpu())
-    trie = ops.count_level_trie(roff.to(DEV), ranks.to(DEV), None, T, F1, prev[pidx], eoff, ext, None)
-    assert trie is not None and torch.equal(ref, trie.cpu())
 
 
 def test_slab_many_passes_and_levels():
@@ -267,26 +265,6 @@ def test_bundling_chain_matches_python_loop(monkeypatch):
     monkeypatch.setattr(ap, "GEN_CHAIN", False)
     b = FastApriori(0.003, config=MinerConfig(min_support=0.003)).run(sh)
     assert a.as_dict() == b.as_dict()
-
-
-@pytest.mark.parametrize("n,ms", [(200000, 0.003), (60000, 0.002)])
-def test_bundle_dfs_matches_slab_and_cpu(monkeypatch, n, ms):
-    # depth-2 prefix reuse over bundled levels == the plain slab bundle == the CPU miner
-    import fastapriori_amd.models.apriori as ap
-    sh = generate_shard(n, Comm(), "cpu", 10.0, 4.0, 60, 80, seed=12)
-    ref = FastApriori(ms, config=MinerConfig(min_support=ms, dedup="off")).run(sh).as_dict()
-    shg = sh.to(DEV)
-    seen = []
-    real = ops.primitives.count_bundle_dfs
-    monkeypatch.setattr(ops.primitives, "count_bundle_dfs",
-                        lambda *a, **k: seen.append(1) or real(*a, **k))
-    monkeypatch.setattr(ap, "BUNDLE_DFS_MIN_M", 2)        # every bundle
-    monkeypatch.setattr(ap, "BUNDLE_DFS", True)           # (opt-in: FA_BUNDLE_DFS=1)
-    a = FastApriori(ms, config=MinerConfig(min_support=ms, dedup="off")).run(shg).as_dict()
-    assert seen, "no bundle took the DFS kernel"
-    monkeypatch.setattr(ap, "BUNDLE_DFS", False)
-    b = FastApriori(ms, config=MinerConfig(min_support=ms, dedup="off")).run(shg).as_dict()
-    assert a == b == ref
 
 
 def test_parse_to_device_roundtrip():
@@ -408,35 +386,22 @@ def test_trim_rows_matches_cpu(weighted):
             assert torch.equal(a, b.cpu())
 
 
-@pytest.mark.parametrize("sw", ["8", "16", "32"])
-@pytest.mark.parametrize("lds_kb", [0, 24])
-def test_trie_kernel_widths_and_passes(monkeypatch, sw, lds_kb):
-    # every slab width, single- and multi-pass (bitmap tiles), unit and dedup weights:
-    # whole-miner results must equal the CPU reference through the deep levels
+@pytest.mark.parametrize("lds_kb", [0, 24, 12])
+def test_slab_kernel_budgets_and_weights(monkeypatch, lds_kb):
+    # single- and multi-pass slab plans (smaller LDS budgets: narrower slabs, more
+    # passes from the bitmap tiles), unit and dedup weights: whole-miner results must
+    # equal the CPU reference through the deep levels
     import fastapriori_amd.ops.primitives as prim
     sh = generate_shard(30000, Comm(), "cpu", 14.0, 6.0, 200, 120, seed=17)
     cfg = dict(min_support=0.004)
     ref = FastApriori(0.004, config=MinerConfig(trim_min_rows=0, level_kernel="bitmap", dedup="off", **cfg)).run(sh)
     assert len(ref.levels) >= 5
-    monkeypatch.setenv("FA_SLAB_SW", sw)
     if lds_kb:
         monkeypatch.setattr(prim, "_LDS_BYTES", lds_kb * 1024)
     for dd in ("off", "on"):
-        got = FastApriori(0.004, config=MinerConfig(trim_min_rows=0, level_kernel="trie", dedup=dd, **cfg)).run(
+        got = FastApriori(0.004, config=MinerConfig(trim_min_rows=0, level_kernel="slab", dedup=dd, **cfg)).run(
             sh.to(DEV))
-        assert ref.as_dict() == got.as_dict(), (sw, lds_kb, dd)
-        if lds_kb:
-            assert prim.LAST_TRIE_PLAN["passes"] >= 1
-
-
-def test_trie_kernel_small_work_items(monkeypatch):
-    import fastapriori_amd.ops.primitives as prim
-    sh = generate_shard(20000, Comm(), "cpu", 12.0, 5.0, 150, 100, seed=19)
-    ref = FastApriori(0.005, config=MinerConfig(min_support=0.005, trim_min_rows=0, level_kernel="bitmap")).run(sh)
-    monkeypatch.setattr(prim, "TRIE_EMAX", 1)
-    got = FastApriori(0.005, config=MinerConfig(min_support=0.005, trim_min_rows=0, level_kernel="trie")).run(
-        sh.to(DEV))
-    assert ref.as_dict() == got.as_dict()
+        assert ref.as_dict() == got.as_dict(), (lds_kb, dd)
 
 
 def test_bundled_levels_on_gpu(monkeypatch):

@@ -137,3 +137,61 @@ def test_read_shard_uses_device_parser(tmp_path, monkeypatch):
     monkeypatch.setattr(io, "parse_file_device", lambda *a, **k: calls.append(1) or orig(*a, **k))
     sh = io.read_shard(p, Comm(device=DEV), DEV)
     assert calls and sh.items.is_cuda and sh.n_lines == 3000 and sh.extras.size == 1000
+
+
+def test_lines_longer_than_the_halo_and_tiles(tmp_path):
+    # the tile parser stages 2 KB before each 16 KB tile: longer lines read their head
+    # from HBM, and a 40 KB line spans whole tiles without a line end
+    rng = np.random.default_rng(5)
+    lines = [" ".join(map(str, rng.integers(0, 1000, L))) for L in (3, 700, 5, 9000, 2, 1, 1200)]
+    p = _write(tmp_path, ("\n".join(lines) + "\n" + "\n".join(lines)).encode())
+    g = _same(p)
+    assert g.extras.size > 0
+
+
+def test_parser_histogram_counts_occurrences(tmp_path):
+    rng = np.random.default_rng(9)
+    lines = [" ".join(map(str, rng.integers(0, 3000, int(rng.integers(0, 40))))) for _ in range(5000)]
+    p = _write(tmp_path, ("\n".join(lines) + "\n").encode())
+    g = _same(p)
+    assert g.hist is not None and g.hist.numel() == g.vocab.size
+    want = torch.bincount(g.items.cpu().long(), minlength=g.vocab.size)
+    want += torch.bincount(torch.from_numpy(g.extras.astype(np.int64)), minlength=g.vocab.size)
+    assert torch.equal(g.hist.cpu(), want)
+
+
+def test_wide_ids_skip_the_parser_histogram(tmp_path):
+    p = _write(tmp_path, b"1 2 3\n9000 2\n")      # id 9001 >= the LDS histogram's 8192 bins
+    g = _same(p)
+    assert g.hist is None
+
+
+def test_repeat_buffer_overflow_parses_again(tmp_path):
+    p = _write(tmp_path, b"1 1 1 2 2\n" * 40000)   # 120K repeats > the first pass's repeat buffer
+    g = _same(p)
+    assert g.extras.size == 120000
+
+
+@pytest.mark.parametrize("slot", [4096, 6000])
+def test_streamed_regions_match_host_parser(tmp_path, monkeypatch, slot):
+    # small ring slots: the bytes arrive in many chunks, each parsed as its copy lands
+    # (lines carried across chunks, a line longer than a chunk, a '\r' in a late chunk
+    # that turns the rest into the final region)
+    rng = np.random.default_rng(13)
+    parts = []
+    for i in range(4000):
+        L = int(rng.integers(0, 30)) if i != 1500 else 3000
+        toks = rng.integers(0, 400, L)
+        parts.append(" ".join(map(str, toks)).encode() + (b"\r\n" if i == 3500 else b"\n"))
+    data = b"".join(parts)
+    monkeypatch.setattr(io, "_RING_SLOT", slot)
+    p = _write(tmp_path, data)
+    _same(p)
+    p2 = _write(tmp_path, data.replace(b"\r\n", b"\n") + b"5 6", name="D2.dat")
+    g = _same(p2)
+    assert g.hist is not None
+    size = len(data)
+    total = 0
+    for b, e in ((0, size // 3), (size // 3, size)):
+        total += _same(p, b, e).n_lines
+    assert total == io.parse_file(p, 0, -1, 0, "cpu").n_lines

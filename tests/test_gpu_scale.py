@@ -1,9 +1,9 @@
 """GPU correctness at scale: the default device path (fused compression, queue-
-scheduled pair kernel, level bundles, depth-2 DFS bundles, trie kernel, transaction
-trimming) against the C++ CPU miner on the same synthetic databases.
+scheduled pair kernel, device level bundles, the slab kernel's class layout,
+transaction trimming) against the C++ CPU miner on the same synthetic databases.
 
 * 2M Quest rows (T10I4 shape), default MinerConfig: trimming is live
-  (trim_min_rows = 1 << 20), bundling and the DFS bundle kernel run.
+  (trim_min_rows = 1 << 20) and the device level bundles run.
 * 400K T40I10 rows at min_sup 0.5 %: >= 8 levels (the deep-k path; trimming forced
   on so every level's trim + re-layout runs).
 Both compare the complete itemset -> count maps (exact integers).

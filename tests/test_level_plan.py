@@ -1,15 +1,14 @@
-"""Planner of the trie-shared level kernel (csrc/host/plan.cpp), checked on CPU.
-
-ops.emulate_trie executes a plan with the kernel's exact semantics (P1/P2/p
-registers, piece flags, pass-local extension offsets) over a bool bitmap; its
-counts must equal brute-force support counts for every split depth, work-item
-size and accumulator capacity (many passes included).
+"""Planner of the slab level kernel (csrc/host/plan.cpp fa_level_plan), checked on
+CPU: ops.primitives.emulate_level_plan executes a plan's pieces and
+emulate_slab_records the 48-B records with k_count_slab_rec's exact semantics
+(class-layout keep flags, pass-local extension offsets) over a bool bitmap; both
+must equal brute-force support counts for every accumulator capacity (many passes
+included), prefix length and layout.
 """
 import numpy as np
 import pytest
 
-from fastapriori_amd import ops
-from fastapriori_amd.ops.host import apriori_gen, plan_trie
+from fastapriori_amd.ops.host import apriori_gen
 
 
 def _level(rng, n_items=14, n_rows=400, k=4, dens=0.45):
@@ -24,70 +23,11 @@ def _level(rng, n_items=14, n_rows=400, k=4, dens=0.45):
     return bits, np.array(prev, dtype=np.int32).reshape(-1, m)
 
 
-@pytest.mark.parametrize("k", [3, 4, 5])
-@pytest.mark.parametrize("emax,cap", [(24, 1 << 20), (3, 1 << 20), (5, 7), (1, 2)])
-@pytest.mark.parametrize("depths", [None, (0, 0), (1, 1), "max"])
-def test_plan_counts_match_brute_force(k, emax, cap, depths):
-    rng = np.random.default_rng(k * 7 + emax)
-    bits, prev = _level(rng, k=k)
-    pidx, eoff, ext = apriori_gen(prev)
-    if ext.size == 0:
-        pytest.skip("no candidates")
-    P = prev[pidx]
-    m = P.shape[1]
-    d1, d2 = (-1, -1) if depths is None else ((m - 1, m - 1) if depths == "max" else depths)
-    plan = plan_trie(P, eoff, emax, cap, d1, d2)
-    g_of_e = np.repeat(np.arange(pidx.size), np.diff(eoff))
-    want = np.array([np.logical_and.reduce(bits[list(P[g]) + [e]]).sum() for g, e in zip(g_of_e, ext)])
-    got = ops.emulate_trie(bits, P, ext, plan)
-    assert np.array_equal(got, want)
-    # structure: pieces cover every extension once; passes respect the capacity
-    cover = np.zeros(ext.size, np.int64)
-    for w0, w1, base in plan.passes.tolist():
-        for a, b in plan.witems[w0:w1]:
-            for off, e0, e1, f in plan.pieces[a:b]:
-                assert e1 - e0 <= emax
-                cover[base + e0:base + e1] += 1
-    assert np.all(cover == 1)
-    nxt = list(plan.passes[1:, 2]) + [ext.size]
-    assert all(b - a <= cap for a, b in zip(plan.passes[:, 2], nxt))
-    assert plan.reads <= plan.reads_unshared
-
-
-def test_weighted_emulation():
-    rng = np.random.default_rng(5)
-    bits, prev = _level(rng, k=3)
-    pidx, eoff, ext = apriori_gen(prev)
-    P = prev[pidx]
-    w = rng.integers(0, 4, bits.shape[1])
-    plan = plan_trie(P, eoff, 8, 1 << 20)
-    g_of_e = np.repeat(np.arange(pidx.size), np.diff(eoff))
-    want = np.array([(np.logical_and.reduce(bits[list(P[g]) + [e]]) * w).sum() for g, e in zip(g_of_e, ext)])
-    assert np.array_equal(ops.emulate_trie(bits, P, ext, plan, w), want)
-
-
-def test_sharing_reduces_reads_on_deep_levels():
-    # downward-closed deep level: every 6-subset of three overlapping 11-itemsets
-    from itertools import combinations
-    rng = np.random.default_rng(1)
-    core = rng.choice(30, 6, replace=False)
-    rows = set()
-    for _ in range(3):
-        big = np.sort(np.concatenate([core, rng.choice(np.setdiff1d(np.arange(30), core), 5, replace=False)]))
-        rows.update(combinations(big.tolist(), 6))
-    prev = np.array(sorted(rows), np.int32)
-    pidx, eoff, ext = apriori_gen(prev)
-    plan = plan_trie(prev[pidx], eoff, 24, 1 << 20)
-    assert ext.size > 100
-    assert plan.reads * 1.5 < plan.reads_unshared
-
-
-@pytest.mark.parametrize("kernel", ["slab", "trie", "auto"])
 @pytest.mark.parametrize("lds_kb", [160, 6, 3])
 @pytest.mark.parametrize("k", [3, 5])
-def test_level_plan_counts(kernel, lds_kb, k):
-    # fa_level_plan (one-call planner feeding the GPU level kernels) for both kernels,
-    # single- and multi-pass, must reproduce brute-force supports
+def test_level_plan_counts(lds_kb, k):
+    # fa_level_plan (one-call planner feeding the GPU level kernel), single- and
+    # multi-pass, must reproduce brute-force supports
     from fastapriori_amd.ops.primitives import emulate_level_plan, emulate_slab_records, level_plan_host
     rng = np.random.default_rng(k)
     bits, prev = _level(rng, n_items=16, k=k)
@@ -95,24 +35,18 @@ def test_level_plan_counts(kernel, lds_kb, k):
     if ext.size == 0:
         pytest.skip("no candidates")
     P = prev[pidx]
-    rc, info, passes, buf = level_plan_host(P, eoff, ext, bits.shape[0], (bits.shape[1] + 63) // 64, kernel,
+    rc, info, passes, buf = level_plan_host(P, eoff, ext, bits.shape[0], (bits.shape[1] + 63) // 64,
                                             lds_bytes=lds_kb * 1024)
     if rc == 4:                      # no slab fits this LDS budget: the caller uses the bitmap kernel
         assert lds_kb < 8
         return
     assert rc == 0
-    if kernel != "auto" and lds_kb == 160:
-        assert info[0] == (1 if kernel == "trie" else 0)
     assert info[6] >= 1 and (info[6] > 1) == (ext.size > info[2])
     g_of_e = np.repeat(np.arange(pidx.size), np.diff(eoff))
     want = np.array([np.logical_and.reduce(bits[list(P[g]) + [e]]).sum() for g, e in zip(g_of_e, ext)])
     got = emulate_level_plan(bits, info, passes, buf, P.shape[1], ext.size)
     assert np.array_equal(got, want)
-    if info[0] == 0:                 # slab plan: the 48-B piece records of k_count_slab_rec agree
-        assert np.array_equal(emulate_slab_records(bits, info, passes, buf, ext.size), want)
-    else:                            # trie plan: the 32-B piece records of k_count_trie agree
-        from fastapriori_amd.ops.primitives import emulate_trie_records
-        assert np.array_equal(emulate_trie_records(bits, info, passes, buf, P.shape[1], ext.size), want)
+    assert np.array_equal(emulate_slab_records(bits, info, passes, buf, ext.size), want)
 
 
 @pytest.mark.parametrize("k", [7, 11, 15])
@@ -126,33 +60,11 @@ def test_slab_records_long_prefixes(k):
     if ext.size == 0:
         pytest.skip("no candidates")
     P = prev[pidx]
-    rc, info, passes, buf = level_plan_host(P, eoff, ext, bits.shape[0], 5, "slab")
-    assert rc == 0 and info[0] == 0
+    rc, info, passes, buf = level_plan_host(P, eoff, ext, bits.shape[0], 5)
+    assert rc == 0
     g_of_e = np.repeat(np.arange(pidx.size), np.diff(eoff))
     want = np.array([np.logical_and.reduce(bits[list(P[g]) + [e]]).sum() for g, e in zip(g_of_e, ext)])
     assert np.array_equal(emulate_slab_records(bits, info, passes, buf, ext.size), want)
-
-
-@pytest.mark.parametrize("k", [6, 10, 14])
-def test_trie_records_long_prefixes(k):
-    # k_count_trie records hold the prefix ids past D1 inline when there are <= 8 of
-    # them, and point into gpre beyond that; extensions past the first four come
-    # from gext
-    from fastapriori_amd.ops.primitives import emulate_trie_records, level_plan_host
-    rng = np.random.default_rng(k)
-    bits, prev = _level(rng, n_items=16, n_rows=300, k=k, dens=0.88)
-    pidx, eoff, ext = apriori_gen(prev)
-    if ext.size == 0:
-        pytest.skip("no candidates")
-    P = prev[pidx]
-    for lds_kb in (160, 6):
-        rc, info, passes, buf = level_plan_host(P, eoff, ext, bits.shape[0], 5, "trie", lds_bytes=lds_kb * 1024)
-        if rc == 4:                  # no slab width fits the small budget
-            continue
-        assert rc == 0 and info[0] == 1
-        g_of_e = np.repeat(np.arange(pidx.size), np.diff(eoff))
-        want = np.array([np.logical_and.reduce(bits[list(P[g]) + [e]]).sum() for g, e in zip(g_of_e, ext)])
-        assert np.array_equal(emulate_trie_records(bits, info, passes, buf, P.shape[1], ext.size), want)
 
 
 def test_level_plan_mixed_prefix_lengths():
@@ -169,8 +81,8 @@ def test_level_plan_mixed_prefix_lengths():
     poff = np.concatenate([[0], np.cumsum(np.concatenate([np.full(g[0].shape[0], g[0].shape[1]) for g in groups]))])
     eoff = np.concatenate([[0], np.cumsum(np.concatenate([np.diff(g[1]) for g in groups]))])
     ext = np.concatenate([g[2] for g in groups]).astype(np.int32)
-    rc, info, passes, buf = level_plan_host(flat, eoff, ext, bits.shape[0], 8, "auto", poff=poff)
-    assert rc == 0 and info[0] == 0          # mixed lengths always take the slab kernel
+    rc, info, passes, buf = level_plan_host(flat, eoff, ext, bits.shape[0], 8, poff=poff)
+    assert rc == 0
     want = []
     for P, eo, ex in groups:
         g_of_e = np.repeat(np.arange(P.shape[0]), np.diff(eo))
@@ -216,8 +128,8 @@ def test_slab_class_layout_counts(k, lds_kb):
     if ext.size == 0:
         pytest.skip("no candidates")
     P = prev[pidx]
-    rc, info, passes, buf = level_plan_host(P, eoff, ext, bits.shape[0], 5, "slab", lds_bytes=lds_kb * 1024, cls=2)
-    assert rc == 0 and info[0] == 0 and info[23] == 1
+    rc, info, passes, buf = level_plan_host(P, eoff, ext, bits.shape[0], 5, lds_bytes=lds_kb * 1024, cls=2)
+    assert rc == 0 and info[23] == 1
     g_of_e = np.repeat(np.arange(pidx.size), np.diff(eoff))
     want = np.array([np.logical_and.reduce(bits[list(P[g]) + [e]]).sum() for g, e in zip(g_of_e, ext)])
     assert np.array_equal(emulate_level_plan(bits, info, passes, buf, P.shape[1], ext.size), want)
@@ -238,8 +150,8 @@ def test_slab_class_layout_chosen_on_deep_levels():
         rows.update(combinations(big.tolist(), 6))
     prev = np.array(sorted(rows), np.int32)
     pidx, eoff, ext = apriori_gen(prev)
-    rc, info, passes, buf = level_plan_host(prev[pidx], eoff, ext, 40, 1 << 14, "slab", cls=1)
-    assert rc == 0 and info[0] == 0
+    rc, info, passes, buf = level_plan_host(prev[pidx], eoff, ext, 40, 1 << 14, cls=1)
+    assert rc == 0
     assert info[22] < 0.85 * info[21] and info[23] == (info[22] < 0.8 * info[21])
-    rc0, info0, _, _ = level_plan_host(prev[pidx], eoff, ext, 40, 1 << 14, "slab", cls=0)
+    rc0, info0, _, _ = level_plan_host(prev[pidx], eoff, ext, 40, 1 << 14, cls=0)
     assert rc0 == 0 and info0[23] == 0 and info0[22] == 0
