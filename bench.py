@@ -107,26 +107,71 @@ def cpu_baseline(config: str, min_sup: float, n_txn: int):
     return rec
 
 
-def _e2e_window(args, comm, n_txn, min_sup, cfgv, miner_cfg, sync):
-    """The reference's "Total time for get freqItemsets" window on a real D.dat."""
+def _pread_floor(path: str) -> float:
+    """ms to pread the whole file into the pinned ring by the same host threads as the
+    device reader (no H2D copy, no parse): the storage / page-cache floor of the window."""
+    from concurrent.futures import ThreadPoolExecutor
+    from fastapriori_amd.utils import io
+    from fastapriori_amd.utils.env import num_threads
+    n = os.path.getsize(path)
     import torch
-    from fastapriori_amd.models.apriori import FastApriori
+    ring = io._ring if io._ring else [torch.empty(io._RING_SLOT, dtype=torch.uint8,
+                                                  pin_memory=torch.cuda.is_available())
+                                      for _ in range(io._RING_SLOTS)]
+    fd = os.open(path, os.O_RDONLY)
+    t0 = time.perf_counter()
+    try:
+        def rd(c):
+            off, m = c * io._RING_SLOT, min(io._RING_SLOT, n - c * io._RING_SLOT)
+            mv = memoryview(ring[c % io._RING_SLOTS].numpy())
+            got = 0
+            while got < m:
+                got += os.preadv(fd, [mv[got:m]], off + got)
+        with ThreadPoolExecutor(min(num_threads(), io._RING_SLOTS)) as ex:
+            list(ex.map(rd, range((n + io._RING_SLOT - 1) // io._RING_SLOT)))
+    finally:
+        os.close(fd)
+    return (time.perf_counter() - t0) * 1e3
+
+
+def _drop_cache(path: str) -> bool:
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        os.fsync(fd)
+        os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+        return True
+    except OSError:
+        return False
+    finally:
+        os.close(fd)
+
+
+def _e2e_window(args, comm, n_txn, min_sup, cfgv, miner_cfg, sync):
+    """The reference's "Total time for get freqItemsets" window (Main.scala:28-32) on a
+    real D.dat, through the CLI's own code path: pipeline.mine_window with a temp path
+    (the three-argument `input output temp` form, per-level checkpoints on): read +
+    parse, mine, write freqItemset, checkpoint.  Cold (page cache dropped) and warm,
+    each next to the pread-only floor of the same file measured in the same run."""
+    import torch
+    from fastapriori_amd.config import JobConfig
+    from fastapriori_amd.pipeline import make_checkpointer, mine_window
     from fastapriori_amd.utils import io
     from fastapriori_amd.utils.metrics import Logger
     _, avg_len, avg_pat, n_pat, n_items, _ = cfgv
     base = args.workdir or os.environ.get("TMPDIR") or "/tmp"
     d = os.path.join(base, f"fa_bench_{args.config}_{n_txn}_{args.seed}")
     path = os.path.join(d, "D.dat")
-    out = os.path.join(d, f"out_{os.getpid() if comm.is_root else 0}", "freqItemset")
+    out = os.path.join(d, f"out_{os.getpid() if comm.is_root else 0}_")
+    tmp = os.path.join(d, f"tmp_{os.getpid() if comm.is_root else 0}")
     t_w = time.perf_counter()
     err = ""
     if comm.is_root:
         try:
             os.makedirs(d, exist_ok=True)
             if not os.path.exists(path):
-                tmp = path + ".tmp"
-                io.write_quest_file(tmp, n_txn, avg_len, avg_pat, n_pat, n_items, seed=args.seed)
-                os.replace(tmp, path)
+                tmpf = path + ".tmp"
+                io.write_quest_file(tmpf, n_txn, avg_len, avg_pat, n_pat, n_items, seed=args.seed)
+                os.replace(tmpf, path)
         except OSError as e:           # e.g. no room for the file: skip the window, keep the bench
             err = f"{type(e).__name__}: {e}"
             shutil.rmtree(d, ignore_errors=True)
@@ -134,43 +179,45 @@ def _e2e_window(args, comm, n_txn, min_sup, cfgv, miner_cfg, sync):
         return {"window": "skipped", "error": err or "the D.dat file could not be written"}, None
     write_s = time.perf_counter() - t_w
     quiet = Logger(comm.rank, enabled=False)
+    jc = JobConfig(input=d + "/", output=out, temp=tmp, min_support=min_sup, device=str(comm.device.type),
+                   dedup=miner_cfg.dedup, pair_strategy=miner_cfg.pair_strategy, overwrite=True)
 
     def one_run():
+        if comm.is_root:
+            shutil.rmtree(tmp, ignore_errors=True)
         sync()
         t0 = time.perf_counter()
-        shard = io.read_shard(path, comm)
-        res = FastApriori(min_sup, comm, miner_cfg, quiet).run(shard)
-        if comm.is_root:
-            io.write_freq_itemsets(res, out, overwrite=True)
-        del shard
+        summ: dict = {}
+        res = mine_window(jc, comm, quiet, make_checkpointer(jc, comm), summ)
         sync()
-        return comm.allreduce_float_max((time.perf_counter() - t0) * 1e3), res
+        return comm.allreduce_float_max((time.perf_counter() - t0) * 1e3), res, summ
 
     # cold: the file's pages dropped from the page cache (every rank's local view)
-    dropped = False
-    if comm.is_root:
-        fd = os.open(path, os.O_RDONLY)
-        try:
-            os.fsync(fd)
-            os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
-            dropped = True
-        except OSError:
-            dropped = False
-        finally:
-            os.close(fd)
+    dropped = _drop_cache(path) if comm.is_root else False
     comm.barrier()
-    cold_ms, res = one_run()
-    warm = [one_run()[0] for _ in range(max(args.e2e_runs, 1))]
+    cold_ms, res, summ = one_run()
+    dropped_floor = _drop_cache(path) if comm.is_root else False
+    floor_cold = _pread_floor(path) if comm.is_root else 0.0
+    warm, bundles = [], summ.get("device_bundles", 0)
+    for _ in range(max(args.e2e_runs, 1)):
+        ms, _, summ = one_run()
+        warm.append(ms)
+    floor_warm = _pread_floor(path) if comm.is_root else 0.0
     warm_ms = min(warm)
     if comm.is_root:
-        shutil.rmtree(os.path.dirname(out), ignore_errors=True)
+        shutil.rmtree(out + "freqItemset", ignore_errors=True)
+        shutil.rmtree(tmp, ignore_errors=True)
     if comm.device.type == "cuda":
         torch.cuda.empty_cache()
     return {
-        "window": "read+parse D.dat, mine, write freqItemset (Main.scala:28-32)",
+        "window": "read+parse D.dat, mine, write freqItemset + checkpoint (Main.scala:28-32), "
+                  "through pipeline.mine_window with a temp path (the CLI's `input output temp` form)",
         "D_bytes": os.path.getsize(path), "file_write_s": round(write_s, 1),
         "cold_ms": round(cold_ms, 1), "cold_cache_dropped": dropped,
+        "pread_floor_cold_ms": round(floor_cold, 1), "pread_floor_cold_dropped": dropped_floor,
         "warm_ms": round(warm_ms, 1), "warm_runs": [round(x, 1) for x in warm],
+        "pread_floor_warm_ms": round(floor_warm, 1),
+        "read_ms_last": summ.get("read_ms"), "device_bundles": bundles,
         "itemsets_per_s_cold": round(res.n_itemsets / (cold_ms / 1e3), 1),
         "itemsets_per_s_warm": round(res.n_itemsets / (warm_ms / 1e3), 1),
         "n_itemsets": res.n_itemsets,

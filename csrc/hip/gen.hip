@@ -705,11 +705,13 @@ static int ag_chain_dev(const int32_t* P1, int64_t n1, int m1, int nw, char* w0,
 //     5 multi (level 0 needs several accumulator passes: host path)  6 n_used
 //     7 end (|F_{k-1}| < k or C_0 = 0: mining is over)  8 + l: n_l  40 + l: C_l
 //     72 + l: G_l (parent rows with >= 1 candidate: the reference's group count)
-//     128 .. 191: used-item bitset of level 0 (4096 bits)
+//     512 .. 1023: used-item bitset of level 0 (kDlBitsW words: F1 <= 32768 bits)
 // ---------------------------------------------------------------------------
 namespace fa {
 
-constexpr int kDlCtl = 256;
+constexpr int kDlCtl = 1024;
+constexpr int kDlBits = 512;       // first word of the used-item bitset in ctl
+constexpr int kDlBitsW = 512;      // its 64-bit words (F1 <= kAgMaxF1 = 32768)
 
 __device__ int64_t agd_block_scan(const int32_t* __restrict__ cnt, int64_t* __restrict__ off, int64_t n,
                                   int64_t* groups = nullptr) {
@@ -771,27 +773,31 @@ __global__ __launch_bounds__(1024) void k_dl_decide0(const int32_t* __restrict__
   c[1] = 1; c[2] = C; c[3] = C; c[9] = C;
 }
 
-// used items of level 0's candidate rows (LDS-privatised, one global atomicOr per word)
+// used items of level 0's candidate rows (LDS-privatised, one global atomicOr per word);
+// w32: the bitset's u32 words in use ((F1 + 31) / 32)
 __global__ __launch_bounds__(256) void k_dl_mark(const int32_t* __restrict__ rows, int m1,
-                                                 long long* __restrict__ c) {
-  __shared__ uint32_t lb[128];
+                                                 long long* __restrict__ c, int w32) {
+  __shared__ uint32_t lb[2 * kDlBitsW];
   if (c[0] && !c[5]) return;         // (a multi level still reports its used items)
-  if (threadIdx.x < 128) lb[threadIdx.x] = 0u;
+  for (int q = threadIdx.x; q < w32; q += 256) lb[q] = 0u;
   __syncthreads();
   const int64_t n = c[5] ? 0 : c[40] * (int64_t)m1;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
     atomicOr(&lb[rows[i] >> 5], 1u << (rows[i] & 31));
   __syncthreads();
-  uint32_t* mk = reinterpret_cast<uint32_t*>(c + 128);
-  if (threadIdx.x < 128 && lb[threadIdx.x]) atomicOr(&mk[threadIdx.x], lb[threadIdx.x]);
+  uint32_t* mk = reinterpret_cast<uint32_t*>(c + kDlBits);
+  for (int q = threadIdx.x; q < w32; q += 256)
+    if (lb[q]) atomicOr(&mk[q], lb[q]);
 }
 
 // n_used, and whether level 0 alone exceeds one accumulator pass
-__global__ void k_dl_post0(long long* __restrict__ c, double lds) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const uint32_t* mk = reinterpret_cast<const uint32_t*>(c + 128);
-  int64_t n_used = 0;
-  for (int q = 0; q < 128; ++q) n_used += __popc(mk[q]);
+__global__ __launch_bounds__(64) void k_dl_post0(long long* __restrict__ c, double lds, int w32) {
+  if (blockIdx.x != 0) return;
+  const uint32_t* mk = reinterpret_cast<const uint32_t*>(c + kDlBits);
+  uint32_t part = 0;
+  for (int q = threadIdx.x; q < w32; q += 64) part += __popc(mk[q]);
+  const int64_t n_used = (int64_t)wave_sum_u32(part);
+  if (threadIdx.x != 0) return;
   c[6] = n_used;
   if (c[1] == 1 && c[40] > d_slab_cap(n_used, c[40], lds)) { c[5] = 1; c[0] = 1; }
 }
@@ -828,7 +834,7 @@ __global__ __launch_bounds__(1024) void k_dl_decide(const int32_t* __restrict__ 
 // entries) while it runs.  kEmit = false: cnt[i] = extensions of row i (+ the clear);
 // true: ext ids at cnt + n + off[i], candidate rows at rows + off[i] * (m + 1), and
 // level l+1's Ext / table (next_ext, ntab; nullptr when no level follows).
-template <bool kEmit>
+template <bool kEmit, int NWL = 1>
 __global__ __launch_bounds__(256) void k_dl_rows(const int32_t* __restrict__ P, int m,
                                                  const int32_t* __restrict__ table, uint32_t mask, int nw,
                                                  const unsigned long long* __restrict__ ext, int32_t* __restrict__ cnt,
@@ -844,17 +850,19 @@ __global__ __launch_bounds__(256) void k_dl_rows(const int32_t* __restrict__ P, 
   const int lane = threadIdx.x & 63;
   const int64_t nwave = (int64_t)gridDim.x * (blockDim.x / 64);
   for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); i < n; i += nwave) {
-    unsigned long long a[1];
-    const int cc = ag_row_bits<1>(P, i, m, table, mask, nw, ext, lane, a);
+    unsigned long long a[NWL];
+    const int cc = ag_row_bits<NWL>(P, i, m, table, mask, nw, ext, lane, a);
     const int incl = wave_scan_incl_dpp(cc);
     if (!kEmit) {
       if (lane == 63) cnt[i] = incl;
       continue;
     }
     const int64_t o = off[i];
-    ag_emit<1>(a, lane, P + i * m, m, o + (incl - cc), cnt + n, rows);
+    ag_emit<NWL>(a, lane, P + i * m, m, o + (incl - cc), cnt + n, rows);
     if (next_ext && wave_last(incl) > 0) {
-      if (lane < nw) next_ext[o * nw + lane] = a[0];
+#pragma unroll
+      for (int j = 0; j < NWL; ++j)
+        if (lane * NWL + j < nw) next_ext[o * nw + lane * NWL + j] = a[j];
       if (lane == 0) {
         // = ag_hash_drop(candidate row (x, y), m + 1, m): x's items, seed m
         const int32_t* x = P + i * m;
@@ -881,7 +889,7 @@ __global__ __launch_bounds__(256) void k_dl_rows(const int32_t* __restrict__ P, 
 FA_API int fa_hip_dl_level0(const int32_t* P0, const long long* n_src, int64_t n_const, int64_t n_bound, int m0,
                             int F1, void* ws, int64_t ws_bytes, long long* ctl, long long* ctl_host,
                             int64_t c_bound, double lds, int64_t* info, int sync, hipStream_t st) {
-  if (m0 < 2 || F1 > 4096 || F1 < 1 || n_bound < 0 || c_bound < 1) return 1;
+  if (m0 < 2 || F1 > kAgMaxF1 || F1 < 1 || n_bound < 0 || c_bound < 1) return 1;
   auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
   const int nw = (F1 + 63) / 64;
   const int64_t nb = std::max<int64_t>(n_bound, 1);
@@ -910,14 +918,21 @@ FA_API int fa_hip_dl_level0(const int32_t* P0, const long long* n_src, int64_t n
   hipLaunchKernelGGL(k_agd_insert, g, dim3(256), 0, st, P0, m0, table, cap - 1, ctl, 0);
   hipLaunchKernelGGL(k_agd_ext, g, dim3(256), 0, st, P0, m0, table, cap - 1, nw, ext, ctl, 0);
   const unsigned nwg = (unsigned)std::min<int64_t>((nb + 3) / 4, 2048);
-  hipLaunchKernelGGL(k_agd_rows<false>, dim3(nwg), dim3(256), 0, st, P0, m0, table, cap - 1, nw, ext, cnt, off, rows,
-                     ctl, 0);
+#define FA_DL0_ROWS(E, N)                                                                                   \
+  hipLaunchKernelGGL((k_agd_rows<E, N>), dim3(nwg), dim3(256), 0, st, P0, m0, table, cap - 1, nw, ext, cnt, off, \
+                     rows, ctl, 0);
+#define FA_DL0_CNT(N) FA_DL0_ROWS(false, N)
+#define FA_DL0_EMIT(N) FA_DL0_ROWS(true, N)
+  FA_AG_NWL_SWITCH(nw, FA_DL0_CNT)
   hipLaunchKernelGGL(k_dl_decide0, dim3(1), dim3(1024), 0, st, cnt, off, ctl, c_bound);
-  hipLaunchKernelGGL(k_agd_rows<true>, dim3(nwg), dim3(256), 0, st, P0, m0, table, cap - 1, nw, ext, cnt, off, rows,
-                     ctl, 0);
+  FA_AG_NWL_SWITCH(nw, FA_DL0_EMIT)
+#undef FA_DL0_EMIT
+#undef FA_DL0_CNT
+#undef FA_DL0_ROWS
+  const int w32 = (F1 + 31) / 32;
   hipLaunchKernelGGL(k_dl_mark, dim3((unsigned)std::min<int64_t>((c_bound * (m0 + 1) + 255) / 256, 1024)), dim3(256),
-                     0, st, rows, m0 + 1, ctl);
-  hipLaunchKernelGGL(k_dl_post0, dim3(1), dim3(64), 0, st, ctl, lds);
+                     0, st, rows, m0 + 1, ctl, w32);
+  hipLaunchKernelGGL(k_dl_post0, dim3(1), dim3(64), 0, st, ctl, lds, w32);
   if (sync) {
     (void)hipMemcpyAsync(ctl_host, ctl, sizeof(long long) * kDlCtl, hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return 7;
@@ -961,11 +976,14 @@ struct DlPost {
   int64_t T, nnz, trim_min_rows, trim_ok, k;
   // out
   int64_t done, sw, cap, n_wg, C, trim;
+  // prefix slab rows of levels with prefixes past 12 ids (levels.hip gpre), int32 [gpre_cap]
+  int32_t* gpre; int64_t gpre_cap;
 };
-static_assert(sizeof(DlPost) == 28 * 8, "DlPost layout (ops.primitives.DlPostC)");
+static_assert(sizeof(DlPost) == 30 * 8, "DlPost layout (ops.primitives.DlPostC)");
 
 FA_API int fa_hip_dl_plan(const int64_t* desc, int L, long long* ctl, int F1, int32_t* item_map, void* rec,
-                          int64_t max_pieces, int32_t* part, int64_t part_cap, hipStream_t st);
+                          int64_t max_pieces, int32_t* part, int64_t part_cap, int32_t* gpre, int64_t gpre_cap,
+                          hipStream_t st);
 FA_API int fa_hip_count_slab_rec(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
                                  const int32_t* item_map, int F1, int n_used, const int32_t* gpre, const void* rec,
                                  int G, int C, const int32_t* wword, uint32_t* out, int sw, int n_wg,
@@ -1004,7 +1022,9 @@ static void dl_post(DlPost* P, const int64_t* desc, int L, long long* ctl, const
     if (cap >= std::min<int64_t>(C, 8192) || (w == 4 && cap >= 1024)) { sw = w; break; }
   }
   if (sw == 0 || C > cap) return;
-  if (fa_hip_dl_plan(desc, L, ctl, F1, P->item_map, P->rec, C, P->part, P->part_cap, st) != 0) return;
+  if (fa_hip_dl_plan(desc, L, ctl, F1, P->item_map, P->rec, C, P->part, P->part_cap, P->gpre, P->gpre_cap,
+                     st) != 0)
+    return;                                        // (e.g. long prefixes past gpre_cap: the caller plans)
   (void)hipMemsetAsync(P->out, 0, 4 * (size_t)C, st);
   P->sw = sw;
   P->cap = cap;
@@ -1016,7 +1036,7 @@ static void dl_post(DlPost* P, const int64_t* desc, int L, long long* ctl, const
   } else if (!P->len_hist || P->T < P->trim_min_rows) {
     if (!P->len_hist && P->T >= P->trim_min_rows) return;   // the caller decides (and counts)
   } else {
-    const uint64_t* mk = reinterpret_cast<const uint64_t*>(ch + 128);
+    const uint64_t* mk = reinterpret_cast<const uint64_t*>(ch + kDlBits);
     double num = 0.0, den = 0.0;
     for (int r = 0; r < F1; ++r) {
       if (P->alive[r]) den += (double)P->c1[r];
@@ -1041,7 +1061,7 @@ static void dl_post(DlPost* P, const int64_t* desc, int L, long long* ctl, const
   const int64_t lds_k = n_used * (sw + 2) * 8 + ((C + 3) & ~(int64_t)3) * 4 + map_b;
   const int64_t per_cu = std::min<int64_t>(std::max<int64_t>(1, (int64_t)P->lds_kernel / std::max<int64_t>(lds_k, 1)), 2);
   P->n_wg = std::max<int64_t>(1, std::min<int64_t>(nslabs, 256 * per_cu));
-  if (fa_hip_count_slab_rec(P->roff, P->ranks, P->src, P->ncols, P->item_map, F1, (int)n_used, nullptr, P->rec, 0,
+  if (fa_hip_count_slab_rec(P->roff, P->ranks, P->src, P->ncols, P->item_map, F1, (int)n_used, P->gpre, P->rec, 0,
                             (int)C, P->wword, P->out, sw, (int)P->n_wg, nullptr, 0, st, nullptr,
                             reinterpret_cast<const int32_t*>(ctl + 221)) != 0)
     return;
@@ -1116,11 +1136,17 @@ FA_API int fa_hip_dl_more(int F1, void* ws, int64_t ws_bytes, int64_t ws_used, l
       Tab nxt;
       if (l + 1 < LM && !tab_alloc(cb, nxt)) return 5;
       const unsigned nwg = (unsigned)std::min<int64_t>((nb + 3) / 4, 2048);
-      hipLaunchKernelGGL(k_dl_rows<false>, dim3(nwg), dim3(256), 0, st, P, m, cur.table, cur.cap - 1, nw, cur.ext,
-                         lv[l].cnt, lv[l].off, lv[l].rows, ctl, l, nxt.table, nxt.cap, nxt.ext);
+#define FA_DLR(E, N)                                                                                          \
+      hipLaunchKernelGGL((k_dl_rows<E, N>), dim3(nwg), dim3(256), 0, st, P, m, cur.table, cur.cap - 1, nw,      \
+                         cur.ext, lv[l].cnt, lv[l].off, lv[l].rows, ctl, l, nxt.table, nxt.cap, nxt.ext);
+#define FA_DLR_CNT(N) FA_DLR(false, N)
+#define FA_DLR_EMIT(N) FA_DLR(true, N)
+      FA_AG_NWL_SWITCH(nw, FA_DLR_CNT)
       hipLaunchKernelGGL(k_dl_decide, dim3(1), dim3(1024), 0, st, lv[l].cnt, lv[l].off, ctl, l, growth, cb, lds);
-      hipLaunchKernelGGL(k_dl_rows<true>, dim3(nwg), dim3(256), 0, st, P, m, cur.table, cur.cap - 1, nw, cur.ext,
-                         lv[l].cnt, lv[l].off, lv[l].rows, ctl, l, nxt.table, nxt.cap, nxt.ext);
+      FA_AG_NWL_SWITCH(nw, FA_DLR_EMIT)
+#undef FA_DLR_EMIT
+#undef FA_DLR_CNT
+#undef FA_DLR
       P = lv[l].rows;
       cur = nxt;
       nb = cb;

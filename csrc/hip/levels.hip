@@ -17,15 +17,18 @@
 //   b = {extension slab rows 0-7 (u16)},  c = {prefix slab rows 4-11 (u16)}
 // A parent row with c extensions gives c / 8 pieces of 8 and one of c % 8;
 // pieces are bucketed by n_ext, 8 first (the lanes of a wave then loop equally
-// long, as plan.cpp's counting sort).  Prefixes are at most 12 items (the chain
-// stops bundles before that).
+// long, as plan.cpp's counting sort).  Prefixes of up to 12 items ride in the
+// record; longer ones (up to kDlMaxM) are written to gpre, the record pointing there.
 #include "fa_hip.h"
 
 namespace fa {
 
 constexpr int kDlMaxL = 32;
-constexpr int kDlCtlN = 256;   // gen.hip kDlCtl
-// ctl words used here: 128 .. 191 used-item bitset (gen.hip), 220 pieces, 221 pieces
+constexpr int kDlInline = 12;  // prefix ids inline in a piece record
+constexpr int kDlMaxM = 40;    // longest prefix a device bundle takes (ops.primitives.DL_MAX_M)
+constexpr int kDlCtlN = 1024;  // gen.hip kDlCtl
+constexpr int kDlBitsN = 512;  // gen.hip kDlBits: first word of the used-item bitset
+// ctl words used here: 512 .. 1023 used-item bitset (gen.hip), 220 pieces, 221 pieces
 // as int32 (the count kernel's G)
 
 struct DlLevels {
@@ -38,6 +41,9 @@ struct DlLevels {
   int64_t base[kDlMaxL];          // candidate index of the level's first candidate
   int64_t rbase[kDlMaxL + 1];     // flattened parent-row index of the level's first row
   int m[kDlMaxL];                 // parent row length (prefix length)
+  int64_t gbase[kDlMaxL];         // m > kDlInline: offset of the level's prefix slab rows in gpre
+  int32_t* gpre;                  // [sum over long-prefix levels of n_l * m_l] (may be null)
+  int64_t w0, w1;                 // candidate window of this plan (a multi-pass level's pass)
   int L;
 };
 
@@ -47,14 +53,25 @@ __device__ __forceinline__ int dl_level_of(const DlLevels& D, int64_t t) {
   return l;
 }
 
-// rank -> slab row from the used-item bitset (one wave)
+// rank -> slab row from the used-item bitset (one wave; lane l owns words 8l .. 8l+7)
 __global__ __launch_bounds__(64) void k_dl_map(const long long* __restrict__ c, int F1, int32_t* __restrict__ item_map) {
-  __shared__ int pre[64];
-  const uint64_t* mk = reinterpret_cast<const uint64_t*>(c + 128);
+  __shared__ int pre[512];
+  const uint64_t* mk = reinterpret_cast<const uint64_t*>(c + kDlBitsN);
   const int lane = threadIdx.x;
-  const uint64_t w = mk[lane];
-  const int pc = __popcll(w);
-  pre[lane] = wave_scan_incl_dpp(pc) - pc;
+  const int nwd = (F1 + 63) >> 6;
+  int cnt8[8], tot = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int w = lane * 8 + j;
+    cnt8[j] = w < nwd ? __popcll(mk[w]) : 0;
+    tot += cnt8[j];
+  }
+  int run = wave_scan_incl_dpp(tot) - tot;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    pre[lane * 8 + j] = run;
+    run += cnt8[j];
+  }
   __syncthreads();
   for (int r = lane; r < F1; r += 64) {
     const uint64_t ww = mk[r >> 6];
@@ -72,10 +89,22 @@ constexpr int kDlPB = 256;        // parent rows per planner block
 
 __device__ __forceinline__ int dl_bucket_count(int cc, int b) { return b == 8 ? (cc >> 3) : ((cc & 7) == b ? 1 : 0); }
 
-__device__ __forceinline__ int dl_row_count(const DlLevels& D, int64_t t, int64_t R) {
+// the candidates of flattened parent row t inside the plan's window [w0, w1): their
+// count, and (first) the bundle index of the first of them
+__device__ __forceinline__ int dl_row_window(const DlLevels& D, int64_t t, int64_t R, int64_t* first) {
   if (t >= R) return 0;
   const int l = dl_level_of(D, t);
-  return D.cnt[l][t - D.rbase[l]];
+  const int64_t i = t - D.rbase[l];
+  const int cc = D.cnt[l][i];
+  if (cc == 0) return 0;
+  const int64_t cb = D.base[l] + D.off[l][i], ce = cb + cc;
+  const int64_t a = cb > D.w0 ? cb : D.w0, b = ce < D.w1 ? ce : D.w1;
+  if (first) *first = a;
+  return b > a ? (int)(b - a) : 0;
+}
+
+__device__ __forceinline__ int dl_row_count(const DlLevels& D, int64_t t, int64_t R) {
+  return dl_row_window(D, t, R, nullptr);
 }
 
 // part[blk * 8 + (b - 1)]: pieces of bucket b in block blk
@@ -132,19 +161,21 @@ __device__ __forceinline__ uint32_t dl_pk(int x, int y) { return (uint32_t)(x & 
 
 __device__ __forceinline__ void dl_write_rec(int4* __restrict__ rec, int64_t p, int64_t cand, int n_ext, int m,
                                              const int (&ids)[12], const int32_t* __restrict__ ex,
-                                             const int32_t* __restrict__ item_map) {
+                                             const int32_t* __restrict__ item_map, int64_t goff) {
   int e8[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) e8[k] = k < n_ext ? item_map[ex[k]] : 0;
   int4 a, b, cc;
   a.x = (int)cand;
-  a.y = n_ext | (m << 8);
+  // prefixes past kDlInline ids: the long-prefix flag, and c.x points at the row in gpre
+  a.y = n_ext | (m << 8) | (goff >= 0 ? 1 << 16 : 0);
   a.z = (int)dl_pk(ids[0], ids[1]);
   a.w = (int)dl_pk(ids[2], ids[3]);
   b.x = (int)dl_pk(e8[0], e8[1]); b.y = (int)dl_pk(e8[2], e8[3]);
   b.z = (int)dl_pk(e8[4], e8[5]); b.w = (int)dl_pk(e8[6], e8[7]);
   cc.x = (int)dl_pk(ids[4], ids[5]); cc.y = (int)dl_pk(ids[6], ids[7]);
   cc.z = (int)dl_pk(ids[8], ids[9]); cc.w = (int)dl_pk(ids[10], ids[11]);
+  if (goff >= 0) cc.x = (int)goff;
   rec[3 * p] = a; rec[3 * p + 1] = b; rec[3 * p + 2] = cc;
 }
 
@@ -154,7 +185,8 @@ __global__ __launch_bounds__(kDlPB) void k_dl_pieces_emit(const DlLevels D, cons
   __shared__ int sh[kDlPB / 64][8];
   const int64_t R = D.rbase[D.L];
   const int64_t t = (int64_t)blockIdx.x * kDlPB + threadIdx.x;
-  const int cc = dl_row_count(D, t, R);
+  int64_t first = 0;
+  const int cc = dl_row_window(D, t, R, &first);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   int excl[9];
 #pragma unroll
@@ -180,13 +212,21 @@ __global__ __launch_bounds__(kDlPB) void k_dl_pieces_emit(const DlLevels D, cons
   int ids[12];
 #pragma unroll
   for (int q = 0; q < 12; ++q) ids[q] = q < m ? item_map[x[q]] : 0;
-  const int64_t o = D.off[l][i];
+  int64_t goff = -1;
+  if (m > kDlInline) {
+    goff = D.gbase[l] + i * m;
+    for (int q = 0; q < m; ++q) D.gpre[goff + q] = item_map[x[q]];
+  }
+  // the window's candidates of this row: ids from the generator's list, indices
+  // relative to the window (the count kernel's accumulators)
+  const int64_t o = D.off[l][i] + (first - (D.base[l] + D.off[l][i]));
   const int32_t* ex = D.cnt[l] + D.n[l] + o;
-  const int64_t cand = D.base[l] + o;
+  const int64_t cand = first - D.w0;
   const int full = cc >> 3;
-  for (int j = 0; j < full; ++j) dl_write_rec(rec, slot[8] + j, cand + 8 * j, 8, m, ids, ex + 8 * j, item_map);
+  for (int j = 0; j < full; ++j)
+    dl_write_rec(rec, slot[8] + j, cand + 8 * j, 8, m, ids, ex + 8 * j, item_map, goff);
   const int rem = cc & 7;
-  if (rem) dl_write_rec(rec, slot[rem], cand + 8 * full, rem, m, ids, ex + 8 * full, item_map);
+  if (rem) dl_write_rec(rec, slot[rem], cand + 8 * full, rem, m, ids, ex + 8 * full, item_map, goff);
 }
 
 // keep support >= mc (FastApriori.scala:152-154): per level, the kept candidate rows
@@ -237,11 +277,17 @@ __global__ __launch_bounds__(1024) void k_dl_threshold(const DlLevels D, const D
   }
 }
 
-static int dl_levels(const int64_t* desc, int L, DlLevels* D) {
+// levels of a bundle from gen.hip's level table; gpre / gpre_cap: room for the prefix
+// slab rows of levels whose prefixes exceed kDlInline ids (returns 1 when too small)
+static int dl_levels(const int64_t* desc, int L, DlLevels* D, int32_t* gpre = nullptr, int64_t gpre_cap = 0) {
   if (L < 1 || L > kDlMaxL) return 1;
   *D = DlLevels{};
   D->L = L;
+  D->w0 = 0;
+  D->w1 = INT64_MAX;
   D->rbase[0] = 0;
+  D->gpre = gpre;
+  int64_t g = 0;
   for (int l = 0; l < L; ++l) {
     const int64_t* d = desc + 8 * l;
     D->P[l] = reinterpret_cast<const int32_t*>((intptr_t)d[0]);
@@ -253,8 +299,14 @@ static int dl_levels(const int64_t* desc, int L, DlLevels* D) {
     D->C[l] = d[6];
     D->base[l] = d[7];
     D->rbase[l + 1] = D->rbase[l] + d[5];
-    if (D->m[l] < 1 || D->m[l] > 12) return 1;
+    if (D->m[l] < 1 || D->m[l] > kDlMaxM) return 1;
+    D->gbase[l] = -1;
+    if (D->m[l] > kDlInline) {
+      D->gbase[l] = g;
+      g += d[5] * D->m[l];
+    }
   }
+  if (g > 0 && gpre_cap >= 0 && (gpre == nullptr || g > gpre_cap)) return 1;   // (cap < 0: not planning)
   return 0;
 }
 
@@ -262,19 +314,36 @@ static int dl_levels(const int64_t* desc, int L, DlLevels* D) {
 
 using namespace fa;
 
+FA_API int fa_hip_dl_plan_window(const int64_t* desc, int L, long long* ctl, int F1, int32_t* item_map, void* rec,
+                                 int64_t max_pieces, int32_t* part, int64_t part_cap, int32_t* gpre,
+                                 int64_t gpre_cap, int64_t w0, int64_t w1, hipStream_t st);
+
 // Single-pass slab plan of a device bundle (desc: gen.hip fa_hip_dl_more's level
 // table, L levels).  item_map: int32 [F1] out (rank -> slab row, -1 unused);
 // rec: int4 [3 * max_pieces] out, max_pieces >= total candidates; part: int32
-// scratch of 8 per 256 parent rows (part_cap).  The piece count
-// lands in ctl[220] (int32 copy at ctl + 221, the count kernel's G).
+// scratch of 8 per 256 parent rows (part_cap); gpre: int32 [gpre_cap] out, the prefix
+// slab rows of levels with prefixes past kDlInline ids (fa_hip_dl_gpre_need).  The
+// piece count lands in ctl[220] (int32 copy at ctl + 221, the count kernel's G).
 FA_API int fa_hip_dl_plan(const int64_t* desc, int L, long long* ctl, int F1, int32_t* item_map, void* rec,
-                          int64_t max_pieces, int32_t* part, int64_t part_cap, hipStream_t st) {
+                          int64_t max_pieces, int32_t* part, int64_t part_cap, int32_t* gpre, int64_t gpre_cap,
+                          hipStream_t st) {
+  return fa_hip_dl_plan_window(desc, L, ctl, F1, item_map, rec, max_pieces, part, part_cap, gpre, gpre_cap, 0, -1, st);
+}
+
+// The plan of the bundle candidates [w0, w1) only (w1 < 0: all): one pass of a level
+// whose candidates exceed one accumulator pass; records index candidates from w0.
+FA_API int fa_hip_dl_plan_window(const int64_t* desc, int L, long long* ctl, int F1, int32_t* item_map, void* rec,
+                                 int64_t max_pieces, int32_t* part, int64_t part_cap, int32_t* gpre,
+                                 int64_t gpre_cap, int64_t w0, int64_t w1, hipStream_t st) {
   DlLevels D;
-  if (dl_levels(desc, L, &D)) return 1;
-  if (F1 < 1 || F1 > 4096) return 1;
+  if (dl_levels(desc, L, &D, gpre, gpre_cap)) return 1;
+  if (F1 < 1 || F1 > 32768) return 1;
   int64_t C = 0;
   for (int l = 0; l < L; ++l) C += D.C[l];
-  if (max_pieces < C) return 1;
+  D.w0 = w0 < 0 ? 0 : w0;
+  D.w1 = w1 < 0 ? C : std::min(w1, C);
+  if (D.w1 <= D.w0) return 1;
+  if (max_pieces < D.w1 - D.w0) return 1;
   const int64_t R = D.rbase[L];
   const int64_t nblk = std::max<int64_t>(1, (R + kDlPB - 1) / kDlPB);
   if (part_cap < 8 * nblk) return 1;
@@ -293,9 +362,17 @@ FA_API int fa_hip_dl_threshold(const int64_t* desc, int L, const uint32_t* count
                                const int64_t* rows_off, int32_t* cnt_out, const int64_t* cnt_off, long long* fsz,
                                hipStream_t st) {
   DlLevels D;
-  if (dl_levels(desc, L, &D)) return 1;
+  if (dl_levels(desc, L, &D, nullptr, -1)) return 1;
   DlOut O{};
   for (int l = 0; l < L; ++l) { O.rows_off[l] = rows_off[l]; O.cnt_off[l] = cnt_off[l]; }
   hipLaunchKernelGGL(k_dl_threshold, dim3(1), dim3(1024), 0, st, D, O, counts, mc, rows_out, cnt_out, fsz);
   FA_LAUNCH_RET();
+}
+
+// int32 entries of gpre a bundle needs (levels with prefixes past kDlInline ids)
+FA_API int64_t fa_hip_dl_gpre_need(const int64_t* desc, int L) {
+  int64_t g = 0;
+  for (int l = 0; l < L; ++l)
+    if (desc[8 * l + 4] > kDlInline) g += desc[8 * l + 5] * desc[8 * l + 4];
+  return g;
 }

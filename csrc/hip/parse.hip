@@ -394,7 +394,7 @@ __global__ __launch_bounds__(1024) void k_scan_small(const int32_t* __restrict__
 // the lanes (coalesced stores).  hpart (may be null): kHistCap counters per block,
 // added to (one row per workgroup: no atomics).
 __global__ __launch_bounds__(256) void k_tcompact(const int64_t* __restrict__ tile_base,
-                                                  const int64_t* __restrict__ tile_xb, int64_t ntiles,
+                                                  const int64_t* __restrict__ tile_xb, int64_t ntiles, int tail,
                                                   const int32_t* __restrict__ dcnt, const int32_t* __restrict__ xcnt,
                                                   const int64_t* __restrict__ lbase,
                                                   const int32_t* __restrict__ scratch,
@@ -410,7 +410,8 @@ __global__ __launch_bounds__(256) void k_tcompact(const int64_t* __restrict__ ti
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   bool over = false, xover = false;
   for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const int64_t j0 = tile_base[t], j1 = tile_base[t + 1];
+    // (the region's unterminated last line, when tail, belongs to its last tile)
+    const int64_t j0 = tile_base[t], j1 = tile_base[t + 1] + (t == ntiles - 1 ? tail : 0);
     int64_t ib = tile_xb[2 * t], xb = tile_xb[2 * t + 1];
     for (int64_t c0 = j0; c0 < j1; c0 += 256) {
       const int64_t j = c0 + threadIdx.x;
@@ -742,13 +743,14 @@ FA_API int fa_hip_scan_small(int k, const int32_t* in, int64_t n, int64_t* out, 
   FA_LAUNCH_RET();
 }
 
-FA_API int fa_hip_tcompact(const int64_t* tile_base, const int64_t* tile_xb, int64_t ntiles, const int32_t* dcnt,
+FA_API int fa_hip_tcompact(const int64_t* tile_base, const int64_t* tile_xb, int64_t ntiles, int tail,
+                           const int32_t* dcnt,
                            const int32_t* xcnt, const int64_t* lbase, const int32_t* scratch, const int32_t* xscratch,
                            int32_t* items, int32_t* extras, int64_t xcap, int64_t* off, int grid,
                            unsigned long long* hpart, int32_t* flags, hipStream_t st) {
   if (ntiles <= 0) return 0;
   if (grid < 1) return 3;
-  hipLaunchKernelGGL(k_tcompact, dim3((unsigned)grid), dim3(256), 0, st, tile_base, tile_xb, ntiles, dcnt, xcnt,
+  hipLaunchKernelGGL(k_tcompact, dim3((unsigned)grid), dim3(256), 0, st, tile_base, tile_xb, ntiles, tail, dcnt, xcnt,
                      lbase, scratch, xscratch, items, extras, xcap, off, hpart, flags);
   FA_LAUNCH_RET();
 }

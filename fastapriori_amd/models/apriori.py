@@ -91,6 +91,9 @@ DEVICE_LEVELS = os.environ.get("FA_DEVICE_LEVELS", "1") == "1"
 # the bundle's plan, trimming decision and slab count queued by the generator's native
 # call right after its synchronisation (gen.hip DlPost), not after a return to Python
 DL_POST = os.environ.get("FA_DL_POST", "1") == "1"
+# a level whose candidates exceed one accumulator pass stays on the device (counted window
+# by window from the used items' bitmap) instead of handing the rest to the host loop
+DL_MULTI = os.environ.get("FA_DL_MULTI", "1") == "1"
 BUNDLE_MAX_PREFIX = int(os.environ.get("FA_BUNDLE_MAX_PREFIX", "9"))
 
 
@@ -283,6 +286,7 @@ class FastApriori:
                            _share=share)
                 self._level_recs.append((rec, f"level{k}"))
                 self._ckpt_level(result, kk)
+            self.stats["host_levels"] = self.stats.get("host_levels", 0) + len(bundle)
             k += len(bundle)
         # drop a trailing empty level (the reference never emits empty levels)
         while len(levels) > 1 and len(levels[-1]) == 0:
@@ -391,18 +395,27 @@ class FastApriori:
                 if c[7]:
                     self._dl_staged = staged
                     break                               # |F_{k-1}| < k or no candidates: done
+                multi = None
                 if c[5]:
-                    nxt = k                             # several accumulator passes: host path
-                    break
+                    # level k alone needs several accumulator passes: counted on the device
+                    # window by window (else the host loop takes over from level k)
+                    multi = self._dl_multipass(S, db, k, F1, c, P0, n_src, n_const, n_bound, m0, lds, st)
+                    if multi is None:
+                        nxt = k
+                        break
+                    c = multi[0]
                 L, n_used = int(c[1]), int(c[6])
                 Cs = S.desc[:L, 6].copy()
                 C = int(Cs.sum())
                 done = int(S.post.done) if post else 0
-                if done == 2:
+                if multi is not None:
+                    cnt = multi[1]
+                elif done == 2:
                     # planned and counted by fa_hip_dl_more's post step (no trim due)
                     cnt = S.post_bufs["out"][:C]
                 else:
-                    bits = np.unpackbits(c[128:192].view(np.uint8), bitorder="little")[:F1]
+                    nwd = (F1 + 63) // 64
+                    bits = np.unpackbits(c[Pm.DL_BITS:Pm.DL_BITS + nwd].view(np.uint8), bitorder="little")[:F1]
                     used = np.flatnonzero(bits)
                     if done == 1:
                         plan = Pm.dl_plan_from_post(S, n_used)
@@ -429,17 +442,60 @@ class FastApriori:
             k += L
         self._dl_flush(S, pend, levels, counts, result)
         self.stats["device_bundles"] = len(pend)
+        self.stats["device_levels"] = int(sum(p["L"] for p in pend))
         return nxt
+
+    def _dl_multipass(self, S, db, k: int, F1: int, c, P0, n_src, n_const: int, n_bound: int, m0: int, lds: int,
+                      st):
+        """Level k of a device bundle whose candidates exceed one accumulator pass
+        (FastApriori.scala:132-160 at any size): its candidates generated again with
+        room for all of them when the bounded generation stopped short, the level's
+        rows trimmed as the host loop would, then counted window by window from the used
+        items' bitmap (ops.primitives.dl_count_multipass).  Returns (control block,
+        int32 counts [C] on the device) or None (no slab width fits: host loop)."""
+        Pm = ops.primitives
+        if not DL_MULTI or self.cfg.max_level and k > self.cfg.max_level:
+            return None
+        C0 = int(c[40])
+        if int(c[1]) == 0:
+            # the bounded generation reported the size only: again, one level, room for C0
+            c = Pm.dl_bundle_gen(S, P0, n_src, n_const, n_bound, m0, F1, C0, lds, BUNDLE_GROWTH, 1, st)
+            if c[4] or c[7] or int(c[1]) != 1 or int(c[40]) != C0:
+                raise RuntimeError(f"device level {k}: regeneration of {C0} candidates disagrees ({c[:8]})")
+        nwd = (F1 + 63) // 64
+        bits = np.unpackbits(c[Pm.DL_BITS:Pm.DL_BITS + nwd].view(np.uint8), bitorder="little")[:F1]
+        used = np.flatnonzero(bits)
+        n_used = int(used.size)
+        if Pm.dl_slab_width(n_used, min(C0, 8192), lds)[0] == 0:
+            return None
+        with self._timer.phase(f"trim{k}"), roctx_range("trim"):
+            self._trim(db, used, k, C0)
+        with self._timer.phase("count"), roctx_range("count_multi"):
+            bm, bmap = self._bitmaps(db, used)
+            used_t = torch.from_numpy(used.astype(np.int64)).to(self._dev)
+            bm_rows = (bmap[used_t] if bmap is not None else used_t).to(torch.int32).contiguous()
+            cnt = Pm.dl_count_multipass(S, F1, n_used, C0, lds, db["roff"], db["ranks"], db["src"], db["ncols"],
+                                        db["wword"], bm, bm_rows,
+                                        self.stats["min_count"] / max(1, self.stats["n_lines"]), self._dev)
+        if cnt is None:
+            return None
+        self.stats["device_multipass"] = self.stats.get("device_multipass", 0) + 1
+        return c, cnt
 
     def _dl_post_setup(self, S, db, k: int, F1: int, c_bound: int, n_bound: int, lds: int) -> None:
         """Fill the post step of fa_hip_dl_more (ops.primitives.DlPostC): buffers, the
         current rows and the trimming inputs of level k (FastApriori._trim_worth_it)."""
         Pm = ops.primitives
-        b = S.post_buffers(F1, c_bound, n_bound + c_bound)
+        m0 = k - 1
+        # prefixes past 12 ids ride in gpre (levels.hip); a bundle needing more than this
+        # room is planned by dl_plan with the exact size instead
+        gpre_n = n_bound * m0 if m0 > 12 else (c_bound * (m0 + 4) if m0 + Pm.DL_MAX_LEVELS > 12 else 0)
+        b = S.post_buffers(F1, c_bound, n_bound + c_bound, min(gpre_n, 1 << 24))
         P = S.post
         P.item_map, P.rec, P.part, P.out = (b["item_map"].data_ptr(), b["rec"].data_ptr(), b["part"].data_ptr(),
                                             b["out"].data_ptr())
         P.rec_cap, P.part_cap, P.out_cap = b["c_cap"], b["part"].numel(), b["c_cap"]
+        P.gpre, P.gpre_cap = b["gpre"].data_ptr(), b["gpre"].numel()
         P.roff, P.ranks = db["roff"].data_ptr(), db["ranks"].data_ptr()
         P.src = db["src"].data_ptr() if db["src"] is not None else None
         P.wword = db["wword"].data_ptr() if db["wword"] is not None else None

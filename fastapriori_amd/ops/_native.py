@@ -86,7 +86,9 @@ _HIP_SIGS = {
     # device-resident level bundles (gen.hip fa_hip_dl_*, levels.hip)
     "fa_hip_dl_level0": (C.c_int, [vp, vp, i64, i64, C.c_int, C.c_int, vp, i64, vp, vp, i64, dbl, vp, C.c_int, vp]),
     "fa_hip_dl_more": (C.c_int, [C.c_int, vp, i64, i64, vp, vp, dbl, C.c_int, dbl, i64, vp, vp, vp, vp]),
-    "fa_hip_dl_plan": (C.c_int, [vp, C.c_int, vp, C.c_int, vp, vp, i64, vp, i64, vp]),
+    "fa_hip_dl_plan": (C.c_int, [vp, C.c_int, vp, C.c_int, vp, vp, i64, vp, i64, vp, i64, vp]),
+    "fa_hip_dl_gpre_need": (i64, [vp, C.c_int]),
+    "fa_hip_dl_plan_window": (C.c_int, [vp, C.c_int, vp, C.c_int, vp, vp, i64, vp, i64, vp, i64, i64, i64, vp]),
     "fa_hip_dl_threshold": (C.c_int, [vp, C.c_int, vp, i64, vp, vp, vp, vp, vp, vp]),
     "fa_hip_trim_scan_count": (C.c_int, [vp, vp, i64, vp, C.c_int, C.c_int, vp, vp, vp, vp, vp]),
     "fa_hip_trim_emit": (C.c_int, [vp, vp, vp, C.c_int, i64, vp, vp, vp, vp, vp, vp, vp, vp]),
@@ -110,7 +112,7 @@ _HIP_SIGS = {
     "fa_hip_tline_count": (C.c_int, [vp, i64, i64, vp, vp]),
     "fa_hip_tparse": (C.c_int, [vp, i64, i64, i64, C.c_int, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "fa_hip_scan_small": (C.c_int, [C.c_int, vp, i64, vp, vp, vp]),
-    "fa_hip_tcompact": (C.c_int, [vp, vp, i64, vp, vp, vp, vp, vp, vp, vp, i64, vp, C.c_int, vp, vp, vp]),
+    "fa_hip_tcompact": (C.c_int, [vp, vp, i64, C.c_int, vp, vp, vp, vp, vp, vp, vp, i64, vp, C.c_int, vp, vp, vp]),
     "fa_hip_hist_reduce": (C.c_int, [vp, C.c_int, vp, vp]),
     "fa_hip_line_count": (C.c_int, [vp, i64, vp, vp]),
     "fa_hip_line_ends": (C.c_int, [vp, i64, vp, vp, vp]),

@@ -1239,7 +1239,8 @@ class TileParse:
                       "fa_hip_scan_small")
         off = torch.empty(nl, dtype=_I64, device=dev)
         grid = max(1, min(self.GRID, tiles))
-        _native.check(lib.fa_hip_tcompact(_p(tile_base), _p(tile_xb), tiles, _p(dcnt), _p(xcnt), _p(lbase),
+        _native.check(lib.fa_hip_tcompact(_p(tile_base), _p(tile_xb), tiles, int(bool(tail)), _p(dcnt), _p(xcnt),
+                                          _p(lbase),
                                           _p(self.scratch), _p(self.xscratch), _p(self.items), _p(self.extras),
                                           self.xcap, _p(off), grid, _p(self.hpart), _p(self.flags), st),
                       "fa_hip_tcompact")
@@ -1339,9 +1340,10 @@ def parse_dict_device(buf: torch.Tensor, n: int, last_is_term: bool):
 # csrc/hip/levels.hip fa_hip_dl_plan / fa_hip_dl_threshold; driven by
 # models.apriori.FastApriori._mine_device)
 # ---------------------------------------------------------------------------
-DL_CTL = 256            # gen.hip kDlCtl
-DL_MAX_F1 = 4096        # the control block's used-item bitset (ctl[128:192])
-DL_MAX_M = 12           # prefix ids inline in the 48-B piece records
+DL_CTL = 1024           # gen.hip kDlCtl
+DL_BITS = 512           # gen.hip kDlBits: the control block's used-item bitset (ctl[512:1024])
+DL_MAX_F1 = 32768       # its bits (and the generator's 8 bitset words per lane)
+DL_MAX_M = 40           # levels.hip kDlMaxM (prefixes past 12 ids go through gpre)
 DL_MAX_LEVELS = 31
 
 
@@ -1354,7 +1356,8 @@ class DlPostC(ctypes.Structure):
                [("ncols", ctypes.c_int64), ("lds_kernel", ctypes.c_double), ("lds_budget", ctypes.c_double)] + \
                [(n, ctypes.c_void_p) for n in ("c1", "alive", "len_hist")] + \
                [(n, ctypes.c_int64) for n in ("T", "nnz", "trim_min_rows", "trim_ok", "k",
-                                               "done", "sw", "cap", "n_wg", "C", "trim")]
+                                               "done", "sw", "cap", "n_wg", "C", "trim")] + \
+               [("gpre", ctypes.c_void_p), ("gpre_cap", ctypes.c_int64)]
 
 
 class DeviceLevelState:
@@ -1378,19 +1381,23 @@ class DeviceLevelState:
     def grow(self, nbytes: int) -> None:
         self.ws = torch.empty(int(nbytes * 1.25) + (1 << 20), dtype=torch.uint8, device=self.dev)
 
-    def post_buffers(self, F1: int, c_cap: int, rows_cap: int):
+    def post_buffers(self, F1: int, c_cap: int, rows_cap: int, gpre_n: int = 0):
         """Grow-only plan / count buffers of the post step: item_map [F1], piece
-        records [c_cap], planner scratch for rows_cap parent rows, counts [c_cap]."""
+        records [c_cap], planner scratch for rows_cap parent rows, counts [c_cap],
+        long-prefix slab rows [gpre_n]."""
         part_n = 8 * ((rows_cap + 255) // 256 + 2)
         b = self.post_bufs
-        if b is None or b["F1"] < F1 or b["c_cap"] < c_cap or b["part"].numel() < part_n:
+        if (b is None or b["F1"] < F1 or b["c_cap"] < c_cap or b["part"].numel() < part_n
+                or b["gpre"].numel() < gpre_n):
             F1, c_cap = max(F1, b["F1"] if b else 0), max(c_cap, b["c_cap"] if b else 0)
             part_n = max(part_n, b["part"].numel() if b else 0)
+            gpre_n = max(gpre_n, b["gpre"].numel() if b else 1)
             b = self.post_bufs = dict(F1=F1, c_cap=c_cap,
                                       item_map=torch.empty(max(F1, 1), dtype=_I32, device=self.dev),
                                       rec=torch.empty(12 * c_cap + 12, dtype=_I32, device=self.dev),
                                       part=torch.empty(part_n, dtype=_I32, device=self.dev),
-                                      out=torch.empty(c_cap, dtype=_I32, device=self.dev))
+                                      out=torch.empty(c_cap, dtype=_I32, device=self.dev),
+                                      gpre=torch.empty(max(gpre_n, 1), dtype=_I32, device=self.dev))
         return b
 
 
@@ -1465,10 +1472,56 @@ def dl_plan(S: DeviceLevelState, L: int, F1: int, n_used: int, C: int, lds: int,
     rec = torch.empty(12 * C + 12, dtype=_I32, device=dev)
     R = int(S.desc[:L, 5].sum())                     # parent rows of the bundle
     part = torch.empty(8 * max(1, (R + 255) // 256), dtype=_I32, device=dev)
-    _native.check(_native.hip().fa_hip_dl_plan(S.desc.ctypes.data, L, _p(S.ctl), F1, _p(item_map), _p(rec), C,
-                                               _p(part), part.numel(), st), "fa_hip_dl_plan")
+    lib = _native.hip()
+    gn = int(lib.fa_hip_dl_gpre_need(S.desc.ctypes.data, L))
+    gpre = torch.empty(max(gn, 1), dtype=_I32, device=dev)
+    _native.check(lib.fa_hip_dl_plan(S.desc.ctypes.data, L, _p(S.ctl), F1, _p(item_map), _p(rec), C,
+                                     _p(part), part.numel(), _p(gpre), gpre.numel(), st), "fa_hip_dl_plan")
     out = torch.zeros(C, dtype=_I32, device=dev)
-    return dict(sw=sw, cap=cap, item_map=item_map, rec=rec, out=out, n_used=n_used, C=C)
+    return dict(sw=sw, cap=cap, item_map=item_map, rec=rec, out=out, n_used=n_used, C=C, gpre=gpre)
+
+
+def dl_count_multipass(S: DeviceLevelState, F1: int, n_used: int, C: int, lds: int, roff, ranks, src, ncols: int,
+                       wword, bm, bm_rows, sup_frac: float, dev) -> torch.Tensor | None:
+    """Counts of a device bundle's single level whose C candidates exceed one
+    accumulator pass: per window of cap candidates, a device plan of that window
+    (levels.hip fa_hip_dl_plan_window) and a slab count from the used items' bitmap
+    (bm [n_used or more][Wp]; bm_rows: slab row -> bitmap row, device int32, or None
+    when bitmap row u is slab row u).  sup_frac: minimum support / rows (count_level's
+    dense test).  Returns int32 [C] (not reduced across ranks), or None when no slab
+    width fits the used items."""
+    sw, cap = dl_slab_width(n_used, min(C, 8192), lds)
+    if sw == 0:
+        return None
+    dense = wword is None and DENSE_MIN_ROWS > 0 and sup_frac * sw * 64 >= DENSE_MIN_ROWS
+    cap = min(cap, C)
+    st = _stream(ranks)
+    lib = _native.hip()
+    item_map = torch.empty(max(F1, 1), dtype=_I32, device=dev)
+    rec = torch.empty(12 * cap + 12, dtype=_I32, device=dev)
+    R = int(S.desc[0, 5])
+    part = torch.empty(8 * max(1, (R + 255) // 256) + 16, dtype=_I32, device=dev)
+    gn = int(lib.fa_hip_dl_gpre_need(S.desc.ctypes.data, 1))
+    gpre = torch.empty(max(gn, 1), dtype=_I32, device=dev)
+    out = torch.zeros(C, dtype=_I32, device=dev)
+    W = (ncols + 63) // 64
+    nslabs = (W + sw - 1) // sw
+    npass = 0
+    for w0 in range(0, C, cap):
+        w1 = min(C, w0 + cap)
+        _native.check(lib.fa_hip_dl_plan_window(S.desc.ctypes.data, 1, _p(S.ctl), F1, _p(item_map), _p(rec), cap,
+                                                _p(part), part.numel(), _p(gpre), gpre.numel(), w0, w1, st),
+                      "fa_hip_dl_plan_window")
+        lds_k = n_used * (sw + 2) * 8 + ((w1 - w0 + 3) & ~3) * 4
+        n_wg = int(max(1, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds_k), 2))))
+        _hip_call("fa_hip_count_slab_rec_cls", _p(roff), _p(ranks), _p(src), ncols, _p(item_map), F1, n_used,
+                  _p(gpre), _p(rec), 0, w1 - w0, _p(wword), out.data_ptr() + 4 * w0, sw, n_wg, _p(bm),
+                  bm.stride(0), st, _p(bm_rows), _p(S.ctl) + 8 * 221, 2 if dense else 0)
+        npass += 1
+    LAST_LEVEL_PLAN.clear()
+    LAST_LEVEL_PLAN.update(kernel="slab_dev_multi", rows=int(roff.numel() - 1), used=n_used, sw=sw, cap=cap,
+                           passes=npass, pieces=-1, slab_reads=0, m=int(S.desc[0, 4]), C=C, dense=bool(dense))
+    return out
 
 
 def dl_plan_from_post(S: DeviceLevelState, n_used: int) -> dict:
@@ -1476,7 +1529,8 @@ def dl_plan_from_post(S: DeviceLevelState, n_used: int) -> dict:
     P, b = S.post, S.post_bufs
     C = int(P.C)
     out = b["out"][:C]
-    return dict(sw=int(P.sw), cap=int(P.cap), item_map=b["item_map"], rec=b["rec"], out=out, n_used=n_used, C=C)
+    return dict(sw=int(P.sw), cap=int(P.cap), item_map=b["item_map"], rec=b["rec"], out=out, n_used=n_used, C=C,
+                gpre=b["gpre"])
 
 
 def dl_count(S: DeviceLevelState, plan: dict, roff, ranks, src, ncols: int, F1: int, wword) -> torch.Tensor:
@@ -1489,8 +1543,9 @@ def dl_count(S: DeviceLevelState, plan: dict, roff, ranks, src, ncols: int, F1: 
     nslabs = (W + sw - 1) // sw
     lds_k = n_used * (sw + 2) * 8 + ((C + 3) & ~3) * 4 + _slab_map_lds(F1)
     n_wg = int(max(1, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds_k), 2))))
-    _hip_call("fa_hip_count_slab_rec", _p(roff), _p(ranks), _p(src), ncols, _p(item_map), F1, n_used, None, _p(rec),
-              0, C, _p(wword), _p(out), sw, n_wg, None, 0, st, None, _p(S.ctl) + 8 * 221)
+    _hip_call("fa_hip_count_slab_rec", _p(roff), _p(ranks), _p(src), ncols, _p(item_map), F1, n_used,
+              _p(plan.get("gpre")), _p(rec), 0, C, _p(wword), _p(out), sw, n_wg, None, 0, st, None,
+              _p(S.ctl) + 8 * 221)
     LAST_LEVEL_PLAN.clear()
     LAST_LEVEL_PLAN.update(kernel="slab_dev", rows=int(roff.numel() - 1), used=n_used, sw=sw, cap=cap, passes=1,
                            pieces=-1, slab_reads=0, m=-1, C=C)

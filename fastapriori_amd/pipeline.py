@@ -56,6 +56,53 @@ def _load_saved(cfg: JobConfig, comm):
     return res
 
 
+def mine_window(cfg: JobConfig, comm, log: Logger, ckpt: Checkpointer | None, summary: dict):
+    """The reference's timed mining window (Main.scala:28-32): read + parse D.dat,
+    mine, write freqItemset (and, with a temp path, the per-level checkpoint).
+    bench.py times this same function for its e2e record."""
+    d_path, out_freq = cfg.input + "D.dat", cfg.output + "freqItemset"
+    resume = _load_checkpoint(ckpt, comm) if (ckpt is not None and cfg.resume) else None
+    # candidate distribution: every rank holds the whole DB
+    t_read = time.time()
+    shard = io.read_shard(d_path, comm if cfg.strategy == "count" else Comm(device=comm.device))
+    summary["read_ms"] = round((time.time() - t_read) * 1000, 1)
+    mcfg = MinerConfig(min_support=cfg.min_support, dedup=cfg.dedup, pair_strategy=cfg.pair_strategy,
+                       max_level=cfg.max_level, parallelism=cfg.strategy)
+    miner = FastApriori(cfg.min_support, comm, mcfg, log, ckpt)
+    result = miner.run(shard, resume=resume)
+    summary["miner"] = dict(miner.stats)
+    summary["device_bundles"] = int(miner.stats.get("device_bundles", 0))
+    trace = summary["miner"].pop("trace", None)
+    if cfg.profile and trace is not None and comm.is_root:
+        # Chrome trace of the mining phases (host spans + hipEvent device spans)
+        tpath = os.path.join(cfg.temp or ".", "fastapriori_trace.json")
+        with open(tpath, "w") as f:
+            json.dump({"traceEvents": trace, "displayTimeUnit": "ms"}, f)
+        summary["trace_path"] = tpath
+    del shard
+    t_write = time.time()
+    if comm.is_root:
+        io.write_freq_itemsets(result, out_freq, overwrite=cfg.overwrite)
+        if cfg.with_counts:
+            io.write_freq_itemsets(result, cfg.output + "freqItems", with_counts=True, overwrite=cfg.overwrite)
+            io.write_items_to_rank(result, cfg.output + "ItemsToRank")
+            io.write_freq_items(result, cfg.output + "FreqItems")
+    if ckpt is not None:
+        # joins the checkpoint writer the device level loop started in the background
+        ckpt.mark_complete(result)
+    comm.barrier()
+    summary["write_ms"] = round((time.time() - t_write) * 1000, 1)
+    return result
+
+
+def make_checkpointer(cfg: JobConfig, comm) -> Checkpointer | None:
+    if cfg.temp and (cfg.checkpoint or cfg.rules_only):
+        # rules-only needs no D.dat: it reloads the mined itemsets (Utils.getAll's use case)
+        fp = None if cfg.rules_only else input_fingerprint(cfg.input + "D.dat", cfg.min_support)
+        return Checkpointer(cfg.temp, comm.rank, fp)
+    return None
+
+
 def run_job(cfg: JobConfig, comm=None) -> dict:
     own_comm = comm is None
     if comm is None:
@@ -66,19 +113,14 @@ def run_job(cfg: JobConfig, comm=None) -> dict:
             shutdown_comm(comm)
         raise RuntimeError(f"--world-size {cfg.world_size} but the process group has {comm.world_size} ranks")
     log = Logger(comm.rank, metrics_path=cfg.metrics_path)
-    d_path, u_path = cfg.input + "D.dat", cfg.input + "U.dat"
-    out_freq, out_rec = cfg.output + "freqItemset", cfg.output + "recommends"
+    u_path = cfg.input + "U.dat"
+    out_rec = cfg.output + "recommends"
     summary: dict = {}
     try:
-        ckpt = None
-        if cfg.temp and (cfg.checkpoint or cfg.rules_only):
-            # rules-only needs no D.dat: it reloads the mined itemsets (Utils.getAll's use case)
-            fp = None if cfg.rules_only else input_fingerprint(d_path, cfg.min_support)
-            ckpt = Checkpointer(cfg.temp, comm.rank, fp)
+        ckpt = make_checkpointer(cfg, comm)
         comm.barrier()
 
         t1 = time.time()
-        result = None
         if cfg.rules_only:
             # the complete checkpoint under temp, else the saved result files of a
             # --with-counts run (freqItems + ItemsToRank: Utils.getAll, Utils.scala:65-81)
@@ -89,40 +131,9 @@ def run_job(cfg: JobConfig, comm=None) -> dict:
                 where = f"under {ckpt.dir} " if ckpt is not None else ""
                 raise FileNotFoundError(f"--rules-only: no complete checkpoint {where}and no "
                                         f"{cfg.output}freqItems + {cfg.output}ItemsToRank (written by --with-counts)")
+            comm.barrier()
         else:
-            resume = _load_checkpoint(ckpt, comm) if (ckpt is not None and cfg.resume) else None
-            # candidate distribution: every rank holds the whole DB
-            t_read = time.time()
-            shard = io.read_shard(d_path, comm if cfg.strategy == "count" else Comm(device=comm.device))
-            summary["read_ms"] = round((time.time() - t_read) * 1000, 1)
-            mcfg = MinerConfig(min_support=cfg.min_support, dedup=cfg.dedup, pair_strategy=cfg.pair_strategy,
-                               max_level=cfg.max_level, parallelism=cfg.strategy)
-            miner = FastApriori(cfg.min_support, comm, mcfg, log, ckpt)
-            result = miner.run(shard, resume=resume)
-            summary["miner"] = dict(miner.stats)
-            summary["device_bundles"] = int(miner.stats.get("device_bundles", 0))
-            trace = summary["miner"].pop("trace", None)
-            if cfg.profile and trace is not None and comm.is_root:
-                # Chrome trace of the mining phases (host spans + hipEvent device spans)
-                tpath = os.path.join(cfg.temp or ".", "fastapriori_trace.json")
-                with open(tpath, "w") as f:
-                    json.dump({"traceEvents": trace, "displayTimeUnit": "ms"}, f)
-                summary["trace_path"] = tpath
-            del shard
-            t_write = time.time()
-            if comm.is_root:
-                io.write_freq_itemsets(result, out_freq, overwrite=cfg.overwrite)
-                if cfg.with_counts:
-                    io.write_freq_itemsets(result, cfg.output + "freqItems", with_counts=True,
-                                           overwrite=cfg.overwrite)
-                    io.write_items_to_rank(result, cfg.output + "ItemsToRank")
-                    io.write_freq_items(result, cfg.output + "FreqItems")
-            if ckpt is not None:
-                # joins the checkpoint writer the device level loop started in the background
-                ckpt.mark_complete(result)
-        comm.barrier()
-        if not cfg.rules_only:
-            summary["write_ms"] = round((time.time() - t_write) * 1000, 1)
+            result = mine_window(cfg, comm, log, ckpt, summary)
         t_mine = int((time.time() - t1) * 1000)
         log.line(f"Total time for get freqItemsets {t_mine}")
 

@@ -3,8 +3,9 @@ fa_hip_dl_*, csrc/hip/levels.hip) against the host-driven level loop and the C++
 CPU miner: identical itemsets, counts and level order (rows lexicographic).
 
 Covers unit and weighted (dedup) layouts, transaction trimming inside a device
-bundle, max_level, the hand-off to the host loop when level k needs several
-accumulator passes (T40I10 shape), and an empty F_2.
+bundle, max_level, levels that need several accumulator passes (T40I10 shape,
+counted on the device window by window), wide vocabularies (F1 > 4096), prefixes
+past the records' 12 inline ids, and an empty F_2.
 Reference semantics: FastApriori.scala:110-160.
 """
 import numpy as np
@@ -58,14 +59,45 @@ def test_device_levels_match_host_loop(monkeypatch, n, ms, kw):
         assert got.as_dict() == cref.as_dict()
 
 
-def test_device_levels_hand_off_multipass_level():
-    # T40I10: level 4's candidates need several accumulator passes -> host loop from there
+def test_multipass_level_stays_on_device(monkeypatch):
+    # T40I10: level 4's candidates need several accumulator passes -> counted on the device
+    # window by window (FastApriori._dl_multipass); FA_DL_MULTI=0 hands off to the host loop
     cpu = generate_shard(150_000, Comm(), "cpu", 40.0, 10.0, 2000, 1000, 3)
-    got, st = _mine(cpu.to(DEV), 0.01)
     ref, _ = _mine(cpu, 0.01)
     assert len(ref.levels) >= 6
+    got, st = _mine(cpu.to(DEV), 0.01)
+    assert st.get("device_multipass", 0) >= 1 and st.get("host_levels", 0) == 0
+    assert st["device_levels"] >= len(ref.levels) - 2 and "fallbacks" not in st
     assert got.as_dict() == ref.as_dict()
-    assert [len(x) for x in got.levels] == [len(x) for x in ref.levels]
+    _same(got, ref)
+    monkeypatch.setattr(ap, "DL_MULTI", False)
+    got2, st2 = _mine(cpu.to(DEV), 0.01)
+    assert st2.get("host_levels", 0) >= 1
+    _same(got2, ref)
+
+
+def test_small_lds_forces_device_multipass(monkeypatch):
+    # a shrunk LDS budget turns T10I4 levels into multi-pass ones: windows, trimming and
+    # the used items' bitmap on the unit and the weighted (dedup) layout
+    import fastapriori_amd.ops.primitives as prim
+    cpu = generate_shard(200_000, Comm(), "cpu", 10.0, 4.0, 2000, 1000, 4)
+    ref, _ = _mine(cpu, 0.002)
+    monkeypatch.setattr(prim, "_LDS_BYTES", 24 * 1024)
+    for dd in ("off", "on"):
+        got, st = _mine(cpu.to(DEV), 0.002, dedup=dd, trim_min_rows=0)
+        assert st.get("device_multipass", 0) >= 1, st
+        _same(got, ref)
+
+
+def test_deep_database_all_levels_on_device():
+    # >= 14 levels (prefixes past the 12 ids a piece record holds inline: levels.hip gpre)
+    cpu = generate_shard(120_000, Comm(), "cpu", 40.0, 10.0, 2000, 1000, 3)
+    ref, _ = _mine(cpu, 0.005)
+    assert len(ref.levels) >= 14
+    got, st = _mine(cpu.to(DEV), 0.005)
+    assert st.get("host_levels", 0) == 0 and st["device_levels"] >= len(ref.levels) - 2, st
+    assert "fallbacks" not in st
+    _same(got, ref)
 
 
 def test_device_levels_no_frequent_pairs():
@@ -91,15 +123,12 @@ def test_device_levels_repeat_runs_identical():
 def test_wide_f1_generates_on_device_without_fallbacks(monkeypatch):
     # F1 = 6319 > 4096: the generator's lanes hold two bitset words each
     # (gen.hip ag_row_bits<2>); no level may fall back to the host generator
-    from fastapriori_amd import ops
     cpu = generate_shard(300_000, Comm(), "cpu", 10.0, 4.0, 6000, 12000, 3)
-    calls = []
-    real = ops.primitives.apriori_gen_chain
-    monkeypatch.setattr(ops.primitives, "apriori_gen_chain", lambda *a, **k: calls.append(a[1]) or real(*a, **k))
     got, st = _mine(cpu.to(DEV), 0.0004)
     ref, _ = _mine(cpu, 0.0004)
     assert len(got.items) > 4096 and len(ref.levels) >= 8
-    assert calls and all(f1 == len(got.items) for f1 in calls)
+    # every level >= 3 in device bundles (gen.hip: 2 bitset words per lane, ctl bitset of F1 bits)
+    assert st.get("host_levels", 0) == 0 and st["device_levels"] >= len(ref.levels) - 2, st
     assert "fallbacks" not in st
     assert got.as_dict() == ref.as_dict()
     _same(got, ref)
