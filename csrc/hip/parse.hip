@@ -140,7 +140,7 @@ constexpr int kTBy = kLB;
 constexpr int kTTile = kTT * kTBy;       // = kLTile: k_tline_count uses the same tiles
 constexpr int kHalo = 2048;
 constexpr int kTLds = kHalo + kTTile + 64;
-constexpr int kSeenT = 32;
+constexpr int kSeenT = 16;
 constexpr int kHistCap = 8192;
 
 __global__ __launch_bounds__(kLT) void k_tline_count(const uint8_t* __restrict__ buf, int64_t a, int64_t lo,
@@ -163,7 +163,11 @@ __global__ __launch_bounds__(kTT) void k_tparse(const uint8_t* __restrict__ buf,
                                                 int32_t* __restrict__ xcnt, int64_t* __restrict__ lbase,
                                                 int32_t* __restrict__ scratch, int32_t* __restrict__ xscratch,
                                                 int32_t* __restrict__ tile_dx, int32_t* __restrict__ flags) {
-  __shared__ uint4 sb4[kTLds / 16];
+  // The tile image in LDS: file byte o (relative to l0) in dword (o >> 2) + (o >> 6).
+  // One dword of padding per 64 bytes: the threads' 64-byte chunks (and the lines they
+  // parse, lock-stepped at similar offsets) then fall on different banks; unpadded,
+  // a 64-byte stride puts all 32 lanes of a ds_read_b32 half on 2 banks (16-way).
+  __shared__ uint32_t sw[kTLds / 4 + kTLds / 64 + 1];
   __shared__ int32_t seen[kSeenT * kTT];      // column per thread: conflict-free
   __shared__ int wsum[kTT / kWave];
   __shared__ long long wmax[kTT / kWave];
@@ -174,11 +178,12 @@ __global__ __launch_bounds__(kTT) void k_tparse(const uint8_t* __restrict__ buf,
     const int64_t p = l0 + 16 * (int64_t)q;
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
     if (p >= 0 && p + 16 <= buf_len) v = *reinterpret_cast<const uint4*>(buf + p);
-    sb4[q] = v;
+    uint32_t* d = sw + 4 * q + (q >> 2);       // a 16-byte piece never straddles a 64-byte chunk
+    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
   }
   __syncthreads();
-  const uint8_t* sb = reinterpret_cast<const uint8_t*>(sb4);
-  const uint32_t* sw = reinterpret_cast<const uint32_t*>(sb4);
+  auto lds_dw = [&](int64_t o) -> uint32_t { return sw[(o >> 2) + (o >> 6)]; };
+  auto lds_b = [&](int64_t o) -> uint32_t { return (lds_dw(o) >> (8 * (o & 3))) & 0xffu; };
   // line ends among this thread's bytes [c0, c0 + 64) that lie in [lo, hi)
   const int64_t c0 = t0 + (int64_t)tid * kTBy;
   unsigned long long M = 0ull;
@@ -186,11 +191,9 @@ __global__ __launch_bounds__(kTT) void k_tparse(const uint8_t* __restrict__ buf,
     const int lb0 = kHalo + tid * kTBy;
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      const uint4 w = sb4[lb0 / 16 + v];
-      const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const uint32_t x = ws[q];
+        const uint32_t x = lds_dw(lb0 + 16 * v + 4 * q);
         const uint32_t xa = x ^ 0x0a0a0a0au, xb = x ^ 0x0d0d0d0du;
         const uint32_t za = (xa - 0x01010101u) & ~xa & 0x80808080u;
         const uint32_t zb = (xb - 0x01010101u) & ~xb & 0x80808080u;
@@ -200,7 +203,7 @@ __global__ __launch_bounds__(kTT) void k_tparse(const uint8_t* __restrict__ buf,
           const int o = v * 16 + q * 4 + k;
           const int64_t i = c0 + o;
           const uint32_t c = (x >> (8 * k)) & 0xffu;
-          const bool t = c == '\n' || (c == '\r' && (i + 1 >= hi || sb[lb0 + o + 1] != '\n'));
+          const bool t = c == '\n' || (c == '\r' && (i + 1 >= hi || lds_b(lb0 + o + 1) != '\n'));
           if (t && i >= lo && i < hi) M |= 1ull << o;
         }
       }
@@ -239,8 +242,8 @@ __global__ __launch_bounds__(kTT) void k_tparse(const uint8_t* __restrict__ buf,
       s0 = -1;
       const int64_t stop = lo > l0 ? lo : l0;
       for (int64_t p = t0 - 1; p >= stop; --p) {
-        const uint32_t c = sb[p - l0];
-        if (c == '\n' || (c == '\r' && sb[p + 1 - l0] != '\n')) { s0 = p + 1; break; }
+        const uint32_t c = lds_b(p - l0);
+        if (c == '\n' || (c == '\r' && lds_b(p + 1 - l0) != '\n')) { s0 = p + 1; break; }
       }
       if (s0 < 0 && lo < l0) {
         for (int64_t p = l0 - 1; p >= lo; --p) {
@@ -250,7 +253,7 @@ __global__ __launch_bounds__(kTT) void k_tparse(const uint8_t* __restrict__ buf,
       }
       if (s0 < 0) s0 = lo;
     }
-    auto byte_at = [&](int64_t p) -> uint32_t { return p >= l0 ? (uint32_t)sb[p - l0] : (uint32_t)buf[p]; };
+    auto byte_at = [&](int64_t p) -> uint32_t { return p >= l0 ? lds_b(p - l0) : (uint32_t)buf[p]; };
     unsigned long long mm = M;
     for (int left = cnt; left > 0 && !bad; --left, ++g) {
       int64_t e0;
@@ -276,7 +279,7 @@ __global__ __launch_bounds__(kTT) void k_tparse(const uint8_t* __restrict__ buf,
       bool lead0 = false;
       unsigned long long f0 = 0ull, f1 = 0ull;
       for (int64_t q = s & ~(int64_t)3; q <= e && !bad; q += 4) {
-        const uint32_t w = q >= l0 ? sw[(q - l0) >> 2] : *reinterpret_cast<const uint32_t*>(buf + q);
+        const uint32_t w = q >= l0 ? lds_dw(q - l0) : *reinterpret_cast<const uint32_t*>(buf + q);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const int64_t p = q + k;
@@ -429,19 +432,30 @@ __global__ __launch_bounds__(256) void k_tcompact(const int64_t* __restrict__ ti
       if (j < j1) off[j] = bd + incl - d;
       const int tot = wave_last(incl);
       const int excl = incl - d;
-      for (int kb = 0; kb < tot; kb += 64) {     // wave-uniform trip count: every lane takes part in the shuffles
-        const int k = kb + lane;
-        int L = 0;                               // the lane whose line holds flattened id k
+      // wave-uniform trip count: every lane takes part in the shuffles; four gathers are
+      // issued before the first of their stores (they are independent of each other)
+      constexpr int kU = 4;
+      for (int kb = 0; kb < tot; kb += 64 * kU) {
+        int32_t id[kU];
 #pragma unroll
-        for (int st = 32; st > 0; st >>= 1)
-          if (__shfl(incl, L + st - 1, 64) <= k) L += st;
-        const int64_t lbL = __shfl(lb, L, 64);
-        const int exL = __shfl(excl, L, 64);
-        if (k < tot) {
-          const int32_t id = lbL < 0 ? 0 : scratch[lbL + (k - exL)];
-          items[bd + k] = id;
-          if (hpart) {
-            if ((uint32_t)id < (uint32_t)kHistCap) atomicAdd(&h[id], 1u); else over = true;
+        for (int u = 0; u < kU; ++u) {
+          const int k = kb + 64 * u + lane;
+          int L = 0;                             // the lane whose line holds flattened id k
+#pragma unroll
+          for (int st = 32; st > 0; st >>= 1)
+            if (__shfl(incl, L + st - 1, 64) <= k) L += st;
+          const int64_t lbL = __shfl(lb, L, 64);
+          const int exL = __shfl(excl, L, 64);
+          id[u] = (k < tot && lbL >= 0) ? scratch[lbL + (k - exL)] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const int k = kb + 64 * u + lane;
+          if (k < tot) {
+            items[bd + k] = id[u];
+            if (hpart) {
+              if ((uint32_t)id[u] < (uint32_t)kHistCap) atomicAdd(&h[id[u]], 1u); else over = true;
+            }
           }
         }
       }

@@ -17,3 +17,7 @@ timeout -k 10 600 python benchmarks/multirank_probe.py --world 8 --n-txn 4000000
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --marker-trace --output-format csv -d "$O/mk40" -o run -- \
   python3 "$R/bench.py" --config T40I10D100M --steps 1 --warmup 0 --e2e off > "$O/mk40.log" 2>&1
+cd $R
+for val in 1 0; do
+  FA_DL_MULTI=$val timeout -k 10 400 python bench.py --config T40I10D100M --steps 3 --warmup 1 --e2e off > $O/T40_multi$val.json 2> $O/T40_multi$val.err
+done
