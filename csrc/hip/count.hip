@@ -1161,6 +1161,10 @@ __device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
   return r;
 }
 
+__device__ __forceinline__ uint32_t and3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x80);
+}
+
 __device__ __forceinline__ int u16_at(const int4& v, int k) {
   const int w = (k >> 1) == 0 ? v.x : (k >> 1) == 1 ? v.y : (k >> 1) == 2 ? v.z : v.w;
   return (k & 1) ? (int)((uint32_t)w >> 16) : (w & 0xFFFF);
@@ -1203,6 +1207,30 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
     for (int q = 0; q < SW / 2; ++q) {
       const uint4 v = r[q];
       p[q].x &= v.x; p[q].y &= v.y; p[q].z &= v.z; p[q].w &= v.w;
+    }
+  };
+  // two prefix rows per VALU op: v_bitop3_b32 p & a & b (truth table 0x80); the
+  // prefix ANDs were ~60 % of the counting VALU of the deep bundles (m ~ 5, 1-2
+  // extensions per piece)
+  auto and_row2 = [&](uint4 (&p)[SW / 2], int u, int w) {
+    const uint4* r = lds4 + (size_t)u * RS;
+    const uint4* t = lds4 + (size_t)w * RS;
+#pragma unroll
+    for (int q = 0; q < SW / 2; ++q) {
+      const uint4 v = r[q], x = t[q];
+      p[q].x = and3(p[q].x, v.x, x.x); p[q].y = and3(p[q].y, v.y, x.y);
+      p[q].z = and3(p[q].z, v.z, x.z); p[q].w = and3(p[q].w, v.w, x.w);
+    }
+  };
+  // AND of prefix rows [j0, j1) of the piece (ids 1-3 in ra, 4-11 in rc), two at a time
+  auto pid = [&](int j) { return j < 4 ? u16_at(ra, 4 + j) : u16_at(rc, j - 4); };
+  auto and_prefix = [&](uint4 (&p)[SW / 2], int j0, int j1) {
+#pragma unroll
+    for (int j = 1; j < 12; j += 2) {
+      if (j >= j0 && j < j1) {
+        if (j + 1 < j1) and_row2(p, pid(j), pid(j + 1));
+        else and_row(p, pid(j));
+      }
     }
   };
   auto acc_add = [&](int e, uint32_t v) { atomicAdd(&acc[e], v); };
@@ -1293,14 +1321,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
           const uint4* r0 = lds4 + (size_t)(ra.z & 0xFFFF) * RS;
 #pragma unroll
           for (int q = 0; q < SW / 2; ++q) qv[q] = r0[q];
-#pragma unroll
-          for (int j = 1; j < 4; ++j)
-            if (j < m - 1) and_row(qv, u16_at(ra, 4 + j));
-          if (m > 5) {
-#pragma unroll
-            for (int j = 4; j < 11; ++j)
-              if (j < m - 1) and_row(qv, u16_at(rc, j - 4));
-          }
+          and_prefix(qv, 1, m - 1);
         }
         if (!(fl & 2)) {
           // the last prefix id rides in the record's bits 19-31 (a runtime u16_at index
@@ -1319,17 +1340,12 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
         for (int q = 0; q < SW / 2; ++q) p[q] = r0[q];
       }
       if (!((ra.y >> 16) & 1)) {
-#pragma unroll
-        for (int j = 1; j < 4; ++j)
-          if (j < m) and_row(p, u16_at(ra, 4 + j));
-        if (m > 4) {
-#pragma unroll
-          for (int j = 4; j < 12; ++j)
-            if (j < m) and_row(p, u16_at(rc, j - 4));
-        }
+        and_prefix(p, 1, m);
       } else {
         const int32_t* pr = gpre + rc.x;            // long prefixes (m > 12): ids from the plan's gpre
-        for (int j = 1; j < m; ++j) and_row(p, pr[j]);
+        int j = 1;
+        for (; j + 1 < m; j += 2) and_row2(p, pr[j], pr[j + 1]);
+        if (j < m) and_row(p, pr[j]);
       }
       }
       // an all-zero prefix skips its extensions; dense levels (dbg & 4: every frequent

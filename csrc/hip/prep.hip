@@ -812,9 +812,32 @@ __device__ __forceinline__ int nth_bit(unsigned long long m, int i) {
   return __builtin_ctzll(m);
 }
 
+// a frequent rank's count in its row's packed 256-rank block counts (byte b = block b;
+// exact while a row holds < 256 items of a block, the pair layout's u8 guard)
+__device__ __forceinline__ unsigned long long blk_inc(uint32_t v) {
+  return v == 0xFFFFFFFFu ? 0ull : 1ull << ((v >> 8) << 3);
+}
+
+// per-workgroup totals of the rows' block counts: aggb[b * gridDim.x + workgroup]
+__device__ __forceinline__ void cmp_block_totals(unsigned long long pc, int nb, int32_t* __restrict__ aggb) {
+  __shared__ int bs[8][4];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    if (b >= nb) break;
+    const int t = wave_last(wave_scan_incl_dpp((int)((pc >> (8 * b)) & 255)));
+    if (lane == 0) bs[b][w] = t;
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < nb)
+    aggb[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] =
+        bs[threadIdx.x][0] + bs[threadIdx.x][1] + bs[threadIdx.x][2] + bs[threadIdx.x][3];
+}
+
 __global__ __launch_bounds__(256) void k_cmp_agg(const int64_t* __restrict__ off, const int32_t* __restrict__ items,
                                                  const int32_t* __restrict__ lut, int64_t n,
-                                                 int32_t* __restrict__ agg, uint32_t* __restrict__ hist) {
+                                                 int32_t* __restrict__ agg, uint32_t* __restrict__ hist,
+                                                 int32_t* __restrict__ aggb, int nb) {
   __shared__ uint32_t buf[kCmpSpan];
   __shared__ uint32_t lh[256];
   __shared__ int sh[8];
@@ -826,11 +849,14 @@ __global__ __launch_bounds__(256) void k_cmp_agg(const int64_t* __restrict__ off
   const bool staged = cmp_stage(buf, items, lut, base, n_in);
   __syncthreads();
   int c = 0;
+  unsigned long long pc = 0;
   for (int64_t i = s; i < e; ++i) {
     const uint32_t v = staged ? buf[i - base] : (uint32_t)lut[items[i]];
     c += v != 0xFFFFFFFFu;
+    if (aggb) pc += blk_inc(v);
   }
   const int kept = c >= 2;
+  if (aggb) cmp_block_totals(kept ? pc : 0ull, nb, aggb);
   int ea, eb, ta, tb;
   cmp_block_scan2(kept, kept ? c : 0, ea, eb, ta, tb, sh);
   if (kept) atomicAdd(&lh[min(c, 255)], 1u);
@@ -855,10 +881,18 @@ __global__ __launch_bounds__(256) void k_cmp_emit(const int64_t* __restrict__ of
                                                   const int64_t* __restrict__ pre_over,
                                                   int32_t* __restrict__ kept_out, int64_t* __restrict__ roff,
                                                   int32_t* __restrict__ ranks, int32_t* __restrict__ over,
-                                                  uint8_t* __restrict__ bcnt, int nb) {
+                                                  uint8_t* __restrict__ bcnt, int nb,
+                                                  const int64_t* __restrict__ preb, uint8_t* __restrict__ lr,
+                                                  int64_t lr_cap, int64_t* __restrict__ lbase,
+                                                  int64_t* __restrict__ ovb) {
   constexpr int N = kCmpN;
   __shared__ uint32_t buf[kCmpSpan];
   __shared__ int sh[8];
+  // fused pair layout (lr != null): row x's block-b segment start in the workgroup's
+  // block-b span minus the row's first block-b index, tabx[x * nb + b]
+  extern __shared__ int32_t tabx[];
+  __shared__ int64_t wgb[8];
+  const bool blk = bcnt != nullptr;
   const int64_t r0 = (int64_t)blockIdx.x * 256, r1 = min(n, r0 + 256);
   const int64_t r = r0 + threadIdx.x;
   const int64_t base = off[r0], n_in = off[r1] - base;
@@ -869,6 +903,7 @@ __global__ __launch_bounds__(256) void k_cmp_emit(const int64_t* __restrict__ of
   const int64_t L = e - s;
   uint32_t a[N];
   int c = 0;
+  unsigned long long pc = 0;      // packed 256-rank block counts of the row (blk_inc)
   if (L <= N) {
 #pragma unroll
     for (int j = 0; j < N; ++j) {
@@ -876,11 +911,13 @@ __global__ __launch_bounds__(256) void k_cmp_emit(const int64_t* __restrict__ of
       if (j < L) v = staged ? buf[s - base + j] : (uint32_t)lut[items[s + j]];
       a[j] = v;
       c += v != 0xFFFFFFFFu;
+      if (blk) pc += blk_inc(v);
     }
   } else {
     for (int64_t i = s; i < e; ++i) {
       const uint32_t v = staged ? buf[i - base] : (uint32_t)lut[items[i]];
       c += v != 0xFFFFFFFFu;
+      if (blk) pc += blk_inc(v);
     }
   }
   const int kept = c >= 2;
@@ -897,27 +934,67 @@ __global__ __launch_bounds__(256) void k_cmp_emit(const int64_t* __restrict__ of
   __syncthreads();
   const int64_t ov_base = pre_over[blockIdx.x];
   const int64_t xk = xr0 + ea;
+  int64_t ovi = -1;
   if (kept) {
     kept_out[xk] = (int32_t)r;
     roff[xk + 1] = obase + eb + c;
     if (ov) {
       int64_t before = ov_base;
       for (int k = 0; k < w; ++k) before += ov_w[k];
-      over[before + __popcll(ob & (lanes_le_mask() >> 1))] = (int32_t)xk;
+      ovi = before + __popcll(ob & (lanes_le_mask() >> 1));
+      over[ovi] = (int32_t)xk;
     }
   }
   const bool mine = kept && L <= N;
   if (mine) bitonic_regs<N>(a);
-  if (bcnt && mine) {
+  if (blk) {
     // per-row item counts of the pair kernel's 256-rank blocks, bcnt[b * T + row]
-    // (the layout of k_block_counts_w; T = kept rows, the scan total), byte-packed:
-    // a row of <= 16 items never carries into the next block's byte
+    // (T = kept rows, the scan total), counted by value while the row was loaded.
+    // Fused pair layout (lr): every block's data in kept-row order, block-major --
+    // the row's block-b segment starts at the workgroup's block-b offset (preb: the
+    // scan of k_cmp_agg's per-workgroup totals) + the block scan below; the first
+    // row of every 64-row batch also writes the batch's base (pair_queue16's base).
     const int64_t bld = pre_rows[gridDim.x];
-    unsigned long long pc = 0;
+    const unsigned long long pk = kept ? pc : 0ull;
+    const unsigned long long fpre = (pk << 8) * 0x0101010101010101ull;   // byte b: items in blocks < b
+    __shared__ int bs2[8][4];
+    const int lane_ = threadIdx.x & 63;
+    int exb[8];
 #pragma unroll
-    for (int j = 0; j < N; ++j)
-      if (j < c) pc += 1ull << ((a[j] >> 8) << 3);
-    for (int b = 0; b < nb; ++b) bcnt[(int64_t)b * bld + xk] = (uint8_t)(pc >> (8 * b));
+    for (int b = 0; b < 8; ++b) {
+      exb[b] = 0;
+      if (b < nb) {
+        const int cb = (int)((pk >> (8 * b)) & 255);
+        const int incl = wave_scan_incl_dpp(cb);
+        exb[b] = incl - cb;
+        if (lane_ == 63) bs2[b][w] = incl;
+      }
+    }
+    if (lr && (int)threadIdx.x < nb) wgb[threadIdx.x] = preb[(int64_t)threadIdx.x * gridDim.x + blockIdx.x];
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      if (b < nb) {
+        for (int k = 0; k < w; ++k) exb[b] += bs2[b][k];
+        if (kept) bcnt[(int64_t)b * bld + xk] = (uint8_t)(pk >> (8 * b));
+        if (lr) {
+          const int t = exb[b] - (int)((fpre >> (8 * b)) & 255);
+          tabx[threadIdx.x * nb + b] = t;
+          if (kept && (xk & 63) == 0) lbase[(int64_t)b * ((bld + 63) >> 6) + (xk >> 6)] = wgb[b] + exb[b];
+          if (ovi >= 0) ovb[ovi * nb + b] = wgb[b] + t;
+        }
+      }
+    }
+    if (lr && mine) {
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        if (j < c) {
+          const int b = (int)(a[j] >> 8);
+          const int64_t pos = b < nb ? wgb[b] + tabx[threadIdx.x * nb + b] + j : -1;
+          if (pos >= 0 && pos < lr_cap) lr[pos] = (uint8_t)a[j];
+        }
+      }
+    }
   }
   // mid rows (staged, kCmpN < L <= 64): wave-wide bitonic sorts on the input span
   // while it is still in LDS.  Slots: rows of <= 32 tokens two per slot (one per
@@ -969,8 +1046,8 @@ __global__ __launch_bounds__(256) void k_cmp_emit(const int64_t* __restrict__ of
         if (j < c) buf[eb + j] = a[j];
     }
     {
-      // mid rows into the staged output (their rows are always staged), and their block counts
-      const int64_t bld = bcnt ? pre_rows[gridDim.x] : 0;
+      // mid rows into the staged output (their rows are always staged), and into the
+      // fused pair layout (their block counts were written with the short rows')
 #pragma unroll
       for (int t = 0; t < kCmpMidPerWave; ++t) {
         if (t < nslot) {                         // wave-uniform
@@ -978,15 +1055,13 @@ __global__ __launch_bounds__(256) void k_cmp_emit(const int64_t* __restrict__ of
           const int src = rw < 0 ? 0 : rw;
           const int idx = t < s32 ? (lane & 31) : lane;
           const int rc = __shfl(c, src, 64), reb = __shfl(eb, src, 64);
-          const int rxk = __shfl((int)xk, src, 64);
           const bool in = rw >= 0 && idx < rc;
-          if (in) buf[reb + idx] = midv[t];
-          if (bcnt) {
-            const unsigned long long half =
-                t < s32 ? ((lane >> 5) ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull) : ~0ull;
-            for (int b = 0; b < nb; ++b) {
-              const int cb = __popcll(__ballot(in && (int)(midv[t] >> 8) == b) & half);
-              if (rw >= 0 && idx == 0) bcnt[(int64_t)b * bld + rxk] = (uint8_t)cb;
+          if (in) {
+            buf[reb + idx] = midv[t];
+            if (lr) {
+              const int b = (int)(midv[t] >> 8);
+              const int64_t pos = b < nb ? wgb[b] + tabx[(w * 64 + rw) * nb + b] + idx : -1;
+              if (pos >= 0 && pos < lr_cap) lr[pos] = (uint8_t)midv[t];
             }
           }
         }
@@ -1286,19 +1361,57 @@ FA_API int fa_hip_trim_emit(const int64_t* roff, const int32_t* ranks, const int
 }
 
 // Two-pass fused compression: agg int32 [3 * nwg], hist u32 [64 * 256] striped copies (zeroed by the caller).
+// aggb (optional, nb <= 8 256-rank blocks): int32 [nb * nwg] per-workgroup block totals
+// (the fused pair layout of k_cmp_emit).
 FA_API int fa_hip_cmp_agg(const int64_t* off, const int32_t* items, const int32_t* lut, int64_t n, int32_t* agg,
-                          uint32_t* hist, hipStream_t st) {
+                          uint32_t* hist, int32_t* aggb, int nb, hipStream_t st) {
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(k_cmp_agg, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, off, items, lut, n, agg, hist);
+  if (aggb && (nb < 1 || nb > 8)) return 1;
+  hipLaunchKernelGGL(k_cmp_agg, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, off, items, lut, n, agg, hist,
+                     aggb, nb);
   FA_LAUNCH_RET();
 }
 
+// bcnt (optional, nb <= 8): u8 [nb * T] per-row block counts.  lr (optional, needs bcnt
+// and preb = the exclusive scan of fa_hip_cmp_agg's aggb, nb * nwg + 1 entries): the
+// pair kernel's blocked local-rank layout, u8 [lr_cap]; lbase: int64 [nb * ceil(T / 64)]
+// batch bases (zeroed padding past it is the caller's); ovb: int64 [rows * nb] the
+// overflow rows' segment bases, finished by fa_hip_lr_rows after the later tiers.
 FA_API int fa_hip_cmp_emit(const int64_t* off, const int32_t* items, const int32_t* lut, int64_t n,
                            const int64_t* pre_rows, const int64_t* pre_items, const int64_t* pre_over, int32_t* kept,
-                           int64_t* roff, int32_t* ranks, int32_t* over, uint8_t* bcnt, int nb, hipStream_t st) {
+                           int64_t* roff, int32_t* ranks, int32_t* over, uint8_t* bcnt, int nb, const int64_t* preb,
+                           uint8_t* lr, int64_t lr_cap, int64_t* lbase, int64_t* ovb, hipStream_t st) {
   if (n <= 0) return 0;
   if (bcnt && (nb < 1 || nb > 8)) return 1;
-  hipLaunchKernelGGL(k_cmp_emit, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, off, items, lut, n, pre_rows,
-                     pre_items, pre_over, kept, roff, ranks, over, bcnt, nb);
+  if (lr && (!bcnt || !preb || !lbase || !ovb)) return 1;
+  const size_t dyn = lr ? (size_t)256 * nb * sizeof(int32_t) : 0;
+  hipLaunchKernelGGL(k_cmp_emit, dim3((unsigned)((n + 255) / 256)), dim3(256), dyn, st, off, items, lut, n, pre_rows,
+                     pre_items, pre_over, kept, roff, ranks, over, bcnt, nb, preb, lr, lr_cap, lbase, ovb);
+  FA_LAUNCH_RET();
+}
+
+// The fused pair layout of the rows k_cmp_emit left to the later tiers (rows[i] = kept
+// row, flags: optional), thread per row over its final sorted ranks.
+__global__ __launch_bounds__(256) void k_lr_rows(const int64_t* __restrict__ roff, const int32_t* __restrict__ ranks,
+                                                 const int32_t* __restrict__ rows, int64_t nrows,
+                                                 const int64_t* __restrict__ ovb, int nb, uint8_t* __restrict__ lr,
+                                                 int64_t lr_cap) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nrows) return;
+  const int64_t x = rows[i];
+  const int64_t r0 = roff[x], r1 = roff[x + 1];
+  for (int64_t k = r0; k < r1; ++k) {
+    const int v = ranks[k];
+    const int b = v >> 8;
+    const int64_t pos = b < nb ? ovb[i * nb + b] + (k - r0) : -1;
+    if (pos >= 0 && pos < lr_cap) lr[pos] = (uint8_t)v;
+  }
+}
+
+FA_API int fa_hip_lr_rows(const int64_t* roff, const int32_t* ranks, const int32_t* rows, int64_t nrows,
+                          const int64_t* ovb, int nb, uint8_t* lr, int64_t lr_cap, hipStream_t st) {
+  if (nrows <= 0) return 0;
+  hipLaunchKernelGGL(k_lr_rows, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, st, roff, ranks, rows, nrows,
+                     ovb, nb, lr, lr_cap);
   FA_LAUNCH_RET();
 }

@@ -72,8 +72,10 @@ _HIP_SIGS = {
                                   C.c_int, dbl]),
     "fa_hip_ag_build": (C.c_int, [vp, i64, C.c_int, vp, C.c_uint32, C.c_int, vp, vp]),
     "fa_hip_ag_rows": (C.c_int, [vp, i64, C.c_int, vp, C.c_uint32, C.c_int, vp, vp, vp, vp, C.c_int, vp]),
-    "fa_hip_cmp_agg": (C.c_int, [vp, vp, vp, i64, vp, vp, vp]),
-    "fa_hip_cmp_emit": (C.c_int, [vp, vp, vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, C.c_int, vp]),
+    "fa_hip_cmp_agg": (C.c_int, [vp, vp, vp, i64, vp, vp, vp, C.c_int, vp]),
+    "fa_hip_cmp_emit": (C.c_int, [vp, vp, vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, C.c_int, vp, vp, i64, vp, vp,
+                                  vp]),
+    "fa_hip_lr_rows": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, vp, i64, vp]),
     "fa_hip_compress_regs_bc": (C.c_int, [vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, i64, C.c_int, vp]),
     "fa_hip_block_counts_rows": (C.c_int, [vp, vp, vp, i64, vp, i64, C.c_int, vp, vp]),
     "fa_hip_block_bsum": (C.c_int, [vp, i64, i64, C.c_int, vp, vp]),

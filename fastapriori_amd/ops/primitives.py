@@ -16,6 +16,7 @@ import ctypes as C
 import ctypes
 import os
 import time
+from dataclasses import dataclass
 
 import numpy as np
 import torch
@@ -234,6 +235,23 @@ def compress(offsets, items, lut, kept, roff, F1: int | None = None) -> torch.Te
 
 
 PAIR_PAD_BATCHES = 3 * 16 + 2   # the pair kernel's pipeline reads up to this many batches past a chunk
+# the emit pass of compress_rows also writes the pair kernel's blocked layout (FA_FUSED_LAYOUT=0: the
+# separate block-scatter pass of pair_counts_horizontal)
+FUSED_LAYOUT = os.environ.get("FA_FUSED_LAYOUT", "1") == "1"
+
+
+@dataclass
+class BlockLayout:
+    """The k = 2 blocked layout of compressed rows (pair_counts_horizontal): cnt = u8
+    [nb * T + pad] per-row counts of 256-rank blocks; lr / base (optional) = the local
+    ranks (u8, block-major, row order) and the int64 [nb * ceil(T / 64) + pad] 64-row
+    batch bases, written by compress_rows' emit pass (no block-scatter pass)."""
+    cnt: torch.Tensor
+    lr: torch.Tensor | None = None
+    base: torch.Tensor | None = None
+
+    def cpu(self):
+        return self.cnt.cpu()
 
 
 # rows hashed by the dedup estimate (FastApriori._want_dedup): linear counting of 2^18
@@ -261,9 +279,13 @@ def compress_rows(offsets, items, lut, F1: int, block_counts: bool = True, probe
     n = offsets.numel() - 1
     nwg = (n + 255) // 256
     st = _stream(items)
+    nb = (F1 + 255) // 256
+    blk = block_counts and 1 <= nb <= 8 and n > 0
+    fused = blk and FUSED_LAYOUT
     agg = torch.empty(3 * max(nwg, 1), dtype=_I32, device=dev)
+    aggb = torch.empty(nb * nwg, dtype=_I32, device=dev) if fused else None
     hist = torch.zeros(64, 256, dtype=_I32, device=dev)
-    _hip_call("fa_hip_cmp_agg", _p(offsets), _p(items), _p(lut), n, _p(agg), _p(hist), st)
+    _hip_call("fa_hip_cmp_agg", _p(offsets), _p(items), _p(lut), n, _p(agg), _p(hist), _p(aggb), nb, st)
     pre = torch.zeros(3, nwg + 1, dtype=_I64, device=dev)
     a3 = agg.view(-1, 3).t().to(_I64).contiguous()
     for q in range(3):   # 1-D scans (the batched innermost-dim scan is ~20x slower here)
@@ -273,12 +295,20 @@ def compress_rows(offsets, items, lut, F1: int, block_counts: bool = True, probe
     roff[0] = 0
     ranks = torch.empty(max(items.numel(), 1), dtype=_I32, device=dev)
     over = torch.empty(max(n, 1), dtype=_I32, device=dev)
-    nb = (F1 + 255) // 256
-    bcnt = None
-    if block_counts and 1 <= nb <= 8:
+    bcnt = lr = lbase = ovb = preb = None
+    lr_cap = 0
+    if blk:
         bcnt = torch.empty(nb * max(n, 1) + PAIR_PAD_BATCHES * 64 + 64, dtype=torch.uint8, device=dev)
+    if fused:
+        # block-major exclusive offsets of the per-workgroup block totals
+        preb = torch.zeros(nb * nwg + 1, dtype=_I64, device=dev)
+        torch.cumsum(aggb, 0, out=preb[1:])
+        lr_cap = max(items.numel(), 1)
+        lr = torch.empty(lr_cap + 1024, dtype=torch.uint8, device=dev)   # pad: aligned dword staging reads
+        lbase = torch.zeros(nb * ((n + 63) // 64) + PAIR_PAD_BATCHES, dtype=_I64, device=dev)
+        ovb = torch.empty(max(n, 1) * nb, dtype=_I64, device=dev)
     _hip_call("fa_hip_cmp_emit", _p(offsets), _p(items), _p(lut), n, _p(pre[0]), _p(pre[1]), _p(pre[2]), _p(kept),
-              _p(roff), _p(ranks), _p(over), _p(bcnt), nb, st)
+              _p(roff), _p(ranks), _p(over), _p(bcnt), nb, _p(preb), _p(lr), lr_cap, _p(lbase), _p(ovb), st)
     if probe is not None:
         # the kernel reads T = pre[0, -1] on the device and hashes the rows the emit
         # pass has finished (<= 16 items; the later tiers write the longer ones)
@@ -300,6 +330,20 @@ def compress_rows(offsets, items, lut, F1: int, block_counts: bool = True, probe
     if bcnt is not None:
         bcnt = bcnt[:nb * T + PAIR_PAD_BATCHES * 64 + 64]
         bcnt[nb * T:].zero_()
+        layout = BlockLayout(bcnt, lr, lbase)
+    out = kept, roff, ranks, hist_h, (layout if bcnt is not None else None)
+    if no:
+        out = _compress_rows_overflow(offsets, items, lut, F1, kept, roff, ranks, over[:no], bcnt, T, nb, st, out)
+        if lr is not None:    # the overflow rows' local ranks, after the later tiers sorted them
+            _hip_call("fa_hip_lr_rows", _p(roff), _p(ranks), _p(over), no, _p(ovb), nb, _p(lr), lr_cap, st)
+    return out
+
+
+def _compress_rows_overflow(offsets, items, lut, F1, kept, roff, ranks, over, bcnt, T, nb, st, out):
+    """The rows of more than 16 tokens compress_rows' emit pass left to the register /
+    wave / LDS tiers (and their block counts)."""
+    dev = items.device
+    no = over.numel()
     if no:
         over = over[:no]
         flag2 = torch.empty(no, dtype=torch.int8, device=dev)
@@ -317,7 +361,7 @@ def compress_rows(offsets, items, lut, F1: int, block_counts: bool = True, probe
             if bcnt is not None:
                 _hip_call("fa_hip_block_counts_rows", _p(roff), _p(ranks), _p(over), no, _p(bcnt), T, nb, _p(flag2),
                           st)
-            return kept, roff, ranks, hist_h, bcnt
+            return out
         over2 = over[torch.nonzero(flag2).flatten()].contiguous()
         n2 = over2.numel()
         if n2:
@@ -330,7 +374,7 @@ def compress_rows(offsets, items, lut, F1: int, block_counts: bool = True, probe
                 _compress_torch(offsets, items, lut, kept, roff, ranks, over3[:n3])
         if bcnt is not None and n2:       # rows of > 64 tokens, finished by the later tiers
             _hip_call("fa_hip_block_counts_rows", _p(roff), _p(ranks), _p(over2), n2, _p(bcnt), T, nb, None, st)
-    return kept, roff, ranks, hist_h, bcnt
+    return out
 
 
 def _compress_torch(offsets, items, lut, kept, roff, ranks, rows):
@@ -409,8 +453,9 @@ def pair_counts_horizontal(roff, ranks, wrow, F1: int, long_rows: bool = True, b
     the 256 x 256 packed-u16 tile kernel for unit-weight rows, or 128 x 128 u32
     tiles with row weights.  long_rows: some row may hold >= 256 items, which
     would overflow a u8 count of a 256-item block -> 128-item blocks.  bcnt: the
-    256-item block counts of these rows from compression (compress_rows), which
-    replace the counting pass.
+    256-item block counts of these rows from compression (compress_rows: a
+    BlockLayout, or its cnt tensor), which replace the counting pass; a BlockLayout
+    with the local ranks and batch bases replaces the scatter pass too.
     """
     T = roff.numel() - 1
     dev = ranks.device
@@ -425,21 +470,29 @@ def pair_counts_horizontal(roff, ranks, wrow, F1: int, long_rows: bool = True, b
             # pipeline loads up to 3 x 16 batches past a chunk unconditionally (those
             # values are never processed; padded bases must be valid lr offsets)
             pad_b = PAIR_PAD_BATCHES
-            bsum = torch.empty(nb * nbatch, dtype=_I64, device=dev)
-            if bcnt is not None and pb == 256 and bcnt.numel() >= nb * T + pad_b * 64:
-                cnt = bcnt
-                _hip_call("fa_hip_block_bsum", _p(cnt), T, T, nb, _p(bsum), st)
+            lay = bcnt if isinstance(bcnt, BlockLayout) else None
+            if lay is not None:
+                bcnt = lay.cnt
+            if (lay is not None and lay.lr is not None and pb == 256 and bcnt.numel() >= nb * T + pad_b * 64
+                    and lay.base.numel() >= nb * nbatch + pad_b):
+                # the emit pass of compress_rows wrote the whole layout
+                cnt, base, lr = bcnt, lay.base, lay.lr
             else:
-                cnt = torch.empty(nb * T + pad_b * 64, dtype=torch.uint8, device=dev)
-                cnt[nb * T:].zero_()
-                _hip_call("fa_hip_block_counts", _p(roff), _p(ranks), T, F1, _p(cnt), _p(bsum), pb, st)
-            base = torch.zeros(nb * nbatch + pad_b, dtype=_I64, device=dev)
-            torch.cumsum(bsum, 0, out=base[:nb * nbatch])
-            base[:nb * nbatch] -= bsum
-            # every rank lands in exactly one block: the layout holds all of them (no readback)
-            total = int(ranks.numel())
-            lr = torch.empty(total + 1024, dtype=torch.uint8, device=dev)   # pad: aligned dword staging reads
-            _hip_call("fa_hip_block_scatter", _p(roff), _p(ranks), T, F1, _p(cnt), _p(base), _p(lr), pb, st)
+                bsum = torch.empty(nb * nbatch, dtype=_I64, device=dev)
+                if bcnt is not None and pb == 256 and bcnt.numel() >= nb * T + pad_b * 64:
+                    cnt = bcnt
+                    _hip_call("fa_hip_block_bsum", _p(cnt), T, T, nb, _p(bsum), st)
+                else:
+                    cnt = torch.empty(nb * T + pad_b * 64, dtype=torch.uint8, device=dev)
+                    cnt[nb * T:].zero_()
+                    _hip_call("fa_hip_block_counts", _p(roff), _p(ranks), T, F1, _p(cnt), _p(bsum), pb, st)
+                base = torch.zeros(nb * nbatch + pad_b, dtype=_I64, device=dev)
+                torch.cumsum(bsum, 0, out=base[:nb * nbatch])
+                base[:nb * nbatch] -= bsum
+                # every rank lands in exactly one block: the layout holds all of them (no readback)
+                total = int(ranks.numel())
+                lr = torch.empty(total + 1024, dtype=torch.uint8, device=dev)   # pad: aligned dword staging reads
+                _hip_call("fa_hip_block_scatter", _p(roff), _p(ranks), T, F1, _p(cnt), _p(base), _p(lr), pb, st)
             if pb == 256:
                 if os.environ.get("FA_PAIR_DEBUG") != "4":   # 4: layout kernels only (benchmarks/pair_probe.py)
                     # work-queue schedule: persistent workgroups keep their tile across

@@ -433,7 +433,7 @@ def test_compress_rows_fused(n, max_len, long_rows):
     row = torch.repeat_interleave(torch.arange(T), (roff[1:] - roff[:-1]).long())
     want = torch.zeros(nb, T, dtype=torch.long)
     want.index_put_((r >> 8, row), torch.ones_like(r), accumulate=True)
-    got = bcnt.cpu()[:nb * T].view(nb, T).long()
+    got = bcnt.cnt.cpu()[:nb * T].view(nb, T).long()
     assert torch.equal(got, want.clamp(max=255))
 
 
@@ -442,10 +442,24 @@ def test_pair_counts_with_compress_block_counts(long_rows):
     # the pair layout built from the emit pass's block counts == the counting pass
     off, items, lut, F1 = _prep(n=90000, V=900, max_len=22, seed=5, long_rows=long_rows)
     kept, roff, ranks, _, bcnt = ops.compress_rows(off.to(DEV), items.to(DEV), lut.to(DEV), F1)
-    assert bcnt is not None
+    assert bcnt is not None and bcnt.lr is not None      # the emit pass wrote the whole layout
     a = ops.pair_counts_horizontal(roff, ranks, None, F1, long_rows=False, bcnt=bcnt)
+    a2 = ops.pair_counts_horizontal(roff, ranks, None, F1, long_rows=False, bcnt=bcnt.cnt)   # + scatter pass
     b = ops.pair_counts_horizontal(roff, ranks, None, F1, long_rows=False)
-    assert torch.equal(a.cpu(), b.cpu()) and int(a.sum()) > 0
+    assert torch.equal(a.cpu(), b.cpu()) and torch.equal(a2.cpu(), b.cpu()) and int(a.sum()) > 0
+    # the fused local ranks and batch bases == the block-scatter pass's
+    import fastapriori_amd.ops.primitives as prim
+    T, nb = roff.numel() - 1, (F1 + 255) // 256
+    nbatch, nnz = (T + 63) // 64, int(ranks.numel())
+    bsum = torch.empty(nb * nbatch, dtype=torch.int64, device=DEV)
+    cnt = bcnt.cnt
+    prim._hip_call("fa_hip_block_bsum", prim._p(cnt), T, T, nb, prim._p(bsum), prim._stream(ranks))
+    base = torch.cumsum(bsum, 0) - bsum
+    lr = torch.zeros(nnz + 1024, dtype=torch.uint8, device=DEV)
+    prim._hip_call("fa_hip_block_scatter", prim._p(roff), prim._p(ranks), T, F1, prim._p(cnt), prim._p(base), prim._p(lr),
+                  256, prim._stream(ranks))
+    assert torch.equal(bcnt.base[:nb * nbatch].cpu(), base.cpu())
+    assert torch.equal(bcnt.lr[:nnz].cpu(), lr[:nnz].cpu())
 
 
 @pytest.mark.parametrize("k", [3, 4, 6])
