@@ -76,7 +76,10 @@ def parse_file(path: str, byte_begin: int = 0, byte_end: int = -1, mode: int = 0
 GPU_PARSE = os.environ.get("FA_GPU_PARSE", "1") == "1"
 DEVICE_DICT = os.environ.get("FA_GPU_PARSE_DICT", "1") == "1"
 _RING_SLOT = 32 << 20
-_RING_SLOTS = 8
+# pinned slots in flight (one reader thread each, up to the host thread count): one
+# thread's pread out of the page cache runs at ~4-6 GB/s, so 8 readers held the
+# 3.9 GB T10I4D100M file at ~35 GB/s, below the ~57 GB/s of the H2D copies
+_RING_SLOTS = int(os.environ.get("FA_RING_SLOTS", "16"))
 _ring: list = []
 
 
