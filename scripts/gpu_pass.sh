@@ -7,7 +7,7 @@
 #   bash scripts/gpu_pass.sh tests [-k EXPR]    GPU tests (optionally a subset)
 #   bash scripts/gpu_pass.sh bench              the bench line of every BASELINE config + the 12.5M-row shard
 #   bash scripts/gpu_pass.sh kernels            rocprofv3 kernel stats of T10I4D100M and T40I10D100M
-#   bash scripts/gpu_pass.sh pmc [REGEX] [CFG]  two PMC passes (one counter set each) of the matching kernels
+#   bash scripts/gpu_pass.sh pmc [REGEX] [CFG]  four PMC passes (SQ sets, FETCH_SIZE, WRITE_SIZE) of the matching kernels
 #   bash scripts/gpu_pass.sh trace [CFG]        kernel + roctx marker trace (benchmarks/gap_attrib.py: GPU idle by host range)
 #   bash scripts/gpu_pass.sh e2e                the reference window's breakdown (benchmarks/e2e_probe.py) + its kernel stats
 #   bash scripts/gpu_pass.sh multirank          8 gloo ranks sharing the GPU: collectives per run (benchmarks/multirank_probe.py)
@@ -60,6 +60,13 @@ case "$MODE" in
     timeout -s KILL 200 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_VMEM SQ_WAVES GRBM_GUI_ACTIVE \
       --kernel-include-regex "$RX" --output-format csv -d "$O/b" -o run -- \
       python3 "$R/bench.py" --config "$CFG" --steps 1 --warmup 0 --e2e off > "$O/b.log" 2>&1
+    # HBM bytes (FETCH_SIZE takes 3 of the 4 TCC counters, WRITE_SIZE 2: one pass each)
+    timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE SQ_WAVES GRBM_GUI_ACTIVE \
+      --kernel-include-regex "$RX" --output-format csv -d "$O/c" -o run -- \
+      python3 "$R/bench.py" --config "$CFG" --steps 1 --warmup 0 --e2e off > "$O/c.log" 2>&1
+    timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE SQ_WAVES GRBM_GUI_ACTIVE \
+      --kernel-include-regex "$RX" --output-format csv -d "$O/d" -o run -- \
+      python3 "$R/bench.py" --config "$CFG" --steps 1 --warmup 0 --e2e off > "$O/d.log" 2>&1
     ;;
   trace)
     CFG=${1:-T10I4D100M}

@@ -294,6 +294,8 @@ def test_slab_class_layout_on_gpu(monkeypatch, lds_kb, dense):
     sh = generate_shard(60000, Comm(), "cpu", 14.0, 6.0, 300, 120, seed=11)
     cfg = dict(min_support=0.004, dedup="off")
     ref = FastApriori(0.004, config=MinerConfig(trim_min_rows=0, level_kernel="bitmap", **cfg)).run(sh)
+    import fastapriori_amd.models.apriori as ap
+    monkeypatch.setattr(ap, "DEVICE_LEVELS", False)    # the host plans (device plans: test_gpu_device_levels)
     monkeypatch.setattr(prim, "SLAB_CLS", 2)
     monkeypatch.setattr(prim, "_LDS_BYTES", lds_kb * 1024 - 512)
     if dense:   # every level "dense": the slab kernel runs without its all-zero-prefix test
