@@ -452,7 +452,9 @@ class FastApriori:
         room for all of them when the bounded generation stopped short, the level's
         rows trimmed as the host loop would, then counted window by window from the used
         items' bitmap (ops.primitives.dl_count_multipass).  Returns (control block,
-        int32 counts [C] on the device) or None (no slab width fits: host loop)."""
+        int32 counts [C] on the device) or None (FA_DL_MULTI=0: the host loop).  When
+        not even 4-word slabs of the used items fit the LDS (wide levels: thousands of
+        used items), the level is counted by the bitmap kernel instead (_dl_bitmap_count)."""
         Pm = ops.primitives
         if not DL_MULTI or self.cfg.max_level and k > self.cfg.max_level:
             return None
@@ -466,10 +468,14 @@ class FastApriori:
         bits = np.unpackbits(c[Pm.DL_BITS:Pm.DL_BITS + nwd].view(np.uint8), bitorder="little")[:F1]
         used = np.flatnonzero(bits)
         n_used = int(used.size)
-        if Pm.dl_slab_width(n_used, min(C0, 8192), lds)[0] == 0:
-            return None
+        wide = Pm.dl_slab_width(n_used, min(C0, 8192), lds)[0] == 0
         with self._timer.phase(f"trim{k}"), roctx_range("trim"):
             self._trim(db, used, k, C0)
+        if wide:
+            with self._timer.phase("count"), roctx_range("count_bitmap"):
+                cnt = self._dl_bitmap_count(S, db, used)
+            self.stats["device_bitmap_levels"] = self.stats.get("device_bitmap_levels", 0) + 1
+            return c, cnt
         with self._timer.phase("count"), roctx_range("count_multi"):
             bm, bmap = self._bitmaps(db, used)
             used_t = torch.from_numpy(used.astype(np.int64)).to(self._dev)
@@ -481,6 +487,35 @@ class FastApriori:
             return None
         self.stats["device_multipass"] = self.stats.get("device_multipass", 0) + 1
         return c, cnt
+
+    def _dl_bitmap_count(self, S, db, used: np.ndarray) -> torch.Tensor:
+        """Counts (int32 [C], bundle order) of the device bundle's single level from the
+        used items' bitmap with the bitmap kernel (ops.count_candidates: every group's
+        prefix ANDed once per word tile, FastApriori.scala:143-154): the candidate rows
+        are read where the generator wrote them (its workspace), grouped by prefix on
+        the device; one readback of the group offsets."""
+        Pm = ops.primitives
+        m, C = int(S.desc[0, 4]), int(S.desc[0, 6])
+        off = int(S.desc[0, 3]) - S.ws.data_ptr()
+        if off < 0 or off % 4 or off + 4 * C * (m + 1) > S.ws.numel():
+            raise RuntimeError("device bundle: candidate rows outside the generator workspace")
+        rows = S.ws[off:off + 4 * C * (m + 1)].view(torch.int32).view(C, m + 1)
+        pre, ext = rows[:, :m], rows[:, m]
+        starts = torch.zeros(1, dtype=torch.int64, device=self._dev)
+        if C > 1:
+            starts = torch.cat([starts, torch.nonzero((pre[1:] != pre[:-1]).any(1)).flatten() + 1])
+        gs = starts.cpu().numpy()
+        ext_off = np.append(gs, C).astype(np.int64)
+        bm, bmap = self._bitmaps(db, used)
+        prefix = pre[starts].to(torch.int64)
+        ext64 = ext.to(torch.int64)
+        if bmap is not None:
+            prefix, ext64 = bmap[prefix], bmap[ext64]
+        cnt = ops.count_candidates(bm, db["W"], prefix.to(torch.int32).contiguous(), ext_off,
+                                   ext64.to(torch.int32).contiguous(), db["wword"])
+        Pm.LAST_LEVEL_PLAN.clear()
+        Pm.LAST_LEVEL_PLAN.update(kernel="bitmap_dev", rows=int(db["roff"].numel() - 1), used=int(used.size), C=C, m=m)
+        return cnt.to(torch.int32)
 
     def _dl_post_setup(self, S, db, k: int, F1: int, c_bound: int, n_bound: int, lds: int) -> None:
         """Fill the post step of fa_hip_dl_more (ops.primitives.DlPostC): buffers, the

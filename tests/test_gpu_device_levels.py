@@ -77,13 +77,20 @@ def test_multipass_level_stays_on_device(monkeypatch):
     _same(got2, ref)
 
 
+def _multipass_lds(ref) -> int:
+    """An LDS budget in which F1 used items fit 4-word slabs (slab rows 48 B) with room
+    for ~|F_3| / 4 accumulators: level 3 then needs several passes."""
+    F1, F3 = len(ref.levels[0]), len(ref.levels[2])
+    return F1 * 48 + 4 * max(1024, F3 // 4) + 2 * F1 + 256
+
+
 def test_small_lds_forces_device_multipass(monkeypatch):
     # a shrunk LDS budget turns T10I4 levels into multi-pass ones: windows, trimming and
     # the used items' bitmap on the unit and the weighted (dedup) layout
     import fastapriori_amd.ops.primitives as prim
     cpu = generate_shard(200_000, Comm(), "cpu", 10.0, 4.0, 2000, 1000, 4)
     ref, _ = _mine(cpu, 0.002)
-    monkeypatch.setattr(prim, "_LDS_BYTES", 24 * 1024)
+    monkeypatch.setattr(prim, "_LDS_BYTES", _multipass_lds(ref))
     for dd in ("off", "on"):
         got, st = _mine(cpu.to(DEV), 0.002, dedup=dd, trim_min_rows=0)
         assert st.get("device_multipass", 0) >= 1, st
@@ -101,23 +108,23 @@ def test_deep_database_all_levels_on_device():
     _same(got, ref)
 
 
-@pytest.mark.parametrize("min_m,lds_kb", [(2.0, None), (2.0, 24), (0.0, None)])
-def test_device_class_layout(monkeypatch, min_m, lds_kb):
+@pytest.mark.parametrize("min_m,small_lds", [(2.0, False), (2.0, True), (0.0, False)])
+def test_device_class_layout(monkeypatch, min_m, small_lds):
     # the class layout of device plans (levels.hip fa_hip_dl_plan_ex: sibling runs on one
     # thread, idle-padded wave rows) on every level (mean prefix >= 2), also window by
     # window on multi-pass levels (shrunk LDS); 0 = never (the size-sorted plan)
     import fastapriori_amd.ops.primitives as prim
     monkeypatch.setattr(prim, "DL_CLS_MIN_M", min_m)
     prim._DL_STATE.clear()
-    if lds_kb:
-        monkeypatch.setattr(prim, "_LDS_BYTES", lds_kb * 1024)
     cpu = generate_shard(120_000, Comm(), "cpu", 40.0, 10.0, 2000, 1000, 3)
     ref, _ = _mine(cpu, 0.006)
+    if small_lds:
+        monkeypatch.setattr(prim, "_LDS_BYTES", _multipass_lds(ref))
     before = prim.CLS_LEVELS[0]
     got, st = _mine(cpu.to(DEV), 0.006)
     assert st.get("host_levels", 0) == 0 and "fallbacks" not in st, st
     assert (prim.CLS_LEVELS[0] > before) == (min_m > 0)
-    if lds_kb:
+    if small_lds:
         assert st.get("device_multipass", 0) >= 1, st
     _same(got, ref)
     prim._DL_STATE.clear()
