@@ -978,21 +978,17 @@ struct DlPost {
   int64_t done, sw, cap, n_wg, C, trim;
   // prefix slab rows of levels with prefixes past 12 ids (levels.hip gpre), int32 [gpre_cap]
   int32_t* gpre; int64_t gpre_cap;
-  // class layout (levels.hip fa_hip_dl_plan_ex): scratch int64 [cls_cap], the mean prefix
-  // length from which it is used (0: never), and (out) whether the plan took it
-  int64_t* cls; int64_t cls_cap; double cls_min_m; int64_t cls_used;
 };
-static_assert(sizeof(DlPost) == 34 * 8, "DlPost layout (ops.primitives.DlPostC)");
+static_assert(sizeof(DlPost) == 30 * 8, "DlPost layout (ops.primitives.DlPostC)");
 
-FA_API int fa_hip_dl_plan_ex(const int64_t* desc, int L, long long* ctl, int F1, int32_t* item_map, void* rec,
-                             int64_t rec_cap, int32_t* part, int64_t part_cap, int32_t* gpre, int64_t gpre_cap,
-                             int64_t w0, int64_t w1, int64_t* cls_scr, int64_t cls_cap, double cls_min_m,
-                             int64_t n_used, hipStream_t st, int64_t* used_cls);
-FA_API int fa_hip_count_slab_rec_cls(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
-                                     const int32_t* item_map, int F1, int n_used, const int32_t* gpre,
-                                     const void* rec, int G, int C, const int32_t* wword, uint32_t* out, int sw,
-                                     int n_wg, const uint64_t* bm, int64_t Wp, hipStream_t st,
-                                     const int32_t* bm_rows, const int32_t* g_dev, int cls);
+FA_API int fa_hip_dl_plan(const int64_t* desc, int L, long long* ctl, int F1, int32_t* item_map, void* rec,
+                          int64_t max_pieces, int32_t* part, int64_t part_cap, int32_t* gpre, int64_t gpre_cap,
+                          hipStream_t st);
+FA_API int fa_hip_count_slab_rec(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
+                                 const int32_t* item_map, int F1, int n_used, const int32_t* gpre, const void* rec,
+                                 int G, int C, const int32_t* wword, uint32_t* out, int sw, int n_wg,
+                                 const uint64_t* bm, int64_t Wp, hipStream_t st, const int32_t* bm_rows,
+                                 const int32_t* g_dev);
 
 // P[Binom(L, p) >= k] (the regularised incomplete beta of FastApriori._trim_worth_it)
 static double binom_tail(int L, double p, int k) {
@@ -1026,10 +1022,8 @@ static void dl_post(DlPost* P, const int64_t* desc, int L, long long* ctl, const
     if (cap >= std::min<int64_t>(C, 8192) || (w == 4 && cap >= 1024)) { sw = w; break; }
   }
   if (sw == 0 || C > cap) return;
-  P->cls_used = 0;
-  if (fa_hip_dl_plan_ex(desc, L, ctl, F1, P->item_map, P->rec, P->rec_cap, P->part, P->part_cap, P->gpre,
-                        P->gpre_cap, 0, -1, P->wword ? nullptr : P->cls, P->cls_cap, P->cls_min_m, n_used, st,
-                        &P->cls_used) != 0)
+  if (fa_hip_dl_plan(desc, L, ctl, F1, P->item_map, P->rec, C, P->part, P->part_cap, P->gpre, P->gpre_cap,
+                     st) != 0)
     return;                                        // (e.g. long prefixes past gpre_cap: the caller plans)
   (void)hipMemsetAsync(P->out, 0, 4 * (size_t)C, st);
   P->sw = sw;
@@ -1067,9 +1061,9 @@ static void dl_post(DlPost* P, const int64_t* desc, int L, long long* ctl, const
   const int64_t lds_k = n_used * (sw + 2) * 8 + ((C + 3) & ~(int64_t)3) * 4 + map_b;
   const int64_t per_cu = std::min<int64_t>(std::max<int64_t>(1, (int64_t)P->lds_kernel / std::max<int64_t>(lds_k, 1)), 2);
   P->n_wg = std::max<int64_t>(1, std::min<int64_t>(nslabs, 256 * per_cu));
-  if (fa_hip_count_slab_rec_cls(P->roff, P->ranks, P->src, P->ncols, P->item_map, F1, (int)n_used, P->gpre, P->rec,
-                                0, (int)C, P->wword, P->out, sw, (int)P->n_wg, nullptr, 0, st, nullptr,
-                                reinterpret_cast<const int32_t*>(ctl + 221), P->cls_used ? 1 : 0) != 0)
+  if (fa_hip_count_slab_rec(P->roff, P->ranks, P->src, P->ncols, P->item_map, F1, (int)n_used, P->gpre, P->rec, 0,
+                            (int)C, P->wword, P->out, sw, (int)P->n_wg, nullptr, 0, st, nullptr,
+                            reinterpret_cast<const int32_t*>(ctl + 221)) != 0)
     return;
   P->done = 2;
 }

@@ -229,249 +229,6 @@ __global__ __launch_bounds__(kDlPB) void k_dl_pieces_emit(const DlLevels D, cons
   if (rem) dl_write_rec(rec, slot[rem], cand + 8 * full, rem, m, ids, ex + 8 * full, item_map, goff);
 }
 
-// ---------------------------------------------------------------------------
-// Class layout of a device plan (the kCls records of k_count_slab_rec; plan.cpp
-// cls_layout is the host version).  Deep levels spend their counting on prefix
-// rows (T40I10D100M level 9: ~8 prefix rows and ~2 extensions per piece).
-// Sibling parent rows -- the same first m-1 items, consecutive in the generator's
-// lexicographic order -- form a class; a class's pieces, in order, are cut into
-// runs of <= kDlRun, and a run executes on one thread in consecutive steps: its
-// first piece ANDs the prefix (kept as q = first m-1 rows and p = q & last row),
-// the next ones keep q (flag 1) and, within one parent row, p (flag 2).  Runs are
-// ordered by length (8 first; lexicographic within a length), 64 runs of one length
-// make a wave row of `length` steps, and wave rows go round-robin to the 16 waves
-// (sorted by length, so no wave carries more than 8 steps over another).  Slot
-// (step t, wave w, lane) = t * 1024 + w * 64 + lane; unused slots hold idle records
-// (no extensions, keep both).  Four kernels: per row (piece count, class start),
-// one workgroup scanning the rows (pieces before each row in its class, class
-// totals, run ordinals, the layout's wave rows), idle fill, per row emit.
-// ---------------------------------------------------------------------------
-constexpr int kDlRun = 8;            // pieces per run (plan.cpp kClsMaxRun)
-constexpr int kDlClsPad = 16384;     // slots a class layout adds to its pieces at most (see fa_hip_dl_plan_ex)
-
-// scratch layout (int64 units) for R rows: np int32 [R], cs int32 [R] (one int64 [R]
-// span), sx int64 [R], st | ctot int32 [R] each (one span), ob8 int64 [R], obp | pad
-// int32 [R] (one span), lay int64 [64]
-struct DlCls {
-  int32_t* np; int32_t* cs; int64_t* sx; int32_t* st; int32_t* ctot; int64_t* ob8; int32_t* obp; int64_t* lay;
-};
-static DlCls dl_cls_view(int64_t* scr, int64_t R) {
-  DlCls X;
-  X.np = reinterpret_cast<int32_t*>(scr);
-  X.cs = X.np + R;
-  X.sx = scr + R;
-  X.st = reinterpret_cast<int32_t*>(scr + 2 * R);
-  X.ctot = X.st + R;
-  X.ob8 = scr + 3 * R;
-  X.obp = reinterpret_cast<int32_t*>(scr + 4 * R);
-  X.lay = scr + 5 * R;
-  return X;
-}
-// lay: [0..8] runs of length s (index s), [10..18] first wave row of bucket s, [20..28]
-// wave rows of bucket s, [30] steps, [31] slots
-
-__global__ __launch_bounds__(kDlPB) void k_dl_cls_rows(const DlLevels D, DlCls X) {
-  const int64_t R = D.rbase[D.L];
-  const int64_t t = (int64_t)blockIdx.x * kDlPB + threadIdx.x;
-  if (t >= R) return;
-  const int l = dl_level_of(D, t);
-  const int64_t i = t - D.rbase[l];
-  const int m = D.m[l];
-  X.np[t] = (dl_row_count(D, t, R) + 7) >> 3;
-  int start = i == 0;
-  if (!start) {
-    const int32_t* x = D.P[l] + i * m;
-    for (int q = 0; q + 1 < m; ++q)
-      if (x[q] != x[q - m]) { start = 1; break; }
-  }
-  X.cs[t] = start;
-}
-
-// workgroup-wide inclusive scan (1024 threads) of an int64 value; total into *tot
-__device__ __forceinline__ int64_t dl_block_scan64(int64_t v, int64_t* wsum, int64_t* tot) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  int64_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int64_t y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) wsum[wv] = x;
-  __syncthreads();
-  int64_t before = 0, all = 0;
-  for (int q = 0; q < 16; ++q) {
-    const int64_t w = wsum[q];
-    if (q < wv) before += w;
-    all += w;
-  }
-  __syncthreads();
-  *tot = all;
-  return before + x;
-}
-
-__device__ __forceinline__ int64_t dl_block_max64(int64_t v, int64_t* wsum) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  int64_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int64_t y = __shfl_up(x, o, 64);
-    if (lane >= o) x = max(x, y);
-  }
-  if (lane == 63) wsum[wv] = x;
-  __syncthreads();
-  int64_t before = -1;
-  for (int q = 0; q < wv; ++q) before = max(before, wsum[q]);
-  __syncthreads();
-  return max(before, x);
-}
-
-// number of r in [0, n) with r % 16 == w (n >= 0)
-__device__ __forceinline__ int64_t dl_mod_count(int64_t n, int w) { return (n + 15 - w) / 16; }
-
-__global__ __launch_bounds__(1024) void k_dl_cls_scan(const DlLevels D, DlCls X, long long* __restrict__ c,
-                                                      int64_t slot_cap) {
-  __shared__ int64_t wsum[16];
-  __shared__ int64_t carry[12];    // 0 pieces, 1 class start, 2 full runs, 3..9 partial runs of length 1..7
-  const int64_t R = D.rbase[D.L];
-  if (threadIdx.x < 12) carry[threadIdx.x] = 0;
-  __syncthreads();
-  // pass 1: exclusive piece prefix and class start row of every row
-  for (int64_t b0 = 0; b0 < R; b0 += 1024) {
-    const int64_t t = b0 + threadIdx.x;
-    const int64_t v = t < R ? X.np[t] : 0;
-    const int64_t f = t < R && X.cs[t] ? t : -1;
-    const int64_t c0 = carry[0], c1 = carry[1];
-    int64_t tot;
-    const int64_t incl = dl_block_scan64(v, wsum, &tot);
-    const int64_t mx = dl_block_max64(f, wsum);
-    if (t < R) {
-      X.sx[t] = c0 + incl - v;
-      X.st[t] = (int32_t)max(mx, c1);
-    }
-    __syncthreads();
-    if (threadIdx.x == 1023) { carry[0] = c0 + tot; carry[1] = max(mx, c1); }
-    __syncthreads();
-  }
-  // pass 2: class totals (at the class's last row) and run ordinals per class
-  if (threadIdx.x < 12 && threadIdx.x != 0 && threadIdx.x != 1) carry[threadIdx.x] = 0;
-  __syncthreads();
-  for (int64_t b0 = 0; b0 < R; b0 += 1024) {
-    const int64_t t = b0 + threadIdx.x;
-    int64_t tot = 0;
-    int32_t s = 0;
-    const bool end = t < R && (t + 1 == R || X.cs[t + 1]);
-    if (end) {
-      s = X.st[t];
-      tot = X.sx[t] + X.np[t] - X.sx[s];
-      X.ctot[s] = (int32_t)tot;
-    }
-    const int64_t full = tot / kDlRun;
-    const int part = (int)(tot % kDlRun);
-    int64_t dummy;
-    const int64_t cf = carry[2];
-    const int64_t inf = dl_block_scan64(full, wsum, &dummy);
-    if (end) X.ob8[s] = cf + inf - full;
-    int64_t cp[kDlRun];
-#pragma unroll
-    for (int q = 1; q < kDlRun; ++q) cp[q] = carry[2 + q];
-    int64_t newc[kDlRun];
-    int64_t tots[kDlRun];
-#pragma unroll
-    for (int q = 1; q < kDlRun; ++q) {
-      const int64_t ind = part == q ? 1 : 0;
-      const int64_t inq = dl_block_scan64(ind, wsum, &tots[q]);
-      if (end && part == q) X.obp[s] = (int32_t)(cp[q] + inq - 1);
-      newc[q] = cp[q] + tots[q];
-    }
-    if (threadIdx.x == 1023) {
-      carry[2] = cf + inf;
-#pragma unroll
-      for (int q = 1; q < kDlRun; ++q) carry[2 + q] = newc[q];
-    }
-    __syncthreads();
-  }
-  // the layout: wave rows of each length bucket (8 first), loads per wave, slots
-  if (threadIdx.x == 0) {
-    int64_t* lay = X.lay;
-    int64_t wr = 0;
-    for (int sl = kDlRun; sl >= 1; --sl) {
-      const int64_t n = sl == kDlRun ? carry[2] : carry[2 + sl];
-      lay[sl] = n;
-      lay[10 + sl] = wr;
-      lay[20 + sl] = (n + 63) / 64;
-      wr += lay[20 + sl];
-    }
-    int64_t steps = 0;
-    for (int w = 0; w < 16; ++w) {
-      int64_t ld = 0;
-      for (int sl = 1; sl <= kDlRun; ++sl)
-        ld += sl * (dl_mod_count(lay[10 + sl] + lay[20 + sl], w) - dl_mod_count(lay[10 + sl], w));
-      steps = max(steps, ld);
-    }
-    int64_t G = steps * 1024;
-    if (G > slot_cap) G = 0;                       // (cannot happen: slot_cap >= pieces + kDlClsPad)
-    lay[30] = steps;
-    lay[31] = G;
-    c[220] = G;
-    reinterpret_cast<int32_t*>(c + 221)[0] = (int32_t)G;
-  }
-}
-
-__global__ __launch_bounds__(256) void k_dl_cls_fill(DlCls X, int4* __restrict__ rec, int64_t slot_cap) {
-  const int64_t G = X.lay[31];
-  const int4 idle = make_int4(0, 3 << 17, 0, 0), z = make_int4(0, 0, 0, 0);
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < G && i < slot_cap; i += (int64_t)gridDim.x * 256) {
-    rec[3 * i] = idle; rec[3 * i + 1] = z; rec[3 * i + 2] = z;
-  }
-}
-
-__global__ __launch_bounds__(kDlPB) void k_dl_cls_emit(const DlLevels D, DlCls X, const int32_t* __restrict__ item_map,
-                                                       int4* __restrict__ rec, int64_t slot_cap) {
-  const int64_t R = D.rbase[D.L];
-  const int64_t t = (int64_t)blockIdx.x * kDlPB + threadIdx.x;
-  if (t >= R) return;
-  int64_t first = 0;
-  const int cc = dl_row_window(D, t, R, &first);
-  if (cc == 0) return;
-  const int64_t* lay = X.lay;
-  const int l = dl_level_of(D, t);
-  const int64_t i = t - D.rbase[l];
-  const int m = D.m[l];
-  const int32_t* x = D.P[l] + i * m;
-  int ids[12];
-#pragma unroll
-  for (int q = 0; q < 12; ++q) ids[q] = q < m ? item_map[x[q]] : 0;
-  const int last = item_map[x[m - 1]];
-  const int64_t o = D.off[l][i] + (first - (D.base[l] + D.off[l][i]));
-  const int32_t* ex = D.cnt[l] + D.n[l] + o;
-  const int64_t cand = first - D.w0;
-  const int32_t s = X.st[t];
-  const int64_t tot = X.ctot[s], cp = X.sx[t] - X.sx[s];
-  const int64_t full = tot / kDlRun;
-  const int np = (cc + 7) >> 3;
-  for (int j = 0; j < np; ++j) {
-    const int64_t ci = cp + j, r = ci / kDlRun;
-    const int pos = (int)(ci % kDlRun);
-    const int len = r < full ? kDlRun : (int)(tot % kDlRun);
-    const int64_t ord = r < full ? X.ob8[s] + r : (int64_t)X.obp[s];
-    const int64_t WR = lay[10 + len] + ord / 64;
-    const int lane = (int)(ord % 64), wave = (int)(WR % 16);
-    int64_t step = pos;
-    for (int sl = kDlRun; sl >= 1; --sl) {       // wave rows before WR on this wave, by bucket
-      const int64_t a = lay[10 + sl], b = min(a + lay[20 + sl], WR);
-      if (b > a) step += sl * (dl_mod_count(b, wave) - dl_mod_count(a, wave));
-    }
-    const int64_t slot = step * 1024 + wave * 64 + lane;
-    if (slot >= slot_cap) continue;
-    const int n_ext = min(8, cc - 8 * j);
-    dl_write_rec(rec, slot, cand + 8 * j, n_ext, m, ids, ex + 8 * j, item_map, -1);
-    const int fl = pos == 0 ? 0 : (1 | (j > 0 ? 2 : 0));
-    int4 a = rec[3 * slot];
-    a.y |= (fl << 17) | (last << 19);
-    rec[3 * slot] = a;
-  }
-}
-
 // keep support >= mc (FastApriori.scala:152-154): per level, the kept candidate rows
 // and counts in candidate order (lexicographic, as the rows were generated), their
 // number into fsz[l].  One workgroup; a bundle holds at most one accumulator pass
@@ -595,57 +352,6 @@ FA_API int fa_hip_dl_plan_window(const int64_t* desc, int L, long long* ctl, int
   hipLaunchKernelGGL(k_dl_pieces_scan, dim3(1), dim3(1024), 0, st, part, nblk, ctl);
   hipLaunchKernelGGL(k_dl_pieces_emit, dim3((unsigned)nblk), dim3(kDlPB), 0, st, D, part, item_map,
                      static_cast<int4*>(rec));
-  FA_LAUNCH_RET();
-}
-
-// int64 entries of the class-layout scratch of a bundle's levels (dl_cls_view)
-FA_API int64_t fa_hip_dl_cls_need(const int64_t* desc, int L) {
-  int64_t R = 0;
-  for (int l = 0; l < L; ++l) R += desc[8 * l + 5];
-  return 5 * R + 64;
-}
-
-// The slab plan of candidates [w0, w1) (w1 < 0: all) in the class layout when it
-// applies -- unit weights (the caller's), every prefix 2..12 items, n_used < 8192
-// (the record's 13-bit last-prefix id), the candidate-weighted mean prefix length
-// >= cls_min_m (> 0), cls_scr of fa_hip_dl_cls_need entries and room for the padded
-// slots (rec_cap >= candidates + kDlClsPad) -- else the size-sorted plan of
-// fa_hip_dl_plan_window.  *used_cls = 1 when the class layout was queued: the count
-// must then run k_count_slab_rec<.., kCls> (fa_hip_count_slab_rec_cls mode 1).
-FA_API int fa_hip_dl_plan_ex(const int64_t* desc, int L, long long* ctl, int F1, int32_t* item_map, void* rec,
-                             int64_t rec_cap, int32_t* part, int64_t part_cap, int32_t* gpre, int64_t gpre_cap,
-                             int64_t w0, int64_t w1, int64_t* cls_scr, int64_t cls_cap, double cls_min_m,
-                             int64_t n_used, hipStream_t st, int64_t* used_cls) {
-  *used_cls = 0;
-  DlLevels D;
-  if (dl_levels(desc, L, &D, nullptr, -1)) return 1;
-  int64_t C = 0;
-  double msum = 0.0;
-  bool ok = cls_scr != nullptr && cls_min_m > 0.0 && n_used > 0 && n_used < 8192 && F1 >= 1 && F1 <= 32768;
-  for (int l = 0; l < L; ++l) {
-    C += D.C[l];
-    msum += (double)D.C[l] * D.m[l];
-    ok = ok && D.m[l] >= 2 && D.m[l] <= kDlInline;
-  }
-  D.w0 = w0 < 0 ? 0 : w0;
-  D.w1 = w1 < 0 ? C : std::min(w1, C);
-  ok = ok && C > 0 && msum >= cls_min_m * (double)C && D.w1 > D.w0 && rec_cap >= (D.w1 - D.w0) + kDlClsPad &&
-       cls_cap >= fa_hip_dl_cls_need(desc, L);
-  if (!ok)
-    return fa_hip_dl_plan_window(desc, L, ctl, F1, item_map, rec, rec_cap, part, part_cap, gpre, gpre_cap, w0, w1,
-                                 st);
-  const int64_t R = D.rbase[L];
-  const int64_t nblk = std::max<int64_t>(1, (R + kDlPB - 1) / kDlPB);
-  const DlCls X = dl_cls_view(cls_scr, R);
-  hipLaunchKernelGGL(k_dl_map, dim3(1), dim3(64), 0, st, ctl, F1, item_map);
-  hipLaunchKernelGGL(k_dl_cls_rows, dim3((unsigned)nblk), dim3(kDlPB), 0, st, D, X);
-  hipLaunchKernelGGL(k_dl_cls_scan, dim3(1), dim3(1024), 0, st, D, X, ctl, rec_cap);
-  const int64_t fb = std::min<int64_t>(4096, (rec_cap + 255) / 256);
-  hipLaunchKernelGGL(k_dl_cls_fill, dim3((unsigned)std::max<int64_t>(fb, 1)), dim3(256), 0, st, X,
-                     static_cast<int4*>(rec), rec_cap);
-  hipLaunchKernelGGL(k_dl_cls_emit, dim3((unsigned)nblk), dim3(kDlPB), 0, st, D, X, item_map, static_cast<int4*>(rec),
-                     rec_cap);
-  *used_cls = 1;
   FA_LAUNCH_RET();
 }
 

@@ -531,8 +531,6 @@ class FastApriori:
                                             b["out"].data_ptr())
         P.rec_cap, P.part_cap, P.out_cap = b["c_cap"], b["part"].numel(), b["c_cap"]
         P.gpre, P.gpre_cap = b["gpre"].data_ptr(), b["gpre"].numel()
-        P.rec_cap = b["slots"]
-        P.cls, P.cls_cap, P.cls_min_m = b["cls"].data_ptr(), b["cls"].numel(), float(Pm.DL_CLS_MIN_M)
         P.roff, P.ranks = db["roff"].data_ptr(), db["ranks"].data_ptr()
         P.src = db["src"].data_ptr() if db["src"] is not None else None
         P.wword = db["wword"].data_ptr() if db["wword"] is not None else None

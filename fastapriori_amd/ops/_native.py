@@ -90,9 +90,6 @@ _HIP_SIGS = {
     "fa_hip_dl_more": (C.c_int, [C.c_int, vp, i64, i64, vp, vp, dbl, C.c_int, dbl, i64, vp, vp, vp, vp]),
     "fa_hip_dl_plan": (C.c_int, [vp, C.c_int, vp, C.c_int, vp, vp, i64, vp, i64, vp, i64, vp]),
     "fa_hip_dl_gpre_need": (i64, [vp, C.c_int]),
-    "fa_hip_dl_cls_need": (i64, [vp, C.c_int]),
-    "fa_hip_dl_plan_ex": (C.c_int, [vp, C.c_int, vp, C.c_int, vp, vp, i64, vp, i64, vp, i64, i64, i64, vp, i64,
-                                    C.c_double, i64, vp, vp]),
     "fa_hip_dl_plan_window": (C.c_int, [vp, C.c_int, vp, C.c_int, vp, vp, i64, vp, i64, vp, i64, i64, i64, vp]),
     "fa_hip_dl_threshold": (C.c_int, [vp, C.c_int, vp, i64, vp, vp, vp, vp, vp, vp]),
     "fa_hip_trim_scan_count": (C.c_int, [vp, vp, i64, vp, C.c_int, C.c_int, vp, vp, vp, vp, vp]),

@@ -1398,10 +1398,6 @@ DL_BITS = 512           # gen.hip kDlBits: the control block's used-item bitset 
 DL_MAX_F1 = 32768       # its bits (and the generator's 8 bitset words per lane)
 DL_MAX_M = 40           # levels.hip kDlMaxM (prefixes past 12 ids go through gpre)
 DL_MAX_LEVELS = 31
-# device plans take the class layout (levels.hip fa_hip_dl_plan_ex) from this candidate-
-# weighted mean prefix length on (0: never); the slots it pads its pieces with at most
-DL_CLS_MIN_M = float(os.environ.get("FA_DL_CLS_MIN_M", "5"))
-DL_CLS_PAD = 16384
 
 
 class DlPostC(ctypes.Structure):
@@ -1414,9 +1410,7 @@ class DlPostC(ctypes.Structure):
                [(n, ctypes.c_void_p) for n in ("c1", "alive", "len_hist")] + \
                [(n, ctypes.c_int64) for n in ("T", "nnz", "trim_min_rows", "trim_ok", "k",
                                                "done", "sw", "cap", "n_wg", "C", "trim")] + \
-               [("gpre", ctypes.c_void_p), ("gpre_cap", ctypes.c_int64)] + \
-               [("cls", ctypes.c_void_p), ("cls_cap", ctypes.c_int64), ("cls_min_m", ctypes.c_double),
-                ("cls_used", ctypes.c_int64)]
+               [("gpre", ctypes.c_void_p), ("gpre_cap", ctypes.c_int64)]
 
 
 class DeviceLevelState:
@@ -1442,25 +1436,21 @@ class DeviceLevelState:
 
     def post_buffers(self, F1: int, c_cap: int, rows_cap: int, gpre_n: int = 0):
         """Grow-only plan / count buffers of the post step: item_map [F1], piece
-        records [c_cap + DL_CLS_PAD slots], planner scratch for rows_cap parent rows
-        (size-sorted and class layouts), counts [c_cap], long-prefix slab rows [gpre_n]."""
+        records [c_cap], planner scratch for rows_cap parent rows, counts [c_cap],
+        long-prefix slab rows [gpre_n]."""
         part_n = 8 * ((rows_cap + 255) // 256 + 2)
-        cls_n = 5 * rows_cap + 64 if DL_CLS_MIN_M > 0 else 1
         b = self.post_bufs
         if (b is None or b["F1"] < F1 or b["c_cap"] < c_cap or b["part"].numel() < part_n
-                or b["gpre"].numel() < gpre_n or b["cls"].numel() < cls_n):
+                or b["gpre"].numel() < gpre_n):
             F1, c_cap = max(F1, b["F1"] if b else 0), max(c_cap, b["c_cap"] if b else 0)
             part_n = max(part_n, b["part"].numel() if b else 0)
             gpre_n = max(gpre_n, b["gpre"].numel() if b else 1)
-            cls_n = max(cls_n, b["cls"].numel() if b else 1)
-            slots = c_cap + (DL_CLS_PAD if DL_CLS_MIN_M > 0 else 0)
-            b = self.post_bufs = dict(F1=F1, c_cap=c_cap, slots=slots,
+            b = self.post_bufs = dict(F1=F1, c_cap=c_cap,
                                       item_map=torch.empty(max(F1, 1), dtype=_I32, device=self.dev),
-                                      rec=torch.empty(12 * slots + 12, dtype=_I32, device=self.dev),
+                                      rec=torch.empty(12 * c_cap + 12, dtype=_I32, device=self.dev),
                                       part=torch.empty(part_n, dtype=_I32, device=self.dev),
                                       out=torch.empty(c_cap, dtype=_I32, device=self.dev),
-                                      gpre=torch.empty(max(gpre_n, 1), dtype=_I32, device=self.dev),
-                                      cls=torch.empty(cls_n, dtype=_I64, device=self.dev))
+                                      gpre=torch.empty(max(gpre_n, 1), dtype=_I32, device=self.dev))
         return b
 
 
@@ -1532,28 +1522,16 @@ def dl_plan(S: DeviceLevelState, L: int, F1: int, n_used: int, C: int, lds: int,
     if sw == 0 or C > cap:
         raise RuntimeError(f"device bundle of {C} candidates over {n_used} items does not fit one pass")
     item_map = torch.empty(max(F1, 1), dtype=_I32, device=dev)
-    slots = C + (DL_CLS_PAD if DL_CLS_MIN_M > 0 else 0)
-    rec = torch.empty(12 * slots + 12, dtype=_I32, device=dev)
+    rec = torch.empty(12 * C + 12, dtype=_I32, device=dev)
     R = int(S.desc[:L, 5].sum())                     # parent rows of the bundle
     part = torch.empty(8 * max(1, (R + 255) // 256), dtype=_I32, device=dev)
     lib = _native.hip()
     gn = int(lib.fa_hip_dl_gpre_need(S.desc.ctypes.data, L))
     gpre = torch.empty(max(gn, 1), dtype=_I32, device=dev)
-    cls, used = _dl_cls_scratch(S, L, dev), np.zeros(1, dtype=np.int64)
-    _native.check(lib.fa_hip_dl_plan_ex(S.desc.ctypes.data, L, _p(S.ctl), F1, _p(item_map), _p(rec), slots,
-                                        _p(part), part.numel(), _p(gpre), gpre.numel(), 0, -1, _p(cls),
-                                        cls.numel() if cls is not None else 0, DL_CLS_MIN_M, n_used, st,
-                                        used.ctypes.data), "fa_hip_dl_plan_ex")
+    _native.check(lib.fa_hip_dl_plan(S.desc.ctypes.data, L, _p(S.ctl), F1, _p(item_map), _p(rec), C,
+                                     _p(part), part.numel(), _p(gpre), gpre.numel(), st), "fa_hip_dl_plan")
     out = torch.zeros(C, dtype=_I32, device=dev)
-    return dict(sw=sw, cap=cap, item_map=item_map, rec=rec, out=out, n_used=n_used, C=C, gpre=gpre,
-                cls=bool(used[0]), cls_scr=cls)
-
-
-def _dl_cls_scratch(S: DeviceLevelState, L: int, dev) -> torch.Tensor | None:
-    """The class layout's planner scratch for the bundle's L levels (None: disabled)."""
-    if DL_CLS_MIN_M <= 0:
-        return None
-    return torch.empty(int(_native.hip().fa_hip_dl_cls_need(S.desc.ctypes.data, L)), dtype=_I64, device=dev)
+    return dict(sw=sw, cap=cap, item_map=item_map, rec=rec, out=out, n_used=n_used, C=C, gpre=gpre)
 
 
 def dl_count_multipass(S: DeviceLevelState, F1: int, n_used: int, C: int, lds: int, roff, ranks, src, ncols: int,
@@ -1573,36 +1551,29 @@ def dl_count_multipass(S: DeviceLevelState, F1: int, n_used: int, C: int, lds: i
     st = _stream(ranks)
     lib = _native.hip()
     item_map = torch.empty(max(F1, 1), dtype=_I32, device=dev)
-    slots = cap + (DL_CLS_PAD if DL_CLS_MIN_M > 0 and wword is None else 0)
-    rec = torch.empty(12 * slots + 12, dtype=_I32, device=dev)
+    rec = torch.empty(12 * cap + 12, dtype=_I32, device=dev)
     R = int(S.desc[0, 5])
     part = torch.empty(8 * max(1, (R + 255) // 256) + 16, dtype=_I32, device=dev)
     gn = int(lib.fa_hip_dl_gpre_need(S.desc.ctypes.data, 1))
     gpre = torch.empty(max(gn, 1), dtype=_I32, device=dev)
-    cls = _dl_cls_scratch(S, 1, dev) if wword is None else None    # (no weighted class-layout kernel)
-    used = np.zeros(1, dtype=np.int64)
     out = torch.zeros(C, dtype=_I32, device=dev)
     W = (ncols + 63) // 64
     nslabs = (W + sw - 1) // sw
-    npass = ncls = 0
+    npass = 0
     for w0 in range(0, C, cap):
         w1 = min(C, w0 + cap)
-        _native.check(lib.fa_hip_dl_plan_ex(S.desc.ctypes.data, 1, _p(S.ctl), F1, _p(item_map), _p(rec), slots,
-                                            _p(part), part.numel(), _p(gpre), gpre.numel(), w0, w1, _p(cls),
-                                            cls.numel() if cls is not None else 0, DL_CLS_MIN_M, n_used, st,
-                                            used.ctypes.data), "fa_hip_dl_plan_ex")
+        _native.check(lib.fa_hip_dl_plan_window(S.desc.ctypes.data, 1, _p(S.ctl), F1, _p(item_map), _p(rec), cap,
+                                                _p(part), part.numel(), _p(gpre), gpre.numel(), w0, w1, st),
+                      "fa_hip_dl_plan_window")
         lds_k = n_used * (sw + 2) * 8 + ((w1 - w0 + 3) & ~3) * 4
         n_wg = int(max(1, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds_k), 2))))
         _hip_call("fa_hip_count_slab_rec_cls", _p(roff), _p(ranks), _p(src), ncols, _p(item_map), F1, n_used,
                   _p(gpre), _p(rec), 0, w1 - w0, _p(wword), out.data_ptr() + 4 * w0, sw, n_wg, _p(bm),
-                  bm.stride(0), st, _p(bm_rows), _p(S.ctl) + 8 * 221, (2 if dense else 0) | int(used[0]))
+                  bm.stride(0), st, _p(bm_rows), _p(S.ctl) + 8 * 221, 2 if dense else 0)
         npass += 1
-        ncls += int(used[0])
-    CLS_LEVELS[0] += int(ncls > 0)
     LAST_LEVEL_PLAN.clear()
     LAST_LEVEL_PLAN.update(kernel="slab_dev_multi", rows=int(roff.numel() - 1), used=n_used, sw=sw, cap=cap,
-                           passes=npass, pieces=-1, slab_reads=0, m=int(S.desc[0, 4]), C=C, dense=bool(dense),
-                           cls=ncls)
+                           passes=npass, pieces=-1, slab_reads=0, m=int(S.desc[0, 4]), C=C, dense=bool(dense))
     return out
 
 
@@ -1612,7 +1583,7 @@ def dl_plan_from_post(S: DeviceLevelState, n_used: int) -> dict:
     C = int(P.C)
     out = b["out"][:C]
     return dict(sw=int(P.sw), cap=int(P.cap), item_map=b["item_map"], rec=b["rec"], out=out, n_used=n_used, C=C,
-                gpre=b["gpre"], cls=bool(P.cls_used))
+                gpre=b["gpre"])
 
 
 def dl_count(S: DeviceLevelState, plan: dict, roff, ranks, src, ncols: int, F1: int, wword) -> torch.Tensor:
@@ -1625,14 +1596,12 @@ def dl_count(S: DeviceLevelState, plan: dict, roff, ranks, src, ncols: int, F1: 
     nslabs = (W + sw - 1) // sw
     lds_k = n_used * (sw + 2) * 8 + ((C + 3) & ~3) * 4 + _slab_map_lds(F1)
     n_wg = int(max(1, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds_k), 2))))
-    cls = bool(plan.get("cls")) and wword is None
-    _hip_call("fa_hip_count_slab_rec_cls", _p(roff), _p(ranks), _p(src), ncols, _p(item_map), F1, n_used,
+    _hip_call("fa_hip_count_slab_rec", _p(roff), _p(ranks), _p(src), ncols, _p(item_map), F1, n_used,
               _p(plan.get("gpre")), _p(rec), 0, C, _p(wword), _p(out), sw, n_wg, None, 0, st, None,
-              _p(S.ctl) + 8 * 221, int(cls))
-    CLS_LEVELS[0] += int(cls)
+              _p(S.ctl) + 8 * 221)
     LAST_LEVEL_PLAN.clear()
     LAST_LEVEL_PLAN.update(kernel="slab_dev", rows=int(roff.numel() - 1), used=n_used, sw=sw, cap=cap, passes=1,
-                           pieces=-1, slab_reads=0, m=-1, C=C, cls=int(cls))
+                           pieces=-1, slab_reads=0, m=-1, C=C)
     # (item_map and rec may be freed now: the caching allocator hands their blocks only
     # to work queued later on this stream)
     return out

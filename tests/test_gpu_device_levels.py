@@ -108,28 +108,6 @@ def test_deep_database_all_levels_on_device():
     _same(got, ref)
 
 
-@pytest.mark.parametrize("min_m,small_lds", [(2.0, False), (2.0, True), (0.0, False)])
-def test_device_class_layout(monkeypatch, min_m, small_lds):
-    # the class layout of device plans (levels.hip fa_hip_dl_plan_ex: sibling runs on one
-    # thread, idle-padded wave rows) on every level (mean prefix >= 2), also window by
-    # window on multi-pass levels (shrunk LDS); 0 = never (the size-sorted plan)
-    import fastapriori_amd.ops.primitives as prim
-    monkeypatch.setattr(prim, "DL_CLS_MIN_M", min_m)
-    prim._DL_STATE.clear()
-    cpu = generate_shard(120_000, Comm(), "cpu", 40.0, 10.0, 2000, 1000, 3)
-    ref, _ = _mine(cpu, 0.006)
-    if small_lds:
-        monkeypatch.setattr(prim, "_LDS_BYTES", _multipass_lds(ref))
-    before = prim.CLS_LEVELS[0]
-    got, st = _mine(cpu.to(DEV), 0.006)
-    assert st.get("host_levels", 0) == 0 and "fallbacks" not in st, st
-    assert (prim.CLS_LEVELS[0] > before) == (min_m > 0)
-    if small_lds:
-        assert st.get("device_multipass", 0) >= 1, st
-    _same(got, ref)
-    prim._DL_STATE.clear()
-
-
 def test_device_levels_no_frequent_pairs():
     cpu = generate_shard(20_000, Comm(), "cpu", 10.0, 4.0, 2000, 1000, 2)
     got, _ = _mine(cpu.to(DEV), 0.2)
