@@ -49,16 +49,24 @@ class Checkpointer:
             return int(fault)
         return 0
 
-    def _write_level(self, result: MiningResult, k: int) -> None:
+    def _write_level(self, result: MiningResult, k: int, meta: bool = True) -> None:
+        """level_k.npz, then (meta) meta.json saying levels 1..k are done: the level file
+        lands before the meta that counts it, so a crash leaves a consistent checkpoint."""
         if self.rank == 0 and k <= len(result.levels):
             def w(tmp):
                 with open(tmp, "wb") as f:
                     np.savez(f, rows=result.levels[k - 1], counts=result.counts[k - 1])
             self._atomic(os.path.join(self.dir, f"level_{k}.npz"), w)
-            meta = {"items": result.items, "min_count": result.min_count, "n_lines": result.n_lines,
-                    "levels_done": k, "fingerprint": self.fingerprint}
-            self._atomic(os.path.join(self.dir, "meta.json"),
-                         lambda tmp: open(tmp, "w", encoding="utf-8").write(json.dumps(meta)))
+            if meta:
+                self._write_meta(result, k)
+
+    def _write_meta(self, result: MiningResult, k: int, complete: bool = False) -> None:
+        meta = {"items": result.items, "min_count": result.min_count, "n_lines": result.n_lines,
+                "levels_done": k, "fingerprint": self.fingerprint}
+        if complete:
+            meta["complete"] = True
+        self._atomic(os.path.join(self.dir, "meta.json"),
+                     lambda tmp: open(tmp, "w", encoding="utf-8").write(json.dumps(meta)))
 
     def save_level(self, result: MiningResult, k: int) -> None:
         self.wait()
@@ -67,8 +75,9 @@ class Checkpointer:
             raise InjectedFault(17)
 
     def save_levels(self, result: MiningResult, ks, background: bool = False) -> None:
-        """Levels ks (ascending), meta.json rewritten after each, so a crash part-way
-        leaves a consistent checkpoint of the levels before it.  background: written by
+        """Levels ks (ascending), then one meta.json counting them (a crash part-way
+        leaves the previous meta: a consistent checkpoint of the levels before the
+        batch).  background: written by
         a thread while the caller goes on (the device level loop hands its levels over
         in one go after its single results readback); wait() joins it.  An injected
         fault at one of the levels is taken synchronously: the levels up to it are
@@ -82,16 +91,19 @@ class Checkpointer:
             raise InjectedFault(17)
         if self.rank != 0 or not ks:
             return
-        if not background:
+        def batch():
             for k in ks:
-                self._write_level(result, k)
+                self._write_level(result, k, meta=False)
+            self._write_meta(result, ks[-1])
+
+        if not background:
+            batch()
             return
         import threading
 
         def work():
             try:
-                for k in ks:
-                    self._write_level(result, k)
+                batch()
             except BaseException as e:       # surfaced by wait()
                 self._error = e
 
@@ -109,15 +121,11 @@ class Checkpointer:
     def mark_complete(self, result: MiningResult) -> None:
         self.wait()
         if self.rank == 0:
-            path = os.path.join(self.dir, "meta.json")
-            meta = json.load(open(path, encoding="utf-8")) if os.path.exists(path) else {}
-            meta.update(items=result.items, min_count=result.min_count, n_lines=result.n_lines,
-                        levels_done=len(result.levels), complete=True, fingerprint=self.fingerprint)
             for k in range(1, len(result.levels) + 1):
                 f = os.path.join(self.dir, f"level_{k}.npz")
                 if not os.path.exists(f):
-                    self._write_level(result, k)
-            self._atomic(path, lambda tmp: open(tmp, "w", encoding="utf-8").write(json.dumps(meta)))
+                    self._write_level(result, k, meta=False)
+            self._write_meta(result, len(result.levels), complete=True)
 
     def load(self, require_complete: bool = False) -> MiningResult | None:
         path = os.path.join(self.dir, "meta.json")

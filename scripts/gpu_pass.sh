@@ -12,6 +12,7 @@
 #   bash scripts/gpu_pass.sh e2e                the reference window's breakdown (benchmarks/e2e_probe.py) + its kernel stats
 #   bash scripts/gpu_pass.sh multirank          8 gloo ranks sharing the GPU: collectives per run (benchmarks/multirank_probe.py)
 #   bash scripts/gpu_pass.sh ab VAR A B [CFG]   alternating bench runs with VAR=A / VAR=B
+#   bash scripts/gpu_pass.sh head             tests + multirank + e2e + kernel stats of T10 and T40 (one HEAD's evidence)
 #   bash scripts/gpu_pass.sh cpu                the C++ CPU comparator of vs_baseline (no GPU work)
 set -e -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -91,6 +92,18 @@ case "$MODE" in
           > "$O/${CFG}_${V}_${val}_$i.json" 2> /dev/null
       done
     done
+    ;;
+  head)
+    # the evidence set of one HEAD: GPU tests, kernel stats of both configs, the 8-rank
+    # rehearsal, the e2e breakdown
+    pytest_gpu > "$O/tests.log" 2>&1
+    timeout -k 10 600 python benchmarks/multirank_probe.py --world 8 --n-txn 4000000 > "$O/multirank.json" 2> "$O/multirank.err"
+    timeout -k 10 400 python benchmarks/e2e_probe.py --reps 3 --job > "$O/probe.json" 2> "$O/probe.err"
+    cd /tmp
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/T10" -o run -- \
+      python3 "$R/bench.py" --steps 1 --warmup 1 --e2e off > "$O/T10.log" 2>&1
+    timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/T40" -o run -- \
+      python3 "$R/bench.py" --config T40I10D100M --steps 1 --warmup 1 --e2e off > "$O/T40.log" 2>&1
     ;;
   cpu)
     for c in T10I4D1K T10I4D100K; do
