@@ -40,7 +40,7 @@ def _timed(fn):
             return fn(self, *a, **kw)
         self._depth += 1
         t0 = time.perf_counter()
-        b0 = self.bytes_reduced
+        b0 = self.bytes_reduced + self.bytes_gathered
         try:
             return fn(self, *a, **kw)
         finally:
@@ -50,7 +50,7 @@ def _timed(fn):
             self.comm_calls += 1
             if self.trace is not None:
                 # (collective, payload bytes it moved per rank, host ms)
-                self.trace.append((fn.__name__, self.bytes_reduced - b0, round(dt, 3)))
+                self.trace.append((fn.__name__, self.bytes_reduced + self.bytes_gathered - b0, round(dt, 3)))
     return wrap
 
 
@@ -61,6 +61,7 @@ class Comm:
     device: torch.device = torch.device("cpu")
     backend: str = "none"
     bytes_reduced: int = 0
+    bytes_gathered: int = 0   # payload bytes received by the all-gathers (Comm.trace)
     force: bool = False     # run the collective code paths even at world size 1 (FA_FORCE_PG)
     comm_ms: float = 0.0    # host time inside collectives (see _timed)
     comm_calls: int = 0
@@ -184,6 +185,7 @@ class Comm:
         t = torch.from_numpy(v.ravel().copy()).to(self._comm_device())
         out = torch.empty(self.world_size * t.numel(), dtype=torch.int64, device=t.device)
         dist.all_gather_into_tensor(out, t)
+        self.bytes_gathered += out.numel() * 8
         return out.cpu().numpy().reshape(self.world_size, -1)
 
     @_timed
@@ -201,6 +203,7 @@ class Comm:
             buf[:a.size] = torch.from_numpy(a).to(dev)
         out = torch.empty(self.world_size * mx, dtype=torch.int64, device=dev)
         dist.all_gather_into_tensor(out, buf)
+        self.bytes_gathered += out.numel() * 8
         o = out.cpu().numpy().reshape(self.world_size, mx)
         return [o[r, :int(sizes[r])] for r in range(self.world_size)]
 
