@@ -366,7 +366,7 @@ class FastApriori:
         pend = []
         tm = self._timer
         nxt = None
-        self._dl_staged = None
+        self._dl_stg = dict(n=0, rows=[], cnt=[], f2=None, ev=None, stream=getattr(self, "_dl_stage_stream", None))
         while True:
             if self.cfg.max_level and k > self.cfg.max_level:
                 break
@@ -384,16 +384,16 @@ class FastApriori:
                 post = DL_POST and max_lv > 1
                 if post:
                     self._dl_post_setup(S, db, k, F1, c_bound, n_bound, lds)
-                # the results so far, copied to the host ahead of this bundle's synchronisation:
-                # when the generator finds the mining over, _dl_flush needs no further round trip
-                staged = self._dl_stage(S, pend) if pend else None
+                # the results not staged yet go to the host on a copy stream while this
+                # bundle runs: when the generator finds the mining over, _dl_flush only waits
+                if pend:
+                    self._dl_stage(S, pend)
                 with roctx_range("gen"):
                     c = Pm.dl_bundle_gen(S, P0, n_src, n_const, n_bound, m0, F1, c_bound, lds, BUNDLE_GROWTH, max_lv,
                                          st, post=post)
                 if c[4]:
                     raise RuntimeError(f"device bundle at level {k}: |F_{k - 1}| exceeds its bound {n_bound}")
                 if c[7]:
-                    self._dl_staged = staged
                     break                               # |F_{k-1}| < k or no candidates: done
                 multi = None
                 if c[5]:
@@ -545,19 +545,40 @@ class FastApriori:
         P.T, P.nnz = int(db["T"]), int(db["ranks"].numel())
         P.trim_min_rows, P.trim_ok, P.k = int(self.cfg.trim_min_rows), int(bool(self.cfg.trim) and db["T"] > 0), k
 
-    def _dl_parts(self, S, pend: list) -> list:
-        f2 = []
-        if self._f2_n_dev is not None:
+    def _dl_stage(self, S, pend: list) -> None:
+        """Queue the D2H copies of the results not staged yet (F_2 once, then each new
+        bundle's rows and counts) into pinned buffers, on a copy stream that waits for
+        the compute stream's work so far: the copies overlap the next bundles' kernels,
+        and every bundle's results cross PCIe once.  (Copying all results so far again
+        at every bundle, on the compute stream, cost T40I10D100M ~10 ms per run.)"""
+        Pm = ops.primitives
+        stg = self._dl_stg
+        todo = []
+        if self._f2_n_dev is not None and stg["f2"] is None:
             nb = self._f2_bound
-            f2 = [self._f2_n_dev.view(torch.int32), self._f2_dev[:nb].reshape(-1), self._f2_cnt_dev[:nb]]
-        return f2 + [S.fsz.view(torch.int32)] + [p["rows"] for p in pend] + [p["cnt"] for p in pend]
-
-    def _dl_stage(self, S, pend: list):
-        """Queue the D2H copy of the results so far into a pinned buffer (no wait)."""
-        blob = torch.cat(self._dl_parts(S, pend))
-        host = ops.primitives.pinned_stage("dl_results").get(4 * blob.numel()).view(torch.int32)
-        host.copy_(blob, non_blocking=True)
-        return len(pend), host
+            stg["f2"] = [None] * 3
+            todo += [("f2", 0, self._f2_n_dev.view(torch.int32)), ("f2", 1, self._f2_dev[:nb].reshape(-1)),
+                     ("f2", 2, self._f2_cnt_dev[:nb])]
+        for i in range(stg["n"], len(pend)):
+            todo += [("rows", i, pend[i]["rows"]), ("cnt", i, pend[i]["cnt"])]
+            stg["rows"].append(None)
+            stg["cnt"].append(None)
+        stg["n"] = len(pend)
+        if not todo:
+            return
+        dev = self._dev
+        cs = stg.get("stream")
+        if cs is None:
+            cs = stg["stream"] = self._dl_stage_stream = torch.cuda.Stream(dev)
+        cs.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(cs):
+            for kind, i, t in todo:
+                h = Pm.pinned_stage(f"dl_{kind}{i}").get(4 * t.numel()).view(torch.int32)
+                h.copy_(t, non_blocking=True)
+                stg[kind][i] = h
+            ev = torch.cuda.Event()
+            ev.record(cs)
+        stg["ev"] = ev
 
     def _dl_flush(self, S, pend: list, levels: list, counts: list, result: MiningResult) -> None:
         """Every device level to the host (the run's one results readback); F_2 too when
@@ -566,29 +587,23 @@ class FastApriori:
         f2 = self._f2_n_dev is not None
         if not pend and not f2:
             return
-        # one readback: F sizes (int64 as int32 pairs), every bundle's rows, then counts
-        nrow = sum(int(p["rows"].numel()) for p in pend)
-        staged, self._dl_staged = self._dl_staged, None
-        if staged is not None and staged[0] == len(pend):
-            blob = staged[1].numpy().copy()               # complete: the generator's sync waited for it
-        else:
-            blob = torch.cat(self._dl_parts(S, pend)).cpu().numpy()
+        # the staged copies (_dl_stage) of whatever is not staged yet, then the F sizes
+        self._dl_stage(S, pend)
+        stg = self._dl_stg
+        fsz = S.fsz.cpu().numpy()                        # (the stream's last work: the thresholds)
+        stg["ev"].synchronize()
         if f2:
             nb = self._f2_bound
-            n2 = int(blob[:2].view(np.int64)[0])
-            levels[1] = np.ascontiguousarray(blob[2:2 + 2 * n2].reshape(n2, 2))
-            counts[1] = blob[2 + 2 * nb:2 + 2 * nb + n2].astype(np.int64)
+            n2 = int(stg["f2"][0].numpy()[:2].view(np.int64)[0])
+            levels[1] = stg["f2"][1].numpy()[:2 * n2].reshape(n2, 2).copy()     # (pinned buffer: reused)
+            counts[1] = stg["f2"][2].numpy()[:n2].astype(np.int64)
             self._log_level2(n2)
-            blob = blob[2 + 3 * nb:]
             self._f2_n_dev = None
         if not pend:
             return
-        nf = S.fsz.numel() * 2
-        fsz = blob[:nf].view(np.int64)
-        rows_h = blob[nf:nf + nrow]
-        cnt_h = blob[nf + nrow:]
-        ro_base = co_base = 0
-        for p in pend:
+        for i, p in enumerate(pend):
+            rows_h, cnt_h = stg["rows"][i].numpy(), stg["cnt"][i].numpy()
+            ro_base = co_base = 0
             for l in range(p["L"]):
                 kk, w = p["k"] + l, p["m0"] + l + 1
                 F = int(fsz[kk])
@@ -615,8 +630,6 @@ class FastApriori:
                                               bytes_reduced=int(p["bytes"] * share), kernel="slab_rec_dev",
                                               hbm_bytes_est=hbm, _share=share),
                                          f"level{p['k']}"))
-            ro_base += int(p["rows"].numel())
-            co_base += int(p["cnt"].numel())
 
     def _run_deferred(self) -> None:
         for d in self._deferred:
