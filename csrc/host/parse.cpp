@@ -16,6 +16,7 @@
 //             and ids agree across ranks by construction.
 //   dict    : any other vocabulary; per-shard dictionary (id -> bytes) plus a
 //             64-bit hash per entry used to agree on identity across ranks.
+#include <immintrin.h>
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -460,12 +461,35 @@ FA_API int64_t fa_next_line_start(const char* data, int64_t size, int64_t pos) {
 // too: such chunks leave the rest of the file to the whole-region path).  Eight
 // bytes per step with an exact zero-byte test, so one host thread keeps up with
 // its share of the pread ring.
+// AVX2 form of the scan: 64 bytes per step (two compares, movemasks and popcounts per
+// 32 bytes); the reader threads call it on every 32 MB chunk as it lands in the pinned
+// ring, so its rate is taken from the pread pipeline's (8 bytes per step: ~3 GB/s).
+__attribute__((target("avx2"))) static void chunk_scan_avx2(const uint8_t* p, int64_t m, int64_t* nl_out,
+                                                           uint64_t* cr_out, int64_t* done) {
+  const __m256i nlv = _mm256_set1_epi8('\n'), crv = _mm256_set1_epi8('\r');
+  int64_t nl = 0;
+  uint32_t cr = 0;
+  int64_t i = 0;
+  for (; i + 64 <= m; i += 64) {
+    const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(p + i));
+    const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(p + i + 32));
+    nl += __builtin_popcount((uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(a, nlv)));
+    nl += __builtin_popcount((uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(b, nlv)));
+    cr |= (uint32_t)_mm256_movemask_epi8(_mm256_or_si256(_mm256_cmpeq_epi8(a, crv), _mm256_cmpeq_epi8(b, crv)));
+  }
+  *nl_out = nl;
+  *cr_out = cr;
+  *done = i;
+}
+
 FA_API void fa_chunk_scan(const uint8_t* p, int64_t m, int64_t* info) {
   const uint64_t lo7 = 0x7F7F7F7F7F7F7F7Full;
   auto zeros = [lo7](uint64_t t) { return ~(((t & lo7) + lo7) | t | lo7); };   // 0x80 per zero byte
   int64_t nl = 0;
   uint64_t cr = 0;
   int64_t i = 0;
+  static const bool avx2 = __builtin_cpu_supports("avx2");
+  if (avx2) chunk_scan_avx2(p, m, &nl, &cr, &i);
   for (; i + 8 <= m; i += 8) {
     uint64_t x;
     std::memcpy(&x, p + i, 8);
