@@ -892,8 +892,6 @@ __global__ __launch_bounds__(256) void k_cmp_emit(const int64_t* __restrict__ of
   // block-b span minus the row's first block-b index, tabx[x * nb + b]
   extern __shared__ int32_t tabx[];
   __shared__ int64_t wgb[8];
-  __shared__ int bs2[8][4];      // per-wave block totals (fused pair layout)
-  __shared__ int lws[9];         // the workgroup's block spans in its staged layout image
   const bool blk = bcnt != nullptr;
   const int64_t r0 = (int64_t)blockIdx.x * 256, r1 = min(n, r0 + 256);
   const int64_t r = r0 + threadIdx.x;
@@ -959,6 +957,7 @@ __global__ __launch_bounds__(256) void k_cmp_emit(const int64_t* __restrict__ of
     const int64_t bld = pre_rows[gridDim.x];
     const unsigned long long pk = kept ? pc : 0ull;
     const unsigned long long fpre = (pk << 8) * 0x0101010101010101ull;   // byte b: items in blocks < b
+    __shared__ int bs2[8][4];
     const int lane_ = threadIdx.x & 63;
     int exb[8];
 #pragma unroll
@@ -986,7 +985,7 @@ __global__ __launch_bounds__(256) void k_cmp_emit(const int64_t* __restrict__ of
         }
       }
     }
-    if (lr && mine && !(staged && tb <= kCmpSpan)) {   // (staged workgroups: through LDS, below)
+    if (lr && mine) {
 #pragma unroll
       for (int j = 0; j < N; ++j) {
         if (j < c) {
@@ -1057,59 +1056,19 @@ __global__ __launch_bounds__(256) void k_cmp_emit(const int64_t* __restrict__ of
           const int idx = t < s32 ? (lane & 31) : lane;
           const int rc = __shfl(c, src, 64), reb = __shfl(eb, src, 64);
           const bool in = rw >= 0 && idx < rc;
-          if (in) buf[reb + idx] = midv[t];
+          if (in) {
+            buf[reb + idx] = midv[t];
+            if (lr) {
+              const int b = (int)(midv[t] >> 8);
+              const int64_t pos = b < nb ? wgb[b] + tabx[(w * 64 + rw) * nb + b] + idx : -1;
+              if (pos >= 0 && pos < lr_cap) lr[pos] = (uint8_t)midv[t];
+            }
+          }
         }
       }
     }
     __syncthreads();
     for (int i = threadIdx.x; i < tb; i += blockDim.x) ranks[obase + i] = (int32_t)buf[i];
-    if (lr) {
-      // the workgroup's local-rank bytes, block-major, staged in LDS (buf, once its
-      // ranks are out) and stored block span by block span with consecutive lanes on
-      // consecutive bytes (scattered per-row byte stores cost ~1.3 ms per T10I4D100M run)
-      if (threadIdx.x == 0) {
-        int at = 0;
-        for (int b = 0; b <= 8; ++b) {
-          lws[b] = at;
-          if (b < nb) at += bs2[b][0] + bs2[b][1] + bs2[b][2] + bs2[b][3];
-        }
-      }
-      uint8_t* lb = reinterpret_cast<uint8_t*>(buf);
-      __syncthreads();
-      if (mine) {
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-          if (j < c) {
-            const int b = (int)(a[j] >> 8);
-            const int pos = b < nb ? lws[b] + tabx[threadIdx.x * nb + b] + j : -1;
-            if (pos >= 0 && pos < tb) lb[pos] = (uint8_t)a[j];
-          }
-        }
-      }
-#pragma unroll
-      for (int t = 0; t < kCmpMidPerWave; ++t) {
-        if (t < nslot) {                         // wave-uniform
-          const int rw = slot_row(t);
-          const int src = rw < 0 ? 0 : rw;
-          const int idx = t < s32 ? (lane & 31) : lane;
-          const int rc = __shfl(c, src, 64);
-          if (rw >= 0 && idx < rc) {
-            const int b = (int)(midv[t] >> 8);
-            const int pos = b < nb ? lws[b] + tabx[(w * 64 + rw) * nb + b] + idx : -1;
-            if (pos >= 0 && pos < tb) lb[pos] = (uint8_t)midv[t];
-          }
-        }
-      }
-      __syncthreads();
-      for (int i = threadIdx.x; i < tb; i += blockDim.x) {
-        int b = 0;
-#pragma unroll
-        for (int q = 1; q < 8; ++q)
-          if (q < nb && i >= lws[q]) b = q;
-        const int64_t dst = wgb[b] + (i - lws[b]);
-        if (dst >= 0 && dst < lr_cap) lr[dst] = lb[i];
-      }
-    }
   } else if (mine) {
 #pragma unroll
     for (int j = 0; j < N; ++j)
@@ -1417,7 +1376,10 @@ FA_API int fa_hip_build_bitmaps(const int64_t* roff, const int32_t* ranks, const
   if (Wp % WT) return 1;
   // contiguous rows with every output row in one tile: the wave-cooperative build (count.hip)
   static const bool wave_ok = !getenv("FA_BITMAP_WAVE") || atoi(getenv("FA_BITMAP_WAVE")) != 0;
-  if (wave_ok && !src && R >= F1) {
+  // (with every rank's row, e.g. T40I10D100M's full 998-item Gram bitmap, the
+  // thread-per-row kernel measured faster: 7.7 vs 14.1 ms; the wave build wins on the
+  // used-item subsets of the multi-pass levels: 1.9 ms)
+  if (wave_ok && !src && R >= F1 && item_map) {
     const int rc = fa_hip_build_bitmaps_wave(roff, ranks, ncols, F1, Wp, WT, bm, item_map, st);
     if (rc != 2) return rc;
   }
