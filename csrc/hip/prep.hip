@@ -327,51 +327,6 @@ __global__ __launch_bounds__(256) void k_compress_staged(
     for (int64_t i = threadIdx.x; i < n_out; i += blockDim.x) ranks[obase + i] = (int32_t)buf[i];
 }
 
-// Rows of <= 64 tokens over F1 <= 1024 ranks (T40I10's 40-token transactions): instead
-// of a 64-element register sorting network per row (k_compress_staged<64>: 16 ms per
-// T40I10D100M run, limited by its 64 + 64 live registers per thread), each thread ORs its
-// row's ranks into a private 1024-bit LDS bitmap (row stride 33 dwords: the 64 lanes'
-// rows start on distinct banks) and emits the set bits in order.  A row whose set size
-// differs from its kept-token count (a repeated token) is left to the next tier by flag.
-constexpr int kBmWords = 32;          // 1024 bits as u32 words
-constexpr int kBmStride = kBmWords + 1;
-
-__global__ __launch_bounds__(256) void k_compress_bitmap(const int64_t* __restrict__ off,
-                                                         const int32_t* __restrict__ items,
-                                                         const int32_t* __restrict__ lut, int64_t T,
-                                                         const int32_t* __restrict__ kept,
-                                                         const int64_t* __restrict__ roff,
-                                                         int32_t* __restrict__ ranks, int8_t* __restrict__ over_flag) {
-  __shared__ uint32_t bmp[256 * kBmStride];
-  const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  uint32_t* my = bmp + threadIdx.x * kBmStride;
-#pragma unroll
-  for (int w = 0; w < kBmWords; ++w) my[w] = 0u;
-  if (x >= T) return;
-  const int64_t t = kept[x];
-  const int64_t s = off[t], L = off[t + 1] - s;
-  if (L > 64) { over_flag[x] = 1; return; }
-  for (int64_t j = 0; j < L; ++j) {
-    const int r = lut[items[s + j]];
-    if (r >= 0) my[r >> 5] |= 1u << (r & 31);
-  }
-  const int64_t o = roff[x], c = roff[x + 1] - o;
-  int n = 0;
-#pragma unroll
-  for (int w = 0; w < kBmWords; ++w) n += __popc(my[w]);
-  if (n != c) { over_flag[x] = 1; return; }
-  over_flag[x] = 0;
-  int64_t k = o;
-#pragma unroll
-  for (int w = 0; w < kBmWords; ++w) {
-    uint32_t b = my[w];
-    while (b) {
-      ranks[k++] = w * 32 + __builtin_ctz(b);
-      b &= b - 1;
-    }
-  }
-}
-
 // Long rows: one 256-thread workgroup per row, bitonic sort in LDS (<= 16384).
 constexpr int kLongMax = 16384;
 __global__ __launch_bounds__(256) void k_compress_lds(
@@ -1411,16 +1366,6 @@ FA_API int fa_hip_dedup_probe(const int64_t* roff, const int32_t* ranks, const i
 }
 
 // Wp must be a multiple of WT.  LDS = R * 2 * WT * 4 bytes.
-// Rows of <= 64 tokens with F1 <= 1024 (k_compress_bitmap); over_flag as the staged tiers.
-FA_API int fa_hip_compress_bitmap(const int64_t* off, const int32_t* items, const int32_t* lut, int64_t T,
-                                  const int32_t* kept, const int64_t* roff, int32_t* ranks, int8_t* over_flag,
-                                  hipStream_t st) {
-  if (T <= 0) return 0;
-  hipLaunchKernelGGL(k_compress_bitmap, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, st, off, items, lut, T, kept,
-                     roff, ranks, over_flag);
-  FA_LAUNCH_RET();
-}
-
 FA_API int fa_hip_build_bitmaps_wave(const int64_t* roff, const int32_t* ranks, int64_t ncols, int32_t F1, int64_t Wp,
                                      int WT, uint64_t* bm, const int32_t* item_map, hipStream_t st);
 

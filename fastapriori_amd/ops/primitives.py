@@ -208,11 +208,8 @@ def compress(offsets, items, lut, kept, roff, F1: int | None = None) -> torch.Te
     flag = torch.empty(T, dtype=torch.int8, device=items.device)
     # long-ish rows (mean > COMPRESS_STAGED64_MEAN_LEN tokens): the 64-token staged tier first
     staged64 = items.numel() > COMPRESS_STAGED64_MEAN_LEN * max(offsets.numel() - 1, 1)
-    # rows of <= 64 tokens over <= 1024 frequent items: per-row rank bitmaps instead of sorting networks
-    kern = "fa_hip_compress_staged"
-    if staged64:
-        kern = "fa_hip_compress_bitmap" if (COMPRESS_BITMAP and F1 is not None and F1 <= 1024) else "fa_hip_compress_staged64"
-    _hip_call(kern, _p(offsets), _p(items), _p(lut), T, _p(kept), _p(roff), _p(ranks), _p(flag), st)
+    _hip_call("fa_hip_compress_staged64" if staged64 else "fa_hip_compress_staged", _p(offsets), _p(items), _p(lut),
+              T, _p(kept), _p(roff), _p(ranks), _p(flag), st)
     over = torch.nonzero(flag).flatten().to(_I32)
     n1 = over.numel()
     over2, n2 = over, n1                 # after the 64-token staged tier: rows of > 64 tokens
@@ -237,7 +234,6 @@ def compress(offsets, items, lut, kept, roff, F1: int | None = None) -> torch.Te
     return ranks[:nnz]
 
 
-COMPRESS_BITMAP = os.environ.get("FA_COMPRESS_BITMAP", "1") == "1"
 PAIR_PAD_BATCHES = 3 * 16 + 2   # the pair kernel's pipeline reads up to this many batches past a chunk
 # the emit pass of compress_rows also writes the pair kernel's blocked layout (FA_FUSED_LAYOUT=0: the
 # separate block-scatter pass of pair_counts_horizontal)
