@@ -186,11 +186,15 @@ def _e2e_window(args, comm, n_txn, min_sup, cfgv, miner_cfg, sync):
         if comm.is_root:
             shutil.rmtree(tmp, ignore_errors=True)
         sync()
+        ck = make_checkpointer(jc, comm)
         t0 = time.perf_counter()
         summ: dict = {}
-        res = mine_window(jc, comm, quiet, make_checkpointer(jc, comm), summ)
+        res = mine_window(jc, comm, quiet, ck, summ)
         sync()
-        return comm.allreduce_float_max((time.perf_counter() - t0) * 1e3), res, summ
+        ms = (time.perf_counter() - t0) * 1e3
+        if ck is not None:
+            ck.wait()                    # (as run_job: the checkpoint completes after the window)
+        return comm.allreduce_float_max(ms), res, summ
 
     # cold: the file's pages dropped from the page cache (every rank's local view)
     dropped = _drop_cache(path) if comm.is_root else False

@@ -88,8 +88,9 @@ def mine_window(cfg: JobConfig, comm, log: Logger, ckpt: Checkpointer | None, su
             io.write_items_to_rank(result, cfg.output + "ItemsToRank")
             io.write_freq_items(result, cfg.output + "FreqItems")
     if ckpt is not None:
-        # joins the checkpoint writer the device level loop started in the background
-        ckpt.mark_complete(result)
+        # the completion follows the level files the device loop queued on the checkpoint
+        # thread; the job joins it at its end (run_job), not inside this window
+        ckpt.mark_complete(result, background=True)
     comm.barrier()
     summary["write_ms"] = round((time.time() - t_write) * 1000, 1)
     return result
@@ -116,6 +117,7 @@ def run_job(cfg: JobConfig, comm=None) -> dict:
     u_path = cfg.input + "U.dat"
     out_rec = cfg.output + "recommends"
     summary: dict = {}
+    ckpt = None
     try:
         ckpt = make_checkpointer(cfg, comm)
         comm.barrier()
@@ -151,6 +153,8 @@ def run_job(cfg: JobConfig, comm=None) -> dict:
         log.metric(phase="job", **{k: v for k, v in summary.items() if not isinstance(v, dict)})
         return summary
     finally:
+        if ckpt is not None:
+            ckpt.wait()                  # the checkpoint is complete before the job returns
         if own_comm:
             shutdown_comm(comm)
 

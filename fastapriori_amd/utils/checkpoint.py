@@ -118,14 +118,37 @@ class Checkpointer:
             e, self._error = self._error, None
             raise e
 
-    def mark_complete(self, result: MiningResult) -> None:
-        self.wait()
-        if self.rank == 0:
-            for k in range(1, len(result.levels) + 1):
-                f = os.path.join(self.dir, f"level_{k}.npz")
-                if not os.path.exists(f):
-                    self._write_level(result, k, meta=False)
-            self._write_meta(result, len(result.levels), complete=True)
+    def mark_complete(self, result: MiningResult, background: bool = False) -> None:
+        """Every level written (the missing ones now), then the meta marked complete.
+        background: after the level writes already queued, on the checkpoint thread, so the
+        mining window does not wait for checkpoint files; wait() (the job's end) joins it."""
+        if self.rank != 0:
+            return
+        if not background:
+            self.wait()
+            self._complete(result)
+            return
+        import threading
+        prev = self._thread
+
+        def work():
+            try:
+                if prev is not None:
+                    prev.join()
+                if self._error is None:
+                    self._complete(result)
+            except BaseException as e:       # surfaced by wait()
+                self._error = e
+
+        self._thread = threading.Thread(target=work, name="fa-ckpt-complete", daemon=True)
+        self._thread.start()
+
+    def _complete(self, result: MiningResult) -> None:
+        for k in range(1, len(result.levels) + 1):
+            f = os.path.join(self.dir, f"level_{k}.npz")
+            if not os.path.exists(f):
+                self._write_level(result, k, meta=False)
+        self._write_meta(result, len(result.levels), complete=True)
 
     def load(self, require_complete: bool = False) -> MiningResult | None:
         path = os.path.join(self.dir, "meta.json")
