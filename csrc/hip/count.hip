@@ -824,19 +824,13 @@ __device__ __forceinline__ fa_v4i unpack16_i8(uint32_t b) {
 // next stage's words are loaded into registers while the current one is counted.
 // On diagonal tiles the wave below the diagonal has no (row < col) entry and skips
 // its MFMAs.
-constexpr int kM4 = 4;                 // 32 x 32 MFMA tiles per wave side (the default tile)
+constexpr int kM4 = 4;                 // 32 x 32 MFMA tiles per wave side
 constexpr int kMT4 = 64 * kM4;         // items per workgroup tile side (2 x 2 waves)
+constexpr int kM4Ld = kMT4 * kMW / 256;   // staged words per thread and operand
 
-// KM x KM MFMA tiles of 32 x 32 per wave: KM = 4 holds 256 accumulator registers per lane
-// (one wave per SIMD); KM = 2 holds 64 (several waves per SIMD to overlap the VALU bit
-// unpacking with other waves' MFMAs, at twice the unpacks and LDS reads per MFMA)
-template <int KM>
 __global__ __launch_bounds__(256) void k_pair_gram_mfma4(const uint64_t* __restrict__ bm, int32_t F1, int64_t Wp,
                                                          int64_t W, int nt, int ntp, int64_t kchunk,
                                                          uint32_t* __restrict__ out, uint32_t scale) {
-  constexpr int kM4 = KM;
-  constexpr int kMT4 = 64 * KM;
-  constexpr int kM4Ld = kMT4 * kMW / 256;   // staged words per thread and operand
   __shared__ uint64_t As[kMT4 * kMS];
   __shared__ uint64_t Bs[kMT4 * kMS];
   const uint32_t logical = xcd_remap(blockIdx.x, gridDim.x);
@@ -1476,20 +1470,14 @@ static int pair_flat_bits(int v) { return v == 0 ? 16 : v == 2 ? 32 : v == 3 ? 6
 FA_API int fa_hip_pair_gram_mfma(const uint64_t* bm, int32_t F1, int64_t Wp, int64_t W, uint32_t* out,
                                  int target_wgs, uint32_t scale, hipStream_t st) {
   if (W <= 0 || F1 < 2) return 0;
-  static const int km = getenv("FA_GRAM_KM") ? atoi(getenv("FA_GRAM_KM")) : 4;
-  const int mt = km == 2 ? 128 : kMT4;
-  const int nt = (F1 + mt - 1) / mt;
+  const int nt = (F1 + kMT4 - 1) / kMT4;
   const int ntp = nt * (nt + 1) / 2;
   int64_t nk = std::max<int64_t>(1, (target_wgs + ntp - 1) / ntp);
   int64_t kchunk = (W + nk - 1) / nk;
   kchunk = std::max<int64_t>(kMW, (kchunk + kMW - 1) / kMW * kMW);
   nk = (W + kchunk - 1) / kchunk;
-  if (km == 2)
-    hipLaunchKernelGGL(k_pair_gram_mfma4<2>, dim3((unsigned)(nk * ntp)), dim3(256), 0, st, bm, F1, Wp, W, nt, ntp,
-                       kchunk, out, scale);
-  else
-    hipLaunchKernelGGL(k_pair_gram_mfma4<4>, dim3((unsigned)(nk * ntp)), dim3(256), 0, st, bm, F1, Wp, W, nt, ntp,
-                       kchunk, out, scale);
+  hipLaunchKernelGGL(k_pair_gram_mfma4, dim3((unsigned)(nk * ntp)), dim3(256), 0, st, bm, F1, Wp, W, nt, ntp,
+                     kchunk, out, scale);
   FA_LAUNCH_RET();
 }
 
