@@ -1063,7 +1063,11 @@ class FastApriori:
         alive[torch.from_numpy(used.astype(np.int64))] = 1
         kept, nroff, nranks, nw, hist = ops.trim_rows(db["roff"], db["ranks"], alive.to(dev), k, db["wrow"])
         K = kept.numel()
-        if K > 0.9 * db["T"] and nranks.numel() > 0.9 * db["ranks"].numel():
+        # a level counted window by window streams its slabs from the used items' bitmap,
+        # whose cost follows the rows only: fewer items alone do not pay for a new layout
+        # (and the bitmap rebuild it forces)
+        multi = bool(C) and db["ranks"].is_cuda and C > ops.primitives.slab_capacity(int(used.size), C)
+        if K > 0.9 * db["T"] and (multi or nranks.numel() > 0.9 * db["ranks"].numel()):
             return   # not worth re-laying out
         db.update(roff=nroff, ranks=nranks, T=K, bm=None, W=0, bcnt=None, bm_items=None, bm_map=None)
         db["alive"] = np.zeros_like(db["alive"])
