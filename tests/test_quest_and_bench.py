@@ -76,3 +76,15 @@ def test_bench_per_rank_record_world8():
         assert p["ms_per_step"] > 0 and p["comm_ms_per_step"] >= 0 and p["collectives_per_step"] > 0
     assert d["ms_per_step"] == max(p["ms_per_step"] for p in pr)
     assert d["rank_spread_ms"] == round(max(p["ms_per_step"] for p in pr) - min(p["ms_per_step"] for p in pr), 3)
+
+
+def test_bench_e2e_window_world2():
+    # the e2e record through pipeline.mine_window (checkpointing on, its completion joined
+    # after the window) with 2 ranks reading their byte ranges of one D.dat
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
+                        "--config", "T10I4D1K", "--steps", "1", "--warmup", "1", "--e2e", "on"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    e = d["e2e"]
+    assert e["n_itemsets"] == d["config"]["n_itemsets"] and e["warm_ms"] > 0 and e["cold_ms"] > 0
