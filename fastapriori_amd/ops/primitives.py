@@ -1470,13 +1470,9 @@ def dl_lds_budget(F1: int) -> int:
     return _LDS_BYTES - _slab_map_lds(F1)
 
 
-# slab widths tried in order by the device multi-pass levels (FA_DL_SW_ORDER, e.g. "32,16,8,4")
-DL_SW_ORDER = tuple(int(x) for x in os.environ.get("FA_DL_SW_ORDER", "16,32,8,4").split(","))
-
-
 def dl_slab_width(n_used: int, C: int, lds: int) -> tuple[int, int]:
     """plan.cpp slab_width: (SW, accumulator capacity) for n_used items and C candidates."""
-    for sw in DL_SW_ORDER:
+    for sw in (16, 32, 8, 4):
         cap = int((lds - n_used * (sw + 2) * 8) // 4)
         if cap >= min(C, 8192) or (sw == 4 and cap >= 1024):
             return sw, cap

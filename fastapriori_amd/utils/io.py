@@ -105,9 +105,6 @@ def _next_line_start(fd: int, size: int, pos: int) -> int:
 
 
 _copy_streams: dict = {}
-# H2D copy streams the chunks alternate over (FA_COPY_STREAMS): more than one lets the
-# runtime keep several copy engines busy
-COPY_STREAMS = max(1, int(os.environ.get("FA_COPY_STREAMS", "1")))
 STREAM_PARSE = os.environ.get("FA_STREAM_PARSE", "1") == "1"
 
 
@@ -138,12 +135,11 @@ def _file_to_device(fd: int, first: int, n: int, dev, parse: bool = False, last_
         return (out, tp.finish()) if parse else out
     if not _ring:
         _ring.extend(torch.empty(_RING_SLOT, dtype=torch.uint8, pin_memory=True) for _ in range(_RING_SLOTS))
-    css = _copy_streams.get((dev, COPY_STREAMS))
-    if css is None:
-        css = _copy_streams[(dev, COPY_STREAMS)] = [torch.cuda.Stream(dev) for _ in range(COPY_STREAMS)]
+    cs = _copy_streams.get(dev)
+    if cs is None:
+        cs = _copy_streams[dev] = torch.cuda.Stream(dev)
     compute = torch.cuda.current_stream(dev)
-    for cs in css:
-        cs.wait_stream(compute)         # the buffer's allocation and zero fill come first
+    cs.wait_stream(compute)             # the buffer's allocation and zero fill come first
     nch = (n + _RING_SLOT - 1) // _RING_SLOT
     events: list = [None] * _RING_SLOTS
     lib = _native.host()
@@ -176,7 +172,6 @@ def _file_to_device(fd: int, first: int, n: int, dev, parse: bool = False, last_
             info = fut.pop(c).result()
             s, off = c % _RING_SLOTS, c * _RING_SLOT
             m = min(_RING_SLOT, n - off)
-            cs = css[c % len(css)]
             with torch.cuda.stream(cs):
                 out[off:off + m].copy_(_ring[s][:m], non_blocking=True)
                 ev = torch.cuda.Event()
@@ -192,8 +187,7 @@ def _file_to_device(fd: int, first: int, n: int, dev, parse: bool = False, last_
                     end = off + int(info[1]) + 1
                     tp.region(rend, end, int(info[0]), tail=False)
                     rend = end
-    for c in range(max(0, nch - len(css)), nch):   # the last copy of every stream
-        compute.wait_event(events[c % _RING_SLOTS])
+    compute.wait_event(events[(nch - 1) % _RING_SLOTS])
     if not parse:
         return out
     tp.region(rend, n, None, tail=not last_is_term)
