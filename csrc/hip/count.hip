@@ -1184,10 +1184,16 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
   constexpr int SWP = SW + 2;                       // row stride: odd number of 16-B slots
   constexpr int RS = SWP / 2;
   uint64_t* slab = reinterpret_cast<uint64_t*>(lds4);
+  // dbg & 8: two u16 counters per accumulator word (unit weights; twice the candidates
+  // per accumulator pass), drained into the u32 global counts before they can carry: a
+  // slab adds at most SW * 64 to a counter
+  const bool acc16 = !kWeighted && (dbg & 8) != 0;
+  const int nacc = acc16 ? (C + 1) >> 1 : C;
+  constexpr int kFlush16 = 65535 / (SW * 64);
   uint32_t* acc = reinterpret_cast<uint32_t*>(slab + (size_t)n_used * SWP);
-  uint16_t* smap = reinterpret_cast<uint16_t*>(acc + ((C + 3) & ~3));
+  uint16_t* smap = reinterpret_cast<uint16_t*>(acc + ((nacc + 3) & ~3));
   const bool map_lds = kBuild == kBuildContig && F1 <= kMapLdsMax;
-  for (int i = threadIdx.x; i < C; i += blockDim.x) acc[i] = 0;
+  for (int i = threadIdx.x; i < nacc; i += blockDim.x) acc[i] = 0;
   if (map_lds) {
     for (int i = threadIdx.x; i < F1; i += blockDim.x) {
       const int v = item_map[i];
@@ -1233,7 +1239,24 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
       }
     }
   };
-  auto acc_add = [&](int e, uint32_t v) { atomicAdd(&acc[e], v); };
+  auto acc_add = [&](int e, uint32_t v) {
+    if (acc16) atomicAdd(&acc[e >> 1], v << ((e & 1) << 4));
+    else atomicAdd(&acc[e], v);
+  };
+  auto flush = [&]() {
+    for (int i = threadIdx.x; i < nacc; i += blockDim.x) {
+      const uint32_t v = acc[i];
+      if (!v) continue;
+      if (acc16) {
+        if (v & 0xFFFFu) atomicAdd(&out[2 * i], v & 0xFFFFu);
+        if ((v >> 16) && 2 * i + 1 < C) atomicAdd(&out[2 * i + 1], v >> 16);
+        acc[i] = 0;
+      } else {
+        atomicAdd(&out[i], v);
+      }
+    }
+  };
+  int nsl = 0;                                      // slabs counted since the last u16 drain
   // contiguous build with one word per wave (SW <= 8; at SW = 16 the span spills): the word's CSR span for the
   // next slab is loaded before this slab's counting, so the build starts without
   // waiting on the row offsets
@@ -1250,6 +1273,10 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
   for (int64_t sb = blockIdx.x; sb < nslabs; sb += gridDim.x) {
     const int64_t w0 = sb * SW;
     __syncthreads();
+    if (acc16 && ++nsl > kFlush16) {               // (the barrier after the build orders it)
+      flush();
+      nsl = 1;
+    }
     if (dbg & 1) {
       // profiling split (FA_SLAB_DEBUG=1): no slab build
     } else if (kBuild == kBuildBM) {
@@ -1392,10 +1419,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < C; i += blockDim.x) {
-    const uint32_t v = acc[i];
-    if (v) atomicAdd(&out[i], v);
-  }
+  flush();
 }
 
 // ---------------------------------------------------------------------------
@@ -1521,14 +1545,17 @@ FA_API int fa_hip_count_candidates(const uint64_t* bm, int64_t Wp, int64_t W, co
 // cls bit 0: the records carry class-layout flags (plan.cpp cls_layout): unit weights
 // run k_count_slab_rec<.., kCls> (the flags are hints: the plain kernel ignores them and
 // recomputes every prefix, with the same counts).  cls bit 1: dense level, no
-// all-zero-prefix test (the counts are the same either way).
+// all-zero-prefix test (the counts are the same either way).  cls bit 2: u16 packed
+// accumulators (unit weights: half the LDS per candidate, drained every 65535 / (SW * 64)
+// slabs).
 FA_API int fa_hip_count_slab_rec_cls(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
                                      const int32_t* item_map, int F1, int n_used, const int32_t* gpre,
                                      const void* rec, int G, int C, const int32_t* wword, uint32_t* out, int sw,
                                      int n_wg, const uint64_t* bm, int64_t Wp, hipStream_t st,
                                      const int32_t* bm_rows, const int32_t* g_dev, int cls) {
   if ((G <= 0 && !g_dev) || C <= 0 || ncols <= 0) return 0;
-  const int64_t n_acc = C;
+  const bool acc16 = (cls & 4) && !wword;   // two u16 counters per accumulator word
+  const int64_t n_acc = acc16 ? (C + 1) / 2 : C;
   const bool contig = !bm && !src;
   const size_t map_b = (contig && F1 <= kMapLdsMax) ? (size_t)(((int64_t)F1 * 2 + 15) & ~(int64_t)15) : 0;
   const size_t lds = (size_t)n_used * (sw + 2) * 8 + (size_t)((n_acc + 3) & ~(int64_t)3) * 4 + map_b;
@@ -1554,7 +1581,8 @@ FA_API int fa_hip_count_slab_rec_cls(const int64_t* roff, const int32_t* ranks, 
 #undef FA_REC_MODE
   if (!kern) return 1;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  const int dbg = (getenv("FA_SLAB_DEBUG") ? atoi(getenv("FA_SLAB_DEBUG")) : 0) | ((cls & 2) ? 4 : 0);
+  const int dbg = (getenv("FA_SLAB_DEBUG") ? atoi(getenv("FA_SLAB_DEBUG")) : 0) | ((cls & 2) ? 4 : 0) |
+                  (acc16 ? 8 : 0);
   hipLaunchKernelGGL(kern, dim3((unsigned)n_wg), dim3(kSlabThreads), lds, st, roff, ranks, src, ncols, item_map, F1,
                      n_used, gpre, (const int4*)rec, G, C, wword, out, bm, Wp, bm_rows, dbg, g_dev);
   FA_LAUNCH_RET();

@@ -1470,10 +1470,16 @@ def dl_lds_budget(F1: int) -> int:
     return _LDS_BYTES - _slab_map_lds(F1)
 
 
-def dl_slab_width(n_used: int, C: int, lds: int) -> tuple[int, int]:
-    """plan.cpp slab_width: (SW, accumulator capacity) for n_used items and C candidates."""
+# window-by-window levels count into two u16 counters per accumulator word (unit weights:
+# twice the candidates per pass, so about half the passes and slab copies)
+DL_ACC16 = os.environ.get("FA_DL_ACC16", "1") == "1"
+
+
+def dl_slab_width(n_used: int, C: int, lds: int, accb: int = 4) -> tuple[int, int]:
+    """plan.cpp slab_width: (SW, accumulator capacity) for n_used items and C candidates
+    (accb: LDS bytes per accumulator)."""
     for sw in (16, 32, 8, 4):
-        cap = int((lds - n_used * (sw + 2) * 8) // 4)
+        cap = int((lds - n_used * (sw + 2) * 8) // accb)
         if cap >= min(C, 8192) or (sw == 4 and cap >= 1024):
             return sw, cap
     return 0, 0
@@ -1543,7 +1549,8 @@ def dl_count_multipass(S: DeviceLevelState, F1: int, n_used: int, C: int, lds: i
     when bitmap row u is slab row u).  sup_frac: minimum support / rows (count_level's
     dense test).  Returns int32 [C] (not reduced across ranks), or None when no slab
     width fits the used items."""
-    sw, cap = dl_slab_width(n_used, min(C, 8192), lds)
+    acc16 = DL_ACC16 and wword is None
+    sw, cap = dl_slab_width(n_used, min(C, 8192), lds, 2 if acc16 else 4)
     if sw == 0:
         return None
     dense = wword is None and DENSE_MIN_ROWS > 0 and sup_frac * sw * 64 >= DENSE_MIN_ROWS
@@ -1565,11 +1572,12 @@ def dl_count_multipass(S: DeviceLevelState, F1: int, n_used: int, C: int, lds: i
         _native.check(lib.fa_hip_dl_plan_window(S.desc.ctypes.data, 1, _p(S.ctl), F1, _p(item_map), _p(rec), cap,
                                                 _p(part), part.numel(), _p(gpre), gpre.numel(), w0, w1, st),
                       "fa_hip_dl_plan_window")
-        lds_k = n_used * (sw + 2) * 8 + ((w1 - w0 + 3) & ~3) * 4
+        nacc = (w1 - w0 + 1) // 2 if acc16 else w1 - w0
+        lds_k = n_used * (sw + 2) * 8 + ((nacc + 3) & ~3) * 4
         n_wg = int(max(1, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds_k), 2))))
         _hip_call("fa_hip_count_slab_rec_cls", _p(roff), _p(ranks), _p(src), ncols, _p(item_map), F1, n_used,
                   _p(gpre), _p(rec), 0, w1 - w0, _p(wword), out.data_ptr() + 4 * w0, sw, n_wg, _p(bm),
-                  bm.stride(0), st, _p(bm_rows), _p(S.ctl) + 8 * 221, 2 if dense else 0)
+                  bm.stride(0), st, _p(bm_rows), _p(S.ctl) + 8 * 221, (2 if dense else 0) | (4 if acc16 else 0))
         npass += 1
     LAST_LEVEL_PLAN.clear()
     LAST_LEVEL_PLAN.update(kernel="slab_dev_multi", rows=int(roff.numel() - 1), used=n_used, sw=sw, cap=cap,

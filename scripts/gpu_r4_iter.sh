@@ -1,10 +1,12 @@
 #!/bin/bash
-# round 4 parameter sweep: headline bundle growth / dense test, T40 slab width order
+# round 4 scratch pass: u16 packed accumulators for window-by-window levels (FA_DL_ACC16)
 set -e -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/sweep
+O=$R/gpurun_out/acc16
 mkdir -p $O
 export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+  tests/test_gpu_device_levels.py tests/test_oracle_deep.py -m gpu > $O/tests.log 2>&1
 run() {   # name, env..., then bench args after --
   local name=$1; shift
   local envs=()
@@ -15,12 +17,7 @@ run() {   # name, env..., then bench args after --
   echo "$name" >> $O/names.txt
 }
 for i in 1 2; do
-  run T10_base FA_X=0 -- --steps 10 --warmup 2
-  run T10_g1 FA_BUNDLE_GROWTH=1.0 -- --steps 10 --warmup 2
-  run T10_g3 FA_BUNDLE_GROWTH=3.0 -- --steps 10 --warmup 2
-  run T10_dense FA_DENSE_MIN_ROWS=0.4 -- --steps 10 --warmup 2
+  run T40_acc16 FA_DL_ACC16=1 -- --config T40I10D100M --steps 2 --warmup 1
+  run T40_acc32 FA_DL_ACC16=0 -- --config T40I10D100M --steps 2 --warmup 1
 done
-for i in 1 2; do
-  run T40_base FA_X=0 -- --config T40I10D100M --steps 2 --warmup 1
-  run T40_sw32 FA_DL_SW_ORDER=32,16,8,4 -- --config T40I10D100M --steps 2 --warmup 1
-done
+run T10_acc16 FA_DL_ACC16=1 -- --steps 10 --warmup 2
