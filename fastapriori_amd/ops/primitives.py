@@ -1550,11 +1550,13 @@ def dl_count_multipass(S: DeviceLevelState, F1: int, n_used: int, C: int, lds: i
     dense test).  Returns int32 [C] (not reduced across ranks), or None when no slab
     width fits the used items."""
     acc16 = DL_ACC16 and wword is None
-    sw, cap = dl_slab_width(n_used, min(C, 8192), lds, 2 if acc16 else 4)
+    accb = 2 if acc16 else 4
+    sw, cap = dl_slab_width(n_used, min(C, 8192), lds, accb)
     if sw == 0:
         return None
     dense = wword is None and DENSE_MIN_ROWS > 0 and sup_frac * sw * 64 >= DENSE_MIN_ROWS
     cap = min(cap, C)
+    cap = -(-C // -(-C // cap))                      # equal windows
     st = _stream(ranks)
     lib = _native.hip()
     item_map = torch.empty(max(F1, 1), dtype=_I32, device=dev)
