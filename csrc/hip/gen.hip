@@ -431,21 +431,22 @@ FA_API int fa_hip_ag_chain(const int32_t* P0, int64_t n0, int m0, int F1, void* 
 // ---------------------------------------------------------------------------
 namespace fa {
 
-__device__ int64_t d_slab_cap(int64_t n_used, int64_t C, double lds) {
+// accb: LDS bytes per accumulator (4, or 2 for count.hip's packed u16 counters)
+__device__ int64_t d_slab_cap(int64_t n_used, int64_t C, double lds, double accb) {
   const int sws[4] = {16, 32, 8, 4};   // plan.cpp slab_width order
   for (int q = 0; q < 4; ++q) {
     const int sw = sws[q];
-    const int64_t cap = (int64_t)((lds - (double)n_used * (sw + 2) * 8) / 4);
+    const int64_t cap = (int64_t)((lds - (double)n_used * (sw + 2) * 8) / accb);
     if (cap >= (C < 8192 ? C : 8192) || (sw == 4 && cap >= 1024)) return cap;
   }
   return 0;
 }
 
-__device__ int64_t d_total_limit(int64_t n_used, double lds) {
+__device__ int64_t d_total_limit(int64_t n_used, double lds, double accb) {
   int64_t lo = 0, hi = (int64_t)1 << 31;
   while (lo < hi) {
     const int64_t mid = (lo + hi + 1) / 2;
-    if (mid <= d_slab_cap(n_used, mid, lds)) lo = mid; else hi = mid - 1;
+    if (mid <= d_slab_cap(n_used, mid, lds, accb)) lo = mid; else hi = mid - 1;
   }
   return lo;
 }
@@ -479,11 +480,11 @@ __global__ void k_agd_setup(long long* __restrict__ c, int64_t n1, int64_t total
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   int64_t n_used = 0;
   for (int q = 0; q < MW; ++q) n_used += __popc(mark[q]);
-  c[0] = total > d_slab_cap(n_used, total, lds) ? 1 : 0;   // level k alone needs several passes
+  c[0] = total > d_slab_cap(n_used, total, lds, 4.0) ? 1 : 0;   // level k alone needs several passes
   c[1] = 1;
   c[2] = total;
   c[3] = last;
-  c[4] = d_total_limit(n_used, lds);
+  c[4] = d_total_limit(n_used, lds, 4.0);
   c[9] = n1;
 }
 
@@ -791,7 +792,7 @@ __global__ __launch_bounds__(256) void k_dl_mark(const int32_t* __restrict__ row
 }
 
 // n_used, and whether level 0 alone exceeds one accumulator pass
-__global__ __launch_bounds__(64) void k_dl_post0(long long* __restrict__ c, double lds, int w32) {
+__global__ __launch_bounds__(64) void k_dl_post0(long long* __restrict__ c, double lds, double accb, int w32) {
   if (blockIdx.x != 0) return;
   const uint32_t* mk = reinterpret_cast<const uint32_t*>(c + kDlBits);
   uint32_t part = 0;
@@ -799,20 +800,20 @@ __global__ __launch_bounds__(64) void k_dl_post0(long long* __restrict__ c, doub
   const int64_t n_used = (int64_t)wave_sum_u32(part);
   if (threadIdx.x != 0) return;
   c[6] = n_used;
-  if (c[1] == 1 && c[40] > d_slab_cap(n_used, c[40], lds)) { c[5] = 1; c[0] = 1; }
+  if (c[1] == 1 && c[40] > d_slab_cap(n_used, c[40], lds, accb)) { c[5] = 1; c[0] = 1; }
 }
 
 // acceptance of speculative level l >= 1 (same rule as k_agd_scan_decide, with the
 // exact one-pass test total + C <= slab capacity(n_used, total + C))
 __global__ __launch_bounds__(1024) void k_dl_decide(const int32_t* __restrict__ cnt, int64_t* __restrict__ off,
                                                      long long* __restrict__ c, int l, double growth, int64_t c_bound,
-                                                     double lds) {
+                                                     double lds, double accb) {
   if (c[0]) return;
   int64_t g = 0;
   const int64_t C = agd_block_scan(cnt, off, c[8 + l], &g);
   if (threadIdx.x != 0) return;
   const int64_t total = c[2], last = c[3];
-  if (C == 0 || (double)C > growth * (double)last || C > c_bound || total + C > d_slab_cap(c[6], total + C, lds)) {
+  if (C == 0 || (double)C > growth * (double)last || C > c_bound || total + C > d_slab_cap(c[6], total + C, lds, accb)) {
     c[0] = 1;
     return;
   }
@@ -883,12 +884,12 @@ __global__ __launch_bounds__(256) void k_dl_rows(const int32_t* __restrict__ P, 
 // (without it the caller queues fa_hip_dl_more and reads everything once).
 // c_bound: the largest C_0 the level may have (one accumulator pass); a larger
 // level is reported as multi (ctl[5]) without its rows.  lds: LDS bytes the slab
-// kernel has for slab + accumulators.  info (int64 out): 0 ws bytes used,
+// kernel has for slab + accumulators; accb: bytes per accumulator (4, or 2: u16).  info (int64 out): 0 ws bytes used,
 // 1 cnt (ext ids at cnt + n), 2 off, 3 candidate rows [C_0][m0 + 1].
 // Returns 0, 1 (bad arguments) or 5 (ws too small: info[0] = bytes needed).
 FA_API int fa_hip_dl_level0(const int32_t* P0, const long long* n_src, int64_t n_const, int64_t n_bound, int m0,
                             int F1, void* ws, int64_t ws_bytes, long long* ctl, long long* ctl_host,
-                            int64_t c_bound, double lds, int64_t* info, int sync, hipStream_t st) {
+                            int64_t c_bound, double lds, double accb, int64_t* info, int sync, hipStream_t st) {
   if (m0 < 2 || F1 > kAgMaxF1 || F1 < 1 || n_bound < 0 || c_bound < 1) return 1;
   auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
   const int nw = (F1 + 63) / 64;
@@ -932,7 +933,7 @@ FA_API int fa_hip_dl_level0(const int32_t* P0, const long long* n_src, int64_t n
   const int w32 = (F1 + 31) / 32;
   hipLaunchKernelGGL(k_dl_mark, dim3((unsigned)std::min<int64_t>((c_bound * (m0 + 1) + 255) / 256, 1024)), dim3(256),
                      0, st, rows, m0 + 1, ctl, w32);
-  hipLaunchKernelGGL(k_dl_post0, dim3(1), dim3(64), 0, st, ctl, lds, w32);
+  hipLaunchKernelGGL(k_dl_post0, dim3(1), dim3(64), 0, st, ctl, lds, accb, w32);
   if (sync) {
     (void)hipMemcpyAsync(ctl_host, ctl, sizeof(long long) * kDlCtl, hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return 7;
@@ -978,17 +979,19 @@ struct DlPost {
   int64_t done, sw, cap, n_wg, C, trim;
   // prefix slab rows of levels with prefixes past 12 ids (levels.hip gpre), int32 [gpre_cap]
   int32_t* gpre; int64_t gpre_cap;
+  // LDS bytes per accumulator: 4, or 2 (unit weights: count.hip's packed u16 counters)
+  double accb;
 };
-static_assert(sizeof(DlPost) == 30 * 8, "DlPost layout (ops.primitives.DlPostC)");
+static_assert(sizeof(DlPost) == 31 * 8, "DlPost layout (ops.primitives.DlPostC)");
 
 FA_API int fa_hip_dl_plan(const int64_t* desc, int L, long long* ctl, int F1, int32_t* item_map, void* rec,
                           int64_t max_pieces, int32_t* part, int64_t part_cap, int32_t* gpre, int64_t gpre_cap,
                           hipStream_t st);
-FA_API int fa_hip_count_slab_rec(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
-                                 const int32_t* item_map, int F1, int n_used, const int32_t* gpre, const void* rec,
-                                 int G, int C, const int32_t* wword, uint32_t* out, int sw, int n_wg,
-                                 const uint64_t* bm, int64_t Wp, hipStream_t st, const int32_t* bm_rows,
-                                 const int32_t* g_dev);
+FA_API int fa_hip_count_slab_rec_cls(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
+                                     const int32_t* item_map, int F1, int n_used, const int32_t* gpre,
+                                     const void* rec, int G, int C, const int32_t* wword, uint32_t* out, int sw,
+                                     int n_wg, const uint64_t* bm, int64_t Wp, hipStream_t st,
+                                     const int32_t* bm_rows, const int32_t* g_dev, int cls);
 
 // P[Binom(L, p) >= k] (the regularised incomplete beta of FastApriori._trim_worth_it)
 static double binom_tail(int L, double p, int k) {
@@ -1018,7 +1021,7 @@ static void dl_post(DlPost* P, const int64_t* desc, int L, long long* ctl, const
   int sw = 0;
   int64_t cap = 0;
   for (int w : {16, 32, 8, 4}) {
-    cap = (int64_t)((P->lds_budget - (double)n_used * (w + 2) * 8) / 4);
+    cap = (int64_t)((P->lds_budget - (double)n_used * (w + 2) * 8) / P->accb);
     if (cap >= std::min<int64_t>(C, 8192) || (w == 4 && cap >= 1024)) { sw = w; break; }
   }
   if (sw == 0 || C > cap) return;
@@ -1058,18 +1061,21 @@ static void dl_post(DlPost* P, const int64_t* desc, int L, long long* ctl, const
   if (P->trim) return;                                      // the caller trims, then counts
   const int64_t W = (P->ncols + 63) / 64, nslabs = (W + sw - 1) / sw;
   const int64_t map_b = F1 <= 8192 ? (((int64_t)F1 * 2 + 15) & ~(int64_t)15) : 0;
-  const int64_t lds_k = n_used * (sw + 2) * 8 + ((C + 3) & ~(int64_t)3) * 4 + map_b;
+  const bool acc16 = P->accb == 2.0 && !P->wword;
+  const int64_t nacc = acc16 ? (C + 1) / 2 : C;
+  const int64_t lds_k = n_used * (sw + 2) * 8 + ((nacc + 3) & ~(int64_t)3) * 4 + map_b;
   const int64_t per_cu = std::min<int64_t>(std::max<int64_t>(1, (int64_t)P->lds_kernel / std::max<int64_t>(lds_k, 1)), 2);
   P->n_wg = std::max<int64_t>(1, std::min<int64_t>(nslabs, 256 * per_cu));
-  if (fa_hip_count_slab_rec(P->roff, P->ranks, P->src, P->ncols, P->item_map, F1, (int)n_used, P->gpre, P->rec, 0,
-                            (int)C, P->wword, P->out, sw, (int)P->n_wg, nullptr, 0, st, nullptr,
-                            reinterpret_cast<const int32_t*>(ctl + 221)) != 0)
+  if (fa_hip_count_slab_rec_cls(P->roff, P->ranks, P->src, P->ncols, P->item_map, F1, (int)n_used, P->gpre, P->rec,
+                                0, (int)C, P->wword, P->out, sw, (int)P->n_wg, nullptr, 0, st, nullptr,
+                                reinterpret_cast<const int32_t*>(ctl + 221), acc16 ? 4 : 0) != 0)
     return;
   P->done = 2;
 }
 
 FA_API int fa_hip_dl_more(int F1, void* ws, int64_t ws_bytes, int64_t ws_used, long long* ctl, long long* ctl_host,
-                          double growth, int max_levels, double lds, int64_t n1_bound, int64_t* desc, int64_t* info,
+                          double growth, int max_levels, double lds, double accb, int64_t n1_bound, int64_t* desc,
+                          int64_t* info,
                           hipStream_t st, void* post) {
   using namespace fa;
   auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
@@ -1077,7 +1083,7 @@ FA_API int fa_hip_dl_more(int F1, void* ws, int64_t ws_bytes, int64_t ws_used, l
   char* const w0 = static_cast<char*>(ws);
   char* w = w0 + ws_used;
   const int LM = std::min(max_levels, 31);
-  const int64_t acc_max = (int64_t)(lds / 4);
+  const int64_t acc_max = (int64_t)(lds / accb);
   int64_t nb = n1_bound;
   int m = (int)desc[4] + 1;
   const int32_t* P = reinterpret_cast<const int32_t*>((intptr_t)desc[3]);
@@ -1142,7 +1148,7 @@ FA_API int fa_hip_dl_more(int F1, void* ws, int64_t ws_bytes, int64_t ws_used, l
 #define FA_DLR_CNT(N) FA_DLR(false, N)
 #define FA_DLR_EMIT(N) FA_DLR(true, N)
       FA_AG_NWL_SWITCH(nw, FA_DLR_CNT)
-      hipLaunchKernelGGL(k_dl_decide, dim3(1), dim3(1024), 0, st, lv[l].cnt, lv[l].off, ctl, l, growth, cb, lds);
+      hipLaunchKernelGGL(k_dl_decide, dim3(1), dim3(1024), 0, st, lv[l].cnt, lv[l].off, ctl, l, growth, cb, lds, accb);
       FA_AG_NWL_SWITCH(nw, FA_DLR_EMIT)
 #undef FA_DLR_EMIT
 #undef FA_DLR_CNT

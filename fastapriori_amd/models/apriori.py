@@ -350,7 +350,10 @@ class FastApriori:
         S = Pm.device_level_state(self._dev)
         F1 = self._F1
         lds = Pm.dl_lds_budget(F1)
-        c_bound = int(lds // 4)
+        # LDS bytes per slab accumulator: packed u16 counters for unit weights (the rows'
+        # weighting does not change while mining: trimming keeps the dedup layout)
+        accb = self._dl_accb = 2.0 if Pm.DL_ACC16 and db["wword"] is None else 4.0
+        c_bound = int(lds // accb)
         st = torch.cuda.current_stream(self._dev).cuda_stream
         f2 = self._f2_dev
         m0, k = 2, 3
@@ -390,7 +393,7 @@ class FastApriori:
                     self._dl_stage(S, pend)
                 with roctx_range("gen"):
                     c = Pm.dl_bundle_gen(S, P0, n_src, n_const, n_bound, m0, F1, c_bound, lds, BUNDLE_GROWTH, max_lv,
-                                         st, post=post)
+                                         st, post=post, accb=accb)
                 if c[4]:
                     raise RuntimeError(f"device bundle at level {k}: |F_{k - 1}| exceeds its bound {n_bound}")
                 if c[7]:
@@ -421,7 +424,7 @@ class FastApriori:
                         plan = Pm.dl_plan_from_post(S, n_used)
                     else:
                         with roctx_range("plan"):
-                            plan = Pm.dl_plan(S, L, F1, n_used, C, lds, self._dev)
+                            plan = Pm.dl_plan(S, L, F1, n_used, C, lds, self._dev, accb)
                     with tm.phase(f"trim{k}"), roctx_range("trim"):
                         self._trim(db, used, k, C, decided=bool(done == 1 and S.post.trim))
                     with tm.phase("count"), roctx_range("count"):
@@ -461,14 +464,15 @@ class FastApriori:
         C0 = int(c[40])
         if int(c[1]) == 0:
             # the bounded generation reported the size only: again, one level, room for C0
-            c = Pm.dl_bundle_gen(S, P0, n_src, n_const, n_bound, m0, F1, C0, lds, BUNDLE_GROWTH, 1, st)
+            c = Pm.dl_bundle_gen(S, P0, n_src, n_const, n_bound, m0, F1, C0, lds, BUNDLE_GROWTH, 1, st,
+                                 accb=self._dl_accb)
             if c[4] or c[7] or int(c[1]) != 1 or int(c[40]) != C0:
                 raise RuntimeError(f"device level {k}: regeneration of {C0} candidates disagrees ({c[:8]})")
         nwd = (F1 + 63) // 64
         bits = np.unpackbits(c[Pm.DL_BITS:Pm.DL_BITS + nwd].view(np.uint8), bitorder="little")[:F1]
         used = np.flatnonzero(bits)
         n_used = int(used.size)
-        wide = Pm.dl_slab_width(n_used, min(C0, 8192), lds)[0] == 0
+        wide = Pm.dl_slab_width(n_used, min(C0, 8192), lds, self._dl_accb)[0] == 0
         with self._timer.phase(f"trim{k}"), roctx_range("trim"):
             self._trim(db, used, k, C0)
         if wide:
@@ -535,6 +539,7 @@ class FastApriori:
         P.src = db["src"].data_ptr() if db["src"] is not None else None
         P.wword = db["wword"].data_ptr() if db["wword"] is not None else None
         P.ncols, P.lds_kernel, P.lds_budget = int(db["ncols"]), float(Pm._LDS_BYTES), float(lds)
+        P.accb = self._dl_accb
         c1 = np.ascontiguousarray(db["c1"], dtype=np.int64)
         alive = np.ascontiguousarray(db["alive"], dtype=np.uint8)
         hist = db.get("len_hist")

@@ -86,8 +86,9 @@ _HIP_SIGS = {
     "fa_hip_count_slab_rec_cls": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, C.c_int, vp, vp, C.c_int, C.c_int, vp,
                                             vp, C.c_int, C.c_int, vp, i64, vp, vp, vp, C.c_int]),
     # device-resident level bundles (gen.hip fa_hip_dl_*, levels.hip)
-    "fa_hip_dl_level0": (C.c_int, [vp, vp, i64, i64, C.c_int, C.c_int, vp, i64, vp, vp, i64, dbl, vp, C.c_int, vp]),
-    "fa_hip_dl_more": (C.c_int, [C.c_int, vp, i64, i64, vp, vp, dbl, C.c_int, dbl, i64, vp, vp, vp, vp]),
+    "fa_hip_dl_level0": (C.c_int, [vp, vp, i64, i64, C.c_int, C.c_int, vp, i64, vp, vp, i64, dbl, dbl, vp, C.c_int,
+                                   vp]),
+    "fa_hip_dl_more": (C.c_int, [C.c_int, vp, i64, i64, vp, vp, dbl, C.c_int, dbl, dbl, i64, vp, vp, vp, vp]),
     "fa_hip_dl_plan": (C.c_int, [vp, C.c_int, vp, C.c_int, vp, vp, i64, vp, i64, vp, i64, vp]),
     "fa_hip_dl_gpre_need": (i64, [vp, C.c_int]),
     "fa_hip_dl_plan_window": (C.c_int, [vp, C.c_int, vp, C.c_int, vp, vp, i64, vp, i64, vp, i64, i64, i64, vp]),

@@ -1410,7 +1410,7 @@ class DlPostC(ctypes.Structure):
                [(n, ctypes.c_void_p) for n in ("c1", "alive", "len_hist")] + \
                [(n, ctypes.c_int64) for n in ("T", "nnz", "trim_min_rows", "trim_ok", "k",
                                                "done", "sw", "cap", "n_wg", "C", "trim")] + \
-               [("gpre", ctypes.c_void_p), ("gpre_cap", ctypes.c_int64)]
+               [("gpre", ctypes.c_void_p), ("gpre_cap", ctypes.c_int64), ("accb", ctypes.c_double)]
 
 
 class DeviceLevelState:
@@ -1470,8 +1470,9 @@ def dl_lds_budget(F1: int) -> int:
     return _LDS_BYTES - _slab_map_lds(F1)
 
 
-# window-by-window levels count into two u16 counters per accumulator word (unit weights:
-# twice the candidates per pass, so about half the passes and slab copies)
+# device-loop levels (one-pass bundles and window-by-window levels) count into two u16
+# counters per accumulator word when the rows have unit weights: twice the candidates per
+# pass, so wider slabs fit beside the accumulators and multi-pass levels need half the passes
 DL_ACC16 = os.environ.get("FA_DL_ACC16", "1") == "1"
 
 
@@ -1486,17 +1487,19 @@ def dl_slab_width(n_used: int, C: int, lds: int, accb: int = 4) -> tuple[int, in
 
 
 def dl_bundle_gen(S: DeviceLevelState, P0: int, n_src: int | None, n_const: int, n_bound: int, m0: int, F1: int,
-                  c_bound: int, lds: int, growth: float, max_levels: int, stream: int, post: bool = False) -> np.ndarray:
+                  c_bound: int, lds: int, growth: float, max_levels: int, stream: int, post: bool = False,
+                  accb: float = 4.0) -> np.ndarray:
     """Candidates of a device bundle: level 0 from F_{k-1} rows P0 and the speculative
     levels 1 .. max_levels-1 (accepted on the device), all queued before ONE
-    synchronisation.  Returns the control block (host int64 [DL_CTL]); S.desc[:L]
+    synchronisation (accb: LDS bytes per slab accumulator, 2 = packed u16 counters).  Returns the control block (host int64 [DL_CTL]); S.desc[:L]
     describes the accepted levels (L = ctl[1])."""
     lib = _native.hip()
     info = np.zeros(2, dtype=np.int64)
     for _ in range(6):
         S.desc[:] = 0
         rc = lib.fa_hip_dl_level0(P0, n_src, n_const, n_bound, m0, F1, _p(S.ws), S.ws.numel(), _p(S.ctl),
-                                  _p(S.ctl_h), c_bound, float(lds), S.info.ctypes.data, int(max_levels <= 1), stream)
+                                  _p(S.ctl_h), c_bound, float(lds), float(accb), S.info.ctypes.data,
+                                  int(max_levels <= 1), stream)
         if rc == 5:
             S.grow(int(S.info[0]))
             continue
@@ -1508,7 +1511,8 @@ def dl_bundle_gen(S: DeviceLevelState, P0: int, n_src: int | None, n_const: int,
             return c.copy()
         S.post.done = 0
         rc = lib.fa_hip_dl_more(F1, _p(S.ws), S.ws.numel(), int(S.info[0]), _p(S.ctl), _p(S.ctl_h), float(growth),
-                                int(max_levels), float(lds), int(c_bound), S.desc.ctypes.data, info.ctypes.data,
+                                int(max_levels), float(lds), float(accb), int(c_bound), S.desc.ctypes.data,
+                                info.ctypes.data,
                                 stream, ctypes.addressof(S.post) if post else None)
         if rc == 5:
             S.grow(int(info[0]))
@@ -1518,13 +1522,13 @@ def dl_bundle_gen(S: DeviceLevelState, P0: int, n_src: int | None, n_const: int,
     raise RuntimeError("device bundle generation: workspace sizing did not converge")
 
 
-def dl_plan(S: DeviceLevelState, L: int, F1: int, n_used: int, C: int, lds: int, dev) -> dict:
+def dl_plan(S: DeviceLevelState, L: int, F1: int, n_used: int, C: int, lds: int, dev, accb: float = 4.0) -> dict:
     """Device piece plan of a bundle's C candidates (levels.hip fa_hip_dl_plan), queued
     on the stream right after the generator's synchronisation: it depends on the
     candidates only, not on the row layout, so the host's trimming decision runs
     while it executes.  Returns the plan for dl_count."""
     st = torch.cuda.current_stream(dev).cuda_stream
-    sw, cap = dl_slab_width(n_used, C, lds)
+    sw, cap = dl_slab_width(n_used, C, lds, accb)
     if sw == 0 or C > cap:
         raise RuntimeError(f"device bundle of {C} candidates over {n_used} items does not fit one pass")
     item_map = torch.empty(max(F1, 1), dtype=_I32, device=dev)
@@ -1537,7 +1541,7 @@ def dl_plan(S: DeviceLevelState, L: int, F1: int, n_used: int, C: int, lds: int,
     _native.check(lib.fa_hip_dl_plan(S.desc.ctypes.data, L, _p(S.ctl), F1, _p(item_map), _p(rec), C,
                                      _p(part), part.numel(), _p(gpre), gpre.numel(), st), "fa_hip_dl_plan")
     out = torch.zeros(C, dtype=_I32, device=dev)
-    return dict(sw=sw, cap=cap, item_map=item_map, rec=rec, out=out, n_used=n_used, C=C, gpre=gpre)
+    return dict(sw=sw, cap=cap, item_map=item_map, rec=rec, out=out, n_used=n_used, C=C, gpre=gpre, accb=accb)
 
 
 def dl_count_multipass(S: DeviceLevelState, F1: int, n_used: int, C: int, lds: int, roff, ranks, src, ncols: int,
@@ -1593,7 +1597,7 @@ def dl_plan_from_post(S: DeviceLevelState, n_used: int) -> dict:
     C = int(P.C)
     out = b["out"][:C]
     return dict(sw=int(P.sw), cap=int(P.cap), item_map=b["item_map"], rec=b["rec"], out=out, n_used=n_used, C=C,
-                gpre=b["gpre"])
+                gpre=b["gpre"], accb=float(P.accb))
 
 
 def dl_count(S: DeviceLevelState, plan: dict, roff, ranks, src, ncols: int, F1: int, wword) -> torch.Tensor:
@@ -1604,11 +1608,13 @@ def dl_count(S: DeviceLevelState, plan: dict, roff, ranks, src, ncols: int, F1: 
     item_map, rec, out = plan["item_map"], plan["rec"], plan["out"]
     W = (ncols + 63) // 64
     nslabs = (W + sw - 1) // sw
-    lds_k = n_used * (sw + 2) * 8 + ((C + 3) & ~3) * 4 + _slab_map_lds(F1)
+    acc16 = plan.get("accb", 4.0) == 2.0 and wword is None
+    nacc = (C + 1) // 2 if acc16 else C
+    lds_k = n_used * (sw + 2) * 8 + ((nacc + 3) & ~3) * 4 + _slab_map_lds(F1)
     n_wg = int(max(1, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds_k), 2))))
-    _hip_call("fa_hip_count_slab_rec", _p(roff), _p(ranks), _p(src), ncols, _p(item_map), F1, n_used,
+    _hip_call("fa_hip_count_slab_rec_cls", _p(roff), _p(ranks), _p(src), ncols, _p(item_map), F1, n_used,
               _p(plan.get("gpre")), _p(rec), 0, C, _p(wword), _p(out), sw, n_wg, None, 0, st, None,
-              _p(S.ctl) + 8 * 221)
+              _p(S.ctl) + 8 * 221, 4 if acc16 else 0)
     LAST_LEVEL_PLAN.clear()
     LAST_LEVEL_PLAN.update(kernel="slab_dev", rows=int(roff.numel() - 1), used=n_used, sw=sw, cap=cap, passes=1,
                            pieces=-1, slab_reads=0, m=-1, C=C)
