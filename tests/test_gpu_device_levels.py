@@ -77,11 +77,13 @@ def test_multipass_level_stays_on_device(monkeypatch):
     _same(got2, ref)
 
 
-def _multipass_lds(ref) -> int:
-    """An LDS budget in which F1 used items fit 4-word slabs (slab rows 48 B) with room
-    for ~|F_3| / 4 accumulators: level 3 then needs several passes."""
+def _multipass_lds(ref, accb: int = 4) -> int:
+    """An LDS budget in which level 3's used items (at most the items of F_2) fit 4-word
+    slabs (slab rows 48 B) with room for ~|F_3| / 4 accumulators of accb bytes: level 3
+    then needs several passes."""
     F1, F3 = len(ref.levels[0]), len(ref.levels[2])
-    return F1 * 48 + 4 * max(1024, F3 // 4) + 2 * F1 + 256
+    U = int(np.unique(np.asarray(ref.levels[1])).size)
+    return U * 48 + accb * max(1024, F3 // 4) + 2 * F1 + 256
 
 
 def test_small_lds_forces_device_multipass(monkeypatch):
@@ -90,8 +92,9 @@ def test_small_lds_forces_device_multipass(monkeypatch):
     import fastapriori_amd.ops.primitives as prim
     cpu = generate_shard(200_000, Comm(), "cpu", 10.0, 4.0, 2000, 1000, 4)
     ref, _ = _mine(cpu, 0.002)
-    monkeypatch.setattr(prim, "_LDS_BYTES", _multipass_lds(ref))
     for dd in ("off", "on"):
+        # unit weights count into packed u16 accumulators (2 B each)
+        monkeypatch.setattr(prim, "_LDS_BYTES", _multipass_lds(ref, 2 if dd == "off" and prim.DL_ACC16 else 4))
         got, st = _mine(cpu.to(DEV), 0.002, dedup=dd, trim_min_rows=0)
         assert st.get("device_multipass", 0) >= 1, st
         _same(got, ref)
