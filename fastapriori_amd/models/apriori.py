@@ -351,8 +351,11 @@ class FastApriori:
         F1 = self._F1
         lds = Pm.dl_lds_budget(F1)
         # LDS bytes per slab accumulator: packed u16 counters for unit weights (the rows'
-        # weighting does not change while mining: trimming keeps the dedup layout)
-        accb = self._dl_accb = 2.0 if Pm.DL_ACC16 and db["wword"] is None else 4.0
+        # weighting does not change while mining: trimming keeps the dedup layout) in
+        # window-by-window levels, and in one-pass bundles with FA_DL_ACC16_BUNDLES=1
+        unit = db["wword"] is None
+        self._dl_mp_accb = 2.0 if Pm.DL_ACC16 and unit else 4.0
+        accb = self._dl_accb = 2.0 if Pm.DL_ACC16_BUNDLES and unit else 4.0
         c_bound = int(lds // accb)
         st = torch.cuda.current_stream(self._dev).cuda_stream
         f2 = self._f2_dev
@@ -472,7 +475,7 @@ class FastApriori:
         bits = np.unpackbits(c[Pm.DL_BITS:Pm.DL_BITS + nwd].view(np.uint8), bitorder="little")[:F1]
         used = np.flatnonzero(bits)
         n_used = int(used.size)
-        wide = Pm.dl_slab_width(n_used, min(C0, 8192), lds, self._dl_accb)[0] == 0
+        wide = Pm.dl_slab_width(n_used, min(C0, 8192), lds, self._dl_mp_accb)[0] == 0
         with self._timer.phase(f"trim{k}"), roctx_range("trim"):
             self._trim(db, used, k, C0)
         if wide:

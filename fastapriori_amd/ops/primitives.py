@@ -1470,10 +1470,13 @@ def dl_lds_budget(F1: int) -> int:
     return _LDS_BYTES - _slab_map_lds(F1)
 
 
-# device-loop levels (one-pass bundles and window-by-window levels) count into two u16
-# counters per accumulator word when the rows have unit weights: twice the candidates per
-# pass, so wider slabs fit beside the accumulators and multi-pass levels need half the passes
+# window-by-window device levels count into two u16 counters per accumulator word when the
+# rows have unit weights: twice the candidates per pass, half the passes.  One-pass bundles
+# can too (FA_DL_ACC16_BUNDLES=1), off by default: the larger capacity makes the generator
+# pick 16-word slabs for level 3 alone and cut the later bundles differently, T10I4D100M
+# 43.2 vs 42.3 ms (docs/PERF_HISTORY.md)
 DL_ACC16 = os.environ.get("FA_DL_ACC16", "1") == "1"
+DL_ACC16_BUNDLES = os.environ.get("FA_DL_ACC16_BUNDLES", "0") == "1"
 
 
 def dl_slab_width(n_used: int, C: int, lds: int, accb: int = 4) -> tuple[int, int]:

@@ -2,10 +2,10 @@
 # round 4 scratch pass: packed u16 accumulators in one-pass device bundles (FA_DL_ACC16)
 set -e -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/acc16b
+O=$R/gpurun_out/acc16c
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu > $O/tests.log 2>&1
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_device_levels.py tests/test_oracle_deep.py -m gpu > $O/tests.log 2>&1
 run() {   # name, env..., then bench args after --
   local name=$1; shift
   local envs=()
@@ -15,13 +15,5 @@ run() {   # name, env..., then bench args after --
   tail -1 $O/$name.json >> $O/all.jsonl
   echo "$name" >> $O/names.txt
 }
-for i in 1 2; do
-  run T10_acc16 FA_DL_ACC16=1 -- --steps 10 --warmup 2
-  run T10_acc32 FA_DL_ACC16=0 -- --steps 10 --warmup 2
-done
-for i in 1 2; do
-  run T40_acc16 FA_DL_ACC16=1 -- --config T40I10D100M --steps 2 --warmup 1
-  run T40_acc32 FA_DL_ACC16=0 -- --config T40I10D100M --steps 2 --warmup 1
-done
-run T10K_acc16 FA_DL_ACC16=1 -- --config T10I4D100K --steps 20 --warmup 3
-run T10K_acc32 FA_DL_ACC16=0 -- --config T10I4D100K --steps 20 --warmup 3
+run T10 FA_X=0 -- --steps 10 --warmup 2
+run T40 FA_X=0 -- --config T40I10D100M --steps 2 --warmup 1
