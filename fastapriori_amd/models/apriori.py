@@ -414,8 +414,10 @@ class FastApriori:
                 Cs = S.desc[:L, 6].copy()
                 C = int(Cs.sum())
                 done = int(S.post.done) if post else 0
+                sw = int(S.post.sw) if done else 0
                 if multi is not None:
                     cnt = multi[1]
+                    sw = int(Pm.LAST_LEVEL_PLAN.get("sw", 0))
                 elif done == 2:
                     # planned and counted by fa_hip_dl_more's post step (no trim due)
                     cnt = S.post_bufs["out"][:C]
@@ -432,6 +434,7 @@ class FastApriori:
                         self._trim(db, used, k, C, decided=bool(done == 1 and S.post.trim))
                     with tm.phase("count"), roctx_range("count"):
                         cnt = Pm.dl_count(S, plan, db["roff"], db["ranks"], db["src"], db["ncols"], F1, db["wword"])
+                    sw = int(plan["sw"])
                 with tm.phase("count"), roctx_range("count"):
                     self.comm.all_reduce_(cnt)
                     rows_a, cnt_a, ro, co = Pm.dl_threshold(S, L, cnt, mc, k)
@@ -439,7 +442,7 @@ class FastApriori:
             hbm_rows = (db["ranks"].numel() * db["ranks"].element_size()
                         + db["roff"].numel() * db["roff"].element_size())
             pend.append(dict(k=k, L=L, m0=m0, C=Cs, rows=rows_a, cnt=cnt_a, ro=ro, co=co, hbm_rows=int(hbm_rows),
-                             n_par=S.desc[:L, 5].copy(),
+                             n_par=S.desc[:L, 5].copy(), sw=sw, used=n_used, T=int(db["roff"].numel() - 1),
                              ms=(time.perf_counter() - t0) * 1e3, bytes=self._bytes_moved() - b0,
                              G=c[72:72 + L].copy()))
             P0 = rows_a.data_ptr() + 4 * int(ro[L - 1])
@@ -636,7 +639,8 @@ class FastApriori:
                 self._level_recs.append((dict(phase="level", k=kk, candidates=int(p["C"][l]), frequent=F,
                                               ms=p["ms"] * share, groups=int(p["G"][l]), bundled_with=p["k"],
                                               bytes_reduced=int(p["bytes"] * share), kernel="slab_rec_dev",
-                                              hbm_bytes_est=hbm, _share=share),
+                                              hbm_bytes_est=hbm, slab_words=p["sw"], used_items=p["used"],
+                                              rows=p["T"], _share=share),
                                          f"level{p['k']}"))
 
     def _run_deferred(self) -> None:

@@ -15,5 +15,6 @@ run() {   # name, env..., then bench args after --
   tail -1 $O/$name.json >> $O/all.jsonl
   echo "$name" >> $O/names.txt
 }
-run T10 FA_X=0 -- --steps 10 --warmup 2
-run T40 FA_X=0 -- --config T40I10D100M --steps 2 --warmup 1
+run T10 FA_METRICS=$O/m_T10.jsonl -- --steps 3 --warmup 1
+run T10_b16 FA_DL_ACC16_BUNDLES=1 FA_METRICS=$O/m_T10_b16.jsonl -- --steps 3 --warmup 1
+run T40 FA_METRICS=$O/m_T40.jsonl -- --config T40I10D100M --steps 1 --warmup 1
