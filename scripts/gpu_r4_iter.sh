@@ -2,10 +2,10 @@
 # round 4 scratch pass: packed u16 accumulators in one-pass device bundles (FA_DL_ACC16)
 set -e -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/acc16c
+O=$R/gpurun_out/mincap
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_device_levels.py tests/test_oracle_deep.py -m gpu > $O/tests.log 2>&1
+FA_DL_MP_MIN_CAP=2048 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_device_levels.py tests/test_oracle_deep.py -m gpu > $O/tests.log 2>&1
 run() {   # name, env..., then bench args after --
   local name=$1; shift
   local envs=()
@@ -15,6 +15,8 @@ run() {   # name, env..., then bench args after --
   tail -1 $O/$name.json >> $O/all.jsonl
   echo "$name" >> $O/names.txt
 }
-run T10 FA_METRICS=$O/m_T10.jsonl -- --steps 3 --warmup 1
-run T10_b16 FA_DL_ACC16_BUNDLES=1 FA_METRICS=$O/m_T10_b16.jsonl -- --steps 3 --warmup 1
-run T40 FA_METRICS=$O/m_T40.jsonl -- --config T40I10D100M --steps 1 --warmup 1
+for i in 1 2; do
+  run T40_c8k FA_X=0 -- --config T40I10D100M --steps 2 --warmup 1
+  run T40_c4k FA_DL_MP_MIN_CAP=4096 -- --config T40I10D100M --steps 2 --warmup 1
+  run T40_c2k FA_DL_MP_MIN_CAP=2048 -- --config T40I10D100M --steps 2 --warmup 1
+done
