@@ -1477,7 +1477,6 @@ def dl_lds_budget(F1: int) -> int:
 # 43.2 vs 42.3 ms (docs/PERF_HISTORY.md)
 DL_ACC16 = os.environ.get("FA_DL_ACC16", "1") == "1"
 DL_ACC16_BUNDLES = os.environ.get("FA_DL_ACC16_BUNDLES", "0") == "1"
-DL_MP_MIN_CAP = int(os.environ.get("FA_DL_MP_MIN_CAP", "8192"))
 
 
 def dl_slab_width(n_used: int, C: int, lds: int, accb: int = 4) -> tuple[int, int]:
@@ -1559,9 +1558,7 @@ def dl_count_multipass(S: DeviceLevelState, F1: int, n_used: int, C: int, lds: i
     width fits the used items."""
     acc16 = DL_ACC16 and wword is None
     accb = 2 if acc16 else 4
-    sw, cap = dl_slab_width(n_used, min(C, DL_MP_MIN_CAP), lds, accb)
-    if sw == 0:
-        sw, cap = dl_slab_width(n_used, min(C, 8192), lds, accb)
+    sw, cap = dl_slab_width(n_used, min(C, 8192), lds, accb)
     if sw == 0:
         return None
     dense = wword is None and DENSE_MIN_ROWS > 0 and sup_frac * sw * 64 >= DENSE_MIN_ROWS
