@@ -828,9 +828,37 @@ constexpr int kM4 = 4;                 // 32 x 32 MFMA tiles per wave side
 constexpr int kMT4 = 64 * kM4;         // items per workgroup tile side (2 x 2 waves)
 constexpr int kM4Ld = kMT4 * kMW / 256;   // staged words per thread and operand
 
+// kFp4: the same tiles on the block-scaled FP4 MFMA (v_mfma_scale_f32_32x32x64_f8f6f4,
+// e2m1 operands, unit scales): a bit becomes the nibble 0b0010 (1.0), one 64-transaction
+// k-step per bitmap word instead of two 32-transaction i8 steps, at the i8 instruction's
+// cycles (twice the K per MFMA).  The f32 sums are exact integers while a workgroup's
+// chunk holds <= 2^24 transactions (fa_hip_pair_gram_mfma caps kchunk).
+typedef int fa_v8i __attribute__((ext_vector_type(8)));
+typedef float fa_v16f __attribute__((ext_vector_type(16)));
+
+// 8 bits -> 8 e2m1 nibbles (bit n -> nibble n = 0b0010)
+__device__ __forceinline__ uint32_t spread8_fp4(uint32_t b) {
+  uint32_t t = ((b << 12) | b) & 0x000F000Fu;
+  t = ((t << 6) | t) & 0x03030303u;
+  t = ((t << 3) | t) & 0x11111111u;
+  return t << 1;
+}
+
+__device__ __forceinline__ fa_v8i unpack32_fp4(uint32_t x) {
+  fa_v8i r;
+  r[0] = (int)spread8_fp4(x & 0xFFu);
+  r[1] = (int)spread8_fp4((x >> 8) & 0xFFu);
+  r[2] = (int)spread8_fp4((x >> 16) & 0xFFu);
+  r[3] = (int)spread8_fp4(x >> 24);
+  r[4] = 0; r[5] = 0; r[6] = 0; r[7] = 0;
+  return r;
+}
+
+template <bool kFp4>
 __global__ __launch_bounds__(256) void k_pair_gram_mfma4(const uint64_t* __restrict__ bm, int32_t F1, int64_t Wp,
                                                          int64_t W, int nt, int ntp, int64_t kchunk,
                                                          uint32_t* __restrict__ out, uint32_t scale) {
+  using AccT = std::conditional_t<kFp4, fa_v16f, fa_v16i>;
   __shared__ uint64_t As[kMT4 * kMS];
   __shared__ uint64_t Bs[kMT4 * kMS];
   const uint32_t logical = xcd_remap(blockIdx.x, gridDim.x);
@@ -842,11 +870,11 @@ __global__ __launch_bounds__(256) void k_pair_gram_mfma4(const uint64_t* __restr
   const int r = lane & 31, h = lane >> 5;
   const int wr = (wv >> 1) * 32 * kM4, wc = (wv & 1) * 32 * kM4;   // the wave's 128 x 128 sub-tile
   const bool live = !(ti == tj && wr > wc);
-  fa_v16i acc[kM4][kM4];
+  AccT acc[kM4][kM4];
 #pragma unroll
   for (int i = 0; i < kM4; ++i)
 #pragma unroll
-    for (int j = 0; j < kM4; ++j) acc[i][j] = fa_v16i{0};
+    for (int j = 0; j < kM4; ++j) acc[i][j] = AccT{0};
   const int64_t k_begin = kc * kchunk, k_end = min(W, k_begin + kchunk);
   uint64_t pa[kM4Ld], pb[kM4Ld];
   auto fetch = [&](int64_t k0) {
@@ -880,6 +908,19 @@ __global__ __launch_bounds__(256) void k_pair_gram_mfma4(const uint64_t* __restr
           a[i] = As[(wr + 32 * i + r) * kMS + w];
           b[i] = Bs[(wc + 32 * i + r) * kMS + w];
         }
+        if constexpr (kFp4) {
+          // one 64-transaction k-step: lane half h takes transactions 32h .. 32h + 31
+          fa_v8i fb[kM4];
+#pragma unroll
+          for (int j = 0; j < kM4; ++j) fb[j] = unpack32_fp4((uint32_t)(b[j] >> (32 * h)));
+#pragma unroll
+          for (int i = 0; i < kM4; ++i) {
+            const fa_v8i fa = unpack32_fp4((uint32_t)(a[i] >> (32 * h)));
+#pragma unroll
+            for (int j = 0; j < kM4; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa, fb[j], acc[i][j], 4, 4, 0, 127, 0, 127);
+          }
+        } else {
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {                  // two 32-transaction k-steps per word
           const int sh = 32 * s2 + 16 * h;
@@ -893,6 +934,7 @@ __global__ __launch_bounds__(256) void k_pair_gram_mfma4(const uint64_t* __restr
             for (int j = 0; j < kM4; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa, fb[j], acc[i][j], 0, 0, 0);
           }
+        }
         }
       }
     }
@@ -908,8 +950,8 @@ __global__ __launch_bounds__(256) void k_pair_gram_mfma4(const uint64_t* __restr
       for (int g = 0; g < 16; ++g) {
         const int row = ti * kMT4 + wr + 32 * i + (g & 3) + 8 * (g >> 2) + 4 * h;
         const int col = tj * kMT4 + wc + 32 * j + r;
-        const int v = acc[i][j][g];
-        if (row < col && col < F1 && v) atomicAdd(&out[(int64_t)row * F1 + col], (uint32_t)v * scale);
+        const uint32_t v = kFp4 ? (uint32_t)(acc[i][j][g] + 0.5f) : (uint32_t)acc[i][j][g];
+        if (row < col && col < F1 && v) atomicAdd(&out[(int64_t)row * F1 + col], v * scale);
       }
 }
 
@@ -1499,9 +1541,15 @@ FA_API int fa_hip_pair_gram_mfma(const uint64_t* bm, int32_t F1, int64_t Wp, int
   int64_t nk = std::max<int64_t>(1, (target_wgs + ntp - 1) / ntp);
   int64_t kchunk = (W + nk - 1) / nk;
   kchunk = std::max<int64_t>(kMW, (kchunk + kMW - 1) / kMW * kMW);
+  const bool fp4 = getenv("FA_GRAM_FP4") && atoi(getenv("FA_GRAM_FP4")) == 1;
+  if (fp4) kchunk = std::min<int64_t>(kchunk, (int64_t)1 << 18);   // f32-exact sums: <= 2^24 transactions
   nk = (W + kchunk - 1) / kchunk;
-  hipLaunchKernelGGL(k_pair_gram_mfma4, dim3((unsigned)(nk * ntp)), dim3(256), 0, st, bm, F1, Wp, W, nt, ntp,
-                     kchunk, out, scale);
+  if (fp4)
+    hipLaunchKernelGGL(k_pair_gram_mfma4<true>, dim3((unsigned)(nk * ntp)), dim3(256), 0, st, bm, F1, Wp, W, nt,
+                       ntp, kchunk, out, scale);
+  else
+    hipLaunchKernelGGL(k_pair_gram_mfma4<false>, dim3((unsigned)(nk * ntp)), dim3(256), 0, st, bm, F1, Wp, W, nt,
+                       ntp, kchunk, out, scale);
   FA_LAUNCH_RET();
 }
 

@@ -1,11 +1,11 @@
 #!/bin/bash
-# round 4 scratch pass: packed u16 accumulators in one-pass device bundles (FA_DL_ACC16)
+# round 4 scratch pass: FP4 matrix-core Gram (FA_GRAM_FP4)
 set -e -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/mincap
+O=$R/gpurun_out/fp4
 mkdir -p $O
 export TMPDIR=/tmp
-FA_DL_MP_MIN_CAP=2048 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_device_levels.py tests/test_oracle_deep.py -m gpu > $O/tests.log 2>&1
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -m gpu -k gram > $O/tests.log 2>&1
 run() {   # name, env..., then bench args after --
   local name=$1; shift
   local envs=()
@@ -16,7 +16,8 @@ run() {   # name, env..., then bench args after --
   echo "$name" >> $O/names.txt
 }
 for i in 1 2; do
-  run T40_c8k FA_X=0 -- --config T40I10D100M --steps 2 --warmup 1
-  run T40_c4k FA_DL_MP_MIN_CAP=4096 -- --config T40I10D100M --steps 2 --warmup 1
-  run T40_c2k FA_DL_MP_MIN_CAP=2048 -- --config T40I10D100M --steps 2 --warmup 1
+  run T40_i8 FA_GRAM_FP4=0 -- --config T40I10D100M --steps 2 --warmup 1
+  run T40_fp4 FA_GRAM_FP4=1 -- --config T40I10D100M --steps 2 --warmup 1
 done
+run web_i8 FA_GRAM_FP4=0 -- --config webdocs --steps 5 --warmup 1
+run web_fp4 FA_GRAM_FP4=1 -- --config webdocs --steps 5 --warmup 1

@@ -486,10 +486,14 @@ def test_apriori_gen_device_matches_host(k):
     assert np.array_equal(got[3], np.concatenate([cand[want[0][g2]], want[2][:, None]], 1))
 
 
+@pytest.mark.parametrize("fp4", ["0", "1"])
 @pytest.mark.parametrize("F1,T", [(37, 5000), (300, 70001), (1000, 9000)])
-def test_pair_gram_mfma_matches_popcount(monkeypatch, F1, T):
-    # i8 MFMA Gram (v_mfma_i32_32x32x32_i8) vs the popcount Gram and the CPU Gram on
-    # asymmetric random bitmaps (F1 not a multiple of the 128 tile, W of the 8-word step)
+def test_pair_gram_mfma_matches_popcount(monkeypatch, F1, T, fp4):
+    # i8 MFMA Gram (v_mfma_i32_32x32x32_i8), and its FP4 form (FA_GRAM_FP4=1:
+    # v_mfma_scale_f32_32x32x64_f8f6f4 on e2m1 0/1 operands), vs the popcount Gram and the
+    # CPU Gram on asymmetric random bitmaps (F1 not a multiple of the 128 tile, W of the
+    # 8-word step)
+    monkeypatch.setenv("FA_GRAM_FP4", fp4)
     rng = np.random.default_rng(F1)
     dens = rng.random(F1) * 0.6
     bits = rng.random((F1, T)) < dens[:, None]
@@ -509,9 +513,11 @@ def test_pair_gram_mfma_matches_popcount(monkeypatch, F1, T):
     assert torch.equal(ref[iu[0], iu[1]], want[iu[0], iu[1]])
 
 
+@pytest.mark.parametrize("fp4", ["0", "1"])
 @pytest.mark.parametrize("F1,classes", [(300, [(1, 700), (2, 40), (3, 600), (7, 3), (9, 520)]),
                                         (37, [(1, 9), (4, 530)])])
-def test_weighted_gram_mfma_matches_popcount(monkeypatch, F1, classes):
+def test_weighted_gram_mfma_matches_popcount(monkeypatch, F1, classes, fp4):
+    monkeypatch.setenv("FA_GRAM_FP4", fp4)
     # deduplicated layouts: one scaled matrix-core launch per weight class of >= 512
     # words, the short classes by the popcount Gram -- exact against the weighted
     # popcount Gram and a numpy reference (FastApriori.scala:233-235)
