@@ -829,27 +829,24 @@ constexpr int kMT4 = 64 * kM4;         // items per workgroup tile side (2 x 2 w
 constexpr int kM4Ld = kMT4 * kMW / 256;   // staged words per thread and operand
 
 // kFp4: the same tiles on the block-scaled FP4 MFMA (v_mfma_scale_f32_32x32x64_f8f6f4,
-// e2m1 operands, unit scales): a bit becomes the nibble 0b0010 (1.0), one 64-transaction
-// k-step per bitmap word instead of two 32-transaction i8 steps, at the i8 instruction's
-// cycles (twice the K per MFMA).  The f32 sums are exact integers while a workgroup's
-// chunk holds <= 2^24 transactions (fa_hip_pair_gram_mfma caps kchunk).
+// e2m1 operands): one 64-transaction k-step per bitmap word instead of two
+// 32-transaction i8 steps, at the i8 instruction's cycles (twice the K per MFMA).  A
+// bit becomes the e2m1 nibble 0b0001 (0.5; both block scales 2^1 make each product 1).
+// The transactions may sit in any k order that A and B share, so element (dword d,
+// nibble n) of a lane takes transaction 4n + d of its 32: dword d is (x >> d) &
+// 0x11111111, two VALU ops, where bits -> i8 bytes cost ~3 per 4 bits.  The f32 sums
+// are exact integers while a workgroup's chunk holds <= 2^24 transactions
+// (fa_hip_pair_gram_mfma caps kchunk).
 typedef int fa_v8i __attribute__((ext_vector_type(8)));
 typedef float fa_v16f __attribute__((ext_vector_type(16)));
-
-// 8 bits -> 8 e2m1 nibbles (bit n -> nibble n = 0b0010)
-__device__ __forceinline__ uint32_t spread8_fp4(uint32_t b) {
-  uint32_t t = ((b << 12) | b) & 0x000F000Fu;
-  t = ((t << 6) | t) & 0x03030303u;
-  t = ((t << 3) | t) & 0x11111111u;
-  return t << 1;
-}
+constexpr int kFp4Scale = 128;   // E8M0 2^1
 
 __device__ __forceinline__ fa_v8i unpack32_fp4(uint32_t x) {
   fa_v8i r;
-  r[0] = (int)spread8_fp4(x & 0xFFu);
-  r[1] = (int)spread8_fp4((x >> 8) & 0xFFu);
-  r[2] = (int)spread8_fp4((x >> 16) & 0xFFu);
-  r[3] = (int)spread8_fp4(x >> 24);
+  r[0] = (int)(x & 0x11111111u);
+  r[1] = (int)((x >> 1) & 0x11111111u);
+  r[2] = (int)((x >> 2) & 0x11111111u);
+  r[3] = (int)((x >> 3) & 0x11111111u);
   r[4] = 0; r[5] = 0; r[6] = 0; r[7] = 0;
   return r;
 }
@@ -918,7 +915,8 @@ __global__ __launch_bounds__(256) void k_pair_gram_mfma4(const uint64_t* __restr
             const fa_v8i fa = unpack32_fp4((uint32_t)(a[i] >> (32 * h)));
 #pragma unroll
             for (int j = 0; j < kM4; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa, fb[j], acc[i][j], 4, 4, 0, 127, 0, 127);
+              acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa, fb[j], acc[i][j], 4, 4, 0, kFp4Scale, 0,
+                                                                          kFp4Scale);
           }
         } else {
 #pragma unroll

@@ -2,7 +2,7 @@
 # round 4 scratch pass: FP4 matrix-core Gram (FA_GRAM_FP4)
 set -e -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/fp4
+O=$R/gpurun_out/fp4b
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -m gpu -k gram > $O/tests.log 2>&1
