@@ -42,9 +42,10 @@ from .data import MiningResult, TransactionShard
 
 # Cost-model constants for choosing the k = 2 kernel (calibrated on MI355X; see
 # docs/PERF.md).  Work units: pair increments for the horizontal kernel, 64-bit
-# word pairs for the Gram kernel.
+# word pairs for the Gram kernel (the FP4 matrix-core form with its bitmap build:
+# T40I10D100M 7.8e11 word pairs in a 46 ms pair phase).
 HORIZONTAL_PAIRS_PER_S = 2.0e11
-GRAM_WORDPAIRS_PER_S = 1.2e13
+GRAM_WORDPAIRS_PER_S = 1.7e13
 # numeric vocabularies at least this wide count F1 with the sketch + exact pass
 F1_SKETCH_MIN_VOCAB = 1 << 20
 # numeric vocabularies up to this wide read the whole F1 histogram back at once

@@ -549,7 +549,7 @@ def gram_segments(W: int, weighted: bool, wcls=None, force_popc: bool = False) -
 
 def pair_counts_gram(bm: torch.Tensor, W: int, wword, wcls=None, force_popc: bool = False) -> torch.Tensor:
     """Pair supports from the item-major bitmaps over words [0, W) -> int64 [F1, F1]
-    (upper triangle).  Device: the int8 matrix-core Gram (k_pair_gram_mfma4) per
+    (upper triangle).  Device: the FP4 matrix-core Gram (k_pair_gram_mfma4) per
     weight class, scaled by the class weight (FastApriori.scala:233-235's weighted
     sum), short classes by the popcount Gram with per-word weights."""
     F1, Wp = bm.shape[0], bm.stride(0)
