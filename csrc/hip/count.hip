@@ -804,7 +804,7 @@ __global__ __launch_bounds__(256) void k_pair_gram_popc(
 // ---------------------------------------------------------------------------
 typedef int fa_v4i __attribute__((ext_vector_type(4)));
 typedef int fa_v16i __attribute__((ext_vector_type(16)));
-constexpr int kMW = 8;       // words staged per step
+constexpr int kMW = 16;      // words staged per step
 constexpr int kMS = kMW + 1; // LDS row stride (words): 72 B rows -> conflict-free ds_read_b64
 
 __device__ __forceinline__ fa_v4i unpack16_i8(uint32_t b) {
@@ -878,7 +878,7 @@ __global__ __launch_bounds__(256) void k_pair_gram_mfma4(const uint64_t* __restr
 #pragma unroll
     for (int it = 0; it < kM4Ld; ++it) {
       const int idx = threadIdx.x + it * 256;
-      const int row = idx >> 3, w = idx & 7;
+      const int row = idx / kMW, w = idx % kMW;
       const int ra = ti * kMT4 + row, rb = tj * kMT4 + row;
       const int64_t kk = k0 + w;
       pa[it] = (ra < F1 && kk < k_end) ? bm[(int64_t)ra * Wp + kk] : 0ull;
@@ -890,7 +890,7 @@ __global__ __launch_bounds__(256) void k_pair_gram_mfma4(const uint64_t* __restr
 #pragma unroll
     for (int it = 0; it < kM4Ld; ++it) {
       const int idx = threadIdx.x + it * 256;
-      const int row = idx >> 3, w = idx & 7;
+      const int row = idx / kMW, w = idx % kMW;
       As[row * kMS + w] = pa[it];
       Bs[row * kMS + w] = pb[it];
     }

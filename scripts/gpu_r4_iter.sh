@@ -1,8 +1,8 @@
 #!/bin/bash
-# round 4 scratch pass: FP4 matrix-core Gram (FA_GRAM_FP4)
+# round 4 scratch pass: Gram staging of 16 words per step
 set -e -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/fp4b
+O=$R/gpurun_out/mw16
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -m gpu -k gram > $O/tests.log 2>&1
@@ -16,8 +16,5 @@ run() {   # name, env..., then bench args after --
   echo "$name" >> $O/names.txt
 }
 for i in 1 2; do
-  run T40_i8 FA_GRAM_FP4=0 -- --config T40I10D100M --steps 2 --warmup 1
-  run T40_fp4 FA_GRAM_FP4=1 -- --config T40I10D100M --steps 2 --warmup 1
+  run T40_mw16 FA_X=0 -- --config T40I10D100M --steps 2 --warmup 1
 done
-run web_i8 FA_GRAM_FP4=0 -- --config webdocs --steps 5 --warmup 1
-run web_fp4 FA_GRAM_FP4=1 -- --config webdocs --steps 5 --warmup 1
