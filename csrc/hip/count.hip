@@ -805,7 +805,7 @@ __global__ __launch_bounds__(256) void k_pair_gram_popc(
 typedef int fa_v4i __attribute__((ext_vector_type(4)));
 typedef int fa_v16i __attribute__((ext_vector_type(16)));
 constexpr int kMW = 16;      // words staged per step
-constexpr int kMS = kMW + 1; // LDS row stride (words): 72 B rows -> conflict-free ds_read_b64
+constexpr int kMS = kMW + 1; // LDS row stride (words): 136 B rows -> conflict-free ds_read_b64
 
 __device__ __forceinline__ fa_v4i unpack16_i8(uint32_t b) {
   fa_v4i r;
