@@ -356,8 +356,7 @@ class FastApriori:
         # window-by-window levels, and in one-pass bundles with FA_DL_ACC16_BUNDLES=1
         unit = db["wword"] is None
         self._dl_mp_accb = 2.0 if Pm.DL_ACC16 and unit else 4.0
-        acc16_first = Pm.DL_ACC16_FIRST and unit
-        accb = self._dl_accb = 2.0 if (Pm.DL_ACC16_BUNDLES or acc16_first) and unit else 4.0
+        accb = self._dl_accb = 2.0 if Pm.DL_ACC16_BUNDLES and unit else 4.0
         c_bound = int(lds // accb)
         st = torch.cuda.current_stream(self._dev).cuda_stream
         f2 = self._f2_dev
@@ -447,10 +446,6 @@ class FastApriori:
                              n_par=S.desc[:L, 5].copy(), sw=sw, used=n_used, T=int(db["roff"].numel() - 1),
                              ms=(time.perf_counter() - t0) * 1e3, bytes=self._bytes_moved() - b0,
                              G=c[72:72 + L].copy()))
-            if acc16_first and not Pm.DL_ACC16_BUNDLES:
-                # packed u16 accumulators for the first bundle only (FA_DL_ACC16_FIRST)
-                accb = self._dl_accb = 4.0
-                c_bound = int(lds // accb)
             P0 = rows_a.data_ptr() + 4 * int(ro[L - 1])
             n_src, n_const, n_bound = S.fsz.data_ptr() + 8 * (k + L - 1), 0, int(Cs[-1])
             m0 += L

@@ -1477,7 +1477,6 @@ def dl_lds_budget(F1: int) -> int:
 # 43.2 vs 42.3 ms (docs/PERF_HISTORY.md)
 DL_ACC16 = os.environ.get("FA_DL_ACC16", "1") == "1"
 DL_ACC16_BUNDLES = os.environ.get("FA_DL_ACC16_BUNDLES", "0") == "1"
-DL_ACC16_FIRST = os.environ.get("FA_DL_ACC16_FIRST", "0") == "1"
 
 
 def dl_slab_width(n_used: int, C: int, lds: int, accb: int = 4) -> tuple[int, int]:

@@ -1,11 +1,11 @@
 #!/bin/bash
-# round 4 scratch pass: u16 accumulators for the first device bundle only (FA_DL_ACC16_FIRST)
+# round 4 scratch pass: Gram staging of 16 words per step
 set -e -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/first
+O=$R/gpurun_out/mw16
 mkdir -p $O
 export TMPDIR=/tmp
-FA_DL_ACC16_FIRST=1 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_device_levels.py tests/test_oracle_deep.py -m gpu > $O/tests.log 2>&1
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -m gpu -k gram > $O/tests.log 2>&1
 run() {   # name, env..., then bench args after --
   local name=$1; shift
   local envs=()
@@ -16,7 +16,5 @@ run() {   # name, env..., then bench args after --
   echo "$name" >> $O/names.txt
 }
 for i in 1 2; do
-  run T10_first FA_DL_ACC16_FIRST=1 FA_METRICS=$O/m_first.jsonl -- --steps 10 --warmup 2
-  run T10_base FA_DL_ACC16_FIRST=0 -- --steps 10 --warmup 2
+  run T40_mw16 FA_X=0 -- --config T40I10D100M --steps 2 --warmup 1
 done
-run T40_first FA_DL_ACC16_FIRST=1 -- --config T40I10D100M --steps 2 --warmup 1
