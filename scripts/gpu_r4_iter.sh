@@ -1,8 +1,8 @@
 #!/bin/bash
-# round 4 scratch pass: Gram staging of 16 words per step
+# round 4 scratch pass: FP4 Gram word loop unrolled by 2
 set -e -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/mw16
+O=$R/gpurun_out/unroll2
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -m gpu -k gram > $O/tests.log 2>&1
