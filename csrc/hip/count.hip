@@ -1210,26 +1210,7 @@ __device__ __forceinline__ int u16_at(const int4& v, int k) {
   return (k & 1) ? (int)((uint32_t)w >> 16) : (w & 0xFFFF);
 }
 
-// 8-lane (SW = 16) / 4-lane (SW = 8) reductions: xor 1, xor 2, then the other half of 8
-__device__ __forceinline__ uint32_t lanes_sum(uint32_t s, int lp) {
-  s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
-  s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x4E, 0xF, 0xF, false);   // quad_perm 2,3,0,1
-  if (lp == 8) s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x141, 0xF, 0xF, false);  // row_half_mirror
-  return s;
-}
-__device__ __forceinline__ uint32_t lanes_or(uint32_t s, int lp) {
-  s |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0xB1, 0xF, 0xF, false);
-  s |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x4E, 0xF, 0xF, false);
-  if (lp == 8) s |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x141, 0xF, 0xF, false);
-  return s;
-}
-
-// kLanes (unit weights, SW = 8 / 16, FA_SLAB_LANES=1): a piece is counted by SW / 2
-// lanes, lane s holding 16 B (words 2s, 2s + 1) of every slab row the piece reads, so
-// the lanes of a piece read one contiguous row (no bank conflicts among them) and the
-// per-extension popcounts are summed across the lanes with DPP before one lane adds
-// them to the accumulator.
-template <int SW, bool kWeighted, int kBuild, bool kCls = false, bool kLanes = false>
+template <int SW, bool kWeighted, int kBuild, bool kCls = false>
 __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
     const int64_t* __restrict__ roff, const int32_t* __restrict__ ranks, const int32_t* __restrict__ src,
     int64_t ncols, const int32_t* __restrict__ item_map, int F1, int n_used, const int32_t* __restrict__ gpre,
@@ -1389,61 +1370,6 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
     }
     __syncthreads();
     load_span(sb + gridDim.x);                      // in flight during the counting below
-    if constexpr (kLanes) {
-      constexpr int LP = SW / 2;                    // lanes per piece
-      constexpr int kStep = kSlabThreads / LP;
-      const int ls = (int)threadIdx.x & (LP - 1);
-      int g = (int)threadIdx.x / LP;
-      int4 la = z4, lb = z4, lc = z4;
-      if (g < G) { la = rec[3 * g]; lb = rec[3 * g + 1]; lc = rec[3 * g + 2]; }
-      for (; g < ((dbg & 2) ? 0 : G); g += kStep) {
-        const int gn = g + kStep;
-        int4 na = z4, nb = z4, nc = z4;
-        if (gn < G) { na = rec[3 * gn]; nb = rec[3 * gn + 1]; nc = rec[3 * gn + 2]; }
-        const int n_ext = la.y & 0xFF, m = (la.y >> 8) & 0xFF;
-        uint4 p = lds4[(size_t)(la.z & 0xFFFF) * RS + ls];
-        auto lid = [&](int j) { return j < 4 ? u16_at(la, 4 + j) : u16_at(lc, j - 4); };
-        auto land1 = [&](int u) {
-          const uint4 v = lds4[(size_t)u * RS + ls];
-          p.x &= v.x; p.y &= v.y; p.z &= v.z; p.w &= v.w;
-        };
-        auto land2 = [&](int u, int w) {
-          const uint4 v = lds4[(size_t)u * RS + ls], x = lds4[(size_t)w * RS + ls];
-          p.x = and3(p.x, v.x, x.x); p.y = and3(p.y, v.y, x.y);
-          p.z = and3(p.z, v.z, x.z); p.w = and3(p.w, v.w, x.w);
-        };
-        if (!((la.y >> 16) & 1)) {
-#pragma unroll
-          for (int j = 1; j < 12; j += 2) {
-            if (j < m) {
-              if (j + 1 < m) land2(lid(j), lid(j + 1));
-              else land1(lid(j));
-            }
-          }
-        } else {
-          const int32_t* pr = gpre + lc.x;
-          int j = 1;
-          for (; j + 1 < m; j += 2) land2(pr[j], pr[j + 1]);
-          if (j < m) land1(pr[j]);
-        }
-        uint32_t any = dbg & 4;
-        if (!any) any = lanes_or(p.x | p.y | p.z | p.w, LP);
-        if (any) {
-          const int e0 = la.x;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            if (k >= n_ext) break;
-            const uint4 v = lds4[(size_t)u16_at(lb, k) * RS + ls];
-            uint32_t s = bcnt_acc(p.x & v.x, 0u);
-            s = bcnt_acc(p.y & v.y, s); s = bcnt_acc(p.z & v.z, s); s = bcnt_acc(p.w & v.w, s);
-            s = lanes_sum(s, LP);
-            if (ls == 0 && s) acc_add(e0 + k, s);
-          }
-        }
-        la = na; lb = nb; lc = nc;
-      }
-      continue;
-    }
     uint32_t wt[SW];
 #pragma unroll
     for (int q = 0; q < SW; ++q) wt[q] = kWeighted ? ((w0 + q < W) ? (uint32_t)wword[w0 + q] : 0u) : 1u;
@@ -1685,12 +1611,9 @@ FA_API int fa_hip_count_slab_rec_cls(const int64_t* roff, const int32_t* ranks, 
                          const int32_t*, const int4*, int, int, const int32_t*, uint32_t*, const uint64_t*, int64_t,
                          const int32_t*, int, const int32_t*);
   KernT kern = nullptr;
-  const bool lanes = getenv("FA_SLAB_LANES") && atoi(getenv("FA_SLAB_LANES")) == 1;
-#define FA_REC_MODE(S, B)                                                                                \
-  kern = wword       ? (KernT)k_count_slab_rec<S, true, B>                                               \
-         : (cls & 1) ? (KernT)k_count_slab_rec<S, false, B, true>                                        \
-         : (lanes && (S == 8 || S == 16)) ? (KernT)k_count_slab_rec<S, false, B, false, (S == 8 || S == 16)> \
-                     : (KernT)k_count_slab_rec<S, false, B>;
+#define FA_REC_MODE(S, B)                                                                     \
+  kern = wword ? (KernT)k_count_slab_rec<S, true, B>                                          \
+               : (cls & 1) ? (KernT)k_count_slab_rec<S, false, B, true> : (KernT)k_count_slab_rec<S, false, B>;
 #define FA_REC_CASE(S)                                    \
   if (sw == S) {                                          \
     if (bm) { FA_REC_MODE(S, kBuildBM) }                  \
