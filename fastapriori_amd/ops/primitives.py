@@ -547,10 +547,6 @@ def gram_segments(W: int, weighted: bool, wcls=None, force_popc: bool = False) -
     return segs
 
 
-# target workgroups of a matrix-core Gram launch (tile pairs x K chunks)
-GRAM_WGS = int(os.environ.get("FA_GRAM_WGS", "4096"))
-
-
 def pair_counts_gram(bm: torch.Tensor, W: int, wword, wcls=None, force_popc: bool = False) -> torch.Tensor:
     """Pair supports from the item-major bitmaps over words [0, W) -> int64 [F1, F1]
     (upper triangle).  Device: the FP4 matrix-core Gram (k_pair_gram_mfma4) per
@@ -564,7 +560,7 @@ def pair_counts_gram(bm: torch.Tensor, W: int, wword, wcls=None, force_popc: boo
             segs = gram_segments(W, wword is not None, wcls, force_popc)
             for a, b, wt in segs:
                 if wt > 0:
-                    _hip_call("fa_hip_pair_gram_mfma", bm.data_ptr() + 8 * a, F1, Wp, b - a, _p(out), GRAM_WGS, wt, st)
+                    _hip_call("fa_hip_pair_gram_mfma", bm.data_ptr() + 8 * a, F1, Wp, b - a, _p(out), 4096, wt, st)
                 else:
                     _hip_call("fa_hip_pair_gram_popc", bm.data_ptr() + 8 * a, F1, Wp, b - a,
                               wword.data_ptr() + 4 * a if wword is not None else None, _p(out), 4096, st)

@@ -1,8 +1,8 @@
 #!/bin/bash
-# round 4 scratch pass: Gram launch size (FA_GRAM_WGS)
+# round 4 scratch pass: FP4 Gram word loop unrolled by 2
 set -e -o pipefail
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/wgs
+O=$R/gpurun_out/unroll2
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -m gpu -k gram > $O/tests.log 2>&1
@@ -16,8 +16,5 @@ run() {   # name, env..., then bench args after --
   echo "$name" >> $O/names.txt
 }
 for i in 1 2; do
-  run T40_w4096 FA_GRAM_WGS=4096 -- --config T40I10D100M --steps 1 --warmup 1
-  run T40_w2048 FA_GRAM_WGS=2048 -- --config T40I10D100M --steps 1 --warmup 1
-  run T40_w1024 FA_GRAM_WGS=1024 -- --config T40I10D100M --steps 1 --warmup 1
-  run T40_w8192 FA_GRAM_WGS=8192 -- --config T40I10D100M --steps 1 --warmup 1
+  run T40_mw16 FA_X=0 -- --config T40I10D100M --steps 2 --warmup 1
 done
