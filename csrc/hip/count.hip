@@ -14,6 +14,7 @@
 //     candidates over a super-chunk of bitmap words; wave reductions into an
 //     LDS accumulator, one coalesced global atomic per candidate per chunk.
 // All accumulation is integer, so results are exact and order-independent.
+#include <algorithm>
 #include <cstdlib>
 
 #include "fa_hip.h"
@@ -1595,6 +1596,12 @@ FA_API int fa_hip_count_candidates(const uint64_t* bm, int64_t Wp, int64_t W, co
 // all-zero-prefix test (the counts are the same either way).  cls bit 2: u16 packed
 // accumulators (unit weights: half the LDS per candidate, drained every 65535 / (SW * 64)
 // slabs).
+// Test hook: at most this many workgroups per slab count (0: no cap).  One workgroup
+// then walks every slab, so the packed-u16 accumulators' mid-run drain (every
+// kFlush16 slabs) runs on inputs of a few hundred thousand rows.
+static int g_slab_max_wg = 0;
+FA_API void fa_hip_debug_slab_max_wg(int n) { g_slab_max_wg = n; }
+
 FA_API int fa_hip_count_slab_rec_cls(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
                                      const int32_t* item_map, int F1, int n_used, const int32_t* gpre,
                                      const void* rec, int G, int C, const int32_t* wword, uint32_t* out, int sw,
@@ -1607,6 +1614,7 @@ FA_API int fa_hip_count_slab_rec_cls(const int64_t* roff, const int32_t* ranks, 
   const size_t map_b = (contig && F1 <= kMapLdsMax) ? (size_t)(((int64_t)F1 * 2 + 15) & ~(int64_t)15) : 0;
   const size_t lds = (size_t)n_used * (sw + 2) * 8 + (size_t)((n_acc + 3) & ~(int64_t)3) * 4 + map_b;
   if (lds > 160 * 1024 - 256) return 3;             // static build_words scratch
+  if (g_slab_max_wg > 0) n_wg = std::min(n_wg, g_slab_max_wg);
   using KernT = void (*)(const int64_t*, const int32_t*, const int32_t*, int64_t, const int32_t*, int, int,
                          const int32_t*, const int4*, int, int, const int32_t*, uint32_t*, const uint64_t*, int64_t,
                          const int32_t*, int, const int32_t*);

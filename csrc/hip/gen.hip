@@ -92,8 +92,53 @@ __device__ __forceinline__ int ag_row_bits(const int32_t* __restrict__ P, int64_
                                            unsigned long long (&a)[NWL]) {
   const int32_t* x = P + i * m;
   const int32_t last = x[m - 1];
-  const int32_t s0 = ag_find(P, m, table, mask, x, m - 1);
   const int lw = last >> 6;
+  if (m <= 64) {
+    // lane p < m probes the class of x without x[p] (p = m - 1: x's own class), so the
+    // m probe chains (table load, row compare, Ext load: dependent round trips) are in
+    // flight at once; walked one after another they made every speculative level's
+    // row kernel 20-35 us of latency at m = 5-9 (the 12.5M-row shard's generator time)
+    const int32_t s = lane < m ? ag_find(P, m, table, mask, x, lane) : 0;
+    if (__ballot(s < 0) != 0ull) {
+#pragma unroll
+      for (int j = 0; j < NWL; ++j) a[j] = 0;
+      return 0;
+    }
+    const int32_t s0 = __shfl(s, m - 1, 64);
+#pragma unroll
+    for (int j = 0; j < NWL; ++j) {
+      const int w = lane * NWL + j;
+      unsigned long long v = 0;
+      if (w < nw && w >= lw) {
+        v = ext[(int64_t)s0 * nw + w];
+        if (w == lw) v &= (last & 63) == 63 ? 0ull : (~0ull << ((last & 63) + 1));
+      }
+      a[j] = v;
+    }
+    // the other m - 1 subsets' Ext words, four loads in flight per step (a step past
+    // m - 2 re-reads x's own class: a subset of it already)
+    for (int p0 = 0; p0 < m - 1; p0 += 4) {
+      unsigned long long t[4][NWL];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int sp = __shfl(s, p0 + u < m - 1 ? p0 + u : m - 1, 64);
+#pragma unroll
+        for (int j = 0; j < NWL; ++j) {
+          const int w = lane * NWL + j;
+          t[u][j] = w < nw ? ext[(int64_t)sp * nw + w] : 0ull;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < NWL; ++j) a[j] &= t[u][j];
+    }
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < NWL; ++j) c += __popcll(a[j]);
+    return c;
+  }
+  const int32_t s0 = ag_find(P, m, table, mask, x, m - 1);
   unsigned long long any = 0;
 #pragma unroll
   for (int j = 0; j < NWL; ++j) {

@@ -177,15 +177,23 @@ class FastApriori:
         counts = [counts1]
         result = MiningResult(items, levels, counts, mc, n_global, self.stats,
                               item_hashes=None if shard.vocab.numeric else self._item_hashes)
+        self._result = result
         # the device level loop reads its levels back once, at the end: its checkpoint
-        # levels are then written in one go (in the background: _finish), else per level
+        # levels are written by a background thread from each bundle's staged copy
+        # (_ckpt_staged), else per level
         self._ckpt_saved = 0
         self._ckpt_deferred = self.ckpt is not None and self._device_levels_planned(resume)
         self._result_items(result, wait=resume is not None or (self.ckpt is not None and not self._ckpt_deferred))
         if resume is not None:
             self._check_resume(resume, result)
         self._ckpt_level(result, 1)
+        self._logged_upto, self._log_stop = 1, False     # the last level whose lines were printed
         if F1 < 2:
+            # the reference still prints level 2 (FastApriori.scala:226, :107-108)
+            self.log.line("2 candidates items 0")
+            self.log.line("2 freq items 0")
+            self.log.line("Use Time 2 items 0")
+            self._logged_upto = 2
             return self._finish(result, t_start)
 
         with roctx_range("compress"), tm.phase("compress"):
@@ -216,15 +224,16 @@ class FastApriori:
         while resumed >= k:                  # levels the checkpoint already holds
             levels.append(resume.levels[k - 1]); counts.append(resume.counts[k - 1])
             k += 1
+        self._logged_upto = max(self._logged_upto, resumed)
         if self._device_levels_ok(resume, levels):
             # device bundles while every bundle fits one accumulator pass; None when
             # mining is complete, else the level the host loop continues from
             k = self._mine_device(db, levels, counts, mc, result)
-            if k is not None and self._ckpt_deferred:
-                # the host loop checkpoints per level from here: the device levels first
-                self._ckpt_deferred = False
-                self._result_items(result)
-                self._ckpt_upto(result, len(levels), background=False)
+        if k is not None and self._ckpt_deferred:
+            # the host loop checkpoints per level from here: the levels before it first
+            self._ckpt_deferred = False
+            self._result_items(result)
+            self._ckpt_upto(result, len(levels), background=False)
         while k is not None and len(levels[-1]) >= k and (self.cfg.max_level == 0 or k <= self.cfg.max_level):
             t0 = time.perf_counter()
             b0 = self._bytes_moved()
@@ -242,7 +251,7 @@ class FastApriori:
                 self.log.line(f"{k} candidate items {0 if prefix_idx is None else int(prefix_idx.size)}")
                 if C == 0:
                     levels.append(np.zeros((0, k), np.int32)); counts.append(np.zeros(0, np.int64))
-                    self.log.line(f"{k} freq items 0")
+                    self._log_level(levels, k, 0, 0, (time.perf_counter() - t0) * 1e3, cand_line=False)
                     break
                 # level bundling: count the next levels' candidates, generated from this
                 # level's candidates, in the same launch (see _plan_bundle)
@@ -273,14 +282,12 @@ class FastApriori:
             c_tot = max(sum(int(b[4].size) for b in bundle), 1)
             for j, (kk, pv, pi, eo, ex) in enumerate(bundle):
                 Fk = levels[kk - 1]
-                if kk > k and self.log.enabled:
-                    # the reference logs the groups generated from F_{k-1}; a bundled
-                    # level counted a superset generated from C_{k-1}
-                    self.log.line(f"{kk} candidate items {int(apriori_gen(levels[kk - 2])[0].size)}")
-                self.log.line(f"{kk} freq items {len(Fk)}")
-                # one launch counts the bundle: each level gets its candidates' share
+                # one launch counts the bundle: each level gets its candidates' share.  The
+                # reference logs the groups generated from F_{k-1}; a bundled level counted
+                # a superset generated from C_{k-1}
                 share = int(ex.size) / c_tot
-                self.log.line(f"Use Time {kk} items {int(ms * share)}")
+                self._log_level(levels, kk, lambda kk=kk: int(apriori_gen(levels[kk - 2])[0].size), len(Fk),
+                                ms * share, cand_line=kk > k)
                 rec = dict(phase="level", k=kk, candidates=int(ex.size), frequent=len(Fk),
                            ms=ms * share, groups=int(pi.size), bundled_with=k, bytes_reduced=int(moved * share),
                            kernel=plan.get("kernel"), hbm_bytes_est=int(hbm_b * share) + 4 * int(ex.size) * (kk + 3),
@@ -294,10 +301,41 @@ class FastApriori:
             levels.pop(); counts.pop()
         return self._finish(result, t_start)
 
+    @staticmethod
+    def _entered(levels: list, kk: int) -> bool:
+        """The reference runs level kk while |F_{kk-1}| >= kk (FastApriori.scala:111)."""
+        return 2 <= kk - 1 <= len(levels) and len(levels[kk - 2]) >= kk
+
+    def _log_level(self, levels: list, kk: int, groups, n_freq: int, ms: float, cand_line: bool = True) -> None:
+        """The three lines of a level the reference enters (FastApriori.scala:114, :118-119);
+        none for a level it never enters -- a bundled level past the stop rule, empty
+        by construction -- nor for any level after it.  groups: the candidate group
+        count, or a callable computing it (only when the lines are printed)."""
+        if self._log_stop or not self._entered(levels, kk):
+            self._log_stop = True
+            return
+        if cand_line and self.log.enabled:
+            self.log.line(f"{kk} candidate items {groups() if callable(groups) else int(groups)}")
+        self.log.line(f"{kk} freq items {n_freq}")
+        self.log.line(f"Use Time {kk} items {int(ms)}")
+        self._logged_upto = kk
+
+    def _log_tail(self, levels: list) -> None:
+        """Levels the reference enters after the last counted one: |F_{k-1}| >= k with no
+        candidates (the device loop stops on C_k = 0 without counting anything)."""
+        if self.cfg.max_level or self._log_stop:
+            return
+        kk = self._logged_upto + 1
+        while self._entered(levels, kk):
+            n = len(levels[kk - 1]) if kk - 1 < len(levels) else 0
+            self._log_level(levels, kk, lambda kk=kk: int(apriori_gen(levels[kk - 2])[0].size), n, 0.0)
+            kk += 1
+
     def _log_level2(self, n2: int) -> None:
         F1 = self._F1
         self.log.line(f"2 freq items {n2}")
         self.log.line(f"Use Time 2 items {int(self._level2_ms)}")
+        self._logged_upto = max(self._logged_upto, 2)
         self._level_recs.append((dict(phase="level", k=2, candidates=F1 * (F1 - 1) // 2, frequent=n2,
                                       ms=self._level2_ms, strategy=self.stats.get("pair_strategy"),
                                       bytes_reduced=self._level2_bytes,
@@ -322,7 +360,7 @@ class FastApriori:
 
     def _ckpt_level(self, result: MiningResult, k: int) -> None:
         """Checkpoint level k now (host level loop), unless the device loop's levels are
-        written together at the end (_ckpt_deferred)."""
+        written from their staged copies by the checkpoint thread (_ckpt_deferred, _ckpt_staged)."""
         if self.ckpt is not None and not self._ckpt_deferred:
             self.ckpt.save_level(result, k)
             self._ckpt_saved = max(self._ckpt_saved, k)
@@ -370,6 +408,11 @@ class FastApriori:
             P0, n_src, n_const, n_bound = f2.data_ptr(), self._f2_n_dev.data_ptr(), 0, self._f2_bound
         else:
             P0, n_src, n_const, n_bound = f2.data_ptr(), None, int(f2.shape[0]), int(f2.shape[0])
+        if self.ckpt is not None and self._ckpt_deferred:
+            # the levels already on the host (F_1; F_2 when it was read back) before any bundle
+            self._result_items(result)
+            n_host = next((i for i, lv in enumerate(levels) if lv is None), len(levels))
+            self._ckpt_upto(result, n_host, background=True)
         pend = []
         tm = self._timer
         nxt = None
@@ -575,7 +618,7 @@ class FastApriori:
             todo += [("rows", i, pend[i]["rows"]), ("cnt", i, pend[i]["cnt"])]
             stg["rows"].append(None)
             stg["cnt"].append(None)
-        stg["n"] = len(pend)
+        first, stg["n"] = stg["n"], len(pend)
         if not todo:
             return
         dev = self._dev
@@ -583,14 +626,73 @@ class FastApriori:
         if cs is None:
             cs = stg["stream"] = self._dl_stage_stream = torch.cuda.Stream(dev)
         cs.wait_stream(torch.cuda.current_stream(dev))
+        ckpt = self.ckpt is not None and self._ckpt_deferred
         with torch.cuda.stream(cs):
             for kind, i, t in todo:
                 h = Pm.pinned_stage(f"dl_{kind}{i}").get(4 * t.numel()).view(torch.int32)
                 h.copy_(t, non_blocking=True)
                 stg[kind][i] = h
+            if ckpt:
+                # the F sizes of every level thresholded so far, for the checkpoint thread
+                fsz_h = Pm.pinned_stage(f"dl_fsz{len(pend)}").get(8 * S.fsz.numel()).view(torch.int64)
+                fsz_h.copy_(S.fsz, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(cs)
         stg["ev"] = ev
+        if ckpt:
+            self._ckpt_staged(pend, first, todo[0][0] == "f2", fsz_h, ev)
+
+    def _dl_decode_f2(self, n2_h, rows_h, cnt_h):
+        n2 = int(n2_h.numpy()[:2].view(np.int64)[0])
+        return rows_h.numpy()[:2 * n2].reshape(n2, 2), cnt_h.numpy()[:n2]
+
+    @staticmethod
+    def _dl_decode(p: dict, rows_h: np.ndarray, cnt_h: np.ndarray, fsz: np.ndarray) -> list:
+        """(k, rows [F_k, k], int32 counts [F_k]) of every level of staged bundle p (views)."""
+        out = []
+        for l in range(p["L"]):
+            kk, w = p["k"] + l, p["m0"] + l + 1
+            F = int(fsz[kk])
+            a, b = int(p["ro"][l]), int(p["co"][l])
+            out.append((kk, rows_h[a:a + F * w].reshape(F, w), cnt_h[b:b + F]))
+        return out
+
+    def _ckpt_staged(self, pend: list, first: int, with_f2: bool, fsz_h, ev) -> None:
+        """Checkpoint the device loop's levels as their staged copies land:
+        the checkpoint thread waits for the copy stream's event, decodes F_2 (when it
+        is in this batch) and bundles pend[first:], and writes their level files and
+        one meta.json -- so a crash inside the device loop leaves every level up to the
+        last staged bundle.  FA_FAULT_AT_LEVEL at one of these levels: the levels up to
+        it are written, then this rank exits (at this bundle boundary, not at the end)."""
+        ck, result, stg = self.ckpt, self._result, self._dl_stg
+        ks = ([2] if with_f2 else []) + [p["k"] + l for p in pend[first:] for l in range(p["L"])]
+        if not ks:
+            return
+        fault = ck.fault_level(self.comm.rank)
+        upto = fault if fault in ks else ks[-1]
+        f2 = stg["f2"] if with_f2 else None
+        bufs = [(p, stg["rows"][i], stg["cnt"][i]) for i, p in enumerate(pend[first:], first)]
+
+        def work():
+            ev.synchronize()
+            fsz = fsz_h.numpy()
+            lv = []
+            if f2 is not None:
+                lv.append((2,) + self._dl_decode_f2(*f2))
+            for p, rh, ch in bufs:
+                lv += self._dl_decode(p, rh.numpy(), ch.numpy(), fsz)
+            for k, rows, cnt in lv:
+                if k <= upto:
+                    ck._write_level(result, k, meta=False, rows=np.ascontiguousarray(rows, np.int32),
+                                    counts=cnt.astype(np.int64))
+            ck._write_meta(result, upto)
+
+        ck.submit(work)
+        self._ckpt_saved = max(self._ckpt_saved, upto)
+        if fault in ks:
+            ck.wait()
+            from ..utils.checkpoint import InjectedFault
+            raise InjectedFault(17)
 
     def _dl_flush(self, S, pend: list, levels: list, counts: list, result: MiningResult) -> None:
         """Every device level to the host (the run's one results readback); F_2 too when
@@ -605,35 +707,26 @@ class FastApriori:
         fsz = S.fsz.cpu().numpy()                        # (the stream's last work: the thresholds)
         stg["ev"].synchronize()
         if f2:
-            nb = self._f2_bound
-            n2 = int(stg["f2"][0].numpy()[:2].view(np.int64)[0])
-            levels[1] = stg["f2"][1].numpy()[:2 * n2].reshape(n2, 2).copy()     # (pinned buffer: reused)
-            counts[1] = stg["f2"][2].numpy()[:n2].astype(np.int64)
-            self._log_level2(n2)
+            r2, c2 = self._dl_decode_f2(*stg["f2"])
+            levels[1] = r2.copy()                                    # (pinned buffer: reused)
+            counts[1] = c2.astype(np.int64)
+            self._log_level2(len(c2))
             self._f2_n_dev = None
         if not pend:
             return
         for i, p in enumerate(pend):
-            rows_h, cnt_h = stg["rows"][i].numpy(), stg["cnt"][i].numpy()
-            ro_base = co_base = 0
-            for l in range(p["L"]):
-                kk, w = p["k"] + l, p["m0"] + l + 1
-                F = int(fsz[kk])
-                a = ro_base + int(p["ro"][l])
-                b = co_base + int(p["co"][l])
-                levels.append(rows_h[a:a + F * w].reshape(F, w).copy())
-                counts.append(cnt_h[b:b + F].astype(np.int64))
-                if kk > p["k"] and self.log.enabled:
-                    # the reference logs the groups generated from F_{k-1}; a bundled
-                    # level counted a superset generated from C_{k-1}
-                    self.log.line(f"{kk} candidate items {int(apriori_gen(levels[kk - 2])[0].size)}")
-                elif self.log.enabled:
-                    self.log.line(f"{kk} candidate items {int(p['G'][l])}")
-                self.log.line(f"{kk} freq items {F}")
-                # one launch counts the whole bundle: a level's time, device time and
-                # streamed bytes are its candidates' share of the bundle's
+            for l, (kk, rows, cnt) in enumerate(self._dl_decode(p, stg["rows"][i].numpy(), stg["cnt"][i].numpy(),
+                                                                fsz)):
+                F = len(cnt)
+                levels.append(rows.copy())
+                counts.append(cnt.astype(np.int64))
+                # the reference logs the groups generated from F_{k-1}; a bundled level
+                # counted a superset generated from C_{k-1}.  One launch counts the whole
+                # bundle: a level's time, device time and streamed bytes are its
+                # candidates' share of the bundle's
                 share = float(p["C"][l]) / max(float(p["C"].sum()), 1.0)
-                self.log.line(f"Use Time {kk} items {int(p['ms'] * share)}")
+                groups = (lambda kk=kk: int(apriori_gen(levels[kk - 2])[0].size)) if kk > p["k"] else int(p["G"][l])
+                self._log_level(levels, kk, groups, F, p["ms"] * share)
                 m = p["m0"] + l              # parent row length of level kk
                 hbm = int(share * p["hbm_rows"] + 4 * int(p["n_par"][l]) * m
                           + 4 * int(p["C"][l]) * (m + 1) + 3 * 4 * int(p["C"][l]))
@@ -690,8 +783,9 @@ class FastApriori:
     def _finish(self, result: MiningResult, t_start: float) -> MiningResult:
         self._result_items(result)
         if getattr(self, "_ckpt_deferred", False):
-            # every level in one batch, written by a background thread while the caller
-            # writes the outputs (Checkpointer.wait / mark_complete join it)
+            # the levels not handed over yet (none after the device loop), written by the
+            # background thread while the caller writes the outputs (Checkpointer.wait /
+            # mark_complete join it)
             self._ckpt_upto(result, len(result.levels), background=True)
         db = getattr(self, "_db_local", None)
         if db is not None:
@@ -699,6 +793,8 @@ class FastApriori:
             g = self.dcomm.all_gather_ints([db["T0"], db["ncols0"]])
             self.stats.update(T=int(g[:, 0].sum()), distinct=int(g[:, 1].sum()))
             self._db_local = None
+        if len(result.levels) >= 2:
+            self._log_tail(result.levels)
         total_k2 = sum(len(c) for c in result.counts[1:])
         self.log.line(f"Total freq items sets {total_k2}")
         self.stats["mine_ms"] = (time.perf_counter() - t_start) * 1e3

@@ -164,6 +164,39 @@ def freq_itemset_lines(res: OracleResult) -> list[str]:
     return lines
 
 
+def mining_log_lines(n_items: int, itemsets) -> list[str]:
+    """The reference's mining lines (FastApriori.scala:226, :107-108, :111-119, :127) with
+    the millisecond values masked as '#', replayed from the frequent itemsets alone:
+    the loop runs while |F_{k-1}| >= k, and a level prints the number of
+    (prefix, extensions) groups genCandidates keeps (:173-190), |F_k| and its time.
+    ``itemsets``: an iterable of rank sets (every size; sizes 1 are ignored)."""
+    by: dict[int, set] = {}
+    for s in itemsets:
+        s = frozenset(s)
+        by.setdefault(len(s), set()).add(s)
+    F1 = n_items
+    out = [f"2 candidates items {F1 * (F1 - 1) // 2}", f"2 freq items {len(by.get(2, ()))}", "Use Time 2 items #"]
+    k = 3
+    while len(by.get(k - 1, ())) >= k:
+        prev = by[k - 1]
+        # y must at least pass the subset test for x's largest item, (x - max x) + y:
+        # only the largest items of x's class mates are tried
+        mates: dict[frozenset, list[int]] = {}
+        for x in prev:
+            mates.setdefault(x - {max(x)}, []).append(max(x))
+        groups = 0
+        for x in prev:
+            top = max(x)
+            for y in mates[x - {top}]:
+                if y > top and all((x - {xi}) | {y} in prev for xi in x):
+                    groups += 1
+                    break
+        out += [f"{k} candidate items {groups}", f"{k} freq items {len(by.get(k, ()))}", f"Use Time {k} items #"]
+        k += 1
+    out.append(f"Total freq items sets {sum(len(v) for kk, v in by.items() if kk >= 2)}")
+    return out
+
+
 def run_oracle(d_lines: list[str], u_lines: list[str], min_support: float):
     D = [java_split_ws(l) for l in d_lines]
     U = [java_split_ws(l) for l in u_lines]

@@ -322,7 +322,34 @@ def init_comm(device: str | None = None, backend: str | None = None, timeout_s: 
         if be == "nccl":
             kw["device_id"] = dev
         dist.init_process_group(**kw)
+        if be == "nccl" and dist.get_world_size() > 1:
+            _check_one_gpu_per_rank(dev)
     return Comm(dist.get_rank(), dist.get_world_size(), dev, be, force=force)
+
+
+def _gpu_key(dev) -> str:
+    """This host's identity of the rank's GPU: its UUID (or PCI bus id), which a launcher
+    that narrows every rank's view to "device 0" does not hide."""
+    import socket
+    props = torch.cuda.get_device_properties(dev)
+    ident = getattr(props, "uuid", None) or getattr(props, "pci_bus_id", None)
+    if ident is None:
+        vis = next((os.environ.get(v) for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES",
+                                                "CUDA_VISIBLE_DEVICES") if os.environ.get(v)), "")
+        ident = f"{vis}/{dev.index}"
+    return f"fa_gpu/{socket.gethostname()}/{ident}"
+
+
+def _check_one_gpu_per_rank(dev) -> None:
+    """RCCL ranks of one communicator must not share a GPU, also when each rank's
+    *_VISIBLE_DEVICES shows it a single device (the same value exported to
+    every local rank).  Every rank counts itself under its GPU's key in the rendezvous
+    store: a second rank on the same GPU sees 2 and fails fast."""
+    store = dist.distributed_c10d._get_default_store()     # noqa: SLF001
+    n = store.add(_gpu_key(dev), 1)
+    if n > 1:
+        raise RuntimeError(f"rank {dist.get_rank()} shares its GPU with another rank: RCCL needs one GPU per rank "
+                           "(FA_DIST_BACKEND=gloo lets ranks share a GPU for tests)")
 
 
 def shutdown_comm(comm: Comm) -> None:

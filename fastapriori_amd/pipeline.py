@@ -152,6 +152,18 @@ def run_job(cfg: JobConfig, comm=None) -> dict:
                        n_rules=ar.rules().n_rules, world_size=comm.world_size)
         log.metric(phase="job", **{k: v for k, v in summary.items() if not isinstance(v, dict)})
         return summary
+    except BaseException as e:
+        # the job's own failure wins: a background checkpoint error is only attached to it
+        if ckpt is not None:
+            try:
+                ckpt.wait()
+            except BaseException as ck_err:   # noqa: BLE001 (logged; the original error propagates)
+                import sys
+                print(f"fastapriori: checkpoint thread also failed: {type(ck_err).__name__}: {ck_err}",
+                      file=sys.stderr)
+                log.metric(phase="checkpoint_error", error=f"{type(ck_err).__name__}: {ck_err}")
+            ckpt = None
+        raise e
     finally:
         if ckpt is not None:
             ckpt.wait()                  # the checkpoint is complete before the job returns

@@ -49,16 +49,42 @@ class Checkpointer:
             return int(fault)
         return 0
 
-    def _write_level(self, result: MiningResult, k: int, meta: bool = True) -> None:
+    def _write_level(self, result: MiningResult, k: int, meta: bool = True, rows=None, counts=None) -> None:
         """level_k.npz, then (meta) meta.json saying levels 1..k are done: the level file
-        lands before the meta that counts it, so a crash leaves a consistent checkpoint."""
-        if self.rank == 0 and k <= len(result.levels):
+        lands before the meta that counts it, so a crash leaves a consistent checkpoint.
+        rows / counts: the level's arrays when result does not hold them yet (the device
+        level loop's staged copies, before its results readback)."""
+        if rows is None and k > len(result.levels):
+            return
+        if self.rank == 0:
+            if rows is None:
+                rows, counts = result.levels[k - 1], result.counts[k - 1]
+
             def w(tmp):
                 with open(tmp, "wb") as f:
-                    np.savez(f, rows=result.levels[k - 1], counts=result.counts[k - 1])
+                    np.savez(f, rows=rows, counts=counts)
             self._atomic(os.path.join(self.dir, f"level_{k}.npz"), w)
             if meta:
                 self._write_meta(result, k)
+
+    def submit(self, fn) -> None:
+        """Run fn on the checkpoint thread after everything submitted before it (the
+        device level loop hands each bundle's staged results over this way); an error
+        is raised by the next wait()."""
+        import threading
+        prev = self._thread
+
+        def work():
+            try:
+                if prev is not None:
+                    prev.join()
+                if self._error is None:
+                    fn()
+            except BaseException as e:       # surfaced by wait()
+                self._error = e
+
+        self._thread = threading.Thread(target=work, name="fa-ckpt", daemon=True)
+        self._thread.start()
 
     def _write_meta(self, result: MiningResult, k: int, complete: bool = False) -> None:
         meta = {"items": result.items, "min_count": result.min_count, "n_lines": result.n_lines,

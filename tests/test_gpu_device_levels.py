@@ -8,12 +8,15 @@ counted on the device window by window), wide vocabularies (F1 > 4096), prefixes
 past the records' 12 inline ids, and an empty F_2.
 Reference semantics: FastApriori.scala:110-160.
 """
+import re
+
 import numpy as np
 import pytest
 import torch
 
 import fastapriori_amd.models.apriori as ap
 from fastapriori_amd.models.apriori import FastApriori, MinerConfig
+from fastapriori_amd.models.oracle import mining_log_lines
 from fastapriori_amd.parallel.comm import Comm
 from fastapriori_amd.utils.io import generate_shard
 from fastapriori_amd.utils.metrics import Logger
@@ -164,9 +167,37 @@ def test_f2_stays_on_device_until_the_flush(monkeypatch):
             got = res
         else:
             ref = res
-        logs[dl] = [l.split(" items")[0] for l in buf.getvalue().splitlines() if "items" in l and "Use Time" not in l]
+        logs[dl] = [re.sub(r"(Use Time \d+ items )\d+$", r"\g<1>#", l[5:]) for l in buf.getvalue().splitlines()
+                    if l.startswith("==== ")]
     _same(got, ref)
     assert got.as_dict() == _mine(cpu, 0.002)[0].as_dict()
-    # "k candidate items" / "k freq items" lines in the same order (counts may differ only for
-    # bundled candidate supersets, which both loops log the same way)
-    assert logs[True] == logs[False]
+    # both loops print exactly the reference's lines (FastApriori.scala:107-127), replayed
+    # from the itemsets by the oracle's loop
+    want = mining_log_lines(len(got.items), got.as_dict().keys())
+    assert logs[True] == want and logs[False] == want
+
+
+def test_u16_window_accumulators_drain_mid_run(monkeypatch):
+    # packed-u16 window accumulators drain into the u32 counts every
+    # 65535 / (SW * 64) slabs.  One workgroup walks every slab (fa_hip_debug_slab_max_wg),
+    # and items 0-3 sit in every row, so their level-3 and level-4 counters pass 65535
+    # several times: a broken mid-run drain would wrap them.
+    import fastapriori_amd.ops.primitives as prim
+    from fastapriori_amd.ops import _native
+    from fastapriori_amd.utils.io import parse_bytes
+    rng = np.random.default_rng(11)
+    n = 300_000
+    extra = np.argsort(rng.random((n, 37)), axis=1)[:, :5] + 4
+    text = "\n".join("0 1 2 3 " + " ".join(map(str, r)) for r in extra.tolist()) + "\n"
+    cpu = parse_bytes(text.encode(), device=torch.device("cpu"))
+    ref, _ = _mine(cpu, 0.002)
+    assert max(ref.counts[2]) > 4 * 65535
+    monkeypatch.setattr(prim, "_LDS_BYTES", _multipass_lds(ref, 2))
+    hip = _native.hip()
+    hip.fa_hip_debug_slab_max_wg(1)
+    try:
+        got, st = _mine(parse_bytes(text.encode(), device=DEV), 0.002, dedup="off", trim_min_rows=1 << 40)
+    finally:
+        hip.fa_hip_debug_slab_max_wg(0)
+    assert st.get("device_multipass", 0) >= 1, st
+    _same(got, ref)

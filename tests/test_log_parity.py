@@ -14,6 +14,9 @@ import sys
 
 import pytest
 
+from fastapriori_amd.models import oracle
+from fastapriori_amd.utils.jvm import java_split_ws
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 GOLDEN_D = "1 2 3\n1 2 4\n2 3 4\n1 2 4\n2 4\n4 5\n1 2\n"
@@ -76,13 +79,40 @@ def test_golden_log_lines_match_the_reference(tmp_path):
     assert _run_cli(tmp_path, GOLDEN_D, GOLDEN_U, 0.25) == GOLDEN_LINES
 
 
+def _mining_part(lines: list[str]) -> list[str]:
+    return lines[:lines.index(next(l for l in lines if l.startswith("Total freq items sets"))) + 1]
+
+
+def _expected(d_text: str, min_sup: float) -> list[str]:
+    # the reference loop replayed from the oracle's itemsets (models/oracle.mining_log_lines)
+    res = oracle.mine([java_split_ws(l) for l in d_text.splitlines()], min_sup)
+    return oracle.mining_log_lines(len(res.items), res.itemsets)
+
+
+# the loop's edges (FastApriori.scala:111-119):
+# STOP_D: F_4 = 4 rows < 5, so the reference never enters level 5 (no level-5 lines,
+# even though a bundle may count level 5 speculatively)
+STOP_D = "1 2 3 4\n1 2 3 5\n1 2 4 5\n1 3 4 5\n" * 2
+# NOCAND_D: F_2 = 3 disjoint pairs (3 >= 3), so level 3 is entered with no candidates
+# and prints all three lines
+NOCAND_D = "1 2\n1 2\n3 4\n3 4\n5 6\n5 6\n"
+EDGE_CASES = [(STOP_D, 0.25, ["3 candidate items 6", "3 freq items 10", "Use Time 3 items #",
+                               "4 candidate items 4", "4 freq items 4", "Use Time 4 items #"]),
+              (NOCAND_D, 0.3, ["3 candidate items 0", "3 freq items 0", "Use Time 3 items #"])]
+
+
 def test_candidate_line_counts_prefix_groups(tmp_path):
-    lines = _run_cli(tmp_path, MULTI_D, MULTI_U, 0.5)
+    lines = _mining_part(_run_cli(tmp_path, MULTI_D, MULTI_U, 0.5))
     assert "3 candidate items 3" in lines          # 3 groups (4 candidates)
-    assert "3 freq items 4" in lines
-    assert "4 candidate items 1" in lines
-    assert "4 freq items 1" in lines
-    assert lines.index("3 candidate items 3") < lines.index("3 freq items 4") < lines.index("4 candidate items 1")
+    assert lines == _expected(MULTI_D, 0.5)
+
+
+@pytest.mark.parametrize("case", range(len(EDGE_CASES)))
+def test_loop_edges_match_the_reference(tmp_path, case):
+    d, sup, levels = EDGE_CASES[case]
+    lines = _mining_part(_run_cli(tmp_path, d, "1\n", sup))
+    assert lines == _expected(d, sup)
+    assert [l for l in lines if not l.startswith(("2 ", "Use Time 2", "Total"))] == levels
 
 
 @pytest.mark.gpu
@@ -94,4 +124,16 @@ def test_golden_log_lines_on_gpu_with_temp(tmp_path):
 @pytest.mark.gpu
 def test_candidate_line_counts_prefix_groups_on_gpu(tmp_path):
     lines = _run_cli(tmp_path, MULTI_D, MULTI_U, 0.5, device="cuda", temp=True)
-    assert "3 candidate items 3" in lines and "4 candidate items 1" in lines
+    assert _mining_part(lines) == _expected(MULTI_D, 0.5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(len(EDGE_CASES)))
+def test_loop_edges_match_the_reference_on_gpu(tmp_path, case):
+    # the device level loop (bundles with speculative levels, device stop test)
+    d, sup, levels = EDGE_CASES[case]
+    for temp in (False, True):
+        sub = tmp_path / f"t{int(temp)}"
+        sub.mkdir()
+        lines = _mining_part(_run_cli(sub, d, "1\n", sup, device="cuda", temp=temp))
+        assert lines == _expected(d, sup), (temp, lines)
