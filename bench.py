@@ -115,19 +115,21 @@ def _pread_floor(path: str) -> float:
     from fastapriori_amd.utils.env import num_threads
     n = os.path.getsize(path)
     import torch
-    ring = io._ring if io._ring else [torch.empty(io._RING_SLOT, dtype=torch.uint8,
+    from fastapriori_amd.tuning import TUNING
+    NS = max(1, int(TUNING.ring_slots))
+    ring = io._ring[:NS] if len(io._ring) >= NS else [torch.empty(io._RING_SLOT, dtype=torch.uint8,
                                                   pin_memory=torch.cuda.is_available())
-                                      for _ in range(io._RING_SLOTS)]
+                                      for _ in range(NS)]
     fd = os.open(path, os.O_RDONLY)
     t0 = time.perf_counter()
     try:
         def rd(c):
             off, m = c * io._RING_SLOT, min(io._RING_SLOT, n - c * io._RING_SLOT)
-            mv = memoryview(ring[c % io._RING_SLOTS].numpy())
+            mv = memoryview(ring[c % NS].numpy())
             got = 0
             while got < m:
                 got += os.preadv(fd, [mv[got:m]], off + got)
-        with ThreadPoolExecutor(min(num_threads(), io._RING_SLOTS)) as ex:
+        with ThreadPoolExecutor(min(num_threads(), NS)) as ex:
             list(ex.map(rd, range((n + io._RING_SLOT - 1) // io._RING_SLOT)))
     finally:
         os.close(fd)
@@ -233,10 +235,22 @@ def _e2e_window(args, comm, n_txn, min_sup, cfgv, miner_cfg, sync):
     }, path
 
 
+def _cpu_ranges(cpus: list) -> str:
+    """[0, 1, 2, 5] -> "0-2,5" (sysfs cpulist form)."""
+    out, i = [], 0
+    while i < len(cpus):
+        j = i
+        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
+            j += 1
+        out.append(str(cpus[i]) if i == j else f"{cpus[i]}-{cpus[j]}")
+        i = j + 1
+    return ",".join(out)
+
+
 def _per_rank(args, comm, miner, shard, own_ms, comm_ms, comm_calls, sync) -> list | None:
     """Per-rank diagnostics of the timed steps, gathered to rank 0: the rank's own
     ms per step, host ms held inside collectives (Comm._timed) and collectives per
-    step; then ONE extra, untimed run with hipEvent phase timers (FA_GPU_TIMING):
+    step; then ONE extra, untimed run with hipEvent phase timers (MinerConfig.timing):
     device time of the top-level phases (F1, compression, pairs, each level or
     bundle; gaps inside a phase count as busy) and the rest of that run's wall time
     as host-bound time.  A bad scaling curve then shows which rank and which part
@@ -244,10 +258,15 @@ def _per_rank(args, comm, miner, shard, own_ms, comm_ms, comm_calls, sync) -> li
     import re
     if args.steps <= 0:
         return None
+    from fastapriori_amd.parallel.affinity import PLACEMENT
+    from fastapriori_amd.utils.env import num_threads
     rec = {"rank": comm.rank, "ms_per_step": round(own_ms, 3), "comm_ms_per_step": round(comm_ms, 3),
-           "collectives_per_step": round(comm_calls, 1)}
+           "collectives_per_step": round(comm_calls, 1),
+           # the rank's host placement (parallel.affinity: its GPU's NUMA-local CPU share)
+           "numa_node": PLACEMENT.get("node"), "cpus": _cpu_ranges(sorted(os.sched_getaffinity(0))),
+           "host_threads": num_threads()}
     if comm.device.type == "cuda":
-        os.environ["FA_GPU_TIMING"] = "1"
+        timing, miner.cfg.timing = miner.cfg.timing, "events"
         try:
             sync()
             t0 = time.perf_counter()
@@ -255,7 +274,7 @@ def _per_rank(args, comm, miner, shard, own_ms, comm_ms, comm_calls, sync) -> li
             sync()
             run_ms = (time.perf_counter() - t0) * 1e3
         finally:
-            os.environ.pop("FA_GPU_TIMING", None)
+            miner.cfg.timing = timing
         ph = miner.stats.get("gpu_phase_ms", {})
         top = {k: v for k, v in ph.items() if re.fullmatch(r"f1|compress|pairs|level\d+", k)}
         gpu = sum(top.values())

@@ -384,7 +384,7 @@ template <bool kDiag>
 __device__ __forceinline__ void pair_rows16_chunk_t(PairRowsLds& L, const uint8_t* __restrict__ cnt,
                                                     const int64_t* __restrict__ base,
                                                     const uint8_t* __restrict__ lr, int64_t T, int64_t nbatch,
-                                                    int bi, int bj, int64_t q0, int64_t q1, int dbg) {
+                                                    int bi, int bj, int64_t q0, int64_t q1) {
   uint32_t* tile = L.tile;
   auto& sa = L.sa;
   auto& sb = L.sb;
@@ -438,7 +438,7 @@ __device__ __forceinline__ void pair_rows16_chunk_t(PairRowsLds& L, const uint8_
     }
     // flattened pairs (staged batches): one lane per (row, pair) instead of per
     // (row, position) -- see the flat branch below; rowtab then lists the rows with pairs
-    const bool flat = stA && stB && !(dbg & (8 | 16)) && !(dbg & (diag ? 32 : 64));
+    const bool flat = stA && stB;
     const int npr = diag ? ci * (ci - 1) / 2 : ci * cj;
     const bool own = flat ? npr > 0 : ci > 0;
     const unsigned long long M = __ballot(own);
@@ -498,7 +498,7 @@ __device__ __forceinline__ void pair_rows16_chunk_t(PairRowsLds& L, const uint8_
             j = (int)(((float)t + 0.5f) * __builtin_amdgcn_rcpf((float)c));
             i = t - j * c;
           }
-          if (f < NP && !(dbg & 1)) {
+          if (f < NP) {
             const int a = (int)As[(px & 0x3FF) + i];
             const int b = (int)Bs[((px >> 10) & 0x3FF) + j];
             atomicAdd(&tile[a * (kPB16 / 2) + ((b >> 1) ^ (a & 31))], (b & 1) ? 0x10000u : 1u);
@@ -524,7 +524,7 @@ __device__ __forceinline__ void pair_rows16_chunk_t(PairRowsLds& L, const uint8_
         int j0 = __shfl(jbeg, row, 64);
         const int j1 = __shfl(jend, row, 64);
         if (diag) j0 = p + 1;
-        if (p < SA && !(dbg & 1)) {
+        if (p < SA) {
           // word of (a, b) = a * 128 + ((b >> 1) ^ (a & 31)): the bank (word mod 32)
           // depends on a as well as b, so the lanes of one row (different a, same b
           // in the off-diagonal tiles) hit different banks (pair_tile16_word)
@@ -537,9 +537,7 @@ __device__ __forceinline__ void pair_rows16_chunk_t(PairRowsLds& L, const uint8_
         }
       };
       int cs = 0;                                    // non-empty rows started before the window
-      if (dbg & 8) {
-        // profiling split: batch-level work only (no windows)
-      } else if (SA <= kRowsStage) {
+      if (SA <= kRowsStage) {
         // row-start masks, 4 windows per LDS round trip
 #pragma unroll
         for (int w0 = 0; w0 < kRowsWin; w0 += 4) {
@@ -594,9 +592,9 @@ __device__ __forceinline__ void pair_rows16_chunk_t(PairRowsLds& L, const uint8_
 __device__ __forceinline__ void pair_rows16_chunk(PairRowsLds& L, const uint8_t* __restrict__ cnt,
                                                   const int64_t* __restrict__ base,
                                                   const uint8_t* __restrict__ lr, int64_t T, int64_t nbatch,
-                                                  int bi, int bj, int64_t q0, int64_t q1, int dbg) {
-  if (bi == bj) pair_rows16_chunk_t<true>(L, cnt, base, lr, T, nbatch, bi, bj, q0, q1, dbg);
-  else pair_rows16_chunk_t<false>(L, cnt, base, lr, T, nbatch, bi, bj, q0, q1, dbg);
+                                                  int bi, int bj, int64_t q0, int64_t q1) {
+  if (bi == bj) pair_rows16_chunk_t<true>(L, cnt, base, lr, T, nbatch, bi, bj, q0, q1);
+  else pair_rows16_chunk_t<false>(L, cnt, base, lr, T, nbatch, bi, bj, q0, q1);
 }
 
 // Packed-u16 tile -> global counts.  With an even row stride (ld) the two
@@ -645,7 +643,7 @@ constexpr int64_t kQSubB = 511;   // batches per sub-chunk: 32704 rows
 __global__ __launch_bounds__(1024) void k_pair_queue16(
     const uint8_t* __restrict__ cnt, const int64_t* __restrict__ base, const uint8_t* __restrict__ lr,
     int64_t T, int64_t nbatch, int32_t F1, int64_t ld, int nb, int nbp, int* __restrict__ qctr, int nsub,
-    uint32_t* __restrict__ out, int dbg) {
+    uint32_t* __restrict__ out) {
   __shared__ PairRowsLds L;
   __shared__ int s_take[2];
   for (int t = threadIdx.x; t < kTriTab; t += blockDim.x) {
@@ -685,7 +683,7 @@ __global__ __launch_bounds__(1024) void k_pair_queue16(
     if (tt < 0 || got < 0) break;
     t = tt;
     if (tt != cur) {
-      if (cur >= 0 && !(dbg & 2)) {
+      if (cur >= 0) {
         int bi, bj;
         tri_index(cur, nb, bi, bj);
         pair_tile16_flush(L.tile, bi, bj, F1, ld, out);
@@ -698,7 +696,7 @@ __global__ __launch_bounds__(1024) void k_pair_queue16(
     int bi, bj;
     tri_index(cur, nb, bi, bj);
     const int64_t q0 = (int64_t)got * kQSubB, q1 = min(nbatch, q0 + kQSubB);
-    pair_rows16_chunk(L, cnt, base, lr, T, nbatch, bi, bj, q0, q1, dbg);
+    pair_rows16_chunk(L, cnt, base, lr, T, nbatch, bi, bj, q0, q1);
     __syncthreads();
     // drain: bit 15 of either counter -> 32768 to the global count
     const int rb0 = bi * kPB16, cb0 = bj * kPB16;
@@ -710,12 +708,12 @@ __global__ __launch_bounds__(1024) void k_pair_queue16(
       int r, c;
       pair_tile16_word(i, rb0, cb0, r, c);
       if (r >= F1) continue;
-      if ((hb & 0x8000u) && c < F1 && !(dbg & 2)) atomicAdd(&out[(int64_t)r * ld + c], 32768u);
-      if ((hb >> 16) && c + 1 < F1 && !(dbg & 2)) atomicAdd(&out[(int64_t)r * ld + c + 1], 32768u);
+      if ((hb & 0x8000u) && c < F1) atomicAdd(&out[(int64_t)r * ld + c], 32768u);
+      if ((hb >> 16) && c + 1 < F1) atomicAdd(&out[(int64_t)r * ld + c + 1], 32768u);
     }
     __syncthreads();
   }
-  if (cur >= 0 && !(dbg & 2)) {
+  if (cur >= 0) {
     int bi, bj;
     tri_index(cur, nb, bi, bj);
     pair_tile16_flush(L.tile, bi, bj, F1, ld, out);
@@ -1216,7 +1214,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
     const int64_t* __restrict__ roff, const int32_t* __restrict__ ranks, const int32_t* __restrict__ src,
     int64_t ncols, const int32_t* __restrict__ item_map, int F1, int n_used, const int32_t* __restrict__ gpre,
     const int4* __restrict__ rec, int G_arg, int C, const int32_t* __restrict__ wword, uint32_t* __restrict__ out,
-    const uint64_t* __restrict__ bm, int64_t Wp, const int32_t* __restrict__ bm_rows, int dbg,
+    const uint64_t* __restrict__ bm, int64_t Wp, const int32_t* __restrict__ bm_rows, int flags,
     const int32_t* __restrict__ g_dev) {
   // g_dev: the piece count from device memory (device-planned bundles, levels.hip)
   const int G = g_dev ? *g_dev : G_arg;
@@ -1225,10 +1223,10 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
   constexpr int SWP = SW + 2;                       // row stride: odd number of 16-B slots
   constexpr int RS = SWP / 2;
   uint64_t* slab = reinterpret_cast<uint64_t*>(lds4);
-  // dbg & 8: two u16 counters per accumulator word (unit weights; twice the candidates
+  // flags & 8: two u16 counters per accumulator word (unit weights; twice the candidates
   // per accumulator pass), drained into the u32 global counts before they can carry: a
   // slab adds at most SW * 64 to a counter
-  const bool acc16 = !kWeighted && (dbg & 8) != 0;
+  const bool acc16 = !kWeighted && (flags & 8) != 0;
   const int nacc = acc16 ? (C + 1) >> 1 : C;
   constexpr int kFlush16 = 65535 / (SW * 64);
   uint32_t* acc = reinterpret_cast<uint32_t*>(slab + (size_t)n_used * SWP);
@@ -1318,9 +1316,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
       flush();
       nsl = 1;
     }
-    if (dbg & 1) {
-      // profiling split (FA_SLAB_DEBUG=1): no slab build
-    } else if (kBuild == kBuildBM) {
+    if (kBuild == kBuildBM) {
       slab_copy_bm<SW, SWP, false>(lds4, n_used, bm, Wp, bm_rows, w0, W);
     } else {
       {
@@ -1378,7 +1374,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
     // the record says the piece is a sibling of this thread's previous one (flag 1),
     // p = q & the last prefix row, kept for the next piece of the same prefix (flag 2)
     uint4 p[SW / 2], qv[SW / 2];
-    for (int g = g0; g < ((dbg & 2) ? 0 : G); g += kSlabThreads) {
+    for (int g = g0; g < G; g += kSlabThreads) {
       // this thread's next piece (after its last one: its first, for the next slab)
       const int gn = g + kSlabThreads < G ? g + kSlabThreads : g0;
       const int4 na = rec[3 * gn], nb = rec[3 * gn + 1], nc = rec[3 * gn + 2];
@@ -1416,9 +1412,9 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
         if (j < m) and_row(p, pr[j]);
       }
       }
-      // an all-zero prefix skips its extensions; dense levels (dbg & 4: every frequent
+      // an all-zero prefix skips its extensions; dense levels (flags & 4: every frequent
       // prefix expects >= 4 rows per slab) skip the test instead (32 VALU ops per piece at SW = 16)
-      uint32_t any = dbg & 4;
+      uint32_t any = flags & 4;
       if (!any) {
 #pragma unroll
         for (int q = 0; q < SW / 2; ++q) any |= p[q].x | p[q].y | p[q].z | p[q].w;
@@ -1522,26 +1518,23 @@ FA_API int fa_hip_build_bitmaps_wave(const int64_t* roff, const int32_t* ranks, 
   FA_LAUNCH_RET();
 }
 
-// FA_PAIR_FLAT: 1 (default) flattened pairs in every tile, 2 in the off-diagonal tiles
-// only, 0 none, 3 diagonal tiles only -> k_pair_queue16 dbg bits 16 / 32 / 64.
-// Measured (T10I4D100M pair call) with the square-root decode of the diagonal tiles:
-// 2 13.7, 1 13.9, 0 14.5, 3 14.8 ms (the per-position loops won); with the triangular
-// decode table (PairRowsLds::tri) 1 beats 2 (headline A/B 45.5-46.3 vs 47.1-47.3 ms).
-static int pair_flat_bits(int v) { return v == 0 ? 16 : v == 2 ? 32 : v == 3 ? 64 : 0; }
+// Flattened pairs in every staged tile (k_pair_queue16): measured against flattening only
+// the off-diagonal tiles, only the diagonal ones and none (T10I4D100M pair call, square-root
+// decode of the diagonal tiles: 13.9 / 13.7 / 14.8 / 14.5 ms; with the triangular decode
+// table PairRowsLds::tri the all-tiles form won the headline A/B, 45.5-46.3 vs 47.1-47.3 ms).
 
 // Gram of words [0, W) of bm's rows on the matrix cores, every count multiplied by
 // scale before it is added to out (a weight class of a deduplicated layout: its
 // columns all carry the same weight, FastApriori.scala:233-235).
 FA_API int fa_hip_pair_gram_mfma(const uint64_t* bm, int32_t F1, int64_t Wp, int64_t W, uint32_t* out,
-                                 int target_wgs, uint32_t scale, hipStream_t st) {
+                                 int target_wgs, uint32_t scale, int fp4, hipStream_t st) {
   if (W <= 0 || F1 < 2) return 0;
   const int nt = (F1 + kMT4 - 1) / kMT4;
   const int ntp = nt * (nt + 1) / 2;
   int64_t nk = std::max<int64_t>(1, (target_wgs + ntp - 1) / ntp);
   int64_t kchunk = (W + nk - 1) / nk;
   kchunk = std::max<int64_t>(kMW, (kchunk + kMW - 1) / kMW * kMW);
-  // FP4 form by default (T40I10D100M pair phase 68 -> 46 ms); FA_GRAM_FP4=0: the i8 form
-  const bool fp4 = !(getenv("FA_GRAM_FP4") && atoi(getenv("FA_GRAM_FP4")) == 0);
+  // fp4: the FP4 form (T40I10D100M pair phase 68 -> 46 ms); 0: the i8 form (a test oracle)
   if (fp4) kchunk = std::min<int64_t>(kchunk, (int64_t)1 << 18);   // f32-exact sums: <= 2^24 transactions
   nk = (W + kchunk - 1) / kchunk;
   if (fp4)
@@ -1636,10 +1629,9 @@ FA_API int fa_hip_count_slab_rec_cls(const int64_t* roff, const int32_t* ranks, 
 #undef FA_REC_MODE
   if (!kern) return 1;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  const int dbg = (getenv("FA_SLAB_DEBUG") ? atoi(getenv("FA_SLAB_DEBUG")) : 0) | ((cls & 2) ? 4 : 0) |
-                  (acc16 ? 8 : 0);
+  const int flags = ((cls & 2) ? 4 : 0) | (acc16 ? 8 : 0);
   hipLaunchKernelGGL(kern, dim3((unsigned)n_wg), dim3(kSlabThreads), lds, st, roff, ranks, src, ncols, item_map, F1,
-                     n_used, gpre, (const int4*)rec, G, C, wword, out, bm, Wp, bm_rows, dbg, g_dev);
+                     n_used, gpre, (const int4*)rec, G, C, wword, out, bm, Wp, bm_rows, flags, g_dev);
   FA_LAUNCH_RET();
 }
 
@@ -1710,8 +1702,6 @@ FA_API int fa_hip_pair_queue16(const uint8_t* cnt, const int64_t* base, const ui
   }
   n_wg = (int)std::min<int64_t>(n_wg, (int64_t)nsub * nbp);
   hipLaunchKernelGGL(k_pair_queue16, dim3((unsigned)n_wg), dim3(64 * kPW), 0, st, cnt, base, lr, T, nbatch, F1, ld,
-                     nb, nbp, qctr, nsub, out,
-                     (getenv("FA_PAIR_DEBUG") ? atoi(getenv("FA_PAIR_DEBUG")) : 0) |
-                         pair_flat_bits(getenv("FA_PAIR_FLAT") ? atoi(getenv("FA_PAIR_FLAT")) : 1));
+                     nb, nbp, qctr, nsub, out);
   FA_LAUNCH_RET();
 }

@@ -457,9 +457,8 @@ FA_API int fa_hip_ag_chain(const int32_t* P0, int64_t n0, int m0, int F1, void* 
     P = rows_out;
     n = C;
     ++m;
-    // levels 1.. without a host round trip per level (FA_GEN_DEVCHAIN=0: the loop below)
-    static const bool devchain = [] { const char* e = getenv("FA_GEN_DEVCHAIN"); return !e || atoi(e) != 0; }();
-    if (first_free && l == 0 && devchain)
+    // levels 1.. without a host round trip per level (other chains: the loop below)
+    if (first_free && l == 0)
       return ag_chain_dev(P, n, m, nw, w0, w, ws_bytes, host, hoff, host_cap, max_levels, growth, total, last, mark,
                           MW, lds, sizes, st);
   }
@@ -1031,7 +1030,7 @@ static_assert(sizeof(DlPost) == 31 * 8, "DlPost layout (ops.primitives.DlPostC)"
 
 FA_API int fa_hip_dl_plan(const int64_t* desc, int L, long long* ctl, int F1, int32_t* item_map, void* rec,
                           int64_t max_pieces, int32_t* part, int64_t part_cap, int32_t* gpre, int64_t gpre_cap,
-                          hipStream_t st);
+                          int sw, hipStream_t st);
 FA_API int fa_hip_count_slab_rec_cls(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
                                      const int32_t* item_map, int F1, int n_used, const int32_t* gpre,
                                      const void* rec, int G, int C, const int32_t* wword, uint32_t* out, int sw,
@@ -1070,7 +1069,7 @@ static void dl_post(DlPost* P, const int64_t* desc, int L, long long* ctl, const
     if (cap >= std::min<int64_t>(C, 8192) || (w == 4 && cap >= 1024)) { sw = w; break; }
   }
   if (sw == 0 || C > cap) return;
-  if (fa_hip_dl_plan(desc, L, ctl, F1, P->item_map, P->rec, C, P->part, P->part_cap, P->gpre, P->gpre_cap,
+  if (fa_hip_dl_plan(desc, L, ctl, F1, P->item_map, P->rec, C, P->part, P->part_cap, P->gpre, P->gpre_cap, sw,
                      st) != 0)
     return;                                        // (e.g. long prefixes past gpre_cap: the caller plans)
   (void)hipMemsetAsync(P->out, 0, 4 * (size_t)C, st);

@@ -229,6 +229,130 @@ __global__ __launch_bounds__(kDlPB) void k_dl_pieces_emit(const DlLevels D, cons
   if (rem) dl_write_rec(rec, slot[rem], cand + 8 * full, rem, m, ids, ex + 8 * full, item_map, goff);
 }
 
+// ---------------------------------------------------------------------------
+// Bank-aware lane assignment of the piece records.
+//
+// k_count_slab_rec reads a piece's slab rows with ds_read_b128, where the LDS serves
+// a wave in four 16-lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}, and the same
+// +32), one cycle per group when its lanes hit distinct 16-B slots of the 256-B bank
+// row (MI355X_MICROARCH.md, LDS).  A slab row of r sits at slot (r * RS + q) mod 16
+// (RS = (SW + 2) / 2 slots: odd), so two lanes of one group conflict whenever their
+// rows differ and agree mod 16.  With the planner's lexicographic order the rows a
+// group reads at one instruction are close to random: the LDS replays 2.3x the
+// conflict-free cycles (PMC: 41-52 % of the slab kernels' LDS cycles are bank
+// conflicts).  Here each aligned window of 64 * ws records that share n_ext and m
+// (one wave step per 64) is re-dealt to the window's 4 * kLaWs lane groups greedily, in
+// record order: a record goes to the group where its rows add the fewest conflicts
+// (a slot holding another row costs its occupancy; the same row broadcasts).  The
+// records only move between lanes -- candidate indices travel with them -- so the
+// counts are unchanged.  CPU model of the T10I4 bundle 3-4 plan: replayed cycles
+// 2.33x -> 1.60x of conflict-free with 4-step windows (16-step windows: 1.29x, but
+// the deal's sequential latency grows with the window).
+// ---------------------------------------------------------------------------
+constexpr int kLaWs = 4;             // wave steps per window: 16 lane groups (one DPP row)
+constexpr int kLaMaxPos = 20;        // 12 inline prefix rows + 8 extensions
+
+__device__ __forceinline__ int la_u16(const int4& v, int k) {
+  const int w = (k >> 1) == 0 ? v.x : (k >> 1) == 1 ? v.y : (k >> 1) == 2 ? v.z : v.w;
+  return (k & 1) ? (int)((uint32_t)w >> 16) : (w & 0xFFFF);
+}
+
+// slab row of the record's read position pos: prefix rows 0..m-1, then extensions
+__device__ __forceinline__ int la_row(const int4& a, const int4& b, const int4& c, int m, int pos) {
+  if (pos < m) return pos < 4 ? la_u16(a, 4 + pos) : la_u16(c, pos - 4);
+  return la_u16(b, pos - m);
+}
+
+// min over each 16-lane DPP row (row_ror 8, 4, 2, 1): every lane of the row gets it
+__device__ __forceinline__ int la_row_min(int v) {
+  v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x128, 0xf, 0xf, false));
+  v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x124, 0xf, 0xf, false));
+  v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x122, 0xf, 0xf, false));
+  v = min(v, __builtin_amdgcn_update_dpp(v, v, 0x121, 0xf, 0xf, false));
+  return v;
+}
+
+// One wave per window of kLaWs * 64 records.  Lane (q, g) = (lane >> 4, lane & 15):
+// g is one of the window's 16 lane groups (ds_read_b128 group g % 4 of wave step
+// g / 4), q takes read positions q, q + 4, ...; a record's cost is summed over q, the
+// winner is the DPP-row minimum.  State per (group, position, slot): the first row
+// seen there (16 bits) and the rows there so far (16 bits), one LDS word.
+__global__ __launch_bounds__(64) void k_dl_lane_assign(int4* __restrict__ rec, const long long* __restrict__ c,
+                                                       int rs) {
+  constexpr int NW = 64 * kLaWs, NG = 4 * kLaWs;
+  constexpr int kPq = kLaMaxPos / 4;             // positions per lane
+  __shared__ int4 win[3 * NW];
+  __shared__ uint16_t rws[NW][kLaMaxPos];        // slab row of every record's read position
+  __shared__ uint32_t st[NG][kLaMaxPos][16];
+  __shared__ int16_t dst[NW];
+  const int G = reinterpret_cast<const int32_t*>(c + 221)[0];
+  const int64_t base = (int64_t)blockIdx.x * NW;
+  if (base + NW > G) return;                       // a partial last window keeps its order
+  const int lane = threadIdx.x;
+  for (int i = lane; i < 3 * NW; i += 64) win[i] = rec[3 * base + i];
+  for (int i = lane; i < NG * kLaMaxPos * 16; i += 64) (&st[0][0][0])[i] = 0xFFFFu;
+  wave_lds_sync();
+  const int y0 = win[0].y & 0x1FFFF;               // n_ext | m << 8 | long-prefix flag
+  bool same = true;
+  for (int i = lane; i < NW; i += 64) same = same && (win[3 * i].y & 0x1FFFF) == y0;
+  if (__ballot(!same) != 0ull) return;             // mixed n_ext / m (bucket or level edge)
+  const int n_ext = y0 & 0xFF, m = (y0 >> 8) & 0xFF;
+  if ((y0 >> 16) || m > 12 || m + n_ext > kLaMaxPos) return;
+  const int R = m + n_ext;
+  for (int i = lane; i < NW; i += 64) {
+    const int4 a = win[3 * i], b = win[3 * i + 1], cc = win[3 * i + 2];
+    for (int pos = 0; pos < R; ++pos) rws[i][pos] = (uint16_t)la_row(a, b, cc, m, pos);
+  }
+  wave_lds_sync();
+  const int g = lane & 15, q = lane >> 4;
+  int fill = 0;                                    // records dealt to group g
+  for (int i = 0; i < NW; ++i) {
+    int rr[kPq];
+    uint32_t w[kPq];
+#pragma unroll
+    for (int t = 0; t < kPq; ++t) {
+      const int pos = q + 4 * t;
+      rr[t] = pos < R ? (int)rws[i][pos] : -1;
+      w[t] = pos < R ? st[g][pos][(rr[t] * rs) & 15] : 0xFFFFu;
+    }
+    int cost = 0;
+#pragma unroll
+    for (int t = 0; t < kPq; ++t) {
+      const int o = (int)(w[t] & 0xFFFF);
+      if (o != 0xFFFF && o != rr[t]) cost += (int)(w[t] >> 16);
+    }
+    cost += __shfl_xor(cost, 16, 64);
+    cost += __shfl_xor(cost, 32, 64);
+    if (fill >= 16) cost = 1 << 20;
+    const int win_g = la_row_min((cost << 4) | g) & 15;
+    if (g == win_g) {
+#pragma unroll
+      for (int t = 0; t < kPq; ++t) {
+        const int pos = q + 4 * t;
+        if (pos >= R) continue;
+        const int o = (int)(w[t] & 0xFFFF);
+        if (o == 0xFFFF) st[g][pos][(rr[t] * rs) & 15] = (uint32_t)rr[t] | (1u << 16);
+        else if (o != rr[t]) st[g][pos][(rr[t] * rs) & 15] = w[t] + (1u << 16);
+      }
+      if (q == 0) {
+        // the fill-th lane of ds_read_b128 group g % 4 in wave step g / 4
+        const int gg = g & 3, k = fill;
+        const int l16 = gg == 0 ? (k < 4 ? k : k < 8 ? 8 + k : 12 + k)
+                      : gg == 1 ? (k < 8 ? 4 + k : k < 12 ? 8 + k : 16 + k)
+                      : gg == 2 ? 32 + (k < 4 ? k : k < 8 ? 8 + k : 12 + k)
+                                : 32 + (k < 8 ? 4 + k : k < 12 ? 8 + k : 16 + k);
+        dst[i] = (int16_t)(64 * (g >> 2) + l16);
+      }
+      ++fill;
+    }
+    wave_lds_sync();
+  }
+  for (int i = lane; i < NW; i += 64) {
+    const int64_t d = base + dst[i];
+    rec[3 * d] = win[3 * i]; rec[3 * d + 1] = win[3 * i + 1]; rec[3 * d + 2] = win[3 * i + 2];
+  }
+}
+
 // keep support >= mc (FastApriori.scala:152-154): per level, the kept candidate rows
 // and counts in candidate order (lexicographic, as the rows were generated), their
 // number into fsz[l].  One workgroup; a bundle holds at most one accumulator pass
@@ -316,7 +440,12 @@ using namespace fa;
 
 FA_API int fa_hip_dl_plan_window(const int64_t* desc, int L, long long* ctl, int F1, int32_t* item_map, void* rec,
                                  int64_t max_pieces, int32_t* part, int64_t part_cap, int32_t* gpre,
-                                 int64_t gpre_cap, int64_t w0, int64_t w1, hipStream_t st);
+                                 int64_t gpre_cap, int64_t w0, int64_t w1, int sw, hipStream_t st);
+
+// Bank-aware lane deal of the plans queued next (k_dl_lane_assign): on / off, set by
+// fastapriori_amd.ops.primitives before the plans are queued (TUNING.lane_deal_min_rows).
+static int g_lane_on = 0;
+FA_API void fa_hip_set_lane_deal(int on) { g_lane_on = on; }
 
 // Single-pass slab plan of a device bundle (desc: gen.hip fa_hip_dl_more's level
 // table, L levels).  item_map: int32 [F1] out (rank -> slab row, -1 unused);
@@ -326,15 +455,16 @@ FA_API int fa_hip_dl_plan_window(const int64_t* desc, int L, long long* ctl, int
 // piece count lands in ctl[220] (int32 copy at ctl + 221, the count kernel's G).
 FA_API int fa_hip_dl_plan(const int64_t* desc, int L, long long* ctl, int F1, int32_t* item_map, void* rec,
                           int64_t max_pieces, int32_t* part, int64_t part_cap, int32_t* gpre, int64_t gpre_cap,
-                          hipStream_t st) {
-  return fa_hip_dl_plan_window(desc, L, ctl, F1, item_map, rec, max_pieces, part, part_cap, gpre, gpre_cap, 0, -1, st);
+                          int sw, hipStream_t st) {
+  return fa_hip_dl_plan_window(desc, L, ctl, F1, item_map, rec, max_pieces, part, part_cap, gpre, gpre_cap, 0, -1, sw,
+                               st);
 }
 
 // The plan of the bundle candidates [w0, w1) only (w1 < 0: all): one pass of a level
 // whose candidates exceed one accumulator pass; records index candidates from w0.
 FA_API int fa_hip_dl_plan_window(const int64_t* desc, int L, long long* ctl, int F1, int32_t* item_map, void* rec,
                                  int64_t max_pieces, int32_t* part, int64_t part_cap, int32_t* gpre,
-                                 int64_t gpre_cap, int64_t w0, int64_t w1, hipStream_t st) {
+                                 int64_t gpre_cap, int64_t w0, int64_t w1, int sw, hipStream_t st) {
   DlLevels D;
   if (dl_levels(desc, L, &D, gpre, gpre_cap)) return 1;
   if (F1 < 1 || F1 > 32768) return 1;
@@ -352,6 +482,12 @@ FA_API int fa_hip_dl_plan_window(const int64_t* desc, int L, long long* ctl, int
   hipLaunchKernelGGL(k_dl_pieces_scan, dim3(1), dim3(1024), 0, st, part, nblk, ctl);
   hipLaunchKernelGGL(k_dl_pieces_emit, dim3((unsigned)nblk), dim3(kDlPB), 0, st, D, part, item_map,
                      static_cast<int4*>(rec));
+  if (g_lane_on && sw > 0) {
+    const int64_t nwin = (D.w1 - D.w0) / (64 * kLaWs);   // pieces <= candidates of the window
+    if (nwin > 0)
+      hipLaunchKernelGGL(k_dl_lane_assign, dim3((unsigned)nwin), dim3(64), 0, st, static_cast<int4*>(rec), ctl,
+                         (sw + 2) / 2);
+  }
   FA_LAUNCH_RET();
 }
 

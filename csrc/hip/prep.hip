@@ -1260,8 +1260,7 @@ __global__ __launch_bounds__(256) void k_txn_freq_count_wv(const int64_t* __rest
 FA_API int fa_hip_txn_freq_count(const int64_t* off, const int32_t* items, int64_t n, int64_t nnz,
                                  const int32_t* lut, int32_t* cnt, hipStream_t st) {
   if (n <= 0) return 0;
-  static const bool wv = !getenv("FA_FREQ_WV") || atoi(getenv("FA_FREQ_WV")) != 0;
-  if (wv && nnz > 8 * n && nnz <= 48 * n) {
+  if (nnz > 8 * n && nnz <= 48 * n) {
     hipLaunchKernelGGL(k_txn_freq_count_wv, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, off, items, n, lut,
                        cnt);
     FA_LAUNCH_RET();
@@ -1375,10 +1374,9 @@ FA_API int fa_hip_build_bitmaps(const int64_t* roff, const int32_t* ranks, const
   if (F1 <= 0 || Wp <= 0) return 0;
   if (Wp % WT) return 1;
   // contiguous rows with every output row in one tile: the wave-cooperative build (count.hip)
-  static const bool wave_ok = !getenv("FA_BITMAP_WAVE") || atoi(getenv("FA_BITMAP_WAVE")) != 0;
   // (T40I10D100M: the full 998-item Gram bitmap 22.8 -> 14.1 ms per build, the used-item
   // subsets of the multi-pass levels ~1.9 ms)
-  if (wave_ok && !src && R >= F1) {
+  if (!src && R >= F1) {
     const int rc = fa_hip_build_bitmaps_wave(roff, ranks, ncols, F1, Wp, WT, bm, item_map, st);
     if (rc != 2) return rc;
   }

@@ -217,7 +217,7 @@ static Cands* apriori_gen_bitset(const int32_t* prev, int64_t n, int m, int nthr
 
 // prev: n rows of m = k-1 ranks, each row ascending, rows lexicographically sorted.
 FA_API Cands* fa_apriori_gen(const int32_t* prev, int64_t n, int m, int nthreads, int64_t* sizes) {
-  if (n > 0 && m >= 2 && std::getenv("FA_APRIORI_GEN_HASH") == nullptr) {
+  if (n > 0 && m >= 2) {
     if (Cands* c = apriori_gen_bitset(prev, n, m, nthreads)) {
       sizes[0] = (int64_t)c->prefix.size();
       sizes[1] = (int64_t)c->ext.size();

@@ -323,7 +323,6 @@ static int parse_buffer(const char* d, int64_t size, int64_t b, int64_t e, int m
   std::vector<int32_t> tmax(nt, -1);
   std::atomic<bool> non_numeric{false};
 
-  const auto t_start = std::chrono::steady_clock::now();
   parallel_for_threads(nt, [&](int t) {
     int64_t lo = (t == 0) ? first : next_line_start(d, size, cuts[t]);
     int64_t hi = cuts[t + 1];
@@ -388,13 +387,8 @@ static int parse_buffer(const char* d, int64_t size, int64_t b, int64_t e, int m
     db->vocab = (int64_t)mx + 1;
   } else {
     // merge thread dictionaries into one shard dictionary, remap ids (parallel)
-    const auto t_tok = std::chrono::steady_clock::now();
     std::vector<std::vector<int32_t>> remap;
     if (!merge_dicts(dicts, nthreads, db, remap)) return 7;
-    if (getenv("FA_PARSE_TIMING"))
-      std::fprintf(stderr, "parse dict: tokenize %.1f ms, merge %.1f ms (%d threads)\n",
-                   std::chrono::duration<double, std::milli>(t_tok - t_start).count(),
-                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_tok).count(), nt);
     parallel_for_threads(std::max(1, std::min(nthreads, nt)), [&](int w) {
       for (int t = w; t < nt; t += std::max(1, std::min(nthreads, nt))) {
         for (auto& v : db->chunks[t].items) v = remap[t][(size_t)v];

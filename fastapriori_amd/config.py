@@ -1,5 +1,10 @@
 """Job configuration: CLI > environment (FA_*) > defaults.
 
+The environment can set the product settings a batch scheduler typically fixes per
+job: FA_MIN_SUPPORT, FA_DEVICE, FA_STRATEGY, FA_PROFILE and FA_METRICS; everything
+else is a command-line flag.  Internal tuning knobs are not here: see tuning.py
+(one FA_TUNE variable for experiments) and docs/ARCHITECTURE.md ("Configuration").
+
 Positional arguments keep the reference's semantics (Main.scala:24-25,
 Utils.scala:21-23,39,48): ``input`` and ``output`` are string PREFIXES —
 ``input + "D.dat"``, ``output + "freqItemset"`` — so directories need a
@@ -52,21 +57,21 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("temp", nargs="?", default="", help="temporary path (per-level checkpoints)")
     p.add_argument("--min-support", type=float, default=_env("FA_MIN_SUPPORT", 0.092))
     p.add_argument("--device", choices=["auto", "cuda", "cpu"], default=_env("FA_DEVICE", "auto"))
-    p.add_argument("--dedup", choices=["auto", "on", "off"], default=_env("FA_DEDUP", "auto"))
+    p.add_argument("--dedup", choices=["auto", "on", "off"], default="auto")
     p.add_argument("--pair-strategy", choices=["auto", "horizontal", "gram"],
-                   default=_env("FA_PAIR_STRATEGY", "auto"))
-    p.add_argument("--with-counts", action="store_true", default=_env("FA_WITH_COUNTS", False))
-    p.add_argument("--resume", action="store_true", default=_env("FA_RESUME", False))
-    p.add_argument("--rules-only", action="store_true", default=_env("FA_RULES_ONLY", False))
+                   default="auto")
+    p.add_argument("--with-counts", action="store_true")
+    p.add_argument("--resume", action="store_true")
+    p.add_argument("--rules-only", action="store_true")
     p.add_argument("--no-checkpoint", dest="checkpoint", action="store_false", default=True)
-    p.add_argument("--overwrite", action="store_true", default=_env("FA_OVERWRITE", False))
+    p.add_argument("--overwrite", action="store_true")
     p.add_argument("--profile", action="store_true", default=_env("FA_PROFILE", False))
     p.add_argument("--metrics", dest="metrics_path", default=os.environ.get("FA_METRICS"))
-    p.add_argument("--max-level", type=int, default=_env("FA_MAX_LEVEL", 0))
+    p.add_argument("--max-level", type=int, default=0)
     p.add_argument("--strategy", choices=["count", "candidate"], default=_env("FA_STRATEGY", "count"),
                    help="count: shard transactions, all-reduce counts; candidate: replicate the DB on every "
                         "rank and split pairs by rows, level candidates by rank")
-    p.add_argument("--world-size", type=int, default=_env("FA_WORLD_SIZE", 0),
+    p.add_argument("--world-size", type=int, default=0,
                    help="number of ranks (one per GPU). Without a torchrun environment the job "
                         "re-launches itself under torch.distributed.run; under torchrun the process "
                         "group must have exactly this many ranks")

@@ -36,6 +36,7 @@ import torch
 from .. import ops
 from ..ops.host import apriori_gen
 from ..parallel.comm import Comm
+from ..tuning import TUNING
 from ..utils.jvm import java_string_key, min_count
 from ..utils.metrics import Logger, Timer, roctx_range
 from .data import MiningResult, TransactionShard
@@ -51,15 +52,6 @@ F1_SKETCH_MIN_VOCAB = 1 << 20
 # numeric vocabularies up to this wide read the whole F1 histogram back at once
 F1_HIST_READBACK = 1 << 16
 F1_MAX_CANDIDATES = ops.primitives.F1_MAX_CANDIDATES
-# level bundling (FastApriori._plan_bundle)
-BUNDLE_LEVELS = os.environ.get("FA_BUNDLE", "1") == "1"
-FUSED_COMPRESS = os.environ.get("FA_FUSED_COMPRESS", "1") == "1"
-# short rows only: 256-row spans must fit the 4096-token LDS stage and most rows the
-# 16-token register sort (T40I10's 40-token rows are faster on the tiered path)
-FUSED_COMPRESS_MEAN_LEN = float(os.environ.get("FA_FUSED_COMPRESS_MEAN_LEN", "12"))
-GEN_DEVICE = os.environ.get("FA_GEN_DEVICE", "1") == "1"
-GEN_CHAIN = os.environ.get("FA_GEN_CHAIN", "1") == "1"
-GEN_DEVICE_MIN_ROWS = int(os.environ.get("FA_GEN_DEVICE_MIN_ROWS", "512"))
 _TRIU_CACHE: dict = {}
 _POW10 = 10 ** np.arange(1, 11, dtype=np.int64)           # numeric token order (_frequent_items)
 _POW10_PAD = 10 ** (10 - np.arange(0, 12).clip(max=10)).astype(np.int64)
@@ -78,26 +70,6 @@ class _Deferred:
         return self.value
 
 
-# k = 2 across ranks: triangles of at least this many pairs are reduce-scattered and
-# thresholded per slice (Comm.reduce_scatter_select) instead of all-reduced.  Below it
-# the triangle is all-reduced and F_2 compacted on the device with no host round trip
-# (_pairs_on_device): for the T10I4 triangle (474K pairs, 1.9 MB) one ring all-reduce
-# over xGMI costs less than the reduce-scatter's three collectives and two host syncs.
-# 4M pairs (F1 ~ 2900, 16 MB) is where the all-reduce's 2(W-1)/W volume starts to dominate.
-PAIR_RS_MIN = int(os.environ.get("FA_PAIR_RS_MIN", str(1 << 22)))
-BUNDLE_GROWTH = float(os.environ.get("FA_BUNDLE_GROWTH", "1.5"))
-# level bundles generated, planned, counted and thresholded on the GPU with no host
-# round trip per bundle beyond the generator's acceptance readbacks (_mine_device)
-DEVICE_LEVELS = os.environ.get("FA_DEVICE_LEVELS", "1") == "1"
-# the bundle's plan, trimming decision and slab count queued by the generator's native
-# call right after its synchronisation (gen.hip DlPost), not after a return to Python
-DL_POST = os.environ.get("FA_DL_POST", "1") == "1"
-# a level whose candidates exceed one accumulator pass stays on the device (counted window
-# by window from the used items' bitmap) instead of handing the rest to the host loop
-DL_MULTI = os.environ.get("FA_DL_MULTI", "1") == "1"
-BUNDLE_MAX_PREFIX = int(os.environ.get("FA_BUNDLE_MAX_PREFIX", "9"))
-
-
 @dataclass
 class MinerConfig:
     min_support: float = 0.092
@@ -105,10 +77,12 @@ class MinerConfig:
     pair_strategy: str = "auto"     # auto | horizontal | gram
     dedup_threshold: float = 0.8    # dedup when distinct/T below this (auto)
     max_level: int = 0              # 0 = unlimited
-    level_kernel: str = os.environ.get("FA_LEVEL_KERNEL", "auto")   # auto (= slab) | slab | bitmap
+    level_kernel: str = "auto"      # auto (= slab) | slab | bitmap
     trim: bool = True               # transaction trimming before every level k >= 3
     f1: str = "auto"                # auto | sketch | histogram  (frequent-item counting)
     trim_min_rows: int = 1 << 20    # no trimming below this many rows (fixed cost > gain)
+    timing: str = "off"             # off | events (hipEvent phase times) | sync (host-synchronised phases)
+    trace: bool = False             # Chrome trace of the phases in stats["trace"] (--profile)
     parallelism: str = "count"      # count: rows sharded, counts all-reduced (default)
                                     # candidate: every rank holds the whole DB; pairs split by rows,
                                     #   level candidates split by rank (FastApriori.scala:98-100,140)
@@ -162,8 +136,8 @@ class FastApriori:
         mc = min_count(self.cfg.min_support, n_global)
         self.stats = {"n_lines": n_global, "min_count": mc}
         # hipEvent phase timing (no synchronisation) whenever metrics are recorded
-        gpu_timing = os.environ.get("FA_GPU_TIMING") == "1" or bool(self.log.metrics_path)
-        tm = Timer(dev, sync=os.environ.get("FA_PHASE_TIMING") == "1", events=gpu_timing)
+        gpu_timing = self.cfg.timing in ("events", "sync") or bool(self.log.metrics_path)
+        tm = Timer(dev, sync=self.cfg.timing == "sync", events=gpu_timing)
         self._timer = tm
         self._level_recs = []     # per-level metric records, emitted by _finish with device times
 
@@ -346,7 +320,7 @@ class FastApriori:
     # k >= 3 on the device (FastApriori.scala:110-121, :132-160)
     # ------------------------------------------------------------------
     def _device_levels_planned(self, resume) -> bool:
-        return (DEVICE_LEVELS and self._dev.type == "cuda" and not self.cand_par
+        return (TUNING.device_levels and self._dev.type == "cuda" and not self.cand_par
                 and 2 <= self._F1 <= ops.primitives.DL_MAX_F1
                 and self.cfg.level_kernel in ("auto", "slab") and self.stats["n_lines"] < (1 << 31)
                 and (self.cfg.max_level == 0 or self.cfg.max_level >= 3))
@@ -391,10 +365,10 @@ class FastApriori:
         lds = Pm.dl_lds_budget(F1)
         # LDS bytes per slab accumulator: packed u16 counters for unit weights (the rows'
         # weighting does not change while mining: trimming keeps the dedup layout) in
-        # window-by-window levels, and in one-pass bundles with FA_DL_ACC16_BUNDLES=1
+        # window-by-window levels; u32 in one-pass bundles (TUNING.dl_acc16)
         unit = db["wword"] is None
-        self._dl_mp_accb = 2.0 if Pm.DL_ACC16 and unit else 4.0
-        accb = self._dl_accb = 2.0 if Pm.DL_ACC16_BUNDLES and unit else 4.0
+        self._dl_mp_accb = 2.0 if TUNING.dl_acc16 and unit else 4.0
+        accb = self._dl_accb = 4.0
         c_bound = int(lds // accb)
         st = torch.cuda.current_stream(self._dev).cuda_stream
         f2 = self._f2_dev
@@ -429,9 +403,10 @@ class FastApriori:
                 max_lv = min(Pm.DL_MAX_M - m0 + 1, Pm.DL_MAX_LEVELS)
                 if self.cfg.max_level:
                     max_lv = min(max_lv, self.cfg.max_level - k + 1)
-                if not BUNDLE_LEVELS or k - 1 > BUNDLE_MAX_PREFIX:
+                if not TUNING.bundle_levels or k - 1 > TUNING.bundle_max_prefix:
                     max_lv = 1
-                post = DL_POST and max_lv > 1
+                post = TUNING.dl_post and max_lv > 1
+                S.rows_hint = int(db["ncols"])
                 if post:
                     self._dl_post_setup(S, db, k, F1, c_bound, n_bound, lds)
                 # the results not staged yet go to the host on a copy stream while this
@@ -439,8 +414,8 @@ class FastApriori:
                 if pend:
                     self._dl_stage(S, pend)
                 with roctx_range("gen"):
-                    c = Pm.dl_bundle_gen(S, P0, n_src, n_const, n_bound, m0, F1, c_bound, lds, BUNDLE_GROWTH, max_lv,
-                                         st, post=post, accb=accb)
+                    c = Pm.dl_bundle_gen(S, P0, n_src, n_const, n_bound, m0, F1, c_bound, lds, TUNING.bundle_growth,
+                                         max_lv, st, post=post, accb=accb)
                 if c[4]:
                     raise RuntimeError(f"device bundle at level {k}: |F_{k - 1}| exceeds its bound {n_bound}")
                 if c[7]:
@@ -509,12 +484,12 @@ class FastApriori:
         not even 4-word slabs of the used items fit the LDS (wide levels: thousands of
         used items), the level is counted by the bitmap kernel instead (_dl_bitmap_count)."""
         Pm = ops.primitives
-        if not DL_MULTI or self.cfg.max_level and k > self.cfg.max_level:
+        if not TUNING.dl_multi or self.cfg.max_level and k > self.cfg.max_level:
             return None
         C0 = int(c[40])
         if int(c[1]) == 0:
             # the bounded generation reported the size only: again, one level, room for C0
-            c = Pm.dl_bundle_gen(S, P0, n_src, n_const, n_bound, m0, F1, C0, lds, BUNDLE_GROWTH, 1, st,
+            c = Pm.dl_bundle_gen(S, P0, n_src, n_const, n_bound, m0, F1, C0, lds, TUNING.bundle_growth, 1, st,
                                  accb=self._dl_accb)
             if c[4] or c[7] or int(c[1]) != 1 or int(c[40]) != C0:
                 raise RuntimeError(f"device level {k}: regeneration of {C0} candidates disagrees ({c[:8]})")
@@ -588,7 +563,7 @@ class FastApriori:
         P.roff, P.ranks = db["roff"].data_ptr(), db["ranks"].data_ptr()
         P.src = db["src"].data_ptr() if db["src"] is not None else None
         P.wword = db["wword"].data_ptr() if db["wword"] is not None else None
-        P.ncols, P.lds_kernel, P.lds_budget = int(db["ncols"]), float(Pm._LDS_BYTES), float(lds)
+        P.ncols, P.lds_kernel, P.lds_budget = int(db["ncols"]), float(TUNING.slab_lds_bytes), float(lds)
         P.accb = self._dl_accb
         c1 = np.ascontiguousarray(db["c1"], dtype=np.int64)
         alive = np.ascontiguousarray(db["alive"], dtype=np.uint8)
@@ -777,7 +752,7 @@ class FastApriori:
                 rec["gpu_ms"] = round(gpu[span] * share, 3)
             self.log.metric(**rec)
         self._level_recs = []
-        if os.environ.get("FA_TRACE") == "1" and tm is not None:
+        if self.cfg.trace and tm is not None:
             self.stats["trace"] = tm.trace(pid=self.comm.rank)
 
     def _finish(self, result: MiningResult, t_start: float) -> MiningResult:
@@ -988,8 +963,8 @@ class FastApriori:
     def _compress(self, shard: TransactionShard, lut: torch.Tensor, F1: int) -> dict:
         dev = shard.items.device
         n_rows = shard.offsets.numel() - 1
-        if (dev.type == "cuda" and n_rows > 0 and FUSED_COMPRESS
-                and shard.items.numel() <= FUSED_COMPRESS_MEAN_LEN * n_rows):
+        if (dev.type == "cuda" and n_rows > 0 and TUNING.fused_compress
+                and shard.items.numel() <= TUNING.fused_compress_mean_len * n_rows):
             # fused two-pass path: kept rows, offsets, sorted ranks and the length histogram
             # the dedup estimate's probe rides along with the compression sizes (one readback)
             self._dedup_probe = {} if self.cfg.dedup == "auto" else None
@@ -1285,8 +1260,7 @@ class FastApriori:
         else:
             nb = (F1 + 255) // 256
             self.stats["pair_hbm_bytes_est"] = int(2 * (4 * nnz + 8 * T) + nnz * (nb + 1) + T * nb * (nb + 1))
-        # read at call time: spawned test ranks set FA_PAIR_RS_MIN after importing this module
-        rs = self.comm.distributed and flat.numel() >= int(os.environ.get("FA_PAIR_RS_MIN", PAIR_RS_MIN))
+        rs = self.comm.distributed and flat.numel() >= TUNING.pair_rs_min
         if self._f2_defer and not rs and iu.is_cuda:
             return self._pairs_on_device(flat, iu, mc, db)
         if rs:
@@ -1299,7 +1273,7 @@ class FastApriori:
             vals = flat[keep]
         # one readback: rows (a, b) and counts
         keep = keep.to(iu.device)
-        if iu.is_cuda and DEVICE_LEVELS:
+        if iu.is_cuda and TUNING.device_levels:
             # F_2 rows stay on the device as the first device bundle's input
             self._f2_dev = torch.stack([iu[0][keep], iu[1][keep]], 1).to(torch.int32).contiguous()
         h = torch.stack([iu[0][keep], iu[1][keep], vals.to(device=iu.device, dtype=torch.int64)]).cpu().numpy()
@@ -1341,7 +1315,7 @@ class FastApriori:
         candidate rows [C, m+1] when want_rows]."""
         dev = self._dev
         n = prev.shape[0]
-        if (dev.type == "cuda" and GEN_DEVICE and n >= GEN_DEVICE_MIN_ROWS and prev.shape[1] >= 2
+        if (dev.type == "cuda" and TUNING.gen_device and n >= TUNING.gen_device_min_rows and prev.shape[1] >= 2
                 and self._F1 <= ops.primitives.AG_DEVICE_MAX_F1):
             return ops.apriori_gen_device(prev, self._F1, dev, want_rows)
         if dev.type == "cuda" and self._F1 > ops.primitives.AG_DEVICE_MAX_F1:
@@ -1360,14 +1334,14 @@ class FastApriori:
         (fa_hip_ag_chain, first_free): the candidate count of each level is the only
         readback.  None when the device chain does not apply (then _gen + _plan_bundle)."""
         dev = self._dev
-        if not (dev.type == "cuda" and GEN_DEVICE and GEN_CHAIN and BUNDLE_LEVELS
-                and self.cfg.level_kernel in ("auto", "slab") and k - 1 <= BUNDLE_MAX_PREFIX
-                and prev.shape[0] >= GEN_DEVICE_MIN_ROWS and prev.shape[1] >= 2
+        if not (dev.type == "cuda" and TUNING.gen_device and TUNING.gen_chain and TUNING.bundle_levels
+                and self.cfg.level_kernel in ("auto", "slab") and k - 1 <= TUNING.bundle_max_prefix
+                and prev.shape[0] >= TUNING.gen_device_min_rows and prev.shape[1] >= 2
                 and self._F1 <= ops.primitives.AG_DEVICE_MAX_F1):
             return None
         max_lv = (self.cfg.max_level - k + 1) if self.cfg.max_level else 64
         with roctx_range("gen_bundle"), self._timer.phase("apriori_gen"):
-            return ops.primitives.apriori_gen_chain(prev, self._F1, dev, max_lv, BUNDLE_GROWTH, 0, 0,
+            return ops.primitives.apriori_gen_chain(prev, self._F1, dev, max_lv, TUNING.bundle_growth, 0, 0,
                                                     first_free=True)
 
     def _bundle_from_chain(self, k: int, prev: np.ndarray, chain: list) -> list:
@@ -1388,7 +1362,7 @@ class FastApriori:
         frequent, hence candidate, k-subsets).  On T10I4 data these supersets are
         within 2-20 % of the real candidate sets, and one slab build + one launch
         replaces several.  Levels are added while the total fits one LDS
-        accumulator pass, a level does not grow past BUNDLE_GROWTH x the previous
+        accumulator pass, a level does not grow past TUNING.bundle_growth x the previous
         one, and prefixes stay short (deep levels prefer the trie kernel).
         Returns [(k, prefix rows source, prefix_idx, ext_off, ext), ...]."""
         bundle = [(k, prev, prefix_idx, ext_off, ext)]
@@ -1397,8 +1371,8 @@ class FastApriori:
             cand_rows = np.concatenate([prev[prefix_idx[g_of_e]], ext[:, None]], axis=1)
         # candidate rows of every bundled level (result assembly: rows[count >= minCount])
         self._bundle_rows = [np.ascontiguousarray(cand_rows, np.int32)]
-        if (not BUNDLE_LEVELS or self.cfg.level_kernel not in ("auto", "slab")
-                or k - 1 > BUNDLE_MAX_PREFIX):
+        if (not TUNING.bundle_levels or self.cfg.level_kernel not in ("auto", "slab")
+                or k - 1 > TUNING.bundle_max_prefix):
             return bundle
         C = int(ext.size)
         items = np.zeros(db["F1"], dtype=bool)
@@ -1411,13 +1385,13 @@ class FastApriori:
         last = C
         kk = k
         dev = self._dev
-        if (dev.type == "cuda" and GEN_DEVICE and GEN_CHAIN and cand.shape[1] >= 2
+        if (dev.type == "cuda" and TUNING.gen_device and TUNING.gen_chain and cand.shape[1] >= 2
                 and self._F1 <= ops.primitives.AG_DEVICE_MAX_F1):
             # all speculative levels in one native call (one 8-byte readback per level)
             max_lv = (self.cfg.max_level - k) if self.cfg.max_level else 64
             tmax = ops.primitives.slab_total_limit(n_used)
-            for pi, eo, ex, nxt in ops.primitives.apriori_gen_chain(cand, self._F1, dev, max_lv, BUNDLE_GROWTH,
-                                                                    total, tmax):
+            for pi, eo, ex, nxt in ops.primitives.apriori_gen_chain(cand, self._F1, dev, max_lv,
+                                                                    TUNING.bundle_growth, total, tmax):
                 kk += 1
                 bundle.append((kk, cand, pi, eo, ex))
                 self._bundle_rows.append(nxt)
@@ -1426,7 +1400,7 @@ class FastApriori:
         while self.cfg.max_level == 0 or kk + 1 <= self.cfg.max_level:
             pi, eo, ex, nxt = self._gen(cand, want_rows=True)
             C2 = int(ex.size)
-            if C2 == 0 or C2 > BUNDLE_GROWTH * last:
+            if C2 == 0 or C2 > TUNING.bundle_growth * last:
                 break
             # later levels only use items of level k's candidates: n_used is fixed
             if total + C2 > ops.primitives.slab_capacity(n_used, total + C2):

@@ -90,9 +90,11 @@ _HIP_SIGS = {
     "fa_hip_dl_level0": (C.c_int, [vp, vp, i64, i64, C.c_int, C.c_int, vp, i64, vp, vp, i64, dbl, dbl, vp, C.c_int,
                                    vp]),
     "fa_hip_dl_more": (C.c_int, [C.c_int, vp, i64, i64, vp, vp, dbl, C.c_int, dbl, dbl, i64, vp, vp, vp, vp]),
-    "fa_hip_dl_plan": (C.c_int, [vp, C.c_int, vp, C.c_int, vp, vp, i64, vp, i64, vp, i64, vp]),
+    "fa_hip_dl_plan": (C.c_int, [vp, C.c_int, vp, C.c_int, vp, vp, i64, vp, i64, vp, i64, C.c_int, vp]),
+    "fa_hip_set_lane_deal": (None, [C.c_int]),
     "fa_hip_dl_gpre_need": (i64, [vp, C.c_int]),
-    "fa_hip_dl_plan_window": (C.c_int, [vp, C.c_int, vp, C.c_int, vp, vp, i64, vp, i64, vp, i64, i64, i64, vp]),
+    "fa_hip_dl_plan_window": (C.c_int, [vp, C.c_int, vp, C.c_int, vp, vp, i64, vp, i64, vp, i64, i64, i64, C.c_int,
+                                        vp]),
     "fa_hip_dl_threshold": (C.c_int, [vp, C.c_int, vp, i64, vp, vp, vp, vp, vp, vp]),
     "fa_hip_trim_scan_count": (C.c_int, [vp, vp, i64, vp, C.c_int, C.c_int, vp, vp, vp, vp, vp]),
     "fa_hip_trim_emit": (C.c_int, [vp, vp, vp, C.c_int, i64, vp, vp, vp, vp, vp, vp, vp, vp]),
@@ -105,7 +107,7 @@ _HIP_SIGS = {
     "fa_hip_block_scatter": (C.c_int, [vp, vp, i64, i32, vp, vp, vp, C.c_int, vp]),
     "fa_hip_pair_queue16": (C.c_int, [vp, vp, vp, i64, C.c_int, i64, vp, vp, C.c_int, vp]),
     "fa_hip_pair_blocked": (C.c_int, [vp, vp, vp, i64, vp, i32, vp, i64, vp]),
-    "fa_hip_pair_gram_mfma": (C.c_int, [vp, i32, i64, i64, vp, C.c_int, C.c_uint32, vp]),
+    "fa_hip_pair_gram_mfma": (C.c_int, [vp, i32, i64, i64, vp, C.c_int, C.c_uint32, C.c_int, vp]),
     "fa_hip_pair_gram_popc": (C.c_int, [vp, i32, i64, i64, vp, vp, C.c_int, vp]),
     "fa_hip_count_candidates": (C.c_int, [vp, i64, i64, vp, C.c_int, vp, vp, vp, C.c_int, vp, vp, vp]),
     "fa_hip_recommend": (C.c_int, [vp, vp, vp, i64, i32, vp, vp, i64, vp, vp]),

@@ -21,6 +21,7 @@ from dataclasses import dataclass
 import numpy as np
 import torch
 
+from ..tuning import TUNING
 from ..utils.env import num_threads
 from . import _native
 
@@ -177,9 +178,8 @@ def txn_freq_count(offsets: torch.Tensor, items: torch.Tensor, lut: torch.Tensor
 
 
 COMPRESS_WAVE_MAX_F1 = 65536
-COMPRESS_WAVE_MEAN_LEN = float(os.environ.get("FA_COMPRESS_WAVE_MEAN_LEN", "48"))
 # mean row length above which the 64-token staged tier (64 KB input span per workgroup) runs first
-COMPRESS_STAGED64_MEAN_LEN = float(os.environ.get("FA_COMPRESS_STAGED64_MEAN_LEN", "16"))   # mean row length above which every row goes to the wave kernel
+COMPRESS_STAGED64_MEAN_LEN = 16.0
 
 
 def compress(offsets, items, lut, kept, roff, F1: int | None = None) -> torch.Tensor:
@@ -201,7 +201,7 @@ def compress(offsets, items, lut, kept, roff, F1: int | None = None) -> torch.Te
         return ranks[:nnz]
     st = _stream(items)
     wave_ok = F1 is not None and F1 <= COMPRESS_WAVE_MAX_F1
-    if wave_ok and items.numel() > COMPRESS_WAVE_MEAN_LEN * max(offsets.numel() - 1, 1):
+    if wave_ok and items.numel() > TUNING.compress_wave_mean_len * max(offsets.numel() - 1, 1):
         _hip_call("fa_hip_compress_wave", _p(offsets), _p(items), _p(lut), None, T, _p(kept), _p(roff),
                   _p(ranks), F1, None, st)
         return ranks[:nnz]
@@ -237,7 +237,6 @@ def compress(offsets, items, lut, kept, roff, F1: int | None = None) -> torch.Te
 PAIR_PAD_BATCHES = 3 * 16 + 2   # the pair kernel's pipeline reads up to this many batches past a chunk
 # the emit pass of compress_rows also writes the pair kernel's blocked layout (FA_FUSED_LAYOUT=0: the
 # separate block-scatter pass of pair_counts_horizontal)
-FUSED_LAYOUT = os.environ.get("FA_FUSED_LAYOUT", "1") == "1"
 
 
 @dataclass
@@ -281,7 +280,7 @@ def compress_rows(offsets, items, lut, F1: int, block_counts: bool = True, probe
     st = _stream(items)
     nb = (F1 + 255) // 256
     blk = block_counts and 1 <= nb <= 8 and n > 0
-    fused = blk and FUSED_LAYOUT
+    fused = blk and TUNING.fused_layout
     agg = torch.empty(3 * max(nwg, 1), dtype=_I32, device=dev)
     aggb = torch.empty(nb * nwg, dtype=_I32, device=dev) if fused else None
     hist = torch.zeros(64, 256, dtype=_I32, device=dev)
@@ -494,16 +493,15 @@ def pair_counts_horizontal(roff, ranks, wrow, F1: int, long_rows: bool = True, b
                 lr = torch.empty(total + 1024, dtype=torch.uint8, device=dev)   # pad: aligned dword staging reads
                 _hip_call("fa_hip_block_scatter", _p(roff), _p(ranks), T, F1, _p(cnt), _p(base), _p(lr), pb, st)
             if pb == 256:
-                if os.environ.get("FA_PAIR_DEBUG") != "4":   # 4: layout kernels only (benchmarks/pair_probe.py)
-                    # work-queue schedule: persistent workgroups keep their tile across
-                    # sub-chunks; even row stride -> two counters per 64-bit flush atomic
-                    ld = F1 + (F1 & 1)
-                    out = torch.zeros((F1, ld), dtype=_I32, device=dev)
-                    nbp = nb * (nb + 1) // 2
-                    qctr = torch.zeros(nbp, dtype=_I32, device=dev)
-                    _hip_call("fa_hip_pair_queue16", _p(cnt), _p(base), _p(lr), T, F1, ld, _p(qctr), _p(out),
-                              int(os.environ.get("FA_PAIR_WG", "0")), st)
-                    out = out[:, :F1]
+                # work-queue schedule: persistent workgroups keep their tile across
+                # sub-chunks; even row stride -> two counters per 64-bit flush atomic
+                ld = F1 + (F1 & 1)
+                out = torch.zeros((F1, ld), dtype=_I32, device=dev)
+                nbp = nb * (nb + 1) // 2
+                qctr = torch.zeros(nbp, dtype=_I32, device=dev)
+                _hip_call("fa_hip_pair_queue16", _p(cnt), _p(base), _p(lr), T, F1, ld, _p(qctr), _p(out),
+                          TUNING.pair_wg, st)
+                out = out[:, :F1]
             else:
                 _hip_call("fa_hip_pair_blocked", _p(cnt), _p(base), _p(lr), T, _p(wrow), F1, _p(out),
                           PAIR_CHUNK_ROWS, st)
@@ -514,9 +512,8 @@ def pair_counts_horizontal(roff, ranks, wrow, F1: int, long_rows: bool = True, b
     return out
 
 
-# weight classes shorter than this many words go to the popcount Gram (a matrix-core
-# launch per short class would cost more than its work)
-GRAM_MFMA_MIN_CLASS_WORDS = int(os.environ.get("FA_GRAM_MFMA_MIN_WORDS", "512"))
+# weight classes shorter than TUNING.gram_mfma_min_class_words words go to the popcount
+# Gram (a matrix-core launch per short class would cost more than its work)
 
 
 def gram_segments(W: int, weighted: bool, wcls=None, force_popc: bool = False) -> list[tuple[int, int, int]]:
@@ -534,7 +531,7 @@ def gram_segments(W: int, weighted: bool, wcls=None, force_popc: bool = False) -
     for wt, nw in zip(*wcls):
         w1 = min(w0 + int(nw), W)
         if w1 > w0:
-            if w1 - w0 >= GRAM_MFMA_MIN_CLASS_WORDS and not force_popc:
+            if w1 - w0 >= TUNING.gram_mfma_min_class_words and not force_popc:
                 if run0 is not None:
                     segs.append((run0, w0, 0))
                     run0 = None
@@ -547,11 +544,13 @@ def gram_segments(W: int, weighted: bool, wcls=None, force_popc: bool = False) -
     return segs
 
 
-def pair_counts_gram(bm: torch.Tensor, W: int, wword, wcls=None, force_popc: bool = False) -> torch.Tensor:
+def pair_counts_gram(bm: torch.Tensor, W: int, wword, wcls=None, force_popc: bool = False,
+                     fp4: bool = True) -> torch.Tensor:
     """Pair supports from the item-major bitmaps over words [0, W) -> int64 [F1, F1]
     (upper triangle).  Device: the FP4 matrix-core Gram (k_pair_gram_mfma4) per
     weight class, scaled by the class weight (FastApriori.scala:233-235's weighted
-    sum), short classes by the popcount Gram with per-word weights."""
+    sum), short classes by the popcount Gram with per-word weights.  fp4=False: the
+    i8 matrix-core form (kept as a test oracle of the FP4 one)."""
     F1, Wp = bm.shape[0], bm.stride(0)
     if bm.is_cuda:
         out = torch.zeros((F1, F1), dtype=_I32, device=bm.device)
@@ -560,7 +559,8 @@ def pair_counts_gram(bm: torch.Tensor, W: int, wword, wcls=None, force_popc: boo
             segs = gram_segments(W, wword is not None, wcls, force_popc)
             for a, b, wt in segs:
                 if wt > 0:
-                    _hip_call("fa_hip_pair_gram_mfma", bm.data_ptr() + 8 * a, F1, Wp, b - a, _p(out), 4096, wt, st)
+                    _hip_call("fa_hip_pair_gram_mfma", bm.data_ptr() + 8 * a, F1, Wp, b - a, _p(out), 4096, wt,
+                              int(fp4), st)
                 else:
                     _hip_call("fa_hip_pair_gram_popc", bm.data_ptr() + 8 * a, F1, Wp, b - a,
                               wword.data_ptr() + 4 * a if wword is not None else None, _p(out), 4096, st)
@@ -694,25 +694,20 @@ def trim_rows(roff, ranks, alive: torch.Tensor, min_len: int, wrow=None):
     return kept, nroff, nranks[:nnz], nw, hist
 
 
-_LDS_BYTES = 160 * 1024 - 512   # minus the slab kernel's static scratch (build_words)
-
-
 def slab_capacity(n_used: int, C: int) -> int:
     """Accumulator capacity (candidates per pass) of the slab kernel for n_used items
     (csrc/host/plan.cpp slab_width); 0 when no width fits."""
     for sw in (16, 32, 8, 4):     # plan.cpp slab_width order
-        cap = int((_LDS_BYTES - n_used * (sw + 2) * 8) // 4)
+        cap = int((TUNING.slab_lds_bytes - n_used * (sw + 2) * 8) // 4)
         if cap >= min(C, 8192) or (sw == 4 and cap >= 1024):
             return cap
     return 0
 
 
-# class layout of slab passes (plan.cpp cls_layout, k_count_slab_rec<.., kCls>): sibling
-# prefixes share their first m-1 rows in registers; 0 disables it
-SLAB_CLS = int(os.environ.get("FA_SLAB_CLS", "1"))
-# count_level: expected rows per slab of the rarest frequent prefix above which the slab
-# kernel skips its all-zero-prefix test (0 disables)
-DENSE_MIN_ROWS = float(os.environ.get("FA_DENSE_MIN_ROWS", "4"))
+# TUNING.slab_cls: class layout of slab passes (plan.cpp cls_layout, k_count_slab_rec<..,
+# kCls>): sibling prefixes share their first m-1 rows in registers; 0 disables it.
+# TUNING.dense_min_rows (count_level): expected rows per slab of the rarest frequent prefix
+# above which the slab kernel skips its all-zero-prefix test (0 disables).
 
 
 def _level_plan_bound(F1: int, C: int, G: int, m: int) -> int:
@@ -728,7 +723,7 @@ def level_plan_host(prefix: np.ndarray, ext_off: np.ndarray, ext: np.ndarray, F1
     C = int(ext.size)
     eo = np.ascontiguousarray(ext_off, dtype=np.int64)
     ex = np.ascontiguousarray(ext, dtype=np.int32)
-    params = _plan_params(lds_bytes or _LDS_BYTES, W, SLAB_CLS if cls is None else cls)
+    params = _plan_params(lds_bytes or TUNING.slab_lds_bytes, W, TUNING.slab_cls if cls is None else cls)
     bound = _level_plan_bound(F1, C, G, m)
     passes = np.zeros((G + C + 2, 3), np.int64)
     info = np.zeros(24, np.int64)
@@ -837,7 +832,7 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
     change); without it a used-item bitmap is built for each multi-pass level.
     sup_frac: the minimum support as a fraction of the rows; when every frequent prefix
     then expects >= 4 rows per slab (e^-4: ~2 % of a slab's prefixes empty at worst), the
-    slab kernel drops its all-zero-prefix test (DENSE_MIN_ROWS).
+    slab kernel drops its all-zero-prefix test (TUNING.dense_min_rows).
     Returns int64 counts [C] (ext order), or None when no LDS slab fits (the
     caller then uses the bitmap kernel)."""
     dev = ranks.device
@@ -849,7 +844,7 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
     ex = np.ascontiguousarray(ext, dtype=np.int32)
     W = (ncols + 63) // 64
     # the class layout has no weighted (dedup) kernel: unit weights only
-    params = _plan_params(_LDS_BYTES, W, SLAB_CLS if wword is None else 0)
+    params = _plan_params(TUNING.slab_lds_bytes, W, TUNING.slab_cls if wword is None else 0)
     bound = _level_plan_bound(F1, C, G, m)
     on_gpu = dev.type == "cuda"
     stage = pinned_stage("level_plan") if on_gpu else None
@@ -893,12 +888,12 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
     st = _stream(ranks)
     bounds = passes[:, 2].tolist() + [C]
     nslabs = (W + sw - 1) // sw
-    dense = wword is None and DENSE_MIN_ROWS > 0 and sup_frac * sw * 64 >= DENSE_MIN_ROWS
+    dense = wword is None and TUNING.dense_min_rows > 0 and sup_frac * sw * 64 >= TUNING.dense_min_rows
     for q, (a, b, e0) in enumerate(passes.tolist()):
         Cq = bounds[q + 1] - e0
         # piece records (k_count_slab_rec): 48 B per piece, loaded one piece ahead
         lds = n_used * (sw + 2) * 8 + Cq * 4 + _slab_map_lds(F1)
-        n_wg = int(max(1, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds), 2))))
+        n_wg = int(max(1, min(nslabs, 256 * min(max(1, TUNING.slab_lds_bytes // lds), 2))))
         _hip_call("fa_hip_count_slab_rec_cls", _p(roff), _p(ranks), _p(src), ncols, base + 4 * o_im, F1,
                   n_used, base + 4 * o_gpre, base + 4 * (o_rec + 12 * a), b - a, Cq, _p(wword),
                   out.data_ptr() + 4 * e0, sw, n_wg, _p(bm), bm.stride(0) if bm is not None else 0, st,
@@ -1006,7 +1001,7 @@ def apriori_gen_chain(rows: np.ndarray, F1: int, dev, max_levels: int, growth: f
         host = host_stage.get(4 * need_host).view(dtype=_I32)
         rc = _native.hip().fa_hip_ag_chain(_p(P), n, m, F1, _p(ws), ws.numel(), host.data_ptr(), host.numel(),
                                            max_levels, growth, total0, tmax, sizes.ctypes.data, st,
-                                           int(first_free), float(_LDS_BYTES))
+                                           int(first_free), float(TUNING.slab_lds_bytes))
         if rc == 5:
             _GEN_WS[dev] = torch.empty(int(sizes[1]), dtype=torch.uint8, device=dev)
             continue
@@ -1430,6 +1425,7 @@ class DeviceLevelState:
         self.post = DlPostC()
         self.post_bufs = None
         self.post_keep = ()
+        self.rows_hint = 0          # rows (columns) the next bundle's count runs over (lane_deal)
 
     def grow(self, nbytes: int) -> None:
         self.ws = torch.empty(int(nbytes * 1.25) + (1 << 20), dtype=torch.uint8, device=self.dev)
@@ -1467,16 +1463,14 @@ def device_level_state(dev) -> DeviceLevelState:
 def dl_lds_budget(F1: int) -> int:
     """LDS bytes left to slab + accumulators in k_count_slab_rec (the rank map's copy
     subtracted, as plan.cpp slab_width does)."""
-    return _LDS_BYTES - _slab_map_lds(F1)
+    return TUNING.slab_lds_bytes - _slab_map_lds(F1)
 
 
-# window-by-window device levels count into two u16 counters per accumulator word when the
-# rows have unit weights: twice the candidates per pass, half the passes.  One-pass bundles
-# can too (FA_DL_ACC16_BUNDLES=1), off by default: the larger capacity makes the generator
-# pick 16-word slabs for level 3 alone and cut the later bundles differently, T10I4D100M
-# 43.2 vs 42.3 ms (docs/PERF_HISTORY.md)
-DL_ACC16 = os.environ.get("FA_DL_ACC16", "1") == "1"
-DL_ACC16_BUNDLES = os.environ.get("FA_DL_ACC16_BUNDLES", "0") == "1"
+# TUNING.dl_acc16: window-by-window device levels count into two u16 counters per
+# accumulator word when the rows have unit weights: twice the candidates per pass, half
+# the passes.  One-pass bundles keep u32 accumulators: with u16 ones the larger capacity
+# made the generator pick 16-word slabs for level 3 alone and cut the later bundles
+# differently, T10I4D100M 43.2 vs 42.3 ms (docs/PERF_HISTORY.md; that arm was removed)
 
 
 def dl_slab_width(n_used: int, C: int, lds: int, accb: int = 4) -> tuple[int, int]:
@@ -1513,6 +1507,7 @@ def dl_bundle_gen(S: DeviceLevelState, P0: int, n_src: int | None, n_const: int,
             S.desc[0, 5:8] = [c[8], c[40], 0]
             return c.copy()
         S.post.done = 0
+        lane_deal(lib, S.rows_hint)    # (the post step's plan)
         rc = lib.fa_hip_dl_more(F1, _p(S.ws), S.ws.numel(), int(S.info[0]), _p(S.ctl), _p(S.ctl_h), float(growth),
                                 int(max_levels), float(lds), float(accb), int(c_bound), S.desc.ctypes.data,
                                 info.ctypes.data,
@@ -1523,6 +1518,13 @@ def dl_bundle_gen(S: DeviceLevelState, P0: int, n_src: int | None, n_const: int,
         _native.check(rc, "fa_hip_dl_more")
         return S.ctl_h.numpy().copy()
     raise RuntimeError("device bundle generation: workspace sizing did not converge")
+
+
+def lane_deal(lib, rows: int) -> None:
+    """Bank-aware lane deal of the next device plans (levels.hip k_dl_lane_assign) for a
+    count over this many rows: on from TUNING.lane_deal_min_rows (its fixed cost is
+    repaid by the slabs it speeds up)."""
+    lib.fa_hip_set_lane_deal(int(0 <= TUNING.lane_deal_min_rows <= rows))
 
 
 def dl_plan(S: DeviceLevelState, L: int, F1: int, n_used: int, C: int, lds: int, dev, accb: float = 4.0) -> dict:
@@ -1541,8 +1543,9 @@ def dl_plan(S: DeviceLevelState, L: int, F1: int, n_used: int, C: int, lds: int,
     lib = _native.hip()
     gn = int(lib.fa_hip_dl_gpre_need(S.desc.ctypes.data, L))
     gpre = torch.empty(max(gn, 1), dtype=_I32, device=dev)
+    lane_deal(lib, S.rows_hint)
     _native.check(lib.fa_hip_dl_plan(S.desc.ctypes.data, L, _p(S.ctl), F1, _p(item_map), _p(rec), C,
-                                     _p(part), part.numel(), _p(gpre), gpre.numel(), st), "fa_hip_dl_plan")
+                                     _p(part), part.numel(), _p(gpre), gpre.numel(), sw, st), "fa_hip_dl_plan")
     out = torch.zeros(C, dtype=_I32, device=dev)
     return dict(sw=sw, cap=cap, item_map=item_map, rec=rec, out=out, n_used=n_used, C=C, gpre=gpre, accb=accb)
 
@@ -1556,12 +1559,12 @@ def dl_count_multipass(S: DeviceLevelState, F1: int, n_used: int, C: int, lds: i
     when bitmap row u is slab row u).  sup_frac: minimum support / rows (count_level's
     dense test).  Returns int32 [C] (not reduced across ranks), or None when no slab
     width fits the used items."""
-    acc16 = DL_ACC16 and wword is None
+    acc16 = TUNING.dl_acc16 and wword is None
     accb = 2 if acc16 else 4
     sw, cap = dl_slab_width(n_used, min(C, 8192), lds, accb)
     if sw == 0:
         return None
-    dense = wword is None and DENSE_MIN_ROWS > 0 and sup_frac * sw * 64 >= DENSE_MIN_ROWS
+    dense = wword is None and TUNING.dense_min_rows > 0 and sup_frac * sw * 64 >= TUNING.dense_min_rows
     cap = min(cap, C)
     cap = -(-C // -(-C // cap))                      # equal windows
     st = _stream(ranks)
@@ -1576,14 +1579,15 @@ def dl_count_multipass(S: DeviceLevelState, F1: int, n_used: int, C: int, lds: i
     W = (ncols + 63) // 64
     nslabs = (W + sw - 1) // sw
     npass = 0
+    lane_deal(lib, ncols)
     for w0 in range(0, C, cap):
         w1 = min(C, w0 + cap)
         _native.check(lib.fa_hip_dl_plan_window(S.desc.ctypes.data, 1, _p(S.ctl), F1, _p(item_map), _p(rec), cap,
-                                                _p(part), part.numel(), _p(gpre), gpre.numel(), w0, w1, st),
+                                                _p(part), part.numel(), _p(gpre), gpre.numel(), w0, w1, sw, st),
                       "fa_hip_dl_plan_window")
         nacc = (w1 - w0 + 1) // 2 if acc16 else w1 - w0
         lds_k = n_used * (sw + 2) * 8 + ((nacc + 3) & ~3) * 4
-        n_wg = int(max(1, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds_k), 2))))
+        n_wg = int(max(1, min(nslabs, 256 * min(max(1, TUNING.slab_lds_bytes // lds_k), 2))))
         _hip_call("fa_hip_count_slab_rec_cls", _p(roff), _p(ranks), _p(src), ncols, _p(item_map), F1, n_used,
                   _p(gpre), _p(rec), 0, w1 - w0, _p(wword), out.data_ptr() + 4 * w0, sw, n_wg, _p(bm),
                   bm.stride(0), st, _p(bm_rows), _p(S.ctl) + 8 * 221, (2 if dense else 0) | (4 if acc16 else 0))
@@ -1614,7 +1618,7 @@ def dl_count(S: DeviceLevelState, plan: dict, roff, ranks, src, ncols: int, F1: 
     acc16 = plan.get("accb", 4.0) == 2.0 and wword is None
     nacc = (C + 1) // 2 if acc16 else C
     lds_k = n_used * (sw + 2) * 8 + ((nacc + 3) & ~3) * 4 + _slab_map_lds(F1)
-    n_wg = int(max(1, min(nslabs, 256 * min(max(1, _LDS_BYTES // lds_k), 2))))
+    n_wg = int(max(1, min(nslabs, 256 * min(max(1, TUNING.slab_lds_bytes // lds_k), 2))))
     _hip_call("fa_hip_count_slab_rec_cls", _p(roff), _p(ranks), _p(src), ncols, _p(item_map), F1, n_used,
               _p(plan.get("gpre")), _p(rec), 0, C, _p(wword), _p(out), sw, n_wg, None, 0, st, None,
               _p(S.ctl) + 8 * 221, 4 if acc16 else 0)

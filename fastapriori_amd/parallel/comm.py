@@ -146,7 +146,8 @@ class Comm:
         return got[0], got[1]
 
     def bucket_elems(self, elem_size: int) -> int:
-        mb = float(os.environ.get("FA_BUCKET_MB", "64"))
+        from ..tuning import TUNING
+        mb = float(TUNING.bucket_mb)
         n = int(mb * (1 << 20)) // elem_size
         q = max(1, self.world_size * 7 * 64)
         return max(q, n // q * q)
@@ -287,6 +288,11 @@ def init_comm(device: str | None = None, backend: str | None = None, timeout_s: 
         local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
+        if world > 1:
+            # NUMA-local CPUs of this rank's GPU, before anything pins host memory
+            from .affinity import bind_local_rank
+            bind_local_rank(dev, int(os.environ.get("LOCAL_RANK", str(rank))),
+                            int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
     else:
         dev = torch.device("cpu")
     # FA_FORCE_PG=1 keeps a process group (and every collective) at world size 1, so a

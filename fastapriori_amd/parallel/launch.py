@@ -25,6 +25,10 @@ def _worker(rank: int, world: int, port: int, fn, args, outdir: str, env: dict):
     os.environ.update(env)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK=str(rank),
                       WORLD_SIZE=str(world))
+    if env.get("FA_TUNE"):
+        # the knobs were read when fn's module imported the package, before this update
+        from ..tuning import TUNING
+        TUNING.apply(env["FA_TUNE"])
     try:
         res = fn(*args)
         payload = ("ok", res)

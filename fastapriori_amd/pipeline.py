@@ -66,8 +66,10 @@ def mine_window(cfg: JobConfig, comm, log: Logger, ckpt: Checkpointer | None, su
     t_read = time.time()
     shard = io.read_shard(d_path, comm if cfg.strategy == "count" else Comm(device=comm.device))
     summary["read_ms"] = round((time.time() - t_read) * 1000, 1)
+    # --profile: hipEvent phase times per level and a Chrome trace of the phases
     mcfg = MinerConfig(min_support=cfg.min_support, dedup=cfg.dedup, pair_strategy=cfg.pair_strategy,
-                       max_level=cfg.max_level, parallelism=cfg.strategy)
+                       max_level=cfg.max_level, parallelism=cfg.strategy,
+                       timing="events" if cfg.profile else "off", trace=cfg.profile)
     miner = FastApriori(cfg.min_support, comm, mcfg, log, ckpt)
     result = miner.run(shard, resume=resume)
     summary["miner"] = dict(miner.stats)
@@ -191,11 +193,9 @@ def main(argv=None) -> int:
     cfg = parse_args(argv)
     if cfg.world_size > 1 and "WORLD_SIZE" not in os.environ:
         return _relaunch(cfg, argv)
-    if cfg.profile:
+    if cfg.profile and not cfg.metrics_path:
         # --profile: JSON-lines metrics (per-level device times, bytes reduced, HBM bytes
-        # estimates) and a Chrome trace of the phases, both under the temp path
-        os.environ.setdefault("FA_METRICS", os.path.join(cfg.temp or ".", "fastapriori_metrics.jsonl"))
-        os.environ.setdefault("FA_TRACE", "1")
-        os.environ.setdefault("FA_GPU_TIMING", "1")
+        # estimates) and a Chrome trace of the phases (mine_window), both under the temp path
+        cfg.metrics_path = os.path.join(cfg.temp or ".", "fastapriori_metrics.jsonl")
     run_job(cfg)
     return 0

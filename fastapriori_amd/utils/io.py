@@ -15,6 +15,7 @@ import torch
 
 from ..models.data import MiningResult, TransactionShard, Vocabulary
 from ..ops import _native
+from ..tuning import TUNING
 from .env import num_threads
 
 
@@ -73,14 +74,20 @@ def parse_file(path: str, byte_begin: int = 0, byte_end: int = -1, mode: int = 0
 # ring of pinned slots, overlapped with the H2D copies) and are tokenised by
 # csrc/hip/parse.hip.  Numeric vocabularies only; anything else returns None and
 # the caller uses the host parser.
-GPU_PARSE = os.environ.get("FA_GPU_PARSE", "1") == "1"
-DEVICE_DICT = os.environ.get("FA_GPU_PARSE_DICT", "1") == "1"
+# (TUNING.gpu_parse / gpu_parse_dict switch it off.)
 _RING_SLOT = 32 << 20
-# pinned slots in flight (one reader thread each, up to the host thread count): one
-# thread's pread out of the page cache runs at ~4-6 GB/s, so 8 readers held the
-# 3.9 GB T10I4D100M file at ~35 GB/s, below the ~57 GB/s of the H2D copies
-_RING_SLOTS = int(os.environ.get("FA_RING_SLOTS", "16"))
+# pinned slots in flight (TUNING.ring_slots; one reader thread each, up to the host
+# thread count): one thread's pread out of the page cache runs at ~4-6 GB/s, so 8
+# readers held the 3.9 GB T10I4D100M file at ~35 GB/s, below the ~57 GB/s of the H2D copies
 _ring: list = []
+
+
+def ring_slots() -> int:
+    """Pinned ring slots in use (allocated on first use, grown when the knob grows)."""
+    ns = max(1, int(TUNING.ring_slots))
+    if len(_ring) < ns:
+        _ring.extend(torch.empty(_RING_SLOT, dtype=torch.uint8, pin_memory=True) for _ in range(ns - len(_ring)))
+    return ns
 
 
 def _next_line_start(fd: int, size: int, pos: int) -> int:
@@ -105,7 +112,6 @@ def _next_line_start(fd: int, size: int, pos: int) -> int:
 
 
 _copy_streams: dict = {}
-STREAM_PARSE = os.environ.get("FA_STREAM_PARSE", "1") == "1"
 
 
 def _file_to_device(fd: int, first: int, n: int, dev, parse: bool = False, last_is_term: bool = True):
@@ -133,24 +139,23 @@ def _file_to_device(fd: int, first: int, n: int, dev, parse: bool = False, last_
         tp = prim.TileParse(out, n, dev, scratch_bytes=min(n, 2 * _RING_SLOT))
     if n == 0:
         return (out, tp.finish()) if parse else out
-    if not _ring:
-        _ring.extend(torch.empty(_RING_SLOT, dtype=torch.uint8, pin_memory=True) for _ in range(_RING_SLOTS))
+    NS = ring_slots()
     cs = _copy_streams.get(dev)
     if cs is None:
         cs = _copy_streams[dev] = torch.cuda.Stream(dev)
     compute = torch.cuda.current_stream(dev)
     cs.wait_stream(compute)             # the buffer's allocation and zero fill come first
     nch = (n + _RING_SLOT - 1) // _RING_SLOT
-    events: list = [None] * _RING_SLOTS
+    events: list = [None] * NS
     lib = _native.host()
 
     def read_chunk(c: int):
-        ev = events[c % _RING_SLOTS]
+        ev = events[c % NS]
         if ev is not None:
             ev.synchronize()          # the slot's previous H2D copy has finished
         off = c * _RING_SLOT
         m = min(_RING_SLOT, n - off)
-        slot = _ring[c % _RING_SLOTS]
+        slot = _ring[c % NS]
         mv = memoryview(slot.numpy())
         got = 0
         while got < m:
@@ -164,21 +169,21 @@ def _file_to_device(fd: int, first: int, n: int, dev, parse: bool = False, last_
         lib.fa_chunk_scan(slot.data_ptr(), m, info.ctypes.data)
         return info
 
-    streaming = parse and STREAM_PARSE
+    streaming = parse and TUNING.stream_parse
     rend = 0                            # parsed up to here (a line start)
-    with ThreadPoolExecutor(min(num_threads(), _RING_SLOTS)) as ex:
-        fut = {c: ex.submit(read_chunk, c) for c in range(min(_RING_SLOTS, nch))}
+    with ThreadPoolExecutor(min(num_threads(), NS)) as ex:
+        fut = {c: ex.submit(read_chunk, c) for c in range(min(NS, nch))}
         for c in range(nch):
             info = fut.pop(c).result()
-            s, off = c % _RING_SLOTS, c * _RING_SLOT
+            s, off = c % NS, c * _RING_SLOT
             m = min(_RING_SLOT, n - off)
             with torch.cuda.stream(cs):
                 out[off:off + m].copy_(_ring[s][:m], non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(cs)
             events[s] = ev
-            if c + _RING_SLOTS < nch:
-                fut[c + _RING_SLOTS] = ex.submit(read_chunk, c + _RING_SLOTS)
+            if c + NS < nch:
+                fut[c + NS] = ex.submit(read_chunk, c + NS)
             if streaming and c + 1 < nch:
                 if info[2]:
                     streaming = False   # a '\r': the rest is the final region
@@ -187,7 +192,7 @@ def _file_to_device(fd: int, first: int, n: int, dev, parse: bool = False, last_
                     end = off + int(info[1]) + 1
                     tp.region(rend, end, int(info[0]), tail=False)
                     rend = end
-    compute.wait_event(events[(nch - 1) % _RING_SLOTS])
+    compute.wait_event(events[(nch - 1) % NS])
     if not parse:
         return out
     tp.region(rend, n, None, tail=not last_is_term)
@@ -228,7 +233,7 @@ def parse_file_device(path: str, byte_begin: int, byte_end: int, device, line_ba
         del buf
         off, items, extras, vocab, hist = got
         return TransactionShard(off, items, extras.cpu().numpy(), Vocabulary(True, vocab), line_base, hist)
-    got = prim.parse_dict_device(buf, n, last_is_term) if DEVICE_DICT else None
+    got = prim.parse_dict_device(buf, n, last_is_term) if TUNING.gpu_parse_dict else None
     del buf
     if got is None:
         return None
@@ -252,7 +257,7 @@ def read_shard(path: str, comm, device: torch.device | str | None = None) -> Tra
         raise FileNotFoundError(path)
     b = size * comm.rank // comm.world_size
     e = size * (comm.rank + 1) // comm.world_size
-    shard = parse_file_device(path, b, e, device) if (GPU_PARSE and device.type == "cuda") else None
+    shard = parse_file_device(path, b, e, device) if (TUNING.gpu_parse and device.type == "cuda") else None
     if shard is None:
         # host parser, straight into pinned buffers when the shard goes to a GPU
         shard = parse_file(path, b, e, 0, device)
@@ -260,7 +265,7 @@ def read_shard(path: str, comm, device: torch.device | str | None = None) -> Tra
     if need_dict and shard.vocab.numeric:
         # another rank saw non-numeric tokens: every rank takes dictionary ids
         shard = (parse_file_device(path, b, e, device, force_dict=True)
-                 if (GPU_PARSE and DEVICE_DICT and device.type == "cuda") else None) or parse_file(path, b, e, 1,
+                 if (TUNING.gpu_parse and TUNING.gpu_parse_dict and device.type == "cuda") else None) or parse_file(path, b, e, 1,
                                                                                                   device)
     counts = comm.all_gather_int(shard.n_lines)
     shard.line_base = int(sum(counts[: comm.rank]))

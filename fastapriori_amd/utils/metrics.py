@@ -41,7 +41,7 @@ class Timer:
     """Phase timer.
 
     * host wall-clock per phase (always); with ``sync`` the device is synchronised at
-      the phase edges (FA_PHASE_TIMING=1: exact but perturbing);
+      the phase edges (MinerConfig.timing = "sync": exact but perturbing);
     * with ``events`` (cuda only) a pair of timing hipEvents is recorded around every
       phase on the current stream -- no synchronisation -- and read back by
       ``finish()`` once the run's final readback has drained the stream

@@ -11,7 +11,7 @@
 #   bash scripts/gpu_pass.sh trace [CFG]        kernel + roctx marker trace (benchmarks/gap_attrib.py: GPU idle by host range)
 #   bash scripts/gpu_pass.sh e2e                the reference window's breakdown (benchmarks/e2e_probe.py) + its kernel stats
 #   bash scripts/gpu_pass.sh multirank          8 gloo ranks sharing the GPU: collectives per run (benchmarks/multirank_probe.py)
-#   bash scripts/gpu_pass.sh ab VAR A B [CFG]   alternating bench runs with VAR=A / VAR=B
+#   bash scripts/gpu_pass.sh ab KNOB A B [CFG]  alternating bench runs with FA_TUNE=KNOB=A / KNOB=B (fastapriori_amd/tuning.py)
 #   bash scripts/gpu_pass.sh head             tests + multirank + e2e + kernel stats of T10 and T40 (one HEAD's evidence)
 #   bash scripts/gpu_pass.sh cpu                the C++ CPU comparator of vs_baseline (no GPU work)
 set -e -o pipefail
@@ -88,7 +88,7 @@ case "$MODE" in
     V=$1; A=$2; B=$3; CFG=${4:-T10I4D100M}
     for i in 1 2; do
       for val in "$A" "$B"; do
-        env "$V=$val" timeout -k 10 500 python bench.py --config "$CFG" --steps 10 --warmup 2 --e2e off \
+        env "FA_TUNE=$V=$val" timeout -k 10 500 python bench.py --config "$CFG" --steps 10 --warmup 2 --e2e off \
           > "$O/${CFG}_${V}_${val}_$i.json" 2> /dev/null
       done
     done

@@ -28,3 +28,23 @@ def native():
     from fastapriori_amd.ops import build
     build.build_host()
     return True
+
+
+@pytest.fixture
+def tune():
+    """tune(name=value, ...) sets fastapriori_amd.tuning.TUNING knobs for one test and
+    restores them afterwards (the config object, not module globals)."""
+    from fastapriori_amd.tuning import TUNING
+    saved = {}
+
+    def set_(**kw):
+        for k, v in kw.items():
+            if not hasattr(TUNING, k):
+                raise AttributeError(f"unknown tuning knob {k}")
+            saved.setdefault(k, getattr(TUNING, k))
+            setattr(TUNING, k, v)
+        return TUNING
+
+    yield set_
+    for k, v in saved.items():
+        setattr(TUNING, k, v)

@@ -91,7 +91,7 @@ def test_pair_reduce_scatter_select(quest_db, world):
     # (forced for every triangle size): bit-identical to the all-reduce path
     ref = spawn_local(_mine_file, 1, quest_db, 0.02, "auto", "horizontal", timeout=TIMEOUT)[0]
     outs = spawn_local(_mine_file, world, quest_db, 0.02, "auto", "horizontal", timeout=TIMEOUT,
-                       env={"FA_PAIR_RS_MIN": "0"})
+                       env={"FA_TUNE": "pair_rs_min=0"})
     _check(outs, ref)
 
 

@@ -15,6 +15,7 @@ import pytest
 import torch
 
 import fastapriori_amd.models.apriori as ap
+from fastapriori_amd.tuning import TUNING
 from fastapriori_amd.models.apriori import FastApriori, MinerConfig
 from fastapriori_amd.models.oracle import mining_log_lines
 from fastapriori_amd.parallel.comm import Comm
@@ -47,11 +48,11 @@ def _same(a, b):
     (200_000, 0.003, {"max_level": 5}),
     (50_000, 0.004, {"pair_strategy": "gram"}),
 ])
-def test_device_levels_match_host_loop(monkeypatch, n, ms, kw):
+def test_device_levels_match_host_loop(tune, n, ms, kw):
     cpu = generate_shard(n, Comm(), "cpu", 10.0, 4.0, 2000, 1000, 5)
     g = cpu.to(DEV)
     got, st = _mine(g, ms, **kw)
-    monkeypatch.setattr(ap, "DEVICE_LEVELS", False)
+    tune(device_levels=False)
     ref, st2 = _mine(g, ms, **kw)
     assert "device_bundles" not in st2
     if len(ref.levels) >= 3:
@@ -62,10 +63,10 @@ def test_device_levels_match_host_loop(monkeypatch, n, ms, kw):
         assert got.as_dict() == cref.as_dict()
 
 
-def test_multipass_level_stays_on_device(monkeypatch):
+def test_multipass_level_stays_on_device(tune):
     # T40I10 at a lower support: levels whose candidates need several accumulator passes
     # are counted on the device window by window (FastApriori._dl_multipass);
-    # FA_DL_MULTI=0 hands them to the host loop instead
+    # dl_multi=False hands them to the host loop instead
     cpu = generate_shard(150_000, Comm(), "cpu", 40.0, 10.0, 2000, 1000, 3)
     ref, _ = _mine(cpu, 0.006)
     assert len(ref.levels) >= 6
@@ -74,7 +75,7 @@ def test_multipass_level_stays_on_device(monkeypatch):
     assert st["device_levels"] >= len(ref.levels) - 2 and "fallbacks" not in st
     assert got.as_dict() == ref.as_dict()
     _same(got, ref)
-    monkeypatch.setattr(ap, "DL_MULTI", False)
+    tune(dl_multi=False)
     got2, st2 = _mine(cpu.to(DEV), 0.006)
     assert st2.get("host_levels", 0) >= 1
     _same(got2, ref)
@@ -89,7 +90,7 @@ def _multipass_lds(ref, accb: int = 4) -> int:
     return U * 48 + accb * max(1024, F3 // 4) + 2 * F1 + 256
 
 
-def test_small_lds_forces_device_multipass(monkeypatch):
+def test_small_lds_forces_device_multipass(tune):
     # a shrunk LDS budget turns T10I4 levels into multi-pass ones: windows, trimming and
     # the used items' bitmap on the unit and the weighted (dedup) layout
     import fastapriori_amd.ops.primitives as prim
@@ -97,7 +98,7 @@ def test_small_lds_forces_device_multipass(monkeypatch):
     ref, _ = _mine(cpu, 0.002)
     for dd in ("off", "on"):
         # unit weights count into packed u16 accumulators (2 B each)
-        monkeypatch.setattr(prim, "_LDS_BYTES", _multipass_lds(ref, 2 if dd == "off" and prim.DL_ACC16 else 4))
+        tune(slab_lds_bytes=_multipass_lds(ref, 2 if dd == "off" and TUNING.dl_acc16 else 4))
         got, st = _mine(cpu.to(DEV), 0.002, dedup=dd, trim_min_rows=0)
         assert st.get("device_multipass", 0) >= 1, st
         _same(got, ref)
@@ -134,7 +135,7 @@ def test_device_levels_repeat_runs_identical():
     assert c.as_dict() == cref.as_dict()
 
 
-def test_wide_f1_generates_on_device_without_fallbacks(monkeypatch):
+def test_wide_f1_generates_on_device_without_fallbacks():
     # F1 = 6319 > 4096: the generator's lanes hold two bitset words each
     # (gen.hip ag_row_bits<2>); no level may fall back to the host generator
     cpu = generate_shard(300_000, Comm(), "cpu", 10.0, 4.0, 6000, 12000, 3)
@@ -148,7 +149,7 @@ def test_wide_f1_generates_on_device_without_fallbacks(monkeypatch):
     _same(got, ref)
 
 
-def test_f2_stays_on_device_until_the_flush(monkeypatch):
+def test_f2_stays_on_device_until_the_flush(tune):
     # F_2 compacted on the device (no readback between the pair kernel and the first
     # bundle): same itemsets, and the reference's log lines in level order
     import io
@@ -156,7 +157,7 @@ def test_f2_stays_on_device_until_the_flush(monkeypatch):
     g = cpu.to(DEV)
     logs = {}
     for dl in (True, False):
-        monkeypatch.setattr(ap, "DEVICE_LEVELS", dl)
+        tune(device_levels=dl)
         buf = io.StringIO()
         lg = Logger(0, enabled=True)
         lg.stream = buf
@@ -177,7 +178,7 @@ def test_f2_stays_on_device_until_the_flush(monkeypatch):
     assert logs[True] == want and logs[False] == want
 
 
-def test_u16_window_accumulators_drain_mid_run(monkeypatch):
+def test_u16_window_accumulators_drain_mid_run(tune):
     # packed-u16 window accumulators drain into the u32 counts every
     # 65535 / (SW * 64) slabs.  One workgroup walks every slab (fa_hip_debug_slab_max_wg),
     # and items 0-3 sit in every row, so their level-3 and level-4 counters pass 65535
@@ -192,7 +193,7 @@ def test_u16_window_accumulators_drain_mid_run(monkeypatch):
     cpu = parse_bytes(text.encode(), device=torch.device("cpu"))
     ref, _ = _mine(cpu, 0.002)
     assert max(ref.counts[2]) > 4 * 65535
-    monkeypatch.setattr(prim, "_LDS_BYTES", _multipass_lds(ref, 2))
+    tune(slab_lds_bytes=_multipass_lds(ref, 2))
     hip = _native.hip()
     hip.fa_hip_debug_slab_max_wg(1)
     try:
@@ -201,3 +202,18 @@ def test_u16_window_accumulators_drain_mid_run(monkeypatch):
         hip.fa_hip_debug_slab_max_wg(0)
     assert st.get("device_multipass", 0) >= 1, st
     _same(got, ref)
+
+
+def test_lane_deal_keeps_counts(tune):
+    # the bank-aware lane deal (levels.hip k_dl_lane_assign) moves piece records between
+    # lanes only: every level identical to the undealt plan, one-pass bundles and
+    # window-by-window levels (T40 shape) alike
+    for args, ms in (((10.0, 4.0, 2000, 1000), 0.002), ((40.0, 10.0, 2000, 1000), 0.006)):
+        cpu = generate_shard(150_000, Comm(), "cpu", *args, 3)
+        g = cpu.to(DEV)
+        tune(lane_deal_min_rows=-1)
+        ref, _ = _mine(g, ms)
+        tune(lane_deal_min_rows=0)
+        got, st = _mine(g, ms)
+        assert st.get("device_bundles", 0) >= 1
+        _same(got, ref)

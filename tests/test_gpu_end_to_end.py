@@ -111,7 +111,7 @@ def test_two_ranks_share_gpu_match_one():
     ref = spawn_local(_gpu_rank, 1, 40000, 0.005, env={"FA_DIST_BACKEND": "gloo"})[0]
     outs = spawn_local(_gpu_rank, 2, 40000, 0.005, env={"FA_DIST_BACKEND": "gloo"})
     assert outs[0] == ref and outs[1] == ref
-    outs = spawn_local(_gpu_rank, 2, 40000, 0.005, env={"FA_DIST_BACKEND": "gloo", "FA_PAIR_RS_MIN": "0"})
+    outs = spawn_local(_gpu_rank, 2, 40000, 0.005, env={"FA_DIST_BACKEND": "gloo", "FA_TUNE": "pair_rs_min=0"})
     assert outs[0] == ref and outs[1] == ref
     assert len(ref) > 100
 
@@ -156,8 +156,8 @@ def _rccl_rank(n, ms, strategy):
 @pytest.mark.parametrize("strategy", ["count", "candidate"])
 def test_rccl_code_paths_match_single_process(strategy):
     ref = spawn_local(_rccl_rank, 1, 60000, 0.004, strategy)[0]
-    # FA_PAIR_RS_MIN=0: the k = 2 triangle takes reduce-scatter + threshold + all-gather on RCCL
-    got = spawn_local(_rccl_rank, 1, 60000, 0.004, strategy, env={"FA_FORCE_PG": "1", "FA_PAIR_RS_MIN": "0"})[0]
+    # FA_TUNE=pair_rs_min=0: the k = 2 triangle takes reduce-scatter + threshold + all-gather on RCCL
+    got = spawn_local(_rccl_rank, 1, 60000, 0.004, strategy, env={"FA_FORCE_PG": "1", "FA_TUNE": "pair_rs_min=0"})[0]
     assert got[0] == ref[0] and got[1] == ref[1] and got[2] == ref[2] and got[3] == ref[3]
     assert got[4] == 1.5 and got[5] > 0 and ref[5] == 0
     if strategy == "count":

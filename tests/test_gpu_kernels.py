@@ -257,12 +257,12 @@ def test_gen_chain_matches_iterated_gen():
     assert len(ops.primitives.apriori_gen_chain(cand, F1, DEV, 4, (c0 - 0.5) / cand.shape[0], 0, 1 << 40)) == 0
 
 
-def test_bundling_chain_matches_python_loop(monkeypatch):
+def test_bundling_chain_matches_python_loop(tune):
     import fastapriori_amd.models.apriori as ap
     sh = generate_shard(200000, Comm(), "cpu", 10.0, 4.0, 60, 80, seed=8).to(DEV)
     cfg = MinerConfig(min_support=0.003)
     a = FastApriori(0.003, config=cfg).run(sh)
-    monkeypatch.setattr(ap, "GEN_CHAIN", False)
+    tune(gen_chain=False)
     b = FastApriori(0.003, config=MinerConfig(min_support=0.003)).run(sh)
     assert a.as_dict() == b.as_dict()
 
@@ -272,13 +272,13 @@ def test_parse_to_device_roundtrip():
     assert sh.items.is_cuda and sh.n_lines == 3
 
 
-def test_slab_multipass_from_bitmap(monkeypatch):
+def test_slab_multipass_from_bitmap(tune):
     # shrink the LDS budget so the accumulator needs several passes -> bitmap-tile path
     import fastapriori_amd.ops.primitives as prim
     sh = generate_shard(30000, Comm(), "cpu", 12.0, 5.0, 200, 100, seed=13)
     cfg = dict(min_support=0.005, dedup="off")
     ref = FastApriori(0.005, config=MinerConfig(trim_min_rows=0, level_kernel="bitmap", **cfg)).run(sh)
-    monkeypatch.setattr(prim, "_LDS_BYTES", 24 * 1024)
+    tune(slab_lds_bytes=24 * 1024)
     got = FastApriori(0.005, config=MinerConfig(trim_min_rows=0, level_kernel="slab", **cfg)).run(sh.to(DEV))
     assert ref.as_dict() == got.as_dict()
     got_w = FastApriori(0.005, config=MinerConfig(trim_min_rows=0, level_kernel="slab", min_support=0.005, dedup="on")).run(sh.to(DEV))
@@ -286,8 +286,8 @@ def test_slab_multipass_from_bitmap(monkeypatch):
 
 
 @pytest.mark.parametrize("lds_kb,dense", [(160, 0), (24, 0), (24, 1e-9)])
-def test_slab_class_layout_on_gpu(monkeypatch, lds_kb, dense):
-    # every slab pass in the class layout (plan.cpp cls_layout, FA_SLAB_CLS=2), so
+def test_slab_class_layout_on_gpu(tune, lds_kb, dense):
+    # every slab pass in the class layout (plan.cpp cls_layout, slab_cls=2), so
     # k_count_slab_rec<.., kCls> runs single-pass (contiguous build) and multi-pass
     # (bitmap copy) levels; counts must equal the bitmap kernel's
     import fastapriori_amd.ops.primitives as prim
@@ -295,11 +295,11 @@ def test_slab_class_layout_on_gpu(monkeypatch, lds_kb, dense):
     cfg = dict(min_support=0.004, dedup="off")
     ref = FastApriori(0.004, config=MinerConfig(trim_min_rows=0, level_kernel="bitmap", **cfg)).run(sh)
     import fastapriori_amd.models.apriori as ap
-    monkeypatch.setattr(ap, "DEVICE_LEVELS", False)    # the host plans (device plans: test_gpu_device_levels)
-    monkeypatch.setattr(prim, "SLAB_CLS", 2)
-    monkeypatch.setattr(prim, "_LDS_BYTES", lds_kb * 1024 - 512)
+    tune(device_levels=False)    # the host plans (device plans: test_gpu_device_levels)
+    tune(slab_cls=2)
+    tune(slab_lds_bytes=lds_kb * 1024 - 512)
     if dense:   # every level "dense": the slab kernel runs without its all-zero-prefix test
-        monkeypatch.setattr(prim, "DENSE_MIN_ROWS", dense)
+        tune(dense_min_rows=dense)
     n0 = prim.CLS_LEVELS[0]
     got = FastApriori(0.004, config=MinerConfig(trim_min_rows=0, level_kernel="slab", **cfg)).run(sh.to(DEV))
     assert len(ref.levels) >= 5
@@ -324,11 +324,11 @@ def test_pair_kernels_agree(long_rows):
 
 
 @pytest.mark.parametrize("F1,n_wg", [(600, 0), (601, 3), (257, 1)])
-def test_pair_queue_drain_and_stealing(monkeypatch, F1, n_wg):
+def test_pair_queue_drain_and_stealing(tune, F1, n_wg):
     """k_pair_queue16 over many sub-chunks: pair counts far above 2^16 (the u16 LDS
     counters drain bit 15 into the global count), odd F1 (u32 flush path), and few
     workgroups for many tiles (tile switches and stealing)."""
-    monkeypatch.setenv("FA_PAIR_WG", str(n_wg))
+    tune(pair_wg=n_wg)
     rng = np.random.default_rng(F1)
     n = 150_000
     lens = rng.integers(2, 9, n)
@@ -389,7 +389,7 @@ def test_trim_rows_matches_cpu(weighted):
 
 
 @pytest.mark.parametrize("lds_kb", [0, 24, 12])
-def test_slab_kernel_budgets_and_weights(monkeypatch, lds_kb):
+def test_slab_kernel_budgets_and_weights(tune, lds_kb):
     # single- and multi-pass slab plans (smaller LDS budgets: narrower slabs, more
     # passes from the bitmap tiles), unit and dedup weights: whole-miner results must
     # equal the CPU reference through the deep levels
@@ -399,21 +399,21 @@ def test_slab_kernel_budgets_and_weights(monkeypatch, lds_kb):
     ref = FastApriori(0.004, config=MinerConfig(trim_min_rows=0, level_kernel="bitmap", dedup="off", **cfg)).run(sh)
     assert len(ref.levels) >= 5
     if lds_kb:
-        monkeypatch.setattr(prim, "_LDS_BYTES", lds_kb * 1024)
+        tune(slab_lds_bytes=lds_kb * 1024)
     for dd in ("off", "on"):
         got = FastApriori(0.004, config=MinerConfig(trim_min_rows=0, level_kernel="slab", dedup=dd, **cfg)).run(
             sh.to(DEV))
         assert ref.as_dict() == got.as_dict(), (lds_kb, dd)
 
 
-def test_bundled_levels_on_gpu(monkeypatch):
+def test_bundled_levels_on_gpu(tune):
     # several levels of different k counted in one slab launch (per-piece prefix lengths)
     from fastapriori_amd.models import apriori as ap
     sh = generate_shard(40000, Comm(), "cpu", 10.0, 4.0, 200, 100, seed=23)
     ref = FastApriori(0.003, config=MinerConfig(min_support=0.003, level_kernel="bitmap")).run(sh)
     got = FastApriori(0.003, config=MinerConfig(min_support=0.003)).run(sh.to(DEV))
     assert ref.as_dict() == got.as_dict() and len(ref.levels) >= 5
-    monkeypatch.setattr(ap, "BUNDLE_LEVELS", False)
+    tune(bundle_levels=False)
     got2 = FastApriori(0.003, config=MinerConfig(min_support=0.003)).run(sh.to(DEV))
     assert ref.as_dict() == got2.as_dict()
 
@@ -486,14 +486,13 @@ def test_apriori_gen_device_matches_host(k):
     assert np.array_equal(got[3], np.concatenate([cand[want[0][g2]], want[2][:, None]], 1))
 
 
-@pytest.mark.parametrize("fp4", ["0", "1"])
+@pytest.mark.parametrize("fp4", [False, True])
 @pytest.mark.parametrize("F1,T", [(37, 5000), (300, 70001), (1000, 9000)])
-def test_pair_gram_mfma_matches_popcount(monkeypatch, F1, T, fp4):
-    # i8 MFMA Gram (v_mfma_i32_32x32x32_i8), and its FP4 form (FA_GRAM_FP4=1:
-    # v_mfma_scale_f32_32x32x64_f8f6f4 on e2m1 0/1 operands), vs the popcount Gram and the
-    # CPU Gram on asymmetric random bitmaps (F1 not a multiple of the 128 tile, W of the
-    # 8-word step)
-    monkeypatch.setenv("FA_GRAM_FP4", fp4)
+def test_pair_gram_mfma_matches_popcount(F1, T, fp4):
+    # i8 MFMA Gram (v_mfma_i32_32x32x32_i8, the test oracle), and its FP4 form (the
+    # product path: v_mfma_scale_f32_32x32x64_f8f6f4 on e2m1 0/1 operands), vs the popcount
+    # Gram and a numpy Gram on asymmetric random bitmaps (F1 not a multiple of the 128
+    # tile, W of the 8-word step)
     rng = np.random.default_rng(F1)
     dens = rng.random(F1) * 0.6
     bits = rng.random((F1, T)) < dens[:, None]
@@ -505,7 +504,7 @@ def test_pair_gram_mfma_matches_popcount(monkeypatch, F1, T, fp4):
     pad[:, :packed.shape[1]] = packed
     words[:, :W] = pad.view(np.uint64)
     bm = torch.from_numpy(words.view(np.int64)).to(DEV)
-    got = ops.pair_counts_gram(bm, W, None).cpu()
+    got = ops.pair_counts_gram(bm, W, None, fp4=fp4).cpu()
     ref = ops.pair_counts_gram(bm, W, None, force_popc=True).cpu()
     want = torch.from_numpy(bits.astype(np.int64) @ bits.astype(np.int64).T)
     iu = torch.triu_indices(F1, F1, 1)
@@ -513,11 +512,10 @@ def test_pair_gram_mfma_matches_popcount(monkeypatch, F1, T, fp4):
     assert torch.equal(ref[iu[0], iu[1]], want[iu[0], iu[1]])
 
 
-@pytest.mark.parametrize("fp4", ["0", "1"])
+@pytest.mark.parametrize("fp4", [False, True])
 @pytest.mark.parametrize("F1,classes", [(300, [(1, 700), (2, 40), (3, 600), (7, 3), (9, 520)]),
                                         (37, [(1, 9), (4, 530)])])
-def test_weighted_gram_mfma_matches_popcount(monkeypatch, F1, classes, fp4):
-    monkeypatch.setenv("FA_GRAM_FP4", fp4)
+def test_weighted_gram_mfma_matches_popcount(F1, classes, fp4):
     # deduplicated layouts: one scaled matrix-core launch per weight class of >= 512
     # words, the short classes by the popcount Gram -- exact against the weighted
     # popcount Gram and a numpy reference (FastApriori.scala:233-235)
@@ -533,7 +531,7 @@ def test_weighted_gram_mfma_matches_popcount(monkeypatch, F1, classes, fp4):
     assert any(w > 1 for _, _, w in segs) and any(w == 0 for _, _, w in segs)
     bm = torch.from_numpy(words).to(DEV)
     ww = torch.from_numpy(wword).to(DEV)
-    got = ops.pair_counts_gram(bm, W, ww, wcls).cpu()
+    got = ops.pair_counts_gram(bm, W, ww, wcls, fp4=fp4).cpu()
     ref = ops.pair_counts_gram(bm, W, ww, wcls, force_popc=True).cpu()
     bits = np.unpackbits(words[:, :W].view(np.uint8), axis=1, bitorder="little").astype(np.int64)
     wcol = np.repeat(wword.astype(np.int64), 64)

@@ -1,7 +1,7 @@
 """The 8-rank design on the one GPU of the test box: 8 gloo ranks share the card and
 run the default device path -- device-compacted F_2, device level bundles with the
 count all-reduce inside the bundle loop -- plus the k = 2 reduce-scatter path
-(FA_PAIR_RS_MIN=0) and candidate distribution.  Every rank's result must be
+(FA_TUNE=pair_rs_min=0) and candidate distribution.  Every rank's result must be
 bit-identical to world size 1 (FastApriori.scala:98-100,140)."""
 import pytest
 
@@ -49,7 +49,7 @@ def test_eight_ranks_default_path_match_one(ref):
 
 
 def test_eight_ranks_pair_reduce_scatter_match_one(ref):
-    outs = spawn_local(_rank, 8, N, MS, "count", env={"FA_DIST_BACKEND": "gloo", "FA_PAIR_RS_MIN": "0"})
+    outs = spawn_local(_rank, 8, N, MS, "count", env={"FA_DIST_BACKEND": "gloo", "FA_TUNE": "pair_rs_min=0"})
     for o in outs:
         assert o["sets"] == ref["sets"] and o["bundles"] > 0 and not o["f2_dev"]
 

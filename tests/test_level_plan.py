@@ -92,7 +92,7 @@ def test_level_plan_mixed_prefix_lengths():
     assert np.array_equal(emulate_slab_records(bits, info, passes, buf, ext.size), np.array(want))
 
 
-def test_bundled_levels_match_unbundled(monkeypatch):
+def test_bundled_levels_match_unbundled(monkeypatch, tune):
     # counting later levels from the previous level's candidates must not change results
     import torch
     from fastapriori_amd.models import apriori as ap
@@ -110,7 +110,7 @@ def test_bundled_levels_match_unbundled(monkeypatch):
     monkeypatch.setattr(FastApriori, "_plan_bundle", spy)
     on = FastApriori(0.003, config=MinerConfig(min_support=0.003)).run(sh)
     assert max(seen) > 1 and len(on.levels) >= 5
-    monkeypatch.setattr(ap, "BUNDLE_LEVELS", False)
+    tune(bundle_levels=False)
     off = FastApriori(0.003, config=MinerConfig(min_support=0.003)).run(sh)
     assert on.as_dict() == off.as_dict() and on.items == off.items
 
