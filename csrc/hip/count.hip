@@ -721,6 +721,88 @@ __global__ __launch_bounds__(1024) void k_pair_queue16(
 }
 
 // ---------------------------------------------------------------------------
+// F_2 = pairs with count >= minCount (FastApriori.scala:236-238), compacted on the
+// device in triangle order (row i ascending, then j): three small kernels instead of
+// the gather / compare / scan / two index_copy passes of torch.  The counts come
+// either as the pair kernel's matrix (pc[i * ld + j], j > i) or as the all-reduced
+// flat triangle (pc[tri(i) + j - i - 1], ld < 0).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int64_t pc_tri_base(int64_t i, int64_t F1) { return i * F1 - i * (i + 1) / 2; }
+
+__device__ __forceinline__ uint32_t pc_at(const uint32_t* __restrict__ pc, int64_t ld, int64_t F1, int64_t i,
+                                          int64_t j) {
+  return ld >= 0 ? pc[i * ld + j] : pc[pc_tri_base(i, F1) + (j - i - 1)];
+}
+
+// one workgroup per row i: its kept pairs
+__global__ __launch_bounds__(256) void k_pairs_keep_count(const uint32_t* __restrict__ pc, int64_t ld, int F1,
+                                                          int64_t mc, int32_t* __restrict__ row_cnt) {
+  __shared__ int part[4];
+  const int i = blockIdx.x;
+  int c = 0;
+  for (int j = i + 1 + threadIdx.x; j < F1; j += 256) c += (int64_t)pc_at(pc, ld, F1, i, j) >= mc;
+  c = (int)wave_sum_u32((uint32_t)c);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) row_cnt[i] = part[0] + part[1] + part[2] + part[3];
+}
+
+// exclusive row offsets (one workgroup), |F_2| into n_out[0]
+__global__ __launch_bounds__(1024) void k_pairs_scan(const int32_t* __restrict__ row_cnt, int F1,
+                                                     int64_t* __restrict__ row_off, int64_t* __restrict__ n_out) {
+  __shared__ int64_t part[16];
+  __shared__ int64_t carry;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int b = 0; b < F1; b += 1024) {
+    const int i = b + threadIdx.x;
+    const int v = i < F1 ? row_cnt[i] : 0;
+    const int incl = wave_scan_incl_dpp(v);
+    if (lane == 63) part[wv] = incl;
+    __syncthreads();
+    int64_t before = carry;
+    for (int q = 0; q < wv; ++q) before += part[q];
+    if (i < F1) row_off[i] = before + incl - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = before + incl;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) n_out[0] = carry;
+}
+
+// one workgroup per row: its kept pairs in j order at row_off[i]
+__global__ __launch_bounds__(256) void k_pairs_emit(const uint32_t* __restrict__ pc, int64_t ld, int F1, int64_t mc,
+                                                    const int64_t* __restrict__ row_off, int32_t* __restrict__ rows,
+                                                    int32_t* __restrict__ cnt) {
+  __shared__ int part[4];
+  __shared__ int64_t carry;
+  const int i = blockIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (threadIdx.x == 0) carry = row_off[i];
+  __syncthreads();
+  for (int j0 = i + 1; j0 < F1; j0 += 256) {
+    const int j = j0 + threadIdx.x;
+    const uint32_t v = j < F1 ? pc_at(pc, ld, F1, i, j) : 0u;
+    const int keep = (j < F1 && (int64_t)v >= mc) ? 1 : 0;
+    const int incl = wave_scan_incl_dpp(keep);
+    if (lane == 63) part[wv] = incl;
+    __syncthreads();
+    int64_t at = carry;
+    for (int q = 0; q < wv; ++q) at += part[q];
+    at += incl - keep;
+    if (keep) {
+      rows[2 * at] = i;
+      rows[2 * at + 1] = j;
+      cnt[at] = (int32_t)v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 255) carry = at + keep;
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k = 2, dense bit-matrix Gram with popcounts.  Tile 64x64 items, K-step 32 words.
 // ---------------------------------------------------------------------------
 constexpr int kGT = 64, kGK = 32, kGS = kGT + 1;   // LDS row stride (u64) breaks bank aliasing
@@ -1703,5 +1785,17 @@ FA_API int fa_hip_pair_queue16(const uint8_t* cnt, const int64_t* base, const ui
   n_wg = (int)std::min<int64_t>(n_wg, (int64_t)nsub * nbp);
   hipLaunchKernelGGL(k_pair_queue16, dim3((unsigned)n_wg), dim3(64 * kPW), 0, st, cnt, base, lr, T, nbatch, F1, ld,
                      nb, nbp, qctr, nsub, out);
+  FA_LAUNCH_RET();
+}
+
+// F_2 of the pair counts (matrix with row stride ld, or the flat triangle when ld < 0):
+// rows int32 [|F_2|][2], cnt int32 [|F_2|] in triangle order, |F_2| into n_out (device
+// int64); row_cnt int32 [F1] and row_off int64 [F1] scratch.
+FA_API int fa_hip_pairs_compact(const uint32_t* pc, int64_t ld, int32_t F1, int64_t mc, int32_t* row_cnt,
+                                int64_t* row_off, int32_t* rows, int32_t* cnt, int64_t* n_out, hipStream_t st) {
+  if (F1 < 2) return 1;
+  hipLaunchKernelGGL(k_pairs_keep_count, dim3((unsigned)F1), dim3(256), 0, st, pc, ld, F1, mc, row_cnt);
+  hipLaunchKernelGGL(k_pairs_scan, dim3(1), dim3(1024), 0, st, row_cnt, F1, row_off, n_out);
+  hipLaunchKernelGGL(k_pairs_emit, dim3((unsigned)F1), dim3(256), 0, st, pc, ld, F1, mc, row_off, rows, cnt);
   FA_LAUNCH_RET();
 }

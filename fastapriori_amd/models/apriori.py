@@ -1227,6 +1227,10 @@ class FastApriori:
         strat = self._pick_pair_strategy(db, F1)
         self.stats["pair_strategy"] = strat
         r, nr = (self.comm.rank, self.comm.world_size) if self.cand_par else (0, 1)
+        C2 = F1 * (F1 - 1) // 2
+        rs = self.comm.distributed and C2 >= TUNING.pair_rs_min
+        # F_2 compacted on the device (no readback before the first device bundle)
+        on_dev = self._f2_defer and not rs and db["ranks"].is_cuda
         if strat == "gram":
             self._bitmaps(db)
             # candidate parallelism: each rank takes a 32-word-aligned slice of the columns
@@ -1234,7 +1238,7 @@ class FastApriori:
             w0, w1 = (W * r // nr) // 32 * 32, (W if r == nr - 1 else (W * (r + 1) // nr) // 32 * 32)
             wword = db["wword"][w0:w1] if db["wword"] is not None else None
             pc = ops.pair_counts_gram(db["bm"][:, w0:], max(w1 - w0, 0), wword,
-                                      self._slice_classes(db.get("wcls"), w0, w1))
+                                      self._slice_classes(db.get("wcls"), w0, w1), raw=on_dev)
         else:
             roff, ranks, wrow = db["roff"], db["ranks"], db["wrow"]
             if nr > 1:   # candidate parallelism: each rank takes a slice of the rows
@@ -1244,25 +1248,18 @@ class FastApriori:
                 roff, ranks = roff[a:b + 1] - ra, ranks[ra:rb]
                 wrow = wrow[a:b] if wrow is not None else None
             pc = ops.pair_counts_horizontal(roff, ranks, wrow, F1, db.get("long_rows", True),
-                                            bcnt=db.get("bcnt") if nr == 1 and wrow is None else None)
+                                            bcnt=db.get("bcnt") if nr == 1 and wrow is None else None, raw=on_dev)
         self._run_deferred()      # host-only work while the pair kernel runs
-        key = (F1, pc.device)
-        if key not in _TRIU_CACHE:
-            _TRIU_CACHE.clear()
-            # upper-triangle positions of the F1 x F1 pair matrix, and their flat offsets
-            iu = torch.triu_indices(F1, F1, 1, device=pc.device)
-            _TRIU_CACHE[key] = (iu, iu[0] * F1 + iu[1])
-        iu, fi = _TRIU_CACHE[key]
-        flat = pc.reshape(-1)[fi]
         T, nnz = int(db["T"]), int(db["ranks"].numel())
         if strat == "gram":
             self.stats["pair_hbm_bytes_est"] = int(F1 * max(db["W"], 1) * 8 * ((F1 + 63) // 64))
         else:
             nb = (F1 + 255) // 256
             self.stats["pair_hbm_bytes_est"] = int(2 * (4 * nnz + 8 * T) + nnz * (nb + 1) + T * nb * (nb + 1))
-        rs = self.comm.distributed and flat.numel() >= TUNING.pair_rs_min
-        if self._f2_defer and not rs and iu.is_cuda:
-            return self._pairs_on_device(flat, iu, mc, db)
+        if on_dev:
+            return self._pairs_on_device(pc, mc, db)
+        iu, fi = self._triu(F1, pc.device)
+        flat = pc.reshape(-1)[fi]
         if rs:
             # X12 as reduce-scatter + local threshold + all-gather of the survivors
             # (F_2 << C_2): each rank thresholds its 1/world slice of the summed triangle
@@ -1279,29 +1276,38 @@ class FastApriori:
         h = torch.stack([iu[0][keep], iu[1][keep], vals.to(device=iu.device, dtype=torch.int64)]).cpu().numpy()
         return np.ascontiguousarray(h[:2].T, dtype=np.int32), h[2].astype(np.int64)
 
-    def _pairs_on_device(self, flat: torch.Tensor, iu, mc: int, db):
+    @staticmethod
+    def _triu(F1: int, dev):
+        """Upper-triangle positions of the F1 x F1 pair matrix and their flat offsets."""
+        key = (F1, dev)
+        if key not in _TRIU_CACHE:
+            _TRIU_CACHE.clear()
+            iu = torch.triu_indices(F1, F1, 1, device=dev)
+            _TRIU_CACHE[key] = (iu, iu[0] * F1 + iu[1])
+        return _TRIU_CACHE[key]
+
+    def _pairs_on_device(self, pc: torch.Tensor, mc: int, db):
         """F_2 = pairs with count >= mc (FastApriori.scala:236-238), compacted on the
-        device in pair order with no host synchronisation: a scan of the keep mask
-        gives every kept pair its row; the rest write to a dump row.  |F_2| stays on
-        the device (the first device bundle reads it); the host copy of F_2 arrives
-        with _dl_flush.  The readback bound: every frequent pair has count >= mc and
-        the counts sum to the pair increments, so |F_2| <= pair increments / mc."""
-        self.comm.all_reduce_(flat, bound=self.stats["n_lines"])
-        C2 = flat.numel()
-        keep = flat >= mc
-        pos = torch.cumsum(keep, 0, dtype=torch.int64)
-        dst = torch.where(keep, pos - 1, C2)
-        pairs = _TRIU_CACHE.get(("i32", self._F1, flat.device))
-        if pairs is None:
-            pairs = _TRIU_CACHE[("i32", self._F1, flat.device)] = torch.stack([iu[0], iu[1]], 1).to(torch.int32)
-        rows = torch.empty((C2 + 1, 2), dtype=torch.int32, device=flat.device)
-        rows.index_copy_(0, dst, pairs)
-        cnt = torch.empty(C2 + 1, dtype=torch.int32, device=flat.device)
-        cnt.index_copy_(0, dst, flat.to(torch.int32))
+        device in pair order with no host synchronisation (count.hip
+        fa_hip_pairs_compact: per-row keep counts, one scan, per-row emit).  pc: the
+        pair kernel's raw int32 counts; across ranks its triangle is gathered and
+        all-reduced first.  |F_2| stays on the device (the first device bundle reads
+        it); the host copy of F_2 arrives with _dl_flush.  The readback bound: every
+        frequent pair has count >= mc and the counts sum to the pair increments, so
+        |F_2| <= pair increments / mc."""
+        F1 = self._F1
+        C2 = F1 * (F1 - 1) // 2
+        if self.comm.distributed:
+            _, fi = self._triu(F1, pc.device)
+            flat = pc.reshape(-1)[fi] if pc.is_contiguous() else pc.contiguous().reshape(-1)[fi]
+            self.comm.all_reduce_(flat, bound=self.stats["n_lines"])
+            rows, cnt, n = ops.primitives.pairs_compact(flat.contiguous(), F1, mc, flat=True)
+        else:
+            rows, cnt, n = ops.primitives.pairs_compact(pc, F1, mc)
         pw = db.get("pair_work_all")      # exact only without rows of >= 255 items (histogram's last bin)
         exact = pw is not None and not db.get("long_rows", True) and not self.cand_par
         bound = min(C2, int(pw) // mc + 1) if exact and mc > 0 else C2
-        self._f2_dev, self._f2_cnt_dev, self._f2_n_dev, self._f2_bound = rows, cnt, pos[-1:], max(int(bound), 1)
+        self._f2_dev, self._f2_cnt_dev, self._f2_n_dev, self._f2_bound = rows, cnt, n, max(int(bound), 1)
         self.stats["f2_on_device"] = True
         return None, None
 

@@ -445,8 +445,10 @@ def build_bitmaps(roff, ranks, src, ncols: int, F1: int, item_map=None, used=Non
     return bm[:F1], W
 
 
-def pair_counts_horizontal(roff, ranks, wrow, F1: int, long_rows: bool = True, bcnt=None) -> torch.Tensor:
-    """Pair supports from the compressed rows -> int64 [F1, F1] (upper triangle).
+def pair_counts_horizontal(roff, ranks, wrow, F1: int, long_rows: bool = True, bcnt=None,
+                           raw: bool = False) -> torch.Tensor:
+    """Pair supports from the compressed rows -> int64 [F1, F1] (upper triangle);
+    raw (device): the kernel's int32 [F1, F1] view as it is (pairs_compact's input).
 
     Device path: per-row block counts + local-rank bytes (blocked layout), then
     the 256 x 256 packed-u16 tile kernel for unit-weight rows, or 128 x 128 u32
@@ -505,11 +507,32 @@ def pair_counts_horizontal(roff, ranks, wrow, F1: int, long_rows: bool = True, b
             else:
                 _hip_call("fa_hip_pair_blocked", _p(cnt), _p(base), _p(lr), T, _p(wrow), F1, _p(out),
                           PAIR_CHUNK_ROWS, st)
-        return out.to(_I64)
+        return out if raw else out.to(_I64)
     out = torch.zeros((F1, F1), dtype=_I64)
     if T > 0 and F1 >= 2:
         _native.host().fa_cpu_pair_horizontal(_p(roff), _p(ranks), T, _p(wrow), F1, _p(out), num_threads())
     return out
+
+
+def pairs_compact(pc: torch.Tensor, F1: int, mc: int, flat: bool = False):
+    """F_2 on the device (count.hip fa_hip_pairs_compact): pairs with count >= mc in
+    triangle order from the raw int32 pair counts (pair_counts_*(raw=True): a matrix
+    with any row stride) or, flat=True, from the all-reduced int32 triangle.  Returns
+    (rows int32 [C2 + 1, 2], counts int32 [C2 + 1], |F_2| int64 [1]) with no host
+    synchronisation."""
+    dev = pc.device
+    C2 = F1 * (F1 - 1) // 2
+    rows = torch.empty((C2 + 1, 2), dtype=_I32, device=dev)
+    cnt = torch.empty(C2 + 1, dtype=_I32, device=dev)
+    n = torch.empty(1, dtype=_I64, device=dev)
+    row_cnt = torch.empty(max(F1, 1), dtype=_I32, device=dev)
+    row_off = torch.empty(max(F1, 1), dtype=_I64, device=dev)
+    if flat:
+        assert pc.is_contiguous() and pc.numel() == C2 and pc.element_size() == 4
+    ld = -1 if flat else pc.stride(0)
+    _hip_call("fa_hip_pairs_compact", _p(pc), ld, F1, int(mc), _p(row_cnt), _p(row_off), _p(rows), _p(cnt), _p(n),
+              _stream(pc))
+    return rows, cnt, n
 
 
 # weight classes shorter than TUNING.gram_mfma_min_class_words words go to the popcount
@@ -545,7 +568,7 @@ def gram_segments(W: int, weighted: bool, wcls=None, force_popc: bool = False) -
 
 
 def pair_counts_gram(bm: torch.Tensor, W: int, wword, wcls=None, force_popc: bool = False,
-                     fp4: bool = True) -> torch.Tensor:
+                     fp4: bool = True, raw: bool = False) -> torch.Tensor:
     """Pair supports from the item-major bitmaps over words [0, W) -> int64 [F1, F1]
     (upper triangle).  Device: the FP4 matrix-core Gram (k_pair_gram_mfma4) per
     weight class, scaled by the class weight (FastApriori.scala:233-235's weighted
@@ -564,7 +587,7 @@ def pair_counts_gram(bm: torch.Tensor, W: int, wword, wcls=None, force_popc: boo
                 else:
                     _hip_call("fa_hip_pair_gram_popc", bm.data_ptr() + 8 * a, F1, Wp, b - a,
                               wword.data_ptr() + 4 * a if wword is not None else None, _p(out), 4096, st)
-        return out.to(_I64)
+        return out if raw else out.to(_I64)
     out = torch.zeros((F1, F1), dtype=_I64)
     if W > 0 and F1 >= 2:
         _native.host().fa_cpu_pair_gram(_p(bm), F1, Wp, W, _p(wword), _p(out), num_threads())
