@@ -1417,6 +1417,120 @@ FA_API int fa_hip_trim_emit(const int64_t* roff, const int32_t* ranks, const int
 // Two-pass fused compression: agg int32 [3 * nwg], hist u32 [64 * 256] striped copies (zeroed by the caller).
 // aggb (optional, nb <= 8 256-rank blocks): int32 [nb * nwg] per-workgroup block totals
 // (the fused pair layout of k_cmp_emit).
+// ---------------------------------------------------------------------------
+// Exclusive scans of k_cmp_agg's per-workgroup aggregates for k_cmp_emit, in three
+// small kernels (chunk sums, one scan of the chunk sums, chunk rescans) instead of
+// torch's conversion, three cumsums and a fourth for the block totals (~10 kernels
+// and two host allocations rounds per run).  Sequences: s < 3 the interleaved agg
+// (kept rows, kept items, overflow rows) of nwg workgroups -> pre[s][0 .. nwg];
+// s = 3 (aggb != null) the block-major block totals, nb * nwg -> preb[0 .. nb * nwg].
+// Also roff[0] = 0.
+// ---------------------------------------------------------------------------
+constexpr int kScanChunk = 4096;      // elements per workgroup (256 threads x 16)
+
+__device__ __forceinline__ int64_t cs_len(int s, int64_t nwg, int nb) { return s < 3 ? nwg : nb * nwg; }
+__device__ __forceinline__ int32_t cs_at(const int32_t* __restrict__ agg, const int32_t* __restrict__ aggb, int s,
+                                         int64_t i) {
+  return s < 3 ? agg[3 * i + s] : aggb[i];
+}
+
+__global__ __launch_bounds__(256) void k_cmp_scan_sums(const int32_t* __restrict__ agg,
+                                                       const int32_t* __restrict__ aggb, int64_t nwg, int nb,
+                                                       int64_t* __restrict__ part, int64_t pstride) {
+  const int s = blockIdx.y;
+  const int64_t n = cs_len(s, nwg, nb), c0 = (int64_t)blockIdx.x * kScanChunk;
+  if (c0 >= n) return;
+  int64_t t = 0;
+#pragma unroll 4
+  for (int k = 0; k < kScanChunk / 256; ++k) {
+    const int64_t i = c0 + k * 256 + threadIdx.x;
+    if (i < n) t += cs_at(agg, aggb, s, i);
+  }
+  __shared__ int64_t w4[4];
+  t = (int64_t)wave_sum_u64((unsigned long long)t);
+  if ((threadIdx.x & 63) == 0) w4[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) part[s * pstride + blockIdx.x] = w4[0] + w4[1] + w4[2] + w4[3];
+}
+
+// exclusive scan of every sequence's chunk sums (one workgroup; <= 1024 chunks each)
+__global__ __launch_bounds__(1024) void k_cmp_scan_parts(int64_t* __restrict__ part, int64_t pstride, int nseq,
+                                                         int64_t nwg, int nb) {
+  __shared__ int64_t wsum[16];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int s = 0; s < nseq; ++s) {
+    const int64_t nch = (cs_len(s, nwg, nb) + kScanChunk - 1) / kScanChunk;
+    const int64_t v = threadIdx.x < nch ? part[s * pstride + threadIdx.x] : 0;
+    // 64-bit inclusive wave scan (shuffles)
+    int64_t incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    int64_t before = 0;
+    for (int q = 0; q < wv; ++q) before += wsum[q];
+    if (threadIdx.x < nch) part[s * pstride + threadIdx.x] = before + incl - v;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void k_cmp_scan_out(const int32_t* __restrict__ agg,
+                                                      const int32_t* __restrict__ aggb, int64_t nwg, int nb,
+                                                      const int64_t* __restrict__ part, int64_t pstride,
+                                                      int64_t* __restrict__ pre, int64_t* __restrict__ preb,
+                                                      int64_t* __restrict__ roff) {
+  const int s = blockIdx.y;
+  const int64_t n = cs_len(s, nwg, nb), c0 = (int64_t)blockIdx.x * kScanChunk;
+  if (s == 0 && blockIdx.x == 0 && threadIdx.x == 0) roff[0] = 0;
+  if (c0 >= n) return;
+  int64_t* out = s < 3 ? pre + s * (nwg + 1) : preb;
+  // each thread: 16 consecutive elements; thread sums scanned across the workgroup
+  constexpr int PER = kScanChunk / 256;
+  int32_t v[PER];
+  int64_t t = 0;
+  const int64_t i0 = c0 + (int64_t)threadIdx.x * PER;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    v[k] = i0 + k < n ? cs_at(agg, aggb, s, i0 + k) : 0;
+    t += v[k];
+  }
+  __shared__ int64_t w4[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int64_t incl = t;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t u = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += u;
+  }
+  if (lane == 63) w4[wv] = incl;
+  __syncthreads();
+  int64_t run = part[s * pstride + blockIdx.x] + incl - t;
+  for (int q = 0; q < wv; ++q) run += w4[q];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    if (i0 + k < n) out[i0 + k] = run;
+    run += v[k];
+    if (i0 + k == n - 1) out[n] = run;          // the sequence total
+  }
+}
+
+FA_API int fa_hip_cmp_scan(const int32_t* agg, const int32_t* aggb, int64_t nwg, int nb, int64_t* part,
+                           int64_t* pre, int64_t* preb, int64_t* roff, hipStream_t st) {
+  if (nwg <= 0) return 0;
+  const int nseq = aggb ? 4 : 3;
+  const int64_t nmax = aggb ? std::max<int64_t>(nwg, (int64_t)nb * nwg) : nwg;
+  const int64_t nch = (nmax + kScanChunk - 1) / kScanChunk;
+  if (nch > 1024) return 1;                       // (n <= 4M workgroups' rows)
+  const dim3 g((unsigned)nch, (unsigned)nseq);
+  hipLaunchKernelGGL(k_cmp_scan_sums, g, dim3(256), 0, st, agg, aggb, nwg, nb, part, nch);
+  hipLaunchKernelGGL(k_cmp_scan_parts, dim3(1), dim3(1024), 0, st, part, nch, nseq, nwg, nb);
+  hipLaunchKernelGGL(k_cmp_scan_out, g, dim3(256), 0, st, agg, aggb, nwg, nb, part, nch, pre, preb, roff);
+  FA_LAUNCH_RET();
+}
+
 FA_API int fa_hip_cmp_agg(const int64_t* off, const int32_t* items, const int32_t* lut, int64_t n, int32_t* agg,
                           uint32_t* hist, int32_t* aggb, int nb, hipStream_t st) {
   if (n <= 0) return 0;

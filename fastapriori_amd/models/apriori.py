@@ -320,7 +320,7 @@ class FastApriori:
     # k >= 3 on the device (FastApriori.scala:110-121, :132-160)
     # ------------------------------------------------------------------
     def _device_levels_planned(self, resume) -> bool:
-        return (TUNING.device_levels and self._dev.type == "cuda" and not self.cand_par
+        return (TUNING.device_levels and self._dev.type == "cuda"
                 and 2 <= self._F1 <= ops.primitives.DL_MAX_F1
                 and self.cfg.level_kernel in ("auto", "slab") and self.stats["n_lines"] < (1 << 31)
                 and (self.cfg.max_level == 0 or self.cfg.max_level >= 3))
@@ -406,7 +406,7 @@ class FastApriori:
                 if not TUNING.bundle_levels or k - 1 > TUNING.bundle_max_prefix:
                     max_lv = 1
                 post = TUNING.dl_post and max_lv > 1
-                S.rows_hint = int(db["ncols"])
+                S.rows_hint = int(self._count_view(db)["ncols"])
                 if post:
                     self._dl_post_setup(S, db, k, F1, c_bound, n_bound, lds)
                 # the results not staged yet go to the host on a copy stream while this
@@ -452,7 +452,8 @@ class FastApriori:
                     with tm.phase(f"trim{k}"), roctx_range("trim"):
                         self._trim(db, used, k, C, decided=bool(done == 1 and S.post.trim))
                     with tm.phase("count"), roctx_range("count"):
-                        cnt = Pm.dl_count(S, plan, db["roff"], db["ranks"], db["src"], db["ncols"], F1, db["wword"])
+                        v = self._count_view(db)
+                        cnt = Pm.dl_count(S, plan, v["roff"], v["ranks"], v["src"], v["ncols"], F1, v["wword"])
                     sw = int(plan["sw"])
                 with tm.phase("count"), roctx_range("count"):
                     self.comm.all_reduce_(cnt)
@@ -500,17 +501,18 @@ class FastApriori:
         wide = Pm.dl_slab_width(n_used, min(C0, 8192), lds, self._dl_mp_accb)[0] == 0
         with self._timer.phase(f"trim{k}"), roctx_range("trim"):
             self._trim(db, used, k, C0)
+        v = self._count_view(db)
         if wide:
             with self._timer.phase("count"), roctx_range("count_bitmap"):
-                cnt = self._dl_bitmap_count(S, db, used)
+                cnt = self._dl_bitmap_count(S, v, used)
             self.stats["device_bitmap_levels"] = self.stats.get("device_bitmap_levels", 0) + 1
             return c, cnt
         with self._timer.phase("count"), roctx_range("count_multi"):
-            bm, bmap = self._bitmaps(db, used)
+            bm, bmap = self._bitmaps(v, used)
             used_t = torch.from_numpy(used.astype(np.int64)).to(self._dev)
             bm_rows = (bmap[used_t] if bmap is not None else used_t).to(torch.int32).contiguous()
-            cnt = Pm.dl_count_multipass(S, F1, n_used, C0, lds, db["roff"], db["ranks"], db["src"], db["ncols"],
-                                        db["wword"], bm, bm_rows,
+            cnt = Pm.dl_count_multipass(S, F1, n_used, C0, lds, v["roff"], v["ranks"], v["src"], v["ncols"],
+                                        v["wword"], bm, bm_rows,
                                         self.stats["min_count"] / max(1, self.stats["n_lines"]), self._dev)
         if cnt is None:
             return None
@@ -546,6 +548,11 @@ class FastApriori:
         Pm.LAST_LEVEL_PLAN.update(kernel="bitmap_dev", rows=int(db["roff"].numel() - 1), used=int(used.size), C=C, m=m)
         return cnt.to(torch.int32)
 
+    def _count_view(self, db) -> dict:
+        """The rows this rank counts: all of its shard (count distribution), or its row
+        slice of the replicated DB (candidate distribution, _cand_rows_view)."""
+        return self._cand_rows_view(db) if self.cand_par else db
+
     def _dl_post_setup(self, S, db, k: int, F1: int, c_bound: int, n_bound: int, lds: int) -> None:
         """Fill the post step of fa_hip_dl_more (ops.primitives.DlPostC): buffers, the
         current rows and the trimming inputs of level k (FastApriori._trim_worth_it)."""
@@ -560,10 +567,14 @@ class FastApriori:
                                             b["out"].data_ptr())
         P.rec_cap, P.part_cap, P.out_cap = b["c_cap"], b["part"].numel(), b["c_cap"]
         P.gpre, P.gpre_cap = b["gpre"].data_ptr(), b["gpre"].numel()
-        P.roff, P.ranks = db["roff"].data_ptr(), db["ranks"].data_ptr()
-        P.src = db["src"].data_ptr() if db["src"] is not None else None
-        P.wword = db["wword"].data_ptr() if db["wword"] is not None else None
-        P.ncols, P.lds_kernel, P.lds_budget = int(db["ncols"]), float(TUNING.slab_lds_bytes), float(lds)
+        # counted rows: the rank's row slice of the replicated DB in candidate mode
+        # (_cand_rows_view); the trimming inputs below stay the whole DB's (every rank
+        # takes the same decision)
+        v = self._count_view(db)
+        P.roff, P.ranks = v["roff"].data_ptr(), v["ranks"].data_ptr()
+        P.src = v["src"].data_ptr() if v["src"] is not None else None
+        P.wword = v["wword"].data_ptr() if v["wword"] is not None else None
+        P.ncols, P.lds_kernel, P.lds_budget = int(v["ncols"]), float(TUNING.slab_lds_bytes), float(lds)
         P.accb = self._dl_accb
         c1 = np.ascontiguousarray(db["c1"], dtype=np.int64)
         alive = np.ascontiguousarray(db["alive"], dtype=np.uint8)

@@ -75,6 +75,7 @@ _HIP_SIGS = {
     "fa_hip_ag_build": (C.c_int, [vp, i64, C.c_int, vp, C.c_uint32, C.c_int, vp, vp]),
     "fa_hip_ag_rows": (C.c_int, [vp, i64, C.c_int, vp, C.c_uint32, C.c_int, vp, vp, vp, vp, C.c_int, vp]),
     "fa_hip_cmp_agg": (C.c_int, [vp, vp, vp, i64, vp, vp, vp, C.c_int, vp]),
+    "fa_hip_cmp_scan": (C.c_int, [vp, vp, i64, C.c_int, vp, vp, vp, vp, vp]),
     "fa_hip_cmp_emit": (C.c_int, [vp, vp, vp, i64, vp, vp, vp, vp, vp, vp, vp, vp, C.c_int, vp, vp, i64, vp, vp,
                                   vp]),
     "fa_hip_lr_rows": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, vp, i64, vp]),

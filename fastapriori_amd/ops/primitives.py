@@ -285,23 +285,24 @@ def compress_rows(offsets, items, lut, F1: int, block_counts: bool = True, probe
     aggb = torch.empty(nb * nwg, dtype=_I32, device=dev) if fused else None
     hist = torch.zeros(64, 256, dtype=_I32, device=dev)
     _hip_call("fa_hip_cmp_agg", _p(offsets), _p(items), _p(lut), n, _p(agg), _p(hist), _p(aggb), nb, st)
-    pre = torch.zeros(3, nwg + 1, dtype=_I64, device=dev)
-    a3 = agg.view(-1, 3).t().to(_I64).contiguous()
-    for q in range(3):   # 1-D scans (the batched innermost-dim scan is ~20x slower here)
-        torch.cumsum(a3[q], 0, out=pre[q, 1:])
+    # exclusive scans of the aggregates (and block totals) + roff[0] = 0: prep.hip fa_hip_cmp_scan
+    pre = torch.empty(3, nwg + 1, dtype=_I64, device=dev)
+    preb = torch.empty(nb * nwg + 1, dtype=_I64, device=dev) if fused else None
     kept = torch.empty(max(n, 1), dtype=_I32, device=dev)
     roff = torch.empty(n + 1, dtype=_I64, device=dev)
-    roff[0] = 0
+    part = torch.empty(4 * ((max(nb, 1) * max(nwg, 1) + 4095) // 4096 + 1), dtype=_I64, device=dev)
+    _hip_call("fa_hip_cmp_scan", _p(agg), _p(aggb), max(nwg, 1) if n > 0 else 0, nb, _p(part), _p(pre), _p(preb),
+              _p(roff), st)
+    if n <= 0:
+        pre.zero_()
+        roff[0] = 0
     ranks = torch.empty(max(items.numel(), 1), dtype=_I32, device=dev)
     over = torch.empty(max(n, 1), dtype=_I32, device=dev)
-    bcnt = lr = lbase = ovb = preb = None
+    bcnt = lr = lbase = ovb = None
     lr_cap = 0
     if blk:
         bcnt = torch.empty(nb * max(n, 1) + PAIR_PAD_BATCHES * 64 + 64, dtype=torch.uint8, device=dev)
     if fused:
-        # block-major exclusive offsets of the per-workgroup block totals
-        preb = torch.zeros(nb * nwg + 1, dtype=_I64, device=dev)
-        torch.cumsum(aggb, 0, out=preb[1:])
         lr_cap = max(items.numel(), 1)
         lr = torch.empty(lr_cap + 1024, dtype=torch.uint8, device=dev)   # pad: aligned dword staging reads
         lbase = torch.zeros(nb * ((n + 63) // 64) + PAIR_PAD_BATCHES, dtype=_I64, device=dev)

@@ -55,6 +55,9 @@ def test_eight_ranks_pair_reduce_scatter_match_one(ref):
 
 
 def test_eight_ranks_candidate_mode_match_one(ref):
+    # candidate distribution on the device level loop: every rank holds the whole DB and
+    # counts its row slice of it in the bundles (FastApriori._count_view)
     outs = spawn_local(_rank, 8, N, MS, "candidate", env={"FA_DIST_BACKEND": "gloo"})
     for o in outs:
         assert o["sets"] == ref["sets"]
+        assert o["bundles"] > 0 and o["f2_dev"] and not o["fallbacks"]
