@@ -1034,6 +1034,154 @@ __global__ __launch_bounds__(256) void k_pair_gram_mfma4(const uint64_t* __restr
       }
 }
 
+// The FP4 Gram, software-pipelined (the product path; k_pair_gram_mfma4<true> above
+// is kept as its reference form).  k_pair_gram_mfma4 kept the matrix pipe busy 41 % of
+// the kernel (PMC, T40I10D100M): one wave per SIMD (256 accumulator registers), all 256
+// VGPRs taken (16-word register prefetch of both operands), so each word's LDS reads
+// went out behind the MFMAs and their s_waitcnt left the pipe idle, plus a 64-bit shift
+// per operand to pick the lane half's 32 transactions.  Here
+//   * a stage is 8 words (half the prefetch registers) double-buffered in LDS, one
+//     barrier per stage;
+//   * the two 32-bit halves of a word sit in separate LDS planes (row stride 9 dwords,
+//     the hi plane 32 dwords off the lo plane mod 64): one conflict-free ds_read_b32 per
+//     operand, no shift;
+//   * the unpacked operands are double-buffered: word w + 1's reads are issued first,
+//     word w's 16 MFMAs follow with w + 1's unpacking interleaved between them
+//     (sched_group_barrier), so the matrix pipe always has the next operands.
+// The prefetch loads are branch-free (clamped addresses, masked values).
+constexpr int kGW = 8;                       // words per stage
+constexpr int kGRow = kGW + 1;                 // plane row stride (dwords)
+constexpr int kGPl = kMT4 * kGRow + 32;     // plane size (dwords): hi plane = lo + 32 mod 64 banks
+constexpr int kGLd = kMT4 * kGW / 256;       // staged words per thread and operand
+
+__global__ __launch_bounds__(256) void k_pair_gram_fp4(const uint64_t* __restrict__ bm, int32_t F1, int64_t Wp,
+                                                       int64_t W, int nt, int ntp, int64_t kchunk,
+                                                       uint32_t* __restrict__ out, uint32_t scale) {
+  __shared__ uint32_t S[2][2][2 * kGPl];      // [buffer][A, B][lo plane, hi plane]
+  const uint32_t logical = xcd_remap(blockIdx.x, gridDim.x);
+  const int tp = (int)(logical % (uint32_t)ntp);
+  const int64_t kc = logical / (uint32_t)ntp;
+  int ti, tj;
+  tri_index(tp, nt, ti, tj);
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int wr = (wv >> 1) * 32 * kM4, wc = (wv & 1) * 32 * kM4;
+  const bool live = !(ti == tj && wr > wc);
+  fa_v16f acc[kM4][kM4];
+#pragma unroll
+  for (int i = 0; i < kM4; ++i)
+#pragma unroll
+    for (int j = 0; j < kM4; ++j) acc[i][j] = fa_v16f{0};
+  const int64_t k_begin = kc * kchunk, k_end = min(W, k_begin + kchunk);
+  uint64_t pa[kGLd], pb[kGLd];
+  uint32_t oka = 0, okb = 0;
+  auto fetch = [&](int64_t k0) {
+    oka = okb = 0;
+#pragma unroll
+    for (int it = 0; it < kGLd; ++it) {
+      const int idx = threadIdx.x + it * 256;
+      const int row = idx / kGW, w = idx % kGW;
+      const int ra = ti * kMT4 + row, rb = tj * kMT4 + row;
+      const int64_t kk = k0 + w;
+      const bool okk = kk < k_end;
+      pa[it] = bm[(int64_t)(ra < F1 ? ra : 0) * Wp + (okk ? kk : k_begin)];
+      pb[it] = bm[(int64_t)(rb < F1 ? rb : 0) * Wp + (okk ? kk : k_begin)];
+      oka |= (uint32_t)(ra < F1 && okk) << it;
+      okb |= (uint32_t)(rb < F1 && okk) << it;
+    }
+  };
+  auto stage = [&](int buf) {
+#pragma unroll
+    for (int it = 0; it < kGLd; ++it) {
+      const int idx = threadIdx.x + it * 256;
+      const int row = idx / kGW, w = idx % kGW;
+      const uint64_t a = ((oka >> it) & 1) ? pa[it] : 0ull;
+      const uint64_t b = ((okb >> it) & 1) ? pb[it] : 0ull;
+      S[buf][0][row * kGRow + w] = (uint32_t)a;
+      S[buf][0][kGPl + row * kGRow + w] = (uint32_t)(a >> 32);
+      S[buf][1][row * kGRow + w] = (uint32_t)b;
+      S[buf][1][kGPl + row * kGRow + w] = (uint32_t)(b >> 32);
+    }
+  };
+  if (k_begin < k_end) {
+    fetch(k_begin);
+    stage(0);
+  }
+  __syncthreads();
+  // the lane's row offsets in its half's plane
+  int oa[kM4], ob[kM4];
+#pragma unroll
+  for (int i = 0; i < kM4; ++i) {
+    oa[i] = h * kGPl + (wr + 32 * i + r) * kGRow;
+    ob[i] = h * kGPl + (wc + 32 * i + r) * kGRow;
+  }
+  int buf = 0;
+  for (int64_t k0 = k_begin; k0 < k_end; k0 += kGW) {
+    const bool more = k0 + kGW < k_end;
+    if (more) fetch(k0 + kGW);                   // global loads in flight during the MFMAs
+    if (live) {
+      const uint32_t* As = S[buf][0];
+      const uint32_t* Bs = S[buf][1];
+      fa_v8i fa0[kM4], fb0[kM4], fa1[kM4], fb1[kM4];
+      uint32_t ra[kM4], rb[kM4];
+#pragma unroll
+      for (int i = 0; i < kM4; ++i) {
+        fa0[i] = unpack32_fp4(As[oa[i]]);
+        fb0[i] = unpack32_fp4(Bs[ob[i]]);
+      }
+      // word w's MFMAs on (fa, fb) with word wn's reads ahead of them and its unpacking
+      // into (na, nb) between them; branch-free: the stage's last step re-reads word 0
+      auto step = [&](fa_v8i* fa, fa_v8i* fb, fa_v8i* na, fa_v8i* nb, int wn) {
+#pragma unroll
+        for (int i = 0; i < kM4; ++i) {
+          ra[i] = As[oa[i] + wn];
+          rb[i] = Bs[ob[i] + wn];
+        }
+#pragma unroll
+        for (int i = 0; i < kM4; ++i)
+#pragma unroll
+          for (int j = 0; j < kM4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[i], fb[j], acc[i][j], 4, 4, 0, kFp4Scale,
+                                                                        0, kFp4Scale);
+#pragma unroll
+        for (int i = 0; i < kM4; ++i) {
+          na[i] = unpack32_fp4(ra[i]);
+          nb[i] = unpack32_fp4(rb[i]);
+        }
+        // the 8 LDS reads, 3 MFMAs (~100 cycles of matrix work to cover the LDS latency),
+        // then one MFMA and 5 VALU (the unpacking, 7 per operand) at a time
+        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+#pragma unroll
+        for (int q = 3; q < kM4 * kM4; ++q) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+        }
+      };
+#pragma unroll 1
+      for (int w = 0; w < kGW; w += 2) {
+        step(fa0, fb0, fa1, fb1, w + 1);
+        step(fa1, fb1, fa0, fb0, (w + 2) & (kGW - 1));
+      }
+    }
+    if (more) stage(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  if (!live) return;
+#pragma unroll
+  for (int i = 0; i < kM4; ++i)
+#pragma unroll
+    for (int j = 0; j < kM4; ++j)
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        const int row = ti * kMT4 + wr + 32 * i + (g & 3) + 8 * (g >> 2) + 4 * h;
+        const int col = tj * kMT4 + wc + 32 * j + r;
+        const uint32_t v = (uint32_t)(acc[i][j][g] + 0.5f);
+        if (row < col && col < F1 && v) atomicAdd(&out[(int64_t)row * F1 + col], v * scale);
+      }
+}
+
 // ---------------------------------------------------------------------------
 // k >= 3: prefix-shared candidate counting.
 // Workgroup = (super-chunk sc of 256*kWPT words) x (group block gb).  Each thread
@@ -1620,7 +1768,7 @@ FA_API int fa_hip_pair_gram_mfma(const uint64_t* bm, int32_t F1, int64_t Wp, int
   if (fp4) kchunk = std::min<int64_t>(kchunk, (int64_t)1 << 18);   // f32-exact sums: <= 2^24 transactions
   nk = (W + kchunk - 1) / kchunk;
   if (fp4)
-    hipLaunchKernelGGL(k_pair_gram_mfma4<true>, dim3((unsigned)(nk * ntp)), dim3(256), 0, st, bm, F1, Wp, W, nt,
+    hipLaunchKernelGGL(k_pair_gram_fp4, dim3((unsigned)(nk * ntp)), dim3(256), 0, st, bm, F1, Wp, W, nt,
                        ntp, kchunk, out, scale);
   else
     hipLaunchKernelGGL(k_pair_gram_mfma4<false>, dim3((unsigned)(nk * ntp)), dim3(256), 0, st, bm, F1, Wp, W, nt,
