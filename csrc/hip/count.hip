@@ -803,13 +803,35 @@ __global__ __launch_bounds__(256) void k_pairs_emit(const uint32_t* __restrict__
 }
 
 // ---------------------------------------------------------------------------
+// Item-major bitmaps in one of two layouts, word w of item row r at
+//   (w >> 3) * bs + r * rs + (w & 7):
+// row-major [F1][Wp] (rs = Wp, bs = 8) -- the multi-pass levels' -- or 8-word blocks
+// [Wp / 8][F1][8] (rs = 8, bs = 8 F1) -- the Gram's: a Gram stage reads 256 rows x 8
+// words as 16 KB contiguous and the build writes each 64-B block of every row into one
+// 8 F1-word run, where row-major puts those 64 B 12.5 MB apart (T40I10D100M: 512 rows a
+// stage; scripts/microbench/bitmap_fetch.cpp: stage fetches 15.3 -> 7.7 ms, build
+// stores 4.4 -> 2.2 ms).  woff (0..7) starts the view inside a block (weight classes
+// and candidate-mode slices that begin off a block boundary).
+// ---------------------------------------------------------------------------
+struct BmView {
+  const uint64_t* p;
+  int64_t rs, bs;
+  int woff;
+  __device__ __forceinline__ int64_t idx(int row, int64_t w) const {
+    w += woff;
+    return (w >> 3) * bs + (int64_t)row * rs + (w & 7);
+  }
+  __device__ __forceinline__ uint64_t operator()(int row, int64_t w) const { return p[idx(row, w)]; }
+};
+
+// ---------------------------------------------------------------------------
 // k = 2, dense bit-matrix Gram with popcounts.  Tile 64x64 items, K-step 32 words.
 // ---------------------------------------------------------------------------
 constexpr int kGT = 64, kGK = 32, kGS = kGT + 1;   // LDS row stride (u64) breaks bank aliasing
 
 template <bool kWeighted>
 __global__ __launch_bounds__(256) void k_pair_gram_popc(
-    const uint64_t* __restrict__ bm, int32_t F1, int64_t Wp, int64_t W,
+    BmView bm, int32_t F1, int64_t W,
     const int32_t* __restrict__ wword, int nt, int ntp, int64_t kchunk, uint32_t* __restrict__ out) {
   __shared__ uint64_t As[kGK * kGS];
   __shared__ uint64_t Bs[kGK * kGS];
@@ -832,8 +854,8 @@ __global__ __launch_bounds__(256) void k_pair_gram_popc(
       const int r = idx / kGK, k = idx % kGK;
       const int ra = ti * kGT + r, rb = tj * kGT + r;
       const int64_t kk = k0 + k;
-      As[k * kGS + r] = (ra < F1 && kk < k_end) ? bm[(int64_t)ra * Wp + kk] : 0ull;
-      Bs[k * kGS + r] = (rb < F1 && kk < k_end) ? bm[(int64_t)rb * Wp + kk] : 0ull;
+      As[k * kGS + r] = (ra < F1 && kk < k_end) ? bm(ra, kk) : 0ull;
+      Bs[k * kGS + r] = (rb < F1 && kk < k_end) ? bm(rb, kk) : 0ull;
     }
     if (kWeighted && threadIdx.x < kGK) {
       const int64_t kk = k0 + threadIdx.x;
@@ -933,7 +955,7 @@ __device__ __forceinline__ fa_v8i unpack32_fp4(uint32_t x) {
 }
 
 template <bool kFp4>
-__global__ __launch_bounds__(256) void k_pair_gram_mfma4(const uint64_t* __restrict__ bm, int32_t F1, int64_t Wp,
+__global__ __launch_bounds__(256) void k_pair_gram_mfma4(BmView bm, int32_t F1,
                                                          int64_t W, int nt, int ntp, int64_t kchunk,
                                                          uint32_t* __restrict__ out, uint32_t scale) {
   using AccT = std::conditional_t<kFp4, fa_v16f, fa_v16i>;
@@ -962,8 +984,8 @@ __global__ __launch_bounds__(256) void k_pair_gram_mfma4(const uint64_t* __restr
       const int row = idx / kMW, w = idx % kMW;
       const int ra = ti * kMT4 + row, rb = tj * kMT4 + row;
       const int64_t kk = k0 + w;
-      pa[it] = (ra < F1 && kk < k_end) ? bm[(int64_t)ra * Wp + kk] : 0ull;
-      pb[it] = (rb < F1 && kk < k_end) ? bm[(int64_t)rb * Wp + kk] : 0ull;
+      pa[it] = (ra < F1 && kk < k_end) ? bm(ra, kk) : 0ull;
+      pb[it] = (rb < F1 && kk < k_end) ? bm(rb, kk) : 0ull;
     }
   };
   if (k_begin < k_end) fetch(k_begin);
@@ -1045,16 +1067,17 @@ __global__ __launch_bounds__(256) void k_pair_gram_mfma4(const uint64_t* __restr
 //   * the two 32-bit halves of a word sit in separate LDS planes (row stride 9 dwords,
 //     the hi plane 32 dwords off the lo plane mod 64): one conflict-free ds_read_b32 per
 //     operand, no shift;
-//   * the unpacked operands are double-buffered: word w + 1's reads are issued first,
-//     word w's 16 MFMAs follow with w + 1's unpacking interleaved between them
-//     (sched_group_barrier), so the matrix pipe always has the next operands.
+//   * the unpacked operands are double-buffered and the raw words read two words
+//     ahead: word w's 16 MFMAs go out with word w + 1's unpacking interleaved between
+//     them (sched_group_barrier) and word w + 2's LDS reads in front, so neither the
+//     matrix pipe nor the unpacking waits on LDS.
 // The prefetch loads are branch-free (clamped addresses, masked values).
 constexpr int kGW = 8;                       // words per stage
 constexpr int kGRow = kGW + 1;                 // plane row stride (dwords)
 constexpr int kGPl = kMT4 * kGRow + 32;     // plane size (dwords): hi plane = lo + 32 mod 64 banks
 constexpr int kGLd = kMT4 * kGW / 256;       // staged words per thread and operand
 
-__global__ __launch_bounds__(256) void k_pair_gram_fp4(const uint64_t* __restrict__ bm, int32_t F1, int64_t Wp,
+__global__ __launch_bounds__(256) void k_pair_gram_fp4(BmView bm, int32_t F1,
                                                        int64_t W, int nt, int ntp, int64_t kchunk,
                                                        uint32_t* __restrict__ out, uint32_t scale) {
   __shared__ uint32_t S[2][2][2 * kGPl];      // [buffer][A, B][lo plane, hi plane]
@@ -1084,8 +1107,8 @@ __global__ __launch_bounds__(256) void k_pair_gram_fp4(const uint64_t* __restric
       const int ra = ti * kMT4 + row, rb = tj * kMT4 + row;
       const int64_t kk = k0 + w;
       const bool okk = kk < k_end;
-      pa[it] = bm[(int64_t)(ra < F1 ? ra : 0) * Wp + (okk ? kk : k_begin)];
-      pb[it] = bm[(int64_t)(rb < F1 ? rb : 0) * Wp + (okk ? kk : k_begin)];
+      pa[it] = bm(ra < F1 ? ra : 0, okk ? kk : k_begin);
+      pb[it] = bm(rb < F1 ? rb : 0, okk ? kk : k_begin);
       oka |= (uint32_t)(ra < F1 && okk) << it;
       okb |= (uint32_t)(rb < F1 && okk) << it;
     }
@@ -1123,19 +1146,24 @@ __global__ __launch_bounds__(256) void k_pair_gram_fp4(const uint64_t* __restric
       const uint32_t* As = S[buf][0];
       const uint32_t* Bs = S[buf][1];
       fa_v8i fa0[kM4], fb0[kM4], fa1[kM4], fb1[kM4];
-      uint32_t ra[kM4], rb[kM4];
+      uint32_t ra[kM4], rb[kM4], qa[kM4], qb[kM4];   // raw words one and two ahead
 #pragma unroll
       for (int i = 0; i < kM4; ++i) {
         fa0[i] = unpack32_fp4(As[oa[i]]);
         fb0[i] = unpack32_fp4(Bs[ob[i]]);
+        ra[i] = As[oa[i] + 1];
+        rb[i] = Bs[ob[i] + 1];
       }
-      // word w's MFMAs on (fa, fb) with word wn's reads ahead of them and its unpacking
-      // into (na, nb) between them; branch-free: the stage's last step re-reads word 0
-      auto step = [&](fa_v8i* fa, fa_v8i* fb, fa_v8i* na, fa_v8i* nb, int wn) {
+      // word w's MFMAs on (fa, fb), the unpacking of word w + 1 (raw words (ca, cb),
+      // read one step earlier, so it never waits on LDS) into (na, nb) between them,
+      // and the reads of word w + 2 into (la, lb) ahead of them; branch-free: the
+      // stage's last two steps re-read words 0 and 1
+      auto step = [&](fa_v8i* fa, fa_v8i* fb, fa_v8i* na, fa_v8i* nb, const uint32_t* ca, const uint32_t* cb,
+                      uint32_t* la, uint32_t* lb, int wl) {
 #pragma unroll
         for (int i = 0; i < kM4; ++i) {
-          ra[i] = As[oa[i] + wn];
-          rb[i] = Bs[ob[i] + wn];
+          la[i] = As[oa[i] + wl];
+          lb[i] = Bs[ob[i] + wl];
         }
 #pragma unroll
         for (int i = 0; i < kM4; ++i)
@@ -1145,23 +1173,25 @@ __global__ __launch_bounds__(256) void k_pair_gram_fp4(const uint64_t* __restric
                                                                         0, kFp4Scale);
 #pragma unroll
         for (int i = 0; i < kM4; ++i) {
-          na[i] = unpack32_fp4(ra[i]);
-          nb[i] = unpack32_fp4(rb[i]);
+          na[i] = unpack32_fp4(ca[i]);
+          nb[i] = unpack32_fp4(cb[i]);
         }
-        // the 8 LDS reads, 3 MFMAs (~100 cycles of matrix work to cover the LDS latency),
-        // then one MFMA and 5 VALU (the unpacking, 7 per operand) at a time
+        // the 8 LDS reads, then one MFMA and 5 VALU (the unpacking, 7 per operand) at a
+        // time (scripts/microbench/gram_mfma.cpp mode 3: 43.7 cycles per MFMA per SIMD,
+        // MFMA alone 41.4; reads one word ahead with 3 MFMAs in front: 59.0)
         __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
 #pragma unroll
-        for (int q = 3; q < kM4 * kM4; ++q) {
+        for (int q = 1; q < kM4 * kM4; ++q) {
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
           __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
         }
+        __builtin_amdgcn_sched_barrier(0);          // each step its own scheduling region
       };
 #pragma unroll 1
       for (int w = 0; w < kGW; w += 2) {
-        step(fa0, fb0, fa1, fb1, w + 1);
-        step(fa1, fb1, fa0, fb0, (w + 2) & (kGW - 1));
+        step(fa0, fb0, fa1, fb1, ra, rb, qa, qb, (w + 2) & (kGW - 1));
+        step(fa1, fb1, fa0, fb0, qa, qb, ra, rb, (w + 3) & (kGW - 1));
       }
     }
     if (more) stage(buf ^ 1);
@@ -1368,6 +1398,9 @@ __device__ __forceinline__ void slab_build_word(uint64_t* __restrict__ slab, int
 // here every thread issues all its loads (after one batched load of the
 // bitmap row ids) before its first LDS store.  ROWW: LDS row stride in words;
 // kSwz: an XOR of the word slot by ((u << 2) & (SW - 4)) (rotated row layouts).
+// ld > 0: a row-major bitmap of row stride ld; ld < 0: the 8-word block layout of
+// block stride -ld (BmView: the Gram's bitmap, reused by the levels after it; slab
+// starts and word pairs stay inside one block).
 template <int SW, int ROWW, bool kSwz>
 __device__ __forceinline__ void slab_copy_bm(uint4* lds4, int n_used, const uint64_t* __restrict__ bm, int64_t Wp,
                                              const int32_t* __restrict__ bm_rows, int64_t w0, int64_t W) {
@@ -1389,7 +1422,8 @@ __device__ __forceinline__ void slab_copy_bm(uint4* lds4, int n_used, const uint
       v[k] = make_uint4(0, 0, 0, 0);
       // rows are Wp (a multiple of 64) words long and zero past W: a pair whose
       // first word is valid may be read whole
-      if (i < total && w < W) v[k] = *reinterpret_cast<const uint4*>(bm + (size_t)br[k] * Wp + w);
+      const int64_t at = Wp > 0 ? (int64_t)br[k] * Wp + w : (w >> 3) * -Wp + (int64_t)br[k] * 8 + (w & 7);
+      if (i < total && w < W) v[k] = *reinterpret_cast<const uint4*>(bm + at);
     }
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
@@ -1704,7 +1738,8 @@ struct MapIdent {
 template <class Map>
 __global__ __launch_bounds__(256) void k_build_bitmaps_w(const int64_t* __restrict__ roff,
                                                          const int32_t* __restrict__ ranks, int64_t ncols, int F1,
-                                                         int64_t Wp, int WT, uint64_t* __restrict__ bm, Map map) {
+                                                         int64_t rs, int64_t bs, int WT, uint64_t* __restrict__ bm,
+                                                         Map map) {
   extern __shared__ uint64_t btile[];   // [F1][WT]
   __shared__ unsigned long long bwords[4 * 2];
   for (int i = threadIdx.x; i < F1 * WT; i += blockDim.x) btile[i] = 0ull;
@@ -1719,7 +1754,7 @@ __global__ __launch_bounds__(256) void k_build_bitmaps_w(const int64_t* __restri
   const int64_t w0 = (int64_t)blockIdx.x * WT;
   for (int i = threadIdx.x; i < F1 * WT; i += blockDim.x) {
     const int u = i / WT, w = i - u * WT;
-    bm[(int64_t)u * Wp + w0 + w] = btile[i];
+    bm[((w0 + w) >> 3) * bs + (int64_t)u * rs + ((w0 + w) & 7)] = btile[i];
   }
 }
 
@@ -1729,20 +1764,22 @@ using namespace fa;
 
 // Contiguous rows, all F1 output rows in one tile (F1 * WT * 8 B of LDS): the wave
 // build above.  Returns 2 when it does not apply (the caller's thread-per-row kernel).
+// blocked: the 8-word block layout (BmView; Wp a multiple of 8).
 FA_API int fa_hip_build_bitmaps_wave(const int64_t* roff, const int32_t* ranks, int64_t ncols, int32_t F1, int64_t Wp,
-                                     int WT, uint64_t* bm, const int32_t* item_map, hipStream_t st) {
+                                     int WT, uint64_t* bm, const int32_t* item_map, int blocked, hipStream_t st) {
   const size_t lds = (size_t)F1 * WT * 8;
-  if (F1 <= 0 || WT <= 0 || Wp % WT || lds > 64 * 1024) return 2;
+  if (F1 <= 0 || WT <= 0 || Wp % WT || Wp % 8 || lds > 64 * 1024) return 2;
+  const int64_t rs = blocked ? 8 : Wp, bs = blocked ? 8 * (int64_t)F1 : 8;
   dim3 g((unsigned)(Wp / WT));
   if (item_map) {
     (void)hipFuncSetAttribute((const void*)k_build_bitmaps_w<MapGlobal>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
-    hipLaunchKernelGGL(k_build_bitmaps_w<MapGlobal>, g, dim3(256), lds, st, roff, ranks, ncols, F1, Wp, WT, bm,
+    hipLaunchKernelGGL(k_build_bitmaps_w<MapGlobal>, g, dim3(256), lds, st, roff, ranks, ncols, F1, rs, bs, WT, bm,
                        MapGlobal{item_map});
   } else {
     (void)hipFuncSetAttribute((const void*)k_build_bitmaps_w<MapIdent>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
-    hipLaunchKernelGGL(k_build_bitmaps_w<MapIdent>, g, dim3(256), lds, st, roff, ranks, ncols, F1, Wp, WT, bm,
+    hipLaunchKernelGGL(k_build_bitmaps_w<MapIdent>, g, dim3(256), lds, st, roff, ranks, ncols, F1, rs, bs, WT, bm,
                        MapIdent{});
   }
   FA_LAUNCH_RET();
@@ -1753,11 +1790,13 @@ FA_API int fa_hip_build_bitmaps_wave(const int64_t* roff, const int32_t* ranks, 
 // decode of the diagonal tiles: 13.9 / 13.7 / 14.8 / 14.5 ms; with the triangular decode
 // table PairRowsLds::tri the all-tiles form won the headline A/B, 45.5-46.3 vs 47.1-47.3 ms).
 
-// Gram of words [0, W) of bm's rows on the matrix cores, every count multiplied by
-// scale before it is added to out (a weight class of a deduplicated layout: its
-// columns all carry the same weight, FastApriori.scala:233-235).
-FA_API int fa_hip_pair_gram_mfma(const uint64_t* bm, int32_t F1, int64_t Wp, int64_t W, uint32_t* out,
-                                 int target_wgs, uint32_t scale, int fp4, hipStream_t st) {
+// Gram of words [0, W) of the bitmap view (bm, rs, bs, woff: BmView) on the matrix
+// cores, every count multiplied by scale before it is added to out (a weight class of
+// a deduplicated layout: its columns all carry the same weight, FastApriori.scala:233-235).
+FA_API int fa_hip_pair_gram_mfma(const uint64_t* bm, int32_t F1, int64_t rs, int64_t bs, int woff, int64_t W,
+                                 uint32_t* out, int target_wgs, uint32_t scale, int fp4, hipStream_t st) {
+  if (woff < 0 || woff > 7) return -22;
+  const BmView v{bm, rs, bs, woff};
   if (W <= 0 || F1 < 2) return 0;
   const int nt = (F1 + kMT4 - 1) / kMT4;
   const int ntp = nt * (nt + 1) / 2;
@@ -1768,17 +1807,19 @@ FA_API int fa_hip_pair_gram_mfma(const uint64_t* bm, int32_t F1, int64_t Wp, int
   if (fp4) kchunk = std::min<int64_t>(kchunk, (int64_t)1 << 18);   // f32-exact sums: <= 2^24 transactions
   nk = (W + kchunk - 1) / kchunk;
   if (fp4)
-    hipLaunchKernelGGL(k_pair_gram_fp4, dim3((unsigned)(nk * ntp)), dim3(256), 0, st, bm, F1, Wp, W, nt,
+    hipLaunchKernelGGL(k_pair_gram_fp4, dim3((unsigned)(nk * ntp)), dim3(256), 0, st, v, F1, W, nt,
                        ntp, kchunk, out, scale);
   else
-    hipLaunchKernelGGL(k_pair_gram_mfma4<false>, dim3((unsigned)(nk * ntp)), dim3(256), 0, st, bm, F1, Wp, W, nt,
+    hipLaunchKernelGGL(k_pair_gram_mfma4<false>, dim3((unsigned)(nk * ntp)), dim3(256), 0, st, v, F1, W, nt,
                        ntp, kchunk, out, scale);
   FA_LAUNCH_RET();
 }
 
-FA_API int fa_hip_pair_gram_popc(const uint64_t* bm, int32_t F1, int64_t Wp, int64_t W,
+FA_API int fa_hip_pair_gram_popc(const uint64_t* bm, int32_t F1, int64_t rs, int64_t bs, int woff, int64_t W,
                                  const int32_t* wword, uint32_t* out, int target_wgs, hipStream_t st) {
+  if (woff < 0 || woff > 7) return -22;
   if (W <= 0 || F1 < 2) return 0;
+  const BmView v{bm, rs, bs, woff};
   const int nt = (F1 + kGT - 1) / kGT;
   const int ntp = nt * (nt + 1) / 2;
   int64_t nk = std::max<int64_t>(1, (target_wgs + ntp - 1) / ntp);
@@ -1787,9 +1828,9 @@ FA_API int fa_hip_pair_gram_popc(const uint64_t* bm, int32_t F1, int64_t Wp, int
   nk = (W + kchunk - 1) / kchunk;
   dim3 g((unsigned)(nk * ntp));
   if (wword)
-    hipLaunchKernelGGL(k_pair_gram_popc<true>, g, dim3(256), 0, st, bm, F1, Wp, W, wword, nt, ntp, kchunk, out);
+    hipLaunchKernelGGL(k_pair_gram_popc<true>, g, dim3(256), 0, st, v, F1, W, wword, nt, ntp, kchunk, out);
   else
-    hipLaunchKernelGGL(k_pair_gram_popc<false>, g, dim3(256), 0, st, bm, F1, Wp, W, wword, nt, ntp, kchunk, out);
+    hipLaunchKernelGGL(k_pair_gram_popc<false>, g, dim3(256), 0, st, v, F1, W, wword, nt, ntp, kchunk, out);
   FA_LAUNCH_RET();
 }
 

@@ -1366,20 +1366,22 @@ FA_API int fa_hip_dedup_probe(const int64_t* roff, const int32_t* ranks, const i
 
 // Wp must be a multiple of WT.  LDS = R * 2 * WT * 4 bytes.
 FA_API int fa_hip_build_bitmaps_wave(const int64_t* roff, const int32_t* ranks, int64_t ncols, int32_t F1, int64_t Wp,
-                                     int WT, uint64_t* bm, const int32_t* item_map, hipStream_t st);
+                                     int WT, uint64_t* bm, const int32_t* item_map, int blocked, hipStream_t st);
 
 FA_API int fa_hip_build_bitmaps(const int64_t* roff, const int32_t* ranks, const int32_t* src,
                                 int64_t ncols, int32_t F1, int64_t Wp, int WT, int R, uint64_t* bm,
-                                const int32_t* item_map, const int32_t* used, hipStream_t st) {
+                                const int32_t* item_map, const int32_t* used, int blocked, hipStream_t st) {
   if (F1 <= 0 || Wp <= 0) return 0;
   if (Wp % WT) return 1;
   // contiguous rows with every output row in one tile: the wave-cooperative build (count.hip)
   // (T40I10D100M: the full 998-item Gram bitmap 22.8 -> 14.1 ms per build, the used-item
-  // subsets of the multi-pass levels ~1.9 ms)
+  // subsets of the multi-pass levels ~1.9 ms).  blocked (the Gram's 8-word block layout,
+  // count.hip BmView) only there: the caller checks that it applies.
   if (!src && R >= F1) {
-    const int rc = fa_hip_build_bitmaps_wave(roff, ranks, ncols, F1, Wp, WT, bm, item_map, st);
+    const int rc = fa_hip_build_bitmaps_wave(roff, ranks, ncols, F1, Wp, WT, bm, item_map, blocked, st);
     if (rc != 2) return rc;
   }
+  if (blocked) return -22;
   dim3 g((unsigned)(Wp / WT), (unsigned)((F1 + R - 1) / R));
   size_t lds = (size_t)R * 2 * WT * 4;
   hipLaunchKernelGGL(k_build_bitmaps, g, dim3(256), lds, st, roff, ranks, src, ncols, F1, Wp, WT, R, bm, item_map,

@@ -508,7 +508,7 @@ class FastApriori:
             self.stats["device_bitmap_levels"] = self.stats.get("device_bitmap_levels", 0) + 1
             return c, cnt
         with self._timer.phase("count"), roctx_range("count_multi"):
-            bm, bmap = self._bitmaps(v, used)
+            bm, bmap = self._bitmaps(v, used, blocked=True)
             used_t = torch.from_numpy(used.astype(np.int64)).to(self._dev)
             bm_rows = (bmap[used_t] if bmap is not None else used_t).to(torch.int32).contiguous()
             cnt = Pm.dl_count_multipass(S, F1, n_used, C0, lds, v["roff"], v["ranks"], v["src"], v["ncols"],
@@ -1175,7 +1175,7 @@ class FastApriori:
             db.update(src=None, ncols=K)
         self.log.metric(phase="trim", k=k, rows=K, nnz=int(nranks.numel()))
 
-    def _bitmaps(self, db, used: np.ndarray | None = None):
+    def _bitmaps(self, db, used: np.ndarray | None = None, blocked: bool = False):
         """Item-major bitmaps for the current row layout (built once, reused by the Gram
         pair kernel and every multi-pass level until a trim).
 
@@ -1184,13 +1184,19 @@ class FastApriori:
         k+1's candidates are built from F_k, whose items are level-k candidate items),
         so the rows of the next levels are a subset until the layout changes.  Returns
         (bm, bm_map): bm_map is the device rank -> bitmap row map, or None when the
-        bitmap is rank-indexed."""
-        have = db.get("bm_items")
-        if db["bm"] is not None and (have is None or (used is not None and have[used].all())):
-            return db["bm"], db.get("bm_map")
+        bitmap is rank-indexed.  blocked: the caller reads either layout (the Gram and
+        the slab kernels' bitmap copies), and a full bitmap is built in 8-word blocks
+        where the wave build applies (ops.build_bitmaps); count_candidates reads the
+        row-major one, so a blocked bitmap is rebuilt for it."""
+        have, bm = db.get("bm_items"), db["bm"]
+        if bm is not None and (bm.dim() == 2 or blocked) and (have is None or (used is not None and have[used].all())):
+            return bm, db.get("bm_map")
         with roctx_range("bitmaps"):
             if used is None:
-                bm, W = ops.build_bitmaps(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"])
+                blk = (blocked and TUNING.bitmap_blocked and db["ranks"].is_cuda
+                       and ops.primitives.blocked_bitmaps_ok(db["src"], db["F1"], db["ncols"]))
+                bm, W = ops.build_bitmaps(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"], blocked=blk)
+                self.stats["bm_blocked"] = bool(blk)
                 db.update(bm=bm, W=W, bm_items=None, bm_map=None)
             else:
                 dev = db["ranks"].device
@@ -1243,13 +1249,13 @@ class FastApriori:
         # F_2 compacted on the device (no readback before the first device bundle)
         on_dev = self._f2_defer and not rs and db["ranks"].is_cuda
         if strat == "gram":
-            self._bitmaps(db)
+            self._bitmaps(db, blocked=True)
             # candidate parallelism: each rank takes a 32-word-aligned slice of the columns
             W = db["W"]
             w0, w1 = (W * r // nr) // 32 * 32, (W if r == nr - 1 else (W * (r + 1) // nr) // 32 * 32)
             wword = db["wword"][w0:w1] if db["wword"] is not None else None
-            pc = ops.pair_counts_gram(db["bm"][:, w0:], max(w1 - w0, 0), wword,
-                                      self._slice_classes(db.get("wcls"), w0, w1), raw=on_dev)
+            pc = ops.pair_counts_gram(db["bm"], max(w1 - w0, 0), wword,
+                                      self._slice_classes(db.get("wcls"), w0, w1), raw=on_dev, w0=w0)
         else:
             roff, ranks, wrow = db["roff"], db["ranks"], db["wrow"]
             if nr > 1:   # candidate parallelism: each rank takes a slice of the rows
@@ -1472,7 +1478,7 @@ class FastApriori:
         eoff = np.concatenate([[0], np.cumsum(np.concatenate([np.diff(eo) for _, _, _, eo, _ in bundle]))])
         ext = np.concatenate([ex for *_, ex in bundle]).astype(np.int32)
         cnt = ops.count_level(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"], flat, eoff, ext,
-                              db["wword"], kernel="slab", poff=poff, full_bm=lambda u: self._bitmaps(db, u),
+                              db["wword"], kernel="slab", poff=poff, full_bm=lambda u: self._bitmaps(db, u, blocked=True),
                               sup_frac=self.stats["min_count"] / max(1, self.stats["n_lines"]))
         if cnt is None:
             return [self._count_level(full_db, pv, pi, eo, ex) for _, pv, pi, eo, ex in bundle]
@@ -1506,7 +1512,7 @@ class FastApriori:
         lk = self.cfg.level_kernel
         if dev.type == "cuda" and lk in ("auto", "slab"):
             cnt = ops.count_level(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"], prev[prefix_idx],
-                                  ext_off, ext, db["wword"], kernel=lk, full_bm=lambda u: self._bitmaps(db, u),
+                                  ext_off, ext, db["wword"], kernel=lk, full_bm=lambda u: self._bitmaps(db, u, blocked=True),
                                   sup_frac=self.stats["min_count"] / max(1, self.stats["n_lines"]))
             if cnt is not None:
                 self.dcomm.all_reduce_(cnt, bound=self.stats["n_lines"])

@@ -104,13 +104,13 @@ _HIP_SIGS = {
     "fa_hip_compress_lds": (C.c_int, [vp, vp, vp, vp, i64, vp, vp, vp, vp, vp, vp]),
     "fa_hip_dedup_probe": (C.c_int, [vp, vp, vp, i64, vp, vp, vp]),
     "fa_hip_row_hash": (C.c_int, [vp, vp, i64, vp, vp, vp]),
-    "fa_hip_build_bitmaps": (C.c_int, [vp, vp, vp, i64, i32, i64, C.c_int, C.c_int, vp, vp, vp, vp]),
+    "fa_hip_build_bitmaps": (C.c_int, [vp, vp, vp, i64, i32, i64, C.c_int, C.c_int, vp, vp, vp, C.c_int, vp]),
     "fa_hip_block_counts": (C.c_int, [vp, vp, i64, i32, vp, vp, C.c_int, vp]),
     "fa_hip_block_scatter": (C.c_int, [vp, vp, i64, i32, vp, vp, vp, C.c_int, vp]),
     "fa_hip_pair_queue16": (C.c_int, [vp, vp, vp, i64, C.c_int, i64, vp, vp, C.c_int, vp]),
     "fa_hip_pair_blocked": (C.c_int, [vp, vp, vp, i64, vp, i32, vp, i64, vp]),
-    "fa_hip_pair_gram_mfma": (C.c_int, [vp, i32, i64, i64, vp, C.c_int, C.c_uint32, C.c_int, vp]),
-    "fa_hip_pair_gram_popc": (C.c_int, [vp, i32, i64, i64, vp, vp, C.c_int, vp]),
+    "fa_hip_pair_gram_mfma": (C.c_int, [vp, i32, i64, i64, C.c_int, i64, vp, C.c_int, C.c_uint32, C.c_int, vp]),
+    "fa_hip_pair_gram_popc": (C.c_int, [vp, i32, i64, i64, C.c_int, i64, vp, vp, C.c_int, vp]),
     "fa_hip_count_candidates": (C.c_int, [vp, i64, i64, vp, C.c_int, vp, vp, vp, C.c_int, vp, vp, vp]),
     "fa_hip_recommend": (C.c_int, [vp, vp, vp, i64, i32, vp, vp, i64, vp, vp]),
     "fa_hip_recommend_indexed": (C.c_int, [vp, vp, vp, vp, vp, i64, i32, vp, vp, i64, vp, vp]),

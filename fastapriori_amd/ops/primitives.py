@@ -426,19 +426,36 @@ def bitmap_geometry(F1: int, ncols: int) -> tuple[int, int, int, int]:
     return W, Wp, WT, R
 
 
-def build_bitmaps(roff, ranks, src, ncols: int, F1: int, item_map=None, used=None) -> tuple[torch.Tensor, int]:
+def blocked_bitmaps_ok(src, F1: int, ncols: int, item_map=None) -> bool:
+    """The 8-word block layout (count.hip BmView) is built by the wave bitmap build
+    only: contiguous rows, every item row in one LDS tile."""
+    _, Wp, WT, R = bitmap_geometry(F1, ncols)
+    return src is None and item_map is None and 0 < F1 <= R and F1 * WT * 8 <= 64 * 1024 and Wp % 8 == 0
+
+
+def build_bitmaps(roff, ranks, src, ncols: int, F1: int, item_map=None, used=None,
+                  blocked: bool = False) -> tuple[torch.Tensor, int]:
     """Item-major bitmaps [F1, Wp] (int64 words) and the valid word count W.
 
     With ``item_map`` (rank -> row, -1 = skip; device) and ``used`` (sorted ranks of
     the mapped items; device) only those F1 = len(used) rows are built (device only).
+    blocked (device, blocked_bitmaps_ok): the Gram's 8-word block layout instead, a
+    [Wp / 8, F1, 8] tensor (pair_counts_gram reads either).
     """
     W, Wp, WT, R = bitmap_geometry(F1, ncols)
     dev = ranks.device
     if ranks.is_cuda:
+        if blocked:
+            if not blocked_bitmaps_ok(src, F1, ncols, item_map):
+                raise ValueError("blocked bitmaps need the wave build (contiguous rows, one LDS tile)")
+            bm = torch.empty((Wp // 8, F1, 8), dtype=_I64, device=dev)
+            _hip_call("fa_hip_build_bitmaps", _p(roff), _p(ranks), None, ncols, F1, Wp, WT, R, _p(bm),
+                      None, None, 1, _stream(ranks))
+            return bm, W
         bm = torch.empty((max(F1, 1), Wp), dtype=_I64, device=dev)
         if F1 > 0:
             _hip_call("fa_hip_build_bitmaps", _p(roff), _p(ranks), _p(src), ncols, F1, Wp, WT, R, _p(bm),
-                      _p(item_map), _p(used), _stream(ranks))
+                      _p(item_map), _p(used), 0, _stream(ranks))
     else:
         bm = torch.zeros((max(F1, 1), Wp), dtype=_I64)
         if F1 > 0:
@@ -568,30 +585,58 @@ def gram_segments(W: int, weighted: bool, wcls=None, force_popc: bool = False) -
     return segs
 
 
+def to_blocked(bm: torch.Tensor) -> torch.Tensor:
+    """Row-major bitmaps [F1, Wp] -> the 8-word block layout [Wp / 8, F1, 8]."""
+    F1, Wp = bm.shape
+    return bm.reshape(F1, Wp // 8, 8).transpose(0, 1).contiguous()
+
+
+def bitmap_ld(bm) -> int:
+    """The slab kernels' bitmap stride argument (count.hip slab_copy_bm): the row
+    stride of a row-major bitmap, minus the block stride of a blocked one, 0 for none."""
+    if bm is None:
+        return 0
+    return -bm.stride(0) if bm.dim() == 3 else bm.stride(0)
+
+
+def _bm_view(bm: torch.Tensor, w0: int):
+    """(F1, row stride, block stride, base pointer, in-block offset) of word w0 of a
+    row-major [F1, Wp] or blocked [Wp / 8, F1, 8] bitmap (count.hip BmView)."""
+    if bm.dim() == 3:
+        F1, rs, bs = bm.shape[1], 8, bm.stride(0)
+    else:
+        F1, rs, bs = bm.shape[0], bm.stride(0), 8
+    return F1, rs, bs, bm.data_ptr() + 8 * (w0 >> 3) * bs, w0 & 7
+
+
 def pair_counts_gram(bm: torch.Tensor, W: int, wword, wcls=None, force_popc: bool = False,
-                     fp4: bool = True, raw: bool = False) -> torch.Tensor:
-    """Pair supports from the item-major bitmaps over words [0, W) -> int64 [F1, F1]
-    (upper triangle).  Device: the FP4 matrix-core Gram (k_pair_gram_mfma4) per
-    weight class, scaled by the class weight (FastApriori.scala:233-235's weighted
-    sum), short classes by the popcount Gram with per-word weights.  fp4=False: the
-    i8 matrix-core form (kept as a test oracle of the FP4 one)."""
-    F1, Wp = bm.shape[0], bm.stride(0)
+                     fp4: bool = True, raw: bool = False, w0: int = 0) -> torch.Tensor:
+    """Pair supports from the item-major bitmaps over words [w0, w0 + W) -> int64
+    [F1, F1] (upper triangle).  bm: row-major [F1, Wp] or (device) the 8-word block
+    layout [Wp / 8, F1, 8] (build_bitmaps(blocked=True)); wword / wcls cover the W
+    words from w0.  Device: the FP4 matrix-core Gram (k_pair_gram_fp4) per weight
+    class, scaled by the class weight (FastApriori.scala:233-235's weighted sum), short
+    classes by the popcount Gram with per-word weights.  fp4=False: the i8 matrix-core
+    form (kept as a test oracle of the FP4 one)."""
+    F1 = bm.shape[1] if bm.dim() == 3 else bm.shape[0]
     if bm.is_cuda:
         out = torch.zeros((F1, F1), dtype=_I32, device=bm.device)
         if W > 0 and F1 >= 2:
             st = _stream(bm)
             segs = gram_segments(W, wword is not None, wcls, force_popc)
             for a, b, wt in segs:
+                _, rs, bs, ptr, woff = _bm_view(bm, w0 + a)
                 if wt > 0:
-                    _hip_call("fa_hip_pair_gram_mfma", bm.data_ptr() + 8 * a, F1, Wp, b - a, _p(out), 4096, wt,
-                              int(fp4), st)
+                    _hip_call("fa_hip_pair_gram_mfma", ptr, F1, rs, bs, woff, b - a, _p(out), 4096, wt, int(fp4), st)
                 else:
-                    _hip_call("fa_hip_pair_gram_popc", bm.data_ptr() + 8 * a, F1, Wp, b - a,
+                    _hip_call("fa_hip_pair_gram_popc", ptr, F1, rs, bs, woff, b - a,
                               wword.data_ptr() + 4 * a if wword is not None else None, _p(out), 4096, st)
         return out if raw else out.to(_I64)
+    assert bm.dim() == 2, "the blocked bitmap layout is device-only"
     out = torch.zeros((F1, F1), dtype=_I64)
     if W > 0 and F1 >= 2:
-        _native.host().fa_cpu_pair_gram(_p(bm), F1, Wp, W, _p(wword), _p(out), num_threads())
+        bm = bm[:, w0:]
+        _native.host().fa_cpu_pair_gram(_p(bm), F1, bm.stride(0), W, _p(wword), _p(out), num_threads())
     return out
 
 
@@ -920,7 +965,7 @@ def count_level(roff, ranks, src, ncols: int, F1: int, prefix: np.ndarray, ext_o
         n_wg = int(max(1, min(nslabs, 256 * min(max(1, TUNING.slab_lds_bytes // lds), 2))))
         _hip_call("fa_hip_count_slab_rec_cls", _p(roff), _p(ranks), _p(src), ncols, base + 4 * o_im, F1,
                   n_used, base + 4 * o_gpre, base + 4 * (o_rec + 12 * a), b - a, Cq, _p(wword),
-                  out.data_ptr() + 4 * e0, sw, n_wg, _p(bm), bm.stride(0) if bm is not None else 0, st,
+                  out.data_ptr() + 4 * e0, sw, n_wg, _p(bm), bitmap_ld(bm), st,
                   bm_rows, None, int(info[23]) | (2 if dense else 0))
     CLS_LEVELS[0] += int(info[23])
     LAST_LEVEL_PLAN.clear()
@@ -1614,7 +1659,7 @@ def dl_count_multipass(S: DeviceLevelState, F1: int, n_used: int, C: int, lds: i
         n_wg = int(max(1, min(nslabs, 256 * min(max(1, TUNING.slab_lds_bytes // lds_k), 2))))
         _hip_call("fa_hip_count_slab_rec_cls", _p(roff), _p(ranks), _p(src), ncols, _p(item_map), F1, n_used,
                   _p(gpre), _p(rec), 0, w1 - w0, _p(wword), out.data_ptr() + 4 * w0, sw, n_wg, _p(bm),
-                  bm.stride(0), st, _p(bm_rows), _p(S.ctl) + 8 * 221, (2 if dense else 0) | (4 if acc16 else 0))
+                  bitmap_ld(bm), st, _p(bm_rows), _p(S.ctl) + 8 * 221, (2 if dense else 0) | (4 if acc16 else 0))
         npass += 1
     LAST_LEVEL_PLAN.clear()
     LAST_LEVEL_PLAN.update(kernel="slab_dev_multi", rows=int(roff.numel() - 1), used=n_used, sw=sw, cap=cap,

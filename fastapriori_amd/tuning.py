@@ -54,6 +54,7 @@ class Tuning:
     lane_deal_min_rows: int = 1 << 25
     pair_wg: int = 0                    # k_pair_queue16 workgroups (0: one per CU)
     gram_mfma_min_class_words: int = 512   # shorter weight classes: the popcount Gram
+    bitmap_blocked: bool = True         # the Gram's bitmap in 8-word blocks (count.hip BmView)
     # ---- I/O (utils/io.py) -------------------------------------------------------
     gpu_parse: bool = True              # D.dat parsed on the GPU behind the H2D copies
     gpu_parse_dict: bool = True         # dictionary-mode tokens too

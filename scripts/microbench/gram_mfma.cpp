@@ -4,7 +4,9 @@
 //   mode 0: nothing (MFMA only, operands rotated between two register sets)
 //   mode 1: the bits -> e2m1 unpacking of the next word's 8 operands (VALU)
 //   mode 2: mode 1 plus the next word's 8 ds_read_b32
-//   mode 3: mode 2 at two waves per SIMD (128-item tiles, 2 x 4 MFMA tiles per wave)
+//   mode 3: mode 2 with the reads two words ahead (raw words double-buffered), so the
+//           unpacking never waits on LDS
+// at tile 4 x 4 (one wave per SIMD) and 2 x 4 (two waves per SIMD).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o /tmp/gram_mfma gram_mfma.cpp
 // Prints one line per mode: ms, MFMA count, cycles per MFMA per SIMD at the measured clock.
 #include <hip/hip_runtime.h>
@@ -44,17 +46,23 @@ __global__ __launch_bounds__(256, TI == 2 ? 2 : 1) void k_bench(const uint32_t* 
   for (int j = 0; j < 4; ++j) fb0[j] = fb1[j] = unpack(in[lane + 64 * j + 512]);
   uint32_t x = in[lane];
   const int base = (threadIdx.x >> 6) * 1024 + lane * 9;
-  auto step = [&](v8i* fa, v8i* fb, v8i* na, v8i* nb, int w) {
+  uint32_t qa[TI], qb[4];                   // mode 3: the word after next
+#pragma unroll
+  for (int i = 0; i < TI; ++i) qa[i] = ra[i] = in[lane + 64 * i + 1];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) qb[j] = rb[j] = in[lane + 64 * j + 513];
+  auto step = [&](v8i* fa, v8i* fb, v8i* na, v8i* nb, uint32_t* ca, uint32_t* cb, uint32_t* la, uint32_t* lb,
+                  int w) {
     if (MODE >= 2) {
 #pragma unroll
-      for (int i = 0; i < TI; ++i) ra[i] = S[(base + 288 * i + w) & 4095];
+      for (int i = 0; i < TI; ++i) la[i] = S[(base + 288 * i + w) & 4095];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) rb[j] = S[(base + 288 * j + 144 + w) & 4095];
+      for (int j = 0; j < 4; ++j) lb[j] = S[(base + 288 * j + 144 + w) & 4095];
     } else if (MODE == 1) {
 #pragma unroll
-      for (int i = 0; i < TI; ++i) ra[i] = x + (uint32_t)(i * 77 + w);
+      for (int i = 0; i < TI; ++i) la[i] = x + (uint32_t)(i * 77 + w);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) rb[j] = x ^ (uint32_t)(j * 91 + w);
+      for (int j = 0; j < 4; ++j) lb[j] = x ^ (uint32_t)(j * 91 + w);
     }
 #pragma unroll
     for (int i = 0; i < TI; ++i)
@@ -63,24 +71,30 @@ __global__ __launch_bounds__(256, TI == 2 ? 2 : 1) void k_bench(const uint32_t* 
         acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[i], fb[j], acc[i][j], 4, 4, 0, 128, 0, 128);
     if (MODE >= 1) {
 #pragma unroll
-      for (int i = 0; i < TI; ++i) na[i] = unpack(ra[i]);
+      for (int i = 0; i < TI; ++i) na[i] = unpack(ca[i]);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) nb[j] = unpack(rb[j]);
+      for (int j = 0; j < 4; ++j) nb[j] = unpack(cb[j]);
     }
     if (MODE >= 2) {
       __builtin_amdgcn_sched_group_barrier(0x100, TI + 4, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, MODE == 3 ? 1 : 3, 0);
 #pragma unroll
-      for (int q = 3; q < TI * 4; ++q) {
+      for (int q = MODE == 3 ? 1 : 3; q < TI * 4; ++q) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, TI == 4 ? 5 : 6, 0);
       }
     }
   };
 #pragma unroll 1
   for (int it = 0; it < iters; ++it) {
-    step(fa0, fb0, fa1, fb1, 2 * it + 1);
-    step(fa1, fb1, fa0, fb0, 2 * it + 2);
+    if (MODE == 3) {
+      // unpack what the previous step loaded, load the word after next
+      step(fa0, fb0, fa1, fb1, ra, rb, qa, qb, 2 * it + 2);
+      step(fa1, fb1, fa0, fb0, qa, qb, ra, rb, 2 * it + 3);
+    } else {
+      step(fa0, fb0, fa1, fb1, ra, rb, ra, rb, 2 * it + 1);
+      step(fa1, fb1, fa0, fb0, ra, rb, ra, rb, 2 * it + 2);
+    }
     x = x * 1664525u + 1013904223u;
   }
   float s = 0.f;
@@ -132,8 +146,11 @@ int main() {
   run<0, 4>(din, dout, wgs, iters, clk, simds);
   run<1, 4>(din, dout, wgs, iters, clk, simds);
   run<2, 4>(din, dout, wgs, iters, clk, simds);
+  run<3, 4>(din, dout, wgs, iters, clk, simds);
   run<0, 2>(din, dout, wgs * 2, iters, clk, simds);
+  run<1, 2>(din, dout, wgs * 2, iters, clk, simds);
   run<2, 2>(din, dout, wgs * 2, iters, clk, simds);
+  run<3, 2>(din, dout, wgs * 2, iters, clk, simds);
   (void)hipFree(din);
   (void)hipFree(dout);
   return 0;

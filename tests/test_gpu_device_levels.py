@@ -81,6 +81,21 @@ def test_multipass_level_stays_on_device(tune):
     _same(got2, ref)
 
 
+def test_blocked_gram_bitmap_feeds_multipass_levels(tune):
+    # the Gram's full bitmap in 8-word blocks (count.hip BmView) is reused by the
+    # window-by-window levels' slab copies (slab_copy_bm, negative stride): same
+    # results as with the row-major bitmap and the host loop
+    cpu = generate_shard(150_000, Comm(), "cpu", 40.0, 10.0, 2000, 1000, 3)
+    ref, _ = _mine(cpu, 0.006)
+    got, st = _mine(cpu.to(DEV), 0.006, pair_strategy="gram")
+    assert st.get("bm_blocked") and st.get("device_multipass", 0) >= 1, st
+    _same(got, ref)
+    tune(bitmap_blocked=False)
+    got2, st2 = _mine(cpu.to(DEV), 0.006, pair_strategy="gram")
+    assert not st2.get("bm_blocked")
+    _same(got2, ref)
+
+
 def _multipass_lds(ref, accb: int = 4) -> int:
     """An LDS budget in which level 3's used items (at most the items of F_2) fit 4-word
     slabs (slab rows 48 B) with room for ~|F_3| / 4 accumulators of accb bytes: level 3

@@ -131,6 +131,15 @@ def test_bitmaps_pairs_candidates(F1_frac):
     gpg = ops.pair_counts_gram(gbm, gW, None).cpu()
     assert torch.equal(ph, gph)
     assert torch.equal(torch.triu(ph, 1), torch.triu(gpg, 1))
+    if ops.primitives.blocked_bitmaps_ok(None, F1, T):
+        # the Gram's 8-word block layout from the wave build, and the Gram on it
+        bbm, bW = ops.build_bitmaps(roff.to(DEV), ranks.to(DEV), None, T, F1, blocked=True)
+        assert bW == W and torch.equal(bbm.cpu(), ops.primitives.to_blocked(bm))
+        assert torch.equal(torch.triu(ph, 1), torch.triu(ops.pair_counts_gram(bbm, bW, None).cpu(), 1))
+        # a word window off the block boundary (candidate-mode column slices)
+        w0 = min(13, W - 1)
+        part = ops.pair_counts_gram(bbm, W - w0, None, w0=w0).cpu()
+        assert torch.equal(torch.triu(part, 1), torch.triu(ops.pair_counts_gram(bm, W - w0, None, w0=w0), 1))
     # level-3 candidates from the frequent pairs
     iu = torch.triu_indices(F1, F1, 1)
     pc = ph[iu[0], iu[1]]
@@ -486,9 +495,10 @@ def test_apriori_gen_device_matches_host(k):
     assert np.array_equal(got[3], np.concatenate([cand[want[0][g2]], want[2][:, None]], 1))
 
 
+@pytest.mark.parametrize("blocked", [False, True])
 @pytest.mark.parametrize("fp4", [False, True])
 @pytest.mark.parametrize("F1,T", [(37, 5000), (300, 70001), (1000, 9000)])
-def test_pair_gram_mfma_matches_popcount(F1, T, fp4):
+def test_pair_gram_mfma_matches_popcount(F1, T, fp4, blocked):
     # i8 MFMA Gram (v_mfma_i32_32x32x32_i8, the test oracle), and its FP4 form (the
     # product path: v_mfma_scale_f32_32x32x64_f8f6f4 on e2m1 0/1 operands), vs the popcount
     # Gram and a numpy Gram on asymmetric random bitmaps (F1 not a multiple of the 128
@@ -504,6 +514,8 @@ def test_pair_gram_mfma_matches_popcount(F1, T, fp4):
     pad[:, :packed.shape[1]] = packed
     words[:, :W] = pad.view(np.uint64)
     bm = torch.from_numpy(words.view(np.int64)).to(DEV)
+    if blocked:   # the 8-word block layout (count.hip BmView)
+        bm = ops.primitives.to_blocked(bm)
     got = ops.pair_counts_gram(bm, W, None, fp4=fp4).cpu()
     ref = ops.pair_counts_gram(bm, W, None, force_popc=True).cpu()
     want = torch.from_numpy(bits.astype(np.int64) @ bits.astype(np.int64).T)
@@ -512,10 +524,11 @@ def test_pair_gram_mfma_matches_popcount(F1, T, fp4):
     assert torch.equal(ref[iu[0], iu[1]], want[iu[0], iu[1]])
 
 
+@pytest.mark.parametrize("blocked", [False, True])
 @pytest.mark.parametrize("fp4", [False, True])
 @pytest.mark.parametrize("F1,classes", [(300, [(1, 700), (2, 40), (3, 600), (7, 3), (9, 520)]),
                                         (37, [(1, 9), (4, 530)])])
-def test_weighted_gram_mfma_matches_popcount(F1, classes, fp4):
+def test_weighted_gram_mfma_matches_popcount(F1, classes, fp4, blocked):
     # deduplicated layouts: one scaled matrix-core launch per weight class of >= 512
     # words, the short classes by the popcount Gram -- exact against the weighted
     # popcount Gram and a numpy reference (FastApriori.scala:233-235)
@@ -530,6 +543,8 @@ def test_weighted_gram_mfma_matches_popcount(F1, classes, fp4):
     segs = ops.primitives.gram_segments(W, True, wcls)
     assert any(w > 1 for _, _, w in segs) and any(w == 0 for _, _, w in segs)
     bm = torch.from_numpy(words).to(DEV)
+    if blocked:   # classes start off the 8-word blocks (700, 740, ...): the view's woff
+        bm = ops.primitives.to_blocked(bm)
     ww = torch.from_numpy(wword).to(DEV)
     got = ops.pair_counts_gram(bm, W, ww, wcls, fp4=fp4).cpu()
     ref = ops.pair_counts_gram(bm, W, ww, wcls, force_popc=True).cpu()
