@@ -45,6 +45,7 @@ class JobConfig:
     max_level: int = 0
     strategy: str = "count"                     # count | candidate distribution
     world_size: int = 0                         # 0: whatever torchrun started; N: launch / require N ranks
+    tiebreak: str = "string"                    # rank order of equal-count items (utils.jvm.item_tiebreak_key)
     extra: dict = field(default_factory=dict)
 
 
@@ -75,6 +76,10 @@ def build_parser() -> argparse.ArgumentParser:
                    help="number of ranks (one per GPU). Without a torchrun environment the job "
                         "re-launches itself under torch.distributed.run; under torchrun the process "
                         "group must have exactly this many ranks")
+    p.add_argument("--tiebreak", choices=["string", "numeric"], default="string",
+                   help="order of frequent items with equal counts (it orders the tokens inside an itemset "
+                        "line; the reference's Spark order is not reproducible): string = java.lang.String "
+                        "order, numeric = integer tokens by value first")
     return p
 
 
@@ -84,4 +89,4 @@ def parse_args(argv=None) -> JobConfig:
                      dedup=a.dedup, pair_strategy=a.pair_strategy, with_counts=a.with_counts, resume=a.resume,
                      rules_only=a.rules_only, checkpoint=a.checkpoint, overwrite=a.overwrite,
                      profile=a.profile, metrics_path=a.metrics_path, max_level=a.max_level,
-                     strategy=a.strategy, world_size=a.world_size)
+                     strategy=a.strategy, world_size=a.world_size, tiebreak=a.tiebreak)

@@ -37,7 +37,7 @@ from .. import ops
 from ..ops.host import apriori_gen
 from ..parallel.comm import Comm
 from ..tuning import TUNING
-from ..utils.jvm import java_string_key, min_count
+from ..utils.jvm import item_tiebreak_key, min_count
 from ..utils.metrics import Logger, Timer, roctx_range
 from .data import MiningResult, TransactionShard
 
@@ -83,6 +83,7 @@ class MinerConfig:
     trim_min_rows: int = 1 << 20    # no trimming below this many rows (fixed cost > gain)
     timing: str = "off"             # off | events (hipEvent phase times) | sync (host-synchronised phases)
     trace: bool = False             # Chrome trace of the phases in stats["trace"] (--profile)
+    tiebreak: str = "string"        # rank order of equal-count items: string | numeric (utils.jvm.item_tiebreak_key)
     parallelism: str = "count"      # count: rows sharded, counts all-reduced (default)
                                     # candidate: every rank holds the whole DB; pairs split by rows,
                                     #   level candidates split by rank (FastApriori.scala:98-100,140)
@@ -146,6 +147,11 @@ class FastApriori:
         F1 = len(counts1)
         self._F1, self._dev = F1, dev
         self._counts1 = counts1
+        # compression's kernels go out right behind the LUT's copy: the host work below
+        # (result, logs, checkpoint) overlaps them instead of idling the GPU
+        # (the phase's two spans add up: Timer sums spans of one name)
+        with roctx_range("compress"), tm.phase("compress"):
+            cmp_pending = self._compress_start(shard, lut, F1) if F1 >= 2 and TUNING.early_compress else None
         self.log.metric(phase="f1", frequent=F1)
         levels = [np.arange(F1, dtype=np.int32).reshape(-1, 1)]
         counts = [counts1]
@@ -171,7 +177,9 @@ class FastApriori:
             return self._finish(result, t_start)
 
         with roctx_range("compress"), tm.phase("compress"):
-            db = self._compress(shard, lut, F1)
+            if cmp_pending is None and F1 >= 2:
+                cmp_pending = self._compress_start(shard, lut, F1)
+            db = self._compress(shard, lut, F1, cmp_pending)
         self._db_local = db
 
         # ---- k = 2 -----------------------------------------------------
@@ -818,7 +826,7 @@ class FastApriori:
                     if shard.extras.size:
                         hist += torch.bincount(torch.from_numpy(shard.extras.astype(np.int64)), minlength=V).to(dev)
                 comm.all_reduce_(hist)
-                if V <= F1_HIST_READBACK and dev.type == "cuda":
+                if V <= F1_HIST_READBACK and dev.type == "cuda" and self.cfg.tiebreak == "string":
                     # narrow vocabulary: the whole histogram in one readback (no nonzero sync),
                     # ranked and mapped to the LUT in one native call (csrc/host/f1.cpp)
                     hh = np.ascontiguousarray(hist.cpu().numpy(), dtype=np.int64)
@@ -852,11 +860,17 @@ class FastApriori:
             # is the order of (digits left-aligned to 10 places, then length): ties of
             # equal counts sort without building strings ("" = id 0 sorts first)
             fid = np.asarray(fid, dtype=np.int64)
-            v = fid - 1
-            d = np.searchsorted(_POW10, v, side="right") + 1
-            key = v * _POW10_PAD[d]
-            key[fid == 0], d[fid == 0] = -1, 0
-            order = np.lexsort((d, key, -np.asarray(fcnt, dtype=np.int64))) if fid.size else np.zeros(0, np.int64)
+            if self.cfg.tiebreak == "numeric":
+                # integer value (id - 1), the empty token (id 0) after every integer
+                key = np.where(fid == 0, np.iinfo(np.int64).max, fid - 1)
+                order = np.lexsort((key, -np.asarray(fcnt, dtype=np.int64))) if fid.size else np.zeros(0, np.int64)
+            else:
+                v = fid - 1
+                d = np.searchsorted(_POW10, v, side="right") + 1
+                key = v * _POW10_PAD[d]
+                key[fid == 0], d[fid == 0] = -1, 0
+                order = (np.lexsort((d, key, -np.asarray(fcnt, dtype=np.int64))) if fid.size
+                         else np.zeros(0, np.int64))
             ids = fid[order]
             items = _Deferred(lambda: ["" if i == 0 else str(i - 1) for i in ids.tolist()])
             self._deferred.append(items)
@@ -917,7 +931,8 @@ class FastApriori:
             got = torch.stack([sel, hashes_t[sel], hist[sel]]).cpu().numpy()
             sel_np, fh, fc = got[0], got[1], got[2]
             fstr = vocab.decode(sel_np)
-        order = sorted(range(len(fstr)), key=lambda e: (-int(fc[e]), java_string_key(fstr[e])))
+        tb = self.cfg.tiebreak
+        order = sorted(range(len(fstr)), key=lambda e: (-int(fc[e]), item_tiebreak_key(fstr[e], tb)))
         items = [fstr[e] for e in order]
         self._item_hashes = np.asarray(fh, dtype=np.int64)[order].view(np.uint64) if order else \
             np.zeros(0, np.uint64)
@@ -971,16 +986,23 @@ class FastApriori:
     # ------------------------------------------------------------------
     # Compression (FastApriori.scala:66-79) and the vertical layout
     # ------------------------------------------------------------------
-    def _compress(self, shard: TransactionShard, lut: torch.Tensor, F1: int) -> dict:
+    def _compress_start(self, shard: TransactionShard, lut: torch.Tensor, F1: int):
+        """Queue the fused two-pass compression (ops.primitives.compress_rows_start) when
+        it applies; _compress finishes it.  None: _compress runs the general path."""
         dev = shard.items.device
         n_rows = shard.offsets.numel() - 1
         if (dev.type == "cuda" and n_rows > 0 and TUNING.fused_compress
                 and shard.items.numel() <= TUNING.fused_compress_mean_len * n_rows):
-            # fused two-pass path: kept rows, offsets, sorted ranks and the length histogram
             # the dedup estimate's probe rides along with the compression sizes (one readback)
             self._dedup_probe = {} if self.cfg.dedup == "auto" else None
-            kept, roff, ranks, hist_t, bcnt = ops.compress_rows(shard.offsets, shard.items, lut, F1,
-                                                                probe=self._dedup_probe)
+            return ops.primitives.compress_rows_start(shard.offsets, shard.items, lut, F1, probe=self._dedup_probe)
+        return None
+
+    def _compress(self, shard: TransactionShard, lut: torch.Tensor, F1: int, pending=None) -> dict:
+        dev = shard.items.device
+        if pending is not None:
+            # fused two-pass path: kept rows, offsets, sorted ranks and the length histogram
+            kept, roff, ranks, hist_t, bcnt = ops.primitives.compress_rows_finish(pending)
             T = kept.numel()
             hist = np.asarray(hist_t, dtype=np.int64).copy()
         else:

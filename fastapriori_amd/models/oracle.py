@@ -25,7 +25,7 @@ import itertools
 from collections import Counter
 from dataclasses import dataclass, field
 
-from ..utils.jvm import java_split_ws, java_string_key, min_count, rule_tiebreak_key
+from ..utils.jvm import item_tiebreak_key, java_split_ws, java_string_key, min_count, rule_tiebreak_key
 
 
 @dataclass
@@ -38,19 +38,19 @@ class OracleResult:
     rules: list[tuple[frozenset, int, float]] = field(default_factory=list)
 
 
-def rank_items(counts: dict[str, int], mc: int) -> list[str]:
+def rank_items(counts: dict[str, int], mc: int, tiebreak: str = "string") -> list[str]:
     freq = [(t, c) for t, c in counts.items() if c >= mc]
-    freq.sort(key=lambda tc: (-tc[1], java_string_key(tc[0])))
+    freq.sort(key=lambda tc: (-tc[1], item_tiebreak_key(tc[0], tiebreak)))
     return [t for t, _ in freq]
 
 
-def mine(lines: list[list[str]], min_support: float, max_enum_len: int = 16) -> OracleResult:
+def mine(lines: list[list[str]], min_support: float, max_enum_len: int = 16, tiebreak: str = "string") -> OracleResult:
     n = len(lines)
     mc = min_count(min_support, n)
     occ = Counter()
     for toks in lines:
         occ.update(toks)
-    items = rank_items(occ, mc)
+    items = rank_items(occ, mc, tiebreak)
     rank = {t: i for i, t in enumerate(items)}
     itemsets: dict[frozenset, int] = {frozenset([i]): occ[t] for i, t in enumerate(items)}
 
@@ -197,8 +197,8 @@ def mining_log_lines(n_items: int, itemsets) -> list[str]:
     return out
 
 
-def run_oracle(d_lines: list[str], u_lines: list[str], min_support: float):
+def run_oracle(d_lines: list[str], u_lines: list[str], min_support: float, tiebreak: str = "string"):
     D = [java_split_ws(l) for l in d_lines]
     U = [java_split_ws(l) for l in u_lines]
-    res = mine(D, min_support)
+    res = mine(D, min_support, tiebreak=tiebreak)
     return freq_itemset_lines(res), recommend(res, U), res

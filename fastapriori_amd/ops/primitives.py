@@ -260,7 +260,7 @@ DEDUP_PROBE_ROWS = 1 << 18
 
 
 def compress_rows(offsets, items, lut, F1: int, block_counts: bool = True, probe: dict | None = None):
-    """Fused two-pass compression (device, short rows; csrc/hip/prep.hip k_cmp_agg /
+    """compress_rows_finish(compress_rows_start(...)).  Fused two-pass compression (device, short rows; csrc/hip/prep.hip k_cmp_agg /
     k_cmp_emit): returns (kept int32 [T], roff int64 [T+1], ranks int32 [nnz],
     length histogram (host int64 [256]), bcnt) with one host synchronisation.  Rows
     of more than 16 tokens are finished by the register / wave tiers of ``compress``
@@ -274,6 +274,12 @@ def compress_rows(offsets, items, lut, F1: int, block_counts: bool = True, probe
     probe (a dict): also run the dedup probe (prep.hip k_dedup_probe) over the first
     min(T, DEDUP_PROBE_ROWS) rows, read back with the sizes: probe["n"] rows hashed,
     probe["filled"] occupied slots of its 2^22-slot bitmap."""
+    return compress_rows_finish(compress_rows_start(offsets, items, lut, F1, block_counts, probe))
+
+
+def compress_rows_start(offsets, items, lut, F1: int, block_counts: bool = True, probe: dict | None = None) -> dict:
+    """Queue compress_rows' kernels and the copy of its sizes to pinned memory, without
+    waiting: the caller's host work overlaps them until compress_rows_finish."""
     dev = items.device
     n = offsets.numel() - 1
     nwg = (n + 255) // 256
@@ -318,14 +324,32 @@ def compress_rows(offsets, items, lut, F1: int, block_counts: bool = True, probe
                   DEDUP_PROBE_ROWS, _p(occ), _p(tail), st)
     # one readback: sizes, the probe's two counts, the row-length histogram
     hs = hist.sum(0, dtype=_I64)
+    sizes = torch.cat([pre[:, -1], tail, hs] if probe is not None else [pre[:, -1], hs])
+    host = pinned_stage("cmp_sizes")
+    got = host.get(8 * sizes.numel())[:8 * sizes.numel()].view(_I64)
+    got.copy_(sizes, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    host.event = ev
+    return dict(offsets=offsets, items=items, lut=lut, F1=F1, probe=probe, got=got, ev=ev, kept=kept, roff=roff,
+                ranks=ranks, over=over, bcnt=bcnt, lr=lr, lbase=lbase, ovb=ovb, lr_cap=lr_cap, nb=nb, st=st)
+
+
+def compress_rows_finish(c: dict):
+    """Wait for compress_rows_start's sizes and finish: slices, the rows past the emit
+    pass (the later tiers), the block layout."""
+    c["ev"].synchronize()
+    got = c["got"].numpy().copy()
+    probe, nb, st, bcnt, lr = c["probe"], c["nb"], c["st"], c["bcnt"], c["lr"]
+    offsets, items, lut, F1 = c["offsets"], c["items"], c["lut"], c["F1"]
     if probe is not None:
-        got = torch.cat([pre[:, -1], tail, hs]).cpu().numpy()
         probe["filled"], probe["n"] = int(got[3]), int(got[4])
         hist_h = got[5:]
     else:
-        got = torch.cat([pre[:, -1], hs]).cpu().numpy()
         hist_h = got[3:]
     T, nnz, no = int(got[0]), int(got[1]), int(got[2])
+    kept, roff, ranks, over, lbase, ovb, lr_cap = (c[k] for k in ("kept", "roff", "ranks", "over", "lbase", "ovb",
+                                                                   "lr_cap"))
     kept, roff, ranks = kept[:T], roff[:T + 1], ranks[:nnz]
     if bcnt is not None:
         bcnt = bcnt[:nb * T + PAIR_PAD_BATCHES * 64 + 64]

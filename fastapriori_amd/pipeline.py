@@ -68,7 +68,7 @@ def mine_window(cfg: JobConfig, comm, log: Logger, ckpt: Checkpointer | None, su
     summary["read_ms"] = round((time.time() - t_read) * 1000, 1)
     # --profile: hipEvent phase times per level and a Chrome trace of the phases
     mcfg = MinerConfig(min_support=cfg.min_support, dedup=cfg.dedup, pair_strategy=cfg.pair_strategy,
-                       max_level=cfg.max_level, parallelism=cfg.strategy,
+                       max_level=cfg.max_level, parallelism=cfg.strategy, tiebreak=cfg.tiebreak,
                        timing="events" if cfg.profile else "off", trace=cfg.profile)
     miner = FastApriori(cfg.min_support, comm, mcfg, log, ckpt)
     result = miner.run(shard, resume=resume)

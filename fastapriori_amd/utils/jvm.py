@@ -31,6 +31,19 @@ def java_string_key(s: str) -> bytes:
     return s.encode("utf-16-be", "surrogatepass")
 
 
+def item_tiebreak_key(s: str, tiebreak: str = "string"):
+    """Order of frequent items with equal counts (the rank tiebreak).
+    The reference keeps Spark's post-shuffle collect() order, which is not
+    reproducible outside Spark; the rank only orders the tokens inside an itemset line
+    (and so the line sort), never which itemsets, counts or rules come out.
+    "string": java.lang.String order (the default); "numeric": integer tokens by value
+    (Integer.parseInt range), before the other tokens in String order."""
+    if tiebreak == "numeric":
+        v = java_parse_int(s)
+        return (0, v, b"") if v is not None else (1, 0, java_string_key(s))
+    return java_string_key(s)
+
+
 def java_trim(s: str) -> str:
     """``String.trim``: strip every char <= U+0020 from both ends."""
     b, e = 0, len(s)

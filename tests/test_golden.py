@@ -81,3 +81,29 @@ def test_refuses_existing_output(tmp_path):
     cfg.overwrite = True
     run_job(cfg, Comm())
     assert open(tmp_path / "o_recommends" / "part-00000").read() == RECS
+
+
+# equal counts of "9" and "10": String order puts "10" first, the numeric tiebreak "9"
+TIE_D = "9 10\n9 10\n9 10 3\n3\n"
+
+
+@pytest.mark.parametrize("tb,want", [("string", ["10", "9", "3"]), ("numeric", ["9", "10", "3"])])
+def test_tiebreak_orders_equal_counts(tmp_path, tb, want):
+    # --tiebreak: the rank order of equal-count items; the itemsets as token
+    # sets and their counts do not depend on it, only the token order inside a line
+    res = FastApriori(0.5, config=MinerConfig(min_support=0.5, tiebreak=tb)).run(parse_bytes(TIE_D.encode()))
+    assert res.items == want
+    lines, _, ores = run_oracle(TIE_D.splitlines(), [], 0.5, tiebreak=tb)
+    assert ores.items == want
+    sets = {frozenset(l.split()) for l in lines}
+    assert sets == {frozenset(l.split()) for l in run_oracle(TIE_D.splitlines(), [], 0.5)[0]}
+    with open(tmp_path / "D.dat", "w") as f:
+        f.write(TIE_D)
+    with open(tmp_path / "U.dat", "w") as f:
+        f.write("9\n")
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-m", "fastapriori_amd", f"{tmp_path}/", f"{tmp_path}/o_", "--min-support",
+                        "0.5", "--device", "cpu", "--tiebreak", tb], capture_output=True, text=True, env=env,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert open(tmp_path / "o_freqItemset" / "part-00000").read() == "\n".join(lines) + "\n"
