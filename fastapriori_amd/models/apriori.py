@@ -783,9 +783,12 @@ class FastApriori:
             self._ckpt_upto(result, len(result.levels), background=True)
         db = getattr(self, "_db_local", None)
         if db is not None:
-            # layout sizes for the metrics, one collective after the last level
-            g = self.dcomm.all_gather_ints([db["T0"], db["ncols0"]])
-            self.stats.update(T=int(g[:, 0].sum()), distinct=int(g[:, 1].sum()))
+            sizes = getattr(self, "_layout_sizes", None)
+            if sizes is None:
+                # layout sizes for the metrics (deduplicated layouts), one collective after the last level
+                g = self.dcomm.all_gather_ints([db["T0"], db["ncols0"]])
+                sizes = int(g[:, 0].sum()), int(g[:, 1].sum())
+            self.stats.update(T=sizes[0], distinct=sizes[1])
             self._db_local = None
         if len(result.levels) >= 2:
             self._log_tail(result.levels)
@@ -1027,11 +1030,14 @@ class FastApriori:
         db["len_hist"] = hist
         # every rank must take the same layout decisions: long rows, dedup and (when the
         # layout stays undeduplicated) the pair strategy, agreed in one collective
+        # (the kept rows ride along: without dedup they are also the layout's columns,
+        # the run's T / distinct metrics, and _finish needs no collective of its own)
         g = self.dcomm.all_gather_ints([int(hist[255] > 0), int(self._want_dedup(db)),
-                                        int(self._pick_gram_local(db, F1)), db["pair_work"]])
+                                        int(self._pick_gram_local(db, F1)), db["pair_work"], T])
         db["long_rows"] = bool(g[:, 0].max())
         db["pair_work_all"] = int(g[:, 3].sum())      # pair increments of every rank (bounds |F_2|)
         db["pair_pick"] = None
+        self._layout_sizes = None if g[:, 1].max() else (int(g[:, 4].sum()),) * 2
         if g[:, 1].max():
             db["bcnt"] = None
             self._dedup(db)

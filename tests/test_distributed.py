@@ -188,3 +188,22 @@ def test_reduce_scatter_select_ignores_padding(thr):
     for idx, val, full in spawn_local(_rs_select, 3, 10, thr):
         want = [i for i, v in enumerate(full) if v >= thr]
         assert idx == want and val == [full[i] for i in want]
+
+
+@pytest.mark.parametrize("dedup,gathers", [("off", 2), ("on", 3)])
+def test_layout_metrics_ride_on_the_decision_gather(dedup, gathers):
+    # the run's T / distinct metrics come with the compression decisions' all-gather
+    # unless a layout was deduplicated (then _finish gathers the distinct rows)
+    from fastapriori_amd.models.apriori import FastApriori, MinerConfig
+    from fastapriori_amd.parallel.comm import Comm
+    from fastapriori_amd.utils.io import generate_shard
+    from fastapriori_amd.utils.metrics import Logger
+    comm = Comm()
+    calls = []
+    orig = comm.all_gather_ints
+    comm.all_gather_ints = lambda v: calls.append(len(v)) or orig(v)
+    sh = generate_shard(3000, comm, "cpu", 10.0, 4.0, 200, 100, 2)
+    m = FastApriori(0.02, comm, MinerConfig(min_support=0.02, dedup=dedup), Logger(0, enabled=False))
+    m.run(sh)
+    assert len(calls) == gathers, calls
+    assert m.stats["T"] > 0 and 0 < m.stats["distinct"] <= m.stats["T"]

@@ -46,6 +46,8 @@ def test_eight_ranks_default_path_match_one(ref):
         assert o["world"] == 8 and o["sets"] == ref["sets"]
         assert o["bundles"] > 0 and o["f2_dev"] and o["calls"] > 0 and o["bytes"] > 0
         assert not o["fallbacks"]
+        # line total, F1, layout decisions, F_2, one per device bundle (no metrics-only gather)
+        assert o["calls"] <= 4 + o["bundles"], o
 
 
 def test_eight_ranks_pair_reduce_scatter_match_one(ref):
