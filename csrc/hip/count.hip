@@ -1473,7 +1473,7 @@ __device__ __forceinline__ int u16_at(const int4& v, int k) {
   return (k & 1) ? (int)((uint32_t)w >> 16) : (w & 0xFFFF);
 }
 
-template <int SW, bool kWeighted, int kBuild, bool kCls = false>
+template <int SW, bool kWeighted, int kBuild, bool kCls = false, bool kAcc16 = false>
 __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
     const int64_t* __restrict__ roff, const int32_t* __restrict__ ranks, const int32_t* __restrict__ src,
     int64_t ncols, const int32_t* __restrict__ item_map, int F1, int n_used, const int32_t* __restrict__ gpre,
@@ -1487,10 +1487,11 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
   constexpr int SWP = SW + 2;                       // row stride: odd number of 16-B slots
   constexpr int RS = SWP / 2;
   uint64_t* slab = reinterpret_cast<uint64_t*>(lds4);
-  // flags & 8: two u16 counters per accumulator word (unit weights; twice the candidates
-  // per accumulator pass), drained into the u32 global counts before they can carry: a
-  // slab adds at most SW * 64 to a counter
-  const bool acc16 = !kWeighted && (flags & 8) != 0;
+  // kAcc16 (flags & 8): two u16 counters per accumulator word (unit weights; twice the
+  // candidates per accumulator pass), drained into the u32 global counts before they can
+  // carry: a slab adds at most SW * 64 to a counter.  A template parameter: a runtime
+  // flag put a scalar branch pair around every accumulator add of the extension loop.
+  constexpr bool acc16 = !kWeighted && kAcc16;
   const int nacc = acc16 ? (C + 1) >> 1 : C;
   constexpr int kFlush16 = 65535 / (SW * 64);
   uint32_t* acc = reinterpret_cast<uint32_t*>(slab + (size_t)n_used * SWP);
@@ -1883,9 +1884,12 @@ FA_API int fa_hip_count_slab_rec_cls(const int64_t* roff, const int32_t* ranks, 
                          const int32_t*, const int4*, int, int, const int32_t*, uint32_t*, const uint64_t*, int64_t,
                          const int32_t*, int, const int32_t*);
   KernT kern = nullptr;
-#define FA_REC_MODE(S, B)                                                                     \
-  kern = wword ? (KernT)k_count_slab_rec<S, true, B>                                          \
-               : (cls & 1) ? (KernT)k_count_slab_rec<S, false, B, true> : (KernT)k_count_slab_rec<S, false, B>;
+#define FA_REC_MODE(S, B)                                                                              \
+  kern = wword ? (KernT)k_count_slab_rec<S, true, B>                                                   \
+         : (cls & 1) ? (acc16 ? (KernT)k_count_slab_rec<S, false, B, true, true>                       \
+                              : (KernT)k_count_slab_rec<S, false, B, true, false>)                      \
+                     : (acc16 ? (KernT)k_count_slab_rec<S, false, B, false, true>                      \
+                              : (KernT)k_count_slab_rec<S, false, B, false, false>);
 #define FA_REC_CASE(S)                                    \
   if (sw == S) {                                          \
     if (bm) { FA_REC_MODE(S, kBuildBM) }                  \
