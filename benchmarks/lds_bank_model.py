@@ -33,12 +33,12 @@ GROUPS = [[*range(0, 4), *range(12, 16), *range(20, 28)], [*range(4, 12), *range
 GROUPS += [[x + 32 for x in g] for g in GROUPS]
 
 
-def mine(n: int, ms: float):
+def mine(n: int, ms: float, avg_len: float = 10.0, pat: float = 4.0):
     from fastapriori_amd.models.apriori import FastApriori, MinerConfig
     from fastapriori_amd.parallel.comm import Comm
     from fastapriori_amd.utils.io import generate_shard
     from fastapriori_amd.utils.metrics import Logger
-    sh = generate_shard(n, Comm(), "cpu", 10.0, 4.0, 2000, 1000, 1)
+    sh = generate_shard(n, Comm(), "cpu", avg_len, pat, 2000, 1000, 1)
     res = FastApriori(ms, config=MinerConfig(min_support=ms), logger=Logger(0, enabled=False)).run(sh)
     return res
 
@@ -174,9 +174,10 @@ def main():
     ap.add_argument("--ms", type=float, default=0.001)
     ap.add_argument("--sw", type=int, default=8)
     ap.add_argument("--levels", default="3,4")
+    ap.add_argument("--t40", action="store_true", help="T40I10 shape (|T| = 40, |I| = 10)")
     a = ap.parse_args()
     rs = (a.sw + 2) // 2
-    res = mine(a.n, a.ms)
+    res = mine(a.n, a.ms, *((40.0, 10.0) if a.t40 else (10.0, 4.0)))
     c1 = np.asarray(res.counts[0])
     for k in map(int, a.levels.split(",")):
         if k - 2 >= len(res.levels):
