@@ -1736,20 +1736,27 @@ struct MapIdent {
   __device__ __forceinline__ int operator()(int r) const { return r; }
 };
 
+// 16 waves (the tile allows 2 workgroups per CU): at WT = 8 two waves split each word's
+// rows (T40I10D100M full build 12.5 ms at 4 waves, 8.3 at 8)
+constexpr int kBwThreads = 1024;
+
 template <class Map>
-__global__ __launch_bounds__(256) void k_build_bitmaps_w(const int64_t* __restrict__ roff,
+__global__ __launch_bounds__(kBwThreads) void k_build_bitmaps_w(const int64_t* __restrict__ roff,
                                                          const int32_t* __restrict__ ranks, int64_t ncols, int F1,
                                                          int64_t rs, int64_t bs, int WT, uint64_t* __restrict__ bm,
                                                          Map map) {
   extern __shared__ uint64_t btile[];   // [F1][WT]
-  __shared__ unsigned long long bwords[4 * 2];
+  __shared__ unsigned long long bwords[kBwThreads / 64 * 2];
   for (int i = threadIdx.x; i < F1 * WT; i += blockDim.x) btile[i] = 0ull;
   __syncthreads();
   const int wv = threadIdx.x >> 6;
-  for (int q = wv; q < WT; q += 4) {
+  constexpr int NW = kBwThreads / 64;
+  const int nsub = NW > WT ? NW / WT : 1;            // waves per word (WT divides NW or NW divides WT)
+  for (int q = wv / nsub; q < WT; q += NW / nsub) {
     const int64_t col0 = ((int64_t)blockIdx.x * WT + q) * 64;
     if (col0 < ncols)
-      slab_build_word_span(btile, WT, q, word_span(roff, col0, ncols), ranks, map, 0, 1, bwords + wv * 2, 0);
+      slab_build_word_span(btile, WT, q, word_span(roff, col0, ncols), ranks, map, wv % nsub, nsub, bwords + wv * 2,
+                           0);
   }
   __syncthreads();
   const int64_t w0 = (int64_t)blockIdx.x * WT;
@@ -1775,12 +1782,12 @@ FA_API int fa_hip_build_bitmaps_wave(const int64_t* roff, const int32_t* ranks, 
   if (item_map) {
     (void)hipFuncSetAttribute((const void*)k_build_bitmaps_w<MapGlobal>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
-    hipLaunchKernelGGL(k_build_bitmaps_w<MapGlobal>, g, dim3(256), lds, st, roff, ranks, ncols, F1, rs, bs, WT, bm,
+    hipLaunchKernelGGL(k_build_bitmaps_w<MapGlobal>, g, dim3(kBwThreads), lds, st, roff, ranks, ncols, F1, rs, bs, WT, bm,
                        MapGlobal{item_map});
   } else {
     (void)hipFuncSetAttribute((const void*)k_build_bitmaps_w<MapIdent>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
-    hipLaunchKernelGGL(k_build_bitmaps_w<MapIdent>, g, dim3(256), lds, st, roff, ranks, ncols, F1, rs, bs, WT, bm,
+    hipLaunchKernelGGL(k_build_bitmaps_w<MapIdent>, g, dim3(kBwThreads), lds, st, roff, ranks, ncols, F1, rs, bs, WT, bm,
                        MapIdent{});
   }
   FA_LAUNCH_RET();
