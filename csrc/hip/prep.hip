@@ -255,15 +255,18 @@ constexpr int kCSpan = 8192;
 
 // SPAN = staged input tokens per workgroup (32 KB at N = 16; 64 KB for the
 // 64-token tier of long-ish rows, e.g. T40I10's 40-token transactions, whose
-// 256-row spans do not fit 8192 and would otherwise be gathered row by row)
-template <int N, int SPAN = kCSpan>
+// 256-row spans do not fit 8192 and would otherwise be gathered row by row).
+// BT = uint16_t (ranks < 0xFFFF, the caller's check): the span at half the LDS, so
+// twice the workgroups per CU (the 64 KB u32 span allowed two, 8 waves per CU).
+template <int N, int SPAN = kCSpan, typename BT = uint32_t>
 __global__ __launch_bounds__(256) void k_compress_staged(
     const int64_t* __restrict__ off, const int32_t* __restrict__ items, const int32_t* __restrict__ lut,
     int64_t T, const int32_t* __restrict__ kept, const int64_t* __restrict__ roff,
     int32_t* __restrict__ ranks, int8_t* __restrict__ over_flag) {
   constexpr int kCSpan = SPAN;
   constexpr int kCPer = kCSpan / 256;   // span elements per thread, loaded with full ILP
-  __shared__ uint32_t buf[kCSpan];
+  constexpr BT kNone = (BT)~(BT)0;      // not frequent: sorts last
+  __shared__ BT buf[kCSpan];
   const int64_t x0 = (int64_t)blockIdx.x * blockDim.x;
   const int64_t x1 = min(T, x0 + (int64_t)blockDim.x);
   const int64_t x = x0 + threadIdx.x;
@@ -292,7 +295,7 @@ __global__ __launch_bounds__(256) void k_compress_staged(
 #pragma unroll
     for (int k = 0; k < kCPer; ++k) {
       const int64_t i = threadIdx.x + k * 256;
-      if (i < n_in) buf[i] = v[k] < 0 ? 0xFFFFFFFFu : (uint32_t)v[k];
+      if (i < n_in) buf[i] = v[k] < 0 ? kNone : (BT)v[k];
     }
   }
   __syncthreads();
@@ -305,7 +308,7 @@ __global__ __launch_bounds__(256) void k_compress_staged(
     for (int j = 0; j < N; ++j) {
       uint32_t v = 0xFFFFFFFFu;
       if (j < L) {
-        if (staged) v = buf[s - base + j];
+        if (staged) { const BT b = buf[s - base + j]; v = b == kNone ? 0xFFFFFFFFu : (uint32_t)b; }
         else { const int32_t r = lut[items[s + j]]; v = r < 0 ? 0xFFFFFFFFu : (uint32_t)r; }
       }
       a[j] = v;
@@ -318,7 +321,7 @@ __global__ __launch_bounds__(256) void k_compress_staged(
 #pragma unroll
     for (int j = 0; j < N; ++j)
       if (j < c) {
-        if (staged) buf[o + j] = a[j];
+        if (staged) buf[o + j] = (BT)a[j];
         else ranks[obase + o + j] = (int32_t)a[j];
       }
   }
@@ -1315,12 +1318,18 @@ FA_API int fa_hip_compress_staged(const int64_t* off, const int32_t* items, cons
 
 // 64-token staged tier for long-ish rows (64 KB input span per workgroup); rows
 // longer than 64 tokens are flagged for the wave / LDS tiers
+// F1 < 0xFFFF (ranks fit u16): the span staged as u16
 FA_API int fa_hip_compress_staged64(const int64_t* off, const int32_t* items, const int32_t* lut, int64_t T,
                                     const int32_t* kept, const int64_t* roff, int32_t* ranks, int8_t* over_flag,
-                                    hipStream_t st) {
+                                    int F1, hipStream_t st) {
   if (T <= 0) return 0;
-  hipLaunchKernelGGL((k_compress_staged<64, 16384>), dim3((unsigned)((T + 255) / 256)), dim3(256), 0, st, off, items,
-                     lut, T, kept, roff, ranks, over_flag);
+  const dim3 g((unsigned)((T + 255) / 256));
+  if (F1 > 0 && F1 < 0xFFFF)
+    hipLaunchKernelGGL((k_compress_staged<64, 16384, uint16_t>), g, dim3(256), 0, st, off, items, lut, T, kept, roff,
+                       ranks, over_flag);
+  else
+    hipLaunchKernelGGL((k_compress_staged<64, 16384>), g, dim3(256), 0, st, off, items, lut, T, kept, roff, ranks,
+                       over_flag);
   FA_LAUNCH_RET();
 }
 

@@ -83,7 +83,7 @@ _HIP_SIGS = {
     "fa_hip_block_counts_rows": (C.c_int, [vp, vp, vp, i64, vp, i64, C.c_int, vp, vp]),
     "fa_hip_block_bsum": (C.c_int, [vp, i64, i64, C.c_int, vp, vp]),
     "fa_hip_compress_staged": (C.c_int, [vp, vp, vp, i64, vp, vp, vp, vp, vp]),
-    "fa_hip_compress_staged64": (C.c_int, [vp, vp, vp, i64, vp, vp, vp, vp, vp]),
+    "fa_hip_compress_staged64": (C.c_int, [vp, vp, vp, i64, vp, vp, vp, vp, C.c_int, vp]),
     "fa_hip_count_slab_rec": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, C.c_int, vp, vp, C.c_int, C.c_int, vp, vp,
                                         C.c_int, C.c_int, vp, i64, vp, vp, vp]),
     "fa_hip_count_slab_rec_cls": (C.c_int, [vp, vp, vp, i64, vp, C.c_int, C.c_int, vp, vp, C.c_int, C.c_int, vp,

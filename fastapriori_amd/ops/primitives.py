@@ -208,8 +208,12 @@ def compress(offsets, items, lut, kept, roff, F1: int | None = None) -> torch.Te
     flag = torch.empty(T, dtype=torch.int8, device=items.device)
     # long-ish rows (mean > COMPRESS_STAGED64_MEAN_LEN tokens): the 64-token staged tier first
     staged64 = items.numel() > COMPRESS_STAGED64_MEAN_LEN * max(offsets.numel() - 1, 1)
-    _hip_call("fa_hip_compress_staged64" if staged64 else "fa_hip_compress_staged", _p(offsets), _p(items), _p(lut),
-              T, _p(kept), _p(roff), _p(ranks), _p(flag), st)
+    if staged64:   # (F1 unknown: the u32 span)
+        _hip_call("fa_hip_compress_staged64", _p(offsets), _p(items), _p(lut), T, _p(kept), _p(roff), _p(ranks),
+                  _p(flag), int(F1 or 0), st)
+    else:
+        _hip_call("fa_hip_compress_staged", _p(offsets), _p(items), _p(lut), T, _p(kept), _p(roff), _p(ranks),
+                  _p(flag), st)
     over = torch.nonzero(flag).flatten().to(_I32)
     n1 = over.numel()
     over2, n2 = over, n1                 # after the 64-token staged tier: rows of > 64 tokens
