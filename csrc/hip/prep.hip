@@ -15,16 +15,21 @@ namespace fa {
 // ---------------------------------------------------------------------------
 constexpr int kLdsBins = 16384;
 
+// The LDS bins are dynamic: V * nrep words, so a T10-scale vocabulary (V ~ 1000) leaves
+// room for many workgroups per CU (a static 64 KB array allowed two).  nrep = 4 gives each
+// wave its own copy of the bins when they fit, so the four waves' atomics never collide.
 template <bool kLds, bool kVec>
 __global__ __launch_bounds__(256) void k_histogram(const int32_t* __restrict__ items, int64_t nnz,
-                                                   int32_t V, uint32_t* __restrict__ counts) {
-  __shared__ uint32_t sh[kLds ? kLdsBins : 1];
+                                                   int32_t V, int nrep, uint32_t* __restrict__ counts) {
+  extern __shared__ uint32_t sh[];
+  uint32_t* mine = sh;
   if (kLds) {
-    for (int i = threadIdx.x; i < V; i += blockDim.x) sh[i] = 0;
+    for (int i = threadIdx.x; i < V * nrep; i += blockDim.x) sh[i] = 0;
+    mine = sh + (nrep > 1 ? (threadIdx.x >> 6) % nrep : 0) * V;
     __syncthreads();
   }
   auto add = [&](int32_t v) {
-    if (kLds) atomicAdd(&sh[v], 1u); else atomicAdd(&counts[v], 1u);
+    if (kLds) atomicAdd(&mine[v], 1u); else atomicAdd(&counts[v], 1u);
   };
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -37,8 +42,11 @@ __global__ __launch_bounds__(256) void k_histogram(const int32_t* __restrict__ i
   for (int64_t i = (n4 << 2) + gid; i < nnz; i += stride) add(items[i]);
   if (kLds) {
     __syncthreads();
-    for (int i = threadIdx.x; i < V; i += blockDim.x)
-      if (sh[i]) atomicAdd(&counts[i], sh[i]);
+    for (int i = threadIdx.x; i < V; i += blockDim.x) {
+      uint32_t c = 0;
+      for (int r = 0; r < nrep; ++r) c += sh[r * V + i];
+      if (c) atomicAdd(&counts[i], c);
+    }
   }
 }
 
@@ -1162,11 +1170,13 @@ FA_API int fa_hip_histogram(const int32_t* items, int64_t nnz, int32_t V, uint32
   const bool aligned = ((uintptr_t)items & 15) == 0;
   dim3 g((unsigned)blocks), b(256);
   if (V <= kLdsBins) {
-    if (aligned) hipLaunchKernelGGL((k_histogram<true, true>), g, b, 0, st, items, nnz, V, counts);
-    else hipLaunchKernelGGL((k_histogram<true, false>), g, b, 0, st, items, nnz, V, counts);
+    const int nrep = V * 4 <= kLdsBins / 4 ? 4 : 1;   // per-wave copies while they stay <= 16 KB
+    const size_t lds = (size_t)V * nrep * 4;
+    if (aligned) hipLaunchKernelGGL((k_histogram<true, true>), g, b, lds, st, items, nnz, V, nrep, counts);
+    else hipLaunchKernelGGL((k_histogram<true, false>), g, b, lds, st, items, nnz, V, nrep, counts);
   } else {
-    if (aligned) hipLaunchKernelGGL((k_histogram<false, true>), g, b, 0, st, items, nnz, V, counts);
-    else hipLaunchKernelGGL((k_histogram<false, false>), g, b, 0, st, items, nnz, V, counts);
+    if (aligned) hipLaunchKernelGGL((k_histogram<false, true>), g, b, 0, st, items, nnz, V, 1, counts);
+    else hipLaunchKernelGGL((k_histogram<false, false>), g, b, 0, st, items, nnz, V, 1, counts);
   }
   FA_LAUNCH_RET();
 }
