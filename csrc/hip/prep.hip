@@ -474,33 +474,99 @@ constexpr int kProbeBits = 1 << 22;
 // rows are finished by later tiers); hashed counts them.
 constexpr int kCmpProbeLen = 16;
 
+// Pass 1 (thread per row): the row's slot, or kNoSlot (past T, or a row longer than
+// kCmpProbeLen), and the workgroup's hashed-row count -- plain stores: 2^18 scattered
+// atomicOr into a 512 KB global bitmap cost ~58 us (device-scope atomics are served
+// behind the XCDs' L2s), more than all the hashing.
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+constexpr int kProbeRange = 1 << 16;                 // slots per pass-2 workgroup (8 KB of LDS)
+
 __global__ __launch_bounds__(256) void k_dedup_probe(const int64_t* __restrict__ roff,
                                                      const int32_t* __restrict__ ranks,
                                                      const int64_t* __restrict__ T_dev, int64_t n_max,
-                                                     uint32_t* __restrict__ occ,
-                                                     unsigned long long* __restrict__ hashed) {
+                                                     uint32_t* __restrict__ slots, uint32_t* __restrict__ part) {
   const int64_t n = min(T_dev[0], n_max);
-  uint32_t mine = 0;
-  for (int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x; x < n; x += (int64_t)gridDim.x * 256) {
+  const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  uint32_t slot = kNoSlot;
+  if (x < n) {
     const int64_t s = roff[x], e = roff[x + 1];
-    if (e - s > kCmpProbeLen) continue;
-    uint64_t a = 0x243F6A8885A308D3ull;
-    for (int64_t i = s; i < e; ++i) a = dmix64(a ^ (uint64_t)(uint32_t)ranks[i]);
-    a = dmix64(a ^ (uint64_t)(e - s));
-    const uint32_t slot = (uint32_t)((a >> 1) & (kProbeBits - 1));      // = (h1 of k_row_hash) mod 2^22
-    atomicOr(&occ[slot >> 5], 1u << (slot & 31));
-    ++mine;
+    const int L = (int)(e - s);
+    if (L <= kCmpProbeLen) {
+      uint32_t v[kCmpProbeLen];
+#pragma unroll
+      for (int j = 0; j < kCmpProbeLen; ++j) v[j] = j < L ? (uint32_t)ranks[s + j] : 0u;
+      uint64_t a = 0x243F6A8885A308D3ull;
+#pragma unroll
+      for (int j = 0; j < kCmpProbeLen; ++j)
+        if (j < L) a = dmix64(a ^ (uint64_t)v[j]);
+      a = dmix64(a ^ (uint64_t)L);
+      slot = (uint32_t)((a >> 1) & (kProbeBits - 1));      // = (h1 of k_row_hash) mod 2^22
+    }
   }
-  mine = wave_sum_u32(mine);
-  if ((threadIdx.x & 63) == 0 && mine) atomicAdd(hashed, (unsigned long long)mine);
+  if (x < n_max) slots[x] = slot;
+  __shared__ uint32_t wsum[4];
+  const uint32_t c = wave_sum_u32(slot != kNoSlot ? 1u : 0u);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
 }
 
-__global__ __launch_bounds__(256) void k_popcount_sum(const uint32_t* __restrict__ w, int64_t n,
+// Pass 2: workgroup j owns slots [j * kProbeRange, (j + 1) * kProbeRange) as an LDS
+// bitmap, marks the slots of every hashed row that fall in it, and adds its occupied
+// count (one atomic per workgroup); workgroup 0 also sums pass 1's row counts.
+// out[0]: occupied slots, out[1]: hashed rows (out[0] zeroed by the caller).
+__global__ __launch_bounds__(1024) void k_probe_count(const uint32_t* __restrict__ slots, int64_t n_max,
+                                                      const uint32_t* __restrict__ part, int nparts,
                                                       unsigned long long* __restrict__ out) {
-  uint32_t c = 0;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) c += __popc(w[i]);
+  __shared__ uint32_t bits[kProbeRange / 32];
+  __shared__ uint32_t wsum[16];
+  for (int i = threadIdx.x; i < kProbeRange / 32; i += 1024) bits[i] = 0u;
+  __syncthreads();
+  const uint32_t lo = (uint32_t)blockIdx.x * kProbeRange;
+  const uint4* s4 = reinterpret_cast<const uint4*>(slots);
+  const int64_t n4 = n_max >> 2;
+  auto mark = [&](uint32_t v) {
+    const uint32_t d = v - lo;                       // kNoSlot and other ranges: d >= kProbeRange
+    if (d < (uint32_t)kProbeRange) atomicOr(&bits[d >> 5], 1u << (d & 31));
+  };
+  // eight 16-B loads in flight per thread (the pass streams 4 B per probed row per workgroup)
+  constexpr int U = 8;
+  int64_t i = threadIdx.x;
+  for (; i + (U - 1) * 1024 < n4; i += U * 1024) {
+    uint4 v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) v[k] = s4[i + k * 1024];
+#pragma unroll
+    for (int k = 0; k < U; ++k) { mark(v[k].x); mark(v[k].y); mark(v[k].z); mark(v[k].w); }
+  }
+  for (; i < n4; i += 1024) {
+    const uint4 v = s4[i];
+    mark(v.x); mark(v.y); mark(v.z); mark(v.w);
+  }
+  for (int64_t j = (n4 << 2) + threadIdx.x; j < n_max; j += 1024) mark(slots[j]);
+  __syncthreads();
+  uint32_t c = 0, h = 0;
+  for (int i = threadIdx.x; i < kProbeRange / 32; i += 1024) c += __popc(bits[i]);
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i < nparts; i += 1024) h += part[i];
   c = wave_sum_u32(c);
-  if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, (unsigned long long)c);
+  h = wave_sum_u32(h);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) wsum[w] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int k = 0; k < 16; ++k) t += wsum[k];
+    if (t) atomicAdd(out, (unsigned long long)t);
+  }
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) wsum[w] = h;
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int k = 0; k < 16; ++k) t += wsum[k];
+    out[1] = t;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1373,13 +1439,16 @@ FA_API int fa_hip_row_hash(const int64_t* roff, const int32_t* ranks, int64_t T,
   FA_LAUNCH_RET();
 }
 
-// occ: 2^17 zeroed u32 words; tail: two zeroed int64 (marked slots, hashed rows)
+// ws: u32 [n_max + ceil(n_max / 256)] scratch (no zeroing); tail: int64 [2] (marked
+// slots, hashed rows), tail[0] zeroed
 FA_API int fa_hip_dedup_probe(const int64_t* roff, const int32_t* ranks, const int64_t* T_dev, int64_t n_max,
-                              uint32_t* occ, unsigned long long* tail, hipStream_t st) {
+                              uint32_t* ws, unsigned long long* tail, hipStream_t st) {
   if (n_max <= 0) return 0;
-  hipLaunchKernelGGL(k_dedup_probe, dim3((unsigned)std::min<int64_t>((n_max + 255) / 256, 4096)), dim3(256), 0, st,
-                     roff, ranks, T_dev, n_max, occ, tail + 1);
-  hipLaunchKernelGGL(k_popcount_sum, dim3(128), dim3(256), 0, st, occ, (int64_t)(kProbeBits / 32), tail);
+  if (n_max > (int64_t)1 << 24) return 1;
+  const int nparts = (int)((n_max + 255) / 256);
+  uint32_t* part = ws + n_max;
+  hipLaunchKernelGGL(k_dedup_probe, dim3((unsigned)nparts), dim3(256), 0, st, roff, ranks, T_dev, n_max, ws, part);
+  hipLaunchKernelGGL(k_probe_count, dim3(kProbeBits / kProbeRange), dim3(1024), 0, st, ws, n_max, part, nparts, tail);
   FA_LAUNCH_RET();
 }
 

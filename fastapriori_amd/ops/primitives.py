@@ -322,10 +322,11 @@ def compress_rows_start(offsets, items, lut, F1: int, block_counts: bool = True,
     if probe is not None:
         # the kernel reads T = pre[0, -1] on the device and hashes the rows the emit
         # pass has finished (<= 16 items; the later tiers write the longer ones)
-        occ = torch.zeros(1 << 17, dtype=_I32, device=dev)
+        # scratch: the rows' slots + per-workgroup row counts (prep.hip, no zeroing)
+        ws = torch.empty(DEDUP_PROBE_ROWS + (DEDUP_PROBE_ROWS + 255) // 256, dtype=_I32, device=dev)
         tail = torch.zeros(2, dtype=_I64, device=dev)
         _hip_call("fa_hip_dedup_probe", _p(roff), _p(ranks), pre[0].data_ptr() + 8 * (pre.shape[1] - 1),
-                  DEDUP_PROBE_ROWS, _p(occ), _p(tail), st)
+                  DEDUP_PROBE_ROWS, _p(ws), _p(tail), st)
     # one readback: sizes, the probe's two counts, the row-length histogram
     hs = hist.sum(0, dtype=_I64)
     sizes = torch.cat([pre[:, -1], tail, hs] if probe is not None else [pre[:, -1], hs])

@@ -448,6 +448,48 @@ def test_compress_rows_fused(n, max_len, long_rows):
     assert torch.equal(got, want.clamp(max=255))
 
 
+def _dmix64(z):
+    # prep.hip dmix64 on uint64 arrays (wrapping arithmetic)
+    z = z + np.uint64(0x9E3779B97F4A7C15)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+@pytest.mark.parametrize("n,dups", [(60000, 0), (300000, 40)])
+def test_dedup_probe_counts(n, dups):
+    # the dedup estimate's probe (prep.hip k_dedup_probe + k_probe_count): hashed rows and
+    # occupied slots of the first min(T, 2^18) kept rows vs the same hash in numpy; dups > 0
+    # repeats a few row patterns (occupied slots < hashed rows)
+    import fastapriori_amd.ops.primitives as prim
+    off, items, lut, F1 = _prep(n=n, V=300, max_len=16, seed=n + dups, long_rows=0, F1_frac=0.9)
+    if dups:
+        o, it = off.numpy(), items.numpy()
+        pat = [it[o[i]:o[i + 1]] for i in range(dups)]
+        rows = [pat[i % dups] if i % 3 == 0 else it[o[i]:o[i + 1]] for i in range(n)]
+        off = torch.zeros(n + 1, dtype=torch.int64)
+        off[1:] = torch.from_numpy(np.cumsum([r.size for r in rows]))
+        items = torch.from_numpy(np.concatenate(rows).astype(np.int32))
+    probe = {}
+    kept, roff, ranks, _, _ = ops.compress_rows(off.to(DEV), items.to(DEV), lut.to(DEV), F1, probe=probe)
+    nmax = min(kept.numel(), prim.DEDUP_PROBE_ROWS)
+    ro, rk = roff.cpu().numpy(), ranks.cpu().numpy().astype(np.uint64)
+    lens = ro[1:nmax + 1] - ro[:nmax]
+    sel = np.flatnonzero(lens <= 16)
+    a = np.full(sel.size, 0x243F6A8885A308D3, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        for j in range(16):
+            live = lens[sel] > j
+            idx = np.where(live, ro[sel] + j, 0)
+            a = np.where(live, _dmix64(a ^ rk[idx]), a)
+        a = _dmix64(a ^ lens[sel].astype(np.uint64))
+    slots = (a >> np.uint64(1)) & np.uint64((1 << 22) - 1)
+    assert probe["n"] == sel.size
+    assert probe["filled"] == np.unique(slots).size
+    if dups:
+        assert probe["filled"] < probe["n"]
+
+
 @pytest.mark.parametrize("long_rows", [0, 12])
 def test_pair_counts_with_compress_block_counts(long_rows):
     # the pair layout built from the emit pass's block counts == the counting pass
