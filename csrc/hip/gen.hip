@@ -750,6 +750,7 @@ static int ag_chain_dev(const int32_t* P1, int64_t n1, int m1, int nw, char* w0,
 //     5 multi (level 0 needs several accumulator passes: host path)  6 n_used
 //     7 end (|F_{k-1}| < k or C_0 = 0: mining is over)  8 + l: n_l  40 + l: C_l
 //     72 + l: G_l (parent rows with >= 1 candidate: the reference's group count)
+//     104 (kDlEmpty): the chain stopped on a speculative level with no candidates
 //     512 .. 1023: used-item bitset of level 0 (kDlBitsW words: F1 <= 32768 bits)
 // ---------------------------------------------------------------------------
 namespace fa {
@@ -757,6 +758,7 @@ namespace fa {
 constexpr int kDlCtl = 1024;
 constexpr int kDlBits = 512;       // first word of the used-item bitset in ctl
 constexpr int kDlBitsW = 512;      // its 64-bit words (F1 <= kAgMaxF1 = 32768)
+constexpr int kDlEmpty = 104;      // 1: the chain stopped on a level without candidates
 
 __device__ int64_t agd_block_scan(const int32_t* __restrict__ cnt, int64_t* __restrict__ off, int64_t n,
                                   int64_t* groups = nullptr) {
@@ -859,6 +861,9 @@ __global__ __launch_bounds__(1024) void k_dl_decide(const int32_t* __restrict__ 
   const int64_t total = c[2], last = c[3];
   if (C == 0 || (double)C > growth * (double)last || C > c_bound || total + C > d_slab_cap(c[6], total + C, lds, accb)) {
     c[0] = 1;
+    // no candidates even from the previous level's candidates (a superset of its
+    // frequent rows): the mining ends with this bundle (the host skips the next one)
+    if (C == 0) c[kDlEmpty] = 1;
     return;
   }
   c[40 + l] = C;

@@ -477,6 +477,12 @@ class FastApriori:
             n_src, n_const, n_bound = S.fsz.data_ptr() + 8 * (k + L - 1), 0, int(Cs[-1])
             m0 += L
             k += L
+            # the next bundle's generator would only find the end (one more host round
+            # trip): |F_{k-1}| <= C_{k-1} < k fails the reference's loop test
+            # (FastApriori.scala:111), or the chain already found no k-candidates from
+            # C_{k-1}, a superset of F_{k-1}
+            if int(Cs[-1]) < k or (multi is None and int(c[Pm.DL_EMPTY])):
+                break
         self._dl_flush(S, pend, levels, counts, result)
         self.stats["device_bundles"] = len(pend)
         self.stats["device_levels"] = int(sum(p["L"] for p in pend))

@@ -1488,6 +1488,7 @@ def parse_dict_device(buf: torch.Tensor, n: int, last_is_term: bool):
 # ---------------------------------------------------------------------------
 DL_CTL = 1024           # gen.hip kDlCtl
 DL_BITS = 512           # gen.hip kDlBits: the control block's used-item bitset (ctl[512:1024])
+DL_EMPTY = 104          # gen.hip kDlEmpty: the chain stopped on a level without candidates
 DL_MAX_F1 = 32768       # its bits (and the generator's 8 bitset words per lane)
 DL_MAX_M = 40           # levels.hip kDlMaxM (prefixes past 12 ids go through gpre)
 DL_MAX_LEVELS = 31
