@@ -289,21 +289,27 @@ __global__ __launch_bounds__(256) void k_compress_staged(
   const int64_t o_row = x < x1 ? roff[x] : 0, o_end = x < x1 ? roff[x + 1] : 0;
   const bool staged = n_in <= kCSpan;
   if (staged) {
-    int32_t v[kCPer];
+    // in chunks of at most 32 loads per thread: 64 in flight at the 64-token tier held
+    // 64 more VGPRs than the row sort needs and capped the workgroups per CU
+    constexpr int kCh = kCPer < 32 ? kCPer : 32;
 #pragma unroll
-    for (int k = 0; k < kCPer; ++k) {
-      const int64_t i = threadIdx.x + k * 256;
-      v[k] = i < n_in ? items[base + i] : 0;
-    }
+    for (int k0 = 0; k0 < kCPer; k0 += kCh) {
+      int32_t v[kCh];
 #pragma unroll
-    for (int k = 0; k < kCPer; ++k) {
-      const int64_t i = threadIdx.x + k * 256;
-      if (i < n_in) v[k] = lut[v[k]];
-    }
+      for (int k = 0; k < kCh; ++k) {
+        const int64_t i = threadIdx.x + (k0 + k) * 256;
+        v[k] = i < n_in ? items[base + i] : 0;
+      }
 #pragma unroll
-    for (int k = 0; k < kCPer; ++k) {
-      const int64_t i = threadIdx.x + k * 256;
-      if (i < n_in) buf[i] = v[k] < 0 ? kNone : (BT)v[k];
+      for (int k = 0; k < kCh; ++k) {
+        const int64_t i = threadIdx.x + (k0 + k) * 256;
+        if (i < n_in) v[k] = lut[v[k]];
+      }
+#pragma unroll
+      for (int k = 0; k < kCh; ++k) {
+        const int64_t i = threadIdx.x + (k0 + k) * 256;
+        if (i < n_in) buf[i] = v[k] < 0 ? kNone : (BT)v[k];
+      }
     }
   }
   __syncthreads();
@@ -1315,16 +1321,24 @@ __global__ __launch_bounds__(256) void k_txn_freq_count_wv(const int64_t* __rest
   const int erel = (int)(off[min(x0 + lane + 1, n)] - base);
   int c = 0;
   constexpr int U = 4;
+  // the next four windows' tokens are loaded before this step's LUT gathers: the token
+  // stream and the gathers overlap instead of alternating
+  int v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) v[u] = 64 * u + lane < nt ? items[base + 64 * u + lane] : -1;
   for (int p0 = 0; p0 < nt; p0 += 64 * U) {
-    int v[U];
+    int nv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int p = p0 + 64 * u + lane;
-      v[u] = p < nt ? items[base + p] : -1;
+      const int p = p0 + 64 * (U + u) + lane;
+      nv[u] = p < nt ? items[base + p] : -1;
     }
+    int lv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) lv[u] = v[u] >= 0 ? lut[v[u]] : -1;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const bool f = v[u] >= 0 && lut[v[u]] >= 0;
+      const bool f = lv[u] >= 0;
       const unsigned long long b = __ballot(f);
       const int lo = max(srel - (p0 + 64 * u), 0), hi = min(erel - (p0 + 64 * u), 64);
       if (hi > lo) {
@@ -1332,6 +1346,8 @@ __global__ __launch_bounds__(256) void k_txn_freq_count_wv(const int64_t* __rest
         c += __popcll(b & m);
       }
     }
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = nv[u];
   }
   if (x0 + lane < n) cnt[x0 + lane] = c;
 }
