@@ -1320,8 +1320,8 @@ __global__ __launch_bounds__(256) void k_txn_freq_count_wv(const int64_t* __rest
   const int srel = (int)(off[min(x0 + lane, n)] - base);
   const int erel = (int)(off[min(x0 + lane + 1, n)] - base);
   int c = 0;
-  constexpr int U = 4;
-  // the next four windows' tokens are loaded before this step's LUT gathers: the token
+  constexpr int U = 8;
+  // the next U windows' tokens are loaded before this step's LUT gathers: the token
   // stream and the gathers overlap instead of alternating
   int v[U];
 #pragma unroll
