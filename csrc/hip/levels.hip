@@ -401,6 +401,116 @@ __global__ __launch_bounds__(1024) void k_dl_threshold(const DlLevels D, const D
   }
 }
 
+// The same threshold over many workgroups, for bundles past a few thousand candidates
+// (the one-workgroup kernel walks T40I10D100M's ~150K-candidate bundles in ~220 us):
+// blocks of kThB candidates of one level each, (1) kept counts per block, (2) one
+// workgroup's exclusive scan of them per level (and fsz), (3) the kept counts and rows
+// at the scanned offsets, rows copied cooperatively (coalesced) from an LDS list.
+constexpr int kThB = 1024;
+struct DlThrBlk {
+  int64_t blk_base[kDlMaxL + 1];  // first block of level l (blocks of level l: [blk_base[l], blk_base[l + 1]))
+};
+
+__device__ __forceinline__ int dlt_level(const DlThrBlk& B, int L, int64_t b) {
+  int l = 0;
+  while (l + 1 < L && b >= B.blk_base[l + 1]) ++l;
+  return l;
+}
+
+__global__ __launch_bounds__(256) void k_dlt_count(const DlLevels D, const DlThrBlk B,
+                                                   const uint32_t* __restrict__ counts, int64_t mc,
+                                                   int32_t* __restrict__ part) {
+  const int64_t b = blockIdx.x;
+  const int l = dlt_level(B, D.L, b);
+  const int64_t C = D.C[l], e0 = (b - B.blk_base[l]) * kThB;
+  const uint32_t* cl = counts + D.base[l];
+  uint32_t k = 0;
+#pragma unroll
+  for (int u = 0; u < kThB / 256; ++u) {
+    const int64_t e = e0 + threadIdx.x + 256 * u;
+    k += (e < C && (int64_t)cl[e] >= mc) ? 1u : 0u;
+  }
+  __shared__ uint32_t ws[4];
+  k = wave_sum_u32(k);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = k;
+  __syncthreads();
+  if (threadIdx.x == 0) part[b] = (int32_t)(ws[0] + ws[1] + ws[2] + ws[3]);
+}
+
+__global__ __launch_bounds__(1024) void k_dlt_scan(const DlThrBlk B, int L, int32_t* __restrict__ part,
+                                                  long long* __restrict__ fsz) {
+  __shared__ int64_t wpart[16];
+  __shared__ int64_t carry;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int l = 0; l < L; ++l) {
+    const int64_t b0 = B.blk_base[l], b1 = B.blk_base[l + 1];
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int64_t q = b0; q < b1; q += 1024) {
+      const int64_t i = q + threadIdx.x;
+      const int v = i < b1 ? part[i] : 0;
+      const int incl = wave_scan_incl_dpp(v);
+      if (lane == 63) wpart[wv] = incl;
+      __syncthreads();
+      int64_t before = carry;
+      for (int k = 0; k < wv; ++k) before += wpart[k];
+      if (i < b1) part[i] = (int32_t)(before + incl - v);
+      __syncthreads();
+      if (threadIdx.x == 1023) carry = before + incl;
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) fsz[l] = carry;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void k_dlt_emit(const DlLevels D, const DlOut O, const DlThrBlk B,
+                                                  const uint32_t* __restrict__ counts, int64_t mc,
+                                                  const int32_t* __restrict__ part, int32_t* __restrict__ rows_out,
+                                                  int32_t* __restrict__ cnt_out) {
+  constexpr int U = kThB / 256;                     // consecutive candidates per thread (in order)
+  __shared__ int16_t kept[kThB];                    // the block's kept candidates, in output order
+  __shared__ int wsum[4];
+  const int64_t b = blockIdx.x;
+  const int l = dlt_level(B, D.L, b);
+  const int64_t C = D.C[l], e0 = (b - B.blk_base[l]) * kThB;
+  const uint32_t* cl = counts + D.base[l];
+  const int w = D.m[l] + 1;
+  uint32_t v[U];
+  int k = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t e = e0 + (int64_t)threadIdx.x * U + u;
+    v[u] = e < C ? cl[e] : 0u;
+    k += (e < C && (int64_t)v[u] >= mc) ? 1 : 0;
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int incl = wave_scan_incl_dpp(k);
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  int pos = incl - k;
+  for (int q = 0; q < wv; ++q) pos += wsum[q];
+  const int nk = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  const int64_t at0 = part[b];
+  int32_t* co = cnt_out + O.cnt_off[l];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t e = e0 + (int64_t)threadIdx.x * U + u;
+    if (e < C && (int64_t)v[u] >= mc) {
+      co[at0 + pos] = (int32_t)v[u];
+      kept[pos] = (int16_t)(threadIdx.x * U + u);
+      ++pos;
+    }
+  }
+  __syncthreads();
+  const int32_t* src = D.rows[l] + e0 * w;
+  int32_t* ro = rows_out + O.rows_off[l] + at0 * w;
+  for (int i = threadIdx.x; i < nk * w; i += 256) {
+    const int kk = i / w, q = i - kk * w;
+    ro[i] = src[(int64_t)kept[kk] * w + q];
+  }
+}
+
 // levels of a bundle from gen.hip's level table; gpre / gpre_cap: room for the prefix
 // slab rows of levels whose prefixes exceed kDlInline ids (returns 1 when too small)
 static int dl_levels(const int64_t* desc, int L, DlLevels* D, int32_t* gpre = nullptr, int64_t gpre_cap = 0) {
@@ -494,15 +604,37 @@ FA_API int fa_hip_dl_plan_window(const int64_t* desc, int L, long long* ctl, int
 // Threshold of a device bundle's counts (bundle candidate order) into per-level
 // outputs: rows_out + rows_off[l] (int32 [F][m_l + 1]), cnt_out + cnt_off[l]
 // (int32 [F]); F of level l into fsz[l] (device).  rows_off / cnt_off: host int64 [L].
+// scratch (optional): int32 [scratch_cap] for the multi-workgroup form (bundles of more
+// than 4096 candidates; one per kThB candidates of each level, fa_hip_dl_threshold_scratch).
 FA_API int fa_hip_dl_threshold(const int64_t* desc, int L, const uint32_t* counts, int64_t mc, int32_t* rows_out,
                                const int64_t* rows_off, int32_t* cnt_out, const int64_t* cnt_off, long long* fsz,
-                               hipStream_t st) {
+                               int32_t* scratch, int64_t scratch_cap, hipStream_t st) {
   DlLevels D;
   if (dl_levels(desc, L, &D, nullptr, -1)) return 1;
   DlOut O{};
   for (int l = 0; l < L; ++l) { O.rows_off[l] = rows_off[l]; O.cnt_off[l] = cnt_off[l]; }
-  hipLaunchKernelGGL(k_dl_threshold, dim3(1), dim3(1024), 0, st, D, O, counts, mc, rows_out, cnt_out, fsz);
+  DlThrBlk B{};
+  int64_t C = 0;
+  for (int l = 0; l < L; ++l) {
+    B.blk_base[l + 1] = B.blk_base[l] + (D.C[l] + kThB - 1) / kThB;
+    C += D.C[l];
+  }
+  const int64_t nblk = B.blk_base[L];
+  if (C <= 4 * kThB || scratch == nullptr || scratch_cap < nblk || nblk < 1) {
+    hipLaunchKernelGGL(k_dl_threshold, dim3(1), dim3(1024), 0, st, D, O, counts, mc, rows_out, cnt_out, fsz);
+  } else {
+    hipLaunchKernelGGL(k_dlt_count, dim3((unsigned)nblk), dim3(256), 0, st, D, B, counts, mc, scratch);
+    hipLaunchKernelGGL(k_dlt_scan, dim3(1), dim3(1024), 0, st, B, L, scratch, fsz);
+    hipLaunchKernelGGL(k_dlt_emit, dim3((unsigned)nblk), dim3(256), 0, st, D, O, B, counts, mc, scratch, rows_out,
+                       cnt_out);
+  }
   FA_LAUNCH_RET();
+}
+
+FA_API int64_t fa_hip_dl_threshold_scratch(const int64_t* desc, int L) {
+  int64_t n = 0;
+  for (int l = 0; l < L; ++l) n += (desc[8 * l + 6] + kThB - 1) / kThB;
+  return n;
 }
 
 // int32 entries of gpre a bundle needs (levels with prefixes past kDlInline ids)

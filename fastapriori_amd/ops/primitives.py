@@ -1742,8 +1742,13 @@ def dl_threshold(S: DeviceLevelState, L: int, counts: torch.Tensor, mc: int, k0:
         rows_off[1:] = np.cumsum(C * w)[:-1]
         cnt_off[1:] = np.cumsum(C)[:-1]
     rows = torch.empty(max(int((C * w).sum()), 1), dtype=_I32, device=dev)
-    cnt = torch.empty(max(int(C.sum()), 1), dtype=_I32, device=dev)
+    # the kept counts + the multi-workgroup threshold's block counts (levels.hip) in one allocation
+    nblk = int(((C + 1023) // 1024).sum())
+    cnt = torch.empty(max(int(C.sum()), 1) + nblk, dtype=_I32, device=dev)
+    scratch = cnt[cnt.numel() - nblk:]
     _native.check(_native.hip().fa_hip_dl_threshold(S.desc.ctypes.data, L, _p(counts), int(mc), _p(rows),
                                                     rows_off.ctypes.data, _p(cnt), cnt_off.ctypes.data,
-                                                    _p(S.fsz) + 8 * k0, _stream(counts)), "fa_hip_dl_threshold")
+                                                    _p(S.fsz) + 8 * k0, _p(scratch), nblk, _stream(counts)),
+                  "fa_hip_dl_threshold")
+    cnt = cnt[:cnt.numel() - nblk]
     return rows, cnt, rows_off, cnt_off
