@@ -1030,8 +1030,11 @@ struct DlPost {
   int32_t* gpre; int64_t gpre_cap;
   // LDS bytes per accumulator: 4, or 2 (unit weights: count.hip's packed u16 counters)
   double accb;
+  // trim when the estimate keeps fewer than this share of the rows, or of the items
+  // (FastApriori._trim_worth_it, TUNING.trim_rows_frac / trim_nnz_frac)
+  double trim_rows_frac, trim_nnz_frac;
 };
-static_assert(sizeof(DlPost) == 31 * 8, "DlPost layout (ops.primitives.DlPostC)");
+static_assert(sizeof(DlPost) == 33 * 8, "DlPost layout (ops.primitives.DlPostC)");
 
 FA_API int fa_hip_dl_plan(const int64_t* desc, int L, long long* ctl, int F1, int32_t* item_map, void* rec,
                           int64_t max_pieces, int32_t* part, int64_t part_cap, int32_t* gpre, int64_t gpre_cap,
@@ -1104,7 +1107,7 @@ static void dl_post(DlPost* P, const int64_t* desc, int L, long long* ctl, const
         est_nnz += h * Lr * p;
       }
       const double T = (double)std::max<int64_t>(P->T, 1), nnz = (double)std::max<int64_t>(P->nnz, 1);
-      P->trim = (est_rows < 0.75 * T || est_nnz < 0.6 * nnz) ? 1 : 0;
+      P->trim = (est_rows < P->trim_rows_frac * T || est_nnz < P->trim_nnz_frac * nnz) ? 1 : 0;
     }
   }
   if (P->trim) return;                                      // the caller trims, then counts

@@ -599,6 +599,7 @@ class FastApriori:
         P.len_hist = hist.ctypes.data if hist is not None else None
         P.T, P.nnz = int(db["T"]), int(db["ranks"].numel())
         P.trim_min_rows, P.trim_ok, P.k = int(self.cfg.trim_min_rows), int(bool(self.cfg.trim) and db["T"] > 0), k
+        P.trim_rows_frac, P.trim_nnz_frac = float(TUNING.trim_rows_frac), float(TUNING.trim_nnz_frac)
 
     def _dl_stage(self, S, pend: list) -> None:
         """Queue the D2H copies of the results not staged yet (F_2 once, then each new
@@ -1169,10 +1170,10 @@ class FastApriori:
             sf[ok] = betainc(k, L[ok] - k + 1, min(p, 1.0))
         est_rows = float((hist * sf).sum())
         est_nnz = float((hist * L * p).sum())
-        rows_ok = est_rows < 0.75 * max(db["T"], 1)
+        rows_ok = est_rows < TUNING.trim_rows_frac * max(db["T"], 1)
         if C and db["ranks"].is_cuda and C > ops.primitives.slab_capacity(int(used.size), C):
             return rows_ok
-        return rows_ok or est_nnz < 0.6 * max(int(db["ranks"].numel()), 1)
+        return rows_ok or est_nnz < TUNING.trim_nnz_frac * max(int(db["ranks"].numel()), 1)
 
     def _len_hist(self, db) -> np.ndarray:
         lens = db["roff"][1:] - db["roff"][:-1]

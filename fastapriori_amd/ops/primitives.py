@@ -1504,7 +1504,8 @@ class DlPostC(ctypes.Structure):
                [(n, ctypes.c_void_p) for n in ("c1", "alive", "len_hist")] + \
                [(n, ctypes.c_int64) for n in ("T", "nnz", "trim_min_rows", "trim_ok", "k",
                                                "done", "sw", "cap", "n_wg", "C", "trim")] + \
-               [("gpre", ctypes.c_void_p), ("gpre_cap", ctypes.c_int64), ("accb", ctypes.c_double)]
+               [("gpre", ctypes.c_void_p), ("gpre_cap", ctypes.c_int64), ("accb", ctypes.c_double)] + \
+               [("trim_rows_frac", ctypes.c_double), ("trim_nnz_frac", ctypes.c_double)]
 
 
 class DeviceLevelState:

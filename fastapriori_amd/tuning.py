@@ -56,6 +56,10 @@ class Tuning:
     pair_wg: int = 0                    # k_pair_queue16 workgroups (0: one per CU)
     gram_mfma_min_class_words: int = 512   # shorter weight classes: the popcount Gram
     bitmap_blocked: bool = True         # the Gram's bitmap in 8-word blocks (count.hip BmView)
+    # transaction trimming before a level (models/apriori.py _trim_worth_it, gen.hip dl_post):
+    # when the binomial estimate keeps fewer than this share of the rows, or of the items
+    trim_rows_frac: float = 0.75
+    trim_nnz_frac: float = 0.6
     # ---- I/O (utils/io.py) -------------------------------------------------------
     gpu_parse: bool = True              # D.dat parsed on the GPU behind the H2D copies
     gpu_parse_dict: bool = True         # dictionary-mode tokens too
