@@ -1073,8 +1073,10 @@ __global__ __launch_bounds__(256) void k_cmp_emit(const int64_t* __restrict__ of
       for (int j = 0; j < N; ++j) {
         if (j < c) {
           const int b = (int)(a[j] >> 8);
-          const int64_t pos = b < nb ? wgb[b] + tabx[threadIdx.x * nb + b] + j : -1;
-          if (pos >= 0 && pos < lr_cap) lr[pos] = (uint8_t)a[j];
+          // b < nb and the position inside lr hold by construction (a frequent rank is
+          // < F1 <= 256 nb; the layout's spans are the scanned block counts): no guards
+          // in this 16-step loop
+          lr[wgb[b] + (int64_t)(tabx[threadIdx.x * nb + b] + j)] = (uint8_t)a[j];
         }
       }
     }
@@ -1143,8 +1145,7 @@ __global__ __launch_bounds__(256) void k_cmp_emit(const int64_t* __restrict__ of
             buf[reb + idx] = midv[t];
             if (lr) {
               const int b = (int)(midv[t] >> 8);
-              const int64_t pos = b < nb ? wgb[b] + tabx[(w * 64 + rw) * nb + b] + idx : -1;
-              if (pos >= 0 && pos < lr_cap) lr[pos] = (uint8_t)midv[t];
+              lr[wgb[b] + (int64_t)(tabx[(w * 64 + rw) * nb + b] + idx)] = (uint8_t)midv[t];
             }
           }
         }
