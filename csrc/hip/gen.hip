@@ -820,6 +820,110 @@ __global__ __launch_bounds__(1024) void k_dl_decide0(const int32_t* __restrict__
   c[1] = 1; c[2] = C; c[3] = C; c[9] = C;
 }
 
+// Level 0's scan over many workgroups when F_{k-1} is large (T40I10D100M's bundles start
+// from up to ~157K parent rows, where the one-workgroup k_dl_decide0 took ~78 us):
+// (1) kDsBlk-row block scans into off[] (block-local) with the block totals, (2) one
+// workgroup scans the totals and takes k_dl_decide0's decisions, (3) the block bases
+// are added to off[].  bs: int64 scratch [3 * nblk].
+constexpr int kDsBlk = 4096;
+
+__global__ __launch_bounds__(1024) void k_ds_blocks(const int32_t* __restrict__ cnt, int64_t* __restrict__ off,
+                                                    const long long* __restrict__ c, int64_t* __restrict__ bs,
+                                                    int nblk) {
+  if (c[0]) return;
+  const int64_t n = c[8];
+  const int64_t b0 = (int64_t)blockIdx.x * kDsBlk;
+  if (b0 >= n) {
+    if (threadIdx.x == 0) { bs[blockIdx.x] = 0; bs[nblk + blockIdx.x] = 0; }
+    return;
+  }
+  __shared__ int wpart[16];
+  __shared__ int wnz[16];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // four consecutive rows per thread, in order
+  int v[4], t = 0, nz = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t i = b0 + 4 * (int64_t)threadIdx.x + u;
+    v[u] = i < n ? cnt[i] : 0;
+    t += v[u];
+    nz += v[u] > 0;
+  }
+  const int incl = wave_scan_incl_dpp(t);
+  const int nzs = (int)wave_sum_u32((uint32_t)nz);
+  if (lane == 63) wpart[wv] = incl;
+  if (lane == 0) wnz[wv] = nzs;
+  __syncthreads();
+  int64_t run = incl - t;
+  for (int q = 0; q < wv; ++q) run += wpart[q];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int64_t i = b0 + 4 * (int64_t)threadIdx.x + u;
+    run += v[u];
+    if (i < n) off[i + 1] = run;
+  }
+  if (threadIdx.x == 0) {
+    int64_t tot = 0, z = 0;
+    for (int q = 0; q < 16; ++q) { tot += wpart[q]; z += wnz[q]; }
+    bs[blockIdx.x] = tot;
+    bs[nblk + blockIdx.x] = z;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_ds_decide0(int64_t* __restrict__ off, long long* __restrict__ c,
+                                                     int64_t* __restrict__ bs, int nblk, int64_t c_bound) {
+  if (c[0]) return;
+  __shared__ int64_t part[16];
+  __shared__ int64_t carry, gz;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (threadIdx.x == 0) { carry = 0; gz = 0; off[0] = 0; }
+  __syncthreads();
+  for (int q0 = 0; q0 < nblk; q0 += 1024) {
+    const int q = q0 + threadIdx.x;
+    const int64_t v = q < nblk ? bs[q] : 0;
+    const int64_t z = q < nblk ? bs[nblk + q] : 0;
+    // 64-bit inclusive scan by shuffles (block totals can pass 2^31 only in theory; cheap here)
+    int64_t incl = v;
+    for (int d = 1; d < 64; d <<= 1) {
+      const int64_t o = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += o;
+    }
+    int64_t zs = z;
+    for (int d = 32; d > 0; d >>= 1) zs += __shfl_xor(zs, d, 64);
+    if (lane == 63) part[wv] = incl;
+    __syncthreads();
+    int64_t before = carry;
+    for (int k = 0; k < wv; ++k) before += part[k];
+    if (q < nblk) bs[2 * nblk + q] = before + incl - v;     // exclusive block base
+    if (lane == 0) atomicAdd((unsigned long long*)&gz, (unsigned long long)zs);
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = before + incl;
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  const int64_t C = carry;
+  c[40] = C;
+  c[72] = gz;
+  if (C == 0) { c[7] = 1; c[0] = 1; return; }
+  if (C > c_bound) { c[5] = 1; c[0] = 1; return; }
+  c[1] = 1; c[2] = C; c[3] = C; c[9] = C;
+}
+
+__global__ __launch_bounds__(1024) void k_ds_add(int64_t* __restrict__ off, const long long* __restrict__ c,
+                                                 const int64_t* __restrict__ bs, int nblk) {
+  // after k_ds_decide0: a multi / empty level 0 (c[0] set) is regenerated or ends, its
+  // offsets unused; c[8] and the block bases are final either way
+  if (c[4]) return;                                     // n past the buffers' bound: nothing ran
+  const int64_t n = c[8];
+  const int64_t b0 = (int64_t)blockIdx.x * kDsBlk;
+  if (b0 >= n || blockIdx.x == 0) return;               // block 0's base is 0
+  const int64_t base = bs[2 * nblk + blockIdx.x];
+  for (int k = threadIdx.x; k < kDsBlk; k += 1024) {
+    const int64_t i = b0 + k;
+    if (i < n) off[i + 1] += base;
+  }
+}
+
 // used items of level 0's candidate rows (LDS-privatised, one global atomicOr per word);
 // w32: the bitset's u32 words in use ((F1 + 31) / 32)
 __global__ __launch_bounds__(256) void k_dl_mark(const int32_t* __restrict__ rows, int m1,
@@ -945,8 +1049,9 @@ FA_API int fa_hip_dl_level0(const int32_t* P0, const long long* n_src, int64_t n
   const int64_t nb = std::max<int64_t>(n_bound, 1);
   uint32_t cap = 16;
   while (cap < 2 * (uint64_t)nb) cap <<= 1;
+  const int nds = nb > 4 * kDsBlk ? (int)((nb + kDsBlk - 1) / kDsBlk) : 0;   // multi-workgroup scan blocks
   const int64_t need = al(4 * (int64_t)cap) + al(8 * nb * nw) + al(8 * (nb + 1)) + al(4 * (nb + c_bound)) +
-                       al(4 * c_bound * (m0 + 1));
+                       al(4 * c_bound * (m0 + 1)) + al(8 * 3 * (int64_t)nds);
   info[0] = need;
   if (need > ws_bytes) return 5;
   char* w = static_cast<char*>(ws);
@@ -954,7 +1059,8 @@ FA_API int fa_hip_dl_level0(const int32_t* P0, const long long* n_src, int64_t n
   unsigned long long* ext = reinterpret_cast<unsigned long long*>(w); w += al(8 * nb * nw);
   int64_t* off = reinterpret_cast<int64_t*>(w); w += al(8 * (nb + 1));
   int32_t* cnt = reinterpret_cast<int32_t*>(w); w += al(4 * (nb + c_bound));
-  int32_t* rows = reinterpret_cast<int32_t*>(w);
+  int32_t* rows = reinterpret_cast<int32_t*>(w); w += al(4 * c_bound * (m0 + 1));
+  int64_t* ds = reinterpret_cast<int64_t*>(w);
   info[1] = (int64_t)(intptr_t)cnt; info[2] = (int64_t)(intptr_t)off; info[3] = (int64_t)(intptr_t)rows;
   hipLaunchKernelGGL(k_dl_setup0, dim3(1), dim3(kDlCtl), 0, st, ctl, n_src, n_const, m0 + 1, nb);
   AgdClear clr{};
@@ -974,7 +1080,13 @@ FA_API int fa_hip_dl_level0(const int32_t* P0, const long long* n_src, int64_t n
 #define FA_DL0_CNT(N) FA_DL0_ROWS(false, N)
 #define FA_DL0_EMIT(N) FA_DL0_ROWS(true, N)
   FA_AG_NWL_SWITCH(nw, FA_DL0_CNT)
-  hipLaunchKernelGGL(k_dl_decide0, dim3(1), dim3(1024), 0, st, cnt, off, ctl, c_bound);
+  if (nds) {
+    hipLaunchKernelGGL(k_ds_blocks, dim3((unsigned)nds), dim3(1024), 0, st, cnt, off, ctl, ds, nds);
+    hipLaunchKernelGGL(k_ds_decide0, dim3(1), dim3(1024), 0, st, off, ctl, ds, nds, c_bound);
+    hipLaunchKernelGGL(k_ds_add, dim3((unsigned)nds), dim3(1024), 0, st, off, ctl, ds, nds);
+  } else {
+    hipLaunchKernelGGL(k_dl_decide0, dim3(1), dim3(1024), 0, st, cnt, off, ctl, c_bound);
+  }
   FA_AG_NWL_SWITCH(nw, FA_DL0_EMIT)
 #undef FA_DL0_EMIT
 #undef FA_DL0_CNT
