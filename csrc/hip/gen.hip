@@ -476,14 +476,23 @@ FA_API int fa_hip_ag_chain(const int32_t* P0, int64_t n0, int m0, int F1, void* 
 namespace fa {
 
 // accb: LDS bytes per accumulator (4, or 2 for count.hip's packed u16 counters)
-__device__ int64_t d_slab_cap(int64_t n_used, int64_t C, double lds, double accb) {
+// capmax (fa_hip_set_cap_max): a bundle may take a narrower slab when that is what holds
+// all of its candidates (the first width whose capacity is >= C, else the largest
+// capacity); 0: the first width holding min(C, 8192), as plan.cpp slab_width
+__device__ int64_t d_slab_cap(int64_t n_used, int64_t C, double lds, double accb, int capmax = 0) {
   const int sws[4] = {16, 32, 8, 4};   // plan.cpp slab_width order
+  int64_t best = 0;
   for (int q = 0; q < 4; ++q) {
     const int sw = sws[q];
     const int64_t cap = (int64_t)((lds - (double)n_used * (sw + 2) * 8) / accb);
+    if (capmax) {
+      if (cap >= C && (sw != 4 || cap >= 1024)) return cap;
+      if (cap > best) best = cap;
+      continue;
+    }
     if (cap >= (C < 8192 ? C : 8192) || (sw == 4 && cap >= 1024)) return cap;
   }
-  return 0;
+  return capmax ? best : 0;
 }
 
 __device__ int64_t d_total_limit(int64_t n_used, double lds, double accb) {
@@ -942,7 +951,8 @@ __global__ __launch_bounds__(256) void k_dl_mark(const int32_t* __restrict__ row
 }
 
 // n_used, and whether level 0 alone exceeds one accumulator pass
-__global__ __launch_bounds__(64) void k_dl_post0(long long* __restrict__ c, double lds, double accb, int w32) {
+__global__ __launch_bounds__(64) void k_dl_post0(long long* __restrict__ c, double lds, double accb, int w32,
+                                                  int capmax) {
   if (blockIdx.x != 0) return;
   const uint32_t* mk = reinterpret_cast<const uint32_t*>(c + kDlBits);
   uint32_t part = 0;
@@ -950,20 +960,21 @@ __global__ __launch_bounds__(64) void k_dl_post0(long long* __restrict__ c, doub
   const int64_t n_used = (int64_t)wave_sum_u32(part);
   if (threadIdx.x != 0) return;
   c[6] = n_used;
-  if (c[1] == 1 && c[40] > d_slab_cap(n_used, c[40], lds, accb)) { c[5] = 1; c[0] = 1; }
+  if (c[1] == 1 && c[40] > d_slab_cap(n_used, c[40], lds, accb, capmax)) { c[5] = 1; c[0] = 1; }
 }
 
 // acceptance of speculative level l >= 1 (same rule as k_agd_scan_decide, with the
 // exact one-pass test total + C <= slab capacity(n_used, total + C))
 __global__ __launch_bounds__(1024) void k_dl_decide(const int32_t* __restrict__ cnt, int64_t* __restrict__ off,
                                                      long long* __restrict__ c, int l, double growth, int64_t c_bound,
-                                                     double lds, double accb) {
+                                                     double lds, double accb, int capmax) {
   if (c[0]) return;
   int64_t g = 0;
   const int64_t C = agd_block_scan(cnt, off, c[8 + l], &g);
   if (threadIdx.x != 0) return;
   const int64_t total = c[2], last = c[3];
-  if (C == 0 || (double)C > growth * (double)last || C > c_bound || total + C > d_slab_cap(c[6], total + C, lds, accb)) {
+  if (C == 0 || (double)C > growth * (double)last || C > c_bound ||
+      total + C > d_slab_cap(c[6], total + C, lds, accb, capmax)) {
     c[0] = 1;
     // no candidates even from the previous level's candidates (a superset of its
     // frequent rows): the mining ends with this bundle (the host skips the next one)
@@ -1031,6 +1042,11 @@ __global__ __launch_bounds__(256) void k_dl_rows(const int32_t* __restrict__ P, 
 
 }  // namespace fa
 
+// Slab capacity rule of the device bundles (d_slab_cap capmax), set by
+// fastapriori_amd.ops.primitives before a bundle is generated (TUNING.slab_cap_max)
+static int g_cap_max = 0;
+FA_API void fa_hip_set_cap_max(int on) { g_cap_max = on; }
+
 // Level 0 of a device bundle: candidates of F_{k-1} = P0 [n][m0] (device; n from
 // n_src[0] when given, else n_const; n_bound >= n sizes the buffers), generated
 // into the front of ws; with sync, ONE synchronisation copies ctl to ctl_host
@@ -1094,7 +1110,7 @@ FA_API int fa_hip_dl_level0(const int32_t* P0, const long long* n_src, int64_t n
   const int w32 = (F1 + 31) / 32;
   hipLaunchKernelGGL(k_dl_mark, dim3((unsigned)std::min<int64_t>((c_bound * (m0 + 1) + 255) / 256, 1024)), dim3(256),
                      0, st, rows, m0 + 1, ctl, w32);
-  hipLaunchKernelGGL(k_dl_post0, dim3(1), dim3(64), 0, st, ctl, lds, accb, w32);
+  hipLaunchKernelGGL(k_dl_post0, dim3(1), dim3(64), 0, st, ctl, lds, accb, w32, g_cap_max);
   if (sync) {
     (void)hipMemcpyAsync(ctl_host, ctl, sizeof(long long) * kDlCtl, hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) return 7;
@@ -1186,7 +1202,9 @@ static void dl_post(DlPost* P, const int64_t* desc, int L, long long* ctl, const
   int64_t cap = 0;
   for (int w : {16, 32, 8, 4}) {
     cap = (int64_t)((P->lds_budget - (double)n_used * (w + 2) * 8) / P->accb);
-    if (cap >= std::min<int64_t>(C, 8192) || (w == 4 && cap >= 1024)) { sw = w; break; }
+    const bool fits = g_cap_max ? cap >= C && (w != 4 || cap >= 1024)
+                                : cap >= std::min<int64_t>(C, 8192) || (w == 4 && cap >= 1024);
+    if (fits) { sw = w; break; }
   }
   if (sw == 0 || C > cap) return;
   if (fa_hip_dl_plan(desc, L, ctl, F1, P->item_map, P->rec, C, P->part, P->part_cap, P->gpre, P->gpre_cap, sw,
@@ -1312,7 +1330,8 @@ FA_API int fa_hip_dl_more(int F1, void* ws, int64_t ws_bytes, int64_t ws_used, l
 #define FA_DLR_CNT(N) FA_DLR(false, N)
 #define FA_DLR_EMIT(N) FA_DLR(true, N)
       FA_AG_NWL_SWITCH(nw, FA_DLR_CNT)
-      hipLaunchKernelGGL(k_dl_decide, dim3(1), dim3(1024), 0, st, lv[l].cnt, lv[l].off, ctl, l, growth, cb, lds, accb);
+      hipLaunchKernelGGL(k_dl_decide, dim3(1), dim3(1024), 0, st, lv[l].cnt, lv[l].off, ctl, l, growth, cb, lds, accb,
+                         g_cap_max);
       FA_AG_NWL_SWITCH(nw, FA_DLR_EMIT)
 #undef FA_DLR_EMIT
 #undef FA_DLR_CNT

@@ -26,6 +26,42 @@ def _env(name: str, default):
     return type(default)(v)
 
 
+# every FA_* variable the package reads (config / tuning / env / checkpoint / comm / build)
+KNOWN_ENV = frozenset({"FA_MIN_SUPPORT", "FA_DEVICE", "FA_STRATEGY", "FA_PROFILE", "FA_METRICS", "FA_TUNE",
+                       "FA_NUM_THREADS", "FA_DIST_BACKEND", "FA_FORCE_PG", "FA_FAULT_AT_LEVEL", "FA_FAULT_RANK",
+                       "FA_HIP_LIB"})
+# variables of earlier versions that are no longer read, with what replaced them (ADVICE r5:
+# a job script still setting one would otherwise run with the default, silently)
+RETIRED_ENV = {"FA_DEDUP": "--dedup", "FA_MAX_LEVEL": "--max-level", "FA_RESUME": "--resume",
+               "FA_WITH_COUNTS": "--with-counts", "FA_WORLD_SIZE": "--world-size",
+               "FA_DL_MULTI": "FA_TUNE=dl_multi=0|1", "FA_BUCKET_MB": "FA_TUNE=bucket_mb=<MiB>",
+               "FA_FUSED_LAYOUT": "FA_TUNE=fused_layout=0|1"}
+_WARNED = False
+
+
+def unread_env(environ=None) -> list[str]:
+    """Warnings for FA_* variables set in the environment that nothing reads."""
+    environ = os.environ if environ is None else environ
+    out = []
+    for k in sorted(environ):
+        if not k.startswith("FA_") or k in KNOWN_ENV:
+            continue
+        hint = RETIRED_ENV.get(k)
+        out.append(f"{k} is no longer read" + (f": use {hint}" if hint else " (unknown FA_* variable)"))
+    return out
+
+
+def warn_unread_env() -> None:
+    """Print unread_env()'s warnings once per process (stderr)."""
+    global _WARNED
+    if _WARNED:
+        return
+    _WARNED = True
+    import sys
+    for w in unread_env():
+        print(f"fastapriori: warning: {w}", file=sys.stderr)
+
+
 @dataclass
 class JobConfig:
     input: str = ""
@@ -85,6 +121,7 @@ def build_parser() -> argparse.ArgumentParser:
 
 def parse_args(argv=None) -> JobConfig:
     a = build_parser().parse_args(argv)
+    warn_unread_env()
     return JobConfig(input=a.input, output=a.output, temp=a.temp, min_support=a.min_support, device=a.device,
                      dedup=a.dedup, pair_strategy=a.pair_strategy, with_counts=a.with_counts, resume=a.resume,
                      rules_only=a.rules_only, checkpoint=a.checkpoint, overwrite=a.overwrite,

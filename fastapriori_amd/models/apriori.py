@@ -376,7 +376,7 @@ class FastApriori:
         # window-by-window levels; u32 in one-pass bundles (TUNING.dl_acc16)
         unit = db["wword"] is None
         self._dl_mp_accb = 2.0 if TUNING.dl_acc16 and unit else 4.0
-        accb = self._dl_accb = 4.0
+        accb = self._dl_accb = 2.0 if TUNING.dl_acc16_bundles and unit else 4.0
         c_bound = int(lds // accb)
         st = torch.cuda.current_stream(self._dev).cuda_stream
         f2 = self._f2_dev
@@ -495,7 +495,7 @@ class FastApriori:
         room for all of them when the bounded generation stopped short, the level's
         rows trimmed as the host loop would, then counted window by window from the used
         items' bitmap (ops.primitives.dl_count_multipass).  Returns (control block,
-        int32 counts [C] on the device) or None (FA_DL_MULTI=0: the host loop).  When
+        int32 counts [C] on the device) or None (TUNING.dl_multi off: the host loop).  When
         not even 4-word slabs of the used items fit the LDS (wide levels: thousands of
         used items), the level is counted by the bitmap kernel instead (_dl_bitmap_count)."""
         Pm = ops.primitives
@@ -688,7 +688,9 @@ class FastApriori:
                                     counts=cnt.astype(np.int64))
             ck._write_meta(result, upto)
 
-        ck.submit(work)
+        if ck.rank == 0:
+            # (every rank holds the same levels; only rank 0 writes them)
+            ck.submit(work)
         self._ckpt_saved = max(self._ckpt_saved, upto)
         if fault in ks:
             ck.wait()

@@ -239,7 +239,7 @@ def compress(offsets, items, lut, kept, roff, F1: int | None = None) -> torch.Te
 
 
 PAIR_PAD_BATCHES = 3 * 16 + 2   # the pair kernel's pipeline reads up to this many batches past a chunk
-# the emit pass of compress_rows also writes the pair kernel's blocked layout (FA_FUSED_LAYOUT=0: the
+# the emit pass of compress_rows also writes the pair kernel's blocked layout (TUNING.fused_layout off: the
 # separate block-scatter pass of pair_counts_horizontal)
 
 
@@ -1573,12 +1573,16 @@ def dl_lds_budget(F1: int) -> int:
 # differently, T10I4D100M 43.2 vs 42.3 ms (docs/PERF_HISTORY.md; that arm was removed)
 
 
-def dl_slab_width(n_used: int, C: int, lds: int, accb: int = 4) -> tuple[int, int]:
+def dl_slab_width(n_used: int, C: int, lds: int, accb: int = 4, cap_max: bool = False) -> tuple[int, int]:
     """plan.cpp slab_width: (SW, accumulator capacity) for n_used items and C candidates
-    (accb: LDS bytes per accumulator)."""
+    (accb: LDS bytes per accumulator).  cap_max (TUNING.slab_cap_max, gen.hip
+    d_slab_cap): the first width whose capacity holds all C candidates."""
     for sw in (16, 32, 8, 4):
         cap = int((lds - n_used * (sw + 2) * 8) // accb)
-        if cap >= min(C, 8192) or (sw == 4 and cap >= 1024):
+        if cap_max:
+            if cap >= C and (sw != 4 or cap >= 1024):
+                return sw, cap
+        elif cap >= min(C, 8192) or (sw == 4 and cap >= 1024):
             return sw, cap
     return 0, 0
 
@@ -1592,6 +1596,7 @@ def dl_bundle_gen(S: DeviceLevelState, P0: int, n_src: int | None, n_const: int,
     describes the accepted levels (L = ctl[1])."""
     lib = _native.hip()
     info = np.zeros(2, dtype=np.int64)
+    lib.fa_hip_set_cap_max(int(TUNING.slab_cap_max))
     for _ in range(6):
         S.desc[:] = 0
         rc = lib.fa_hip_dl_level0(P0, n_src, n_const, n_bound, m0, F1, _p(S.ws), S.ws.numel(), _p(S.ctl),
@@ -1633,7 +1638,7 @@ def dl_plan(S: DeviceLevelState, L: int, F1: int, n_used: int, C: int, lds: int,
     candidates only, not on the row layout, so the host's trimming decision runs
     while it executes.  Returns the plan for dl_count."""
     st = torch.cuda.current_stream(dev).cuda_stream
-    sw, cap = dl_slab_width(n_used, C, lds, accb)
+    sw, cap = dl_slab_width(n_used, C, lds, accb, TUNING.slab_cap_max)
     if sw == 0 or C > cap:
         raise RuntimeError(f"device bundle of {C} candidates over {n_used} items does not fit one pass")
     item_map = torch.empty(max(F1, 1), dtype=_I32, device=dev)

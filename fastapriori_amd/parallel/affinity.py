@@ -74,28 +74,38 @@ def plan_affinity(local_rank: int, bdfs: list[str], allowed: list[int], sysfs: s
         peers = [r for r, b in enumerate(bdfs) if gpu_node(b, sysfs)[0] == node]
         j, n = peers.index(local_rank), len(peers)
     else:
-        # narrowed view: an even spread of the local ranks over the GPUs' nodes (>= 1)
-        lw = max(1, local_world or 1)
-        nodes = max(1, len({p for p in _gpu_nodes(sysfs) if p >= 0}) or 1)
-        n = max(1, -(-lw // nodes))
-        j = (local_rank // nodes) % n
+        # narrowed view: the rank's peers are unknown, but its GPU's position
+        # among the node's GPUs in sysfs (PCI order) gives every GPU of the node its own
+        # slice, whatever order the launcher hands GPUs to local ranks in
+        same = [b for b, nd in _gpu_devices(sysfs) if nd == node]
+        if mine.lower() in same:
+            j, n = same.index(mine.lower()), len(same)
+        else:
+            # not listed: an even spread of the local ranks over the GPUs' nodes (>= 1)
+            lw = max(1, local_world or 1)
+            nodes = max(1, len({nd for _, nd in _gpu_devices(sysfs) if nd >= 0}) or 1)
+            n = max(1, -(-lw // nodes))
+            j = (local_rank // nodes) % n
     part = cpus[j * len(cpus) // n:(j + 1) * len(cpus) // n] or cpus
     return {"node": node, "cpus": part, "threads": len(part), "peers": n}
 
 
-def _gpu_nodes(sysfs: str) -> list[int]:
-    """NUMA nodes of the display / processing-accelerator PCI devices (class 0x03, 0x12)."""
+def _gpu_devices(sysfs: str) -> list[tuple[str, int]]:
+    """(bdf, NUMA node) of the AMD display / processing-accelerator PCI devices (class
+    0x03 / 0x12, vendor 0x1002 when sysfs names one: a board's management VGA is not a
+    peer), in PCI address order."""
     base = os.path.join(sysfs, "bus", "pci", "devices")
     out = []
     try:
-        names = os.listdir(base)
+        names = sorted(os.listdir(base))
     except OSError:
         return out
     for b in names:
         cls = _read(os.path.join(base, b, "class")) or ""
-        if cls.startswith(("0x03", "0x12")):
+        vendor = _read(os.path.join(base, b, "vendor"))
+        if cls.startswith(("0x03", "0x12")) and vendor in (None, "0x1002"):
             node = _read(os.path.join(base, b, "numa_node"))
-            out.append(int(node) if node not in (None, "") else -1)
+            out.append((b.lower(), int(node) if node not in (None, "") else -1))
     return out
 
 

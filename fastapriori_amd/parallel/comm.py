@@ -12,10 +12,15 @@ identical candidate lists and only count vectors move (SURVEY §2.4 plan):
   X24     recommendations                     -> gather to rank 0
 
 On ROCm the ``nccl`` backend is RCCL, riding xGMI between the GPUs of a node;
-``gloo`` serves CPU-only runs and tests.  Large vectors are reduced in buckets
-sized for xGMI: 7 point-to-point links per GPU mean one ring uses ~2 of them,
-so buckets are a multiple of world_size * 7 chunks and small enough that RCCL
-can pipeline them (``FA_BUCKET_MB``, default 64 MiB).
+``gloo`` serves CPU-only runs and tests.  What matters on xGMI is how many bytes
+each collective moves, not how they are cut: a mining run issues six collectives
+and the largest payload is the k = 2 triangle (T10I4D100M: 1.9 MB, one ring
+all-reduce of ~22 us on one ~153 GB/s link).  Triangles from
+``TUNING.pair_rs_min`` pairs on go as a reduce-scatter + local threshold +
+all-gather of the survivors instead (``reduce_scatter_select``).  Vectors longer
+than ``TUNING.bucket_mb`` (64 MiB: F1 past ~5800 items) are reduced in buckets of
+that size, a multiple of world_size elements, so that no single call pins a huge
+staging buffer; below it there is exactly one call per vector.
 """
 from __future__ import annotations
 
@@ -146,10 +151,11 @@ class Comm:
         return got[0], got[1]
 
     def bucket_elems(self, elem_size: int) -> int:
+        """Elements per all-reduce call: TUNING.bucket_mb MiB, rounded down to a multiple
+        of world_size (every bucket splits evenly into RCCL's per-rank chunks)."""
         from ..tuning import TUNING
-        mb = float(TUNING.bucket_mb)
-        n = int(mb * (1 << 20)) // elem_size
-        q = max(1, self.world_size * 7 * 64)
+        n = int(float(TUNING.bucket_mb) * (1 << 20)) // elem_size
+        q = max(1, self.world_size)
         return max(q, n // q * q)
 
     @_timed
@@ -333,28 +339,43 @@ def init_comm(device: str | None = None, backend: str | None = None, timeout_s: 
     return Comm(dist.get_rank(), dist.get_world_size(), dev, be, force=force)
 
 
-def _gpu_key(dev) -> str:
-    """This host's identity of the rank's GPU: its UUID (or PCI bus id), which a launcher
-    that narrows every rank's view to "device 0" does not hide."""
+def _gpu_key(dev, props=None, host: str | None = None) -> str:
+    """This host's identity of the rank's GPU, which a launcher that narrows every rank's
+    view to "device 0" does not hide: its PCI address (domain:bus:device, unique on a
+    host), else its UUID unless that is blank or all zeros (a build reporting
+    one UUID for every device would fail every rank after the first), else the visible-
+    devices variable and index."""
     import socket
-    props = torch.cuda.get_device_properties(dev)
-    ident = getattr(props, "uuid", None) or getattr(props, "pci_bus_id", None)
+    from .affinity import gpu_bdf
+    props = props if props is not None else torch.cuda.get_device_properties(dev)
+    host = host if host is not None else socket.gethostname()
+    ident = None
+    try:
+        if int(props.pci_bus_id) or int(props.pci_device_id) or int(props.pci_domain_id):
+            ident = "pci:" + gpu_bdf(props)
+    except (AttributeError, TypeError, ValueError):
+        ident = None
+    if ident is None:
+        u = str(getattr(props, "uuid", "") or "")
+        if u.strip("0-{}").strip() and u.lower() not in ("none", "null"):
+            ident = "uuid:" + u
     if ident is None:
         vis = next((os.environ.get(v) for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES",
                                                 "CUDA_VISIBLE_DEVICES") if os.environ.get(v)), "")
-        ident = f"{vis}/{dev.index}"
-    return f"fa_gpu/{socket.gethostname()}/{ident}"
+        ident = f"vis:{vis}/{getattr(dev, 'index', dev)}"
+    return f"fa_gpu/{host}/{ident}"
 
 
-def _check_one_gpu_per_rank(dev) -> None:
+def _check_one_gpu_per_rank(dev, store=None, key: str | None = None, rank: int | None = None) -> None:
     """RCCL ranks of one communicator must not share a GPU, also when each rank's
     *_VISIBLE_DEVICES shows it a single device (the same value exported to
     every local rank).  Every rank counts itself under its GPU's key in the rendezvous
     store: a second rank on the same GPU sees 2 and fails fast."""
-    store = dist.distributed_c10d._get_default_store()     # noqa: SLF001
-    n = store.add(_gpu_key(dev), 1)
+    store = store if store is not None else dist.distributed_c10d._get_default_store()     # noqa: SLF001
+    n = store.add(key if key is not None else _gpu_key(dev), 1)
     if n > 1:
-        raise RuntimeError(f"rank {dist.get_rank()} shares its GPU with another rank: RCCL needs one GPU per rank "
+        r = dist.get_rank() if rank is None else rank
+        raise RuntimeError(f"rank {r} shares its GPU with another rank: RCCL needs one GPU per rank "
                            "(FA_DIST_BACKEND=gloo lets ranks share a GPU for tests)")
 
 

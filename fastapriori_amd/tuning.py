@@ -49,6 +49,10 @@ class Tuning:
     slab_cls: int = 1                   # class layout of host-planned slab passes: 0 off, 1 model, 2 always
     dense_min_rows: float = 4.0         # skip the all-zero-prefix test above this many rows per slab
     dl_acc16: bool = True               # packed u16 accumulators in window-by-window levels (unit weights)
+    dl_acc16_bundles: bool = False      # ... and in one-pass device bundles
+    # bundle capacity = the largest over the slab widths (a bundle takes a narrower slab
+    # when that holds all of it) instead of the first width holding 8192 candidates
+    slab_cap_max: bool = False
     # bank-aware lane deal of device slab plans (levels.hip k_dl_lane_assign) from this many
     # rows (-1: off): ~0.18 ms per bundle against ~5 % of the slab counts (T10I4D100M
     # 42.1 -> 41.2 ms; the 12.5M-row shard 6.50 -> 6.85 ms, hence the threshold)

@@ -87,6 +87,11 @@ class Checkpointer:
         self._thread.start()
 
     def _write_meta(self, result: MiningResult, k: int, complete: bool = False) -> None:
+        if self.rank != 0:
+            # rank 0 alone publishes the checkpoint: another rank's meta could count levels
+            # whose files rank 0 has not written yet (or land in a directory that does not
+            # exist on its node)
+            return
         meta = {"items": result.items, "min_count": result.min_count, "n_lines": result.n_lines,
                 "levels_done": k, "fingerprint": self.fingerprint}
         if complete:

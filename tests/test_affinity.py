@@ -64,3 +64,60 @@ def test_narrowed_view_spreads_ranks_over_nodes(tmp_path):
 def test_no_locality_means_no_binding(tmp_path):
     p = plan_affinity(0, ["0000:99:00.0"], list(range(16)), str(tmp_path))
     assert p["cpus"] == [] and p["threads"] == 0
+
+
+def test_narrowed_view_blocked_gpu_order_gets_disjoint_slices(tmp_path):
+    # GPUs 0-3 on node 0 and 4-7 on node 1 handed to local ranks 0-7 in order,
+    # each rank seeing only its own GPU: the slice comes from the GPU's position among its
+    # node's GPUs, so the four ranks of a node get four disjoint slices
+    _fake_sysfs(str(tmp_path), GPUS)
+    shares = [plan_affinity(lr, [GPUS[lr][0]], list(range(128)), str(tmp_path), local_world=8)["cpus"]
+              for lr in range(8)]
+    assert all(len(s) == 16 for s in shares)
+    assert len({c for s in shares for c in s}) == 128
+
+
+def test_narrowed_view_ignores_non_amd_display_devices(tmp_path):
+    # a management VGA on node 0 (vendor 0x1a03) is no peer of the GPUs there
+    _fake_sysfs(str(tmp_path), GPUS)
+    d = os.path.join(str(tmp_path), "bus", "pci", "devices", "0000:01:00.0")
+    os.makedirs(d)
+    for name, val in (("numa_node", "0"), ("local_cpulist", "0-63"), ("class", "0x030000"), ("vendor", "0x1a03")):
+        with open(os.path.join(d, name), "w") as f:
+            f.write(val + "\n")
+    p = plan_affinity(0, [GPUS[0][0]], list(range(128)), str(tmp_path), local_world=8)
+    assert p["peers"] == 4 and p["cpus"] == list(range(0, 16))
+
+
+class _Props:
+    def __init__(self, bus, dev=0, dom=0, uuid=""):
+        self.pci_bus_id, self.pci_device_id, self.pci_domain_id, self.uuid = bus, dev, dom, uuid
+
+
+def test_gpu_key_uses_pci_address_not_a_shared_uuid():
+    # a ROCm build reporting the same (or an all-zero) UUID for every GPU must
+    # not make distinct GPUs collide; the PCI address keys them
+    from fastapriori_amd.parallel.comm import _gpu_key
+    same = "00000000-0000-0000-0000-000000000000"
+    a = _gpu_key(0, _Props(0x05, uuid=same), host="h")
+    b = _gpu_key(0, _Props(0x15, uuid=same), host="h")
+    assert a != b and a.startswith("fa_gpu/h/pci:0000:05:00.0")
+    # no PCI address: a real UUID keys it; an all-zero one does not
+    assert _gpu_key(0, _Props(0, uuid="GPU-1234abcd"), host="h").endswith("uuid:GPU-1234abcd")
+    assert "uuid" not in _gpu_key(0, _Props(0, uuid=same), host="h")
+
+
+def test_one_gpu_per_rank_check_on_a_store():
+    from datetime import timedelta
+
+    import torch.distributed as dist
+
+    from fastapriori_amd.parallel.comm import _check_one_gpu_per_rank, _gpu_key
+    store = dist.HashStore()
+    store.set_timeout(timedelta(seconds=5))
+    k0 = _gpu_key(0, _Props(0x05), host="h")
+    k1 = _gpu_key(1, _Props(0x15), host="h")
+    _check_one_gpu_per_rank(None, store, k0, rank=0)
+    _check_one_gpu_per_rank(None, store, k1, rank=1)          # another GPU: fine
+    with pytest.raises(RuntimeError, match="shares its GPU"):
+        _check_one_gpu_per_rank(None, store, k0, rank=2)      # a second rank on GPU 0

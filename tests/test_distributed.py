@@ -207,3 +207,29 @@ def test_layout_metrics_ride_on_the_decision_gather(dedup, gathers):
     m.run(sh)
     assert len(calls) == gathers, calls
     assert m.stats["T"] > 0 and 0 < m.stats["distinct"] <= m.stats["T"]
+
+
+def _bucketed_sum(n: int):
+    import torch
+    from fastapriori_amd.parallel.comm import init_comm, shutdown_comm
+    from fastapriori_amd.tuning import TUNING
+    comm = init_comm("cpu")
+    try:
+        g = torch.Generator().manual_seed(5 + comm.rank)
+        t = torch.randint(0, 1 << 20, (n,), generator=g, dtype=torch.int64)
+        one = comm.all_reduce_(t.clone())
+        calls0 = comm.comm_calls
+        TUNING.bucket_mb = 1000 * 8 / (1 << 20)          # ~1000 int64 per bucket: forces bucketing
+        b = comm.bucket_elems(8)
+        buck = comm.all_reduce_(t.clone())
+        return one.tolist(), buck.tolist(), b, comm.comm_calls - calls0, comm.world_size
+    finally:
+        shutdown_comm(comm)
+
+
+def test_bucketed_all_reduce_is_bit_identical():
+    # 3 ranks, a 10,007-entry vector in ~1000-element buckets (a multiple of world_size):
+    # the same sums as one all-reduce of the whole vector
+    for one, buck, b, calls, w in spawn_local(_bucketed_sum, 3, 10_007):
+        assert b % w == 0 and b < 10_007
+        assert buck == one and calls == 1

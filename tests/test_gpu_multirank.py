@@ -63,3 +63,50 @@ def test_eight_ranks_candidate_mode_match_one(ref):
     for o in outs:
         assert o["sets"] == ref["sets"]
         assert o["bundles"] > 0 and o["f2_dev"] and not o["fallbacks"]
+
+
+def _job_rank(d, resume):
+    from fastapriori_amd.config import JobConfig
+    from fastapriori_amd.parallel.comm import init_comm, shutdown_comm
+    from fastapriori_amd.pipeline import run_job
+    comm = init_comm("cuda")
+    try:
+        cfg = JobConfig(input=f"{d}/", output=f"{d}/{'b' if resume else 'a'}_", temp=f"{d}/tmp", min_support=0.02,
+                        device="cuda", resume=resume)
+        s = run_job(cfg, comm)
+        return dict(bundles=s.get("device_bundles", 0), n=s["n_itemsets"])
+    finally:
+        shutdown_comm(comm)
+
+
+def test_two_ranks_device_loop_checkpoint_fault_resume(tmp_path):
+    # only rank 0 writes the device loop's staged checkpoint (level files and
+    # meta.json).  2 gloo ranks on the GPU, an injected crash of rank 0 at the level-3
+    # bundle boundary, then --resume: meta.json counts exactly the level files present,
+    # and the resumed job writes what a fresh world-1 job writes.
+    import json
+    import os
+
+    from fastapriori_amd.config import JobConfig
+    from fastapriori_amd.parallel.comm import Comm
+    from fastapriori_amd.pipeline import run_job
+    from fastapriori_amd.utils.io import write_quest_file
+    write_quest_file(str(tmp_path / "D.dat"), 3000, 9.0, 4.0, 40, 40, seed=3)
+    write_quest_file(str(tmp_path / "U.dat"), 400, 9.0, 4.0, 40, 40, seed=3, users=True)
+    env = {"FA_DIST_BACKEND": "gloo", "FA_FAULT_AT_LEVEL": "3", "FA_FAULT_RANK": "0"}
+    with pytest.raises(RuntimeError, match="InjectedFault"):
+        spawn_local(_job_rank, 2, str(tmp_path), False, env=env, timeout=300)
+    ck = tmp_path / "tmp" / "fastapriori_ckpt"
+    meta = json.load(open(ck / "meta.json"))
+    done = int(meta["levels_done"])
+    assert done == 3 and not meta.get("complete")
+    present = sorted(int(f[6:-4]) for f in os.listdir(ck) if f.startswith("level_") and f.endswith(".npz"))
+    assert present == list(range(1, done + 1)), present
+    outs = spawn_local(_job_rank, 2, str(tmp_path), True, env={"FA_DIST_BACKEND": "gloo"}, timeout=300)
+    assert all(o["bundles"] > 0 for o in outs)
+    import torch
+    run_job(JobConfig(input=f"{tmp_path}/", output=f"{tmp_path}/c_", min_support=0.02, device="cuda"),
+            Comm(device=torch.device("cuda", 0)))
+    for name in ("freqItemset", "recommends"):
+        assert (open(tmp_path / f"b_{name}/part-00000").read()
+                == open(tmp_path / f"c_{name}/part-00000").read())

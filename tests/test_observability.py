@@ -80,3 +80,15 @@ def test_fallbacks_are_reported_by_the_run_that_took_them(tmp_path):
     ar = AssociationRules(res, logger=Logger(0, enabled=False))
     ar.run(parse_bytes(b"1\n2\n"))
     assert "fallbacks" not in ar.stats
+
+
+def test_retired_env_variables_are_reported():
+    # a job script still setting a variable of an earlier version is told
+    # what replaced it, instead of running with the default silently
+    from fastapriori_amd.config import unread_env
+    w = unread_env({"FA_DEDUP": "on", "FA_DL_MULTI": "0", "FA_TUNE": "x=1", "FA_MIN_SUPPORT": "0.1",
+                    "FA_TYPO": "1", "HOME": "/"})
+    assert any(x.startswith("FA_DEDUP is no longer read: use --dedup") for x in w)
+    assert any("FA_DL_MULTI" in x and "dl_multi" in x for x in w)
+    assert any("FA_TYPO" in x and "unknown" in x for x in w)
+    assert not any(x.startswith(("FA_TUNE", "FA_MIN_SUPPORT")) for x in w)
