@@ -212,8 +212,10 @@ def _e2e_window(args, comm, n_txn, min_sup, cfgv, miner_cfg, sync):
         warm.append(ms)
     floor_warm = _pread_floor(path) if comm.is_root else 0.0
     warm_ms = min(warm)
+    rec = _recommend_window(args, comm, d, jc, res, cfgv, sync)
     if comm.is_root:
         shutil.rmtree(out + "freqItemset", ignore_errors=True)
+        shutil.rmtree(out + "recommends", ignore_errors=True)
         shutil.rmtree(tmp, ignore_errors=True)
     if comm.device.type == "cuda":
         torch.cuda.empty_cache()
@@ -232,7 +234,49 @@ def _e2e_window(args, comm, n_txn, min_sup, cfgv, miner_cfg, sync):
         "itemsets_per_s_cold": round(res.n_itemsets / (cold_ms / 1e3), 1),
         "itemsets_per_s_warm": round(res.n_itemsets / (warm_ms / 1e3), 1),
         "n_itemsets": res.n_itemsets,
+        "recommend": rec,
     }, path
+
+
+U_LINES = 1_000_000
+
+
+def _recommend_window(args, comm, d, jc, res, cfgv, sync) -> dict:
+    """The reference's "Total time for get recommends" window (Main.scala:34-37) through
+    the CLI's own function (pipeline.recommend_window): read + parse a U.dat of U_LINES
+    user baskets (Quest transactions of the same config), build the rules from the mined
+    itemsets (generation, cut, sort), recommend, write recommends.  The first run and
+    the best of the warm runs."""
+    from fastapriori_amd.pipeline import recommend_window
+    from fastapriori_amd.utils import io
+    from fastapriori_amd.utils.metrics import Logger
+    _, avg_len, avg_pat, n_pat, n_items, _ = cfgv
+    upath = os.path.join(d, "U.dat")
+    err = ""
+    if comm.is_root and not os.path.exists(upath):
+        try:
+            io.write_quest_file(upath + ".tmp", U_LINES, avg_len, avg_pat, n_pat, n_items, seed=args.seed + 1,
+                                users=True)
+            os.replace(upath + ".tmp", upath)
+        except OSError as e:
+            err = f"{type(e).__name__}: {e}"
+    if comm.allreduce_int(1 if err else 0, "max"):
+        return {"window": "skipped", "error": err or "U.dat could not be written"}
+    quiet = Logger(comm.rank, enabled=False)
+    runs, summ = [], {}
+    for _ in range(1 + max(args.e2e_runs, 1)):
+        sync()
+        t0 = time.perf_counter()
+        summ = {}
+        recommend_window(jc, comm, quiet, res, summ)
+        sync()
+        runs.append(comm.allreduce_float_max((time.perf_counter() - t0) * 1e3))
+    return {"window": "read+parse U.dat, rules (generation, cut, sort), recommend, write recommends "
+                      "(Main.scala:34-37), through pipeline.recommend_window",
+            "U_lines": U_LINES, "U_bytes": os.path.getsize(upath), "first_ms": round(runs[0], 1),
+            "warm_ms": round(min(runs[1:]), 1), "runs_ms": [round(x, 1) for x in runs],
+            "n_rules": summ.get("n_rules"), "n_users": summ.get("n_users"),
+            "n_recommended": summ.get("n_recommended")}
 
 
 def _cpu_ranges(cpus: list) -> str:
@@ -370,6 +414,12 @@ def main() -> int:
             return 3
 
     base = cpu_baseline(args.config, min_sup, n_txn)
+    # correctness at benchmark scale (outside the timed region): the result's digest
+    # (MiningResult.digest: the set of (itemset, count) in token space) against the C++
+    # CPU path's on the same data, when benchmarks/cpu_baselines.json holds one
+    digest = res.digest() if res is not None else None
+    want = base.get("digest") if base else None
+    digest_ok = None if (want is None or digest is None) else digest == want
     if comm.is_root:
         line = {
             "metric": f"itemsets/sec (mining wall-clock), {args.config} min_sup={min_sup:g}",
@@ -388,6 +438,8 @@ def main() -> int:
                           "itemsets_per_s": base["itemsets_per_s"], "ms": base["ms"],
                           "threads": base.get("threads"), "source": "benchmarks/cpu_baselines.json"}
                          if base else None),
+            "digest": digest,
+            "digest_ok": digest_ok,
             "dtype": "int32/uint64-bitmap (exact integer counts)",
             "data": (f"synthetic {'Zipf-topic' if webdocs else 'Quest'} {args.config} "
                      f"(n={n_txn}, seed={args.seed}), generated in-process"),
@@ -406,6 +458,9 @@ def main() -> int:
         }
         print(json.dumps(line), flush=True)
     shutdown_comm(comm)
+    if digest_ok is False:
+        print(f"bench.py: result digest {digest} differs from the CPU path's {want}", file=sys.stderr)
+        return 4
     return 0
 
 

@@ -18,6 +18,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def _ranges(cpus: list) -> str:
+    out, i = [], 0
+    while i < len(cpus):
+        j = i
+        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
+            j += 1
+        out.append(str(cpus[i]) if i == j else f"{cpus[i]}-{cpus[j]}")
+        i = j + 1
+    return ",".join(out)
+
+
 def _rank(n, cfgv, ms):
     import torch
     from fastapriori_amd.models.apriori import FastApriori, MinerConfig
@@ -35,7 +46,13 @@ def _rank(n, cfgv, ms):
         torch.cuda.synchronize()
         tr = comm.trace
         comm.trace = None
-        return dict(rank=comm.rank, n_itemsets=res.n_itemsets, levels=[len(c) for c in res.counts],
+        from fastapriori_amd.parallel.affinity import PLACEMENT
+        from fastapriori_amd.utils.env import num_threads
+        cpus = sorted(os.sched_getaffinity(0))
+        place = dict(numa_node=PLACEMENT.get("node"), peers=PLACEMENT.get("peers"), cpus=_ranges(cpus),
+                     n_cpus=len(cpus), host_threads=num_threads())
+        return dict(rank=comm.rank, n_itemsets=res.n_itemsets, levels=[len(c) for c in res.counts], place=place,
+                    cpu_list=cpus,
                     bundles=int(m.stats.get("device_bundles", 0)), f2_on_device=bool(m.stats.get("f2_on_device")),
                     collectives=tr, calls=len(tr), bytes=int(sum(b for _, b, _ in tr)),
                     digest=hash(tuple(sorted((tuple(sorted(k)), v) for k, v in res.as_dict().items()))))
@@ -62,7 +79,12 @@ def main() -> int:
                           n_itemsets=r0["n_itemsets"], bundles=r0["bundles"], f2_on_device=r0["f2_on_device"],
                           calls_per_run=r0["calls"], bytes_per_rank=r0["bytes"],
                           calls_world1=one["calls"], collectives_rank0=r0["collectives"],
-                          all_ranks_same_calls=len({o["calls"] for o in outs}) == 1)), flush=True)
+                          all_ranks_same_calls=len({o["calls"] for o in outs}) == 1,
+                          # every rank's host placement on this box's real /sys (parallel.affinity:
+                          # the GPU's NUMA node, its CPUs split among the local ranks)
+                          placement=[dict(rank=o["rank"], **o["place"]) for o in outs],
+                          cpu_slices_disjoint=sum(len(o["cpu_list"]) for o in outs)
+                          == len({c for o in outs for c in o["cpu_list"]}))), flush=True)
     return 0 if same else 1
 
 

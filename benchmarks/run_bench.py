@@ -87,7 +87,8 @@ def _cpu(a, cfg):
     return {"metric": f"CPU mining ms (C++ path, {num_threads()} threads), {a.config} min_sup={ms}",
             "n_txn": n, "min_support": ms, "threads": num_threads(), "ms": round(t_ms, 1),
             "runs_ms": [round(t, 1) for t in times], "n_itemsets": res.n_itemsets,
-            "itemsets_per_s": round(res.n_itemsets / (t_ms / 1e3), 1), "torch_threads": torch.get_num_threads()}
+            "itemsets_per_s": round(res.n_itemsets / (t_ms / 1e3), 1), "torch_threads": torch.get_num_threads(),
+            "digest": res.digest()}
 
 
 def main():

@@ -1507,7 +1507,12 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
   const int64_t W = (ncols + 63) >> 6;
   const int64_t nslabs = (W + SW - 1) / SW;
   const int4 z4 = make_int4(0, 0, 0, 0);
-  const int g0 = (int)threadIdx.x;
+  // candidate distribution (flags bits 8-15: this rank, 16-23: ranks - 1): the rank counts
+  // the 64-piece chunks part, part + nparts, ... over all rows, one chunk per wave step, so
+  // a wave still walks 64 consecutive records (the lane deal stays valid)
+  const int ppart = (flags >> 8) & 0xFF, npart = ((flags >> 16) & 0xFF) + 1;
+  const int gstep = kSlabThreads * npart;
+  const int g0 = (ppart + npart * (int)(threadIdx.x >> 6)) * 64 + (int)(threadIdx.x & 63);
   int4 ra = z4, rb = z4, rc = z4;
   if (g0 < G) { ra = rec[3 * g0]; rb = rec[3 * g0 + 1]; rc = rec[3 * g0 + 2]; }
 
@@ -1639,9 +1644,9 @@ __global__ __launch_bounds__(kSlabThreads) void k_count_slab_rec(
     // the record says the piece is a sibling of this thread's previous one (flag 1),
     // p = q & the last prefix row, kept for the next piece of the same prefix (flag 2)
     uint4 p[SW / 2], qv[SW / 2];
-    for (int g = g0; g < G; g += kSlabThreads) {
+    for (int g = g0; g < G; g += gstep) {
       // this thread's next piece (after its last one: its first, for the next slab)
-      const int gn = g + kSlabThreads < G ? g + kSlabThreads : g0;
+      const int gn = g + gstep < G ? g + gstep : g0;
       const int4 na = rec[3 * gn], nb = rec[3 * gn + 1], nc = rec[3 * gn + 2];
       const int n_ext = ra.y & 0xFF, m = (ra.y >> 8) & 0xFF;
       if constexpr (kCls) {
@@ -1873,6 +1878,16 @@ FA_API int fa_hip_count_candidates(const uint64_t* bm, int64_t Wp, int64_t W, co
 // kFlush16 slabs) runs on inputs of a few hundred thousand rows.
 static int g_slab_max_wg = 0;
 FA_API void fa_hip_debug_slab_max_wg(int n) { g_slab_max_wg = n; }
+// Candidate distribution of the slab counts launched next (fastapriori_amd
+// FastApriori._piece_part with --strategy candidate): this rank counts the 64-piece
+// chunks part, part + nparts, ... (k_count_slab_rec flags bits 8-23); (0, 1): every piece.
+static int g_piece_part = 0, g_piece_nparts = 1;
+FA_API int fa_hip_set_piece_part(int part, int nparts) {
+  if (nparts < 1 || nparts > 256 || part < 0 || part >= nparts) return 1;
+  g_piece_part = part;
+  g_piece_nparts = nparts;
+  return 0;
+}
 
 FA_API int fa_hip_count_slab_rec_cls(const int64_t* roff, const int32_t* ranks, const int32_t* src, int64_t ncols,
                                      const int32_t* item_map, int F1, int n_used, const int32_t* gpre,
@@ -1880,6 +1895,9 @@ FA_API int fa_hip_count_slab_rec_cls(const int64_t* roff, const int32_t* ranks, 
                                      int n_wg, const uint64_t* bm, int64_t Wp, hipStream_t st,
                                      const int32_t* bm_rows, const int32_t* g_dev, int cls) {
   if ((G <= 0 && !g_dev) || C <= 0 || ncols <= 0) return 0;
+  // the class-layout flags name a thread's previous piece in the undivided plan: with the
+  // pieces divided among ranks the plain kernel recomputes every prefix instead
+  if (g_piece_nparts > 1) cls &= ~1;
   const bool acc16 = (cls & 4) && !wword;   // two u16 counters per accumulator word
   const int64_t n_acc = acc16 ? (C + 1) / 2 : C;
   const bool contig = !bm && !src;
@@ -1911,7 +1929,7 @@ FA_API int fa_hip_count_slab_rec_cls(const int64_t* roff, const int32_t* ranks, 
 #undef FA_REC_MODE
   if (!kern) return 1;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  const int flags = ((cls & 2) ? 4 : 0) | (acc16 ? 8 : 0);
+  const int flags = ((cls & 2) ? 4 : 0) | (acc16 ? 8 : 0) | (g_piece_part << 8) | ((g_piece_nparts - 1) << 16);
   hipLaunchKernelGGL(kern, dim3((unsigned)n_wg), dim3(kSlabThreads), lds, st, roff, ranks, src, ncols, item_map, F1,
                      n_used, gpre, (const int4*)rec, G, C, wword, out, bm, Wp, bm_rows, flags, g_dev);
   FA_LAUNCH_RET();

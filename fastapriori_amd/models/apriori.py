@@ -86,7 +86,8 @@ class MinerConfig:
     tiebreak: str = "string"        # rank order of equal-count items: string | numeric (utils.jvm.item_tiebreak_key)
     parallelism: str = "count"      # count: rows sharded, counts all-reduced (default)
                                     # candidate: every rank holds the whole DB; pairs split by rows,
-                                    #   level candidates split by rank (FastApriori.scala:98-100,140)
+                                    #   level candidates split by rank: the device bundles' piece
+                                    #   records, the host loop's prefix groups (FastApriori.scala:98-100,140)
 
 
 class FastApriori:
@@ -353,6 +354,13 @@ class FastApriori:
             self._ckpt_saved = K
 
     def _mine_device(self, db, levels: list, counts: list, mc: int, result: MiningResult):
+        self._piece_part(True)
+        try:
+            return self._mine_device_loop(db, levels, counts, mc, result)
+        finally:
+            self._piece_part(False)
+
+    def _mine_device_loop(self, db, levels: list, counts: list, mc: int, result: MiningResult):
         """Level bundles with no host round trip beyond the generator's (csrc/hip/gen.hip
         fa_hip_dl_level0 / fa_hip_dl_more, csrc/hip/levels.hip).
 
@@ -463,6 +471,9 @@ class FastApriori:
                         v = self._count_view(db)
                         cnt = Pm.dl_count(S, plan, v["roff"], v["ranks"], v["src"], v["ncols"], F1, v["wword"])
                     sw = int(plan["sw"])
+                # candidate distribution: the candidates this rank counted (non-zero
+                # before the sum; read back with the results, for the stats)
+                nz = torch.count_nonzero(cnt) if self.cand_par else None
                 with tm.phase("count"), roctx_range("count"):
                     self.comm.all_reduce_(cnt)
                     rows_a, cnt_a, ro, co = Pm.dl_threshold(S, L, cnt, mc, k)
@@ -472,7 +483,7 @@ class FastApriori:
             pend.append(dict(k=k, L=L, m0=m0, C=Cs, rows=rows_a, cnt=cnt_a, ro=ro, co=co, hbm_rows=int(hbm_rows),
                              n_par=S.desc[:L, 5].copy(), sw=sw, used=n_used, T=int(db["roff"].numel() - 1),
                              ms=(time.perf_counter() - t0) * 1e3, bytes=self._bytes_moved() - b0,
-                             G=c[72:72 + L].copy()))
+                             G=c[72:72 + L].copy(), nz=nz))
             P0 = rows_a.data_ptr() + 4 * int(ro[L - 1])
             n_src, n_const, n_bound = S.fsz.data_ptr() + 8 * (k + L - 1), 0, int(Cs[-1])
             m0 += L
@@ -484,6 +495,9 @@ class FastApriori:
             if int(Cs[-1]) < k or (multi is None and int(c[Pm.DL_EMPTY])):
                 break
         self._dl_flush(S, pend, levels, counts, result)
+        if self.cand_par and pend:
+            self.stats["cand_counted"] = int(sum(int(p["nz"]) for p in pend if p["nz"] is not None))
+            self.stats["cand_total"] = int(sum(int(p["C"].sum()) for p in pend))
         self.stats["device_bundles"] = len(pend)
         self.stats["device_levels"] = int(sum(p["L"] for p in pend))
         return nxt
@@ -556,6 +570,20 @@ class FastApriori:
         ext64 = ext.to(torch.int64)
         if bmap is not None:
             prefix, ext64 = bmap[prefix], bmap[ext64]
+        if self.cand_par:
+            # candidate distribution: this rank's extension-balanced range of the groups,
+            # the other counts 0 (the all-reduce assembles them, as _count_level)
+            r, nr = self.comm.rank, self.comm.world_size
+            g0, g1 = (int(np.searchsorted(ext_off, C * q // nr, side="left")) for q in (r, r + 1))
+            g1 = gs.size if r == nr - 1 else g1
+            e0, e1 = int(ext_off[g0]), int(ext_off[g1])
+            cnt = torch.zeros(C, dtype=torch.int32, device=self._dev)
+            if g1 > g0:
+                part = ops.count_candidates(bm, db["W"], prefix[g0:g1].to(torch.int32).contiguous(),
+                                            ext_off[g0:g1 + 1] - e0, ext64[e0:e1].to(torch.int32).contiguous(),
+                                            db["wword"])
+                cnt[e0:e1] = part.to(torch.int32)
+            return cnt
         cnt = ops.count_candidates(bm, db["W"], prefix.to(torch.int32).contiguous(), ext_off,
                                    ext64.to(torch.int32).contiguous(), db["wword"])
         Pm.LAST_LEVEL_PLAN.clear()
@@ -563,9 +591,18 @@ class FastApriori:
         return cnt.to(torch.int32)
 
     def _count_view(self, db) -> dict:
-        """The rows this rank counts: all of its shard (count distribution), or its row
-        slice of the replicated DB (candidate distribution, _cand_rows_view)."""
-        return self._cand_rows_view(db) if self.cand_par else db
+        """The rows the device bundles count: all of this rank's rows -- its shard (count
+        distribution), or the whole replicated DB (candidate distribution: the rank
+        counts its share of the plan's pieces over every row, _piece_part)."""
+        return db
+
+    def _piece_part(self, on: bool) -> None:
+        """Candidate distribution of the device bundles (FastApriori.scala:98-100,140):
+        every slab count launched from here on counts only this rank's chunks of the
+        piece records (count.hip fa_hip_set_piece_part), so each candidate is counted
+        by one rank over all rows and the all-reduce assembles the full vector."""
+        r, n = (self.comm.rank, self.comm.world_size) if (on and self.cand_par) else (0, 1)
+        ops.primitives.set_piece_part(r, n)
 
     def _dl_post_setup(self, S, db, k: int, F1: int, c_bound: int, n_bound: int, lds: int) -> None:
         """Fill the post step of fa_hip_dl_more (ops.primitives.DlPostC): buffers, the
@@ -581,9 +618,8 @@ class FastApriori:
                                             b["out"].data_ptr())
         P.rec_cap, P.part_cap, P.out_cap = b["c_cap"], b["part"].numel(), b["c_cap"]
         P.gpre, P.gpre_cap = b["gpre"].data_ptr(), b["gpre"].numel()
-        # counted rows: the rank's row slice of the replicated DB in candidate mode
-        # (_cand_rows_view); the trimming inputs below stay the whole DB's (every rank
-        # takes the same decision)
+        # counted rows: all of the rank's rows (candidate mode: the whole DB, this rank's
+        # piece chunks, _piece_part); every rank takes the same trimming decision
         v = self._count_view(db)
         P.roff, P.ranks = v["roff"].data_ptr(), v["ranks"].data_ptr()
         P.src = v["src"].data_ptr() if v["src"] is not None else None
@@ -1472,51 +1508,27 @@ class FastApriori:
             cand = nxt
         return bundle
 
-    def _cand_rows_view(self, db) -> dict:
-        """Candidate mode: this rank's 1/W slice of the replicated rows.
-
-        Bundled levels (one launch over many levels' candidates) are split by rows
-        like the k = 2 pairs, not by candidate groups: every rank holds the whole
-        DB, so any split is local, and the row split keeps the bundle kernel's
-        one-launch plans intact.  The all-reduce over the rank group sums the slices.
-        Unweighted rows: a row range (absolute offsets into the shared ranks);
-        weighted (dedup) layout: a range of 64-column words."""
-        key = (id(db["roff"]), db["T"], db["ncols"], id(db["src"]))
-        if getattr(self, "_cand_view_key", None) == key:
-            return self._cand_view
-        r, nr = self.comm.rank, self.comm.world_size
-        v = dict(db)
-        v.update(bm=None, W=0, bm_items=None, bm_map=None)
-        if db["src"] is None:
-            T = db["T"]
-            a, b = T * r // nr, T * (r + 1) // nr
-            v.update(roff=db["roff"][a:b + 1], T=b - a, ncols=b - a)
-        else:
-            W = (db["ncols"] + 63) // 64
-            w0, w1 = W * r // nr, W * (r + 1) // nr
-            v.update(src=db["src"][64 * w0:64 * w1].contiguous(), ncols=64 * (w1 - w0),
-                     wword=db["wword"][w0:w1].contiguous())
-        self._cand_view_key, self._cand_view = key, v
-        return v
-
     def _count_bundle(self, db, bundle: list) -> list:
         """Counts of every level of a bundle (one launch on the GPU).  The all-reduce is
-        over the rank group in both modes: row shards (count mode) or this rank's row
-        slice of the replicated DB (candidate mode, _cand_rows_view)."""
+        over the rank group in both modes: row shards (count mode) or this rank's share
+        of the plan's pieces over the whole replicated DB (candidate mode, _piece_part)."""
         if len(bundle) == 1 or db["ranks"].device.type != "cuda":
             return [self._count_level(db, pv, pi, eo, ex) for _, pv, pi, eo, ex in bundle]
         full_db = db
-        if self.cand_par:
-            db = self._cand_rows_view(db)
         pre = [pv[pi] for _, pv, pi, _, _ in bundle]
         poff = np.concatenate([[0], np.cumsum(np.concatenate([np.full(p.shape[0], p.shape[1]) for p in pre]))])
         flat = np.concatenate([p.ravel() for p in pre]).astype(np.int32)
         sizes = [int(ex.size) for *_, ex in bundle]
         eoff = np.concatenate([[0], np.cumsum(np.concatenate([np.diff(eo) for _, _, _, eo, _ in bundle]))])
         ext = np.concatenate([ex for *_, ex in bundle]).astype(np.int32)
-        cnt = ops.count_level(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"], flat, eoff, ext,
-                              db["wword"], kernel="slab", poff=poff, full_bm=lambda u: self._bitmaps(db, u, blocked=True),
-                              sup_frac=self.stats["min_count"] / max(1, self.stats["n_lines"]))
+        self._piece_part(True)
+        try:
+            cnt = ops.count_level(db["roff"], db["ranks"], db["src"], db["ncols"], db["F1"], flat, eoff, ext,
+                                  db["wword"], kernel="slab", poff=poff,
+                                  full_bm=lambda u: self._bitmaps(db, u, blocked=True),
+                                  sup_frac=self.stats["min_count"] / max(1, self.stats["n_lines"]))
+        finally:
+            self._piece_part(False)
         if cnt is None:
             return [self._count_level(full_db, pv, pi, eo, ex) for _, pv, pi, eo, ex in bundle]
         self.comm.all_reduce_(cnt, bound=self.stats["n_lines"])

@@ -136,6 +136,31 @@ class MiningResult:
     def n_itemsets(self) -> int:
         return int(sum(len(c) for c in self.counts))
 
+    def digest(self) -> str:
+        """SHA-256 (hex) of the result as a set of (itemset, count) in token space:
+        independent of the rank order of equal-count items (--tiebreak), of the level
+        row order and of the device that mined it, so a GPU run at benchmark scale can be
+        checked against the C++ CPU path's digest (benchmarks/cpu_baselines.json).
+        Items are numbered by their tokens' sorted order; every itemset becomes its
+        ascending item numbers, rows are sorted, and each level hashes as
+        (k, F_k, rows int32 LE, counts int64 LE) after the sorted token list."""
+        import hashlib
+        toks = [str(t) for t in self.items]
+        order = sorted(range(len(toks)), key=lambda r: toks[r])
+        canon = np.empty(max(len(toks), 1), dtype=np.int32)
+        canon[np.asarray(order, dtype=np.int64)] = np.arange(len(toks), dtype=np.int32)
+        h = hashlib.sha256()
+        h.update("\n".join(toks[r] for r in order).encode("utf-8", "surrogatepass") + b"\0")
+        for k, (rows, cnt) in enumerate(zip(self.levels, self.counts), 1):
+            rows = np.asarray(rows, dtype=np.int64).reshape(-1, k)
+            cnt = np.asarray(cnt, dtype=np.int64).ravel()
+            c = np.sort(canon[rows], axis=1) if rows.size else np.zeros((0, k), np.int32)
+            idx = np.lexsort(c.T[::-1]) if len(c) else np.zeros(0, np.int64)
+            h.update(np.array([k, len(c)], dtype="<i8").tobytes())
+            h.update(np.ascontiguousarray(c[idx], dtype="<i4").tobytes())
+            h.update(np.ascontiguousarray(cnt[idx], dtype="<i8").tobytes())
+        return h.hexdigest()
+
     def as_dict(self) -> dict[frozenset, int]:
         out = {}
         for rows, cnt in zip(self.levels, self.counts):

@@ -95,6 +95,7 @@ _HIP_SIGS = {
     "fa_hip_dl_plan": (C.c_int, [vp, C.c_int, vp, C.c_int, vp, vp, i64, vp, i64, vp, i64, C.c_int, vp]),
     "fa_hip_set_lane_deal": (None, [C.c_int]),
     "fa_hip_set_cap_max": (None, [C.c_int]),
+    "fa_hip_set_piece_part": (C.c_int, [C.c_int, C.c_int]),
     "fa_hip_dl_gpre_need": (i64, [vp, C.c_int]),
     "fa_hip_dl_plan_window": (C.c_int, [vp, C.c_int, vp, C.c_int, vp, vp, i64, vp, i64, vp, i64, i64, i64, C.c_int,
                                         vp]),

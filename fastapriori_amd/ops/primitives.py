@@ -1625,6 +1625,12 @@ def dl_bundle_gen(S: DeviceLevelState, P0: int, n_src: int | None, n_const: int,
     raise RuntimeError("device bundle generation: workspace sizing did not converge")
 
 
+def set_piece_part(part: int, nparts: int) -> None:
+    """The share of the piece records the slab counts launched from now on count
+    (count.hip fa_hip_set_piece_part: 64-piece chunks part, part + nparts, ...); (0, 1): all."""
+    _native.check(_native.hip().fa_hip_set_piece_part(int(part), int(nparts)), "fa_hip_set_piece_part")
+
+
 def lane_deal(lib, rows: int) -> None:
     """Bank-aware lane deal of the next device plans (levels.hip k_dl_lane_assign) for a
     count over this many rows: on from TUNING.lane_deal_min_rows (its fixed cost is

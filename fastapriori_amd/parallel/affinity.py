@@ -122,10 +122,20 @@ def bind_local_rank(dev, local_rank: int, local_world: int, sysfs: str = "/sys")
         return PLACEMENT
     import torch
     n = torch.cuda.device_count()
+    narrowed = any(os.environ.get(v) for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES",
+                                               "CUDA_VISIBLE_DEVICES"))
     try:
-        bdfs = [gpu_bdf(torch.cuda.get_device_properties(i)) for i in range(n)] if n == local_world else \
-            [gpu_bdf(torch.cuda.get_device_properties(dev))]
-        idx = local_rank if n == local_world else 0
+        if n == local_world:
+            bdfs = [gpu_bdf(torch.cuda.get_device_properties(i)) for i in range(n)]
+            idx = local_rank
+        elif n == 1 and local_world > 1 and not narrowed:
+            # every local rank on the one visible GPU (gloo ranks sharing a card: tests, the
+            # multi-rank rehearsal): the node's CPUs split among all of them
+            bdfs = [gpu_bdf(torch.cuda.get_device_properties(dev))] * local_world
+            idx = local_rank
+        else:
+            bdfs = [gpu_bdf(torch.cuda.get_device_properties(dev))]
+            idx = 0
         plan = plan_affinity(idx, bdfs, sorted(os.sched_getaffinity(0)), sysfs, local_world)
     except (RuntimeError, AttributeError, ValueError, OSError):
         return PLACEMENT

@@ -98,6 +98,22 @@ def mine_window(cfg: JobConfig, comm, log: Logger, ckpt: Checkpointer | None, su
     return result
 
 
+def recommend_window(cfg: JobConfig, comm, log: Logger, result, summary: dict) -> list:
+    """The reference's second timed window (Main.scala:34-37): read + parse U.dat,
+    rules (generation, cut, sort), one recommendation per user line, write
+    recommends.  bench.py times this same function for its e2e record."""
+    users = io.read_shard(cfg.input + "U.dat", comm)
+    ar = AssociationRules(result, comm, log)
+    recs = ar.run(users)
+    if comm.is_root:
+        io.write_lines(recs, cfg.output + "recommends", overwrite=cfg.overwrite)
+    comm.barrier()
+    summary["n_rules"] = ar.rules().n_rules
+    if recs is not None:                   # rank 0 holds every user's recommendation
+        summary.update(n_users=len(recs), n_recommended=sum(1 for r in recs if r != "0"))
+    return recs
+
+
 def make_checkpointer(cfg: JobConfig, comm) -> Checkpointer | None:
     if cfg.temp and (cfg.checkpoint or cfg.rules_only):
         # rules-only needs no D.dat: it reloads the mined itemsets (Utils.getAll's use case)
@@ -116,8 +132,6 @@ def run_job(cfg: JobConfig, comm=None) -> dict:
             shutdown_comm(comm)
         raise RuntimeError(f"--world-size {cfg.world_size} but the process group has {comm.world_size} ranks")
     log = Logger(comm.rank, metrics_path=cfg.metrics_path)
-    u_path = cfg.input + "U.dat"
-    out_rec = cfg.output + "recommends"
     summary: dict = {}
     ckpt = None
     try:
@@ -142,16 +156,11 @@ def run_job(cfg: JobConfig, comm=None) -> dict:
         log.line(f"Total time for get freqItemsets {t_mine}")
 
         t2 = time.time()
-        users = io.read_shard(u_path, comm)
-        ar = AssociationRules(result, comm, log)
-        recs = ar.run(users)
-        if comm.is_root:
-            io.write_lines(recs, out_rec, overwrite=cfg.overwrite)
-        comm.barrier()
+        recommend_window(cfg, comm, log, result, summary)
         t_rec = int((time.time() - t2) * 1000)
         log.line(f"Total time for get recommends {t_rec}")
         summary.update(mine_ms=t_mine, recommend_ms=t_rec, n_itemsets=result.n_itemsets,
-                       n_rules=ar.rules().n_rules, world_size=comm.world_size)
+                       world_size=comm.world_size)
         log.metric(phase="job", **{k: v for k, v in summary.items() if not isinstance(v, dict)})
         return summary
     except BaseException as e:

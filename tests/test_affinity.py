@@ -121,3 +121,13 @@ def test_one_gpu_per_rank_check_on_a_store():
     _check_one_gpu_per_rank(None, store, k1, rank=1)          # another GPU: fine
     with pytest.raises(RuntimeError, match="shares its GPU"):
         _check_one_gpu_per_rank(None, store, k0, rank=2)      # a second rank on GPU 0
+
+
+def test_ranks_sharing_one_gpu_split_its_node(tmp_path):
+    # gloo ranks sharing the one visible GPU (the multi-rank rehearsal): bind_local_rank
+    # plans with that GPU repeated per local rank, so the node's CPUs split 8 ways
+    _fake_sysfs(str(tmp_path), GPUS)
+    bdfs = [GPUS[5][0]] * 8
+    shares = [plan_affinity(lr, bdfs, list(range(128)), str(tmp_path))["cpus"] for lr in range(8)]
+    assert all(len(s) == 8 for s in shares)
+    assert len({c for s in shares for c in s}) == 64 and set().union(*shares) == set(range(64, 128))

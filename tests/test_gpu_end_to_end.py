@@ -118,8 +118,9 @@ def test_two_ranks_share_gpu_match_one():
 
 @pytest.mark.parametrize("dedup", ["off", "on"])
 def test_two_ranks_share_gpu_candidate_mode(dedup):
-    # candidate distribution with level bundles counted on each rank's row slice of the
-    # replicated DB (FastApriori._cand_rows_view: row ranges, or word ranges when dedup)
+    # candidate distribution: each rank counts its blocks of the device bundles' piece
+    # records over the whole replicated DB (FastApriori._piece_part), unit and weighted
+    # (dedup) layouts
     ref = spawn_local(_gpu_rank, 1, 40000, 0.005, "count", dedup, env={"FA_DIST_BACKEND": "gloo"})[0]
     outs = spawn_local(_gpu_rank, 2, 40000, 0.005, "candidate", dedup, env={"FA_DIST_BACKEND": "gloo"})
     assert outs[0] == ref and outs[1] == ref

@@ -26,6 +26,7 @@ def _rank(n, ms, par):
         c0, b0 = comm.comm_calls, comm.bytes_reduced
         res = m.run(sh)
         return dict(sets=res.as_dict(), bundles=int(m.stats.get("device_bundles", 0)),
+                    cand_counted=m.stats.get("cand_counted"), cand_total=m.stats.get("cand_total"),
                     f2_dev=bool(m.stats.get("f2_on_device", False)), calls=comm.comm_calls - c0,
                     bytes=comm.bytes_reduced - b0, fallbacks=list(ops.primitives.FALLBACKS),
                     world=comm.world_size)
@@ -63,6 +64,13 @@ def test_eight_ranks_candidate_mode_match_one(ref):
     for o in outs:
         assert o["sets"] == ref["sets"]
         assert o["bundles"] > 0 and o["f2_dev"] and not o["fallbacks"]
+    # each rank counted its own ~1/8 of the bundles' candidates (over all rows), not all
+    # of them over 1/8 of the rows: the ranks' non-zero local counts add up to at most
+    # the candidates, and no rank holds much more than its share
+    tot = outs[0]["cand_total"]
+    counted = [o["cand_counted"] for o in outs]
+    assert tot > 8 * 512 and sum(counted) <= tot, (tot, counted)
+    assert max(counted) <= tot / 8 * 1.5 + 512 and min(counted) > 0, (tot, counted)
 
 
 def _job_rank(d, resume):
