@@ -76,6 +76,8 @@ def parse_args(argv=None):
                          "(auto: on for file-backed configs)")
     ap.add_argument("--e2e-runs", type=int, default=2, help="warm-cache e2e runs after the cold one")
     ap.add_argument("--workdir", default="", help="where the e2e D.dat is written (default $TMPDIR)")
+    ap.add_argument("--no-digest-check", action="store_true",
+                    help="report the result digest without failing on a mismatch (timing-only kernel variants)")
     return ap.parse_args(argv)
 
 
@@ -458,7 +460,7 @@ def main() -> int:
         }
         print(json.dumps(line), flush=True)
     shutdown_comm(comm)
-    if digest_ok is False:
+    if digest_ok is False and not args.no_digest_check:
         print(f"bench.py: result digest {digest} differs from the CPU path's {want}", file=sys.stderr)
         return 4
     return 0
