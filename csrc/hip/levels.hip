@@ -54,9 +54,8 @@ __device__ __forceinline__ int dl_level_of(const DlLevels& D, int64_t t) {
 }
 
 // rank -> slab row from the used-item bitset (one wave; lane l owns words 8l .. 8l+7)
-__global__ __launch_bounds__(64) void k_dl_map(const long long* __restrict__ c, int F1, int32_t* __restrict__ item_map) {
+__global__ __launch_bounds__(64) void k_dl_map(const uint64_t* __restrict__ mk, int F1, int32_t* __restrict__ item_map) {
   __shared__ int pre[512];
-  const uint64_t* mk = reinterpret_cast<const uint64_t*>(c + kDlBitsN);
   const int lane = threadIdx.x;
   const int nwd = (F1 + 63) >> 6;
   int cnt8[8], tot = 0;
@@ -551,6 +550,10 @@ using namespace fa;
 FA_API int fa_hip_dl_plan_window(const int64_t* desc, int L, long long* ctl, int F1, int32_t* item_map, void* rec,
                                  int64_t max_pieces, int32_t* part, int64_t part_cap, int32_t* gpre,
                                  int64_t gpre_cap, int64_t w0, int64_t w1, int sw, hipStream_t st);
+FA_API int fa_hip_dl_plan_window_bits(const int64_t* desc, int L, long long* ctl, int F1, const uint64_t* used_bits,
+                                      int32_t* item_map, void* rec, int64_t max_pieces, int32_t* part,
+                                      int64_t part_cap, int32_t* gpre, int64_t gpre_cap, int64_t w0, int64_t w1,
+                                      int sw, hipStream_t st);
 
 // Bank-aware lane deal of the plans queued next (k_dl_lane_assign): on / off, set by
 // fastapriori_amd.ops.primitives before the plans are queued (TUNING.lane_deal_min_rows).
@@ -575,6 +578,17 @@ FA_API int fa_hip_dl_plan(const int64_t* desc, int L, long long* ctl, int F1, in
 FA_API int fa_hip_dl_plan_window(const int64_t* desc, int L, long long* ctl, int F1, int32_t* item_map, void* rec,
                                  int64_t max_pieces, int32_t* part, int64_t part_cap, int32_t* gpre,
                                  int64_t gpre_cap, int64_t w0, int64_t w1, int sw, hipStream_t st) {
+  return fa_hip_dl_plan_window_bits(desc, L, ctl, F1, nullptr, item_map, rec, max_pieces, part, part_cap, gpre,
+                                    gpre_cap, w0, w1, sw, st);
+}
+
+// ... with the window's own used items (used_bits: device bitset of F1 bits, e.g. the OR
+// of fa_hip_dl_chunk_bits' chunks of the window; nullptr: the level's, ctl's bitset):
+// the slab rows of the window are only the items its candidates use
+FA_API int fa_hip_dl_plan_window_bits(const int64_t* desc, int L, long long* ctl, int F1, const uint64_t* used_bits,
+                                      int32_t* item_map, void* rec, int64_t max_pieces, int32_t* part,
+                                      int64_t part_cap, int32_t* gpre, int64_t gpre_cap, int64_t w0, int64_t w1,
+                                      int sw, hipStream_t st) {
   DlLevels D;
   if (dl_levels(desc, L, &D, gpre, gpre_cap)) return 1;
   if (F1 < 1 || F1 > 32768) return 1;
@@ -587,7 +601,8 @@ FA_API int fa_hip_dl_plan_window(const int64_t* desc, int L, long long* ctl, int
   const int64_t R = D.rbase[L];
   const int64_t nblk = std::max<int64_t>(1, (R + kDlPB - 1) / kDlPB);
   if (part_cap < 8 * nblk) return 1;
-  hipLaunchKernelGGL(k_dl_map, dim3(1), dim3(64), 0, st, ctl, F1, item_map);
+  const uint64_t* mk = used_bits ? used_bits : reinterpret_cast<const uint64_t*>(ctl + kDlBitsN);
+  hipLaunchKernelGGL(k_dl_map, dim3(1), dim3(64), 0, st, mk, F1, item_map);
   hipLaunchKernelGGL(k_dl_pieces_count, dim3((unsigned)nblk), dim3(kDlPB), 0, st, D, part);
   hipLaunchKernelGGL(k_dl_pieces_scan, dim3(1), dim3(1024), 0, st, part, nblk, ctl);
   hipLaunchKernelGGL(k_dl_pieces_emit, dim3((unsigned)nblk), dim3(kDlPB), 0, st, D, part, item_map,
@@ -598,6 +613,36 @@ FA_API int fa_hip_dl_plan_window(const int64_t* desc, int L, long long* ctl, int
       hipLaunchKernelGGL(k_dl_lane_assign, dim3((unsigned)nwin), dim3(64), 0, st, static_cast<int4*>(rec), ctl,
                          (sw + 2) / 2);
   }
+  FA_LAUNCH_RET();
+}
+
+// Used-item bitset of every chunk of `chunk` candidates of a single-level plan's
+// candidate rows (desc level 0: rows [C][m + 1]): out[j * nwd .. (j + 1) * nwd) for
+// chunk j (nwd = ceil(F1 / 64) <= 512).  The window planner of a multi-pass level
+// (ops.primitives.dl_count_multipass) grows each window chunk by chunk while its
+// candidates fit the accumulators left by its own used items' slab rows.
+__global__ __launch_bounds__(256) void k_dl_chunk_bits(const int32_t* __restrict__ rows, int64_t C, int w, int chunk,
+                                                       int nwd, unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long lb[512];
+  for (int i = threadIdx.x; i < nwd; i += 256) lb[i] = 0ull;
+  __syncthreads();
+  const int64_t c0 = (int64_t)blockIdx.x * chunk, c1 = min(C, c0 + chunk);
+  for (int64_t e = c0 * w + threadIdx.x; e < c1 * w; e += 256) {
+    const int r = rows[e];
+    atomicOr(&lb[r >> 6], 1ull << (r & 63));
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nwd; i += 256) out[(int64_t)blockIdx.x * nwd + i] = lb[i];
+}
+
+FA_API int fa_hip_dl_chunk_bits(const int64_t* desc, int F1, int chunk, uint64_t* out, hipStream_t st) {
+  const int nwd = (F1 + 63) / 64;
+  const int64_t C = desc[6];
+  if (F1 < 1 || nwd > 512 || chunk < 1 || C < 1) return 1;
+  const int32_t* rows = reinterpret_cast<const int32_t*>((intptr_t)desc[3]);
+  const int64_t nch = (C + chunk - 1) / chunk;
+  hipLaunchKernelGGL(k_dl_chunk_bits, dim3((unsigned)nch), dim3(256), 0, st, rows, C, (int)desc[4] + 1, chunk, nwd,
+                     reinterpret_cast<unsigned long long*>(out));
   FA_LAUNCH_RET();
 }
 

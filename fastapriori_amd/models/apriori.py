@@ -541,7 +541,8 @@ class FastApriori:
             bm_rows = (bmap[used_t] if bmap is not None else used_t).to(torch.int32).contiguous()
             cnt = Pm.dl_count_multipass(S, F1, n_used, C0, lds, v["roff"], v["ranks"], v["src"], v["ncols"],
                                         v["wword"], bm, bm_rows,
-                                        self.stats["min_count"] / max(1, self.stats["n_lines"]), self._dev)
+                                        self.stats["min_count"] / max(1, self.stats["n_lines"]), self._dev,
+                                        bmap=bmap)
         if cnt is None:
             return None
         self.stats["device_multipass"] = self.stats.get("device_multipass", 0) + 1

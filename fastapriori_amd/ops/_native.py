@@ -99,6 +99,9 @@ _HIP_SIGS = {
     "fa_hip_dl_gpre_need": (i64, [vp, C.c_int]),
     "fa_hip_dl_plan_window": (C.c_int, [vp, C.c_int, vp, C.c_int, vp, vp, i64, vp, i64, vp, i64, i64, i64, C.c_int,
                                         vp]),
+    "fa_hip_dl_plan_window_bits": (C.c_int, [vp, C.c_int, vp, C.c_int, vp, vp, vp, i64, vp, i64, vp, i64, i64, i64,
+                                             C.c_int, vp]),
+    "fa_hip_dl_chunk_bits": (C.c_int, [vp, C.c_int, C.c_int, vp, vp]),
     "fa_hip_dl_threshold": (C.c_int, [vp, C.c_int, vp, i64, vp, vp, vp, vp, vp, vp, i64, vp]),
     "fa_hip_trim_scan_count": (C.c_int, [vp, vp, i64, vp, C.c_int, C.c_int, vp, vp, vp, vp, vp]),
     "fa_hip_trim_emit": (C.c_int, [vp, vp, vp, C.c_int, i64, vp, vp, vp, vp, vp, vp, vp, vp]),

@@ -1662,24 +1662,35 @@ def dl_plan(S: DeviceLevelState, L: int, F1: int, n_used: int, C: int, lds: int,
 
 
 def dl_count_multipass(S: DeviceLevelState, F1: int, n_used: int, C: int, lds: int, roff, ranks, src, ncols: int,
-                       wword, bm, bm_rows, sup_frac: float, dev) -> torch.Tensor | None:
+                       wword, bm, bm_rows, sup_frac: float, dev, bmap=None) -> torch.Tensor | None:
     """Counts of a device bundle's single level whose C candidates exceed one
-    accumulator pass: per window of cap candidates, a device plan of that window
-    (levels.hip fa_hip_dl_plan_window) and a slab count from the used items' bitmap
-    (bm [n_used or more][Wp]; bm_rows: slab row -> bitmap row, device int32, or None
-    when bitmap row u is slab row u).  sup_frac: minimum support / rows (count_level's
-    dense test).  Returns int32 [C] (not reduced across ranks), or None when no slab
-    width fits the used items."""
+    accumulator pass: per window of candidates, a device plan of that window
+    (levels.hip fa_hip_dl_plan_window[_bits]) and a slab count from the used items'
+    bitmap (bm [n_used or more][Wp]; bm_rows: slab row -> bitmap row, device int32, or
+    None when bitmap row u is slab row u).  sup_frac: minimum support / rows
+    (count_level's dense test).  Returns int32 [C] (not reduced across ranks), or None
+    when no slab width fits the used items.
+
+    TUNING.mp_window_items: every window's slab holds only the items ITS candidates
+    use (bmap: device rank -> bitmap row, None = rank-indexed bitmap), and windows grow
+    chunk by chunk (dl_window_plan) while their candidates fit what those rows leave
+    of the LDS: deep T40I10 levels use 2-3x fewer items per window than per level, so
+    every pass copies fewer slab rows and fewer passes are needed."""
     acc16 = TUNING.dl_acc16 and wword is None
     accb = 2 if acc16 else 4
     sw, cap = dl_slab_width(n_used, min(C, 8192), lds, accb)
     if sw == 0:
         return None
-    dense = wword is None and TUNING.dense_min_rows > 0 and sup_frac * sw * 64 >= TUNING.dense_min_rows
-    cap = min(cap, C)
-    cap = -(-C // -(-C // cap))                      # equal windows
     st = _stream(ranks)
     lib = _native.hip()
+    wins = None
+    if TUNING.mp_window_items:
+        wins = dl_window_plan(S, F1, C, lds, accb, st, dev)
+    if not wins:
+        cap = min(cap, C)
+        cap = -(-C // -(-C // cap))                      # equal windows
+        wins = [(w0, min(C, w0 + cap), sw, None) for w0 in range(0, C, cap)]
+    cap = max(w1 - w0 for w0, w1, _, _ in wins)
     item_map = torch.empty(max(F1, 1), dtype=_I32, device=dev)
     rec = torch.empty(12 * cap + 12, dtype=_I32, device=dev)
     R = int(S.desc[0, 5])
@@ -1688,25 +1699,73 @@ def dl_count_multipass(S: DeviceLevelState, F1: int, n_used: int, C: int, lds: i
     gpre = torch.empty(max(gn, 1), dtype=_I32, device=dev)
     out = torch.zeros(C, dtype=_I32, device=dev)
     W = (ncols + 63) // 64
-    nslabs = (W + sw - 1) // sw
-    npass = 0
+    npass, used_sum = 0, 0
     lane_deal(lib, ncols)
-    for w0 in range(0, C, cap):
-        w1 = min(C, w0 + cap)
-        _native.check(lib.fa_hip_dl_plan_window(S.desc.ctypes.data, 1, _p(S.ctl), F1, _p(item_map), _p(rec), cap,
-                                                _p(part), part.numel(), _p(gpre), gpre.numel(), w0, w1, sw, st),
-                      "fa_hip_dl_plan_window")
+    for w0, w1, wsw, bits in wins:
+        nu, rows_w, bits_p = n_used, bm_rows, None
+        if bits is not None:
+            used_w = np.flatnonzero(np.unpackbits(bits.view(np.uint8), bitorder="little")[:F1])
+            nu = int(used_w.size)
+            bits_t = torch.from_numpy(bits.view(np.int64).copy()).to(dev, non_blocking=False)
+            used_t = torch.from_numpy(used_w.astype(np.int64)).to(dev)
+            rows_w = (bmap[used_t] if bmap is not None else used_t).to(_I32).contiguous()
+            bits_p = bits_t
+        dense = wword is None and TUNING.dense_min_rows > 0 and sup_frac * wsw * 64 >= TUNING.dense_min_rows
+        nslabs = (W + wsw - 1) // wsw
+        _native.check(lib.fa_hip_dl_plan_window_bits(S.desc.ctypes.data, 1, _p(S.ctl), F1, _p(bits_p), _p(item_map),
+                                                     _p(rec), cap, _p(part), part.numel(), _p(gpre), gpre.numel(),
+                                                     w0, w1, wsw, st), "fa_hip_dl_plan_window_bits")
         nacc = (w1 - w0 + 1) // 2 if acc16 else w1 - w0
-        lds_k = n_used * (sw + 2) * 8 + ((nacc + 3) & ~3) * 4
+        lds_k = nu * (wsw + 2) * 8 + ((nacc + 3) & ~3) * 4
         n_wg = int(max(1, min(nslabs, 256 * min(max(1, TUNING.slab_lds_bytes // lds_k), 2))))
-        _hip_call("fa_hip_count_slab_rec_cls", _p(roff), _p(ranks), _p(src), ncols, _p(item_map), F1, n_used,
-                  _p(gpre), _p(rec), 0, w1 - w0, _p(wword), out.data_ptr() + 4 * w0, sw, n_wg, _p(bm),
-                  bitmap_ld(bm), st, _p(bm_rows), _p(S.ctl) + 8 * 221, (2 if dense else 0) | (4 if acc16 else 0))
+        _hip_call("fa_hip_count_slab_rec_cls", _p(roff), _p(ranks), _p(src), ncols, _p(item_map), F1, nu,
+                  _p(gpre), _p(rec), 0, w1 - w0, _p(wword), out.data_ptr() + 4 * w0, wsw, n_wg, _p(bm),
+                  bitmap_ld(bm), st, _p(rows_w), _p(S.ctl) + 8 * 221, (2 if dense else 0) | (4 if acc16 else 0))
         npass += 1
+        used_sum += nu
     LAST_LEVEL_PLAN.clear()
     LAST_LEVEL_PLAN.update(kernel="slab_dev_multi", rows=int(roff.numel() - 1), used=n_used, sw=sw, cap=cap,
-                           passes=npass, pieces=-1, slab_reads=0, m=int(S.desc[0, 4]), C=C, dense=bool(dense))
+                           passes=npass, pieces=-1, slab_reads=0, m=int(S.desc[0, 4]), C=C,
+                           window_used_avg=round(used_sum / max(npass, 1), 1))
     return out
+
+
+def dl_window_plan(S: DeviceLevelState, F1: int, C: int, lds: int, accb: int, st: int, dev,
+                   chunk: int = 1024) -> list | None:
+    """Windows of a multi-pass level's C candidates (device bundle level 0) sized by their
+    own used items: the used-item bitset of every chunk of candidates
+    (levels.hip fa_hip_dl_chunk_bits, one small readback), then, greedily, the longest run
+    of chunks whose item union leaves accumulators for all of its candidates at the
+    widest slab holding min(candidates, 8192) (dl_slab_width).  Returns [(w0, w1, sw,
+    uint64 bitset [nwd])], or None when F1 is too wide for the bitsets."""
+    nwd = (F1 + 63) // 64
+    if nwd > 512 or C < 1:
+        return None
+    nch = -(-C // chunk)
+    bits_d = torch.empty(nch * nwd, dtype=_I64, device=dev)
+    _native.check(_native.hip().fa_hip_dl_chunk_bits(S.desc.ctypes.data, F1, chunk, _p(bits_d), st),
+                  "fa_hip_dl_chunk_bits")
+    bits = bits_d.cpu().numpy().view(np.uint64).reshape(nch, nwd)
+    pop8 = np.array([bin(i).count("1") for i in range(256)], dtype=np.int64)
+    wins = []
+    j = 0
+    while j < nch:
+        acc = np.zeros(nwd, dtype=np.uint64)
+        k, best = j, None
+        while k < nch:
+            a2 = acc | bits[k]
+            n = int(pop8[a2.view(np.uint8)].sum())
+            cand = min((k + 1) * chunk, C) - j * chunk
+            sw, cap = dl_slab_width(n, min(cand, 8192), lds, accb)
+            if sw == 0 or cap < cand:
+                break
+            acc, best = a2, sw
+            k += 1
+        if best is None:
+            return None                              # one chunk does not fit: the level-wide windows
+        wins.append((j * chunk, min(k * chunk, C), best, acc))
+        j = k
+    return wins
 
 
 def dl_plan_from_post(S: DeviceLevelState, n_used: int) -> dict:

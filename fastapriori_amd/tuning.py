@@ -50,6 +50,7 @@ class Tuning:
     dense_min_rows: float = 4.0         # skip the all-zero-prefix test above this many rows per slab
     dl_acc16: bool = True               # packed u16 accumulators in window-by-window levels (unit weights)
     dl_acc16_bundles: bool = False      # ... and in one-pass device bundles
+    mp_window_items: bool = True        # window-by-window levels: each window's slab holds only its own used items
     # bundle capacity = the largest over the slab widths (a bundle takes a narrower slab
     # when that holds all of it) instead of the first width holding 8192 candidates
     slab_cap_max: bool = False
