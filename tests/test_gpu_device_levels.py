@@ -232,3 +232,18 @@ def test_lane_deal_keeps_counts(tune):
         got, st = _mine(g, ms)
         assert st.get("device_bundles", 0) >= 1
         _same(got, ref)
+
+
+def test_window_items_keep_counts(tune):
+    # window-by-window levels whose windows hold only their own used items
+    # (TUNING.mp_window_items, ops.primitives.dl_window_plan): every level identical to
+    # the level-wide windows, on the T40 shape
+    cpu = generate_shard(150_000, Comm(), "cpu", 40.0, 10.0, 2000, 1000, 3)
+    g = cpu.to(DEV)
+    tune(mp_window_items=False)
+    ref, _ = _mine(g, 0.006)
+    tune(mp_window_items=True)
+    got, st = _mine(g, 0.006)
+    assert st.get("device_multipass", 0) >= 1 and "fallbacks" not in st, st
+    assert len(ref.levels) >= 6
+    _same(got, ref)
