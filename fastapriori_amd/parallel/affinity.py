@@ -148,3 +148,36 @@ def bind_local_rank(dev, local_rank: int, local_world: int, sysfs: str = "/sys")
             env.set_num_threads(plan["threads"])
     PLACEMENT.update(plan)
     return PLACEMENT
+
+
+def shared_slice(cpus: list[int], idx: int, n: int) -> list[int]:
+    """Sharer idx of n's part of a GPU's CPU slice (at least one CPU each)."""
+    part = cpus[idx * len(cpus) // n:(idx + 1) * len(cpus) // n]
+    return part or [cpus[idx % len(cpus)]]
+
+
+def refine_for_shared_gpu(key: str, store, barrier) -> dict:
+    """Ranks sharing one GPU (gloo ranks on a one-GPU box: tests, the 8-rank rehearsal)
+    were each bound to that GPU's whole CPU slice by bind_local_rank, which cannot tell
+    them apart before the process group exists.  After it does: every rank counts itself
+    under its GPU's key in the rendezvous store, and the k ranks on one GPU split its
+    slice k ways (disjoint CPU sets, host threads sized to them).  No-op without a
+    binding or when the GPU is the rank's own."""
+    from ..utils import env
+    if not PLACEMENT.get("cpus"):
+        return PLACEMENT
+    idx = int(store.add(f"fa_place/{key}", 1)) - 1
+    barrier()
+    n = int(store.add(f"fa_place/{key}", 0))
+    if n <= 1:
+        return PLACEMENT
+    part = shared_slice(list(PLACEMENT["cpus"]), idx, n)
+    try:
+        os.sched_setaffinity(0, part)
+    except OSError:
+        return PLACEMENT
+    if not os.environ.get("FA_NUM_THREADS"):
+        env.set_num_threads(len(part))
+    PLACEMENT.update(cpus=part, threads=len(part), gpu_sharers=n)
+    return PLACEMENT
+

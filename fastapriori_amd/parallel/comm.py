@@ -336,6 +336,14 @@ def init_comm(device: str | None = None, backend: str | None = None, timeout_s: 
         dist.init_process_group(**kw)
         if be == "nccl" and dist.get_world_size() > 1:
             _check_one_gpu_per_rank(dev)
+        elif dev.type == "cuda" and dist.get_world_size() > 1:
+            # gloo ranks sharing a GPU split its CPU slice (parallel.affinity)
+            from .affinity import refine_for_shared_gpu
+            try:
+                refine_for_shared_gpu(_gpu_key(dev), dist.distributed_c10d._get_default_store(),   # noqa: SLF001
+                                      dist.barrier)
+            except (RuntimeError, AttributeError, ValueError):
+                pass
     return Comm(dist.get_rank(), dist.get_world_size(), dev, be, force=force)
 
 

@@ -131,3 +131,36 @@ def test_ranks_sharing_one_gpu_split_its_node(tmp_path):
     shares = [plan_affinity(lr, bdfs, list(range(128)), str(tmp_path))["cpus"] for lr in range(8)]
     assert all(len(s) == 8 for s in shares)
     assert len({c for s in shares for c in s}) == 64 and set().union(*shares) == set(range(64, 128))
+
+
+def test_ranks_sharing_a_gpu_split_its_slice_after_rendezvous():
+    # gloo ranks on one GPU were bound to the GPU's whole slice (a narrowed view cannot tell
+    # them apart); after the rendezvous the k sharers split it k ways, disjoint
+    from fastapriori_amd.parallel.affinity import shared_slice
+    slice_ = list(range(160, 192))
+    parts = [shared_slice(slice_, i, 8) for i in range(8)]
+    assert all(len(p) == 4 for p in parts) and sorted(c for p in parts for c in p) == slice_
+    # more sharers than CPUs: one CPU each (shared, but never empty)
+    assert [shared_slice([3, 4], i, 3) for i in range(3)] == [[3], [3], [4]]
+
+
+def test_refine_binds_through_the_store(monkeypatch):
+    from fastapriori_amd.parallel import affinity
+    calls = {}
+    monkeypatch.setattr(affinity.os, "sched_setaffinity", lambda pid, cpus: calls.setdefault("cpus", list(cpus)))
+
+    class Store:
+        def __init__(self):
+            self.v = {}
+
+        def add(self, k, d):
+            self.v[k] = self.v.get(k, 0) + d
+            return self.v[k]
+    st = Store()
+    st.add("fa_place/g", 3)                     # three other sharers arrived first
+    affinity.PLACEMENT.clear()
+    affinity.PLACEMENT.update(node=0, cpus=list(range(32)), threads=32, peers=4)
+    monkeypatch.setenv("FA_NUM_THREADS", "2")
+    p = affinity.refine_for_shared_gpu("g", st, lambda: None)
+    assert p["gpu_sharers"] == 4 and p["cpus"] == list(range(24, 32)) and calls["cpus"] == list(range(24, 32))
+    affinity.PLACEMENT.clear()
