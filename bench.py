@@ -265,7 +265,7 @@ def _recommend_window(args, comm, d, jc, res, cfgv, sync) -> dict:
     if comm.allreduce_int(1 if err else 0, "max"):
         return {"window": "skipped", "error": err or "U.dat could not be written"}
     quiet = Logger(comm.rank, enabled=False)
-    runs, summ = [], {}
+    runs, summ, steps = [], {}, []
     for _ in range(1 + max(args.e2e_runs, 1)):
         sync()
         t0 = time.perf_counter()
@@ -273,12 +273,13 @@ def _recommend_window(args, comm, d, jc, res, cfgv, sync) -> dict:
         recommend_window(jc, comm, quiet, res, summ)
         sync()
         runs.append(comm.allreduce_float_max((time.perf_counter() - t0) * 1e3))
+        steps.append(summ.get("recommend_steps_ms"))
     return {"window": "read+parse U.dat, rules (generation, cut, sort), recommend, write recommends "
                       "(Main.scala:34-37), through pipeline.recommend_window",
             "U_lines": U_LINES, "U_bytes": os.path.getsize(upath), "first_ms": round(runs[0], 1),
             "warm_ms": round(min(runs[1:]), 1), "runs_ms": [round(x, 1) for x in runs],
             "n_rules": summ.get("n_rules"), "n_users": summ.get("n_users"),
-            "n_recommended": summ.get("n_recommended")}
+            "n_recommended": summ.get("n_recommended"), "steps_ms_first": steps[0], "steps_ms_last": steps[-1]}
 
 
 def _cpu_ranges(cpus: list) -> str:

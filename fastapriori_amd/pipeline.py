@@ -102,12 +102,22 @@ def recommend_window(cfg: JobConfig, comm, log: Logger, result, summary: dict) -
     """The reference's second timed window (Main.scala:34-37): read + parse U.dat,
     rules (generation, cut, sort), one recommendation per user line, write
     recommends.  bench.py times this same function for its e2e record."""
+    t0 = time.perf_counter()
     users = io.read_shard(cfg.input + "U.dat", comm)
+    t1 = time.perf_counter()
     ar = AssociationRules(result, comm, log)
+    ar.rules()
+    t2 = time.perf_counter()
     recs = ar.run(users)
+    t3 = time.perf_counter()
     if comm.is_root:
         io.write_lines(recs, cfg.output + "recommends", overwrite=cfg.overwrite)
     comm.barrier()
+    t4 = time.perf_counter()
+    # host wall time of each step (a step's device work ends inside the next host readback)
+    summary["recommend_steps_ms"] = {k: round(v * 1e3, 1) for k, v in
+                                     (("read_U", t1 - t0), ("rules", t2 - t1), ("recommend", t3 - t2),
+                                      ("write", t4 - t3))}
     summary["n_rules"] = ar.rules().n_rules
     if recs is not None:                   # rank 0 holds every user's recommendation
         summary.update(n_users=len(recs), n_recommended=sum(1 for r in recs if r != "0"))
