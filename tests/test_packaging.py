@@ -14,8 +14,17 @@ U = "1\n2\n7 8\n2 4\n4 1 2\n3\n1\n"
 
 
 def test_wheel_installs_and_runs_outside_the_tree(tmp_path):
+    # build from a copy of the project files, so the in-tree build's build/ and egg-info
+    # land there and not in the checkout
+    import shutil
+    src = tmp_path / "src"
+    src.mkdir()
+    for f in ("setup.py", "pyproject.toml", "README.md"):
+        shutil.copy(os.path.join(ROOT, f), src / f)
+    for d in ("fastapriori_amd", "csrc"):
+        shutil.copytree(os.path.join(ROOT, d), src / d, ignore=shutil.ignore_patterns("__pycache__"))
     wh = tmp_path / "wh"
-    r = subprocess.run([sys.executable, "-m", "pip", "wheel", ROOT, "--no-build-isolation", "--no-deps", "-w",
+    r = subprocess.run([sys.executable, "-m", "pip", "wheel", str(src), "--no-build-isolation", "--no-deps", "-w",
                         str(wh), "-q"], capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stderr[-3000:]
     whl = glob.glob(str(wh / "fastapriori_amd-*.whl"))
