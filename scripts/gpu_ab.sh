@@ -33,6 +33,7 @@ for i in 1 2; do
     fi
   done
 done
+[ -n "$NOKT" ] && exit 0          # NOKT=1: bench lines only, no kernel traces
 cd /tmp
 for s in "$@"; do
   t=$(tag "$s")
