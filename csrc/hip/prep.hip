@@ -51,6 +51,67 @@ __global__ __launch_bounds__(256) void k_histogram(const int32_t* __restrict__ i
 }
 
 // ---------------------------------------------------------------------------
+// F1 ranking on the device (FastApriori.scala:55-62; the order of csrc/host/f1.cpp
+// fa_f1_rank_numeric): the frequent ids (support >= thr) by support descending, ties
+// by a unique tie key -- Java String order of the decimal token (string: the digits
+// left-aligned to 10 places, then the length; id 0 = "" first) or the integer value
+// (numeric: id 0 last).  Every workgroup stages all V (support, tie key) pairs in
+// LDS and each thread ranks one id by counting the ids ahead of it, so the id -> rank
+// LUT is written without a host round trip: the compression kernels queue right
+// behind it while the host reads the ranking back.  pack (int64 [2 V + 1]): [0] the
+// number of frequent ids F, [1 .. F] the ids in rank order, [V + 1 .. V + F] their supports.
+// ---------------------------------------------------------------------------
+constexpr int kF1RankMax = 2048;
+
+__device__ __forceinline__ int64_t f1_tie_key(int64_t fid, int numeric) {
+  if (numeric) return fid == 0 ? INT64_MAX : fid - 1;
+  if (fid == 0) return -16;                       // "" sorts first (key -1, length 0)
+  const int64_t v = fid - 1;
+  int digits = 1;
+  int64_t p = 10;
+  while (digits < 11 && v >= p) { ++digits; p *= 10; }
+  int64_t pad = 1;
+  for (int i = 0; i < 10 - min(digits, 10); ++i) pad *= 10;
+  return v * pad * 16 + digits;                   // (key, length) in one order-preserving int64
+}
+
+__global__ __launch_bounds__(256) void k_f1_rank(const int64_t* __restrict__ hist, int32_t V, int64_t thr,
+                                                 int numeric, int32_t* __restrict__ lut, int64_t* __restrict__ pack) {
+  __shared__ int64_t sc[kF1RankMax], sk[kF1RankMax];
+  __shared__ int nf[4];
+  int mine = 0;
+  for (int i = threadIdx.x; i < V; i += blockDim.x) {
+    const int64_t c = hist[i];
+    sc[i] = c >= thr ? c : -1;
+    sk[i] = f1_tie_key(i, numeric);
+    mine += c >= thr;
+  }
+  __syncthreads();
+  const int v = (int)blockIdx.x * blockDim.x + (int)threadIdx.x;
+  if (v < V) {
+    const int64_t c = sc[v], k = sk[v];
+    if (c < 0) {
+      lut[v] = -1;
+    } else {
+      int r = 0;
+      for (int j = 0; j < V; ++j) {               // (every lane reads the same word: a broadcast)
+        const int64_t cj = sc[j];
+        r += (cj > c) | ((cj == c) & (sk[j] < k));
+      }
+      lut[v] = r;
+      pack[1 + r] = v;
+      pack[1 + V + r] = c;
+    }
+  }
+  if (blockIdx.x == 0) {
+    mine = (int)wave_sum_u32((uint32_t)mine);
+    if ((threadIdx.x & 63) == 0) nf[threadIdx.x >> 6] = mine;
+    __syncthreads();
+    if (threadIdx.x == 0) pack[0] = (int64_t)nf[0] + nf[1] + nf[2] + nf[3];
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Heavy-hitter F1 for wide vocabularies (webdocs-scale: millions of ids, where
 // a V-bin histogram means one global atomic per token plus a V-sized
 // all-reduce).  Pass 1: a 2-row count-min sketch (2 x 16K u32 bins = 128 KB of
@@ -1251,6 +1312,14 @@ FA_API int fa_hip_histogram(const int32_t* items, int64_t nnz, int32_t V, uint32
     if (aligned) hipLaunchKernelGGL((k_histogram<false, true>), g, b, 0, st, items, nnz, V, 1, counts);
     else hipLaunchKernelGGL((k_histogram<false, false>), g, b, 0, st, items, nnz, V, 1, counts);
   }
+  FA_LAUNCH_RET();
+}
+
+// F1 ranking + id -> rank LUT on the device (k_f1_rank); hist int64 [V], V <= kF1RankMax.
+FA_API int fa_hip_f1_rank(const int64_t* hist, int32_t V, int64_t thr, int numeric, int32_t* lut, int64_t* pack,
+                          hipStream_t st) {
+  if (V < 1 || V > kF1RankMax || thr < 1) return 1;
+  hipLaunchKernelGGL(k_f1_rank, dim3((unsigned)((V + 255) / 256)), dim3(256), 0, st, hist, V, thr, numeric, lut, pack);
   FA_LAUNCH_RET();
 }
 

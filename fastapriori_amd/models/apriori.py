@@ -143,16 +143,31 @@ class FastApriori:
         self._timer = tm
         self._level_recs = []     # per-level metric records, emitted by _finish with device times
 
+        self._f1_pending = None
+        cmp_pending = None
         with roctx_range("F1"), tm.phase("f1"):
             items, counts1, lut = self._frequent_items(shard, mc)
+        f1p = self._f1_pending
+        if f1p is not None:
+            # ranked on the device: compression goes out right behind the ranking (its
+            # block layout sized by the vocabulary width, which bounds F1) and the host
+            # reads the ranking back while it runs -- no GPU idle between F1 and compression
+            with roctx_range("compress"), tm.phase("compress"):
+                if TUNING.early_compress:
+                    cmp_pending = self._compress_start(shard, lut, f1p.V)
+            with roctx_range("F1"):
+                ids, counts1 = f1p.finish()
+            items = _Deferred(lambda: ["" if i == 0 else str(i - 1) for i in ids.tolist()])
+            self._deferred.append(items)
         F1 = len(counts1)
         self._F1, self._dev = F1, dev
         self._counts1 = counts1
         # compression's kernels go out right behind the LUT's copy: the host work below
         # (result, logs, checkpoint) overlaps them instead of idling the GPU
         # (the phase's two spans add up: Timer sums spans of one name)
-        with roctx_range("compress"), tm.phase("compress"):
-            cmp_pending = self._compress_start(shard, lut, F1) if F1 >= 2 and TUNING.early_compress else None
+        if f1p is None:
+            with roctx_range("compress"), tm.phase("compress"):
+                cmp_pending = self._compress_start(shard, lut, F1) if F1 >= 2 and TUNING.early_compress else None
         self.log.metric(phase="f1", frequent=F1)
         levels = [np.arange(F1, dtype=np.int32).reshape(-1, 1)]
         counts = [counts1]
@@ -875,6 +890,12 @@ class FastApriori:
                     if shard.extras.size:
                         hist += torch.bincount(torch.from_numpy(shard.extras.astype(np.int64)), minlength=V).to(dev)
                 comm.all_reduce_(hist)
+                if (dev.type == "cuda" and TUNING.f1_rank_device and 2 <= V <= ops.primitives.F1_RANK_DEVICE_MAX
+                        and self.cfg.tiebreak in ("string", "numeric")):
+                    # narrow vocabulary: ranked on the device (prep.hip k_f1_rank); the LUT is
+                    # there at once and the ranking comes back while compression runs (_run)
+                    self._f1_pending = ops.primitives.f1_rank_start(hist, thr, self.cfg.tiebreak == "numeric")
+                    return None, None, self._f1_pending.lut
                 if V <= F1_HIST_READBACK and dev.type == "cuda" and self.cfg.tiebreak == "string":
                     # narrow vocabulary: the whole histogram in one readback (no nonzero sync),
                     # ranked and mapped to the LUT in one native call (csrc/host/f1.cpp)
@@ -1051,6 +1072,9 @@ class FastApriori:
         dev = shard.items.device
         if pending is not None:
             # fused two-pass path: kept rows, offsets, sorted ranks and the length histogram
+            # (started before F1 was known when F1 was ranked on the device: its block
+            # layout then has ceil(V / 256) blocks, the ones past F1's empty)
+            pending["F1"] = F1
             kept, roff, ranks, hist_t, bcnt = ops.primitives.compress_rows_finish(pending)
             T = kept.numel()
             hist = np.asarray(hist_t, dtype=np.int64).copy()

@@ -109,6 +109,46 @@ def histogram(items: torch.Tensor, V: int) -> torch.Tensor:
     return out
 
 
+F1_RANK_DEVICE_MAX = 2048   # prep.hip kF1RankMax
+
+
+class F1Pending:
+    """The device F1 ranking of f1_rank_start: the id -> rank LUT is on the device
+    already (kernels that read it can be queued); finish() waits for the ranking's copy
+    to pinned memory and returns (frequent ids, their supports) in rank order."""
+
+    def __init__(self, lut: torch.Tensor, host: torch.Tensor, ev, V: int):
+        self.lut, self._host, self._ev, self.V = lut, host, ev, V
+        self._got = None
+
+    def finish(self):
+        if self._got is None:
+            self._ev.synchronize()
+            h = self._host.numpy()
+            F = int(h[0])
+            self._got = h[1:1 + F].copy(), h[1 + self.V:1 + self.V + F].copy()
+        return self._got
+
+
+def f1_rank_start(hist: torch.Tensor, thr: int, numeric_tiebreak: bool) -> F1Pending:
+    """Rank the frequent ids of an int64 [V] histogram on the device (prep.hip k_f1_rank:
+    FastApriori.scala:55-62's order, csrc/host/f1.cpp fa_f1_rank_numeric's) and queue
+    the ranking's copy to pinned memory, without waiting (F1Pending)."""
+    V = hist.numel()
+    assert hist.is_cuda and hist.dtype == _I64 and 1 <= V <= F1_RANK_DEVICE_MAX and thr >= 1
+    dev = hist.device
+    lut = torch.empty(V, dtype=_I32, device=dev)
+    pack = torch.empty(2 * V + 1, dtype=_I64, device=dev)
+    _hip_call("fa_hip_f1_rank", _p(hist), V, int(thr), int(bool(numeric_tiebreak)), _p(lut), _p(pack), _stream(hist))
+    stage = pinned_stage("f1_rank")
+    host = stage.get(8 * pack.numel()).view(_I64)
+    host.copy_(pack, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    stage.event = ev
+    return F1Pending(lut, host, ev, V)
+
+
 # ---------------------------------------------------------------------------
 # Heavy-hitter F1 (wide vocabularies; csrc/hip/prep.hip k_f1_sketch/k_f1_exact)
 # ---------------------------------------------------------------------------

@@ -41,6 +41,7 @@ class Tuning:
     # ---- compression (ops/primitives.py) ------------------------------------------
     fused_compress: bool = True         # two-pass fused compression for short rows
     early_compress: bool = True         # compression queued before the F1 bookkeeping (host overlap)
+    f1_rank_device: bool = True         # narrow numeric vocabularies ranked on the device (no F1 host round trip)
     fused_compress_mean_len: float = 12.0
     fused_layout: bool = True           # the emit pass writes the pair kernel's blocked layout
     compress_wave_mean_len: float = 48.0

@@ -51,3 +51,41 @@ def test_ties_follow_java_string_order():
     F = _native.host().fa_f1_rank_numeric(hh.ctypes.data, V, 1, ids.ctypes.data, cnt.ctypes.data, lut.ctypes.data)
     got = ["" if i == 0 else str(i - 1) for i in ids[:F]]
     assert got == sorted(toks, key=java_string_key)
+
+
+def _numeric_rank(hh, thr):
+    fid = np.flatnonzero(hh >= thr).astype(np.int64)
+    key = np.where(fid == 0, np.iinfo(np.int64).max, fid - 1)
+    order = np.lexsort((key, -hh[fid]))
+    return fid[order], hh[fid][order]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("numeric", [False, True])
+@pytest.mark.parametrize("V,hi,thr", [(2, 3, 1), (7, 3, 1), (1001, 40, 20), (1001, 3, 1), (2048, 9, 2)])
+def test_device_rank_matches_host(V, hi, thr, numeric):
+    """prep.hip k_f1_rank (ops.primitives.f1_rank_start) against the host ranking: the
+    same ids and supports in rank order, the same id -> rank LUT (many ties at hi = 3)."""
+    import torch
+    from fastapriori_amd.ops import primitives as P
+    hh = np.random.default_rng(V + hi).integers(0, hi, V).astype(np.int64)
+    hh[min(V - 1, 10)] = hi + 5                       # a sure frequent id
+    pend = P.f1_rank_start(torch.from_numpy(hh).cuda(), thr, numeric)
+    ids, cnt = pend.finish()
+    ref_ids, ref_cnt = (_numeric_rank if numeric else _numpy_rank)(hh, thr)
+    assert np.array_equal(ids, ref_ids) and np.array_equal(cnt, ref_cnt)
+    want = np.full(V, -1, np.int32)
+    want[ref_ids] = np.arange(ref_ids.size, dtype=np.int32)
+    assert np.array_equal(pend.lut.cpu().numpy(), want)
+
+
+@pytest.mark.gpu
+def test_device_rank_java_string_ties():
+    import torch
+    from fastapriori_amd.ops import primitives as P
+    toks = ["", "0", "1", "10", "100", "11", "2", "9", "99", "1000", "101"]
+    fids = [0] + [int(t) + 1 for t in toks[1:]]
+    hh = np.zeros(max(fids) + 1, np.int64)
+    hh[fids] = 5
+    ids, _ = P.f1_rank_start(torch.from_numpy(hh).cuda(), 1, False).finish()
+    assert ["" if i == 0 else str(i - 1) for i in ids] == sorted(toks, key=java_string_key)
