@@ -554,14 +554,67 @@ class FastApriori:
             bm, bmap = self._bitmaps(v, used, blocked=True)
             used_t = torch.from_numpy(used.astype(np.int64)).to(self._dev)
             bm_rows = (bmap[used_t] if bmap is not None else used_t).to(torch.int32).contiguous()
+            wr = None
+            if (self.cfg.trim and TUNING.window_trim and v["wword"] is None and v["src"] is None
+                    and v["T"] >= self.cfg.trim_min_rows):
+                wr = lambda used_w: self._window_rows(v, used_w, k)        # noqa: E731
             cnt = Pm.dl_count_multipass(S, F1, n_used, C0, lds, v["roff"], v["ranks"], v["src"], v["ncols"],
                                         v["wword"], bm, bm_rows,
                                         self.stats["min_count"] / max(1, self.stats["n_lines"]), self._dev,
-                                        bmap=bmap)
+                                        bmap=bmap, window_rows=wr)
+            plan = Pm.LAST_LEVEL_PLAN
+            if plan.get("windows_trimmed"):
+                self.stats["window_trims"] = self.stats.get("window_trims", 0) + int(plan["windows_trimmed"])
         if cnt is None:
             return None
         self.stats["device_multipass"] = self.stats.get("device_multipass", 0) + 1
         return c, cnt
+
+    def _window_rows(self, db, used_w: np.ndarray, k: int):
+        """Rows of one window of a multi-pass level (ops.primitives.dl_count_multipass):
+        a window's candidates use only its own items (used_w), so a row holding fewer
+        than k of them contains none of its k-candidates.  When the binomial estimate
+        (_trim_worth_it's, with the window's items) keeps few enough rows, those rows are
+        trimmed to the window's items (ops.trim_rows) and the window counts from a bitmap
+        of its items over them: (ncols, bitmap [len(used_w), Wp], bitmap row u = slab
+        row u).  Deep T40I10 levels: windows use a third to a half of their level's items,
+        so half or more of the level's rows drop out of a window.  None: the window counts
+        the level's rows.  (FastApriori.scala:132-160 counts every row per candidate.)"""
+        est = self._trim_estimate(db, used_w, k)
+        if est is None or est >= TUNING.window_trim_rows_frac * db["T"]:
+            return None
+        dev = db["ranks"].device
+        alive = torch.zeros(db["F1"], dtype=torch.int8)
+        alive[torch.from_numpy(used_w.astype(np.int64))] = 1
+        with roctx_range("window_trim"):
+            kept, nroff, nranks, _, _ = ops.trim_rows(db["roff"], db["ranks"], alive.to(dev), k, None)
+            K = int(kept.numel())
+            if K == 0:
+                return 0, None
+            imap = np.full(max(db["F1"], 1), -1, dtype=np.int32)
+            imap[used_w] = np.arange(used_w.size, dtype=np.int32)
+            bm, _ = ops.build_bitmaps(nroff, nranks, None, K, int(used_w.size), torch.from_numpy(imap).to(dev),
+                                      torch.from_numpy(np.ascontiguousarray(used_w, dtype=np.int32)).to(dev))
+        return K, bm
+
+    def _trim_estimate(self, db, used: np.ndarray, k: int):
+        """Rows expected to keep >= k of the items `used` (the binomial model of
+        _trim_worth_it), or None without a length histogram."""
+        from scipy.special import betainc
+        hist = db.get("len_hist")
+        if hist is None:
+            return None
+        c1, alive = db["c1"], db["alive"]
+        denom = float(c1[alive].sum())
+        if denom <= 0:
+            return None
+        p = min(float(c1[used].sum()) / denom, 1.0)
+        L = np.arange(hist.size)
+        sf = np.zeros(hist.size)
+        ok = L >= k
+        if p > 0:
+            sf[ok] = betainc(k, L[ok] - k + 1, p)
+        return float((hist * sf).sum())
 
     def _dl_bitmap_count(self, S, db, used: np.ndarray) -> torch.Tensor:
         """Counts (int32 [C], bundle order) of the device bundle's single level from the

@@ -1702,7 +1702,7 @@ def dl_plan(S: DeviceLevelState, L: int, F1: int, n_used: int, C: int, lds: int,
 
 
 def dl_count_multipass(S: DeviceLevelState, F1: int, n_used: int, C: int, lds: int, roff, ranks, src, ncols: int,
-                       wword, bm, bm_rows, sup_frac: float, dev, bmap=None) -> torch.Tensor | None:
+                       wword, bm, bm_rows, sup_frac: float, dev, bmap=None, window_rows=None) -> torch.Tensor | None:
     """Counts of a device bundle's single level whose C candidates exceed one
     accumulator pass: per window of candidates, a device plan of that window
     (levels.hip fa_hip_dl_plan_window[_bits]) and a slab count from the used items'
@@ -1715,7 +1715,12 @@ def dl_count_multipass(S: DeviceLevelState, F1: int, n_used: int, C: int, lds: i
     use (bmap: device rank -> bitmap row, None = rank-indexed bitmap), and windows grow
     chunk by chunk (dl_window_plan) while their candidates fit what those rows leave
     of the LDS: deep T40I10 levels use 2-3x fewer items per window than per level, so
-    every pass copies fewer slab rows and fewer passes are needed."""
+    every pass copies fewer slab rows and fewer passes are needed.
+
+    window_rows (optional, with per-window items): used_w (sorted ranks of a window's
+    items) -> None, or (ncols_w, bm_w): the bitmap of exactly those items over the rows
+    that hold >= k of them (FastApriori._window_rows: a row with fewer holds none of the
+    window's k-candidates), counted instead of the level's bitmap."""
     acc16 = TUNING.dl_acc16 and wword is None
     accb = 2 if acc16 else 4
     sw, cap = dl_slab_width(n_used, min(C, 8192), lds, accb)
@@ -1738,18 +1743,27 @@ def dl_count_multipass(S: DeviceLevelState, F1: int, n_used: int, C: int, lds: i
     gn = int(lib.fa_hip_dl_gpre_need(S.desc.ctypes.data, 1))
     gpre = torch.empty(max(gn, 1), dtype=_I32, device=dev)
     out = torch.zeros(C, dtype=_I32, device=dev)
-    W = (ncols + 63) // 64
-    npass, used_sum = 0, 0
+    npass, used_sum, rows_sum, trimmed = 0, 0, 0, 0
     lane_deal(lib, ncols)
     for w0, w1, wsw, bits in wins:
-        nu, rows_w, bits_p = n_used, bm_rows, None
+        nu, rows_w, bits_p, bm_w, ncols_w = n_used, bm_rows, None, bm, ncols
         if bits is not None:
             used_w = np.flatnonzero(np.unpackbits(bits.view(np.uint8), bitorder="little")[:F1])
             nu = int(used_w.size)
             bits_t = torch.from_numpy(bits.view(np.int64).copy()).to(dev, non_blocking=False)
-            used_t = torch.from_numpy(used_w.astype(np.int64)).to(dev)
-            rows_w = (bmap[used_t] if bmap is not None else used_t).to(_I32).contiguous()
             bits_p = bits_t
+            got = window_rows(used_w) if window_rows is not None else None
+            if got is not None:
+                # the window's own rows: its items' bitmap, bitmap row u = slab row u
+                ncols_w, bm_w = got
+                rows_w = None
+                trimmed += 1
+            else:
+                used_t = torch.from_numpy(used_w.astype(np.int64)).to(dev)
+                rows_w = (bmap[used_t] if bmap is not None else used_t).to(_I32).contiguous()
+        if ncols_w == 0:
+            continue                                     # no row holds k of the window's items
+        W = (ncols_w + 63) // 64
         dense = wword is None and TUNING.dense_min_rows > 0 and sup_frac * wsw * 64 >= TUNING.dense_min_rows
         nslabs = (W + wsw - 1) // wsw
         _native.check(lib.fa_hip_dl_plan_window_bits(S.desc.ctypes.data, 1, _p(S.ctl), F1, _p(bits_p), _p(item_map),
@@ -1758,15 +1772,17 @@ def dl_count_multipass(S: DeviceLevelState, F1: int, n_used: int, C: int, lds: i
         nacc = (w1 - w0 + 1) // 2 if acc16 else w1 - w0
         lds_k = nu * (wsw + 2) * 8 + ((nacc + 3) & ~3) * 4
         n_wg = int(max(1, min(nslabs, 256 * min(max(1, TUNING.slab_lds_bytes // lds_k), 2))))
-        _hip_call("fa_hip_count_slab_rec_cls", _p(roff), _p(ranks), _p(src), ncols, _p(item_map), F1, nu,
-                  _p(gpre), _p(rec), 0, w1 - w0, _p(wword), out.data_ptr() + 4 * w0, wsw, n_wg, _p(bm),
-                  bitmap_ld(bm), st, _p(rows_w), _p(S.ctl) + 8 * 221, (2 if dense else 0) | (4 if acc16 else 0))
+        _hip_call("fa_hip_count_slab_rec_cls", _p(roff), _p(ranks), _p(src), ncols_w, _p(item_map), F1, nu,
+                  _p(gpre), _p(rec), 0, w1 - w0, _p(wword), out.data_ptr() + 4 * w0, wsw, n_wg, _p(bm_w),
+                  bitmap_ld(bm_w), st, _p(rows_w), _p(S.ctl) + 8 * 221, (2 if dense else 0) | (4 if acc16 else 0))
         npass += 1
         used_sum += nu
+        rows_sum += ncols_w
     LAST_LEVEL_PLAN.clear()
     LAST_LEVEL_PLAN.update(kernel="slab_dev_multi", rows=int(roff.numel() - 1), used=n_used, sw=sw, cap=cap,
                            passes=npass, pieces=-1, slab_reads=0, m=int(S.desc[0, 4]), C=C,
-                           window_used_avg=round(used_sum / max(npass, 1), 1))
+                           window_used_avg=round(used_sum / max(npass, 1), 1),
+                           window_rows_avg=round(rows_sum / max(npass, 1)), windows_trimmed=trimmed)
     return out
 
 

@@ -44,3 +44,22 @@ def test_t40_deep_levels_match_cpu():
     assert len(ref.levels) >= 8
     assert [len(x) for x in got.levels] == [len(x) for x in ref.levels]
     assert got.as_dict() == ref.as_dict()
+
+
+@pytest.mark.parametrize("frac", [0.7, 1.01])
+def test_t40_window_trim_matches_cpu(frac):
+    """Window-by-window levels counted over each window's own rows (FastApriori._window_rows:
+    rows holding >= k of the window's items, trimmed + a bitmap of those items): every
+    window trimmed (frac 1.01) and the cost model's choice (0.7) both give the CPU miner's
+    exact counts, and the trimmed windows really ran."""
+    from fastapriori_amd.tuning import override
+    cpu = generate_shard(400_000, Comm(), "cpu", 40.0, 10.0, 2000, 1000, 5)
+    ref = _mine(cpu, 0.005, trim_min_rows=0)
+    with override(window_trim=True, window_trim_rows_frac=frac):
+        m = FastApriori(0.005, config=MinerConfig(min_support=0.005, trim_min_rows=0), logger=Logger(0, enabled=False))
+        got = m.run(cpu.to(DEV))
+    assert m.stats.get("device_multipass", 0) >= 1, m.stats
+    if frac > 1:
+        assert m.stats.get("window_trims", 0) >= m.stats["device_multipass"], m.stats
+    assert [len(x) for x in got.levels] == [len(x) for x in ref.levels]
+    assert got.as_dict() == ref.as_dict()
