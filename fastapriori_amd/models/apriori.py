@@ -581,13 +581,20 @@ class FastApriori:
         so half or more of the level's rows drop out of a window.  None: the window counts
         the level's rows.  (FastApriori.scala:132-160 counts every row per candidate.)"""
         est = self._trim_estimate(db, used_w, k)
-        if est is None or est >= TUNING.window_trim_rows_frac * db["T"]:
+        if est is None or est >= TUNING.window_trim_est_frac * db["T"]:
             return None
         dev = db["ranks"].device
         alive = torch.zeros(db["F1"], dtype=torch.int8)
         alive[torch.from_numpy(used_w.astype(np.int64))] = 1
         with roctx_range("window_trim"):
-            kept, nroff, nranks, _, _ = ops.trim_rows(db["roff"], db["ranks"], alive.to(dev), k, None)
+            # the estimate decides; the exact count only stops a trim that would keep
+            # nearly every row (an exact gate at 0.7-0.8 measured slower: windows keeping
+            # ~80 % of the rows still gain, docs/PERF_HISTORY.md)
+            got = ops.trim_rows(db["roff"], db["ranks"], alive.to(dev), k, None,
+                                max_keep=int(TUNING.window_trim_rows_frac * db["T"]))
+            if got is None:
+                return None
+            kept, nroff, nranks, _, _ = got
             K = int(kept.numel())
             if K == 0:
                 return 0, None

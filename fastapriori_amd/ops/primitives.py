@@ -769,8 +769,11 @@ def count_candidates(bm: torch.Tensor, W: int, prefix: torch.Tensor, ext_off: np
 TRIM_HIST_BINS = 256   # csrc/hip/prep.hip kTrimHist
 
 
-def trim_rows(roff, ranks, alive: torch.Tensor, min_len: int, wrow=None):
+def trim_rows(roff, ranks, alive: torch.Tensor, min_len: int, wrow=None, max_keep: int | None = None):
     """Keep rows with >= min_len alive items, dropping the dead items.
+
+    max_keep (device path): when more rows than this would be kept, return None after
+    the counting pass (the emit pass is skipped).
 
     alive: int8 [F1] on the rows' device.  Returns (kept row ids int32, new roff,
     new ranks, new wrow, histogram of new row lengths int64 [256], lengths >= 255
@@ -795,6 +798,8 @@ def trim_rows(roff, ranks, alive: torch.Tensor, min_len: int, wrow=None):
         torch.cumsum(bk[0], 0, dtype=_I64, out=bases[0, 1:])    # two 1-D scans: the [2, nb] scan
         torch.cumsum(bk[1], 0, dtype=_I64, out=bases[1, 1:])    # along dim 1 runs on 2 threads' worth
         K, nnz = (int(v) for v in bases[:, -1].tolist())
+        if max_keep is not None and K > max_keep:
+            return None
         nroff = torch.empty(K + 1, dtype=_I64, device=dev)
         nroff[K:] = nnz
         nranks = torch.empty(max(nnz, 1), dtype=_I32, device=dev)

@@ -53,10 +53,12 @@ class Tuning:
     dl_acc16_bundles: bool = False      # ... and in one-pass device bundles
     mp_window_items: bool = True        # window-by-window levels: each window's slab holds only its own used items
     # window-by-window levels: a window counts only the rows holding >= k of its own items
-    # (trimmed + a bitmap of its items) when the binomial estimate keeps fewer than this
-    # share of the level's rows (FastApriori._window_rows)
+    # (trimmed + a bitmap of its items) when the binomial estimate keeps fewer than
+    # window_trim_est_frac of the level's rows, unless the exact count keeps more than
+    # window_trim_rows_frac of them (FastApriori._window_rows)
     window_trim: bool = True
-    window_trim_rows_frac: float = 0.7
+    window_trim_est_frac: float = 0.7
+    window_trim_rows_frac: float = 0.95
     # bundle capacity = the largest over the slab widths (a bundle takes a narrower slab
     # when that holds all of it) instead of the first width holding 8192 candidates
     slab_cap_max: bool = False
