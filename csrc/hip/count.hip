@@ -1862,6 +1862,140 @@ FA_API int fa_hip_count_candidates(const uint64_t* bm, int64_t Wp, int64_t W, co
   FA_LAUNCH_RET();
 }
 
+// ---------------------------------------------------------------------------
+// A window's own rows, in the bitmap domain (FastApriori._window_rows): a window of a
+// window-by-window level counts k-candidates over its items U only, so only the rows
+// holding >= k of U matter.  k_win_alive: per 64-row word q of the level's bitmap, the
+// mask of rows with >= k bits among U's bitmap rows (a bit-sliced counter: one plane per
+// count bit, ripple-carry adds) and its popcount.  k_win_compact: every U row's words
+// compressed to the alive rows (software PEXT, Hacker's Delight 7-4, with the six move
+// masks of the word's alive mask computed once for all of U) and written at the alive
+// rows' running bit offset: one wave per 64 words assembles its output span in LDS,
+// stores the words inside it and ORs the two it shares with its neighbours.  The result
+// is a row-major bitmap of U over the alive rows only -- no pass over the transaction
+// rows, no trimmed copy of them.
+// bm element (bitmap row r, word q): ld > 0 row-major (row stride ld), ld < 0 the 8-word
+// blocked layout of block stride -ld (slab_copy_bm).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t bm_word(const uint64_t* __restrict__ bm, int64_t ld, int64_t r, int64_t q) {
+  return ld > 0 ? bm[r * ld + q] : bm[(q >> 3) * -ld + r * 8 + (q & 7)];
+}
+
+constexpr int kWinPlanes = 11;   // counts up to 2047 items
+
+__global__ __launch_bounds__(256) void k_win_alive(const uint64_t* __restrict__ bm, int64_t ld,
+                                                   const int32_t* __restrict__ rows, int n_items, int64_t W, int k,
+                                                   int planes, uint64_t* __restrict__ alive, int32_t* __restrict__ cnt) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= W) return;
+  uint64_t pl[kWinPlanes];
+#pragma unroll
+  for (int p = 0; p < kWinPlanes; ++p) pl[p] = 0ull;
+  for (int u = 0; u < n_items; ++u) {
+    uint64_t c = bm_word(bm, ld, rows[u], q);
+#pragma unroll
+    for (int p = 0; p < kWinPlanes; ++p) {
+      if (p >= planes) break;
+      const uint64_t t = pl[p] & c;
+      pl[p] ^= c;
+      c = t;
+    }
+  }
+  // count >= k, bit-sliced, from the top plane down
+  uint64_t gt = 0ull, eq = ~0ull;
+#pragma unroll
+  for (int p = kWinPlanes - 1; p >= 0; --p) {
+    if (p >= planes) continue;
+    if ((k >> p) & 1) {
+      eq &= pl[p];
+    } else {
+      gt |= eq & pl[p];
+      eq &= ~pl[p];
+    }
+  }
+  const uint64_t a = (k >> planes) ? 0ull : (gt | eq);
+  alive[q] = a;
+  cnt[q] = __popcll(a);
+}
+
+__global__ __launch_bounds__(64) void k_win_compact(const uint64_t* __restrict__ bm, int64_t ld,
+                                                    const int32_t* __restrict__ rows, int n_items, int64_t W,
+                                                    const uint64_t* __restrict__ alive, const int64_t* __restrict__ off,
+                                                    uint64_t* __restrict__ out, int64_t ldo) {
+  __shared__ unsigned long long buf[66];
+  const int lane = threadIdx.x;
+  const int64_t q0 = (int64_t)blockIdx.x * 64, q = q0 + lane;
+  const int64_t qe = min(W, q0 + 64) - 1;                 // the wave's last word
+  const uint64_t m0 = q < W ? alive[q] : 0ull;
+  const int n = __popcll(m0);
+  const int64_t base = off[q0];                            // the wave's first output bit
+  const int64_t end = off[qe] + __popcll(alive[qe]);      // one past its last
+  if (end == base) return;                                 // (uniform: no alive row in these words)
+  const int s = (int)(base & 63) + (q < W ? (int)(off[q] - base) : 0);
+  const int nwords = (int)(((base & 63) + (end - base) + 63) >> 6);
+  const int64_t w0 = base >> 6;
+  // the six move masks of m0 (compress, Hacker's Delight 7-4)
+  uint64_t mv[6];
+  {
+    uint64_t m = m0, mk = ~m0 << 1;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      uint64_t mp = mk ^ (mk << 1);
+      mp ^= mp << 2; mp ^= mp << 4; mp ^= mp << 8; mp ^= mp << 16; mp ^= mp << 32;
+      mv[i] = mp & m;
+      m = (m ^ mv[i]) | (mv[i] >> (1 << i));
+      mk &= ~mp;
+    }
+  }
+  for (int u = 0; u < n_items; ++u) {
+    buf[lane] = 0ull;
+    if (lane < 2) buf[64 + lane] = 0ull;
+    __syncthreads();
+    if (n) {
+      uint64_t x = bm_word(bm, ld, rows[u], q) & m0;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const uint64_t t = x & mv[i];
+        x = (x ^ t) | (t >> (1 << i));
+      }
+      const int w = s >> 6, sh = s & 63;
+      atomicOr(&buf[w], (unsigned long long)(x << sh));
+      if (sh + n > 64) atomicOr(&buf[w + 1], (unsigned long long)(x >> (64 - sh)));
+    }
+    __syncthreads();
+    uint64_t* o = out + (int64_t)u * ldo + w0;
+    for (int j = lane; j < nwords; j += 64) {
+      const unsigned long long v = buf[j];
+      if (j == 0 || j == nwords - 1) {
+        if (v) atomicOr(reinterpret_cast<unsigned long long*>(o + j), v);   // shared with a neighbour wave
+      } else {
+        o[j] = v;
+      }
+    }
+  }
+}
+
+FA_API int fa_hip_win_alive(const uint64_t* bm, int64_t ld, const int32_t* rows, int n_items, int64_t W, int k,
+                            uint64_t* alive, int32_t* cnt, hipStream_t st) {
+  if (W <= 0) return 0;
+  int planes = 1;
+  while ((1 << planes) <= n_items) ++planes;
+  if (n_items < 1 || planes > kWinPlanes || k < 1 || ld == 0) return 1;
+  hipLaunchKernelGGL(k_win_alive, dim3((unsigned)((W + 255) / 256)), dim3(256), 0, st, bm, ld, rows, n_items, W, k,
+                     planes, alive, cnt);
+  FA_LAUNCH_RET();
+}
+
+// out: zeroed, [n_items][ldo] words, ldo >= ceil(K / 64); off: exclusive prefix of k_win_alive's counts [W]
+FA_API int fa_hip_win_compact(const uint64_t* bm, int64_t ld, const int32_t* rows, int n_items, int64_t W,
+                              const uint64_t* alive, const int64_t* off, uint64_t* out, int64_t ldo, hipStream_t st) {
+  if (W <= 0 || n_items < 1) return 0;
+  if (ld == 0 || ldo < 1) return 1;
+  hipLaunchKernelGGL(k_win_compact, dim3((unsigned)((W + 63) / 64)), dim3(64), 0, st, bm, ld, rows, n_items, W, alive,
+                     off, out, ldo);
+  FA_LAUNCH_RET();
+}
+
 // Slab counting from piece records (k_count_slab_rec; records: plan.cpp, 3 x int4
 // per piece).  LDS: slab + accumulator (16-B aligned) + u16 map when F1 <= 8192
 // and the slab is built from contiguous rows.  Returns 3 when that exceeds the LDS.

@@ -557,7 +557,7 @@ class FastApriori:
             wr = None
             if (self.cfg.trim and TUNING.window_trim and v["wword"] is None and v["src"] is None
                     and v["T"] >= self.cfg.trim_min_rows):
-                wr = lambda used_w: self._window_rows(v, used_w, k)        # noqa: E731
+                wr = lambda used_w: self._window_rows(v, used_w, k, bm, bmap)        # noqa: E731
             cnt = Pm.dl_count_multipass(S, F1, n_used, C0, lds, v["roff"], v["ranks"], v["src"], v["ncols"],
                                         v["wword"], bm, bm_rows,
                                         self.stats["min_count"] / max(1, self.stats["n_lines"]), self._dev,
@@ -570,39 +570,30 @@ class FastApriori:
         self.stats["device_multipass"] = self.stats.get("device_multipass", 0) + 1
         return c, cnt
 
-    def _window_rows(self, db, used_w: np.ndarray, k: int):
+    def _window_rows(self, db, used_w: np.ndarray, k: int, bm, bmap):
         """Rows of one window of a multi-pass level (ops.primitives.dl_count_multipass):
         a window's candidates use only its own items (used_w), so a row holding fewer
-        than k of them contains none of its k-candidates.  When the binomial estimate
-        (_trim_worth_it's, with the window's items) keeps few enough rows, those rows are
-        trimmed to the window's items (ops.trim_rows) and the window counts from a bitmap
-        of its items over them: (ncols, bitmap [len(used_w), Wp], bitmap row u = slab
-        row u).  Deep T40I10 levels: windows use a third to a half of their level's items,
-        so half or more of the level's rows drop out of a window.  None: the window counts
-        the level's rows.  (FastApriori.scala:132-160 counts every row per candidate.)"""
+        than k of them contains none of its k-candidates.  Unless the binomial estimate
+        (_trim_worth_it's, with the window's items) keeps most of the level's rows, the
+        level's bitmap bm is compressed to the rows that hold >= k of the window's items
+        (ops.primitives.window_bitmap: count.hip k_win_alive / k_win_compact, in the
+        bitmap domain, no pass over the transaction rows), and the window counts from
+        that: (ncols, bitmap [len(used_w), Wp], bitmap row u = slab row u).  Deep T40I10
+        levels: windows use a third to a half of their level's items, so a third to half
+        of the level's rows drop out of a window.  None: the window counts the level's
+        rows (the exact count kept more than TUNING.window_trim_rows_frac of them).
+        (FastApriori.scala:132-160 counts every row per candidate.)"""
+        if bm is None:
+            return None
         est = self._trim_estimate(db, used_w, k)
         if est is None or est >= TUNING.window_trim_est_frac * db["T"]:
             return None
         dev = db["ranks"].device
-        alive = torch.zeros(db["F1"], dtype=torch.int8)
-        alive[torch.from_numpy(used_w.astype(np.int64))] = 1
-        with roctx_range("window_trim"):
-            # the estimate decides; the exact count only stops a trim that would keep
-            # nearly every row (an exact gate at 0.7-0.8 measured slower: windows keeping
-            # ~80 % of the rows still gain, docs/PERF_HISTORY.md)
-            got = ops.trim_rows(db["roff"], db["ranks"], alive.to(dev), k, None,
-                                max_keep=int(TUNING.window_trim_rows_frac * db["T"]))
-            if got is None:
-                return None
-            kept, nroff, nranks, _, _ = got
-            K = int(kept.numel())
-            if K == 0:
-                return 0, None
-            imap = np.full(max(db["F1"], 1), -1, dtype=np.int32)
-            imap[used_w] = np.arange(used_w.size, dtype=np.int32)
-            bm, _ = ops.build_bitmaps(nroff, nranks, None, K, int(used_w.size), torch.from_numpy(imap).to(dev),
-                                      torch.from_numpy(np.ascontiguousarray(used_w, dtype=np.int32)).to(dev))
-        return K, bm
+        used_t = torch.from_numpy(used_w.astype(np.int64)).to(dev)
+        rows_w = (bmap[used_t] if bmap is not None else used_t).to(torch.int32).contiguous()
+        with roctx_range("window_rows"):
+            return ops.primitives.window_bitmap(bm, rows_w, (int(db["ncols"]) + 63) // 64, k,
+                                                max_keep=int(TUNING.window_trim_rows_frac * db["T"]))
 
     def _trim_estimate(self, db, used: np.ndarray, k: int):
         """Rows expected to keep >= k of the items `used` (the binomial model of

@@ -769,11 +769,8 @@ def count_candidates(bm: torch.Tensor, W: int, prefix: torch.Tensor, ext_off: np
 TRIM_HIST_BINS = 256   # csrc/hip/prep.hip kTrimHist
 
 
-def trim_rows(roff, ranks, alive: torch.Tensor, min_len: int, wrow=None, max_keep: int | None = None):
+def trim_rows(roff, ranks, alive: torch.Tensor, min_len: int, wrow=None):
     """Keep rows with >= min_len alive items, dropping the dead items.
-
-    max_keep (device path): when more rows than this would be kept, return None after
-    the counting pass (the emit pass is skipped).
 
     alive: int8 [F1] on the rows' device.  Returns (kept row ids int32, new roff,
     new ranks, new wrow, histogram of new row lengths int64 [256], lengths >= 255
@@ -798,8 +795,6 @@ def trim_rows(roff, ranks, alive: torch.Tensor, min_len: int, wrow=None, max_kee
         torch.cumsum(bk[0], 0, dtype=_I64, out=bases[0, 1:])    # two 1-D scans: the [2, nb] scan
         torch.cumsum(bk[1], 0, dtype=_I64, out=bases[1, 1:])    # along dim 1 runs on 2 threads' worth
         K, nnz = (int(v) for v in bases[:, -1].tolist())
-        if max_keep is not None and K > max_keep:
-            return None
         nroff = torch.empty(K + 1, dtype=_I64, device=dev)
         nroff[K:] = nnz
         nranks = torch.empty(max(nnz, 1), dtype=_I32, device=dev)
@@ -1789,6 +1784,33 @@ def dl_count_multipass(S: DeviceLevelState, F1: int, n_used: int, C: int, lds: i
                            window_used_avg=round(used_sum / max(npass, 1), 1),
                            window_rows_avg=round(rows_sum / max(npass, 1)), windows_trimmed=trimmed)
     return out
+
+
+def window_bitmap(bm: torch.Tensor, rows_w: torch.Tensor, W: int, k: int, max_keep: int | None = None):
+    """The bitmap of a window's items over only the rows holding >= k of them, from the
+    level's bitmap (count.hip k_win_alive / k_win_compact; FastApriori._window_rows).
+    bm: the level's bitmap (row-major or 8-word blocked), rows_w: device int32 [n] its
+    rows of the window's items (sorted by rank), W: its valid words.  Returns (K rows,
+    int64 [n, Wp'] row-major bitmap, row u = item u), (0, None) when no row qualifies,
+    or None when more than max_keep rows do (one host synchronisation, for K)."""
+    n = int(rows_w.numel())
+    dev = bm.device
+    st = _stream(bm)
+    ld = bitmap_ld(bm)
+    alive = torch.empty(max(W, 1), dtype=_I64, device=dev)
+    cnt = torch.empty(max(W, 1), dtype=_I32, device=dev)
+    _hip_call("fa_hip_win_alive", _p(bm), ld, _p(rows_w), n, W, int(k), _p(alive), _p(cnt), st)
+    off = torch.zeros(W + 1, dtype=_I64, device=dev)
+    torch.cumsum(cnt[:W], 0, out=off[1:])
+    K = int(off[W].item())
+    if max_keep is not None and K > max_keep:
+        return None
+    if K == 0:
+        return 0, None
+    w2 = (K + 63) // 64
+    out = torch.zeros((n, -(-w2 // 64) * 64), dtype=_I64, device=dev)
+    _hip_call("fa_hip_win_compact", _p(bm), ld, _p(rows_w), n, W, _p(alive), _p(off), _p(out), out.stride(0), st)
+    return K, out
 
 
 def dl_window_plan(S: DeviceLevelState, F1: int, C: int, lds: int, accb: int, st: int, dev,

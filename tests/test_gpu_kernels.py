@@ -596,3 +596,45 @@ def test_weighted_gram_mfma_matches_popcount(F1, classes, fp4, blocked):
     iu = torch.triu_indices(F1, F1, 1)
     assert torch.equal(got[iu[0], iu[1]], want[iu[0], iu[1]])
     assert torch.equal(ref[iu[0], iu[1]], want[iu[0], iu[1]])
+
+
+def _unpack_rows(words: np.ndarray, ncols: int) -> np.ndarray:
+    """uint64 words [n, W] -> bool [n, ncols] (column c = bit c & 63 of word c >> 6)."""
+    b = np.unpackbits(words.astype(np.uint64).view(np.uint8).reshape(words.shape[0], -1), axis=1, bitorder="little")
+    return b[:, :ncols].astype(bool)
+
+
+@pytest.mark.parametrize("blocked", [False, True])
+@pytest.mark.parametrize("ncols,n_items,k,dens", [(64 * 37 + 5, 9, 3, 0.3), (64 * 300, 70, 9, 0.12),
+                                                  (64 * 5 + 63, 3, 2, 0.5), (64 * 80, 40, 39, 0.9),
+                                                  (1000, 12, 13, 0.5)])
+def test_window_bitmap_matches_numpy(blocked, ncols, n_items, k, dens):
+    """count.hip k_win_alive / k_win_compact (ops.primitives.window_bitmap) against numpy:
+    the rows holding >= k of the window's items, each item's bits compressed to them
+    (window rows gathered from a larger bitmap, in either layout; edge words, K = 0)."""
+    rng = np.random.default_rng(ncols + n_items + k)
+    F = n_items + 17
+    bits = rng.random((F, ncols)) < dens
+    W = (ncols + 63) // 64
+    Wp = -(-W // 64) * 64
+    words = np.zeros((F, Wp * 64), dtype=np.uint8)
+    words[:, :ncols] = bits
+    wrd = np.packbits(words, axis=1, bitorder="little").view(np.uint64)          # [F, Wp]
+    if blocked:
+        bm = torch.from_numpy(np.ascontiguousarray(wrd.reshape(F, Wp // 8, 8).transpose(1, 0, 2)).view(np.int64)).to(DEV)
+    else:
+        bm = torch.from_numpy(wrd.view(np.int64)).to(DEV)
+    rows = np.sort(rng.choice(F, n_items, replace=False)).astype(np.int32)
+    got = ops.primitives.window_bitmap(bm, torch.from_numpy(rows).to(DEV), W, k)
+    alive = bits[rows].sum(0) >= k
+    K = int(alive.sum())
+    assert got[0] == K
+    if K == 0:
+        assert got[1] is None
+        return
+    out = got[1].cpu().numpy().view(np.uint64)
+    assert out.shape[0] == n_items and out.shape[1] * 64 >= K
+    want = bits[rows][:, alive]
+    assert np.array_equal(_unpack_rows(out, K), want)
+    assert not _unpack_rows(out, out.shape[1] * 64)[:, K:].any()       # zero past the K rows
+    assert ops.primitives.window_bitmap(bm, torch.from_numpy(rows).to(DEV), W, k, max_keep=K - 1) is None
