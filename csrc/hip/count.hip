@@ -1963,13 +1963,14 @@ __global__ __launch_bounds__(64) void k_win_compact(const uint64_t* __restrict__
       if (sh + n > 64) atomicOr(&buf[w + 1], (unsigned long long)(x >> (64 - sh)));
     }
     __syncthreads();
-    uint64_t* o = out + (int64_t)u * ldo + w0;
     for (int j = lane; j < nwords; j += 64) {
       const unsigned long long v = buf[j];
+      const int64_t gw = w0 + j;
+      uint64_t* o = ldo > 0 ? out + (int64_t)u * ldo + gw : out + (gw >> 3) * -ldo + (int64_t)u * 8 + (gw & 7);
       if (j == 0 || j == nwords - 1) {
-        if (v) atomicOr(reinterpret_cast<unsigned long long*>(o + j), v);   // shared with a neighbour wave
+        if (v) atomicOr(reinterpret_cast<unsigned long long*>(o), v);   // shared with a neighbour wave
       } else {
-        o[j] = v;
+        *o = v;
       }
     }
   }
@@ -1986,11 +1987,13 @@ FA_API int fa_hip_win_alive(const uint64_t* bm, int64_t ld, const int32_t* rows,
   FA_LAUNCH_RET();
 }
 
-// out: zeroed, [n_items][ldo] words, ldo >= ceil(K / 64); off: exclusive prefix of k_win_alive's counts [W]
+// out: zeroed, row-major [n_items][ldo] words (ldo >= ceil(K / 64)), or ldo < 0: the 8-word
+// blocked layout [Wp / 8][n_items][8] (ldo = -8 n_items; what the slab copies stream best);
+// off: exclusive prefix of k_win_alive's counts [W]
 FA_API int fa_hip_win_compact(const uint64_t* bm, int64_t ld, const int32_t* rows, int n_items, int64_t W,
                               const uint64_t* alive, const int64_t* off, uint64_t* out, int64_t ldo, hipStream_t st) {
   if (W <= 0 || n_items < 1) return 0;
-  if (ld == 0 || ldo < 1) return 1;
+  if (ld == 0 || ldo == 0) return 1;
   hipLaunchKernelGGL(k_win_compact, dim3((unsigned)((W + 63) / 64)), dim3(64), 0, st, bm, ld, rows, n_items, W, alive,
                      off, out, ldo);
   FA_LAUNCH_RET();

@@ -557,7 +557,7 @@ class FastApriori:
             wr = None
             if (self.cfg.trim and TUNING.window_trim and v["wword"] is None and v["src"] is None
                     and v["T"] >= self.cfg.trim_min_rows):
-                wr = lambda used_w: self._window_rows(v, used_w, k, bm, bmap)        # noqa: E731
+                wr = lambda used_w, nc: self._window_rows(v, used_w, k, bm, bmap, nc)        # noqa: E731
             cnt = Pm.dl_count_multipass(S, F1, n_used, C0, lds, v["roff"], v["ranks"], v["src"], v["ncols"],
                                         v["wword"], bm, bm_rows,
                                         self.stats["min_count"] / max(1, self.stats["n_lines"]), self._dev,
@@ -570,7 +570,7 @@ class FastApriori:
         self.stats["device_multipass"] = self.stats.get("device_multipass", 0) + 1
         return c, cnt
 
-    def _window_rows(self, db, used_w: np.ndarray, k: int, bm, bmap):
+    def _window_rows(self, db, used_w: np.ndarray, k: int, bm, bmap, n_cand: int):
         """Rows of one window of a multi-pass level (ops.primitives.dl_count_multipass):
         a window's candidates use only its own items (used_w), so a row holding fewer
         than k of them contains none of its k-candidates.  Unless the binomial estimate
@@ -581,19 +581,26 @@ class FastApriori:
         that: (ncols, bitmap [len(used_w), Wp], bitmap row u = slab row u).  Deep T40I10
         levels: windows use a third to a half of their level's items, so a third to half
         of the level's rows drop out of a window.  None: the window counts the level's
-        rows (the exact count kept more than TUNING.window_trim_rows_frac of them).
+        rows: the rows kept would save less than the compaction costs.  That cost follows
+        the window's items x the level's bitmap words, the window's count its candidates x
+        ~(k + 1) slab rows read per candidate, so the window is compacted only below
+        1 - TUNING.window_trim_cost * items / (candidates * (k + 1)) of the level's rows
+        (capped at TUNING.window_trim_rows_frac; T40I10D100M: ~0.8 for a level-5 window of
+        ~370 items, ~0.97 for a level-9 one of ~150).
         (FastApriori.scala:132-160 counts every row per candidate.)"""
         if bm is None:
             return None
+        keep = min(TUNING.window_trim_rows_frac,
+                   1.0 - TUNING.window_trim_cost * used_w.size / max(1, n_cand * (k + 1)))
         est = self._trim_estimate(db, used_w, k)
-        if est is None or est >= TUNING.window_trim_est_frac * db["T"]:
+        if keep <= 0 or est is None or est >= TUNING.window_trim_est_frac * db["T"]:
             return None
         dev = db["ranks"].device
         used_t = torch.from_numpy(used_w.astype(np.int64)).to(dev)
         rows_w = (bmap[used_t] if bmap is not None else used_t).to(torch.int32).contiguous()
         with roctx_range("window_rows"):
             return ops.primitives.window_bitmap(bm, rows_w, (int(db["ncols"]) + 63) // 64, k,
-                                                max_keep=int(TUNING.window_trim_rows_frac * db["T"]))
+                                                max_keep=int(keep * db["T"]))
 
     def _trim_estimate(self, db, used: np.ndarray, k: int):
         """Rows expected to keep >= k of the items `used` (the binomial model of

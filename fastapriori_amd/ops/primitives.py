@@ -1717,8 +1717,8 @@ def dl_count_multipass(S: DeviceLevelState, F1: int, n_used: int, C: int, lds: i
     of the LDS: deep T40I10 levels use 2-3x fewer items per window than per level, so
     every pass copies fewer slab rows and fewer passes are needed.
 
-    window_rows (optional, with per-window items): used_w (sorted ranks of a window's
-    items) -> None, or (ncols_w, bm_w): the bitmap of exactly those items over the rows
+    window_rows (optional, with per-window items): (used_w, candidates), used_w the
+    sorted ranks of a window's items -> None, or (ncols_w, bm_w): the bitmap of exactly those items over the rows
     that hold >= k of them (FastApriori._window_rows: a row with fewer holds none of the
     window's k-candidates), counted instead of the level's bitmap."""
     acc16 = TUNING.dl_acc16 and wword is None
@@ -1752,7 +1752,7 @@ def dl_count_multipass(S: DeviceLevelState, F1: int, n_used: int, C: int, lds: i
             nu = int(used_w.size)
             bits_t = torch.from_numpy(bits.view(np.int64).copy()).to(dev, non_blocking=False)
             bits_p = bits_t
-            got = window_rows(used_w) if window_rows is not None else None
+            got = window_rows(used_w, w1 - w0) if window_rows is not None else None
             if got is not None:
                 # the window's own rows: its items' bitmap, bitmap row u = slab row u
                 ncols_w, bm_w = got
@@ -1786,19 +1786,33 @@ def dl_count_multipass(S: DeviceLevelState, F1: int, n_used: int, C: int, lds: i
     return out
 
 
-def window_bitmap(bm: torch.Tensor, rows_w: torch.Tensor, W: int, k: int, max_keep: int | None = None):
+WINDOW_SAMPLE = 16   # window_bitmap: the share of the words (1 / this) that decides max_keep
+
+
+def window_bitmap(bm: torch.Tensor, rows_w: torch.Tensor, W: int, k: int, max_keep: int | None = None,
+                  blocked: bool = True):
     """The bitmap of a window's items over only the rows holding >= k of them, from the
     level's bitmap (count.hip k_win_alive / k_win_compact; FastApriori._window_rows).
     bm: the level's bitmap (row-major or 8-word blocked), rows_w: device int32 [n] its
     rows of the window's items (sorted by rank), W: its valid words.  Returns (K rows,
-    int64 [n, Wp'] row-major bitmap, row u = item u), (0, None) when no row qualifies,
-    or None when more than max_keep rows do (one host synchronisation, for K)."""
+    bitmap of the window's items over them, row u = item u: the 8-word blocked layout
+    [Wp' / 8, n, 8] (blocked; what slab_copy_bm streams best: a row-major one measured
+    slower at T40I10D100M's levels 3-8) or row-major [n, Wp']), (0, None) when no row qualifies,
+    or None when more than max_keep rows do -- judged on the first 1/WINDOW_SAMPLE of the
+    words, then on all of them (a host synchronisation each)."""
     n = int(rows_w.numel())
     dev = bm.device
     st = _stream(bm)
     ld = bitmap_ld(bm)
     alive = torch.empty(max(W, 1), dtype=_I64, device=dev)
     cnt = torch.empty(max(W, 1), dtype=_I32, device=dev)
+    if max_keep is not None and W >= 64 * WINDOW_SAMPLE:
+        # the first 1/WINDOW_SAMPLE of the words first (rows are in no particular order):
+        # a window that would keep too many rows costs that much of a pass, not a pass
+        ws = W // WINDOW_SAMPLE
+        _hip_call("fa_hip_win_alive", _p(bm), ld, _p(rows_w), n, ws, int(k), _p(alive), _p(cnt), st)
+        if int(cnt[:ws].sum().item()) * (W / ws) > max_keep:
+            return None
     _hip_call("fa_hip_win_alive", _p(bm), ld, _p(rows_w), n, W, int(k), _p(alive), _p(cnt), st)
     off = torch.zeros(W + 1, dtype=_I64, device=dev)
     torch.cumsum(cnt[:W], 0, out=off[1:])
@@ -1807,9 +1821,14 @@ def window_bitmap(bm: torch.Tensor, rows_w: torch.Tensor, W: int, k: int, max_ke
         return None
     if K == 0:
         return 0, None
-    w2 = (K + 63) // 64
-    out = torch.zeros((n, -(-w2 // 64) * 64), dtype=_I64, device=dev)
-    _hip_call("fa_hip_win_compact", _p(bm), ld, _p(rows_w), n, W, _p(alive), _p(off), _p(out), out.stride(0), st)
+    wp = -(-((K + 63) // 64) // 64) * 64
+    if blocked:
+        out = torch.zeros((wp // 8, n, 8), dtype=_I64, device=dev)
+        ldo = -out.stride(0)
+    else:
+        out = torch.zeros((n, wp), dtype=_I64, device=dev)
+        ldo = out.stride(0)
+    _hip_call("fa_hip_win_compact", _p(bm), ld, _p(rows_w), n, W, _p(alive), _p(off), _p(out), ldo, st)
     return K, out
 
 

@@ -53,12 +53,14 @@ class Tuning:
     dl_acc16_bundles: bool = False      # ... and in one-pass device bundles
     mp_window_items: bool = True        # window-by-window levels: each window's slab holds only its own used items
     # window-by-window levels: a window counts only the rows holding >= k of its own items
-    # (trimmed + a bitmap of its items) when the binomial estimate keeps fewer than
-    # window_trim_est_frac of the level's rows, unless the exact count keeps more than
-    # window_trim_rows_frac of them (FastApriori._window_rows)
+    # (its items' bitmap compacted to them, count.hip k_win_compact) when the binomial
+    # estimate keeps fewer than window_trim_est_frac of the level's rows and the count
+    # (a sample, then exact) fewer than min(window_trim_rows_frac,
+    # 1 - window_trim_cost * items / (candidates * (k + 1))) (FastApriori._window_rows)
     window_trim: bool = True
-    window_trim_est_frac: float = 0.7
-    window_trim_rows_frac: float = 0.95
+    window_trim_est_frac: float = 0.95
+    window_trim_rows_frac: float = 0.97
+    window_trim_cost: float = 100.0
     # bundle capacity = the largest over the slab widths (a bundle takes a narrower slab
     # when that holds all of it) instead of the first width holding 8192 candidates
     slab_cap_max: bool = False

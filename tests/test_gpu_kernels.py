@@ -604,11 +604,12 @@ def _unpack_rows(words: np.ndarray, ncols: int) -> np.ndarray:
     return b[:, :ncols].astype(bool)
 
 
+@pytest.mark.parametrize("out_blocked", [False, True])
 @pytest.mark.parametrize("blocked", [False, True])
 @pytest.mark.parametrize("ncols,n_items,k,dens", [(64 * 37 + 5, 9, 3, 0.3), (64 * 300, 70, 9, 0.12),
                                                   (64 * 5 + 63, 3, 2, 0.5), (64 * 80, 40, 39, 0.9),
                                                   (1000, 12, 13, 0.5)])
-def test_window_bitmap_matches_numpy(blocked, ncols, n_items, k, dens):
+def test_window_bitmap_matches_numpy(blocked, out_blocked, ncols, n_items, k, dens):
     """count.hip k_win_alive / k_win_compact (ops.primitives.window_bitmap) against numpy:
     the rows holding >= k of the window's items, each item's bits compressed to them
     (window rows gathered from a larger bitmap, in either layout; edge words, K = 0)."""
@@ -625,7 +626,7 @@ def test_window_bitmap_matches_numpy(blocked, ncols, n_items, k, dens):
     else:
         bm = torch.from_numpy(wrd.view(np.int64)).to(DEV)
     rows = np.sort(rng.choice(F, n_items, replace=False)).astype(np.int32)
-    got = ops.primitives.window_bitmap(bm, torch.from_numpy(rows).to(DEV), W, k)
+    got = ops.primitives.window_bitmap(bm, torch.from_numpy(rows).to(DEV), W, k, blocked=out_blocked)
     alive = bits[rows].sum(0) >= k
     K = int(alive.sum())
     assert got[0] == K
@@ -633,6 +634,8 @@ def test_window_bitmap_matches_numpy(blocked, ncols, n_items, k, dens):
         assert got[1] is None
         return
     out = got[1].cpu().numpy().view(np.uint64)
+    if out_blocked:                                                # [Wp / 8, n, 8] -> [n, Wp]
+        out = np.ascontiguousarray(out.transpose(1, 0, 2)).reshape(n_items, -1)
     assert out.shape[0] == n_items and out.shape[1] * 64 >= K
     want = bits[rows][:, alive]
     assert np.array_equal(_unpack_rows(out, K), want)
