@@ -593,14 +593,20 @@ class FastApriori:
         keep = min(TUNING.window_trim_rows_frac,
                    1.0 - TUNING.window_trim_cost * used_w.size / max(1, n_cand * (k + 1)))
         est = self._trim_estimate(db, used_w, k)
+        wlog = self.stats.setdefault("window_log", [])
+        rec = dict(k=k, items=int(used_w.size), cand=int(n_cand), keep=round(keep, 3),
+                   est=None if est is None else round(est / max(1, db["T"]), 3))
+        wlog.append(rec)
         if keep <= 0 or est is None or est >= TUNING.window_trim_est_frac * db["T"]:
             return None
         dev = db["ranks"].device
         used_t = torch.from_numpy(used_w.astype(np.int64)).to(dev)
         rows_w = (bmap[used_t] if bmap is not None else used_t).to(torch.int32).contiguous()
         with roctx_range("window_rows"):
-            return ops.primitives.window_bitmap(bm, rows_w, (int(db["ncols"]) + 63) // 64, k,
-                                                max_keep=int(keep * db["T"]))
+            got = ops.primitives.window_bitmap(bm, rows_w, (int(db["ncols"]) + 63) // 64, k,
+                                               max_keep=int(keep * db["T"]))
+        rec["kept"] = None if got is None else round(got[0] / max(1, db["T"]), 3)
+        return got
 
     def _trim_estimate(self, db, used: np.ndarray, k: int):
         """Rows expected to keep >= k of the items `used` (the binomial model of
