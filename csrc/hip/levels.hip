@@ -271,11 +271,27 @@ __device__ __forceinline__ int la_row_min(int v) {
   return v;
 }
 
+// Sum of v over the four 16-lane rows, in every lane (lanes l, l ^ 16, l ^ 32, l ^ 48):
+// gfx950's v_permlane16_swap / v_permlane32_swap, VALU exchanges instead of two
+// ds_bpermute round trips through the LDS.
+__device__ __forceinline__ int la_qsum(int v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  v = (int)a[0] + (int)a[1];
+  const auto b = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return (int)b[0] + (int)b[1];
+}
+
+// test hook: out[lane] = la_qsum(lane) for one wave (tests/test_gpu_kernels.py)
+__global__ __launch_bounds__(64) void k_la_qsum_probe(int* out) { out[threadIdx.x] = la_qsum((int)threadIdx.x); }
+
 // One wave per window of kLaWs * 64 records.  Lane (q, g) = (lane >> 4, lane & 15):
 // g is one of the window's 16 lane groups (ds_read_b128 group g % 4 of wave step
 // g / 4), q takes read positions q, q + 4, ...; a record's cost is summed over q, the
 // winner is the DPP-row minimum.  State per (group, position, slot): the first row
-// seen there (16 bits) and the rows there so far (16 bits), one LDS word.
+// seen there (16 bits) and the rows there so far (16 bits), one LDS word.  Lane (q, g)
+// alone reads and writes the state of group g at its positions, so the greedy steps
+// need no LDS barrier (a wave's LDS operations complete in order); the next record's
+// rows are read ahead, and the cost sum crosses rows by lane swaps (la_qsum).
 __global__ __launch_bounds__(64) void k_dl_lane_assign(int4* __restrict__ rec, const long long* __restrict__ c,
                                                        int rs) {
   constexpr int NW = 64 * kLaWs, NG = 4 * kLaWs;
@@ -305,14 +321,19 @@ __global__ __launch_bounds__(64) void k_dl_lane_assign(int4* __restrict__ rec, c
   wave_lds_sync();
   const int g = lane & 15, q = lane >> 4;
   int fill = 0;                                    // records dealt to group g
+  int rn[kPq];
+#pragma unroll
+  for (int t = 0; t < kPq; ++t) rn[t] = q + 4 * t < R ? (int)rws[0][q + 4 * t] : -1;
   for (int i = 0; i < NW; ++i) {
     int rr[kPq];
     uint32_t w[kPq];
 #pragma unroll
+    for (int t = 0; t < kPq; ++t) rr[t] = rn[t];
+#pragma unroll
     for (int t = 0; t < kPq; ++t) {
       const int pos = q + 4 * t;
-      rr[t] = pos < R ? (int)rws[i][pos] : -1;
       w[t] = pos < R ? st[g][pos][(rr[t] * rs) & 15] : 0xFFFFu;
+      rn[t] = (pos < R && i + 1 < NW) ? (int)rws[i + 1][pos] : -1;
     }
     int cost = 0;
 #pragma unroll
@@ -320,8 +341,7 @@ __global__ __launch_bounds__(64) void k_dl_lane_assign(int4* __restrict__ rec, c
       const int o = (int)(w[t] & 0xFFFF);
       if (o != 0xFFFF && o != rr[t]) cost += (int)(w[t] >> 16);
     }
-    cost += __shfl_xor(cost, 16, 64);
-    cost += __shfl_xor(cost, 32, 64);
+    cost = la_qsum(cost);
     if (fill >= 16) cost = 1 << 20;
     const int win_g = la_row_min((cost << 4) | g) & 15;
     if (g == win_g) {
@@ -344,8 +364,8 @@ __global__ __launch_bounds__(64) void k_dl_lane_assign(int4* __restrict__ rec, c
       }
       ++fill;
     }
-    wave_lds_sync();
   }
+  wave_lds_sync();
   for (int i = lane; i < NW; i += 64) {
     const int64_t d = base + dst[i];
     rec[3 * d] = win[3 * i]; rec[3 * d + 1] = win[3 * i + 1]; rec[3 * d + 2] = win[3 * i + 2];
@@ -554,6 +574,11 @@ FA_API int fa_hip_dl_plan_window_bits(const int64_t* desc, int L, long long* ctl
                                       int32_t* item_map, void* rec, int64_t max_pieces, int32_t* part,
                                       int64_t part_cap, int32_t* gpre, int64_t gpre_cap, int64_t w0, int64_t w1,
                                       int sw, hipStream_t st);
+
+FA_API int fa_hip_debug_la_qsum(int* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_la_qsum_probe, dim3(1), dim3(64), 0, st, out);
+  FA_LAUNCH_RET();
+}
 
 // Bank-aware lane deal of the plans queued next (k_dl_lane_assign): on / off, set by
 // fastapriori_amd.ops.primitives before the plans are queued (TUNING.lane_deal_min_rows).

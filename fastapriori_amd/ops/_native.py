@@ -64,6 +64,7 @@ _HOST_SIGS = {
 _HIP_SIGS = {
     "fa_hip_histogram": (C.c_int, [vp, i64, i32, vp, vp]),
     "fa_hip_f1_rank": (C.c_int, [vp, i32, i64, C.c_int, vp, vp, vp]),
+    "fa_hip_debug_la_qsum": (C.c_int, [vp, vp]),
     "fa_hip_win_alive": (C.c_int, [vp, i64, vp, C.c_int, i64, C.c_int, vp, vp, vp]),
     "fa_hip_win_compact": (C.c_int, [vp, i64, vp, C.c_int, i64, vp, vp, vp, i64, vp]),
     "fa_hip_debug_slab_max_wg": (None, [C.c_int]),

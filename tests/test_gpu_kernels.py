@@ -641,3 +641,14 @@ def test_window_bitmap_matches_numpy(blocked, out_blocked, ncols, n_items, k, de
     assert np.array_equal(_unpack_rows(out, K), want)
     assert not _unpack_rows(out, out.shape[1] * 64)[:, K:].any()       # zero past the K rows
     assert ops.primitives.window_bitmap(bm, torch.from_numpy(rows).to(DEV), W, k, max_keep=K - 1) is None
+
+
+def test_lane_deal_cross_row_sum():
+    """levels.hip la_qsum (v_permlane16_swap / v_permlane32_swap): every lane of a wave gets
+    the sum over lanes l, l ^ 16, l ^ 32, l ^ 48 -- the lane deal's four 16-lane rows must
+    agree on every record's cost, or they would deal it to different groups."""
+    out = torch.zeros(64, dtype=torch.int32, device=DEV)
+    _native.check(_native.hip().fa_hip_debug_la_qsum(out.data_ptr(), torch.cuda.current_stream().cuda_stream),
+                  "fa_hip_debug_la_qsum")
+    lane = np.arange(64)
+    assert np.array_equal(out.cpu().numpy(), 4 * (lane & 15) + 0 + 16 + 32 + 48)
