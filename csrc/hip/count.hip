@@ -1930,13 +1930,19 @@ __global__ __launch_bounds__(256) void k_win_alive(const uint64_t* __restrict__ 
   cnt[q] = __popcll(a);
 }
 
-__global__ __launch_bounds__(64) void k_win_compact(const uint64_t* __restrict__ bm, int64_t ld,
-                                                    const int32_t* __restrict__ rows, int n_items, int64_t W,
-                                                    const uint64_t* __restrict__ alive, const int64_t* __restrict__ off,
-                                                    uint64_t* __restrict__ out, int64_t ldo) {
-  __shared__ unsigned long long buf[kWinBatch][66];
-  const int lane = threadIdx.x;
-  const int64_t q0 = (int64_t)blockIdx.x * 64, q = q0 + lane;
+__global__ __launch_bounds__(256) void k_win_compact(const uint64_t* __restrict__ bm, int64_t ld,
+                                                     const int32_t* __restrict__ rows, int n_items, int64_t W,
+                                                     const uint64_t* __restrict__ alive,
+                                                     const int64_t* __restrict__ off, uint64_t* __restrict__ out,
+                                                     int64_t ldo) {
+  // four independent waves per workgroup, each with its own buffers and only wave-level
+  // LDS ordering (wave_lds_sync): a __syncthreads fence drains the wave's outstanding
+  // stores and loads (s_waitcnt vmcnt(0)) at every round
+  __shared__ unsigned long long bufs[4][kWinBatch][66];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  unsigned long long (&buf)[kWinBatch][66] = bufs[wv];
+  const int64_t q0 = ((int64_t)blockIdx.x * 4 + wv) * 64, q = q0 + lane;
+  if (q0 >= W) return;
   const int64_t qe = min(W, q0 + 64) - 1;                 // the wave's last word
   const uint64_t m0 = q < W ? alive[q] : 0ull;
   const int n = __popcll(m0);
@@ -1959,15 +1965,14 @@ __global__ __launch_bounds__(64) void k_win_compact(const uint64_t* __restrict__
       mk &= ~mp;
     }
   }
-  // kWinBatch items per round: their words loaded together, one LDS buffer each, two
-  // barriers per round instead of per item (per-item rounds: ~2.6 ms per T40I10D100M window)
+  // kWinBatch items per round: their words loaded together, one LDS buffer each
   for (int u0 = 0; u0 < n_items; u0 += kWinBatch) {
     const int nb = min(kWinBatch, n_items - u0);
     uint64_t x[kWinBatch];
 #pragma unroll
     for (int b = 0; b < kWinBatch; ++b) x[b] = (n && b < nb) ? bm_word(bm, ld, rows[u0 + b], q) : 0ull;
     for (int i = lane; i < nb * 66; i += 64) (&buf[0][0])[i] = 0ull;
-    __syncthreads();
+    wave_lds_sync();
     if (n) {
       const int w = s >> 6, sh = s & 63;
 #pragma unroll
@@ -1983,7 +1988,7 @@ __global__ __launch_bounds__(64) void k_win_compact(const uint64_t* __restrict__
         if (sh + n > 64) atomicOr(&buf[b][w + 1], (unsigned long long)(y >> (64 - sh)));
       }
     }
-    __syncthreads();
+    wave_lds_sync();
     for (int b = 0; b < nb; ++b) {
       const int64_t u = u0 + b;
       for (int j = lane; j < nwords; j += 64) {
@@ -1997,7 +2002,7 @@ __global__ __launch_bounds__(64) void k_win_compact(const uint64_t* __restrict__
         }
       }
     }
-    __syncthreads();                                     // (the buffers are cleared next round)
+    wave_lds_sync();                                     // (the buffers are cleared next round)
   }
 }
 
@@ -2019,8 +2024,8 @@ FA_API int fa_hip_win_compact(const uint64_t* bm, int64_t ld, const int32_t* row
                               const uint64_t* alive, const int64_t* off, uint64_t* out, int64_t ldo, hipStream_t st) {
   if (W <= 0 || n_items < 1) return 0;
   if (ld == 0 || ldo == 0) return 1;
-  hipLaunchKernelGGL(k_win_compact, dim3((unsigned)((W + 63) / 64)), dim3(64), 0, st, bm, ld, rows, n_items, W, alive,
-                     off, out, ldo);
+  hipLaunchKernelGGL(k_win_compact, dim3((unsigned)((W + 255) / 256)), dim3(256), 0, st, bm, ld, rows, n_items, W,
+                     alive, off, out, ldo);
   FA_LAUNCH_RET();
 }
 
