@@ -608,9 +608,13 @@ class FastApriori:
         rec["kept"] = None if got is None else round(got[0] / max(1, db["T"]), 3)
         return got
 
-    def _trim_estimate(self, db, used: np.ndarray, k: int):
-        """Rows expected to keep >= k of the items `used` (the binomial model of
-        _trim_worth_it), or None without a length histogram."""
+    @staticmethod
+    def _trim_estimate(db, used: np.ndarray, k: int, with_nnz: bool = False):
+        """Rows expected to keep >= k of the items `used` (and, with_nnz, the item
+        occurrences they keep): item occurrences survive with probability p = (supports
+        of `used`) / (supports of the items still in the rows), a row of length L keeps
+        >= k with P[Binom(L, p) >= k] = I_p(k, L - k + 1) (regularised incomplete beta).
+        None without a length histogram or items."""
         from scipy.special import betainc
         hist = db.get("len_hist")
         if hist is None:
@@ -625,7 +629,8 @@ class FastApriori:
         ok = L >= k
         if p > 0:
             sf[ok] = betainc(k, L[ok] - k + 1, p)
-        return float((hist * sf).sum())
+        rows = float((hist * sf).sum())
+        return (rows, float((hist * L * p).sum())) if with_nnz else rows
 
     def _dl_bitmap_count(self, S, db, used: np.ndarray) -> torch.Tensor:
         """Counts (int32 [C], bundle order) of the device bundle's single level from the
@@ -1281,22 +1286,10 @@ class FastApriori:
         """
         if db["T"] < self.cfg.trim_min_rows:   # a trim's fixed cost (2 launches + a host sync) dominates
             return False
-        from scipy.special import betainc
-        c1 = db["c1"]
-        alive = db["alive"]
-        denom = float(c1[alive].sum())
-        if denom <= 0:
+        got = self._trim_estimate(db, used, k, with_nnz=True)
+        if got is None:
             return False
-        p = float(c1[used].sum()) / denom
-        hist = db["len_hist"]
-        L = np.arange(hist.size)
-        # P[Binom(L, p) >= k] = I_p(k, L - k + 1) (regularised incomplete beta), 0 for L < k
-        sf = np.zeros(hist.size)
-        ok = L >= k
-        if p > 0:
-            sf[ok] = betainc(k, L[ok] - k + 1, min(p, 1.0))
-        est_rows = float((hist * sf).sum())
-        est_nnz = float((hist * L * p).sum())
+        est_rows, est_nnz = got
         rows_ok = est_rows < TUNING.trim_rows_frac * max(db["T"], 1)
         if C and db["ranks"].is_cuda and C > ops.primitives.slab_capacity(int(used.size), C):
             return rows_ok
