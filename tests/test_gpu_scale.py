@@ -56,7 +56,7 @@ def test_t40_window_trim_matches_cpu(frac):
     cpu = generate_shard(400_000, Comm(), "cpu", 40.0, 10.0, 2000, 1000, 5)
     ref = _mine(cpu, 0.005, trim_min_rows=0)
     with override(window_trim=True, window_trim_est_frac=frac, window_trim_rows_frac=max(frac, 0.97),
-                  window_trim_cost=0.0 if frac > 1 else 100.0):
+                  window_trim_cost=0.0 if frac > 1 else 100.0, window_trim_min_rows=0):
         m = FastApriori(0.005, config=MinerConfig(min_support=0.005, trim_min_rows=0), logger=Logger(0, enabled=False))
         got = m.run(cpu.to(DEV))
     assert m.stats.get("device_multipass", 0) >= 1, m.stats
