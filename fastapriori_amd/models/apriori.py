@@ -556,7 +556,8 @@ class FastApriori:
             bm_rows = (bmap[used_t] if bmap is not None else used_t).to(torch.int32).contiguous()
             wr = None
             if (self.cfg.trim and TUNING.window_trim and v["wword"] is None and v["src"] is None
-                    and v["T"] >= max(self.cfg.trim_min_rows, TUNING.window_trim_min_rows)):
+                    and v["T"] >= self.cfg.trim_min_rows
+                    and v.get("T0", v["T"]) >= TUNING.window_trim_min_rows):
                 wr = lambda used_w, nc: self._window_rows(v, used_w, k, bm, bmap, nc)        # noqa: E731
             cnt = Pm.dl_count_multipass(S, F1, n_used, C0, lds, v["roff"], v["ranks"], v["src"], v["ncols"],
                                         v["wword"], bm, bm_rows,

@@ -61,8 +61,10 @@ class Tuning:
     window_trim_est_frac: float = 0.95
     window_trim_rows_frac: float = 0.97
     window_trim_cost: float = 100.0
-    # ... on levels of at least this many rows (T40I10D10M, 10M rows: windows of a tenth
-    # of the work, where the compaction's fixed costs ate the gain: 70.6 -> 73.6 ms)
+    # ... when the rank's shard had at least this many rows after compression (T40I10D10M,
+    # 10M rows: windows of a tenth of the work, where the compaction's fixed costs ate the
+    # gain: 70.6 -> 73.6 ms; the shard's size, not the level's: T40I10D100M's level 11
+    # keeps ~20M rows and still gains, 21.8 -> 16.5 ms)
     window_trim_min_rows: int = 1 << 25
     # bundle capacity = the largest over the slab widths (a bundle takes a narrower slab
     # when that holds all of it) instead of the first width holding 8192 candidates
