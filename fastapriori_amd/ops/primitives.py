@@ -548,8 +548,9 @@ def pair_counts_horizontal(roff, ranks, wrow, F1: int, long_rows: bool = True, b
     T = roff.numel() - 1
     dev = ranks.device
     if ranks.is_cuda:
-        out = torch.zeros((F1, F1), dtype=_I32, device=dev)
-        if T > 0 and F1 >= 2:
+        if T <= 0 or F1 < 2:
+            out = torch.zeros((F1, F1), dtype=_I32, device=dev)
+        else:
             st = _stream(ranks)
             pb = 128 if (wrow is not None or long_rows) else 256       # u16 tiles need unit weights
             nb = (F1 + pb - 1) // pb
@@ -585,13 +586,14 @@ def pair_counts_horizontal(roff, ranks, wrow, F1: int, long_rows: bool = True, b
                 # work-queue schedule: persistent workgroups keep their tile across
                 # sub-chunks; even row stride -> two counters per 64-bit flush atomic
                 ld = F1 + (F1 & 1)
-                out = torch.zeros((F1, ld), dtype=_I32, device=dev)
                 nbp = nb * (nb + 1) // 2
-                qctr = torch.zeros(nbp, dtype=_I32, device=dev)
+                zb = torch.zeros(F1 * ld + nbp, dtype=_I32, device=dev)      # counts + queue counters: one fill
+                out, qctr = zb[:F1 * ld].view(F1, ld), zb[F1 * ld:]
                 _hip_call("fa_hip_pair_queue16", _p(cnt), _p(base), _p(lr), T, F1, ld, _p(qctr), _p(out),
                           TUNING.pair_wg, st)
                 out = out[:, :F1]
             else:
+                out = torch.zeros((F1, F1), dtype=_I32, device=dev)
                 _hip_call("fa_hip_pair_blocked", _p(cnt), _p(base), _p(lr), T, _p(wrow), F1, _p(out),
                           PAIR_CHUNK_ROWS, st)
         return out if raw else out.to(_I64)
