@@ -589,7 +589,7 @@ class FastApriori:
         (capped at TUNING.window_trim_rows_frac; T40I10D100M: ~0.8 for a level-5 window of
         ~370 items, ~0.97 for a level-9 one of ~150).
         (FastApriori.scala:132-160 counts every row per candidate.)"""
-        if bm is None:
+        if bm is None or used_w.size > ops.primitives.WINDOW_MAX_ITEMS:
             return None
         keep = min(TUNING.window_trim_rows_frac,
                    1.0 - TUNING.window_trim_cost * used_w.size / max(1, n_cand * (k + 1)))

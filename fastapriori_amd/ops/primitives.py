@@ -1789,6 +1789,7 @@ def dl_count_multipass(S: DeviceLevelState, F1: int, n_used: int, C: int, lds: i
 
 
 WINDOW_SAMPLE = 16   # window_bitmap: the share of the words (1 / this) that decides max_keep
+WINDOW_MAX_ITEMS = 2047   # count.hip k_win_alive: bit-sliced counts of up to 11 planes
 
 
 def window_bitmap(bm: torch.Tensor, rows_w: torch.Tensor, W: int, k: int, max_keep: int | None = None,
