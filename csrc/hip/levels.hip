@@ -298,7 +298,8 @@ __global__ __launch_bounds__(64) void k_dl_lane_assign(int4* __restrict__ rec, c
   constexpr int kPq = kLaMaxPos / 4;             // positions per lane
   __shared__ int4 win[3 * NW];
   __shared__ uint16_t rws[NW][kLaMaxPos];        // slab row of every record's read position
-  __shared__ uint32_t st[NG][kLaMaxPos][16];
+  __shared__ uint32_t st[kLaMaxPos][16][NG];       // [position][slot][group]: a read of one slot by the
+                                                  // 16 groups hits 16 banks (group-major: one bank)
   __shared__ int16_t dst[NW];
   const int G = reinterpret_cast<const int32_t*>(c + 221)[0];
   const int64_t base = (int64_t)blockIdx.x * NW;
@@ -323,17 +324,27 @@ __global__ __launch_bounds__(64) void k_dl_lane_assign(int4* __restrict__ rec, c
   int fill = 0;                                    // records dealt to group g
   int rn[kPq];
 #pragma unroll
-  for (int t = 0; t < kPq; ++t) rn[t] = q + 4 * t < R ? (int)rws[0][q + 4 * t] : -1;
+  for (int t = 0; t < kPq; ++t) {
+    const int v = (int)rws[0][q + 4 * t < R ? q + 4 * t : 0];
+    rn[t] = q + 4 * t < R ? v : -1;
+  }
   for (int i = 0; i < NW; ++i) {
     int rr[kPq];
     uint32_t w[kPq];
 #pragma unroll
     for (int t = 0; t < kPq; ++t) rr[t] = rn[t];
+    // unconditional reads (clamped position, result masked): a read under a branch made
+    // the compiler wait for each one before the next (five LDS round trips per step)
+    const int i1 = i + 1 < NW ? i + 1 : i;
 #pragma unroll
     for (int t = 0; t < kPq; ++t) {
       const int pos = q + 4 * t;
-      w[t] = pos < R ? st[g][pos][(rr[t] * rs) & 15] : 0xFFFFu;
-      rn[t] = (pos < R && i + 1 < NW) ? (int)rws[i + 1][pos] : -1;
+      const bool ok = pos < R;
+      const int pc = ok ? pos : 0;
+      const uint32_t sv = st[pc][(rr[t] * rs) & 15][g];
+      const int rv = (int)rws[i1][pc];
+      w[t] = ok ? sv : 0xFFFFu;
+      rn[t] = ok ? rv : -1;
     }
     int cost = 0;
 #pragma unroll
@@ -348,10 +359,11 @@ __global__ __launch_bounds__(64) void k_dl_lane_assign(int4* __restrict__ rec, c
 #pragma unroll
       for (int t = 0; t < kPq; ++t) {
         const int pos = q + 4 * t;
-        if (pos >= R) continue;
+        // the slot's new state, branch-free (one masked store per position): first row
+        // seen there, one more row there, or unchanged (the same row broadcasts)
         const int o = (int)(w[t] & 0xFFFF);
-        if (o == 0xFFFF) st[g][pos][(rr[t] * rs) & 15] = (uint32_t)rr[t] | (1u << 16);
-        else if (o != rr[t]) st[g][pos][(rr[t] * rs) & 15] = w[t] + (1u << 16);
+        const uint32_t nv = o == 0xFFFF ? ((uint32_t)rr[t] | (1u << 16)) : (o != rr[t] ? w[t] + (1u << 16) : w[t]);
+        if (pos < R) st[pos][(rr[t] * rs) & 15][g] = nv;
       }
       if (q == 0) {
         // the fill-th lane of ds_read_b128 group g % 4 in wave step g / 4
